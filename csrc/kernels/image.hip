@@ -1,0 +1,159 @@
+// K1 — fused camera-frame preprocessing (reference: communicator/ros_inference.py:131,140-141
+// cv2.resize + clients/preprocess/yolov5_preprocess.py:20-24 transpose/astype//255,
+// detectron_preprocess.py:20-24 (no /255), utils/preprocess.py:147-157 INCEPTION/VGG/COCO).
+//
+// One pass: uint8 HWC (RGB or BGR) -> bilinear resize (OpenCV INTER_LINEAR
+// pixel-centre convention, optional uint8 re-quantisation like cv2's u8
+// output) -> optional letterbox (YOLOv5 style, pad value 114) -> per-channel
+// affine (x*scale+bias) -> NCHW or NHWC(4-padded) in fp32/fp16/bf16.
+//
+// Each thread produces 4 horizontally adjacent output pixels so that the
+// stores are 8-16 B per lane per plane (vectorised, cdna_hip_programming.md
+// Guideline 13).  Source reads go through L1/L2 (each source pixel is re-read
+// by ~1-4 output pixels); the kernel is store-bound.
+#include "tca_common.h"
+
+using namespace tca;
+
+namespace {
+
+struct PrepParams {
+  int src_h, src_w, src_row_stride, src_c;
+  long src_batch_stride;
+  int swap_rb;
+  int dst_h, dst_w, dst_c, dst_layout;  // layout 0 = NCHW, 1 = NHWC
+  int reg_top, reg_left, reg_h, reg_w;  // resized region inside dst
+  float pad_value;
+  int quantize_u8;
+  float sc0, sc1, sc2, b0, b1, b2;
+};
+
+__device__ __forceinline__ void coord(float dst, float scale, int src_n, int& i0, int& i1, float& a) {
+  float f = (dst + 0.5f) * scale - 0.5f;
+  int s = (int)floorf(f);
+  a = f - (float)s;
+  if (s < 0) { s = 0; a = 0.f; }
+  if (s >= src_n - 1) { s = src_n - 1; a = 0.f; }
+  i0 = s;
+  i1 = min(s + 1, src_n - 1);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ src, T* __restrict__ dst, PrepParams p,
+                                                   int batch) {
+  const int qw = (p.dst_w + 3) >> 2;
+  long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)batch * p.dst_h * qw;
+  if (gid >= total) return;
+  const int q = (int)(gid % qw);
+  const int y = (int)((gid / qw) % p.dst_h);
+  const int b = (int)(gid / ((long)qw * p.dst_h));
+  const uint8_t* s = src + (long)b * p.src_batch_stride;
+  const float sx_scale = (float)p.src_w / (float)p.reg_w;
+  const float sy_scale = (float)p.src_h / (float)p.reg_h;
+
+  float out[4][3];
+  const int ly = y - p.reg_top;
+  const bool row_in = ly >= 0 && ly < p.reg_h;
+  int y0 = 0, y1 = 0;
+  float ay = 0.f;
+  if (row_in) coord((float)ly, sy_scale, p.src_h, y0, y1, ay);
+  const uint8_t* r0 = s + (long)y0 * p.src_row_stride;
+  const uint8_t* r1 = s + (long)y1 * p.src_row_stride;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int x = q * 4 + k;
+    const int lx = x - p.reg_left;
+    if (!row_in || lx < 0 || lx >= p.reg_w || x >= p.dst_w) {
+      out[k][0] = out[k][1] = out[k][2] = p.pad_value;
+      continue;
+    }
+    int x0, x1;
+    float ax;
+    coord((float)lx, sx_scale, p.src_w, x0, x1, ax);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float v00 = r0[x0 * p.src_c + c], v01 = r0[x1 * p.src_c + c];
+      float v10 = r1[x0 * p.src_c + c], v11 = r1[x1 * p.src_c + c];
+      float top = v00 + ax * (v01 - v00);
+      float bot = v10 + ax * (v11 - v10);
+      float v = top + ay * (bot - top);
+      if (p.quantize_u8) v = fminf(fmaxf(rintf(v), 0.f), 255.f);
+      out[k][c] = v;
+    }
+  }
+  const float sc[3] = {p.sc0, p.sc1, p.sc2};
+  const float bi[3] = {p.b0, p.b1, p.b2};
+  T* d = dst;
+  if (p.dst_layout == 0) {  // NCHW
+    const long plane = (long)p.dst_h * p.dst_w;
+    const long base = (long)b * p.dst_c * plane + (long)y * p.dst_w + q * 4;
+    const bool full = q * 4 + 3 < p.dst_w && ((p.dst_w & 3) == 0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int sc_c = p.swap_rb ? 2 - c : c;
+      T v4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v4[k] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+      T* o = d + base + (long)c * plane;
+      if (full) {
+        if constexpr (sizeof(T) == 4) {
+          *reinterpret_cast<float4*>(o) = *reinterpret_cast<float4*>(v4);
+        } else {
+          *reinterpret_cast<uint2*>(o) = *reinterpret_cast<uint2*>(v4);
+        }
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (q * 4 + k < p.dst_w) o[k] = v4[k];
+      }
+    }
+    if (p.dst_c == 4) {
+      T* o = d + base + 3 * plane;
+      for (int k = 0; k < 4; ++k)
+        if (q * 4 + k < p.dst_w) o[k] = from_f32<T>(0.f);
+    }
+  } else {  // NHWC with dst_c in {3, 4}
+    const long base = (((long)b * p.dst_h + y) * p.dst_w + q * 4) * p.dst_c;
+    for (int k = 0; k < 4; ++k) {
+      if (q * 4 + k >= p.dst_w) break;
+      T px[4];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int sc_c = p.swap_rb ? 2 - c : c;
+        px[c] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+      }
+      px[3] = from_f32<T>(0.f);
+      T* o = d + base + (long)k * p.dst_c;
+      if (p.dst_c == 4 && sizeof(T) == 2) {
+        *reinterpret_cast<uint2*>(o) = *reinterpret_cast<uint2*>(px);
+      } else {
+        for (int c = 0; c < p.dst_c; ++c) o[c] = px[c];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// Preprocess `batch` frames of identical geometry.
+TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src_h, int src_w, int src_row_stride,
+                                 int src_c, int swap_rb, void* dst, int dst_dtype, int dst_layout, int dst_c,
+                                 int dst_h, int dst_w, int batch, int reg_top, int reg_left, int reg_h, int reg_w,
+                                 float pad_value, int quantize_u8, float sc0, float sc1, float sc2, float b0,
+                                 float b1, float b2, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (src_c < 3 || (dst_c != 3 && dst_c != 4) || reg_h <= 0 || reg_w <= 0) return (int)hipErrorInvalidValue;
+  PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
+               reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
+  const long total = (long)batch * dst_h * ((dst_w + 3) / 4);
+  const int bs = 256;
+  dim3 grid((unsigned)((total + bs - 1) / bs));
+  const uint8_t* s = (const uint8_t*)src;
+  switch (dst_dtype) {
+    case kF32: prep_kernel<float><<<grid, bs, 0, stream>>>(s, (float*)dst, p, batch); break;
+    case kF16: prep_kernel<__half><<<grid, bs, 0, stream>>>(s, (__half*)dst, p, batch); break;
+    case kBF16: prep_kernel<__hip_bfloat16><<<grid, bs, 0, stream>>>(s, (__hip_bfloat16*)dst, p, batch); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  TCA_LAUNCH_CHECK();
+}

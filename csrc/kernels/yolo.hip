@@ -1,0 +1,182 @@
+// K3 — YOLOv5 Detect decode fused with the candidate filter
+// (reference: clients/postprocess/yolov5_postprocess.py:36-92 — obj > conf_thres,
+// cls *= obj, xywh2xyxy, best class (or multi-label), conf > conf_thres, class filter;
+// the decode itself is what the exported ONNX model does inside the server).
+//
+// Reads the three raw head maps (NCHW or NHWC, fp32/fp16/bf16) directly, so
+// the 25200 x 85 decoded tensor never has to exist on the hot path.  One
+// thread per (image, level, anchor, y, x): objectness is read first and the
+// 80 class logits only for the few cells that pass — argmax over logits is
+// argmax over sigmoids, so only one extra sigmoid per passing cell.
+// Passing candidates are stream-compacted per image with one LDS counter and
+// one global atomic per block; a 64-bit key (score, ~anchor index) makes the
+// later sort deterministic although slot order is not.
+//
+// Optionally (decoded != nullptr) every cell's full decoded row is written
+// as fp32 [B, N, 5+nc] — the KServe output contract of the reference's ONNX
+// YOLOv5 (examples/YOLOv5/config.pbtxt:13-18) served by our own server.
+#include "tca_common.h"
+
+using namespace tca;
+
+namespace {
+
+struct YoloHeads {
+  const void* head[3];
+  int h[3], w[3], stride[3];
+  float anchor[3][4][2];  // up to 4 anchors per level
+};
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long i) { return to_f32(p[i]); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layout, int batch, int na, int nc,
+                                                          float conf_thres, int multi_label,
+                                                          const uint32_t* __restrict__ class_mask,
+                                                          float* __restrict__ cand_box, float* __restrict__ cand_score,
+                                                          int* __restrict__ cand_cls, uint64_t* __restrict__ cand_key,
+                                                          int* __restrict__ cand_count, int cap,
+                                                          float* __restrict__ decoded) {
+  __shared__ int s_cnt, s_base;
+  const int no = nc + 5;
+  const int C = na * no;
+  const int n0 = na * hd.h[0] * hd.w[0], n1 = na * hd.h[1] * hd.w[1], n2 = na * hd.h[2] * hd.w[2];
+  const int N = n0 + n1 + n2;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int aidx = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = aidx < N;
+
+  // Candidate production: up to nc per thread in multi-label mode, 1 otherwise.
+  float box[4] = {0.f, 0.f, 0.f, 0.f};
+  float best = -1.f;
+  int best_c = 0;
+  bool pass = false;
+  int l = 0, rem = live ? aidx : 0;
+  if (rem >= n0) { rem -= n0; l = 1; if (rem >= n1) { rem -= n1; l = 2; } }
+  const int H = hd.h[l], W = hd.w[l];
+  const int a = rem / (H * W);
+  const int yx = rem - a * H * W;
+  const int y = yx / W, x = yx - y * W;
+  const T* hp = (const T*)hd.head[l];
+  long base, cstride;
+  if (layout == 0) {  // NCHW
+    base = ((long)b * C + (long)a * no) * H * W + yx;
+    cstride = (long)H * W;
+  } else {  // NHWC
+    base = ((long)b * H * W + yx) * C + (long)a * no;
+    cstride = 1;
+  }
+  float obj = 0.f;
+  if (live) {
+    obj = sigmoidf_(ld(hp, base + 4 * cstride));
+    const bool need_full = decoded != nullptr;
+    if (obj > conf_thres || need_full) {
+      const float sx = sigmoidf_(ld(hp, base)), sy = sigmoidf_(ld(hp, base + cstride));
+      const float sw = sigmoidf_(ld(hp, base + 2 * cstride)), sh = sigmoidf_(ld(hp, base + 3 * cstride));
+      const float st = (float)hd.stride[l];
+      const float cx = (sx * 2.f - 0.5f + (float)x) * st;
+      const float cy = (sy * 2.f - 0.5f + (float)y) * st;
+      const float bw = (sw * 2.f) * (sw * 2.f) * hd.anchor[l][a][0];
+      const float bh = (sh * 2.f) * (sh * 2.f) * hd.anchor[l][a][1];
+      box[0] = cx - bw * 0.5f; box[1] = cy - bh * 0.5f; box[2] = cx + bw * 0.5f; box[3] = cy + bh * 0.5f;
+      if (need_full) {
+        float* drow = decoded + ((long)b * N + aidx) * no;
+        drow[0] = cx; drow[1] = cy; drow[2] = bw; drow[3] = bh; drow[4] = obj;
+        for (int c = 0; c < nc; ++c) drow[5 + c] = sigmoidf_(ld(hp, base + (5 + c) * cstride));
+      }
+      if (obj > conf_thres && !multi_label) {
+        float m = -INFINITY;
+        int mc = 0;
+        for (int c = 0; c < nc; ++c) {
+          if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+          float v = ld(hp, base + (5 + c) * cstride);
+          if (v > m) { m = v; mc = c; }
+        }
+        if (m > -INFINITY) {
+          best = sigmoidf_(m) * obj;
+          best_c = mc;
+          pass = best > conf_thres;
+        }
+      }
+    }
+  }
+
+  if (!multi_label) {
+    // block-level compaction: one LDS atomic per passing thread, one global per block
+    int my = -1;
+    if (pass) my = atomicAdd(&s_cnt, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&cand_count[b], s_cnt) : 0;
+    __syncthreads();
+    if (pass) {
+      int slot = s_base + my;
+      if (slot < cap) {
+        long o = (long)b * cap + slot;
+        cand_box[o * 4 + 0] = box[0]; cand_box[o * 4 + 1] = box[1];
+        cand_box[o * 4 + 2] = box[2]; cand_box[o * 4 + 3] = box[3];
+        cand_score[o] = best; cand_cls[o] = best_c; cand_key[o] = make_score_key(best, (uint32_t)aidx);
+      }
+    }
+  } else if (live && obj > conf_thres) {
+    for (int c = 0; c < nc; ++c) {
+      if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+      float s = sigmoidf_(ld(hp, base + (5 + c) * cstride)) * obj;
+      if (s > conf_thres) {
+        int slot = atomicAdd(&cand_count[b], 1);
+        if (slot < cap) {
+          long o = (long)b * cap + slot;
+          cand_box[o * 4 + 0] = box[0]; cand_box[o * 4 + 1] = box[1];
+          cand_box[o * 4 + 2] = box[2]; cand_box[o * 4 + 3] = box[3];
+          cand_score[o] = s; cand_cls[o] = c; cand_key[o] = make_score_key(s, (uint32_t)(aidx * nc + c));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const void* head2, int dtype, int layout,
+                                   int batch, int na, int nc, const int* hw /*[6]*/, const int* strides /*[3]*/,
+                                   const float* anchors /*[3][na][2] host*/, float conf_thres, int multi_label,
+                                   const uint32_t* class_mask, float* cand_box, float* cand_score, int* cand_cls,
+                                   uint64_t* cand_key, int* cand_count, int cap, float* decoded,
+                                   hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (na > 4 || na <= 0) return (int)hipErrorInvalidValue;
+  YoloHeads hd;
+  hd.head[0] = head0; hd.head[1] = head1; hd.head[2] = head2;
+  for (int l = 0; l < 3; ++l) {
+    hd.h[l] = hw[2 * l]; hd.w[l] = hw[2 * l + 1]; hd.stride[l] = strides[l];
+    for (int a = 0; a < 4; ++a) {
+      hd.anchor[l][a][0] = a < na ? anchors[(l * na + a) * 2] : 0.f;
+      hd.anchor[l][a][1] = a < na ? anchors[(l * na + a) * 2 + 1] : 0.f;
+    }
+  }
+  hipError_t e = hipMemsetAsync(cand_count, 0, sizeof(int) * batch, stream);
+  if (e != hipSuccess) return (int)e;
+  long N = 0;
+  for (int l = 0; l < 3; ++l) N += (long)na * hd.h[l] * hd.w[l];
+  const int bs = 256;
+  dim3 grid((unsigned)((N + bs - 1) / bs), (unsigned)batch);
+  switch (dtype) {
+    case kF32:
+      yolo_filter_kernel<float><<<grid, bs, 0, stream>>>(hd, layout, batch, na, nc, conf_thres, multi_label, class_mask,
+                                                         cand_box, cand_score, cand_cls, cand_key, cand_count, cap, decoded);
+      break;
+    case kF16:
+      yolo_filter_kernel<__half><<<grid, bs, 0, stream>>>(hd, layout, batch, na, nc, conf_thres, multi_label, class_mask,
+                                                          cand_box, cand_score, cand_cls, cand_key, cand_count, cap, decoded);
+      break;
+    case kBF16:
+      yolo_filter_kernel<__hip_bfloat16><<<grid, bs, 0, stream>>>(hd, layout, batch, na, nc, conf_thres, multi_label,
+                                                                  class_mask, cand_box, cand_score, cand_cls, cand_key,
+                                                                  cand_count, cap, decoded);
+      break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  TCA_LAUNCH_CHECK();
+}

@@ -1,0 +1,139 @@
+"""ctypes bindings to the in-tree native libraries.
+
+Every op in ``triton_client_amd.ops`` dispatches on the tensor's device:
+GPU tensors go to the HIP kernels here — never silently to a PyTorch
+fallback; if the library is missing on a machine with a GPU the call raises
+(the CPU path exists only for CPU tensors, i.e. config 1 "CPU-only" runs and
+the GPU-less CI host).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+from . import _build
+
+_LOCK = threading.Lock()
+_KERNELS: Optional[ctypes.CDLL] = None
+_RUNTIME: Optional[ctypes.CDLL] = None
+_HIP: Optional[ctypes.CDLL] = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+
+# name -> argtypes (restype is always int = hipError_t)
+_KERNEL_SIGS = {
+    "tca_image_preprocess": [P, L, I, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P],
+    "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
+    "tca_topk_sort": [P, P, I, I, I, P, P, P],
+    "tca_nms_mask": [I, P, I, P, P, P, I, I, I, F, I, P, I, P],
+    "tca_nms_reduce": [P, P, P, I, I, P, I, P, P, I, I, P, P, P, P, P, P],
+    "tca_box_iou": [P, I, P, I, P, P],
+    "tca_pc2_unpack": [P, P, P, I, I, I, P, P, I, F, P, I, P, P, P, P],
+    "tca_pc2_blocks_per_frame": [I],
+    "tca_vox_blocks_per_frame": [I],
+    "tca_voxelize": [P, I, I, P, I, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P],
+    "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
+    "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
+    "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, P],
+    "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load_hip() -> ctypes.CDLL:
+    global _HIP
+    if _HIP is None:
+        for cand in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+            try:
+                _HIP = ctypes.CDLL(cand)
+                break
+            except OSError:
+                continue
+        if _HIP is not None:
+            _HIP.hipGetErrorString.restype = ctypes.c_char_p
+            _HIP.hipGetErrorString.argtypes = [I]
+    return _HIP
+
+
+def _lib_path(name: str) -> str:
+    return os.path.join(_build.LIBDIR, name)
+
+
+def kernels(auto_build: bool = True) -> ctypes.CDLL:
+    """The HIP kernel library. Builds it in-tree if missing (hipcc present)."""
+    global _KERNELS
+    if _KERNELS is not None:
+        return _KERNELS
+    with _LOCK:
+        if _KERNELS is not None:
+            return _KERNELS
+        path = _lib_path("libtca_kernels.so")
+        if not os.path.exists(path) and auto_build:
+            _build.build(verbose=False)
+        if not os.path.exists(path):
+            raise NativeError(f"{path} is missing: run `python -m triton_client_amd._build` (hipcc, gfx950)")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _KERNEL_SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = I
+        _KERNELS = lib
+        return lib
+
+
+def runtime(auto_build: bool = True) -> ctypes.CDLL:
+    global _RUNTIME
+    if _RUNTIME is not None:
+        return _RUNTIME
+    with _LOCK:
+        if _RUNTIME is not None:
+            return _RUNTIME
+        path = _lib_path("libtca_runtime.so")
+        if not os.path.exists(path) and auto_build:
+            _build.build(verbose=False)
+        if not os.path.exists(path):
+            raise NativeError(f"{path} is missing: run `python -m triton_client_amd._build`")
+        _RUNTIME = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        from . import _runtime_sigs  # noqa: F401  (declares argtypes)
+        _runtime_sigs.declare(_RUNTIME)
+        return _RUNTIME
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        hip = _load_hip()
+        msg = hip.hipGetErrorString(rc).decode() if hip is not None else f"code {rc}"
+        raise NativeError(f"{what} failed: {msg} ({rc})")
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(kernels(), name)
+    check(fn(*args), name)
+
+
+def ptr(t) -> int:
+    """Device/host pointer of a tensor (0 for None)."""
+    return 0 if t is None else int(t.data_ptr())
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False

@@ -1,0 +1,105 @@
+"""K1 — camera frame preprocessing (resize/letterbox + normalise + layout).
+
+Reference: ``communicator/ros_inference.py:131-141`` (decode, BGR→RGB flip,
+``cv2.resize`` stretch to the model size) and
+``clients/preprocess/yolov5_preprocess.py:20-24`` (HWC→CHW, fp32, /255);
+``clients/preprocess/detectron_preprocess.py:20-24`` (no /255);
+``utils/preprocess.py:147-157`` (INCEPTION / VGG / COCO scaling — the only
+implementation of the CLI's ``-s`` flag).
+
+Fixes vs reference: the reference passes (H, W) to
+``cv2.resize``'s (W, H) — wrong for non-square models; here dst is always
+(H, W).  ``mode="letterbox"`` adds the aspect-preserving YOLOv5 letterbox.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native
+from . import golden
+from ._ws import DTYPE_CODE
+
+SCALING_PRESETS = {
+    # name: (scale per channel, bias per channel)
+    "COCO": ((1 / 255.0,) * 3, (0.0,) * 3),
+    "YOLO": ((1 / 255.0,) * 3, (0.0,) * 3),
+    "NONE": ((1.0,) * 3, (0.0,) * 3),
+    "INCEPTION": ((1 / 127.5,) * 3, (-1.0,) * 3),
+    "VGG": ((1.0,) * 3, (-123.0, -117.0, -104.0)),
+}
+
+
+@dataclass
+class FrameXform:
+    """How model-input pixels map back to the original frame (for boxes)."""
+    gain_x: float
+    gain_y: float
+    pad_x: float
+    pad_y: float
+    orig_w: int
+    orig_h: int
+
+    def as_list(self):
+        return [self.gain_x, self.gain_y, self.pad_x, self.pad_y, float(self.orig_w), float(self.orig_h)]
+
+    def unmap_boxes(self, boxes: np.ndarray) -> np.ndarray:
+        b = boxes.astype(np.float32).copy()
+        b[:, [0, 2]] = np.clip((b[:, [0, 2]] - self.pad_x) / self.gain_x, 0, self.orig_w)
+        b[:, [1, 3]] = np.clip((b[:, [1, 3]] - self.pad_y) / self.gain_y, 0, self.orig_h)
+        return b
+
+
+def frame_xform(src_hw: Tuple[int, int], dst_hw: Tuple[int, int], mode: str) -> Tuple[FrameXform, tuple]:
+    top, left, nh, nw, gx, gy = golden.letterbox_params(src_hw, dst_hw, mode)
+    return FrameXform(gx, gy, float(left), float(top), src_hw[1], src_hw[0]), (top, left, nh, nw)
+
+
+def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stretch",
+               scaling: str | Tuple[Sequence[float], Sequence[float]] = "COCO", dtype: torch.dtype = torch.float32,
+               layout: str = "NCHW", out_channels: int = 3, swap_rb: bool = False, pad_value: float = 114.0,
+               quantize_u8: bool = True, out: torch.Tensor | None = None, stream=None):
+    """frames: [B, H, W, C>=3] uint8 (or [H, W, C]). Returns (tensor, FrameXform).
+
+    layout "NCHW" → [B, C, H, W] contiguous; "NHWC" → [B, C, H, W] view of a
+    channels_last buffer (C = out_channels, 3 or 4; the 4th channel is 0).
+    """
+    if frames.dim() == 3:
+        frames = frames.unsqueeze(0)
+    B, h0, w0, c0 = frames.shape
+    H, W = dst_hw
+    scale, bias = SCALING_PRESETS[scaling.upper()] if isinstance(scaling, str) else scaling
+    xf, (top, left, nh, nw) = frame_xform((h0, w0), (H, W), mode)
+    if frames.device.type == "cuda":
+        frames = frames.contiguous()
+        if out is None:
+            if layout == "NCHW":
+                out = torch.empty((B, out_channels, H, W), dtype=dtype, device=frames.device)
+            else:
+                out = torch.empty((B, H, W, out_channels), dtype=dtype, device=frames.device).permute(0, 3, 1, 2)
+        _native.call(
+            "tca_image_preprocess", _native.ptr(frames), h0 * w0 * c0, h0, w0, w0 * c0, c0, int(swap_rb),
+            _native.ptr(out), DTYPE_CODE[dtype], 0 if layout == "NCHW" else 1, out_channels, H, W, B, top, left,
+            nh, nw, float(pad_value), int(quantize_u8), float(scale[0]), float(scale[1]), float(scale[2]),
+            float(bias[0]), float(bias[1]), float(bias[2]), _native.stream_ptr(stream))
+        return out, xf
+    # CPU path (config 1 / GPU-less host)
+    res = []
+    for b in range(B):
+        img = frames[b].numpy()
+        o = golden.preprocess_image(img, (H, W), mode, scale, bias, swap_rb, pad_value, "NHWC")
+        if out_channels == 4:
+            o = np.concatenate([o, np.zeros_like(o[..., :1])], -1)
+        res.append(o)
+    arr = torch.from_numpy(np.stack(res)).to(dtype)
+    if layout == "NCHW":
+        t = arr.permute(0, 3, 1, 2).contiguous()
+    else:
+        t = arr.permute(0, 3, 1, 2)
+    if out is not None:
+        out.copy_(t)
+        return out, xf
+    return t, xf

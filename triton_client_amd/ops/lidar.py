@@ -1,0 +1,332 @@
+"""LiDAR per-frame ops: PointCloud2 unpack (K6), voxelisation (K7), fused
+PillarVFE + BEV scatter (K8/K9), anchor decode (K11) + rotated-IoU NMS (K10).
+
+GPU tensors run the HIP kernels (``csrc/kernels/{pointcloud,voxelize,pillars,
+anchors,nms}.hip``); CPU tensors run vectorised NumPy with identical
+semantics (tested against ``golden``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..config.lidar import PointPillarsConfig, VoxelConfig, anchor_grid
+from . import golden
+from ._ws import Workspace, dtype_code, layout_of
+from .nms import Candidates, NmsResult, SORT_CAP, sort_and_nms, sort_and_nms_cpu
+
+INT_MAX = 0x7FFFFFFF
+
+# sensor_msgs/PointField datatype codes
+PF_INT8, PF_UINT8, PF_INT16, PF_UINT16, PF_INT32, PF_UINT32, PF_FLOAT32, PF_FLOAT64 = range(1, 9)
+PF_NP = {1: np.int8, 2: np.uint8, 3: np.int16, 4: np.uint16, 5: np.int32, 6: np.uint32, 7: np.float32, 8: np.float64}
+
+
+def _carr(ctype, vals):
+    return (ctype * len(vals))(*vals)
+
+
+# ----------------------------------------------------------------------------- K6
+@dataclass
+class PointLayout:
+    point_step: int
+    offsets: Tuple[int, int, int, int]  # x, y, z, intensity
+    dtypes: Tuple[int, int, int, int]
+
+    @staticmethod
+    def xyzi_f32(point_step: int = 16) -> "PointLayout":
+        return PointLayout(point_step, (0, 4, 8, 12), (PF_FLOAT32,) * 4)
+
+
+def pc2_unpack(ws: Optional[Workspace], data: torch.Tensor, frame_off: torch.Tensor, frame_n: torch.Tensor,
+               layout: PointLayout, max_points: int, normalize_intensity: bool = True, z_offset: float = 0.0,
+               out_stride: int = 4, stream=None):
+    """data: uint8 bytes of B PointCloud2 payloads; frame_off [B] int64 byte
+    offsets, frame_n [B] int32 point counts.  Returns (points [B, max_points,
+    out_stride] fp32, count [B] int32).  Semantics of
+    ``read_points(skip_nans=True)`` + ``i /= max(i)`` + ``z += z_offset``
+    (reference ros_inference3d.py:125-128)."""
+    B = frame_n.shape[0]
+    if data.device.type == "cuda":
+        out = ws.get("pc2_points", (B, max_points, out_stride), torch.float32)
+        cnt = ws.get("pc2_count", (B,), torch.int32)
+        bpf = _native.kernels().tca_pc2_blocks_per_frame(max_points)
+        blk = ws.get("pc2_blocks", (B, bpf), torch.int32)
+        imax = ws.get("pc2_imax", (B,), torch.int32)
+        _native.call("tca_pc2_unpack", _native.ptr(data), _native.ptr(frame_off), _native.ptr(frame_n), B, max_points,
+                     layout.point_step, _carr(ctypes.c_int, layout.offsets), _carr(ctypes.c_int, layout.dtypes),
+                     int(normalize_intensity), float(z_offset), _native.ptr(out), out_stride, _native.ptr(cnt),
+                     _native.ptr(blk), _native.ptr(imax), _native.stream_ptr(stream))
+        return out, cnt
+    raw = data.numpy()
+    offs, ns = frame_off.numpy(), frame_n.numpy()
+    out = np.zeros((B, max_points, out_stride), np.float32)
+    cnt = np.zeros((B,), np.int32)
+    for b in range(B):
+        n = min(int(ns[b]), max_points)
+        rec = raw[int(offs[b]):int(offs[b]) + n * layout.point_step].reshape(n, layout.point_step)
+        cols = []
+        for off, dt in zip(layout.offsets, layout.dtypes):
+            w = np.dtype(PF_NP[dt]).itemsize
+            cols.append(rec[:, off:off + w].copy().view(PF_NP[dt]).reshape(-1).astype(np.float32))
+        p = np.stack(cols, 1)
+        p = p[~np.isnan(p).any(1)]
+        if normalize_intensity and len(p):
+            m = p[:, 3].max()
+            if m > 0 and np.isfinite(m):
+                p[:, 3] = p[:, 3] * np.float32(1.0 / m)
+        p[:, 2] += np.float32(z_offset)
+        out[b, :len(p), :4] = p
+        cnt[b] = len(p)
+    return torch.from_numpy(out), torch.from_numpy(cnt)
+
+
+# ----------------------------------------------------------------------------- K7
+def voxelize_np(points: np.ndarray, cfg: VoxelConfig, nfeat: Optional[int] = None):
+    """Vectorised spconv-semantics voxeliser (one frame). Returns
+    voxels [V, P, F], coords [V, 3] (z, y, x), num_points [V], plus per-voxel
+    sorted point indices [V, P] (-1 padded)."""
+    F = nfeat or points.shape[1]
+    r = np.asarray(cfg.point_cloud_range, np.float32)
+    vs = np.asarray(cfg.voxel_size, np.float32)
+    nx, ny, nz = cfg.grid_size
+    P, V = cfg.max_points_per_voxel, cfg.max_voxels
+    c = np.floor((points[:, :3] - r[:3]) / vs).astype(np.int64)
+    ok = (c >= 0).all(1) & (c[:, 0] < nx) & (c[:, 1] < ny) & (c[:, 2] < nz)
+    pidx = np.nonzero(ok)[0]
+    cell = (c[pidx, 2] * ny + c[pidx, 1]) * nx + c[pidx, 0]
+    uniq, first, inv = np.unique(cell, return_index=True, return_inverse=True)
+    rank_of_uniq = np.empty(len(uniq), np.int64)
+    rank_of_uniq[np.argsort(first, kind="stable")] = np.arange(len(uniq))
+    vid = rank_of_uniq[inv]
+    nvox = min(len(uniq), V)
+    keep = vid < nvox
+    pidx, vid = pidx[keep], vid[keep]
+    order = np.argsort(vid, kind="stable")  # stable → point order within voxel
+    vid_s, pidx_s = vid[order], pidx[order]
+    starts = np.searchsorted(vid_s, np.arange(nvox))
+    rank = np.arange(len(vid_s)) - starts[vid_s]
+    sel = rank < P
+    voxels = np.zeros((nvox, P, F), np.float32)
+    slots = np.full((nvox, P), -1, np.int64)
+    voxels[vid_s[sel], rank[sel]] = points[pidx_s[sel], :F]
+    slots[vid_s[sel], rank[sel]] = pidx_s[sel]
+    num = np.bincount(vid_s, minlength=nvox)[:nvox]
+    num = np.minimum(num, P).astype(np.int32)
+    ucell = np.empty(nvox, np.int64)
+    ucell[rank_of_uniq[rank_of_uniq < nvox]] = uniq[rank_of_uniq < nvox]
+    coords = np.stack([ucell // (nx * ny), (ucell // nx) % ny, ucell % nx], 1).astype(np.int32)
+    return voxels, coords, num, slots
+
+
+class Voxelizer:
+    """Batched voxeliser with persistent, self-resetting GPU scratch."""
+
+    def __init__(self, cfg: VoxelConfig, batch: int, max_points: int, device="cuda", nfeat: Optional[int] = None,
+                 materialize: bool = True):
+        self.cfg, self.B, self.max_points = cfg, batch, max_points
+        self.device = torch.device(device)
+        self.nfeat = nfeat or cfg.num_point_features
+        self.materialize = materialize
+        if self.device.type == "cuda":
+            self.ws = Workspace(self.device)
+            cells = cfg.num_cells
+            V, P = cfg.max_voxels, cfg.max_points_per_voxel
+            g = self.ws.get
+            self.cell_first = g("cell_first", (batch, cells), torch.int32, init=INT_MAX)
+            self.cell_vid = g("cell_vid", (batch, cells), torch.int32, init=-1)
+            self.point_cell = g("point_cell", (batch, max_points), torch.int32)
+            bpf = _native.kernels().tca_vox_blocks_per_frame(max_points)
+            self.block_count = g("block_count", (batch, bpf), torch.int32)
+            self.slots = g("slots", (batch, V, P), torch.int32, init=INT_MAX)
+            self.vcount = g("vcount", (batch, V), torch.int32, init=0)
+            self.voxels = g("voxels", (batch, V, P, self.nfeat), torch.float32, init=0) if materialize else None
+            self.coords = g("coords", (batch, V, 4), torch.int32, init=0)
+            self.num_points = g("num_points", (batch, V), torch.int32, init=0)
+            self.voxel_count = g("voxel_count", (batch,), torch.int32, init=0)
+            self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
+            self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
+            self._grid = _carr(ctypes.c_int, cfg.grid_size)
+
+    def _launch(self, points, npts, mode, gather, stream):
+        cfg = self.cfg
+        _native.call("tca_voxelize", _native.ptr(points), points.shape[-1], self.max_points, _native.ptr(npts),
+                     points.shape[0], self._range, self._vsize, self._grid, cfg.max_points_per_voxel,
+                     cfg.max_voxels, self.nfeat, _native.ptr(self.cell_first), _native.ptr(self.cell_vid),
+                     _native.ptr(self.point_cell), _native.ptr(self.block_count), _native.ptr(self.slots),
+                     _native.ptr(self.vcount), _native.ptr(self.voxels), _native.ptr(self.coords),
+                     _native.ptr(self.num_points), _native.ptr(self.voxel_count), mode, int(gather),
+                     _native.stream_ptr(stream))
+
+    def assign(self, points: torch.Tensor, npts: torch.Tensor, stream=None) -> None:
+        """Stage a-c: voxel ids, coords, sorted slot lists (GPU only)."""
+        self._launch(points, npts, 1, False, stream)
+
+    def finish(self, points: torch.Tensor, npts: torch.Tensor, gather: bool, stream=None) -> None:
+        """Stage d: (optionally) gather voxels, write num_points, reset scratch."""
+        self._launch(points, npts, 2, gather and self.materialize, stream)
+
+    def __call__(self, points: torch.Tensor, npts: torch.Tensor, stream=None):
+        """points [B, max_points, F], npts [B] → (voxels [B,V,P,F], coords [B,V,4]
+        (b,z,y,x), num_points [B,V], voxel_count [B]).  Rows >= voxel_count are
+        stale/padding."""
+        if points.device.type == "cuda":
+            self._launch(points, npts, 3, True, stream)
+            return self.voxels, self.coords, self.num_points, self.voxel_count
+        cfg = self.cfg
+        B = points.shape[0]
+        V, P = cfg.max_voxels, cfg.max_points_per_voxel
+        vox = np.zeros((B, V, P, self.nfeat), np.float32)
+        co = np.zeros((B, V, 4), np.int32)
+        nump = np.zeros((B, V), np.int32)
+        vc = np.zeros((B,), np.int32)
+        pn = points.numpy()
+        for b in range(B):
+            v, c, n, _ = voxelize_np(pn[b, :int(npts[b])], cfg, self.nfeat)
+            k = len(n)
+            vox[b, :k], nump[b, :k], vc[b] = v, n, k
+            co[b, :k, 0] = b
+            co[b, :k, 1:] = c
+        return torch.from_numpy(vox), torch.from_numpy(co), torch.from_numpy(nump), torch.from_numpy(vc)
+
+
+# ----------------------------------------------------------------------------- K8/K9
+class PillarEncoder:
+    """Fused PillarVFE (BN folded) + scatter into an NHWC bf16 BEV canvas."""
+
+    def __init__(self, cfg: VoxelConfig, weight: torch.Tensor, bias: torch.Tensor, batch: int, device="cuda",
+                 channels: int = 64):
+        self.cfg, self.B, self.C = cfg, batch, channels
+        self.device = torch.device(device)
+        self.W = weight.detach().float().contiguous().to(self.device)  # [64, 10]
+        self.b = bias.detach().float().contiguous().to(self.device)
+        nx, ny, _ = cfg.grid_size
+        self.nx, self.ny = nx, ny
+        if self.device.type == "cuda":
+            self.ws = Workspace(self.device)
+            # NHWC canvas, zero-initialised once; cleared per frame by cell list
+            self.canvas = self.ws.get("canvas", (batch, ny, nx, channels), torch.bfloat16, init=0)
+            self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
+            self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
+
+    def canvas_nchw(self) -> torch.Tensor:
+        return self.canvas.permute(0, 3, 1, 2)  # channels_last view
+
+    def clear(self, vox: Voxelizer, stream=None) -> None:
+        """Zero the cells written for the voxels currently in ``vox`` (call
+        before the voxeliser overwrites its coords with the next frame)."""
+        _native.call("tca_pillar_canvas_clear", _native.ptr(vox.coords), _native.ptr(vox.voxel_count), self.B,
+                     self.cfg.max_voxels, self.nx, self.ny, self.C, _native.ptr(self.canvas),
+                     _native.stream_ptr(stream))
+
+    def encode_from_slots(self, points: torch.Tensor, vox: Voxelizer, feat_out: Optional[torch.Tensor] = None,
+                          stream=None) -> torch.Tensor:
+        _native.call("tca_pillar_vfe_slots", _native.ptr(points), points.shape[-1], vox.max_points,
+                     _native.ptr(vox.slots), _native.ptr(vox.vcount), _native.ptr(vox.coords),
+                     _native.ptr(vox.voxel_count), self.B, self.cfg.max_voxels, self.cfg.max_points_per_voxel,
+                     _native.ptr(self.W), _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny,
+                     _native.ptr(self.canvas), _native.ptr(feat_out), _native.stream_ptr(stream))
+        return self.canvas_nchw()
+
+    def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
+        _native.call("tca_pillar_vfe_voxels", _native.ptr(voxels), _native.ptr(num_points), _native.ptr(coords),
+                     _native.ptr(voxel_count), self.B, voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
+                     _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas),
+                     _native.ptr(feat_out), _native.stream_ptr(stream))
+        return self.canvas_nchw()
+
+
+def pillar_features_reference(voxels: torch.Tensor, num_points: torch.Tensor, coords: torch.Tensor,
+                              cfg: VoxelConfig, W: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """fp32 PyTorch reference of the fused kernel's per-pillar output."""
+    from ..models.pointpillars import pillar_point_features
+    f = pillar_point_features(voxels.float(), num_points, coords, cfg)
+    return torch.relu(f @ W.t().float() + b.float()).max(dim=1).values
+
+
+# ----------------------------------------------------------------------------- K11 + K10
+class AnchorPostprocess:
+    """PointPillars head → boxes: decode + score filter + top-k + rotated NMS."""
+
+    def __init__(self, cfg: PointPillarsConfig, batch: int, device="cuda"):
+        self.cfg, self.B = cfg, batch
+        self.device = torch.device(device)
+        x0, xs, y0, ys, table = anchor_grid(cfg)
+        self.x0, self.xs, self.y0, self.ys = x0, xs, y0, ys
+        self.table = np.asarray(table, np.float32)  # [A, 6]
+        self._table = _carr(ctypes.c_float, self.table.flatten().tolist())
+        self.H, self.W = cfg.feature_map_size
+        self.A = cfg.num_anchors_per_loc
+        self.C = cfg.num_classes
+        self.cap = min(self.H * self.W * self.A, 1 << 20)
+        if self.device.type == "cuda":
+            self.ws = Workspace(self.device)
+
+    def __call__(self, cls: torch.Tensor, box: torch.Tensor, dir_: torch.Tensor, stream=None) -> NmsResult:
+        if cls.device.type != "cuda":
+            return self.cpu(cls, box, dir_)
+        cfg = self.cfg
+        lay, c = layout_of(cls)
+        b_ = layout_of(box)[1]
+        d_ = layout_of(dir_)[1]
+        if layout_of(box)[0] != lay or layout_of(dir_)[0] != lay:
+            c, b_, d_, lay = cls.contiguous(), box.contiguous(), dir_.contiguous(), 0
+        B = c.shape[0]
+        cand = Candidates.alloc(self.ws, "anc_", B, self.cap, 7)
+        _native.call("tca_anchor_decode_filter", _native.ptr(c), _native.ptr(b_), _native.ptr(d_), dtype_code(c), lay,
+                     B, self.H, self.W, self.A, self.C, cfg.num_dir_bins, self._table, float(self.x0),
+                     float(self.xs), float(self.y0), float(self.ys), float(cfg.dir_offset),
+                     float(cfg.dir_limit_offset), float(cfg.score_thresh), _native.ptr(cand.box),
+                     _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count),
+                     self.cap, _native.stream_ptr(stream))
+        return sort_and_nms(self.ws, cand, 1, cfg.nms_thresh, cfg.nms_pre_max, cfg.nms_post_max, True, None,
+                            prefix="anc_nms_", stream=stream)
+
+    def decode_cpu(self, cls, box, dir_):
+        """Reference decode (OpenPCDet semantics) → (boxes [B, N, 7], scores, labels)."""
+        cfg = self.cfg
+        B = cls.shape[0]
+        H, W, A, C = self.H, self.W, self.A, self.C
+        cl = cls.float().permute(0, 2, 3, 1).reshape(B, H * W * A, C)
+        bx = box.float().permute(0, 2, 3, 1).reshape(B, H * W * A, 7)
+        dr = dir_.float().permute(0, 2, 3, 1).reshape(B, H * W * A, cfg.num_dir_bins)
+        t = torch.from_numpy(self.table)
+        ys_, xs_ = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+        xa = (self.x0 + xs_.float() * self.xs).reshape(-1, 1).expand(-1, A).reshape(-1)
+        ya = (self.y0 + ys_.float() * self.ys).reshape(-1, 1).expand(-1, A).reshape(-1)
+        tt = t.repeat(H * W, 1)
+        dxa, dya, dza, za, ra, diag = tt.unbind(1)
+        out = torch.stack([bx[..., 0] * diag + xa, bx[..., 1] * diag + ya, bx[..., 2] * dza + za,
+                           torch.exp(bx[..., 3]) * dxa, torch.exp(bx[..., 4]) * dya, torch.exp(bx[..., 5]) * dza,
+                           bx[..., 6] + ra], -1)
+        period = 2 * np.pi / cfg.num_dir_bins
+        dl = dr.argmax(-1).float()
+        val = out[..., 6] - cfg.dir_offset
+        lim = val - torch.floor(val / period + cfg.dir_limit_offset) * period
+        out[..., 6] = lim + cfg.dir_offset + period * dl
+        score, lab = torch.sigmoid(cl).max(-1)
+        return out, score, lab.int() + 1
+
+    def cpu(self, cls, box, dir_) -> NmsResult:
+        cfg = self.cfg
+        boxes, scores, labels = self.decode_cpu(cls, box, dir_)
+        B = boxes.shape[0]
+        mo = cfg.nms_post_max
+        ob = np.zeros((B, mo, 7), np.float32)
+        os_ = np.zeros((B, mo), np.float32)
+        oc = np.zeros((B, mo), np.int32)
+        cnt = np.zeros((B,), np.int32)
+        for b in range(B):
+            s = scores[b].numpy()
+            idx = np.nonzero(s >= cfg.score_thresh)[0]
+            keep = sort_and_nms_cpu(boxes[b].numpy()[idx], s[idx], labels[b].numpy()[idx], idx, 1, cfg.nms_thresh,
+                                    cfg.nms_pre_max, mo, True)
+            k = idx[keep]
+            n = len(k)
+            ob[b, :n], os_[b, :n], oc[b, :n], cnt[b] = boxes[b].numpy()[k], s[k], labels[b].numpy()[k], n
+        return NmsResult(torch.from_numpy(ob), torch.from_numpy(os_), torch.from_numpy(oc), torch.from_numpy(cnt))

@@ -1,0 +1,147 @@
+"""YOLOv5 postprocess: Detect decode + candidate filter (K3) + top-k/NMS (K4)
++ box rescale to the original frame, as one device-resident chain.
+
+Reference: ``clients/postprocess/yolov5_postprocess.py:28-125`` and the box
+rescale at ``communicator/ros_inference.py:100-115``.  Fixes (SURVEY
+Appendix A5/A10): an empty result is an empty detection set (the reference
+returns the AssertionError object); output dtypes follow the data.
+
+Deviations, documented: candidates beyond 8192 per image are cut to the top
+8192 by score before NMS (reference: 30000); merge-NMS (off by default in the
+reference, ``merge = False``) is only available on the CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.yolov5 import STRIDES
+from . import golden
+from ._ws import Workspace, dtype_code, layout_of
+from .image import FrameXform
+from .nms import Candidates, NmsResult, SORT_CAP, sort_and_nms
+
+
+class YoloPostprocess:
+    def __init__(self, nc: int, anchors: torch.Tensor | Sequence, img_hw=(640, 640), conf_thres: float = 0.3,
+                 iou_thres: float = 0.45, max_det: int = 300, max_nms: int = 8192, agnostic: bool = False,
+                 multi_label: bool = False, classes: Optional[Sequence[int]] = None, device="cuda"):
+        self.nc = nc
+        a = torch.as_tensor(anchors, dtype=torch.float32).reshape(3, -1, 2)
+        self.anchors = a.cpu()
+        self.na = a.shape[1]
+        self.img_hw = tuple(img_hw)
+        self.conf_thres, self.iou_thres = conf_thres, iou_thres
+        self.max_det, self.max_nms = max_det, min(max_nms, SORT_CAP)
+        self.agnostic, self.multi_label = agnostic, multi_label
+        self.classes = None if classes is None else list(classes)
+        self.device = torch.device(device)
+        self.ws = Workspace(self.device) if self.device.type == "cuda" else None
+        grids = [(self.img_hw[0] // s, self.img_hw[1] // s) for s in STRIDES]
+        self.hw = (ctypes.c_int * 6)(*[v for g in grids for v in g])
+        self.strides = (ctypes.c_int * 3)(*STRIDES)
+        self.anc = (ctypes.c_float * a.numel())(*a.flatten().tolist())
+        self.num_anchors_total = sum(self.na * gh * gw for gh, gw in grids)
+        self._class_mask = None
+        if self.classes is not None and self.ws is not None:
+            words = (nc + 31) // 32
+            m = np.zeros(words, np.uint32)
+            for c in self.classes:
+                m[c >> 5] |= np.uint32(1 << (c & 31))
+            self._class_mask = torch.from_numpy(m.view(np.int32)).to(self.device)
+
+    # -------------------------------------------------------------- GPU
+    def __call__(self, heads: List[torch.Tensor], xform: Optional[FrameXform] = None, decoded_out: bool = False,
+                 stream=None):
+        """heads: 3 raw head maps [B, na*(5+nc), H, W] (NCHW or channels_last).
+        Returns NmsResult with box [B, max_det, 4] (xyxy, original-frame pixels if
+        xform given), score, cls, count — and the decoded [B, N, 5+nc] tensor
+        when decoded_out (KServe contract)."""
+        if heads[0].device.type != "cuda":
+            return self.cpu(heads, xform)
+        lay, h0 = layout_of(heads[0])
+        hs = [h0] + [layout_of(h)[1] for h in heads[1:]]
+        if any(layout_of(h)[0] != lay for h in hs):
+            hs = [h.contiguous() for h in hs]
+            lay = 0
+        B = hs[0].shape[0]
+        cap = self.num_anchors_total * (self.nc if self.multi_label else 1)
+        cap = min(cap, 1 << 20)
+        cand = Candidates.alloc(self.ws, "yolo_", B, cap, 4)
+        decoded = None
+        if decoded_out:
+            decoded = self.ws.get("decoded", (B, self.num_anchors_total, self.nc + 5), torch.float32)
+        _native.call("tca_yolo_decode_filter", _native.ptr(hs[0]), _native.ptr(hs[1]), _native.ptr(hs[2]),
+                     dtype_code(hs[0]), lay, B, self.na, self.nc, self.hw, self.strides, self.anc,
+                     float(self.conf_thres), int(self.multi_label), _native.ptr(self._class_mask),
+                     _native.ptr(cand.box), _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key),
+                     _native.ptr(cand.count), cap, _native.ptr(decoded), _native.stream_ptr(stream))
+        res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
+                           xform.as_list() if xform is not None else None, prefix="yolo_nms_", stream=stream)
+        return (res, decoded) if decoded_out else res
+
+    # -------------------------------------------------------------- CPU
+    def decode_cpu(self, heads: List[torch.Tensor]) -> torch.Tensor:
+        from ..models.yolov5 import yolo_decode_reference
+        return yolo_decode_reference([h.float().contiguous() for h in heads], self.anchors)
+
+    def cpu(self, heads, xform: Optional[FrameXform] = None) -> NmsResult:
+        return self.postprocess_decoded(self.decode_cpu(heads).numpy(), xform)
+
+    def postprocess_decoded(self, pred: np.ndarray, xform: Optional[FrameXform] = None) -> NmsResult:
+        """Reference-semantics postprocess of a decoded [B, N, 5+nc] array (what
+        a KServe YOLOv5 returns).  Vectorised NumPy, class-aware greedy NMS."""
+        B, N, no = pred.shape
+        nc = no - 5
+        outs = []
+        for b in range(B):
+            x = pred[b]
+            idx = np.nonzero(x[:, 4] > self.conf_thres)[0]
+            x = x[idx]
+            if self.classes is not None:
+                allowed = np.zeros(nc, bool)
+                allowed[self.classes] = True
+            cls_conf = x[:, 5:] * x[:, 4:5]
+            box = np.stack([x[:, 0] - x[:, 2] / 2, x[:, 1] - x[:, 3] / 2, x[:, 0] + x[:, 2] / 2,
+                            x[:, 1] + x[:, 3] / 2], 1).astype(np.float32)
+            if self.multi_label:
+                ii, jj = np.nonzero(cls_conf > self.conf_thres)
+                if self.classes is not None:
+                    keep = allowed[jj]
+                    ii, jj = ii[keep], jj[keep]
+                bx, sc, cl, tie = box[ii], cls_conf[ii, jj].astype(np.float32), jj, idx[ii] * nc + jj
+            else:
+                if self.classes is not None:
+                    cls_conf = np.where(allowed[None, :], cls_conf, -1.0)
+                j = cls_conf.argmax(1) if len(cls_conf) else np.zeros((0,), np.int64)
+                conf = cls_conf[np.arange(len(j)), j].astype(np.float32)
+                sel = conf > self.conf_thres
+                bx, sc, cl, tie = box[sel], conf[sel], j[sel], idx[sel]
+            from .nms import sort_and_nms_cpu
+            keep = sort_and_nms_cpu(bx, sc, cl.astype(np.int32), tie, 0, self.iou_thres, self.max_nms,
+                                    self.max_det, self.agnostic)
+            kb = bx[keep]
+            if xform is not None:
+                kb = xform.unmap_boxes(kb)
+            outs.append((kb, sc[keep], cl[keep].astype(np.int32)))
+        md = self.max_det
+        box = np.zeros((B, md, 4), np.float32)
+        score = np.zeros((B, md), np.float32)
+        cls = np.zeros((B, md), np.int32)
+        count = np.zeros((B,), np.int32)
+        for b, (kb, ks, kc) in enumerate(outs):
+            n = len(ks)
+            box[b, :n], score[b, :n], cls[b, :n], count[b] = kb, ks, kc, n
+        return NmsResult(torch.from_numpy(box), torch.from_numpy(score), torch.from_numpy(cls), torch.from_numpy(count))
+
+
+def detections_nx6(res: NmsResult) -> List[np.ndarray]:
+    """Reference output format: per image [n, 6] = x1, y1, x2, y2, conf, cls."""
+    out = []
+    for d in res.per_image():
+        out.append(np.concatenate([d["box"], d["score"][:, None], d["cls"][:, None].astype(np.float32)], 1))
+    return out
