@@ -111,4 +111,7 @@ __device__ __forceinline__ uint64_t make_score_key(float score, uint32_t idx) {
   return ((uint64_t)float_to_ordered(score) << 32) | (uint64_t)(0xffffffffu - idx);
 }
 
+// Zero n ints on `stream` with a kernel (graph-capture safe; see util.hip).
+int zero_i32_async(int* p, int n, hipStream_t stream);
+
 }  // namespace tca

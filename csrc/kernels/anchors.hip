@@ -113,8 +113,8 @@ TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const voi
   AnchorTable tb;
   for (int a = 0; a < 8; ++a)
     for (int k = 0; k < 6; ++k) tb.v[a][k] = a < A ? table[a * 6 + k] : 0.f;
-  hipError_t e = hipMemsetAsync(cand_count, 0, sizeof(int) * batch, stream);
-  if (e != hipSuccess) return (int)e;
+  int e = zero_i32_async(cand_count, batch, stream);
+  if (e) return e;
   dim3 grid((H * W * A + 255) / 256, batch);
 #define LAUNCH(T)                                                                                              \
   anchor_decode_kernel<T><<<grid, 256, 0, stream>>>((const T*)cls, (const T*)box, (const T*)dir, layout, H, W, A, C, \

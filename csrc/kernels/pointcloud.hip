@@ -156,8 +156,8 @@ TCA_API int tca_pc2_unpack(const void* data, const long* frame_off, const int* f
   FieldDesc fd;
   for (int f = 0; f < 4; ++f) { fd.off[f] = field_off[f]; fd.dtype[f] = field_dtype[f]; }
   const int bpf = (max_points + kPtsPerBlock - 1) / kPtsPerBlock;
-  hipError_t e = hipMemsetAsync(frame_imax, 0, sizeof(uint32_t) * batch, stream);
-  if (e != hipSuccess) return (int)e;
+  int e = zero_i32_async((int*)frame_imax, batch, stream);
+  if (e) return e;
   dim3 grid(bpf, batch);
   const uint8_t* d = (const uint8_t*)data;
   pc2_count_kernel<<<grid, kBlock, 0, stream>>>(d, frame_off, frame_n, point_step, fd, bpf, block_count, frame_imax);

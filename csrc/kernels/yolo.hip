@@ -156,8 +156,8 @@ TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const v
       hd.anchor[l][a][1] = a < na ? anchors[(l * na + a) * 2 + 1] : 0.f;
     }
   }
-  hipError_t e = hipMemsetAsync(cand_count, 0, sizeof(int) * batch, stream);
-  if (e != hipSuccess) return (int)e;
+  int e = zero_i32_async(cand_count, batch, stream);
+  if (e) return e;
   long N = 0;
   for (int l = 0; l < 3; ++l) N += (long)na * hd.h[l] * hd.w[l];
   const int bs = 256;

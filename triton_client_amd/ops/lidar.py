@@ -220,9 +220,12 @@ class PillarEncoder:
     def clear(self, vox: Voxelizer, stream=None) -> None:
         """Zero the cells written for the voxels currently in ``vox`` (call
         before the voxeliser overwrites its coords with the next frame)."""
-        _native.call("tca_pillar_canvas_clear", _native.ptr(vox.coords), _native.ptr(vox.voxel_count), self.B,
-                     self.cfg.max_voxels, self.nx, self.ny, self.C, _native.ptr(self.canvas),
-                     _native.stream_ptr(stream))
+        self.clear_coords(vox.coords, vox.voxel_count, stream)
+
+    def clear_coords(self, coords: torch.Tensor, voxel_count: torch.Tensor, stream=None) -> None:
+        """coords [B, V, 4] (b, z, y, x), voxel_count [B]."""
+        _native.call("tca_pillar_canvas_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
+                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), _native.stream_ptr(stream))
 
     def encode_from_slots(self, points: torch.Tensor, vox: Voxelizer, feat_out: Optional[torch.Tensor] = None,
                           stream=None) -> torch.Tensor:
@@ -234,8 +237,9 @@ class PillarEncoder:
         return self.canvas_nchw()
 
     def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
+        """voxels [B, V, P, 4], num_points [B, V], coords [B, V, 4], voxel_count [B]."""
         _native.call("tca_pillar_vfe_voxels", _native.ptr(voxels), _native.ptr(num_points), _native.ptr(coords),
-                     _native.ptr(voxel_count), self.B, voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
+                     _native.ptr(voxel_count), voxels.shape[0], voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
                      _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas),
                      _native.ptr(feat_out), _native.stream_ptr(stream))
         return self.canvas_nchw()

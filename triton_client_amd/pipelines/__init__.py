@@ -1,0 +1,5 @@
+"""Device-resident per-frame pipelines (one per sensor family) and the
+hipGraph runner that replays a whole step with one launch."""
+from .camera import CameraPipeline  # noqa: F401
+from .lidar import LidarPipeline  # noqa: F401
+from .graph import GraphRunner  # noqa: F401
