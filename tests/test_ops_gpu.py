@@ -220,3 +220,53 @@ def test_anchor_postprocess_gpu_vs_cpu(cuda):
     k = min(n_r, n_g, 50)
     np.testing.assert_allclose(got.box[0, :k].cpu().numpy(), ref.box[0, :k].numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_array_equal(got.cls[0, :k].cpu().numpy(), ref.cls[0, :k].numpy())
+
+
+@pytest.mark.parametrize("cin,cout,k,s,p,act", [
+    (16, 32, 3, 2, 1, 2), (32, 32, 3, 1, 1, 2), (64, 64, 3, 1, 1, 1), (64, 128, 3, 2, 1, 1),
+    (128, 256, 1, 1, 0, 2), (24, 16, 1, 1, 0, 0), (8, 16, 6, 2, 2, 2), (256, 72, 1, 1, 0, 0)])
+def test_fused_conv_vs_fp32(cuda, cin, cout, k, s, p, act):
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(0)
+    conv = nn.Conv2d(cin, cout, k, s, p, bias=True)
+    B, H, W = 2, 37, 29
+    x = torch.randn(B, H, W, cin)
+    fc = FusedConv(conv, act=act, device=cuda)
+    xg = x.to(cuda, torch.bfloat16)
+    y = fc(NHWC(xg))
+    torch.cuda.synchronize()
+    ref = fc(NHWC(x.to(torch.bfloat16).float()), out=NHWC(torch.empty(*y.shape, dtype=torch.float32)))
+    got = y.tensor().float().cpu()
+    r = ref.tensor()[..., :cout]
+    err = (got[..., :cout] - r).abs().max().item()
+    assert err < 0.02 * max(1.0, r.abs().max().item()), err
+
+
+def test_fused_conv_slices_residual_and_transpose(cuda):
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(1)
+    B, H, W = 2, 20, 24
+    buf = torch.randn(B, H, W, 48).to(cuda, torch.bfloat16)  # read channels [16, 48)
+    conv = nn.Conv2d(32, 16, 3, 1, 1)
+    fc = FusedConv(conv, act=2, device=cuda)
+    out = torch.zeros(B, H, W, 64, dtype=torch.bfloat16, device=cuda)
+    res = torch.randn(B, H, W, 40).to(cuda, torch.bfloat16)
+    fc(NHWC(buf, 16, 32), out=NHWC(out, 8, 16), res=NHWC(res, 24, 16))
+    torch.cuda.synchronize()
+    xin = buf[..., 16:48].float().permute(0, 3, 1, 2).cpu()
+    ref = torch.nn.functional.silu(conv(xin)) + res[..., 24:40].float().permute(0, 3, 1, 2).cpu()
+    got = out[..., 8:24].float().permute(0, 3, 1, 2).cpu()
+    assert (got - ref).abs().max().item() < 0.05
+    assert out[..., :8].abs().sum().item() == 0 and out[..., 24:].abs().sum().item() == 0
+    # transpose conv k=s=2 and 4 via pixel shuffle
+    for s_ in (2, 4):
+        ct = nn.ConvTranspose2d(64, 32, s_, stride=s_, bias=True)
+        x = torch.randn(B, 9, 7, 64)
+        fct = FusedConv(ct, act=1, device=cuda)
+        y = fct(NHWC(x.to(cuda, torch.bfloat16)))
+        torch.cuda.synchronize()
+        ref = torch.relu(ct(x.to(torch.bfloat16).float().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
+        assert y.shape == (B, 9 * s_, 7 * s_, 32)
+        assert (y.tensor().float().cpu() - ref).abs().max().item() < 0.05

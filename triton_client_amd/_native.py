@@ -40,6 +40,8 @@ _KERNEL_SIGS = {
     "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
     "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, P],
+    "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
+    "tca_zero_i32": [P, I, P],
     "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
 }
 

@@ -1,0 +1,134 @@
+"""Fused NHWC bf16 convolution (``csrc/kernels/conv_mfma.hip``).
+
+:class:`FusedConv` packs a (BN-folded) ``Conv2d`` / ``ConvTranspose2d``
+(k == stride) into the kernel's GEMM layout once and runs
+``act(conv(x) + bias) (+ residual)`` in one launch, reading and writing
+channel slices of wider NHWC buffers (:class:`NHWC`), so the detectors'
+concatenations are free.  CPU tensors take an fp32 PyTorch path with the
+same semantics (used for tests on the GPU-less host).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+from ..models.common import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_SILU, apply_act
+
+
+@dataclass
+class NHWC:
+    """A channel slice [off, off + c) of an NHWC buffer ``t`` [B, H, W, C]."""
+    t: torch.Tensor
+    off: int = 0
+    c: Optional[int] = None
+
+    def __post_init__(self):
+        if self.c is None:
+            self.c = self.t.shape[-1] - self.off
+
+    @property
+    def shape(self):
+        return (*self.t.shape[:3], self.c)
+
+    def tensor(self) -> torch.Tensor:
+        return self.t[..., self.off:self.off + self.c]
+
+    def nchw(self) -> torch.Tensor:
+        return self.tensor().permute(0, 3, 1, 2)
+
+
+def _ceil(x, m):
+    return (x + m - 1) // m * m
+
+
+class FusedConv:
+    def __init__(self, conv: nn.Module, act: int = ACT_NONE, device="cuda", cin_pad: Optional[int] = None,
+                 cout_pad: Optional[int] = None):
+        w = conv.weight.detach().float()
+        b = conv.bias.detach().float() if conv.bias is not None else None
+        self.transpose = isinstance(conv, nn.ConvTranspose2d)
+        self.device = torch.device(device)
+        self.act = act
+        if self.transpose:
+            cin, cout, kh, kw = w.shape
+            s = conv.stride[0]
+            assert kh == kw == s and conv.padding[0] == 0, "only k == stride transpose convs"
+            self.shuffle, self.k, self.s, self.p = s, 1, 1, 0
+            self.cout_real = cout
+            # GEMM N index = (sy*s + sx)*cout + co
+            wg = w.permute(2, 3, 1, 0).reshape(s * s * cout, cin)  # [N, Cin]
+            bias = b.repeat(s * s) if b is not None else None
+            self.ref = conv
+        else:
+            cout, cin, kh, kw = w.shape
+            assert kh == kw
+            self.shuffle, self.k, self.s, self.p = 0, kh, conv.stride[0], conv.padding[0]
+            self.cout_real = cout
+            wg = w
+            bias = b
+            self.ref = conv
+        self.cin = cin
+        self.cin_p = cin_pad or _ceil(cin, 8)
+        if self.transpose:
+            wk = torch.zeros(wg.shape[0], self.cin_p)
+            wk[:, :cin] = wg
+            K = self.cin_p
+        else:
+            wk = torch.zeros(cout, kh, kw, self.cin_p)
+            wk[..., :cin] = wg.permute(0, 2, 3, 1)
+            wk = wk.reshape(cout, -1)
+            K = kh * kw * self.cin_p
+        N = wk.shape[0]
+        self.N = cout_pad or _ceil(N, 8)
+        self.K, self.Kp = K, _ceil(K, 32)
+        W = torch.zeros(self.N, self.Kp)
+        W[:N, :K] = wk
+        self.bias = torch.zeros(self.N)
+        if bias is not None:
+            self.bias[:N] = bias
+        self.w_gemm = W.to(self.device, torch.bfloat16).contiguous()
+        self.b_gemm = self.bias.to(self.device).contiguous()
+        # fp32 copies for the CPU path
+        self.w_f32, self.b_f32 = w, b
+
+    def out_hw(self, H, W):
+        if self.transpose:
+            return H * self.shuffle, W * self.shuffle
+        return (H + 2 * self.p - self.k) // self.s + 1, (W + 2 * self.p - self.k) // self.s + 1
+
+    def out_channels(self) -> int:
+        return self.cout_real if self.transpose else self.N
+
+    def __call__(self, x: NHWC, out: Optional[NHWC] = None, res: Optional[NHWC] = None, tile: int = 0,
+                 stream=None) -> NHWC:
+        B, H, W, C = x.shape
+        Ho, Wo = self.out_hw(H, W)
+        if out is None:
+            out = NHWC(torch.empty((B, Ho, Wo, self.out_channels()), dtype=torch.bfloat16, device=x.t.device))
+        if x.t.device.type != "cuda":
+            return self._cpu(x, out, res)
+        assert C == self.cin_p, (C, self.cin_p)
+        gh, gw = (H, W) if self.transpose else (Ho, Wo)
+        _native.call("tca_conv_nhwc", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                     _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
+                     self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, self.act,
+                     _native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
+                     res.off if res is not None else 0, self.shuffle, tile, _native.stream_ptr(stream))
+        return out
+
+    def _cpu(self, x: NHWC, out: NHWC, res: Optional[NHWC]) -> NHWC:
+        xi = x.nchw().float()[:, : self.cin]
+        if self.transpose:
+            y = F.conv_transpose2d(xi, self.w_f32, self.b_f32, stride=self.shuffle)
+        else:
+            y = F.conv2d(xi, self.w_f32, self.b_f32, stride=self.s, padding=self.p)
+        y = apply_act(y, self.act)
+        if res is not None:
+            y = y + res.nchw().float()[:, : y.shape[1]]
+        out.tensor()[..., : y.shape[1]].copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
+        return out

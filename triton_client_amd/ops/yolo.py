@@ -63,6 +63,12 @@ class YoloPostprocess:
         when decoded_out (KServe contract)."""
         if heads[0].device.type != "cuda":
             return self.cpu(heads, xform)
+        cand, decoded = self._filter(heads, decoded_out, stream)
+        res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
+                           xform.as_list() if xform is not None else None, prefix="yolo_nms_", stream=stream)
+        return (res, decoded) if decoded_out else res
+
+    def _filter(self, heads, decoded_out: bool, stream=None):
         lay, h0 = layout_of(heads[0])
         hs = [h0] + [layout_of(h)[1] for h in heads[1:]]
         if any(layout_of(h)[0] != lay for h in hs):
@@ -80,9 +86,13 @@ class YoloPostprocess:
                      float(self.conf_thres), int(self.multi_label), _native.ptr(self._class_mask),
                      _native.ptr(cand.box), _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key),
                      _native.ptr(cand.count), cap, _native.ptr(decoded), _native.stream_ptr(stream))
-        res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
-                           xform.as_list() if xform is not None else None, prefix="yolo_nms_", stream=stream)
-        return (res, decoded) if decoded_out else res
+        return cand, decoded
+
+    def decode(self, heads: List[torch.Tensor], stream=None) -> torch.Tensor:
+        """Decoded [B, N, 5+nc] fp32 (the ONNX YOLOv5 output contract)."""
+        if heads[0].device.type != "cuda":
+            return self.decode_cpu(heads)
+        return self._filter(heads, True, stream)[1]
 
     # -------------------------------------------------------------- CPU
     def decode_cpu(self, heads: List[torch.Tensor]) -> torch.Tensor:

@@ -1,0 +1,161 @@
+"""Servable model contract for the in-process KServe-v2 server.
+
+A :class:`ServedModel` owns a Triton-compatible ``ModelConfig`` (the tensor
+contract the reference's clients negotiate via ``ModelMetadata`` /
+``ModelConfig``, e.g. ``examples/pointpillar_kitti/config.pbtxt``) and an
+``execute`` that maps named numpy inputs to named numpy outputs — the role of
+``TritonPythonModel.execute`` in the reference's Python-backend models
+(``examples/pointpillar_kitti/1/model.py:119-186``).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from abc import ABC, abstractmethod
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..proto import config_dtype_to_kserve, model_config_pb2 as mc, service_pb2 as pb
+
+DT = {"FP32": mc.TYPE_FP32, "FP16": mc.TYPE_FP16, "INT32": mc.TYPE_INT32, "INT64": mc.TYPE_INT64,
+      "UINT8": mc.TYPE_UINT8, "BOOL": mc.TYPE_BOOL, "FP64": mc.TYPE_FP64, "INT16": mc.TYPE_INT16}
+
+
+def tensor_spec(name: str, dtype: str, dims: Sequence[int], fmt: Optional[str] = None,
+                reshape: Optional[Sequence[int]] = None, output: bool = False):
+    t = mc.ModelOutput() if output else mc.ModelInput()
+    t.name = name
+    t.data_type = DT[dtype]
+    t.dims.extend(list(dims))
+    if fmt and not output:
+        t.format = {"NCHW": mc.ModelInput.FORMAT_NCHW, "NHWC": mc.ModelInput.FORMAT_NHWC}[fmt]
+    if reshape:
+        t.reshape.shape.extend(list(reshape))
+    return t
+
+
+@dataclass
+class ModelStats:
+    inference_count: int = 0
+    execution_count: int = 0
+    success_ns: int = 0
+    fail_count: int = 0
+    compute_ns: int = 0
+    last_inference_ms: int = 0
+    lock: threading.Lock = field(default_factory=threading.Lock)
+
+
+class InferError(Exception):
+    """Raised by execute() for a client error (bad shape/dtype) → INVALID_ARGUMENT."""
+
+
+class ServedModel(ABC):
+    platform = "amd_mi355x"
+    backend = "triton_client_amd"
+    max_batch_size = 0
+
+    def __init__(self, name: str, version: str = "1"):
+        self.name = name
+        self.version = version
+        self.ready = False
+        self.stats = ModelStats()
+        self._config: Optional[mc.ModelConfig] = None
+        self._lock = threading.Lock()  # one execution at a time per instance (GPU graph buffers)
+
+    # ---------------------------------------------------------------- contract
+    @abstractmethod
+    def inputs(self) -> List[mc.ModelInput]:
+        ...
+
+    @abstractmethod
+    def outputs(self) -> List[mc.ModelOutput]:
+        ...
+
+    @abstractmethod
+    def execute(self, inputs: Dict[str, np.ndarray], requested: Sequence[str]) -> Dict[str, np.ndarray]:
+        ...
+
+    def load(self) -> None:
+        """Allocate / build / warm up.  Sets ready."""
+        self.ready = True
+
+    def unload(self) -> None:
+        self.ready = False
+
+    def instance_kind(self) -> int:
+        return mc.ModelInstanceGroup.KIND_GPU
+
+    # ---------------------------------------------------------------- derived
+    def config(self) -> mc.ModelConfig:
+        if self._config is None:
+            c = mc.ModelConfig(name=self.name, platform=self.platform, backend=self.backend,
+                               max_batch_size=self.max_batch_size)
+            c.input.extend(self.inputs())
+            c.output.extend(self.outputs())
+            c.instance_group.add(kind=self.instance_kind(), count=1)
+            self._config = c
+        return self._config
+
+    def metadata(self) -> pb.ModelMetadataResponse:
+        cfg = self.config()
+        md = pb.ModelMetadataResponse(name=self.name, versions=[self.version], platform=self.platform)
+        for t in cfg.input:
+            shape = list(t.dims)
+            md.inputs.add(name=t.name, datatype=config_dtype_to_kserve(t.data_type), shape=shape)
+        for t in cfg.output:
+            md.outputs.add(name=t.name, datatype=config_dtype_to_kserve(t.data_type), shape=list(t.dims))
+        return md
+
+    def validate(self, inputs: Dict[str, np.ndarray]) -> None:
+        for spec in self.config().input:
+            if spec.name not in inputs:
+                raise InferError(f"missing input '{spec.name}' for model '{self.name}'")
+            a = inputs[spec.name]
+            dims = list(spec.reshape.shape) if len(spec.reshape.shape) else list(spec.dims)
+            if len(dims) != a.ndim and list(spec.dims) and len(spec.dims) != a.ndim:
+                raise InferError(f"input '{spec.name}': rank {a.ndim}, expected {len(dims)}")
+            ref = dims if len(dims) == a.ndim else list(spec.dims)
+            for d, s in zip(ref, a.shape):
+                if d != -1 and d != s:
+                    raise InferError(f"input '{spec.name}': shape {list(a.shape)} does not match {ref}")
+
+    def __call__(self, inputs: Dict[str, np.ndarray], requested: Sequence[str]) -> Dict[str, np.ndarray]:
+        t0 = time.perf_counter_ns()
+        try:
+            self.validate(inputs)
+            with self._lock:
+                out = self.execute(inputs, requested)
+        except Exception:
+            with self.stats.lock:
+                self.stats.fail_count += 1
+            raise
+        dt = time.perf_counter_ns() - t0
+        with self.stats.lock:
+            self.stats.inference_count += 1
+            self.stats.execution_count += 1
+            self.stats.success_ns += dt
+            self.stats.compute_ns += dt
+            self.stats.last_inference_ms = int(time.time() * 1000)
+        return out
+
+
+class EchoModel(ServedModel):
+    """Identity model for protocol tests: output ``OUTPUT{i}`` = ``INPUT{i}``."""
+
+    def __init__(self, name: str = "echo", n: int = 1, dtype: str = "FP32", dims=(-1,)):
+        super().__init__(name)
+        self.n, self.dtype, self.dims = n, dtype, list(dims)
+
+    def inputs(self):
+        return [tensor_spec(f"INPUT{i}", self.dtype, self.dims) for i in range(self.n)]
+
+    def outputs(self):
+        return [tensor_spec(f"OUTPUT{i}", self.dtype, self.dims, output=True) for i in range(self.n)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_CPU
+
+    def execute(self, inputs, requested):
+        return {f"OUTPUT{i}": inputs[f"INPUT{i}"] for i in range(self.n)}

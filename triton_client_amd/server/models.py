@@ -1,0 +1,194 @@
+"""Servable detectors with the reference's Triton tensor contracts.
+
+* :class:`YoloV5Model` — ``YOLOv5nCROP`` / ``weed_detector`` (512, 2 classes,
+  ``examples/YOLOv5/config.pbtxt``) and ``YOLOv5nCOCO`` (640, 80 classes,
+  ``.vscode/launch.json:12``): input ``images`` FP32 NCHW [3,H,W] (reshape
+  [1,3,H,W]), output ``output`` FP32 [1, N, 5+nc] decoded rows — what the
+  reference's ONNX export returns.  On MI355X: bf16 channels_last network +
+  the HIP decode kernel writing the decoded tensor.
+* :class:`PointPillarsModel` — ``pointpillar_kitti``
+  (``examples/pointpillar_kitti/config.pbtxt``): inputs ``voxels`` [-1,P,4],
+  ``voxel_coords`` INT32 [-1,4] (b,z,y,x), ``voxel_num_points`` INT32 [-1];
+  outputs ``pred_boxes`` [-1,7], ``pred_scores`` [-1], ``pred_labels`` INT64
+  [-1] (1-based).  On MI355X: MFMA PillarVFE+scatter from the received
+  voxels, bf16 backbone, anchor decode + rotated NMS kernels.  The voxel
+  geometry is published in ``ModelConfig.parameters`` so clients voxelise
+  with the model's own parameters (fixes SURVEY Appendix A9).
+
+Weights are random-init (He + LSUV on a synthetic sample, detection-head
+prior calibrated) exactly like the bench; ``--weights`` loading of a
+state_dict is supported for real checkpoints.
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..config.lidar import PointPillarsConfig, VoxelConfig
+from ..proto import model_config_pb2 as mc
+from .model import InferError, ServedModel, tensor_spec
+
+
+def _device(device) -> torch.device:
+    if device in (None, "auto"):
+        return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    return torch.device(device)
+
+
+class YoloV5Model(ServedModel):
+    def __init__(self, name: str = "YOLOv5nCOCO", variant: str = "n", nc: int = 80, img: int = 640,
+                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0):
+        super().__init__(name)
+        self.variant, self.nc, self.img = variant, nc, img
+        self.device = _device(device)
+        self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+        from ..models.yolov5 import YoloConfig
+        self.N = YoloConfig(variant, nc, (img, img)).num_predictions()
+
+    def inputs(self):
+        return [tensor_spec("images", "FP32", [3, self.img, self.img], fmt="NCHW", reshape=[1, 3, self.img, self.img])]
+
+    def outputs(self):
+        return [tensor_spec("output", "FP32", [1, self.N, 5 + self.nc], output=True)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_GPU if self.device.type == "cuda" else mc.ModelInstanceGroup.KIND_CPU
+
+    def load(self):
+        from ..pipelines.camera import CameraPipeline
+        from ..models.yolov5 import build_yolov5
+        from ..utils.synthetic import camera_frame
+
+        model = build_yolov5(self.variant, self.nc, self.img, self.seed)
+        if self.weights:
+            model.load_state_dict(torch.load(self.weights, map_location="cpu", weights_only=True))
+        if self.device.type == "cuda":
+            self.pipe = CameraPipeline(model, batch=1, src_hw=(self.img, self.img), img_hw=(self.img, self.img),
+                                       mode="stretch", device=self.device)
+            if not self.weights:
+                self.pipe.frames[0].copy_(torch.from_numpy(camera_frame(self.img, self.img, self.seed)))
+                self.pipe.calibrate_detection_density(self.calibrate_target)
+            self.model = self.pipe.model
+            self.x = torch.empty((1, self.img, self.img, 3), dtype=torch.bfloat16, device=self.device).permute(0, 3, 1, 2)
+        else:
+            from ..models.common import fuse_model
+            self.model = fuse_model(model.eval())
+        self.ready = True
+
+    @torch.no_grad()
+    def execute(self, inputs, requested):
+        x = inputs["images"].reshape(1, 3, self.img, self.img)
+        if self.device.type == "cuda":
+            self.x.copy_(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(self.device, non_blocking=True))
+            heads = self.model(self.x)
+            dec = self.pipe.post.decode(heads)
+            out = dec.cpu().numpy()
+        else:
+            heads = self.model(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)))
+            from ..models.yolov5 import yolo_decode_reference
+            out = yolo_decode_reference(heads, self.model.anchors).numpy()
+        return {"output": out.astype(np.float32, copy=False)}
+
+
+class PointPillarsModel(ServedModel):
+    def __init__(self, name: str = "pointpillar_kitti", cfg: Optional[PointPillarsConfig] = None, device="auto",
+                 weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 2000.0):
+        super().__init__(name)
+        self.cfg = cfg or PointPillarsConfig()
+        self.device = _device(device)
+        self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+        self.P = self.cfg.voxel.max_points_per_voxel
+
+    def inputs(self):
+        return [tensor_spec("voxels", "FP32", [-1, self.P, 4]), tensor_spec("voxel_coords", "INT32", [-1, 4]),
+                tensor_spec("voxel_num_points", "INT32", [-1])]
+
+    def outputs(self):
+        return [tensor_spec("pred_boxes", "FP32", [-1, 7], output=True),
+                tensor_spec("pred_scores", "FP32", [-1], output=True),
+                tensor_spec("pred_labels", "INT64", [-1], output=True)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_GPU if self.device.type == "cuda" else mc.ModelInstanceGroup.KIND_CPU
+
+    def config(self):
+        c = super().config()
+        v = self.cfg.voxel
+        for k, val in (("point_cloud_range", list(v.point_cloud_range)), ("voxel_size", list(v.voxel_size)),
+                       ("max_points_per_voxel", v.max_points_per_voxel), ("max_voxels", v.max_voxels),
+                       ("class_names", list(self.cfg.class_names))):
+            c.parameters[k].string_value = json.dumps(val)
+        return c
+
+    def load(self):
+        from ..models.pointpillars import build_pointpillars
+        model = build_pointpillars(self.cfg, self.seed)
+        if self.weights:
+            model.load_state_dict(torch.load(self.weights, map_location="cpu", weights_only=True))
+        if self.device.type == "cuda":
+            from ..pipelines.lidar import LidarPipeline
+            from ..ops.lidar import PillarEncoder
+            from ..utils.synthetic import LidarSpec, lidar_sweep
+
+            spec = LidarSpec(sensor_height=3.23)
+            maxp = ((spec.points_per_sweep + 1023) // 1024) * 1024
+            self.pipe = LidarPipeline(model, batch=1, max_points=maxp, device=self.device)
+            if not self.weights:
+                c = lidar_sweep(spec, self.seed)
+                raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+                self.pipe.data[: raw.numel()].copy_(raw)
+                self.pipe.frame_n.fill_(c.shape[0])
+                self.pipe.calibrate_detection_density(self.calibrate_target)
+            v = self.cfg.voxel
+            V = v.max_voxels
+            self.enc = self.pipe.enc
+            self.voxels = torch.zeros((1, V, self.P, 4), dtype=torch.float32, device=self.device)
+            self.coords = torch.zeros((1, V, 4), dtype=torch.int32, device=self.device)
+            self.nump = torch.zeros((1, V), dtype=torch.int32, device=self.device)
+            self.vcount = torch.zeros((1,), dtype=torch.int32, device=self.device)
+            self.enc.clear(self.pipe.vox)  # start from an empty canvas
+            self.model = self.pipe.model
+        else:
+            from ..models.common import fuse_model
+            self.model = fuse_model(model.eval())
+        self.ready = True
+
+    @torch.no_grad()
+    def execute(self, inputs, requested):
+        vox = inputs["voxels"]
+        co = inputs["voxel_coords"]
+        n = inputs["voxel_num_points"]
+        V = vox.shape[0]
+        if vox.shape[1] != self.P or vox.shape[2] < 4:
+            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
+        if V > self.cfg.voxel.max_voxels:
+            raise InferError(f"{V} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+        if self.device.type == "cuda":
+            self.enc.clear_coords(self.coords, self.vcount)
+            self.voxels[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(vox[..., :4], np.float32)))
+            self.coords[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(co, np.int32)))
+            self.coords[0, :V, 0] = 0
+            self.nump[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(n, np.int32)))
+            self.vcount.fill_(V)
+            canvas = self.enc.encode_from_voxels(self.voxels, self.nump, self.coords, self.vcount)
+            cls, box, dr = self.model.bev_forward(canvas)
+            res = self.pipe.post(cls, box, dr)
+        else:
+            from ..models.pointpillars import pillar_point_features, scatter_to_bev
+            from ..ops.lidar import AnchorPostprocess
+            v = torch.from_numpy(np.ascontiguousarray(vox[..., :4], np.float32))
+            c = torch.from_numpy(np.ascontiguousarray(co, np.int32)).clone()
+            c[:, 0] = 0
+            f = pillar_point_features(v, torch.from_numpy(n.astype(np.int64)), c, self.cfg.voxel)
+            pf = self.model.vfe(f)
+            nx, ny, _ = self.cfg.voxel.grid_size
+            canvas = scatter_to_bev(pf, c, 1, ny, nx, channels_last=False)
+            cls, box, dr = self.model.bev_forward(canvas)
+            res = AnchorPostprocess(self.cfg, 1, device="cpu").cpu(cls, box, dr)
+        k = int(res.count[0])
+        return {"pred_boxes": res.box[0, :k].cpu().numpy().astype(np.float32),
+                "pred_scores": res.score[0, :k].cpu().numpy().astype(np.float32),
+                "pred_labels": res.cls[0, :k].cpu().numpy().astype(np.int64)}
