@@ -23,7 +23,7 @@ struct AnchorTable {
 template <typename T>
 __global__ void __launch_bounds__(256) anchor_decode_kernel(
     const T* __restrict__ cls, const T* __restrict__ box, const T* __restrict__ dir, int layout, int H, int W, int A,
-    int C, int bins, AnchorTable tb, float x0, float xs, float y0, float ys, float dir_offset, float dir_limit_offset,
+    int C, int bins, int ld_cls, int ld_box, int ld_dir, AnchorTable tb, float x0, float xs, float y0, float ys, float dir_offset, float dir_limit_offset,
     float score_thresh, float* __restrict__ cand_box, float* __restrict__ cand_score, int* __restrict__ cand_label,
     uint64_t* __restrict__ cand_key, int* __restrict__ cand_count, int cap) {
   __shared__ int s_cnt, s_base;
@@ -40,14 +40,15 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
     const int a = aidx % A;
     const int yx = aidx / A;
     const int y = yx / W, x = yx - y * W;
-    auto at = [&](const T* base, int nch, int ch) -> float {
-      long off = layout == 0 ? (((long)b * nch + ch) * H + y) * W + x : (((long)b * H + y) * W + x) * nch + ch;
+    // NCHW: nch channels; NHWC: channel stride ld (a slice of a wider tensor)
+    auto at = [&](const T* base, int nch, int ld, int ch) -> float {
+      long off = layout == 0 ? (((long)b * nch + ch) * H + y) * W + x : (((long)b * H + y) * W + x) * ld + ch;
       return to_f32(base[off]);
     };
     float best = -INFINITY;
     int bc = 0;
     for (int c = 0; c < C; ++c) {
-      const float v = at(cls, A * C, a * C + c);
+      const float v = at(cls, A * C, ld_cls, a * C + c);
       if (v > best) { best = v; bc = c; }
     }
     score = sigmoidf_(best);
@@ -59,7 +60,7 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
       const float dxa = t[0], dya = t[1], dza = t[2], ra = t[4], diag = t[5];
       float e[7];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) e[k] = at(box, A * 7, a * 7 + k);
+      for (int k = 0; k < 7; ++k) e[k] = at(box, A * 7, ld_box, a * 7 + k);
       out[0] = e[0] * diag + xa;
       out[1] = e[1] * diag + ya;
       out[2] = e[2] * dza + za;
@@ -71,7 +72,7 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
         float bd = -INFINITY;
         int dl = 0;
         for (int d = 0; d < bins; ++d) {
-          const float v = at(dir, A * bins, a * bins + d);
+          const float v = at(dir, A * bins, ld_dir, a * bins + d);
           if (v > bd) { bd = v; dl = d; }
         }
         const float period = 2.f * 3.14159265358979f / (float)bins;
@@ -104,7 +105,8 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
 
 // table: host [A][6] (dxa, dya, dza, za, rot, diag).
 TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const void* dir, int dtype, int layout, int batch,
-                                     int H, int W, int A, int C, int bins, const float* table, float x0, float xs,
+                                     int H, int W, int A, int C, int bins, int ld_cls, int ld_box, int ld_dir,
+                                     const float* table, float x0, float xs,
                                      float y0, float ys, float dir_offset, float dir_limit_offset, float score_thresh,
                                      float* cand_box, float* cand_score, int* cand_label, uint64_t* cand_key,
                                      int* cand_count, int cap, hipStream_t stream) {
@@ -118,7 +120,8 @@ TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const voi
   dim3 grid((H * W * A + 255) / 256, batch);
 #define LAUNCH(T)                                                                                              \
   anchor_decode_kernel<T><<<grid, 256, 0, stream>>>((const T*)cls, (const T*)box, (const T*)dir, layout, H, W, A, C, \
-                                                    bins, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset,          \
+                                                    bins, ld_cls > 0 ? ld_cls : A * C, ld_box > 0 ? ld_box : A * 7,  \
+                                                    ld_dir > 0 ? ld_dir : A * bins, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset,          \
                                                     score_thresh, cand_box, cand_score, cand_label, cand_key,        \
                                                     cand_count, cap)
   switch (dtype) {

@@ -251,7 +251,8 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
   if (a.K > Kp) return (int)hipErrorInvalidValue;
   // tile: 0 = auto
-  if (tile == 0) tile = N <= 32 ? 1 : (N <= 64 ? 2 : 3);
+  // measured on MI355X (tools/bench_conv.py): 128x32 for N<=32, 128x64 for N<=64, 64x128 above
+  if (tile == 0) tile = N <= 32 ? 1 : (N <= 64 ? 2 : 5);
   switch (tile) {
     case 1: return launch<128, 32, 4, 1>(a, stream);
     case 2: return launch<128, 64, 4, 1>(a, stream);

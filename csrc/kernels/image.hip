@@ -112,6 +112,20 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
       for (int k = 0; k < 4; ++k)
         if (q * 4 + k < p.dst_w) o[k] = from_f32<T>(0.f);
     }
+  } else if (p.dst_c == 8 && sizeof(T) == 2) {  // NHWC, 3 channels + 5 zero pad: one 16-B store per pixel
+    const long base = (((long)b * p.dst_h + y) * p.dst_w + q * 4) * 8;
+    for (int k = 0; k < 4; ++k) {
+      if (q * 4 + k >= p.dst_w) break;
+      T px[8];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int sc_c = p.swap_rb ? 2 - c : c;
+        px[c] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+      }
+#pragma unroll
+      for (int c = 3; c < 8; ++c) px[c] = from_f32<T>(0.f);
+      *reinterpret_cast<uint4*>(d + base + (long)k * 8) = *reinterpret_cast<uint4*>(px);
+    }
   } else {  // NHWC with dst_c in {3, 4}
     const long base = (((long)b * p.dst_h + y) * p.dst_w + q * 4) * p.dst_c;
     for (int k = 0; k < 4; ++k) {
@@ -142,7 +156,9 @@ TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src
                                  float pad_value, int quantize_u8, float sc0, float sc1, float sc2, float b0,
                                  float b1, float b2, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (src_c < 3 || (dst_c != 3 && dst_c != 4) || reg_h <= 0 || reg_w <= 0) return (int)hipErrorInvalidValue;
+  if (src_c < 3 || (dst_c != 3 && dst_c != 4 && !(dst_c == 8 && dst_layout == 1 && dst_dtype != kF32)) || reg_h <= 0 ||
+      reg_w <= 0)
+    return (int)hipErrorInvalidValue;
   PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
                reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
   const long total = (long)batch * dst_h * ((dst_w + 3) / 4);

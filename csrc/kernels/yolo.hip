@@ -24,6 +24,7 @@ namespace {
 struct YoloHeads {
   const void* head[3];
   int h[3], w[3], stride[3];
+  int ldc[3];  // NHWC channel stride per level (>= na*(5+nc)); ignored for NCHW
   float anchor[3][4][2];  // up to 4 anchors per level
 };
 
@@ -66,7 +67,7 @@ __global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layo
     base = ((long)b * C + (long)a * no) * H * W + yx;
     cstride = (long)H * W;
   } else {  // NHWC
-    base = ((long)b * H * W + yx) * C + (long)a * no;
+    base = ((long)b * H * W + yx) * hd.ldc[l] + (long)a * no;
     cstride = 1;
   }
   float obj = 0.f;
@@ -141,6 +142,7 @@ __global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layo
 
 TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const void* head2, int dtype, int layout,
                                    int batch, int na, int nc, const int* hw /*[6]*/, const int* strides /*[3]*/,
+                                   const int* ldc /*[3] or null*/,
                                    const float* anchors /*[3][na][2] host*/, float conf_thres, int multi_label,
                                    const uint32_t* class_mask, float* cand_box, float* cand_score, int* cand_cls,
                                    uint64_t* cand_key, int* cand_count, int cap, float* decoded,
@@ -151,6 +153,7 @@ TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const v
   hd.head[0] = head0; hd.head[1] = head1; hd.head[2] = head2;
   for (int l = 0; l < 3; ++l) {
     hd.h[l] = hw[2 * l]; hd.w[l] = hw[2 * l + 1]; hd.stride[l] = strides[l];
+    hd.ldc[l] = ldc ? ldc[l] : na * (nc + 5);
     for (int a = 0; a < 4; ++a) {
       hd.anchor[l][a][0] = a < na ? anchors[(l * na + a) * 2] : 0.f;
       hd.anchor[l][a][1] = a < na ? anchors[(l * na + a) * 2 + 1] : 0.f;

@@ -28,7 +28,7 @@ F = ctypes.c_float
 # name -> argtypes (restype is always int = hipError_t)
 _KERNEL_SIGS = {
     "tca_image_preprocess": [P, L, I, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P],
-    "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
+    "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
     "tca_topk_sort": [P, P, I, I, I, P, P, P],
     "tca_nms_mask": [I, P, I, P, P, P, I, I, I, F, I, P, I, P],
     "tca_nms_reduce": [P, P, P, I, I, P, I, P, P, I, I, P, P, P, P, P, P],
@@ -42,7 +42,9 @@ _KERNEL_SIGS = {
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, P],
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_zero_i32": [P, I, P],
-    "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
+    "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
+    "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, P],
+    "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, P],
 }
 
 

@@ -1,0 +1,219 @@
+"""Concat-free NHWC execution plans of the detectors on the fused MFMA conv.
+
+Every activation is an NHWC bf16 buffer allocated once per batch size (so a
+whole forward is hipGraph-capturable with stable addresses); a layer whose
+output feeds a concatenation writes straight into its channel slice of the
+concat buffer (C3's two branches, SPPF's pyramid, PANet's skip joins, the BEV
+neck's three up-sampled scales), so no concat kernel ever runs.
+
+* :class:`FastYOLOv5`  — same math as :class:`~.yolov5.YOLOv5` (BN folded),
+  input ``[B, H, W, 8]`` (3 RGB channels + 5 zero pad so Cin % 8 == 0),
+  outputs the three Detect maps as NHWC slices (255 of 256 channels).
+* :class:`FastBEV`     — BaseBEVBackbone + AnchorHeadSingle of
+  :class:`~.pointpillars.PointPillars`; the three head 1x1 convs are merged
+  into one 384→72 GEMM; outputs cls / box / dir as slices of it.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops.conv import NHWC, FusedConv, maxpool_nhwc, upsample2x_nhwc
+from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
+
+
+def _fc(m: ConvBNAct, device, **kw) -> FusedConv:
+    assert m.fused, "call fuse_model() first"
+    return FusedConv(m.conv, act=m.act, device=device, **kw)
+
+
+class _Buffers:
+    def __init__(self, device, dtype=None):
+        self.device = torch.device(device)
+        # bf16 on the GPU; fp32 on the CPU reference path (exact comparisons in tests)
+        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.bufs = []
+
+    def new(self, B, H, W, C) -> NHWC:
+        t = torch.zeros((B, H, W, C), dtype=self.dtype, device=self.device)
+        self.bufs.append(t)
+        return NHWC(t)
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.bufs)
+
+
+class _C3Plan:
+    """C3: cv3(cat(m(cv1(x)), cv2(x))) with the cat buffer written in place."""
+
+    def __init__(self, c3, B, H, W, bufs: _Buffers, device):
+        self.cv1, self.cv2, self.cv3 = _fc(c3.cv1, device), _fc(c3.cv2, device), _fc(c3.cv3, device)
+        self.m = [(_fc(b.cv1, device), _fc(b.cv2, device), b.add) for b in c3.m]
+        c_ = self.cv1.N
+        self.c_ = c_
+        self.cat = bufs.new(B, H, W, 2 * c_)
+        self.a = [bufs.new(B, H, W, c_), bufs.new(B, H, W, c_)]
+        self.tmp = bufs.new(B, H, W, c_)
+        self.out_c = self.cv3.N
+
+    def __call__(self, x: NHWC, out: NHWC) -> NHWC:
+        c_ = self.c_
+        cur = self.cv1(x, out=self.a[0])
+        for i, (b1, b2, add) in enumerate(self.m):
+            last = i == len(self.m) - 1
+            dst = NHWC(self.cat.t, 0, c_) if last else self.a[(i + 1) % 2]
+            u = b1(cur, out=self.tmp)
+            b2(u, out=dst, res=cur if add else None)
+            cur = dst
+        self.cv2(x, out=NHWC(self.cat.t, c_, c_))
+        return self.cv3(self.cat, out=out)
+
+
+class FastYOLOv5:
+    IN_CHANNELS = 8
+
+    def __init__(self, model, batch: int, img_hw: Tuple[int, int] = (640, 640), device="cuda"):
+        self.device = torch.device(device)
+        H, W = img_hw
+        B = batch
+        bufs = self.bufs = _Buffers(self.device)
+        m = model
+        self.x = bufs.new(B, H, W, self.IN_CHANNELS)
+        self.b0 = _fc(m.b0, device, cin_pad=self.IN_CHANNELS)
+        self.b1, self.b3, self.b5, self.b7 = (_fc(getattr(m, n), device) for n in ("b1", "b3", "b5", "b7"))
+        h2, w2 = H // 2, W // 2
+        s4, s8, s16, s32 = (H // 4, W // 4), (H // 8, W // 8), (H // 16, W // 16), (H // 32, W // 32)
+        self.t0 = bufs.new(B, h2, w2, self.b0.N)
+        self.t1 = bufs.new(B, *s4, self.b1.N)
+        self.c3_2 = _C3Plan(m.b2, B, *s4, bufs, device)
+        self.t2 = bufs.new(B, *s4, self.c3_2.out_c)
+        self.t3 = bufs.new(B, *s8, self.b3.N)
+        self.c3_4 = _C3Plan(m.b4, B, *s8, bufs, device)
+        c_p3 = self.c3_4.out_c
+        self.h14 = _fc(m.h14, device)
+        self.cat17 = bufs.new(B, *s8, self.h14.N + c_p3)  # [up(h14) | p3]
+        self.p3 = NHWC(self.cat17.t, self.h14.N, c_p3)
+        self.t5 = bufs.new(B, *s16, self.b5.N)
+        self.c3_6 = _C3Plan(m.b6, B, *s16, bufs, device)
+        c_p4 = self.c3_6.out_c
+        self.h10 = _fc(m.h10, device)
+        self.cat13 = bufs.new(B, *s16, self.h10.N + c_p4)  # [up(h10) | p4]
+        self.p4 = NHWC(self.cat13.t, self.h10.N, c_p4)
+        self.t7 = bufs.new(B, *s32, self.b7.N)
+        self.c3_8 = _C3Plan(m.b8, B, *s32, bufs, device)
+        self.t8 = bufs.new(B, *s32, self.c3_8.out_c)
+        # SPPF
+        self.sp1, self.sp2 = _fc(m.b9.cv1, device), _fc(m.b9.cv2, device)
+        cs = self.sp1.N
+        self.spcat = bufs.new(B, *s32, 4 * cs)
+        self.t9 = bufs.new(B, *s32, self.sp2.N)
+        self.k = m.b9.k
+        # head
+        self.h18, self.h21 = _fc(m.h18, device), _fc(m.h21, device)
+        self.cat23 = bufs.new(B, *s32, self.h21.N + self.h10.N)  # [h21 | h10]
+        self.h10_out = NHWC(self.cat23.t, self.h21.N, self.h10.N)
+        self.c3_13 = _C3Plan(m.h13, B, *s16, bufs, device)
+        self.t13 = bufs.new(B, *s16, self.c3_13.out_c)
+        self.cat20 = bufs.new(B, *s16, self.h18.N + self.h14.N)  # [h18 | h14]
+        self.h14_out = NHWC(self.cat20.t, self.h18.N, self.h14.N)
+        self.c3_17 = _C3Plan(m.h17, B, *s8, bufs, device)
+        self.o3 = bufs.new(B, *s8, self.c3_17.out_c)
+        self.c3_20 = _C3Plan(m.h20, B, *s16, bufs, device)
+        self.o4 = bufs.new(B, *s16, self.c3_20.out_c)
+        self.c3_23 = _C3Plan(m.h23, B, *s32, bufs, device)
+        self.o5 = bufs.new(B, *s32, self.c3_23.out_c)
+        self.det = [FusedConv(c, act=ACT_NONE, device=device) for c in m.detect]
+        self.dout = [bufs.new(B, *s, d.N) for s, d in zip((s8, s16, s32), self.det)]
+        self.no_real = m.detect[0].out_channels
+
+    def input_view(self) -> torch.Tensor:
+        """[B, 3, H, W] channels_last view of the RGB part of the input buffer
+        (what the preprocess kernel writes; channels 3..7 stay zero)."""
+        return self.x.t.permute(0, 3, 1, 2)
+
+    def forward(self) -> List[NHWC]:
+        t = self.b0(self.x, out=self.t0)
+        t = self.b1(t, out=self.t1)
+        t = self.c3_2(t, out=self.t2)
+        t = self.b3(t, out=self.t3)
+        p3 = self.c3_4(t, out=self.p3)
+        t = self.b5(p3, out=self.t5)
+        p4 = self.c3_6(t, out=self.p4)
+        t = self.b7(p4, out=self.t7)
+        t = self.c3_8(t, out=self.t8)
+        cs = self.sp1.N
+        y0 = self.sp1(t, out=NHWC(self.spcat.t, 0, cs))
+        y1 = maxpool_nhwc(y0, NHWC(self.spcat.t, cs, cs), self.k)
+        y2 = maxpool_nhwc(y1, NHWC(self.spcat.t, 2 * cs, cs), self.k)
+        maxpool_nhwc(y2, NHWC(self.spcat.t, 3 * cs, cs), self.k)
+        t9 = self.sp2(self.spcat, out=self.t9)
+        h10 = self.h10(t9, out=self.h10_out)
+        upsample2x_nhwc(h10, NHWC(self.cat13.t, 0, self.h10.N))
+        t13 = self.c3_13(self.cat13, out=self.t13)
+        h14 = self.h14(t13, out=self.h14_out)
+        upsample2x_nhwc(h14, NHWC(self.cat17.t, 0, self.h14.N))
+        o3 = self.c3_17(self.cat17, out=self.o3)
+        self.h18(o3, out=NHWC(self.cat20.t, 0, self.h18.N))
+        o4 = self.c3_20(self.cat20, out=self.o4)
+        self.h21(o4, out=NHWC(self.cat23.t, 0, self.h21.N))
+        o5 = self.c3_23(self.cat23, out=self.o5)
+        outs = []
+        for d, o, dst in zip(self.det, (o3, o4, o5), self.dout):
+            d(o, out=dst)
+            outs.append(NHWC(dst.t, 0, self.no_real))
+        return outs
+
+
+class FastBEV:
+    """PointPillars BEV backbone + anchor head on fused convs."""
+
+    def __init__(self, model, batch: int, device="cuda"):
+        self.device = torch.device(device)
+        cfg = model.cfg
+        nx, ny, _ = cfg.voxel.grid_size
+        B = batch
+        bufs = self.bufs = _Buffers(self.device)
+        bb = model.backbone
+        self.blocks = []
+        H, W = ny, nx
+        for blk in bb.blocks:
+            convs = [_fc(c, device) for c in blk]
+            s = convs[0].s
+            H, W = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+            pp = [bufs.new(B, H, W, convs[0].N), bufs.new(B, H, W, convs[0].N)]
+            self.blocks.append((convs, pp, H, W))
+        self.ups = []
+        up_c = [u.conv.out_channels for u in bb.deblocks]
+        H0, W0 = self.blocks[0][2] * int(max(1, bb.deblocks[0].s)), self.blocks[0][3] * int(max(1, bb.deblocks[0].s))
+        if bb.deblocks[0].s < 1:
+            H0, W0 = self.blocks[0][2] // int(round(1 / bb.deblocks[0].s)), self.blocks[0][3] // int(round(1 / bb.deblocks[0].s))
+        self.out_hw = (H0, W0)
+        self.cat = bufs.new(B, H0, W0, sum(up_c))
+        off = 0
+        for u, c in zip(bb.deblocks, up_c):
+            assert u.fused, "call fuse_model() first"
+            self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device), off, c))
+            off += c
+        hd = model.head
+        merged = nn.Conv2d(hd.conv_cls.in_channels,
+                           hd.conv_cls.out_channels + hd.conv_box.out_channels + hd.conv_dir.out_channels, 1)
+        with torch.no_grad():
+            merged.weight.copy_(torch.cat([hd.conv_cls.weight, hd.conv_box.weight, hd.conv_dir.weight]).float())
+            merged.bias.copy_(torch.cat([hd.conv_cls.bias, hd.conv_box.bias, hd.conv_dir.bias]).float())
+        self.head = FusedConv(merged, act=ACT_NONE, device=device)
+        self.n_cls, self.n_box, self.n_dir = (hd.conv_cls.out_channels, hd.conv_box.out_channels,
+                                              hd.conv_dir.out_channels)
+        self.hout = bufs.new(B, H0, W0, self.head.N)
+
+    def forward(self, canvas: NHWC):
+        x = canvas
+        for (convs, pp, H, W), (up, off, c) in zip(self.blocks, self.ups):
+            for i, cv in enumerate(convs):
+                x = cv(x, out=pp[i % 2])
+            up(x, out=NHWC(self.cat.t, off, c))
+        self.head(self.cat, out=self.hout)
+        t = self.hout.t
+        return (NHWC(t, 0, self.n_cls), NHWC(t, self.n_cls, self.n_box),
+                NHWC(t, self.n_cls + self.n_box, self.n_dir))

@@ -132,3 +132,27 @@ class FusedConv:
             y = y + res.nchw().float()[:, : y.shape[1]]
         out.tensor()[..., : y.shape[1]].copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
         return out
+
+
+def maxpool_nhwc(x: NHWC, out: NHWC, k: int = 5, stream=None) -> NHWC:
+    """k x k max-pool, stride 1, pad k//2 (SPPF), slice → slice."""
+    B, H, W, C = x.shape
+    if x.t.device.type != "cuda":
+        y = F.max_pool2d(x.nchw().float(), k, 1, k // 2)
+        out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
+        return out
+    _native.call("tca_maxpool_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, k, _native.ptr(out.t),
+                 out.t.shape[-1], out.off, _native.stream_ptr(stream))
+    return out
+
+
+def upsample2x_nhwc(x: NHWC, out: NHWC, stream=None) -> NHWC:
+    """Nearest 2x upsample, slice → slice."""
+    B, H, W, C = x.shape
+    if x.t.device.type != "cuda":
+        y = F.interpolate(x.nchw().float(), scale_factor=2.0, mode="nearest")
+        out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
+        return out
+    _native.call("tca_upsample2x_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, _native.ptr(out.t),
+                 out.t.shape[-1], out.off, _native.stream_ptr(stream))
+    return out

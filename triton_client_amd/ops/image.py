@@ -91,8 +91,8 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
     for b in range(B):
         img = frames[b].numpy()
         o = golden.preprocess_image(img, (H, W), mode, scale, bias, swap_rb, pad_value, "NHWC")
-        if out_channels == 4:
-            o = np.concatenate([o, np.zeros_like(o[..., :1])], -1)
+        if out_channels > 3:
+            o = np.concatenate([o, np.zeros(o.shape[:-1] + (out_channels - 3,), o.dtype)], -1)
         res.append(o)
     arr = torch.from_numpy(np.stack(res)).to(dtype)
     if layout == "NCHW":

@@ -271,19 +271,32 @@ class AnchorPostprocess:
         if self.device.type == "cuda":
             self.ws = Workspace(self.device)
 
-    def __call__(self, cls: torch.Tensor, box: torch.Tensor, dir_: torch.Tensor, stream=None) -> NmsResult:
-        if cls.device.type != "cuda":
-            return self.cpu(cls, box, dir_)
+    def __call__(self, cls, box, dir_, stream=None) -> NmsResult:
+        """cls/box/dir: [B, C, H, W] tensors (NCHW or channels_last) or NHWC
+        channel-slice views of one merged head output."""
+        from .conv import NHWC
+        if isinstance(cls, NHWC):
+            if cls.t.device.type != "cuda":
+                return self.cpu(cls.nchw(), box.nchw(), dir_.nchw())
+            es = cls.t.element_size()
+            pc, pb, pd = (_native.ptr(v.t) + v.off * es for v in (cls, box, dir_))
+            lds = (cls.t.shape[-1], box.t.shape[-1], dir_.t.shape[-1])
+            lay, dt, B = 1, dtype_code(cls.t), cls.t.shape[0]
+        else:
+            if cls.device.type != "cuda":
+                return self.cpu(cls, box, dir_)
+            lay, c = layout_of(cls)
+            b_ = layout_of(box)[1]
+            d_ = layout_of(dir_)[1]
+            if layout_of(box)[0] != lay or layout_of(dir_)[0] != lay:
+                c, b_, d_, lay = cls.contiguous(), box.contiguous(), dir_.contiguous(), 0
+            pc, pb, pd = _native.ptr(c), _native.ptr(b_), _native.ptr(d_)
+            lds = (0, 0, 0)
+            dt, B = dtype_code(c), c.shape[0]
         cfg = self.cfg
-        lay, c = layout_of(cls)
-        b_ = layout_of(box)[1]
-        d_ = layout_of(dir_)[1]
-        if layout_of(box)[0] != lay or layout_of(dir_)[0] != lay:
-            c, b_, d_, lay = cls.contiguous(), box.contiguous(), dir_.contiguous(), 0
-        B = c.shape[0]
         cand = Candidates.alloc(self.ws, "anc_", B, self.cap, 7)
-        _native.call("tca_anchor_decode_filter", _native.ptr(c), _native.ptr(b_), _native.ptr(d_), dtype_code(c), lay,
-                     B, self.H, self.W, self.A, self.C, cfg.num_dir_bins, self._table, float(self.x0),
+        _native.call("tca_anchor_decode_filter", pc, pb, pd, dt, lay,
+                     B, self.H, self.W, self.A, self.C, cfg.num_dir_bins, *lds, self._table, float(self.x0),
                      float(self.xs), float(self.y0), float(self.ys), float(cfg.dir_offset),
                      float(cfg.dir_limit_offset), float(cfg.score_thresh), _native.ptr(cand.box),
                      _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count),

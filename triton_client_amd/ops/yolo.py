@@ -26,6 +26,11 @@ from .image import FrameXform
 from .nms import Candidates, NmsResult, SORT_CAP, sort_and_nms
 
 
+def _on_gpu(t) -> bool:
+    t = getattr(t, "t", t)
+    return t.device.type == "cuda"
+
+
 class YoloPostprocess:
     def __init__(self, nc: int, anchors: torch.Tensor | Sequence, img_hw=(640, 640), conf_thres: float = 0.3,
                  iou_thres: float = 0.45, max_det: int = 300, max_nms: int = 8192, agnostic: bool = False,
@@ -61,7 +66,7 @@ class YoloPostprocess:
         Returns NmsResult with box [B, max_det, 4] (xyxy, original-frame pixels if
         xform given), score, cls, count — and the decoded [B, N, 5+nc] tensor
         when decoded_out (KServe contract)."""
-        if heads[0].device.type != "cuda":
+        if not _on_gpu(heads[0]):
             return self.cpu(heads, xform)
         cand, decoded = self._filter(heads, decoded_out, stream)
         res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
@@ -69,20 +74,28 @@ class YoloPostprocess:
         return (res, decoded) if decoded_out else res
 
     def _filter(self, heads, decoded_out: bool, stream=None):
-        lay, h0 = layout_of(heads[0])
-        hs = [h0] + [layout_of(h)[1] for h in heads[1:]]
-        if any(layout_of(h)[0] != lay for h in hs):
-            hs = [h.contiguous() for h in hs]
-            lay = 0
-        B = hs[0].shape[0]
+        from .conv import NHWC
+        ldc = None
+        if isinstance(heads[0], NHWC):  # slices of padded NHWC buffers (fused-conv plan)
+            ptrs = [_native.ptr(h.t) + h.off * h.t.element_size() for h in heads]
+            ldc = (ctypes.c_int * 3)(*[h.t.shape[-1] for h in heads])
+            lay, dt, B = 1, dtype_code(heads[0].t), heads[0].t.shape[0]
+        else:
+            lay, h0 = layout_of(heads[0])
+            hs = [h0] + [layout_of(h)[1] for h in heads[1:]]
+            if any(layout_of(h)[0] != lay for h in hs):
+                hs = [h.contiguous() for h in hs]
+                lay = 0
+            ptrs = [_native.ptr(h) for h in hs]
+            dt, B = dtype_code(hs[0]), hs[0].shape[0]
         cap = self.num_anchors_total * (self.nc if self.multi_label else 1)
         cap = min(cap, 1 << 20)
         cand = Candidates.alloc(self.ws, "yolo_", B, cap, 4)
         decoded = None
         if decoded_out:
             decoded = self.ws.get("decoded", (B, self.num_anchors_total, self.nc + 5), torch.float32)
-        _native.call("tca_yolo_decode_filter", _native.ptr(hs[0]), _native.ptr(hs[1]), _native.ptr(hs[2]),
-                     dtype_code(hs[0]), lay, B, self.na, self.nc, self.hw, self.strides, self.anc,
+        _native.call("tca_yolo_decode_filter", ptrs[0], ptrs[1], ptrs[2],
+                     dt, lay, B, self.na, self.nc, self.hw, self.strides, ldc, self.anc,
                      float(self.conf_thres), int(self.multi_label), _native.ptr(self._class_mask),
                      _native.ptr(cand.box), _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key),
                      _native.ptr(cand.count), cap, _native.ptr(decoded), _native.stream_ptr(stream))
@@ -90,14 +103,17 @@ class YoloPostprocess:
 
     def decode(self, heads: List[torch.Tensor], stream=None) -> torch.Tensor:
         """Decoded [B, N, 5+nc] fp32 (the ONNX YOLOv5 output contract)."""
-        if heads[0].device.type != "cuda":
+        if not _on_gpu(heads[0]):
             return self.decode_cpu(heads)
         return self._filter(heads, True, stream)[1]
 
     # -------------------------------------------------------------- CPU
     def decode_cpu(self, heads: List[torch.Tensor]) -> torch.Tensor:
         from ..models.yolov5 import yolo_decode_reference
-        return yolo_decode_reference([h.float().contiguous() for h in heads], self.anchors)
+        from .conv import NHWC
+        C = self.na * (self.nc + 5)
+        hs = [h.nchw()[:, :C] if isinstance(h, NHWC) else h for h in heads]
+        return yolo_decode_reference([h.float().contiguous() for h in hs], self.anchors)
 
     def cpu(self, heads, xform: Optional[FrameXform] = None) -> NmsResult:
         return self.postprocess_decoded(self.decode_cpu(heads).numpy(), xform)

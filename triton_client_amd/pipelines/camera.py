@@ -25,7 +25,7 @@ class CameraPipeline:
     def __init__(self, model: Optional[YOLOv5] = None, batch: int = 16, src_hw: Tuple[int, int] = (720, 1280),
                  img_hw: Tuple[int, int] = (640, 640), mode: str = "letterbox", dtype: torch.dtype = torch.bfloat16,
                  conf_thres: float = 0.3, iou_thres: float = 0.45, max_det: int = 300, device="cuda",
-                 variant: str = "n", nc: int = 80, seed: int = 0, swap_rb: bool = False):
+                 variant: str = "n", nc: int = 80, seed: int = 0, swap_rb: bool = False, fast: bool = True):
         self.device = torch.device(device)
         self.B, self.src_hw, self.img_hw, self.mode, self.dtype = batch, tuple(src_hw), tuple(img_hw), mode, dtype
         self.swap_rb = swap_rb
@@ -39,6 +39,16 @@ class CameraPipeline:
         self.xform, _ = frame_xform(self.src_hw, self.img_hw, mode)
         self.post = YoloPostprocess(model.cfg.nc, model.anchors.cpu(), img_hw, conf_thres, iou_thres, max_det,
                                     device=self.device)
+        # fused-MFMA concat-free plan (built lazily so calibration edits to the
+        # module weights are picked up); the PyTorch module path stays for
+        # validation and for CPU runs
+        self.use_fast = fast and self.device.type == "cuda"
+        self.fast = None
+
+    def build_fast(self):
+        from ..models.fast import FastYOLOv5
+        self.fast = FastYOLOv5(self.model, self.B, self.img_hw, self.device)
+        return self.fast
 
     @torch.no_grad()
     def calibrate_detection_density(self, target_per_frame: float = 100.0, lsuv: bool = True) -> float:
@@ -82,6 +92,11 @@ class CameraPipeline:
     @torch.no_grad()
     def step(self):
         """Capture-safe: reads ``self.frames``, returns the NmsResult buffers."""
+        if self.use_fast:
+            f = self.fast or self.build_fast()
+            preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", f.IN_CHANNELS,
+                       swap_rb=self.swap_rb, out=f.x.t.permute(0, 3, 1, 2))
+            return self.post(f.forward(), self.xform)
         preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", 3, swap_rb=self.swap_rb,
                    out=self.inp)
         heads = self.model(self.inp)

@@ -30,7 +30,7 @@ class LidarPipeline:
     def __init__(self, model: Optional[PointPillars] = None, batch: int = 16, max_points: int = 131072,
                  layout: Optional[PointLayout] = None, z_offset: float = 1.5, normalize_intensity: bool = True,
                  dtype: torch.dtype = torch.bfloat16, device="cuda", cfg: Optional[PointPillarsConfig] = None,
-                 seed: int = 0):
+                 seed: int = 0, fast: bool = True):
         self.device = torch.device(device)
         self.B, self.max_points, self.dtype = batch, max_points, dtype
         self.layout = layout or PointLayout.xyzi_f32()
@@ -51,6 +51,13 @@ class LidarPipeline:
         self.enc = PillarEncoder(v, model.vfe.fused_weight.float(), model.vfe.fused_bias.float(), batch,
                                  device=self.device, channels=self.cfg.vfe_filters)
         self.post = AnchorPostprocess(self.cfg, batch, device=self.device)
+        self.use_fast = fast and self.device.type == "cuda"
+        self.fast = None
+
+    def build_fast(self):
+        from ..models.fast import FastBEV
+        self.fast = FastBEV(self.model, self.B, self.device)
+        return self.fast
 
     @torch.no_grad()
     def calibrate_detection_density(self, target_per_frame: float = 2000.0, lsuv: bool = True) -> float:
@@ -98,5 +105,9 @@ class LidarPipeline:
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
+        if self.use_fast:
+            from ..ops.conv import NHWC
+            f = self.fast or self.build_fast()
+            return self.post(*f.forward(NHWC(self.enc.canvas)))
         cls, box, dir_ = self.model.bev_forward(canvas)
         return self.post(cls, box, dir_)

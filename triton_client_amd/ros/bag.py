@@ -1,0 +1,96 @@
+"""Bag files: record / replay topic streams (reference: ``rosbag.Bag`` in
+``communicator/bag_inference{2d,3d}.py``, ``tools/bag_stitch.py``).
+
+``rosbag`` is not installed, so this is a compact self-describing format
+with the same API (``Bag(path, 'r'|'w')``, ``write(topic, msg, t)``,
+``read_messages(topics=...)`` → ``(topic, msg, t)``, ``get_message_count``):
+a magic header, then length-prefixed msgpack records
+``{topic, type, t_ns, msg}`` where ``msg`` is the message's field dict
+(bytes payloads stay binary, no pickling — a bag never executes code when
+read).  Reading streams record by record (large bags are never loaded whole).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Iterator, Optional, Sequence, Tuple
+
+import msgpack
+
+from . import msgs
+
+MAGIC = b"TCABAG1\n"
+
+
+class Bag:
+    def __init__(self, path: str, mode: str = "r"):
+        if mode not in ("r", "w", "a"):
+            raise ValueError("mode must be r, w or a")
+        self.path, self.mode = path, mode
+        self._f = open(path, {"r": "rb", "w": "wb", "a": "ab"}[mode])
+        if mode == "w":
+            self._f.write(MAGIC)
+        elif mode == "r":
+            if self._f.read(len(MAGIC)) != MAGIC:
+                raise ValueError(f"{path}: not a triton_client_amd bag")
+
+    def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
+        t = t or getattr(getattr(msg, "header", None), "stamp", None) or msgs.Time.now()
+        rec = msgpack.packb({"topic": topic, "type": msgs.TYPE_NAMES.get(type(msg), type(msg).__name__),
+                             "t": t.to_nsec(), "msg": msgs.to_dict(msg)}, use_bin_type=True)
+        self._f.write(struct.pack("<Q", len(rec)))
+        self._f.write(rec)
+
+    def _records(self) -> Iterator[dict]:
+        self._f.seek(len(MAGIC))
+        while True:
+            hdr = self._f.read(8)
+            if len(hdr) < 8:
+                return
+            (n,) = struct.unpack("<Q", hdr)
+            yield msgpack.unpackb(self._f.read(n), raw=False)
+
+    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0) -> Iterator[Tuple[str, object, msgs.Time]]:
+        """Yields (topic, msg, t).  ``start_seq`` resumes a replay after the
+        first ``start_seq`` matching messages."""
+        k = 0
+        for r in self._records():
+            if topics and r["topic"] not in topics:
+                continue
+            k += 1
+            if k <= start_seq:
+                continue
+            cls = msgs.MSG_TYPES.get(r["type"])
+            m = msgs.from_dict(cls, r["msg"]) if cls else r["msg"]
+            t = msgs.Time(r["t"] // 1_000_000_000, r["t"] % 1_000_000_000)
+            yield r["topic"], m, t
+
+    def get_message_count(self, topic_filters: Optional[Sequence[str]] = None) -> int:
+        return sum(1 for r in self._records() if not topic_filters or r["topic"] in topic_filters)
+
+    def get_type_and_topic_info(self):
+        info = {}
+        for r in self._records():
+            d = info.setdefault(r["topic"], {"type": r["type"], "count": 0})
+            d["count"] += 1
+        return info
+
+    def close(self) -> None:
+        self._f.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def stitch(src: str, dst: str, n: int = 500, topics: Optional[Sequence[str]] = None) -> int:
+    """Copy the first n messages (reference tools/bag_stitch.py)."""
+    k = 0
+    with Bag(src) as bi, Bag(dst, "w") as bo:
+        for topic, m, t in bi.read_messages(topics):
+            if k >= n:
+                break
+            bo.write(topic, m, t)
+            k += 1
+    return k

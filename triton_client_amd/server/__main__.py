@@ -1,0 +1,32 @@
+"""Standalone server: python -m triton_client_amd.server --models YOLOv5nCOCO,pointpillar_kitti"""
+import argparse
+import logging
+
+from . import KServeServer, ModelRepository
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="KServe-v2 (Triton protocol) server on MI355X")
+    ap.add_argument("--models", default="YOLOv5nCOCO,pointpillar_kitti")
+    ap.add_argument("--model-repository", default=None, help="Triton-style directory of config.pbtxt files")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8001)
+    ap.add_argument("--metrics-port", type=int, default=8002)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--workers", type=int, default=8)
+    args = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    if args.model_repository:
+        repo = ModelRepository.from_directory(args.model_repository, args.device)
+    else:
+        repo = ModelRepository(args.device)
+        for m in filter(None, args.models.split(",")):
+            repo.load(m.strip())
+    srv = KServeServer(repo, f"{args.host}:{args.port}", max_workers=args.workers,
+                       metrics_port=args.metrics_port if args.metrics_port > 0 else None).start()
+    logging.info("KServe-v2 server on %s, models: %s", srv.target, [m.name for m in repo.models()])
+    srv.wait()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,269 @@
+"""In-process / standalone KServe-v2 (Triton-protocol) gRPC server.
+
+Replaces the external Triton server the reference talks to
+(``README.md:62-67``; gRPC :8001, metrics :8002).  Implements
+``GRPCInferenceService`` with generic handlers over the runtime-built
+protobuf types (``triton_client_amd.proto``): ServerLive/Ready, ModelReady,
+ServerMetadata, ModelMetadata, ModelConfig, ModelInfer, ModelStreamInfer,
+ModelStatistics, RepositoryIndex/Load/Unload.  The same server doubles as
+the test backend with an optional fault injector (delay /
+drop / corrupt — SURVEY §5.3) and exports Triton-named Prometheus metrics.
+
+Run standalone::
+
+    python -m triton_client_amd.server --models YOLOv5nCOCO,pointpillar_kitti --port 8001
+"""
+from __future__ import annotations
+
+import random
+import threading
+import time
+from concurrent import futures
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import grpc
+import numpy as np
+
+from ..proto import KSERVE_TO_NP, SERVICE, service_pb2 as pb
+from .model import InferError, ServedModel
+from .repository import ModelRepository
+
+_BF16 = "BF16"
+
+
+@dataclass
+class FaultInjector:
+    delay_s: float = 0.0
+    drop_rate: float = 0.0
+    corrupt_rate: float = 0.0
+    seed: int = 0
+
+    def __post_init__(self):
+        self._rng = random.Random(self.seed)
+        self._lock = threading.Lock()
+
+    def roll(self, p: float) -> bool:
+        if p <= 0:
+            return False
+        with self._lock:
+            return self._rng.random() < p
+
+
+def _np_dtype(dt: str):
+    if dt == _BF16:
+        return np.dtype(np.uint16)
+    return np.dtype(KSERVE_TO_NP[dt])
+
+
+def _kserve_dtype(a: np.ndarray) -> str:
+    from ..proto import NP_TO_KSERVE
+    return NP_TO_KSERVE[str(a.dtype)]
+
+
+def decode_inputs(req) -> Dict[str, np.ndarray]:
+    out = {}
+    raw = list(req.raw_input_contents)
+    for i, t in enumerate(req.inputs):
+        shape = tuple(int(s) for s in t.shape)
+        if i < len(raw) and raw:
+            a = np.frombuffer(raw[i], dtype=_np_dtype(t.datatype))
+        else:  # typed contents
+            c = t.contents
+            src = {"FP32": c.fp32_contents, "FP64": c.fp64_contents, "INT32": c.int_contents,
+                   "INT64": c.int64_contents, "UINT32": c.uint_contents, "UINT64": c.uint64_contents,
+                   "BOOL": c.bool_contents}.get(t.datatype)
+            if src is None:
+                raise InferError(f"unsupported typed contents for {t.datatype}")
+            a = np.asarray(src, dtype=_np_dtype(t.datatype))
+        if a.size != int(np.prod(shape)):
+            raise InferError(f"input '{t.name}': {a.size} elements do not match shape {list(shape)}")
+        out[t.name] = a.reshape(shape)
+    return out
+
+
+def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], corrupt: bool = False):
+    resp = pb.ModelInferResponse(model_name=model.name, model_version=model.version, id=req.id)
+    names = [o.name for o in req.outputs] or list(outputs.keys())
+    for n in names:
+        if n not in outputs:
+            raise InferError(f"unknown output '{n}' for model '{model.name}'")
+        a = np.ascontiguousarray(outputs[n])
+        t = resp.outputs.add(name=n, datatype=_kserve_dtype(a))
+        t.shape.extend(a.shape)
+        b = a.tobytes()
+        if corrupt and len(b):
+            b = bytes(len(b))  # zeroed payload: detectable by clients, keeps the shape contract
+        resp.raw_output_contents.append(b)
+    return resp
+
+
+class GRPCInferenceServicer:
+    def __init__(self, repo: ModelRepository, fault: Optional[FaultInjector] = None, metrics=None,
+                 server_name: str = "triton_client_amd", version: str = "0.1.0"):
+        self.repo = repo
+        self.fault = fault or FaultInjector()
+        self.metrics = metrics
+        self.server_name, self.version = server_name, version
+
+    # -------------------------------------------------------------- health / metadata
+    def ServerLive(self, req, ctx):
+        return pb.ServerLiveResponse(live=True)
+
+    def ServerReady(self, req, ctx):
+        return pb.ServerReadyResponse(ready=self.repo.all_ready())
+
+    def ModelReady(self, req, ctx):
+        m = self.repo.get(req.name, req.version)
+        return pb.ModelReadyResponse(ready=bool(m and m.ready))
+
+    def ServerMetadata(self, req, ctx):
+        return pb.ServerMetadataResponse(name=self.server_name, version=self.version,
+                                         extensions=["classification", "model_repository", "statistics",
+                                                     "binary_tensor_data", "schedule_policy"])
+
+    def _model(self, name, version, ctx) -> ServedModel:
+        m = self.repo.get(name, version)
+        if m is None:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, f"Request for unknown model: '{name}' is not found")
+        if not m.ready:
+            ctx.abort(grpc.StatusCode.UNAVAILABLE, f"Request for unknown model: '{name}' is not ready")
+        return m
+
+    def ModelMetadata(self, req, ctx):
+        return self._model(req.name, req.version, ctx).metadata()
+
+    def ModelConfig(self, req, ctx):
+        return pb.ModelConfigResponse(config=self._model(req.name, req.version, ctx).config())
+
+    def ModelStatistics(self, req, ctx):
+        resp = pb.ModelStatisticsResponse()
+        for m in self.repo.models(req.name or None):
+            st = m.stats
+            ms = resp.model_stats.add(name=m.name, version=m.version, last_inference=st.last_inference_ms,
+                                      inference_count=st.inference_count, execution_count=st.execution_count)
+            ms.inference_stats.success.count = st.inference_count
+            ms.inference_stats.success.ns = st.success_ns
+            ms.inference_stats.fail.count = st.fail_count
+            ms.inference_stats.compute_infer.count = st.execution_count
+            ms.inference_stats.compute_infer.ns = st.compute_ns
+        return resp
+
+    def RepositoryIndex(self, req, ctx):
+        resp = pb.RepositoryIndexResponse()
+        for name, state in self.repo.index():
+            if req.ready and state != "READY":
+                continue
+            resp.models.add(name=name, version="1", state=state)
+        return resp
+
+    def RepositoryModelLoad(self, req, ctx):
+        try:
+            self.repo.load(req.model_name)
+        except KeyError as e:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
+        return pb.RepositoryModelLoadResponse()
+
+    def RepositoryModelUnload(self, req, ctx):
+        self.repo.unload(req.model_name)
+        return pb.RepositoryModelUnloadResponse()
+
+    # -------------------------------------------------------------- inference
+    def _infer(self, req, ctx):
+        t0 = time.perf_counter()
+        m = self._model(req.model_name, req.model_version, ctx)
+        if self.fault.delay_s:
+            time.sleep(self.fault.delay_s)
+        if self.fault.roll(self.fault.drop_rate):
+            ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
+        try:
+            inputs = decode_inputs(req)
+            outputs = m(inputs, [o.name for o in req.outputs])
+            resp = encode_response(m, req, outputs, corrupt=self.fault.roll(self.fault.corrupt_rate))
+        except InferError as e:
+            if self.metrics:
+                self.metrics.request(m.name, False, time.perf_counter() - t0)
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        if self.metrics:
+            self.metrics.request(m.name, True, time.perf_counter() - t0)
+        return resp
+
+    def ModelInfer(self, req, ctx):
+        return self._infer(req, ctx)
+
+    def ModelStreamInfer(self, req_iter, ctx):
+        for req in req_iter:
+            try:
+                resp = self._infer(req, _StreamCtx(ctx))
+                yield pb.ModelStreamInferResponse(infer_response=resp)
+            except _StreamAbort as e:
+                yield pb.ModelStreamInferResponse(error_message=str(e))
+
+
+class _StreamAbort(Exception):
+    pass
+
+
+class _StreamCtx:
+    """Per-request errors on a stream become error_message responses."""
+
+    def __init__(self, ctx):
+        self._ctx = ctx
+
+    def abort(self, code, details):
+        raise _StreamAbort(details)
+
+
+def _handlers(servicer: GRPCInferenceServicer):
+    from ..proto import SERVICE_METHODS
+    h = {}
+    for rpc, req, resp, cs, ss in SERVICE_METHODS:
+        fn = getattr(servicer, rpc)
+        de = getattr(pb, req).FromString
+        ser = getattr(pb, resp).SerializeToString
+        if cs and ss:
+            h[rpc] = grpc.stream_stream_rpc_method_handler(fn, request_deserializer=de, response_serializer=ser)
+        else:
+            h[rpc] = grpc.unary_unary_rpc_method_handler(fn, request_deserializer=de, response_serializer=ser)
+    return grpc.method_handlers_generic_handler(SERVICE, h)
+
+
+class KServeServer:
+    def __init__(self, repo: ModelRepository, address: str = "127.0.0.1:8001", max_workers: int = 8,
+                 max_message_bytes: int = 512 << 20, fault: Optional[FaultInjector] = None,
+                 metrics_port: Optional[int] = None):
+        self.repo = repo
+        self.address = address
+        metrics = None
+        if metrics_port is not None:
+            from ..utils.metrics import ServerMetrics
+            metrics = ServerMetrics(port=metrics_port)
+        self.servicer = GRPCInferenceServicer(repo, fault, metrics)
+        opts = [("grpc.max_send_message_length", max_message_bytes),
+                ("grpc.max_receive_message_length", max_message_bytes)]
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers), options=opts)
+        self.server.add_generic_rpc_handlers((_handlers(self.servicer),))
+        self.port = self.server.add_insecure_port(address)
+        if self.port == 0:
+            raise RuntimeError(f"could not bind {address}")
+
+    @property
+    def target(self) -> str:
+        host = self.address.rsplit(":", 1)[0]
+        return f"{host}:{self.port}"
+
+    def start(self) -> "KServeServer":
+        self.server.start()
+        return self
+
+    def stop(self, grace: float = 0.5) -> None:
+        self.server.stop(grace)
+
+    def wait(self) -> None:
+        self.server.wait_for_termination()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

@@ -1,0 +1,144 @@
+"""Model repository: name → servable factory, load/unload/index.
+
+Known model names mirror the reference's deployments
+(``examples/*/config.pbtxt``, ``docker/server/models/weed_detector``,
+``.vscode/launch.json:8-47``).  A Triton-style directory
+(``<repo>/<model>/config.pbtxt``) can also be scanned: each config's name
+selects the factory and its declared tensor dims (e.g. image size) are
+honoured.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Callable, Dict, Iterable, List, Optional, Tuple
+
+from .model import EchoModel, ServedModel
+
+Factory = Callable[..., ServedModel]
+
+
+def _yolo(name, variant="n", nc=80, img=640):
+    def f(device="auto", **kw):
+        from .models import YoloV5Model
+        return YoloV5Model(name, variant, nc, img, device=device, **kw)
+    return f
+
+
+def _pointpillars(name):
+    def f(device="auto", **kw):
+        from .models import PointPillarsModel
+        return PointPillarsModel(name, device=device, **kw)
+    return f
+
+
+def _family(name: str) -> Optional[str]:
+    n = name.lower()
+    if "yolo" in n or "weed" in n:
+        return "yolo"
+    if "pointpillar" in n or "pillar" in n:
+        return "pointpillars"
+    if "retina" in n or "fcos" in n or "detectron" in n or n == "test_model":
+        return "detectron"
+    if "centerpoint" in n:
+        return "centerpoint"
+    if "echo" in n:
+        return "echo"
+    return None
+
+
+FACTORIES: Dict[str, Factory] = {
+    "YOLOv5nCOCO": _yolo("YOLOv5nCOCO", "n", 80, 640),
+    "YOLOv5n": _yolo("YOLOv5n", "n", 80, 640),
+    "YOLOv5nCROP": _yolo("YOLOv5nCROP", "n", 2, 512),
+    "weed_detector": _yolo("weed_detector", "n", 2, 512),
+    "pointpillar_kitti": _pointpillars("pointpillar_kitti"),
+    "pointpillar_python": _pointpillars("pointpillar_python"),
+    "echo": lambda device="auto", **kw: EchoModel("echo"),
+}
+
+
+def register_factory(name: str, factory: Factory) -> None:
+    FACTORIES[name] = factory
+
+
+class ModelRepository:
+    def __init__(self, device="auto"):
+        self.device = device
+        self._models: Dict[str, ServedModel] = {}
+        self._lock = threading.Lock()
+
+    def add(self, model: ServedModel, load: bool = True) -> ServedModel:
+        if load and not model.ready:
+            model.load()
+        with self._lock:
+            self._models[model.name] = model
+        return model
+
+    def load(self, name: str, **kw) -> ServedModel:
+        with self._lock:
+            m = self._models.get(name)
+        if m is not None and m.ready:
+            return m
+        if m is None:
+            if name not in FACTORIES:
+                raise KeyError(f"no factory for model '{name}'")
+            m = FACTORIES[name](device=self.device, **kw)
+        return self.add(m)
+
+    def unload(self, name: str) -> None:
+        with self._lock:
+            m = self._models.get(name)
+        if m is not None:
+            m.unload()
+
+    def get(self, name: str, version: str = "") -> Optional[ServedModel]:
+        with self._lock:
+            m = self._models.get(name)
+        if m is None or (version and version != m.version):
+            return None
+        return m
+
+    def models(self, name: Optional[str] = None) -> List[ServedModel]:
+        with self._lock:
+            ms = list(self._models.values())
+        return [m for m in ms if name is None or m.name == name]
+
+    def index(self) -> List[Tuple[str, str]]:
+        with self._lock:
+            loaded = {n: ("READY" if m.ready else "UNAVAILABLE") for n, m in self._models.items()}
+        names = sorted(set(FACTORIES) | set(loaded))
+        return [(n, loaded.get(n, "UNLOADED")) for n in names]
+
+    def all_ready(self) -> bool:
+        with self._lock:
+            return all(m.ready for m in self._models.values())
+
+    @staticmethod
+    def from_directory(path: str, device="auto", load: bool = True) -> "ModelRepository":
+        """Scan a Triton model repository; each ``config.pbtxt`` picks a family."""
+        from ..proto import parse_config_pbtxt
+
+        repo = ModelRepository(device)
+        for entry in sorted(os.listdir(path)):
+            cfgp = os.path.join(path, entry, "config.pbtxt")
+            if not os.path.isfile(cfgp):
+                continue
+            with open(cfgp) as f:
+                cfg = parse_config_pbtxt(f.read())
+            name = cfg.name or entry
+            fam = _family(name)
+            if name in FACTORIES:
+                m = FACTORIES[name](device=device)
+            elif fam == "yolo":
+                dims = list(cfg.input[0].dims)
+                out = list(cfg.output[0].dims)
+                from .models import YoloV5Model
+                m = YoloV5Model(name, "n", out[-1] - 5, dims[-1], device=device)
+            elif fam == "pointpillars":
+                from .models import PointPillarsModel
+                m = PointPillarsModel(name, device=device)
+            else:
+                continue
+            repo.add(m, load=load)
+        return repo
