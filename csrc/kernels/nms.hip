@@ -213,9 +213,13 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
                                                       const int* __restrict__ sorted_n, int cap, int pre_max,
                                                       int mask_words, float thr, int agnostic,
                                                       uint64_t* __restrict__ mask) {
-  __shared__ float sbox[64][8];
-  __shared__ float scs[64][2];
+  // one wave per block; tiles of 64 rows x 64 columns of the sorted list
+  __shared__ float sbox[64][8];   // column boxes (+ [7] = circumradius for MODE 1)
+  __shared__ float rbox[64][8];   // row boxes (MODE 1)
+  __shared__ float scs[64][2], rcs[64][2];
   __shared__ int scls[64];
+  __shared__ unsigned short pairs[64 * 64];
+  __shared__ unsigned long long rowbits[64];
   const int b = blockIdx.y, tid = threadIdx.x;
   const int n = sorted_n[b];
   const int nb = (n + 63) >> 6;
@@ -232,28 +236,69 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
       const int s = ob[j];
       for (int d = 0; d < nbox; ++d) sbox[tid][d] = bb[(long)s * box_dim + d];
       scls[tid] = cb_[s];
-      if (MODE == 1) sincosf(sbox[tid][6], &scs[tid][1], &scs[tid][0]);
+      if (MODE == 1) {
+        sincosf(sbox[tid][6], &scs[tid][1], &scs[tid][0]);
+        sbox[tid][7] = 0.5f * sqrtf(sbox[tid][3] * sbox[tid][3] + sbox[tid][4] * sbox[tid][4]);
+      }
     }
-    __syncthreads();
     const int i = rb * 64 + tid;
+    if (MODE == 0) {
+      __syncthreads();
+      if (i < n) {
+        const int s = ob[i];
+        float me[4];
+        for (int d = 0; d < 4; ++d) me[d] = bb[(long)s * box_dim + d];
+        const int mc = cb_[s];
+        uint64_t bits = 0;
+        const int jmax = min(64, n - cbk * 64);
+        for (int jj = 0; jj < jmax; ++jj) {
+          const int jg = cbk * 64 + jj;
+          if (jg <= i) continue;
+          if (!agnostic && scls[jj] != mc) continue;
+          if (iou_aa(me, sbox[jj]) > thr) bits |= (1ull << jj);
+        }
+        mb[(long)i * mask_words + cbk] = bits;
+      }
+      __syncthreads();
+      continue;
+    }
+    // MODE 1: cheap circumcircle test over all 64x64 pairs, compact the
+    // candidates (wave ballot + popcount), then evaluate only those densely.
+    float rx = 0.f, ry = 0.f, rr = -1.f;
+    int rc = 0;
     if (i < n) {
       const int s = ob[i];
-      float me[8];
-      for (int d = 0; d < nbox; ++d) me[d] = bb[(long)s * box_dim + d];
-      const int mc = cb_[s];
-      float mcos = 1.f, msin = 0.f;
-      if (MODE == 1) sincosf(me[6], &msin, &mcos);
-      uint64_t bits = 0;
-      const int jmax = min(64, n - cbk * 64);
-      for (int jj = 0; jj < jmax; ++jj) {
-        const int jg = cbk * 64 + jj;
-        if (jg <= i) continue;
-        if (!agnostic && scls[jj] != mc) continue;
-        const float v = MODE == 0 ? iou_aa(me, sbox[jj]) : iou_bev(me, sbox[jj], mcos, msin, scs[jj][0], scs[jj][1]);
-        if (v > thr) bits |= (1ull << jj);
-      }
-      mb[(long)i * mask_words + cbk] = bits;
+      for (int d = 0; d < 7; ++d) rbox[tid][d] = bb[(long)s * box_dim + d];
+      sincosf(rbox[tid][6], &rcs[tid][1], &rcs[tid][0]);
+      rx = rbox[tid][0];
+      ry = rbox[tid][1];
+      rr = 0.5f * sqrtf(rbox[tid][3] * rbox[tid][3] + rbox[tid][4] * rbox[tid][4]);
+      rc = cb_[s];
     }
+    rowbits[tid] = 0ull;
+    __syncthreads();
+    int cnt = 0;  // wave-uniform
+    const int jmax = min(64, n - cbk * 64);
+    const unsigned long long lt = (tid == 0) ? 0ull : (~0ull >> (64 - tid));
+    for (int jj = 0; jj < jmax; ++jj) {
+      const int jg = cbk * 64 + jj;
+      bool c = false;
+      if (i < n && jg > i && (agnostic || scls[jj] == rc)) {
+        const float dx = sbox[jj][0] - rx, dy = sbox[jj][1] - ry, rs = sbox[jj][7] + rr;
+        c = dx * dx + dy * dy <= rs * rs;
+      }
+      const unsigned long long bal = __ballot(c);
+      if (c) pairs[cnt + __popcll(bal & lt)] = (unsigned short)((tid << 6) | jj);
+      cnt += __popcll(bal);
+    }
+    __syncthreads();
+    for (int p = tid; p < cnt; p += 64) {
+      const int r = pairs[p] >> 6, cc = pairs[p] & 63;
+      const float v = iou_bev(rbox[r], sbox[cc], rcs[r][0], rcs[r][1], scs[cc][0], scs[cc][1]);
+      if (v > thr) atomicOr(&rowbits[r], 1ull << cc);
+    }
+    __syncthreads();
+    if (i < n) mb[(long)i * mask_words + cbk] = rowbits[tid];
     __syncthreads();
   }
 }

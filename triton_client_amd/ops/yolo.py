@@ -27,7 +27,9 @@ from .nms import Candidates, NmsResult, SORT_CAP, sort_and_nms
 
 
 def _on_gpu(t) -> bool:
-    t = getattr(t, "t", t)
+    from .conv import NHWC
+    if isinstance(t, NHWC):
+        t = t.t
     return t.device.type == "cuda"
 
 
