@@ -1,0 +1,83 @@
+"""Entry points (main/main3d/bag2d/bag3d/evaluate/record) on the CPU with
+synthetic bags; remote engines against the in-process KServe server."""
+import json
+import os
+
+import pytest
+import yaml
+
+from triton_client_amd.cli import bag2d, bag3d, evaluate, main as main2d, main3d, record
+from triton_client_amd.ros import Bag, reset_default_bus
+from triton_client_amd.server import KServeServer, ModelRepository
+from triton_client_amd.server.models import YoloV5Model
+
+
+@pytest.fixture(scope="module")
+def bags(tmp_path_factory):
+    d = tmp_path_factory.mktemp("bags")
+    cam, pc = str(d / "cam.bag"), str(d / "pc.bag")
+    assert record.main([cam, "--frames", "4", "--cam", "96x160", "--gt"]) == 0
+    assert record.main([pc, "--frames", "2", "--no-camera", "--lidar", "--rings", "16", "--columns", "256"]) == 0
+    return d, cam, pc
+
+
+@pytest.fixture(scope="module")
+def server():
+    repo = ModelRepository("cpu")
+    repo.add(YoloV5Model("YOLOv5n", img=128, device="cpu"))
+    srv = KServeServer(repo, "127.0.0.1:0").start()
+    yield srv
+    srv.stop()
+
+
+def test_reference_flags_parse():
+    f = main2d.parse_args(["-v", "-a", "-m", "YOLOv5nCROP", "-x", "1", "-b", "2", "-c", "2", "-s", "VGG", "-i", "local"])
+    assert (f.verbose, f.async_set, f.model_name, f.model_version, f.batch_size, f.classes, f.scaling,
+            f.image_src) == (True, True, "YOLOv5nCROP", "1", 2, 2, "VGG", "local")
+    f3 = main3d.parse_args(["--streaming"])
+    assert f3.streaming and f3.model_name == "pointpillar_kitti" and f3.score_thresh == 0.5 and f3.labels == "2"
+
+
+def test_bag2d_local_and_remote(bags, server, tmp_path):
+    d, cam, _ = bags
+    out = str(tmp_path / "png")
+    assert bag2d.main(["--bag", cam, "--engine", "local", "--device", "cpu", "--out", out,
+                       "--frames-per-step", "2"]) == 0
+    assert len(os.listdir(out)) == 4
+    params = tmp_path / "p.yaml"
+    params.write_text(yaml.safe_dump({"grpc_channel": server.target, "sub_topic": "/camera/color/image_raw",
+                                      "pub_topic": "/det", "gt_topic": "/camera/color/Detection2DArray"}))
+    ob = str(tmp_path / "o.bag")
+    assert bag2d.main(["--bag", cam, "--params", str(params), "-m", "YOLOv5n", "--out", "", "--out-bag", ob,
+                       "-a"]) == 0
+    with Bag(ob) as b:
+        assert sum(1 for t, _, _ in b.read_messages(topics=["/det"])) == 4
+
+
+def test_bag3d_local(bags, tmp_path):
+    _, _, pc = bags
+    ob = str(tmp_path / "pc_out.bag")
+    assert bag3d.main(["--bag", pc, "--engine", "local", "--device", "cpu", "--out-bag", ob, "--labels", "all",
+                       "--score-thresh", "0"]) == 0
+    with Bag(ob) as b:
+        out = [m for t, m, _ in b.read_messages(topics=["/detections_3d"])]
+    assert len(out) == 2 and all(len(m.boxes) > 0 for m in out)
+
+
+def test_evaluate_bag(bags, tmp_path):
+    _, cam, _ = bags
+    js = str(tmp_path / "eval.json")
+    assert evaluate.main(["--bag", cam, "--engine", "local", "--device", "cpu", "-m", "YOLOv5nCROP",
+                          "--eval-port", "0", "--json", js]) == 0
+    s = json.load(open(js))
+    assert s["matched_images"] == 4 and 0.0 <= s["map50_95"] <= 1.0
+
+
+def test_main_plays_bag_through_topic_bus(bags, server, tmp_path):
+    _, cam, _ = bags
+    reset_default_bus()
+    params = tmp_path / "p.yaml"
+    params.write_text(yaml.safe_dump({"grpc_channel": server.target, "sub_topic": "/camera/color/image_raw",
+                                      "pub_topic": "/det", "gt_topic": "/gt"}))
+    assert main2d.main(["--params", str(params), "--play", cam, "--spin-timeout", "60"]) == 0
+    reset_default_bus()

@@ -110,10 +110,8 @@ class PointPillarPostprocess(Postprocess):
         return Postprocess.load_class_names(namesfile or os.path.join(DATA, "nuScenes.names"))
 
     def extract_boxes(self, prediction) -> Dict[str, np.ndarray]:
-        names = [t.name for t in prediction.outputs]
-        out = {}
-        for i, n in enumerate(names):
-            out[n] = self.output_array(prediction, i)
+        names = self.output_names(prediction)
+        out = {n: self.output_array(prediction, i) for i, n in enumerate(names)}
         boxes = out.get("pred_boxes", self.output_array(prediction, 0))
         scores = out.get("pred_scores", self.output_array(prediction, 1))
         labels = out.get("pred_labels", self.output_array(prediction, 2))

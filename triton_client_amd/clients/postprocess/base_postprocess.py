@@ -29,8 +29,19 @@ class Postprocess(ABC):
             return [ln.rstrip() for ln in fp.read().splitlines() if ln.strip()]
 
     @staticmethod
-    def output_array(response, i: int) -> np.ndarray:
-        """Output i of a ModelInferResponse as a typed, shaped array (no copy)."""
+    def output_names(response) -> List[str]:
+        if hasattr(response, "order"):  # channel.wire.ParsedResponse
+            return list(response.order)
+        return [t.name for t in response.outputs]
+
+    @staticmethod
+    def output_array(response, i) -> np.ndarray:
+        """Output i (index or name) of a ModelInferResponse — or of the C++
+        codec's ParsedResponse — as a typed, shaped array (no copy)."""
+        if hasattr(response, "order"):
+            return response[i]
+        if isinstance(i, str):
+            i = [t.name for t in response.outputs].index(i)
         t = response.outputs[i]
         dt = _DT.get(t.datatype, np.float32)
         return np.frombuffer(response.raw_output_contents[i], dtype=dt).reshape(tuple(t.shape))

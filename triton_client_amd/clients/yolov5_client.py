@@ -48,7 +48,10 @@ class Yolov5postprocess(Postprocess):
         """ModelInferResponse (decoded [B, N, 5+nc] output 0) → list of [n, 6]
         arrays (x1, y1, x2, y2, conf, cls) in model-input pixels.  An empty
         list entry means no detections (the reference returned the exception)."""
-        pred = self.output_array(prediction, 0) if hasattr(prediction, "raw_output_contents") else prediction
+        if hasattr(prediction, "raw_output_contents") or hasattr(prediction, "order"):
+            pred = self.output_array(prediction, 0)
+        else:
+            pred = prediction
         pred = np.asarray(pred, np.float32)
         if pred.ndim == 2:
             pred = pred[None]

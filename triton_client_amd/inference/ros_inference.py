@@ -1,0 +1,98 @@
+"""Live 2D inference driver (reference ``communicator/ros_inference.py:25-175``).
+
+Subscribes to the camera topic (``CompressedImage`` JPEG or raw ``Image``,
+SURVEY Appendix A3), runs the engine (local MI355X pipeline or remote KServe
+server), draws the boxes and publishes an annotated ``Image`` (rgb8) carrying
+the *input* header (A4) — plus a ``vision_msgs/Detection2DArray`` on
+``<pub_topic>/detections`` (the intent of ``utils/pred2ros_msg.py:21-52``).
+An empty detection set still publishes the frame (fixes A5).
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ..ros import compat, msgs
+from ..utils.draw import draw_detections
+from .base_inference import BaseInference
+from .engines import Detector2D, RemoteDetector2D
+
+
+def decode_image_msg(msg) -> np.ndarray:
+    """CompressedImage (jpeg/png) or Image → HxWx3 uint8 RGB (reference :119-133)."""
+    if isinstance(msg, msgs.CompressedImage) or (hasattr(msg, "format") and not hasattr(msg, "encoding")):
+        if "compressed" in msg.format or msg.format.lower() in ("jpeg", "jpg", "png"):
+            return compat.jpeg_decode_rgb(msg.data)
+    return compat.imgmsg_to_numpy(msg, "rgb8")
+
+
+def detections_to_msg(dets: np.ndarray, header: msgs.Header, source: Optional[msgs.Image] = None) -> msgs.Detection2DArray:
+    out = msgs.Detection2DArray(header=header)
+    src = msgs.Image(header=header) if source is None else source
+    for d in np.asarray(dets).reshape(-1, 6):
+        x1, y1, x2, y2, conf, c = (float(v) for v in d)
+        out.detections.append(msgs.Detection2D(
+            header=header, results=[msgs.ObjectHypothesisWithPose(id=int(c), score=conf)],
+            bbox=msgs.BoundingBox2D(center=msgs.Pose2D((x1 + x2) / 2, (y1 + y2) / 2, 0.0), size_x=x2 - x1,
+                                    size_y=y2 - y1),
+            source_img=src))
+    return out
+
+
+class RosInference(BaseInference):
+    def __init__(self, channel=None, client=None, engine: Optional[Detector2D] = None, params: Optional[dict] = None,
+                 bus=None, letterbox: bool = False, conf_thres: float = 0.3, draw: bool = True,
+                 publish_detections: bool = True, queue_size: Optional[int] = 1, metrics=None, mode: str = "sync",
+                 wire: str = "raw"):
+        super().__init__(channel, client)
+        self._params = params or {}
+        self.engine = engine or RemoteDetector2D(channel, client, letterbox=letterbox, conf_thres=conf_thres,
+                                                 mode=mode, wire=wire)
+        self.class_names = list(getattr(self.engine, "names", []) or [])
+        self.bus, self.draw, self.publish_detections = bus, draw, publish_detections
+        self.queue_size, self.metrics = queue_size, metrics
+        self.frames = 0
+        self.sub = self.pub = self.det_pub = None
+
+    # ------------------------------------------------------------------ run
+    def start_inference(self, spin: bool = True, timeout: Optional[float] = None):
+        p = self.params
+        self.pub = compat.Publisher(p["pub_topic"], msgs.Image, queue_size=10, bus=self.bus)
+        if self.publish_detections:
+            self.det_pub = compat.Publisher(p["pub_topic"] + "/detections", msgs.Detection2DArray, queue_size=10,
+                                            bus=self.bus)
+        self.sub = compat.Subscriber(p["sub_topic"], msgs.CompressedImage, self._callback, queue_size=self.queue_size,
+                                     bus=self.bus)
+        if spin:
+            compat.spin(self.bus, timeout)
+
+    def stop(self):
+        if self.sub is not None:
+            self.sub.unregister()
+            self.sub = None
+
+    # ------------------------------------------------------------------ work
+    def process(self, images: Sequence) -> List[tuple]:
+        """Messages → [(annotated Image msg, Detection2DArray, dets [n,6])]."""
+        t0 = time.perf_counter()
+        rgb = [decode_image_msg(m) for m in images]
+        dets = self.engine.detect(rgb)
+        out = []
+        for m, img, d in zip(images, rgb, dets):
+            if self.draw:
+                img = draw_detections(img.copy(), d, self.class_names)
+            im = compat.numpy_to_imgmsg(img, "rgb8", header=m.header)
+            out.append((im, detections_to_msg(d, m.header), d))
+        self.frames += len(images)
+        if self.metrics is not None:
+            self.metrics.stage("frame", (time.perf_counter() - t0) / max(len(images), 1))
+            self.metrics.frame(len(images))
+        return out
+
+    def _callback(self, msg):
+        for im, det, _ in self.process([msg]):
+            self.pub.publish(im)
+            if self.det_pub is not None:
+                self.det_pub.publish(det)

@@ -1,0 +1,105 @@
+"""Live 3D inference driver (reference ``communicator/ros_inference3d.py:44-213``).
+
+PointCloud2 in → boxes out as a jsk ``BoundingBoxArray`` (default) or a
+``vision_msgs/Detection3DArray``, header stamp/frame_id copied from the
+cloud.  Reference behaviours kept as configurable defaults:
+z offset +1.5 before voxelising (removed from the output boxes), intensity
+normalised by its max, only label 2 (Pedestrian) with score > 0.5 published,
+jsk dimensions swapped (x = dy, y = dx).  Fixed: the Detection3DArray yaw is
+taken from the box's own dimension (index 6 for 7-d boxes, 8 for 9-d; A8).
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ..ros import compat, msgs
+from .base_inference import BaseInference
+from .engines import Detector3D, RemoteDetector3D
+
+
+def select_boxes(pred: dict, labels: Optional[Sequence[int]] = (2,), score_thresh: float = 0.5) -> np.ndarray:
+    """Indices kept for publishing (reference :156 keeps label==2 & score>0.5)."""
+    s, l_ = pred["pred_scores"], pred["pred_labels"]
+    keep = s > score_thresh
+    if labels is not None:
+        keep &= np.isin(l_, np.asarray(labels))
+    return np.nonzero(keep)[0]
+
+
+def boxes_to_jsk(pred: dict, idx, header: msgs.Header) -> msgs.BoundingBoxArray:
+    arr = msgs.BoundingBoxArray(header=header)
+    b = pred["pred_boxes"]
+    for i in idx:
+        x = b[i]
+        arr.boxes.append(msgs.BoundingBox(
+            header=header,
+            pose=msgs.Pose(msgs.Point(float(x[0]), float(x[1]), float(x[2])), compat.yaw2quaternion(float(x[6]))),
+            dimensions=msgs.Vector3(float(x[4]), float(x[3]), float(x[5])),
+            value=float(pred["pred_scores"][i]), label=int(pred["pred_labels"][i])))
+    return arr
+
+
+def boxes_to_detection3d(pred: dict, idx, header: msgs.Header) -> msgs.Detection3DArray:
+    arr = msgs.Detection3DArray(header=header)
+    b = pred["pred_boxes"]
+    yaw_i = 8 if b.shape[-1] >= 9 else 6
+    for i in idx:
+        x = b[i]
+        arr.detections.append(msgs.Detection3D(
+            header=header,
+            results=[msgs.ObjectHypothesisWithPose(id=int(pred["pred_labels"][i]), score=float(pred["pred_scores"][i]))],
+            bbox=msgs.BoundingBox3D(
+                center=msgs.Pose(msgs.Point(float(x[0]), float(x[1]), float(x[2])),
+                                 compat.yaw2quaternion(float(x[yaw_i]))),
+                size=msgs.Vector3(float(x[3]), float(x[4]), float(x[5])))))
+    return arr
+
+
+class RosInference3D(BaseInference):
+    def __init__(self, channel=None, client=None, engine: Optional[Detector3D] = None, params: Optional[dict] = None,
+                 bus=None, jsk: bool = True, labels: Optional[Sequence[int]] = (2,), score_thresh: float = 0.5,
+                 z_offset: float = 1.5, queue_size: Optional[int] = 50, metrics=None, mode: str = "sync",
+                 wire: str = "raw"):
+        super().__init__(channel, client)
+        self._params = params or {}
+        self.engine = engine or RemoteDetector3D(channel, client, z_offset=z_offset, mode=mode, wire=wire)
+        self.bus, self.jsk, self.labels, self.score_thresh = bus, jsk, labels, score_thresh
+        self.queue_size, self.metrics = queue_size, metrics
+        self.frames = 0
+        self.sub = self.pub = None
+
+    def start_inference(self, spin: bool = True, timeout: Optional[float] = None):
+        p = self.params
+        t = msgs.BoundingBoxArray if self.jsk else msgs.Detection3DArray
+        self.pub = compat.Publisher(p["pub_topic"], t, queue_size=1, bus=self.bus)
+        self.sub = compat.Subscriber(p["sub_topic"], msgs.PointCloud2, self._pc_callback,
+                                     queue_size=self.queue_size, bus=self.bus)
+        if spin:
+            compat.spin(self.bus, timeout)
+
+    def stop(self):
+        if self.sub is not None:
+            self.sub.unregister()
+            self.sub = None
+
+    def to_msg(self, pred: dict, header: msgs.Header):
+        idx = select_boxes(pred, self.labels, self.score_thresh)
+        hdr = msgs.Header(seq=header.seq, stamp=header.stamp, frame_id=header.frame_id)
+        return boxes_to_jsk(pred, idx, hdr) if self.jsk else boxes_to_detection3d(pred, idx, hdr)
+
+    def process(self, clouds: Sequence[msgs.PointCloud2]) -> List[tuple]:
+        t0 = time.perf_counter()
+        preds = self.engine.detect(clouds)
+        out = [(self.to_msg(p, c.header), p) for c, p in zip(clouds, preds)]
+        self.frames += len(clouds)
+        if self.metrics is not None:
+            self.metrics.stage("frame3d", (time.perf_counter() - t0) / max(len(clouds), 1))
+            self.metrics.frame(len(clouds))
+        return out
+
+    def _pc_callback(self, msg):
+        for m, _ in self.process([msg]):
+            self.pub.publish(m)

@@ -82,12 +82,12 @@ class YoloV5Model(ServedModel):
     def execute(self, inputs, requested):
         x = inputs["images"].reshape(1, 3, self.img, self.img)
         if self.device.type == "cuda":
-            self.x.copy_(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(self.device, non_blocking=True))
+            self.x.copy_(torch.from_numpy(np.require(x, np.float32, ['C', 'W'])).to(self.device, non_blocking=True))
             heads = self.model(self.x)
             dec = self.pipe.post.decode(heads)
             out = dec.cpu().numpy()
         else:
-            heads = self.model(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)))
+            heads = self.model(torch.from_numpy(np.require(x, np.float32, ['C', 'W'])))
             from ..models.yolov5 import yolo_decode_reference
             out = yolo_decode_reference(heads, self.model.anchors).numpy()
         return {"output": out.astype(np.float32, copy=False)}
@@ -168,10 +168,10 @@ class PointPillarsModel(ServedModel):
             raise InferError(f"{V} voxels > max_voxels {self.cfg.voxel.max_voxels}")
         if self.device.type == "cuda":
             self.enc.clear_coords(self.coords, self.vcount)
-            self.voxels[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(vox[..., :4], np.float32)))
-            self.coords[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(co, np.int32)))
+            self.voxels[0, :V].copy_(torch.from_numpy(np.require(vox[..., :4], np.float32, ['C', 'W'])))
+            self.coords[0, :V].copy_(torch.from_numpy(np.require(co, np.int32, ['C', 'W'])))
             self.coords[0, :V, 0] = 0
-            self.nump[0, :V].copy_(torch.from_numpy(np.ascontiguousarray(n, np.int32)))
+            self.nump[0, :V].copy_(torch.from_numpy(np.require(n, np.int32, ['C', 'W'])))
             self.vcount.fill_(V)
             canvas = self.enc.encode_from_voxels(self.voxels, self.nump, self.coords, self.vcount)
             cls, box, dr = self.model.bev_forward(canvas)
@@ -179,8 +179,8 @@ class PointPillarsModel(ServedModel):
         else:
             from ..models.pointpillars import pillar_point_features, scatter_to_bev
             from ..ops.lidar import AnchorPostprocess
-            v = torch.from_numpy(np.ascontiguousarray(vox[..., :4], np.float32))
-            c = torch.from_numpy(np.ascontiguousarray(co, np.int32)).clone()
+            v = torch.from_numpy(np.require(vox[..., :4], np.float32, ['C', 'W']))
+            c = torch.from_numpy(np.require(co, np.int32, ['C', 'W'])).clone()
             c[:, 0] = 0
             f = pillar_point_features(v, torch.from_numpy(n.astype(np.int64)), c, self.cfg.voxel)
             pf = self.model.vfe(f)
