@@ -81,3 +81,28 @@ def test_main_plays_bag_through_topic_bus(bags, server, tmp_path):
                                       "pub_topic": "/det", "gt_topic": "/gt"}))
     assert main2d.main(["--params", str(params), "--play", cam, "--spin-timeout", "60"]) == 0
     reset_default_bus()
+
+
+def test_bag2d_data_parallel_torchrun(bags, tmp_path):
+    """torchrun --nproc-per-node 2 bag2d --engine local: frames sharded over 2 gloo ranks."""
+    import socket
+    import subprocess
+    import sys
+
+    _, cam, _ = bags
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ob = str(tmp_path / "dp.bag")
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "triton_client_amd.cli.bag2d",
+                        "--bag", cam, "--engine", "local", "--device", "cpu", "--out", "", "--out-bag", ob,
+                        "--frames-per-step", "4", "-m", "YOLOv5nCROP"],
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    with Bag(ob) as b:
+        dets = [m for t, m, _ in b.read_messages(topics=["/aver_01/camera_color/detection/detections"])]
+    assert len(dets) == 4 and [d.header.seq for d in dets] == [0, 1, 2, 3]

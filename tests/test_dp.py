@@ -1,0 +1,124 @@
+"""Data parallelism on the CPU: gloo, world_size 2 and 3, 127.0.0.1 rendezvous.
+
+The same code paths run over RCCL on GPUs (FrameExchange's grouped p2p,
+parameter broadcast, the DP detectors used by the bag drivers)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class FakeDetector:
+    """Deterministic, rank-independent: one box per frame from its pixel stats."""
+    names = ["x"]
+
+    def detect(self, frames):
+        out = []
+        for f in frames:
+            m = float(f.mean())
+            k = int(f[0, 0, 0]) % 4
+            out.append(np.array([[m, m, m + 10, m + 10, 0.5, j] for j in range(k)], np.float32).reshape(-1, 6))
+        return out
+
+
+class FakeDetector3D:
+    names = ["a"]
+
+    def detect(self, clouds):
+        from triton_client_amd.ros.compat import cloud_to_numpy
+        out = []
+        for c in clouds:
+            p = cloud_to_numpy(c)
+            k = len(p) % 5
+            out.append({"pred_boxes": np.tile(p[:1, [0, 1, 2, 3, 0, 1, 2]], (k, 1)).astype(np.float32),
+                        "pred_scores": np.full(k, p[:, 3].mean(), np.float32),
+                        "pred_labels": np.arange(k, dtype=np.int64)})
+        return out
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import faulthandler
+    faulthandler.dump_traceback_later(int(os.environ.get("TCA_DP_TEST_DUMP", "150")), exit=True)
+    try:
+        from triton_client_amd.models.common import broadcast_parameters
+        from triton_client_amd.parallel.dp import (DataParallelDetector2D, DataParallelDetector3D, FrameExchange,
+                                                   allreduce_max, barrier, init_distributed, shutdown)
+        from triton_client_amd.ros import compat, msgs
+
+        info = init_distributed("gloo")
+        assert dist.get_backend() == "gloo"
+        # scatter / gather of tensor sets
+        ex = FrameExchange(info)
+        src = [[torch.full((3, 4), float(r)), torch.arange(5) + r] for r in range(world)] if info.is_main else None
+        dst = [torch.empty(3, 4), torch.empty(5, dtype=torch.int64)]
+        ex.scatter(src, dst)
+        assert torch.equal(dst[0], torch.full((3, 4), float(rank))) and torch.equal(dst[1], torch.arange(5) + rank)
+        g = [[torch.empty(2), torch.empty(1, dtype=torch.int32)] for _ in range(world)] if info.is_main else None
+        ex.gather([torch.full((2,), 10.0 * rank), torch.tensor([rank], dtype=torch.int32)], g)
+        if info.is_main:
+            for r in range(world):
+                assert torch.equal(g[r][0], torch.full((2,), 10.0 * r)) and int(g[r][1]) == r
+        # parameter broadcast
+        lin = torch.nn.Linear(4, 3)
+        torch.nn.init.constant_(lin.weight, float(rank))
+        broadcast_parameters(lin)
+        assert float(lin.weight.detach().abs().sum()) == 0.0
+        assert allreduce_max(info, float(rank)) == world - 1
+        # DP 2D detector: rank 0 drives, others serve
+        frames = [np.full((8, 12, 3), 7 * i, np.uint8) for i in range(7)]
+        dp = DataParallelDetector2D(FakeDetector(), info, max_det=8)
+        clouds = [compat.create_cloud_xyzi(np.random.default_rng(i).random((20 + 3 * i, 4)).astype(np.float32),
+                                           msgs.Header(seq=i)) for i in range(5)]
+        dp3 = DataParallelDetector3D(FakeDetector3D(), info, max_out=8)
+        if info.is_main:
+            got = dp.detect(frames)
+            want = FakeDetector().detect(frames)
+            assert len(got) == len(want)
+            for a, b in zip(got, want):
+                np.testing.assert_array_equal(a, b)
+            mixed = dp.detect([frames[1], np.full((4, 4, 3), 9, np.uint8)])
+            np.testing.assert_array_equal(mixed[1], FakeDetector().detect([np.full((4, 4, 3), 9, np.uint8)])[0])
+            dp.close()
+            got3 = dp3.detect(clouds)
+            want3 = FakeDetector3D().detect(clouds)
+            for a, b in zip(got3, want3):
+                for k in a:
+                    np.testing.assert_allclose(a[k], b[k], rtol=1e-6)
+            dp3.close()
+        else:
+            assert dp.serve() == 3  # one 7-frame batch + the 2 single-frame calls of the mixed batch
+            assert dp3.serve() == 1
+        barrier(info)
+        shutdown(info)
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res

@@ -6,7 +6,7 @@ import os
 import sys
 
 from .common import DATA, add_framework_flags, add_reference_flags, load_params, setup_logging
-from .engines import engine_2d
+from .engines import engine_2d, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -28,10 +28,22 @@ def main(argv=None) -> int:
 
     params = load_params(flags.params, flags.server)
     engine, channel, client = engine_2d(flags, params)
+    info = None
+    if flags.engine == "local":
+        engine, info = maybe_data_parallel(engine)
+        if info is not None and not info.is_main:  # worker rank: serve shards until rank 0 is done
+            engine.serve()
+            from ..parallel.dp import shutdown
+            shutdown(info)
+            return 0
     drv = BagInference2D(channel, client, engine=engine, params=params, bagfile=flags.bag, out_dir=flags.out or None,
                          out_bag=flags.out_bag, batch=max(1, flags.frames_per_step), save_png=bool(flags.out),
                          start_seq=flags.start_seq, max_frames=flags.max_frames)
     n = drv.start_inference()
+    if info is not None:
+        engine.close()
+        from ..parallel.dp import shutdown
+        shutdown(info)
     fps = n / drv.elapsed if drv.elapsed > 0 else 0.0
     print(f"processed {n} frames in {drv.elapsed:.2f}s ({fps:.1f} FPS)", file=sys.stderr)
     return 0

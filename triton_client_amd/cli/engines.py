@@ -54,3 +54,24 @@ def engine_3d(flags, params):
     client = make_client(flags, ch)
     eng = RemoteDetector3D(ch, client, z_offset=flags.z_offset, mode=rpc_mode(flags), wire=flags.wire)
     return eng, ch, client
+
+
+def maybe_data_parallel(engine, three_d: bool = False):
+    """Under torchrun (WORLD_SIZE > 1) wrap a *local* engine so rank 0's frames
+    are sharded over every GPU (RCCL scatter/gather).  Returns (engine, info);
+    non-main ranks must call ``engine.serve()`` instead of running a driver."""
+    import os
+
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return engine, None
+    from ..parallel.dp import DataParallelDetector2D, DataParallelDetector3D, init_distributed
+
+    info = init_distributed()
+    if hasattr(engine, "calibrate_synthetic"):
+        engine.calibrate_synthetic()
+    if hasattr(engine, "model"):
+        from ..models.common import broadcast_parameters
+
+        broadcast_parameters(engine.model)  # every replica runs rank 0's weights
+    wrap = DataParallelDetector3D(engine, info) if three_d else DataParallelDetector2D(engine, info)
+    return wrap, info

@@ -114,6 +114,14 @@ class LocalDetector2D(Detector2D):
         self._pipes[hw] = entry
         return entry
 
+    def calibrate_synthetic(self, seed: int = 0) -> None:
+        """Set the random-init head prior from a synthetic frame (same on every
+        rank, so data-parallel replicas agree before the parameter broadcast)."""
+        if self.calibrate_target is not None:
+            from ..utils.synthetic import camera_frame
+
+            self._pipe(self.img, camera_frame(self.img[0], self.img[1], seed))
+
     @torch.no_grad()
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
         out: List[Optional[np.ndarray]] = [None] * len(frames)
@@ -188,6 +196,20 @@ class LocalDetector3D(Detector3D):
         ent = (p, GraphRunner(p.step, enabled=self.graph), pinned, torch.zeros(self.B, dtype=torch.int32))
         self._pipes[key] = ent
         return ent
+
+    def calibrate_synthetic(self, seed: int = 0) -> None:
+        """Set the random-init head prior from a synthetic sweep (rank-independent)."""
+        if self.calibrate_target is None:
+            return
+        from ..ros.compat import cloud_layout, create_cloud_xyzi
+        from ..utils.synthetic import LidarSpec, lidar_sweep
+
+        pts = lidar_sweep(LidarSpec(sensor_height=3.23), seed)
+        cloud = create_cloud_xyzi(np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4))
+        if self.device.type == "cuda":
+            self._pipe(cloud_layout(cloud), cloud.width, cloud)
+        else:
+            self._detect_cpu(cloud)
 
     @torch.no_grad()
     def detect(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
