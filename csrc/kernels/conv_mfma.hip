@@ -62,6 +62,66 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 // byte offset of 16-B chunk c (0..3) of row r in a [rows][64 B] swizzled tile
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); }
 
+// ---- shared epilogue: acc[i][j] holds D = B^T-tile x A^T-tile: col (lane&15) -> m,
+// rows (lane>>4)*4 + r -> n.  Bias/act, bf16 tile staged in LDS, 16-B coalesced
+// stores (+ residual, + pixel-shuffle addressing).
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                         unsigned char* smem, int m0, int n0) {
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  constexpr int LD = BN + 8;  // +16 B per row: the 16 rows a lane group writes hit distinct banks
+  __hip_bfloat16* st = reinterpret_cast<__hip_bfloat16*>(smem);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = wm * TM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int nl = wn * TN + j * 16 + fq * 4;
+      __hip_bfloat16 q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + nl + r;
+        float v = acc[i][j][r];
+        if (a.bias && n < a.N) v += a.bias[n];
+        q[r] = __float2bfloat16(act_fn(v, a.act));
+      }
+      *reinterpret_cast<uint2*>(st + ml * LD + nl) = *reinterpret_cast<uint2*>(q);
+    }
+  }
+  __syncthreads();
+  // coalesced 16-B stores: each thread writes 8 consecutive channels of a pixel
+  constexpr int VEC_PER_ROW = BN / 8;
+  for (int id = tid; id < BM * VEC_PER_ROW; id += WM * WN * 64) {
+    const int ml = id / VEC_PER_ROW, c8 = (id % VEC_PER_ROW) * 8;
+    const int m = m0 + ml, n = n0 + c8;
+    if (m >= a.M || n >= a.N) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(st + ml * LD + c8);
+    const int ox = m % a.Wo, oy = (m / a.Wo) % a.Ho, b = m / (a.Wo * a.Ho);
+    long o;
+    if (a.shuffle > 0) {  // n = (sy, sx, co) -> out[b, oy*s+sy, ox*s+sx, co]
+      const int s = a.shuffle, coutr = a.N / (s * s);
+      const int sy = n / (s * coutr), sx = (n / coutr) % s, co = n % coutr;
+      o = (((long)b * a.Ho * s + oy * s + sy) * (a.Wo * s) + ox * s + sx) * a.ldo + a.co_off + co;
+    } else {
+      o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n;
+    }
+    if (a.res) {
+      const __hip_bfloat16* rp = a.res + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldr + a.r_off + n;
+      uint4 r = *reinterpret_cast<const uint4*>(rp);
+      const __hip_bfloat16* x = reinterpret_cast<const __hip_bfloat16*>(&v);
+      const __hip_bfloat16* y = reinterpret_cast<const __hip_bfloat16*>(&r);
+      __hip_bfloat16 z[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = __float2bfloat16(__bfloat162float(x[e]) + __bfloat162float(y[e]));
+      v = *reinterpret_cast<uint4*>(z);
+    }
+    *reinterpret_cast<uint4*>(a.out + o) = v;
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
   static_assert(WM * WN == 4, "4 waves");
@@ -72,7 +132,7 @@ __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
   constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int EPI = BM * BN * 2;
+  constexpr int EPI = BM * (BN + 8) * 2;
   constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
@@ -174,54 +234,185 @@ __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: acc[i][j] holds D = B^T-tile x A^T-tile: col (lane&15) -> m,
-  // rows (lane>>4)*4 + r -> n.  Apply bias/act, stage bf16 tile [BM][BN] in LDS.
-  __hip_bfloat16* st = reinterpret_cast<__hip_bfloat16*>(smem);
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ml = wm * TM + i * 16 + fr;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int nl = wn * TN + j * 16 + fq * 4 + r;
-        const int n = n0 + nl;
-        float v = acc[i][j][r];
-        if (a.bias && n < a.N) v += a.bias[n];
-        v = act_fn(v, a.act);
-        st[ml * BN + nl] = __float2bfloat16(v);
-      }
-    }
+  epilogue<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+}
+
+
+// ============================================================================
+// v2: BK = 64, both operands staged global -> LDS by global_load_lds_dwordx4
+// (no VGPR round trip, no per-chunk branches).  Contract: Cin % 64 == 0, so a
+// 64-deep K step never straddles a filter tap and the tap (ky, kx, ci0) is
+// wave-uniform and advanced incrementally (no divisions in the loop).
+// Out-of-image taps and M / N tails load from a zeroed device page.  LDS rows
+// are 128 B; glds writes them lane-linearly, so the bank swizzle (16-B slot
+// ^= (row >> 1) & 7: the 16 rows of a ds_read_b128 lane group land on 16
+// distinct (bank-row half, slot) pairs) is applied to the per-lane SOURCE
+// chunk and to the fragment read (cdna_hip_programming.md rule 21).  Two LDS
+// stages; the next stage's loads stay in flight across the barrier (counted
+// vmcnt + raw s_barrier, never vmcnt(0) in the loop).  Tiles are walked
+// XCD-major so the N-tiles of one pixel panel share an L2.
+// ============================================================================
+__device__ uint4 g_conv_zero_page[64];  // 1 KiB of zeros (static device memory is zero-initialised)
+
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* gbl_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t)g, (lds_void_t)l, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+
+__device__ __forceinline__ int swz2(int row) { return (row >> 1) & 7; }
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+__global__ void __launch_bounds__(WM * WN * 64) conv_glds_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int BK = 64, ROWB = 128;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split over the waves' 8-row DMAs");
+  constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);  // glds per wave per K step
+  constexpr int NL = A_INS + B_INS;
+  constexpr int EPI = BM * (BN + 8) * 2;
+  constexpr int LDS = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  // XCD-aware bijective remap: consecutive logical tiles (the N-tiles of one
+  // M panel, then neighbouring panels) run on the same XCD / L2.
+  const int nmt = (a.M + BM - 1) / BM, nnt = (a.N + BN - 1) / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  __syncthreads();
-  // coalesced 16-B stores: each thread writes 8 consecutive channels of a pixel
-  constexpr int VEC_PER_ROW = BN / 8;
-  for (int id = tid; id < BM * VEC_PER_ROW; id += 256) {
-    const int ml = id / VEC_PER_ROW, c8 = (id % VEC_PER_ROW) * 8;
-    const int m = m0 + ml, n = n0 + c8;
-    if (m >= a.M || n >= a.N) continue;
-    uint4 v = *reinterpret_cast<const uint4*>(st + ml * BN + c8);
-    const int ox = m % a.Wo, oy = (m / a.Wo) % a.Ho, b = m / (a.Wo * a.Ho);
-    long o;
-    if (a.shuffle > 0) {  // n = (sy, sx, co) -> out[b, oy*s+sy, ox*s+sx, co]
-      const int s = a.shuffle, coutr = a.N / (s * s);
-      const int sy = n / (s * coutr), sx = (n / coutr) % s, co = n % coutr;
-      o = (((long)b * a.Ho * s + oy * s + sy) * (a.Wo * s) + ox * s + sx) * a.ldo + a.co_off + co;
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  // ---- per-lane load descriptors: row within the tile, logical chunk
+  const int lrow = lane >> 3, lslot = lane & 7;
+  long a_base[A_INS];
+  int a_iy0[A_INS], a_ix0[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wid * A_INS + j) * 8 + lrow;
+    const int m = m0 + row;
+    const int c = lslot ^ swz2(row);
+    if (m < a.M) {
+      const int ox = m % a.Wo, t = m / a.Wo, oy = t % a.Ho, b = t / a.Ho;
+      a_iy0[j] = oy * a.S - a.P;
+      a_ix0[j] = ox * a.S - a.P;
+      a_base[j] = (((long)b * a.H + a_iy0[j]) * a.W + a_ix0[j]) * a.ldi + a.ci_off + c * 8;
     } else {
-      o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n;
+      a_iy0[j] = -(1 << 28);  // never in bounds
+      a_ix0[j] = 0;
+      a_base[j] = 0;
     }
-    if (a.res) {
-      const __hip_bfloat16* rp = a.res + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldr + a.r_off + n;
-      uint4 r = *reinterpret_cast<const uint4*>(rp);
-      const __hip_bfloat16* x = reinterpret_cast<const __hip_bfloat16*>(&v);
-      const __hip_bfloat16* y = reinterpret_cast<const __hip_bfloat16*>(&r);
-      __hip_bfloat16 z[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = __float2bfloat16(__bfloat162float(x[e]) + __bfloat162float(y[e]));
-      v = *reinterpret_cast<uint4*>(z);
-    }
-    *reinterpret_cast<uint4*>(a.out + o) = v;
   }
+  const __hip_bfloat16* b_ptr[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wid * B_INS + j) * 8 + lrow;
+    const int n = n0 + row;
+    b_ptr[j] = n < a.N ? a.w + (long)n * a.Kp + (lslot ^ swz2(row)) * 8 : nullptr;
+  }
+  const long tap_stride_x = a.ldi, tap_stride_y = (long)a.W * a.ldi;
+
+  auto issue = [&](int kt, int buf, int ky, int kx, int ci0) {
+    unsigned char* sa = smem + buf * STAGE;
+    unsigned char* sb = sa + A_BYTES;
+    const long toff = ky * tap_stride_y + kx * tap_stride_x + ci0;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const void* g = ok ? (const void*)(a.in + a_base[j] + toff) : (const void*)g_conv_zero_page;
+      glds16(g, sa + (wid * A_INS + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const void* g = b_ptr[j] ? (const void*)(b_ptr[j] + kt * BK) : (const void*)g_conv_zero_page;
+      glds16(g, sb + (wid * B_INS + j) * 1024);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kp / BK;
+  int ky = 0, kx = 0, ci0 = 0;  // tap of the next stage to issue (wave-uniform)
+  auto advance = [&]() {
+    ci0 += BK;
+    if (ci0 == a.Cin) {
+      ci0 = 0;
+      if (++kx == a.KW) { kx = 0; ++ky; }
+    }
+  };
+  // prologue: STAGES-1 stages in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) {
+      issue(s, s, ky, kx, ci0);
+      advance();
+    }
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % STAGES;
+    const int nx = kt + STAGES - 1;
+    if (nx < nk) {
+      issue(nx, nx % STAGES, ky, kx, ci0);
+      advance();
+    }
+    // retire stage kt: the stages issued after it may stay in flight
+    const int after = (nk - 1 - kt) < (STAGES - 1) ? (nk - 1 - kt) : (STAGES - 1);
+    if (STAGES >= 3 && after >= 2) wait_vmcnt<2 * NL>();
+    else if (after >= 1) wait_vmcnt<NL>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const unsigned char* sa = smem + cur * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], bfg[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * TN + j * 16 + fr;
+        bfg[j] = *reinterpret_cast<const bf16x8*>(sb + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is restaged
+    asm volatile("" ::: "memory");
+  }
+  epilogue<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES = 2>
+int launch_glds(const ConvArgs& a, hipStream_t stream) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  conv_glds_kernel<BM, BN, WM, WN, STAGES><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -252,8 +443,30 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   if (a.K > Kp) return (int)hipErrorInvalidValue;
   // tile: 0 = auto
   // measured on MI355X (tools/bench_conv.py): 128x32 for N<=32, 128x64 for N<=64, 64x128 above
-  if (tile == 0) tile = N <= 32 ? 1 : (N <= 64 ? 2 : 5);
+  const bool v2ok = (Cin % 64) == 0 && (Kp % 64) == 0 && Kp == a.K;
+  // auto tile (measured on MI355X, tools/bench_conv.py -> profiles/conv_tiles_r1.md):
+  // v2 (glds, 8 waves): 128x64 for N <= 64; 128x128 (4x2 waves) for wide-M layers,
+  // 64x128 (2x4 waves) when M is small; v1 (register staging) when Cin % 64 != 0
+  if (tile == 0) tile = v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 32 ? 1 : (N <= 64 ? 2 : 5));
+  if (tile >= 10 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
+    case 11: return launch_glds<128, 64, 4, 1>(a, stream);
+    case 12: return launch_glds<128, 128, 2, 2>(a, stream);
+    case 13: return launch_glds<256, 64, 4, 1>(a, stream);
+    case 14: return launch_glds<128, 256, 2, 2>(a, stream);
+    case 15: return launch_glds<64, 128, 1, 4>(a, stream);
+    case 16: return launch_glds<128, 64, 4, 1, 3>(a, stream);
+    case 17: return launch_glds<128, 128, 2, 2, 3>(a, stream);
+    case 18: return launch_glds<64, 128, 1, 4, 3>(a, stream);
+    case 19: return launch_glds<256, 128, 4, 2>(a, stream);      // 8 waves
+    case 20: return launch_glds<128, 128, 4, 2>(a, stream);      // 8 waves
+    case 21: return launch_glds<256, 64, 8, 1>(a, stream);       // 8 waves
+    case 22: return launch_glds<128, 64, 4, 2>(a, stream);       // 8 waves, 32x32 per wave
+    case 23: return launch_glds<128, 64, 8, 1>(a, stream);       // 8 waves, 16x64 per wave
+    case 24: return launch_glds<64, 128, 2, 4>(a, stream);       // 8 waves, 32x32 per wave
+    case 25: return launch_glds<128, 128, 2, 4>(a, stream);      // 8 waves, 64x32 per wave
+    case 26: return launch_glds<256, 64, 4, 2>(a, stream);       // 8 waves, 64x32 per wave
+    case 27: return launch_glds<128, 256, 2, 4>(a, stream);      // 8 waves, 64x64 per wave
     case 1: return launch<128, 32, 4, 1>(a, stream);
     case 2: return launch<128, 64, 4, 1>(a, stream);
     case 3: return launch<128, 128, 2, 2>(a, stream);

@@ -270,3 +270,37 @@ def test_fused_conv_slices_residual_and_transpose(cuda):
         ref = torch.relu(ct(x.to(torch.bfloat16).float().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
         assert y.shape == (B, 9 * s_, 7 * s_, 32)
         assert (y.tensor().float().cpu() - ref).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("tile", [11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27])
+def test_fused_conv_glds_tiles(cuda, tile):
+    """v2 (global_load_lds, BK=64) tiles: Cin % 64 == 0 shapes with stride, channel
+    slices, residual, M/N tails and a pixel-shuffle transpose conv, vs fp32."""
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(tile)
+    B, H, W = 2, 23, 31  # M tail: 2*23*31 = 1426 (not a multiple of any BM)
+    for cin, cout, k, s, act in ((64, 64, 3, 1, 1), (128, 72, 3, 2, 2), (192, 256, 1, 1, 0)):
+        conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=True)
+        fc = FusedConv(conv, act=act, device=cuda)
+        buf = torch.randn(B, H, W, cin + 64).to(cuda, torch.bfloat16)
+        xin = NHWC(buf, 64, cin)  # channels [64, 64+cin)
+        Ho, Wo = (H + 2 * (k // 2) - k) // s + 1, (W + 2 * (k // 2) - k) // s + 1
+        res = torch.randn(B, Ho, Wo, fc.N + 16).to(cuda, torch.bfloat16)
+        out = torch.zeros(B, Ho, Wo, fc.N + 8, dtype=torch.bfloat16, device=cuda)
+        fc(xin, out=NHWC(out, 8, fc.N), res=NHWC(res, 16, fc.N), tile=tile)
+        torch.cuda.synchronize()
+        x32 = buf[..., 64:64 + cin].float().permute(0, 3, 1, 2).cpu()
+        acts = {0: lambda t: t, 1: torch.relu, 2: torch.nn.functional.silu}
+        ref = acts[act](conv(x32)) + res[..., 16:16 + cout].float().permute(0, 3, 1, 2).cpu()
+        got = out[..., 8:8 + cout].float().permute(0, 3, 1, 2).cpu()
+        err = (got - ref).abs().max().item()
+        assert err < 0.03 * max(1.0, ref.abs().max().item()), (cin, cout, k, s, err)
+        assert out[..., :8].abs().sum().item() == 0
+    ct = nn.ConvTranspose2d(128, 64, 2, stride=2, bias=True)
+    fct = FusedConv(ct, act=1, device=cuda)
+    x = torch.randn(B, 9, 7, 128)
+    y = fct(NHWC(x.to(cuda, torch.bfloat16)), tile=tile)
+    torch.cuda.synchronize()
+    ref = torch.relu(ct(x.to(torch.bfloat16).float().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
+    assert (y.tensor().float().cpu() - ref).abs().max().item() < 0.05
