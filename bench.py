@@ -36,9 +36,11 @@ from triton_client_amd.parallel.dp import (FrameExchange, allreduce_max, barrier
                                            shutdown)
 
 METRIC = "end-to-end FPS (sensor->detection) YOLOv5n-640 + PointPillars at 1/2/4/8 GPU"
-# Reference-equivalent FPS measured on the dev host with tools/reference_equivalent.py
-# (the reference's per-frame CPU logic for the same frame pair).
-REFERENCE_EQUIVALENT_FPS = None
+# Reference-equivalent FPS: tools/reference_equivalent.py on an MI355X box (the
+# reference client's per-frame logic — batch 1, sync KServe RPC, struct-loop
+# response decode, Python read_points — for the same camera + LiDAR frame pair,
+# models served on the same GPU).  profiles/reference_equivalent_r1.json, BASELINE.md.
+REFERENCE_EQUIVALENT_FPS = 3.2319
 
 
 def parse():

@@ -447,7 +447,7 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   // auto tile (measured on MI355X, tools/bench_conv.py -> profiles/conv_tiles_r1.md):
   // v2 (glds, 8 waves): 128x64 for N <= 64; 128x128 (4x2 waves) for wide-M layers,
   // 64x128 (2x4 waves) when M is small; v1 (register staging) when Cin % 64 != 0
-  if (tile == 0) tile = v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 32 ? 1 : (N <= 64 ? 2 : 5));
+  if (tile == 0) tile = N <= 32 ? 1 : v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 64 ? 2 : 5);
   if (tile >= 10 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 11: return launch_glds<128, 64, 4, 1>(a, stream);
