@@ -1,0 +1,172 @@
+"""CenterPoint-PP (det3d, nuScenes): model, fast plan, decode/NMS, kernels."""
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+
+from triton_client_amd.config.lidar import NUSC_PILLARS, CenterPointConfig
+from triton_client_amd.models.centerpoint import (build_centerpoint, decode_reference, merged_task_outputs,
+                                                  pfn_point_features)
+from triton_client_amd.models.common import fuse_model, randomize_bn
+from triton_client_amd.ops.conv import NHWC
+from triton_client_amd.ops.lidar import voxelize_np
+from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+
+def _small_cfg(**kw):
+    v = dataclasses.replace(NUSC_PILLARS, point_cloud_range=(-12.8, -12.8, -5.0, 12.8, 12.8, 3.0), max_voxels=4000)
+    return CenterPointConfig(voxel=v, **kw)
+
+
+def _model(cfg, seed=0):
+    m = build_centerpoint(cfg, seed)
+    randomize_bn(m, 3)
+    m = fuse_model(m.eval())
+    with torch.no_grad():  # tame the random regression heads (exp(dim)) like the pipeline calibration
+        for t in m.head.tasks:
+            for n, c in t.out.items():
+                s = 0.05 if n != "hm" else 0.3
+                c.weight.mul_(s)
+                c.bias.mul_(s)
+    return m
+
+
+def _cloud(cfg, seed=0):
+    pts = lidar_sweep(LidarSpec(rings=16, azimuth_steps=512, sensor_height=1.8), seed)
+    p = np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4)
+    p = p[~np.isnan(p).any(1)]
+    return np.concatenate([p, np.zeros((len(p), 1), np.float32)], 1)
+
+
+def test_fast_centerpoint_cpu_matches_module():
+    from triton_client_amd.models.fast import FastCenterPoint
+    cfg = _small_cfg()
+    m = _model(cfg)
+    nx, ny, _ = cfg.voxel.grid_size
+    canvas = torch.zeros(2, ny, nx, 64)
+    canvas[:, ::3, ::2] = torch.rand(2, (ny + 2) // 3, (nx + 1) // 2, 64)
+    with torch.no_grad():
+        ref = merged_task_outputs(m.bev_forward(canvas.permute(0, 3, 1, 2)))
+        f = FastCenterPoint(m, 2, device="cpu")
+        out = f.forward(NHWC(canvas)).t
+    for t, r in enumerate(ref):
+        o = out[..., f.task_offsets[t]:f.task_offsets[t] + r.shape[1]].permute(0, 3, 1, 2)
+        torch.testing.assert_close(o, r, rtol=1e-4, atol=1e-4)
+
+
+def test_pfn_features_and_model_forward_shapes():
+    cfg = _small_cfg()
+    m = _model(cfg)
+    p5 = _cloud(cfg)
+    v, zyx, num, _ = voxelize_np(p5, cfg.voxel, 5)
+    coords = torch.from_numpy(np.pad(zyx, ((0, 0), (1, 0))).astype(np.int32))
+    f = pfn_point_features(torch.from_numpy(v), torch.from_numpy(num.astype(np.int64)), coords, cfg.voxel)
+    assert f.shape == (len(v), cfg.voxel.max_points_per_voxel, 10)
+    assert (f[torch.arange(20).view(1, -1).expand(len(v), -1) >= torch.from_numpy(num).view(-1, 1)] == 0).all()
+    with torch.no_grad():
+        out = m(torch.from_numpy(v), torch.from_numpy(num.astype(np.int64)), coords, 1)
+    H, W = cfg.feature_map_size
+    assert len(out) == 6 and out[0]["hm"].shape == (1, 1, H, W) and out[1]["hm"].shape == (1, 2, H, W)
+
+
+def test_postprocess_cpu_and_class_thresholds():
+    from triton_client_amd.ops.centerpoint import NUSC_CLASS_THRESH, CenterPointPostprocess
+    cfg = _small_cfg()
+    m = _model(cfg)
+    H, W = cfg.feature_map_size
+    with torch.no_grad():
+        canvas = torch.rand(1, 64, *[s * cfg.out_size_factor for s in (H, W)])
+        mo = merged_task_outputs(m.bev_forward(canvas))
+    head = torch.zeros(1, H, W, 96)
+    for t, o in enumerate(mo):
+        head[..., 16 * t:16 * t + o.shape[1]] = o.permute(0, 2, 3, 1)
+    pp = CenterPointPostprocess(cfg, 1, [16 * t for t in range(6)], device="cpu")
+    res = pp(head).per_image()[0]
+    offs = [0, 1, 3, 5, 6, 8]
+    ref = decode_reference(mo, cfg, offs)[0]
+    np.testing.assert_allclose(np.sort(res["pred_scores"]), np.sort(ref[1]), rtol=1e-6)
+    assert res["pred_boxes"].shape[1] == 9
+    assert len(res["pred_scores"]) > 0
+    pp2 = CenterPointPostprocess(cfg, 1, [16 * t for t in range(6)], device="cpu", class_thresh=NUSC_CLASS_THRESH)
+    r2 = pp2(head).per_image()[0]
+    for c, th in NUSC_CLASS_THRESH.items():
+        assert (r2["pred_scores"][r2["pred_labels"] == c] > th).all()
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_pfn2_kernel_vs_fp32(cuda):
+    from triton_client_amd.ops.centerpoint import PFNEncoder
+    cfg = _small_cfg()
+    m = _model(cfg)
+    p5 = _cloud(cfg, 1)
+    v, zyx, num, _ = voxelize_np(p5, cfg.voxel, 5)
+    V = len(v)
+    coords = np.pad(zyx, ((0, 0), (1, 0))).astype(np.int32)
+    enc = PFNEncoder(cfg.voxel, m.pfn, 1, device=cuda)
+    feat = torch.zeros((1, cfg.voxel.max_voxels, 64), dtype=torch.float32, device=cuda)
+    vox = torch.zeros((1, cfg.voxel.max_voxels, 20, 5), device=cuda)
+    vox[0, :V] = torch.from_numpy(v).to(cuda)
+    nump = torch.zeros((1, cfg.voxel.max_voxels), dtype=torch.int32, device=cuda)
+    nump[0, :V] = torch.from_numpy(num).to(cuda)
+    co = torch.zeros((1, cfg.voxel.max_voxels, 4), dtype=torch.int32, device=cuda)
+    co[0, :V] = torch.from_numpy(coords).to(cuda)
+    vc = torch.tensor([V], dtype=torch.int32, device=cuda)
+    enc.encode_from_voxels(vox, nump, co, vc, feat_out=feat)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        f = pfn_point_features(torch.from_numpy(v), torch.from_numpy(num.astype(np.int64)),
+                               torch.from_numpy(coords), cfg.voxel)
+        ref = m.pfn.float()(f)
+    got = feat[0, :V].cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 0.02 * max(1.0, ref.abs().max().item()), err
+    # the canvas holds the same features (bf16) at each pillar's cell
+    cv = enc.canvas[0].float().cpu()
+    np.testing.assert_allclose(cv[coords[:, 2], coords[:, 3]].numpy(), got.numpy(), rtol=0.02, atol=0.02)
+
+
+@pytest.mark.gpu
+def test_centerhead_decode_gpu_matches_cpu(cuda):
+    from triton_client_amd.ops.centerpoint import CenterPointPostprocess
+    cfg = _small_cfg()
+    m = _model(cfg)
+    H, W = cfg.feature_map_size
+    with torch.no_grad():
+        canvas = torch.rand(2, 64, H * 4, W * 4)
+        mo = merged_task_outputs(m.bev_forward(canvas))
+    head = torch.zeros(2, H, W, 96)
+    for t, o in enumerate(mo):
+        head[..., 16 * t:16 * t + o.shape[1]] = o.permute(0, 2, 3, 1)
+    offs = [16 * t for t in range(6)]
+    ref = CenterPointPostprocess(cfg, 2, offs, device="cpu")(head).per_image()
+    got = CenterPointPostprocess(cfg, 2, offs, device=cuda)(head.to(cuda)).per_image()
+    for r, g in zip(ref, got):
+        assert abs(len(r["pred_scores"]) - len(g["pred_scores"])) <= 2
+        k = min(20, len(r["pred_scores"]))
+        np.testing.assert_allclose(np.sort(g["pred_scores"])[::-1][:k], np.sort(r["pred_scores"])[::-1][:k],
+                                   rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_centerpoint_pipeline_graph(cuda):
+    from triton_client_amd.pipelines import CenterPointPipeline, GraphRunner
+    pipe = CenterPointPipeline(batch=2, max_points=32768, device=cuda)
+    for b in range(2):
+        c = lidar_sweep(LidarSpec(rings=32, azimuth_steps=1024, sensor_height=1.8), b)
+        raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+        pipe.data[b * pipe.frame_bytes: b * pipe.frame_bytes + raw.numel()].copy_(raw)
+        pipe.frame_n[b] = c.shape[0]
+    d = pipe.calibrate_detection_density(300.0)
+    assert -30 < d < 30
+    eager = pipe.step()
+    torch.cuda.synchronize()
+    e = eager.per_image()
+    run = GraphRunner(pipe.step)
+    g = run().per_image()
+    g2 = run().per_image()
+    assert all(len(x["pred_scores"]) > 0 for x in e)
+    for a, b, c in zip(e, g, g2):
+        np.testing.assert_array_equal(b["pred_boxes"], c["pred_boxes"])
+        assert a["pred_boxes"].shape[1] == 9 and len(a["pred_scores"]) <= 6 * 83

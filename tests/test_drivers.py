@@ -265,3 +265,25 @@ def test_evaluate_inference_live_and_bag(tmp_path):
                             metrics_port=None)
     s2 = ev2.evaluate_bag(bag, batch=4)
     assert s2.matched_images == 6 and abs(s2.map50 - 0.995) < 1e-6
+
+
+def test_centerpoint_served_over_kserve():
+    """centerpoint_pp contract: 5-feature voxels in (voxel geometry from the served
+    config), 9-d det3d boxes out; Detection3DArray reads yaw at index 8."""
+    from triton_client_amd.config.lidar import NUSC_PILLARS, CenterPointConfig
+    from triton_client_amd.server.models import CenterPointModel
+    v = dataclasses.replace(NUSC_PILLARS, point_cloud_range=(-12.8, -12.8, -5.0, 12.8, 12.8, 3.0), max_voxels=4000)
+    cfg = CenterPointConfig(voxel=v, score_thresh=0.0, nms_pre_max=16, nms_post_max=4)
+    repo = ModelRepository("cpu")
+    repo.add(CenterPointModel("centerpoint_pp", cfg=cfg, device="cpu"))
+    with KServeServer(repo, "127.0.0.1:0") as srv:
+        ch = GRPCChannel({"grpc_channel": srv.target}, Flags("centerpoint_pp"))
+        eng = RemoteDetector3D(ch, Pointpillars_client(), z_offset=0.0)
+        assert eng.pre.cfg.num_point_features == 5 and eng.pre.cfg == v
+        p = eng.detect([_cloud(3)])[0]
+        assert p["pred_boxes"].shape[1] == 9 and len(p["pred_scores"]) == 6 * 4
+        assert set(np.unique(p["pred_labels"])) <= set(range(10))
+        m = boxes_to_detection3d(p, [0], msgs.Header())
+        q = m.detections[0].bbox.center.orientation
+        assert abs(q.z - np.sin(p["pred_boxes"][0, 8] / 2)) < 1e-5
+        ch.close()

@@ -45,8 +45,9 @@ def voxel_config_from_model(model_config) -> Optional[VoxelConfig]:
     if p is None or "voxel_size" not in p:
         return None
     g = lambda k: json.loads(p[k].string_value)  # noqa: E731
+    nf = int(g("num_point_features")) if "num_point_features" in p else 4
     return VoxelConfig(tuple(g("point_cloud_range")), tuple(g("voxel_size")), int(g("max_points_per_voxel")),
-                       int(g("max_voxels")), 4)
+                       int(g("max_voxels")), nf)
 
 
 class PointpillarPreprocess:

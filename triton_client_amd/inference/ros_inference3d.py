@@ -32,11 +32,12 @@ def select_boxes(pred: dict, labels: Optional[Sequence[int]] = (2,), score_thres
 def boxes_to_jsk(pred: dict, idx, header: msgs.Header) -> msgs.BoundingBoxArray:
     arr = msgs.BoundingBoxArray(header=header)
     b = pred["pred_boxes"]
+    yaw_i = 8 if b.shape[-1] >= 9 else 6
     for i in idx:
         x = b[i]
         arr.boxes.append(msgs.BoundingBox(
             header=header,
-            pose=msgs.Pose(msgs.Point(float(x[0]), float(x[1]), float(x[2])), compat.yaw2quaternion(float(x[6]))),
+            pose=msgs.Pose(msgs.Point(float(x[0]), float(x[1]), float(x[2])), compat.yaw2quaternion(float(x[yaw_i]))),
             dimensions=msgs.Vector3(float(x[4]), float(x[3]), float(x[5])),
             value=float(pred["pred_scores"][i]), label=int(pred["pred_labels"][i])))
     return arr

@@ -12,6 +12,8 @@ neck's three up-sampled scales), so no concat kernel ever runs.
 * :class:`FastBEV`     — BaseBEVBackbone + AnchorHeadSingle of
   :class:`~.pointpillars.PointPillars`; the three head 1x1 convs are merged
   into one 384→72 GEMM; outputs cls / box / dir as slices of it.
+* :class:`FastCenterPoint` — det3d RPN + CenterHead of
+  :class:`~.centerpoint.CenterPoint` (merged head GEMMs, see the class).
 """
 from __future__ import annotations
 
@@ -166,16 +168,11 @@ class FastYOLOv5:
         return outs
 
 
-class FastBEV:
-    """PointPillars BEV backbone + anchor head on fused convs."""
+class _BEVBackbonePlan:
+    """BaseBEVBackbone / det3d RPN: down blocks (ping-pong buffers) and deblocks
+    writing straight into their channel slices of the concat buffer."""
 
-    def __init__(self, model, batch: int, device="cuda"):
-        self.device = torch.device(device)
-        cfg = model.cfg
-        nx, ny, _ = cfg.voxel.grid_size
-        B = batch
-        bufs = self.bufs = _Buffers(self.device)
-        bb = model.backbone
+    def __init__(self, bb, B: int, ny: int, nx: int, bufs: _Buffers, device):
         self.blocks = []
         H, W = ny, nx
         for blk in bb.blocks:
@@ -186,9 +183,12 @@ class FastBEV:
             self.blocks.append((convs, pp, H, W))
         self.ups = []
         up_c = [u.conv.out_channels for u in bb.deblocks]
-        H0, W0 = self.blocks[0][2] * int(max(1, bb.deblocks[0].s)), self.blocks[0][3] * int(max(1, bb.deblocks[0].s))
-        if bb.deblocks[0].s < 1:
-            H0, W0 = self.blocks[0][2] // int(round(1 / bb.deblocks[0].s)), self.blocks[0][3] // int(round(1 / bb.deblocks[0].s))
+        s0 = bb.deblocks[0].s
+        if s0 < 1:
+            k = int(round(1 / s0))
+            H0, W0 = self.blocks[0][2] // k, self.blocks[0][3] // k
+        else:
+            H0, W0 = self.blocks[0][2] * int(round(s0)), self.blocks[0][3] * int(round(s0))
         self.out_hw = (H0, W0)
         self.cat = bufs.new(B, H0, W0, sum(up_c))
         off = 0
@@ -196,6 +196,28 @@ class FastBEV:
             assert u.fused, "call fuse_model() first"
             self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device), off, c))
             off += c
+
+    def forward(self, canvas: NHWC) -> NHWC:
+        x = canvas
+        for (convs, pp, H, W), (up, off, c) in zip(self.blocks, self.ups):
+            for i, cv in enumerate(convs):
+                x = cv(x, out=pp[i % 2])
+            up(x, out=NHWC(self.cat.t, off, c))
+        return self.cat
+
+
+class FastBEV:
+    """PointPillars BEV backbone + anchor head on fused convs."""
+
+    def __init__(self, model, batch: int, device="cuda"):
+        self.device = torch.device(device)
+        cfg = model.cfg
+        nx, ny, _ = cfg.voxel.grid_size
+        B = batch
+        bufs = self.bufs = _Buffers(self.device)
+        self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)
+        self.blocks, self.ups, self.cat, self.out_hw = self.bb.blocks, self.bb.ups, self.bb.cat, self.bb.out_hw
+        H0, W0 = self.out_hw
         hd = model.head
         merged = nn.Conv2d(hd.conv_cls.in_channels,
                            hd.conv_cls.out_channels + hd.conv_box.out_channels + hd.conv_dir.out_channels, 1)
@@ -208,12 +230,72 @@ class FastBEV:
         self.hout = bufs.new(B, H0, W0, self.head.N)
 
     def forward(self, canvas: NHWC):
-        x = canvas
-        for (convs, pp, H, W), (up, off, c) in zip(self.blocks, self.ups):
-            for i, cv in enumerate(convs):
-                x = cv(x, out=pp[i % 2])
-            up(x, out=NHWC(self.cat.t, off, c))
-        self.head(self.cat, out=self.hout)
+        self.head(self.bb.forward(canvas), out=self.hout)
         t = self.hout.t
         return (NHWC(t, 0, self.n_cls), NHWC(t, self.n_cls, self.n_box),
                 NHWC(t, self.n_cls + self.n_box, self.n_dir))
+
+
+class FastCenterPoint:
+    """CenterPoint-PP RPN + CenterHead on fused convs.
+
+    * shared conv 3x3 384→64 (+BN+ReLU);
+    * all tasks' first-level head convs (6 tasks × 6 heads × conv3x3 64→64
+      +BN+ReLU) as ONE 64→2304 GEMM into a [B,H,W,2304] buffer;
+    * per task, its heads' final 3x3 convs as one conv over the task's 384-channel
+      slice with block-diagonal weights (out = reg2|height1|dim3|rot2|vel2|hm nc,
+      padded to 16) writing channels [16t, 16t+16) of the merged head output —
+      the layout :class:`~..ops.centerpoint.CenterPointPostprocess` decodes.
+    """
+
+    TASK_STRIDE = 16
+
+    def __init__(self, model, batch: int, device="cuda"):
+        from .centerpoint import HEAD_ORDER
+
+        self.device = torch.device(device)
+        cfg = self.cfg = model.cfg
+        nx, ny, _ = cfg.voxel.grid_size
+        B = batch
+        bufs = self.bufs = _Buffers(self.device)
+        self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)
+        H0, W0 = self.bb.out_hw
+        hd = model.head
+        self.shared = _fc(hd.shared, device)
+        self.sh = bufs.new(B, H0, W0, self.shared.N)
+        names = list(HEAD_ORDER) + ["hm"]
+        pre = [t.pre[n] for t in hd.tasks for n in names]
+        c_mid = pre[0].conv.out_channels
+        big = nn.Conv2d(pre[0].conv.in_channels, c_mid * len(pre), 3, 1, 1)
+        with torch.no_grad():
+            big.weight.copy_(torch.cat([m.conv.weight for m in pre]).float())
+            big.bias.copy_(torch.cat([m.conv.bias for m in pre]).float())
+        self.pre = FusedConv(big, act=ACT_RELU, device=device)
+        self.mid = bufs.new(B, H0, W0, self.pre.N)
+        self.c_task_in = c_mid * len(names)
+        self.finals = []
+        for t, task in enumerate(hd.tasks):
+            outs = [task.out[n] for n in names]
+            n_out = sum(o.out_channels for o in outs)
+            assert n_out <= self.TASK_STRIDE
+            conv = nn.Conv2d(self.c_task_in, self.TASK_STRIDE, 3, 1, 1)
+            with torch.no_grad():
+                conv.weight.zero_()
+                conv.bias.zero_()
+                o0 = 0
+                for h, o in enumerate(outs):
+                    conv.weight[o0:o0 + o.out_channels, h * c_mid:(h + 1) * c_mid] = o.weight.float()
+                    conv.bias[o0:o0 + o.out_channels] = o.bias.float()
+                    o0 += o.out_channels
+            self.finals.append(FusedConv(conv, act=ACT_NONE, device=device))
+        self.task_offsets = [t * self.TASK_STRIDE for t in range(len(hd.tasks))]
+        self.hout = bufs.new(B, H0, W0, self.TASK_STRIDE * len(hd.tasks))
+
+    def forward(self, canvas: NHWC) -> NHWC:
+        cat = self.bb.forward(canvas)
+        self.shared(cat, out=self.sh)
+        self.pre(self.sh, out=self.mid)
+        for t, fc in enumerate(self.finals):
+            fc(NHWC(self.mid.t, t * self.c_task_in, self.c_task_in),
+               out=NHWC(self.hout.t, t * self.TASK_STRIDE, self.TASK_STRIDE))
+        return self.hout

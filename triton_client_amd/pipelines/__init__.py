@@ -3,3 +3,4 @@ hipGraph runner that replays a whole step with one launch."""
 from .camera import CameraPipeline  # noqa: F401
 from .lidar import LidarPipeline  # noqa: F401
 from .graph import GraphRunner  # noqa: F401
+from .centerpoint import CenterPointPipeline  # noqa: F401,E402

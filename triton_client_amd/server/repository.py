@@ -47,6 +47,13 @@ def _family(name: str) -> Optional[str]:
     return None
 
 
+def _centerpoint(name):
+    def f(device="auto", **kw):
+        from .models import CenterPointModel
+        return CenterPointModel(name, device=device, **kw)
+    return f
+
+
 FACTORIES: Dict[str, Factory] = {
     "YOLOv5nCOCO": _yolo("YOLOv5nCOCO", "n", 80, 640),
     "YOLOv5n": _yolo("YOLOv5n", "n", 80, 640),
@@ -54,6 +61,8 @@ FACTORIES: Dict[str, Factory] = {
     "weed_detector": _yolo("weed_detector", "n", 2, 512),
     "pointpillar_kitti": _pointpillars("pointpillar_kitti"),
     "pointpillar_python": _pointpillars("pointpillar_python"),
+    "centerpoint_pp": _centerpoint("centerpoint_pp"),
+    "centerpoint": _centerpoint("centerpoint"),
     "echo": lambda device="auto", **kw: EchoModel("echo"),
 }
 
