@@ -81,6 +81,16 @@ struct Reader {
       default: return ok = false;
     }
   }
+  // length-delimited payload: returns its start and advances past it, or
+  // fails (ok = false) when the declared length runs past the buffer
+  const uint8_t* take(uint64_t* len) {
+    const uint64_t l = varint();
+    if (!ok || (uint64_t)(end - p) < l) { ok = false; *len = 0; return p; }
+    const uint8_t* s = p;
+    p += l;
+    *len = l;
+    return s;
+  }
 };
 
 }  // namespace
@@ -150,49 +160,57 @@ TCA_API long tca_kserve_encode_request(const char* model_name, const char* model
 // Returns 0 on success, -1 malformed, -2 capacity exceeded.
 TCA_API int tca_kserve_parse_response(const uint8_t* buf, long len, int max_out, long* meta, int64_t* shapes,
                                       int max_dims, long* raw, long* counts) {
+  if (!buf || len < 0 || max_out < 0 || max_dims < 0) return -1;
   Reader r{buf, buf + len};
   int n_out = 0, n_raw = 0, nd_total = 0;
-  counts[2] = counts[3] = 0;
+  counts[0] = counts[1] = counts[2] = counts[3] = 0;
   while (r.p < r.end && r.ok) {
     const uint64_t tag = r.varint();
     const int field = (int)(tag >> 3), wire = (int)(tag & 7);
     if (!r.ok) break;
     if (field == 1 && wire == 2) {
-      const uint64_t l = r.varint();
-      counts[2] = r.p - buf;
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
+      counts[2] = s - buf;
       counts[3] = (long)l;
-      r.p += l;
     } else if (field == 5 && wire == 2) {
-      const uint64_t l = r.varint();
-      if (!r.ok || (uint64_t)(r.end - r.p) < l) return -1;
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
       if (n_out >= max_out) return -2;
-      Reader t{r.p, r.p + l};
+      Reader t{s, s + l};
       long* m = meta + n_out * 8;
       m[0] = m[1] = m[2] = m[3] = 0;
       m[4] = 0;
       m[5] = nd_total;
       while (t.p < t.end && t.ok) {
         const uint64_t tt = t.varint();
+        if (!t.ok) break;
         const int f = (int)(tt >> 3), w = (int)(tt & 7);
-        if (f == 1 && w == 2) {
-          const uint64_t sl = t.varint();
-          m[0] = t.p - buf; m[1] = (long)sl; t.p += sl;
-        } else if (f == 2 && w == 2) {
-          const uint64_t sl = t.varint();
-          m[2] = t.p - buf; m[3] = (long)sl; t.p += sl;
+        if ((f == 1 || f == 2) && w == 2) {
+          uint64_t sl;
+          const uint8_t* q = t.take(&sl);
+          if (!t.ok) break;
+          m[f == 1 ? 0 : 2] = q - buf;
+          m[f == 1 ? 1 : 3] = (long)sl;
         } else if (f == 3 && w == 2) {  // packed int64
-          const uint64_t sl = t.varint();
-          const uint8_t* e = t.p + sl;
-          Reader s{t.p, e};
-          while (s.p < s.end && s.ok) {
+          uint64_t sl;
+          const uint8_t* q = t.take(&sl);
+          if (!t.ok) break;
+          Reader sr{q, q + sl};
+          while (sr.p < sr.end && sr.ok) {
+            const uint64_t d = sr.varint();
+            if (!sr.ok) return -1;
             if (nd_total >= max_dims) return -2;
-            shapes[nd_total++] = (int64_t)s.varint();
+            shapes[nd_total++] = (int64_t)d;
             ++m[4];
           }
-          t.p = e;
         } else if (f == 3 && w == 0) {  // unpacked int64
+          const uint64_t d = t.varint();
+          if (!t.ok) break;
           if (nd_total >= max_dims) return -2;
-          shapes[nd_total++] = (int64_t)t.varint();
+          shapes[nd_total++] = (int64_t)d;
           ++m[4];
         } else if (!t.skip(w)) {
           return -1;
@@ -200,15 +218,14 @@ TCA_API int tca_kserve_parse_response(const uint8_t* buf, long len, int max_out,
       }
       if (!t.ok) return -1;
       ++n_out;
-      r.p += l;
     } else if (field == 6 && wire == 2) {
-      const uint64_t l = r.varint();
-      if (!r.ok || (uint64_t)(r.end - r.p) < l) return -1;
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
       if (n_raw >= max_out) return -2;
-      raw[n_raw * 2] = r.p - buf;
+      raw[n_raw * 2] = s - buf;
       raw[n_raw * 2 + 1] = (long)l;
       ++n_raw;
-      r.p += l;
     } else if (!r.skip(wire)) {
       return -1;
     }

@@ -39,6 +39,7 @@ import torch
 
 from ..ops.image import frame_xform, preprocess
 from ..ros import msgs
+from ..utils.trace import trace_range
 
 
 def _device(device) -> torch.device:
@@ -136,8 +137,9 @@ class LocalDetector2D(Detector2D):
                     for j, i in enumerate(chunk):
                         pinned[j].numpy()[...] = frames[i][..., :3]
                     p.frames.copy_(pinned, non_blocking=True)
-                    res = run()
-                    per = res.per_image()
+                    with trace_range("camera_graph"):
+                        res = run()
+                        per = res.per_image()
                     for j, i in enumerate(chunk):
                         d = per[j]
                         out[i] = np.concatenate([d["box"], d["score"][:, None],
@@ -241,8 +243,9 @@ class LocalDetector3D(Detector3D):
                         nh[j] = n
                     p.data.copy_(pinned, non_blocking=True)
                     p.frame_n.copy_(nh, non_blocking=True)
-                    res = run()
-                    per = res.per_image()
+                    with trace_range("lidar_graph"):
+                        res = run()
+                        per = res.per_image()
                     for j, i in enumerate(chunk):
                         d = per[j]
                         box = d["box"].astype(np.float32).copy()
@@ -426,8 +429,11 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         return np.asarray(d, np.float32).reshape(-1, 6) if len(d) else _empty2d()
 
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
-        preps = [self._prep(f) for f in frames]
-        resps = self._run([[(self.input_name, self.dtype, a)] for a, _ in preps], self.requested)
+        from ..utils.trace import trace_range
+        with trace_range("preprocess"):
+            preps = [self._prep(f) for f in frames]
+        with trace_range("rpc"):
+            resps = self._run([[(self.input_name, self.dtype, a)] for a, _ in preps], self.requested)
         out = []
         for (a, xf), r in zip(preps, resps):
             d = self._extract(r)

@@ -16,6 +16,7 @@ import numpy as np
 
 from ..ros import compat, msgs
 from ..utils.draw import draw_detections
+from ..utils.metrics import StageTimer
 from .base_inference import BaseInference
 from .engines import Detector2D, RemoteDetector2D
 
@@ -77,14 +78,18 @@ class RosInference(BaseInference):
     def process(self, images: Sequence) -> List[tuple]:
         """Messages → [(annotated Image msg, Detection2DArray, dets [n,6])]."""
         t0 = time.perf_counter()
-        rgb = [decode_image_msg(m) for m in images]
-        dets = self.engine.detect(rgb)
+        timer = StageTimer(self.metrics)
+        with timer("decode"):
+            rgb = [decode_image_msg(m) for m in images]
+        with timer("detect"):
+            dets = self.engine.detect(rgb)
         out = []
-        for m, img, d in zip(images, rgb, dets):
-            if self.draw:
-                img = draw_detections(img.copy(), d, self.class_names)
-            im = compat.numpy_to_imgmsg(img, "rgb8", header=m.header)
-            out.append((im, detections_to_msg(d, m.header), d))
+        with timer("draw_publish"):
+            for m, img, d in zip(images, rgb, dets):
+                if self.draw:
+                    img = draw_detections(img.copy(), d, self.class_names)
+                im = compat.numpy_to_imgmsg(img, "rgb8", header=m.header)
+                out.append((im, detections_to_msg(d, m.header), d))
         self.frames += len(images)
         if self.metrics is not None:
             self.metrics.stage("frame", (time.perf_counter() - t0) / max(len(images), 1))

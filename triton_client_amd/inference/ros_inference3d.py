@@ -16,6 +16,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from ..ros import compat, msgs
+from ..utils.metrics import StageTimer
 from .base_inference import BaseInference
 from .engines import Detector3D, RemoteDetector3D
 
@@ -93,8 +94,11 @@ class RosInference3D(BaseInference):
 
     def process(self, clouds: Sequence[msgs.PointCloud2]) -> List[tuple]:
         t0 = time.perf_counter()
-        preds = self.engine.detect(clouds)
-        out = [(self.to_msg(p, c.header), p) for c, p in zip(clouds, preds)]
+        timer = StageTimer(self.metrics)
+        with timer("detect3d"):
+            preds = self.engine.detect(clouds)
+        with timer("boxes_publish"):
+            out = [(self.to_msg(p, c.header), p) for c, p in zip(clouds, preds)]
         self.frames += len(clouds)
         if self.metrics is not None:
             self.metrics.stage("frame3d", (time.perf_counter() - t0) / max(len(clouds), 1))

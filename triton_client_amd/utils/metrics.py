@@ -111,7 +111,8 @@ class EvalMetrics:
 
 
 class StageTimer:
-    """with timer('preprocess'): ... → ClientMetrics.stage()."""
+    """with timer('preprocess'): ... → ClientMetrics.stage() + a roctx range of
+    the same name (utils/trace.py)."""
 
     def __init__(self, metrics: Optional[ClientMetrics]):
         self.m = metrics
@@ -125,9 +126,13 @@ class _Ctx:
         self.m, self.name = m, name
 
     def __enter__(self):
+        from .trace import push
+        push(self.name)
         self.t = time.perf_counter()
         return self
 
     def __exit__(self, *exc):
+        from .trace import pop
+        pop()
         if self.m is not None:
             self.m.stage(self.name, time.perf_counter() - self.t)
