@@ -106,3 +106,25 @@ def test_bag2d_data_parallel_torchrun(bags, tmp_path):
     with Bag(ob) as b:
         dets = [m for t, m, _ in b.read_messages(topics=["/aver_01/camera_color/detection/detections"])]
     assert len(dets) == 4 and [d.header.seq for d in dets] == [0, 1, 2, 3]
+
+
+def test_bagtools_and_bev(bags, tmp_path):
+    import numpy as np
+    from triton_client_amd.cli import bagtools
+    from triton_client_amd.utils.visualize import boxes_to_corners_3d, render_bev
+    _, cam, pc = bags
+    assert bagtools.main(["info", cam]) == 0
+    dst = str(tmp_path / "cut.bag")
+    assert bagtools.main(["stitch", cam, dst, "-n", "3"]) == 0
+    with Bag(dst) as b:
+        assert b.get_message_count() == 3
+    out = str(tmp_path / "pcs")
+    assert bagtools.main(["extract-pc", pc, out, "--bev"]) == 0
+    files = sorted(os.listdir(out))
+    assert files == ["000000.npy", "000000.png", "000001.npy", "000001.png"]
+    pts = np.load(os.path.join(out, "000000.npy"))
+    assert pts.shape[1] == 4 and np.isfinite(pts).all()
+    c = boxes_to_corners_3d(np.array([[1.0, 2.0, 0.0, 4.0, 2.0, 1.5, np.pi / 2]]))
+    np.testing.assert_allclose(c[0, :, 0].max() - c[0, :, 0].min(), 2.0, atol=1e-9)  # rotated 90°: x extent = dy
+    img = render_bev(pts, boxes=np.array([[20.0, 0.0, -1.0, 4.0, 2.0, 1.5, 0.3]]))
+    assert img.shape == (691, 794, 3) and (img[..., 1] == 230).any()
