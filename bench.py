@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
     ap.add_argument("--only", choices=["both", "camera", "lidar"], default="both")
+    ap.add_argument("--camera-model", choices=["yolov5n", "retinanet", "fcos"], default="yolov5n",
+                    help="2D detector: YOLOv5n-640 (headline) or Detectron2 RetinaNet / FCOS R50-FPN at 800x1344")
     ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint"], default="pointpillars",
                     help="3D detector: PointPillars KITTI (headline) or CenterPoint-PP nuScenes")
     ap.add_argument("--json-out", default=None)
@@ -87,7 +89,13 @@ def main():
     use_lid = args.only in ("both", "lidar")
 
     torch.manual_seed(0)
-    cam = CameraPipeline(batch=B, src_hw=(H0, W0), device=dev) if use_cam else None
+    det2 = args.camera_model != "yolov5n"
+    if use_cam and det2:
+        from triton_client_amd.config.detectron import DetectronConfig
+        from triton_client_amd.pipelines import DetectronPipeline
+        cam = DetectronPipeline(batch=B, src_hw=(H0, W0), cfg=DetectronConfig(arch=args.camera_model), device=dev)
+    else:
+        cam = CameraPipeline(batch=B, src_hw=(H0, W0), device=dev) if use_cam else None
     if use_lid and cp:
         from triton_client_amd.pipelines import CenterPointPipeline
         lid = CenterPointPipeline(batch=B, max_points=max_points, device=dev)
@@ -140,7 +148,8 @@ def main():
                 lid.frame_n.copy_(n_host[0])
     if args.ingest == "local" or info.is_main:
         if use_cam:
-            calib["yolo_logit_shift"] = cam.calibrate_detection_density(args.target_2d)
+            calib["detectron_logit_shift" if det2 else "yolo_logit_shift"] = cam.calibrate_detection_density(
+                min(args.target_2d, 300.0) if det2 else args.target_2d)
         if use_lid:
             key = "centerpoint_hm_shift" if cp else "pp_logit_shift"
             calib[key] = lid.calibrate_detection_density(args.target_3d)
@@ -271,6 +280,8 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(info, elapsed)
 
+    cam_name = {"yolov5n": "YOLOv5n-640 (COCO, 80 cls)", "retinanet": "RetinaNet R50-FPN 800x1344 (COCO)",
+                "fcos": "FCOS R50-FPN 800x1344 (COCO)"}[args.camera_model]
     if info.is_main:
         frames = info.world * B * args.steps
         fps = frames / elapsed
@@ -298,8 +309,7 @@ def main():
                      f"(PointCloud2 16 B/pt, ~2% NaN dropouts); random-init weights (He-normal + LSUV rescaling on "
                      f"sample frames), detection-head bias offset calibrated so ~{args.target_2d:g} 2D / ~{args.target_3d:g} 3D candidates per frame reach NMS"),
             "config": {
-                "model": ({"both": "YOLOv5n-640 (COCO, 80 cls) + ", "camera": "YOLOv5n-640 (COCO, 80 cls)",
-                           "lidar": ""}[args.only]
+                "model": ({"both": cam_name + " + ", "camera": cam_name, "lidar": ""}[args.only]
                           + ("" if args.only == "camera" else
                              ("CenterPoint-PP (nuScenes, 10 cls)" if cp else "PointPillars (KITTI, 3 cls)"))),
                 "global_batch": info.world * B,

@@ -72,6 +72,8 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[B
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int fr = lane & 15, fq = lane >> 4;
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res != nullptr;  // act(conv + residual) instead of act(conv) + residual
   constexpr int LD = BN + 8;  // +16 B per row: the 16 rows a lane group writes hit distinct banks
   __hip_bfloat16* st = reinterpret_cast<__hip_bfloat16*>(smem);
 #pragma unroll
@@ -86,7 +88,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[B
         const int n = n0 + nl + r;
         float v = acc[i][j][r];
         if (a.bias && n < a.N) v += a.bias[n];
-        q[r] = __float2bfloat16(act_fn(v, a.act));
+        q[r] = __float2bfloat16(post_res ? v : act_fn(v, act));
       }
       *reinterpret_cast<uint2*>(st + ml * LD + nl) = *reinterpret_cast<uint2*>(q);
     }
@@ -115,7 +117,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, const f32x4 (&acc)[B
       const __hip_bfloat16* y = reinterpret_cast<const __hip_bfloat16*>(&r);
       __hip_bfloat16 z[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = __float2bfloat16(__bfloat162float(x[e]) + __bfloat162float(y[e]));
+      for (int e = 0; e < 8; ++e) {
+        const float sum = __bfloat162float(x[e]) + __bfloat162float(y[e]);
+        z[e] = __float2bfloat16(post_res ? act_fn(sum, act) : sum);
+      }
       v = *reinterpret_cast<uint4*>(z);
     }
     *reinterpret_cast<uint4*>(a.out + o) = v;

@@ -46,6 +46,11 @@ _KERNEL_SIGS = {
     "tca_pfn2_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
     "tca_pfn2_voxels": [P, I, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
     "tca_centerhead_decode": [P, I, I, I, I, I, I, P, P, I, F, P, P, I, P, P, P, P, P, P, I, P],
+    "tca_maxpool2d_nhwc": [P, I, I, I, I, I, I, I, I, I, P, I, I, I, I, P],
+    "tca_retina_decode": [P, P, I, I, I, I, I, I, I, I, I, P, F, F, F, F, I, I, P, P, P, P, P, I, I, P],
+    "tca_fcos_decode": [P, P, P, I, I, I, I, I, I, I, I, I, F, F, F, I, I, P, P, P, P, P, I, I, P],
+    "tca_segment_merge": [P, P, P, P, I, I, P, P, I, I, I, P, P, P, P, P, I, P],
+    "tca_group_norm_nhwc": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, P],
     "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, P],
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, P],
 }

@@ -392,6 +392,10 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         from ..proto import model_config_pb2 as mc
 
         self.nhwc = self.format == mc.ModelInput.FORMAT_NHWC
+        # the tensor shape sent is the model's declared one (reference ros_inference.py:64-68:
+        # [c, h, w] / [h, w, c]; Triton's `reshape` adds the batch dim), or [1, ...] when the
+        # model declares an explicit batch dimension
+        self.batch_dim = len(self.model_metadata.inputs[0].shape) == 4
         # the reference requests all 4 outputs of a Detectron model, else the first one
         # (ros_inference.py:70-87)
         self.requested = list(self.output_names) if len(self.output_names) == 4 else list(self.output_names[:1])
@@ -399,7 +403,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         if ch.input is not None:
             ch.input.name, ch.input.datatype = self.input_name, self.dtype
             ch.input.ClearField("shape")
-            ch.input.shape.extend([1, self.h, self.w, c] if self.nhwc else [1, c, self.h, self.w])
+            shape = [self.h, self.w, c] if self.nhwc else [c, self.h, self.w]
+            ch.input.shape.extend(([1] if self.batch_dim else []) + shape)
             _set_outputs(ch, self.requested)
         self.pre, self.post = client.get_preprocess(), client.get_postprocess()
         self.scaling = scaling or getattr(self.pre, "scaling", "COCO")
@@ -416,6 +421,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
                            "NHWC" if self.nhwc else "NCHW")
         if self.nhwc:
             x = x.permute(0, 2, 3, 1)
+        if not self.batch_dim:
+            x = x[0]
         a = x.cpu().numpy()
         a = np.ascontiguousarray(a.astype(_NP_OF.get(self.dtype, np.float32), copy=False))
         return a, xf

@@ -299,3 +299,179 @@ class FastCenterPoint:
             fc(NHWC(self.mid.t, t * self.c_task_in, self.c_task_in),
                out=NHWC(self.hout.t, t * self.TASK_STRIDE, self.TASK_STRIDE))
         return self.hout
+
+
+def _conv_out(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+class FastDetectron:
+    """Detectron2 RetinaNet / FCOS (ResNet-50-FPN) on fused convs.
+
+    * input ``x`` [B, H, W, 8]: the K1 kernel writes normalised RGB + 5 zero pad
+      channels (mean/std folded into K1's per-channel scale / bias);
+    * bottleneck outputs relu(conv3 + shortcut) via the post-residual epilogue;
+    * FPN top-down add fused as the lateral conv's residual (upsample2x → lateral);
+    * RetinaNet: the cls and box towers' first convs share their input, so they
+      run as one 256→512 GEMM; the head weights are shared over levels, each
+      level has its own output buffers;
+    * FCOS: GroupNorm(32)+ReLU kernels between the tower convs.
+    """
+
+    IN_CHANNELS = 8
+
+    def __init__(self, model, batch: int, device="cuda"):
+        from ..ops.conv import FusedConv
+
+        self.device = torch.device(device)
+        cfg = self.cfg = model.cfg
+        B = self.B = batch
+        H, W = cfg.input_hw
+        bufs = self.bufs = _Buffers(self.device)
+        self.x = bufs.new(B, H, W, self.IN_CHANNELS)
+        bb = model.backbone
+        self.stem = _fc(bb.stem, device, cin_pad=self.IN_CHANNELS)
+        h, w = _conv_out(H, 7, 2, 3), _conv_out(W, 7, 2, 3)
+        self.stem_out = bufs.new(B, h, w, 64)
+        h, w = _conv_out(h, 3, 2, 1), _conv_out(w, 3, 2, 1)
+        self.pool = bufs.new(B, h, w, 64)
+        self.stages = []
+        x_c = 64
+        for st in bb.stages:
+            blocks = []
+            for blk in st:
+                c1, c2, c3 = _fc(blk.conv1, device), _fc(blk.conv2, device), blk.conv3
+                s = blk.conv1.s if blk.conv1.s > 1 else blk.conv2.s
+                ho, wo = _conv_out(h, 1, s, 0), _conv_out(w, 1, s, 0)
+                f3 = FusedConv(c3.conv, act=ACT_RELU, device=device, post_res=True)
+                sc = _fc(blk.shortcut, device) if blk.shortcut is not None else None
+                t1, t2 = bufs.new(B, ho, wo, c1.N), bufs.new(B, ho, wo, c2.N)
+                sbuf = bufs.new(B, ho, wo, sc.N) if sc is not None else None
+                out = bufs.new(B, ho, wo, f3.N)
+                blocks.append((c1, c2, f3, sc, t1, t2, sbuf, out))
+                h, w, x_c = ho, wo, f3.N
+            self.stages.append(blocks)
+        fpn = model.fpn
+        C = cfg.fpn_channels
+        self.lv_hw = [blocks[-1][7].shape[1:3] for blocks in self.stages[1:]]  # res3..res5
+        self.lat = [_fc(m, device) for m in fpn.lateral]
+        self.outc = [_fc(m, device) for m in fpn.output]
+        self.lat_buf = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw]
+        self.up_buf = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw[:2]]
+        self.p = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw]
+        self.p6p7_from_c5 = fpn.p6p7_from_c5
+        p6 = fpn.p6.conv
+        self.p6 = FusedConv(p6, act=ACT_NONE, device=device)
+        self.p6r = FusedConv(p6, act=ACT_RELU, device=device)
+        self.p7 = _fc(fpn.p7, device)
+        h5, w5 = self.lv_hw[2]
+        h6, w6 = _conv_out(h5, 3, 2, 1), _conv_out(w5, 3, 2, 1)
+        h7, w7 = _conv_out(h6, 3, 2, 1), _conv_out(w6, 3, 2, 1)
+        self.p.append(bufs.new(B, h6, w6, C))
+        self.p6relu = bufs.new(B, h6, w6, C)
+        self.p.append(bufs.new(B, h7, w7, C))
+        self.level_hw = [tuple(t.shape[1:3]) for t in self.p]
+        # ---- head
+        hd = model.head
+        self.fcos = cfg.arch == "fcos"
+        if self.fcos:
+            cls_convs = [m for m in hd.cls_subnet if isinstance(m, nn.Conv2d)]
+            box_convs = [m for m in hd.bbox_subnet if isinstance(m, nn.Conv2d)]
+            self.gn_cls = [m for m in hd.cls_subnet if isinstance(m, nn.GroupNorm)]
+            self.gn_box = [m for m in hd.bbox_subnet if isinstance(m, nn.GroupNorm)]
+            act = ACT_NONE
+        else:
+            cls_convs = [m.conv for m in hd.cls_subnet]
+            box_convs = [m.conv for m in hd.bbox_subnet]
+            act = ACT_RELU
+        first = nn.Conv2d(C, 2 * C, 3, 1, 1)
+        with torch.no_grad():
+            first.weight.copy_(torch.cat([cls_convs[0].weight, box_convs[0].weight]).float())
+            first.bias.copy_(torch.cat([cls_convs[0].bias, box_convs[0].bias]).float())
+        self.t_first = FusedConv(first, act=act, device=device)
+        self.t_cls = [FusedConv(m, act=act, device=device) for m in cls_convs[1:]]
+        self.t_box = [FusedConv(m, act=act, device=device) for m in box_convs[1:]]
+        self.cls_score = FusedConv(hd.cls_score, act=ACT_NONE, device=device)
+        if self.fcos:
+            merged = nn.Conv2d(C, 5, 3, 1, 1)
+            with torch.no_grad():
+                merged.weight.copy_(torch.cat([hd.bbox_pred.weight, hd.ctrness.weight]).float())
+                merged.bias.copy_(torch.cat([hd.bbox_pred.bias, hd.ctrness.bias]).float())
+            self.box_pred = FusedConv(merged, act=ACT_NONE, device=device)
+            dev = self.device
+            f32 = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
+            self.gn_params = [(f32(torch.cat([gc.weight, gb.weight])), f32(torch.cat([gc.bias, gb.bias])))
+                              for gc, gb in zip(self.gn_cls[:1], self.gn_box[:1])]
+            self.gn_params += [((f32(gc.weight), f32(gc.bias)), (f32(gb.weight), f32(gb.bias)))
+                               for gc, gb in zip(self.gn_cls[1:], self.gn_box[1:])]
+            self.gn_groups = self.gn_cls[0].num_groups
+            self.gn_eps = self.gn_cls[0].eps
+        else:
+            self.box_pred = FusedConv(hd.bbox_pred, act=ACT_NONE, device=device)
+        self.lvl = []
+        for hh, ww in self.level_hw:
+            self.lvl.append(dict(first=bufs.new(B, hh, ww, 2 * C), a=bufs.new(B, hh, ww, C), b=bufs.new(B, hh, ww, C),
+                                 c=bufs.new(B, hh, ww, C), d=bufs.new(B, hh, ww, C),
+                                 cls=bufs.new(B, hh, ww, self.cls_score.N), box=bufs.new(B, hh, ww, self.box_pred.N)))
+        from ..ops._ws import Workspace
+        self.ws = Workspace(self.device) if self.device.type == "cuda" else None
+
+    def input_view(self) -> torch.Tensor:
+        return self.x.t.permute(0, 3, 1, 2)
+
+    def _gn(self, x: NHWC, gamma, beta, groups=None):
+        from ..ops.detectron import group_norm_nhwc
+        group_norm_nhwc(x, gamma, beta, groups or self.gn_groups, self.gn_eps, relu=True, ws=self.ws)
+
+    def forward(self):
+        from ..ops.conv import maxpool2d_nhwc, upsample2x_nhwc
+
+        self.stem(self.x, out=self.stem_out)
+        maxpool2d_nhwc(self.stem_out, self.pool, 3, 2, 1)
+        x = self.pool
+        feats = []
+        for blocks in self.stages:
+            for c1, c2, f3, sc, t1, t2, sbuf, out in blocks:
+                c1(x, out=t1)
+                c2(t1, out=t2)
+                res = sc(x, out=sbuf) if sc is not None else x
+                f3(t2, out=out, res=res)
+                x = out
+            feats.append(x)
+        c3, c4, c5 = feats[1], feats[2], feats[3]
+        cs = [c3, c4, c5]
+        self.lat[2](c5, out=self.lat_buf[2])
+        self.outc[2](self.lat_buf[2], out=self.p[2])
+        for i in (1, 0):
+            upsample2x_nhwc(self.lat_buf[i + 1], self.up_buf[i])
+            self.lat[i](cs[i], out=self.lat_buf[i], res=self.up_buf[i])
+            self.outc[i](self.lat_buf[i], out=self.p[i])
+        src6 = c5 if self.p6p7_from_c5 else self.p[2]
+        self.p6(src6, out=self.p[3])
+        self.p6r(src6, out=self.p6relu)
+        self.p7(self.p6relu, out=self.p[4])
+        C = self.cfg.fpn_channels
+        outs = []
+        for lv, p in zip(self.lvl, self.p):
+            f = self.t_first(p, out=lv["first"])
+            if self.fcos:
+                g, b = self.gn_params[0]
+                self._gn(f, g, b, 2 * self.gn_groups)  # both towers at once: 512 channels, 64 groups of 8
+            c_in, b_in = NHWC(f.t, 0, C), NHWC(f.t, C, C)
+            cbuf, bbuf = (lv["a"], lv["b"]), (lv["c"], lv["d"])
+            for k, (cc, cb) in enumerate(zip(self.t_cls, self.t_box)):
+                c_in = cc(c_in, out=cbuf[k % 2])
+                b_in = cb(b_in, out=bbuf[k % 2])
+                if self.fcos:
+                    (gc, bc), (gb, bb2) = self.gn_params[k + 1]
+                    self._gn(c_in, gc, bc)
+                    self._gn(b_in, gb, bb2)
+            self.cls_score(c_in, out=lv["cls"])
+            self.box_pred(b_in, out=lv["box"])
+            if self.fcos:
+                outs.append((NHWC(lv["cls"].t, 0, self.cfg.num_classes), NHWC(lv["box"].t, 0, 4),
+                             NHWC(lv["box"].t, 4, 1)))
+            else:
+                outs.append((NHWC(lv["cls"].t, 0, self.cfg.num_anchors * self.cfg.num_classes),
+                             NHWC(lv["box"].t, 0, self.cfg.num_anchors * 4)))
+        return outs

@@ -48,12 +48,13 @@ def _ceil(x, m):
 
 class FusedConv:
     def __init__(self, conv: nn.Module, act: int = ACT_NONE, device="cuda", cin_pad: Optional[int] = None,
-                 cout_pad: Optional[int] = None):
+                 cout_pad: Optional[int] = None, post_res: bool = False):
         w = conv.weight.detach().float()
         b = conv.bias.detach().float() if conv.bias is not None else None
         self.transpose = isinstance(conv, nn.ConvTranspose2d)
         self.device = torch.device(device)
         self.act = act
+        self.post_res = post_res  # act(conv + residual): ResNet bottleneck output
         if self.transpose:
             cin, cout, kh, kw = w.shape
             s = conv.stride[0]
@@ -116,7 +117,8 @@ class FusedConv:
         gh, gw = (H, W) if self.transpose else (Ho, Wo)
         _native.call("tca_conv_nhwc", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                      _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
-                     self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, self.act,
+                     self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off,
+                     self.act | (16 if (self.post_res and res is not None) else 0),
                      _native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
                      res.off if res is not None else 0, self.shuffle, tile, _native.stream_ptr(stream))
         return out
@@ -127,9 +129,12 @@ class FusedConv:
             y = F.conv_transpose2d(xi, self.w_f32, self.b_f32, stride=self.shuffle)
         else:
             y = F.conv2d(xi, self.w_f32, self.b_f32, stride=self.s, padding=self.p)
-        y = apply_act(y, self.act)
-        if res is not None:
-            y = y + res.nchw().float()[:, : y.shape[1]]
+        if res is not None and self.post_res:
+            y = apply_act(y + res.nchw().float()[:, : y.shape[1]], self.act)
+        else:
+            y = apply_act(y, self.act)
+            if res is not None:
+                y = y + res.nchw().float()[:, : y.shape[1]]
         out.tensor()[..., : y.shape[1]].copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
         return out
 
@@ -143,6 +148,19 @@ def maxpool_nhwc(x: NHWC, out: NHWC, k: int = 5, stream=None) -> NHWC:
         return out
     _native.call("tca_maxpool_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, k, _native.ptr(out.t),
                  out.t.shape[-1], out.off, _native.stream_ptr(stream))
+    return out
+
+
+def maxpool2d_nhwc(x: NHWC, out: NHWC, k: int = 3, s: int = 2, p: int = 1, stream=None) -> NHWC:
+    """k x k max-pool with stride / padding (ResNet stem), slice → slice; out holds Ho x Wo."""
+    B, H, W, C = x.shape
+    Ho, Wo = out.shape[1], out.shape[2]
+    if x.t.device.type != "cuda":
+        y = F.max_pool2d(x.nchw().float(), k, s, p)
+        out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
+        return out
+    _native.call("tca_maxpool2d_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, k, s, p,
+                 _native.ptr(out.t), Ho, Wo, out.t.shape[-1], out.off, _native.stream_ptr(stream))
     return out
 
 

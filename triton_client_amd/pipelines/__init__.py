@@ -4,3 +4,4 @@ from .camera import CameraPipeline  # noqa: F401
 from .lidar import LidarPipeline  # noqa: F401
 from .graph import GraphRunner  # noqa: F401
 from .centerpoint import CenterPointPipeline  # noqa: F401,E402
+from .detectron import DetectronPipeline  # noqa: F401,E402

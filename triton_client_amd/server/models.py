@@ -309,3 +309,80 @@ class CenterPointModel(ServedModel):
             pp = CenterPointPostprocess(self.cfg, 1, [16 * t for t in range(len(mo))], "cpu", self.class_thresh)
             out = pp(head.permute(0, 2, 3, 1)).per_image()[0]
         return out
+
+
+class DetectronModel(ServedModel):
+    """Detectron2 RetinaNet / FCOS with the reference's served contract
+    (``examples/RetinaNet_detectron/config.pbtxt``): input ``input__00`` FP32 NCHW
+    [3, 640, 480] RGB 0..255 (the model normalises), outputs ``bboxex__0`` FP32
+    [-1, 4] (xyxy, input pixels), ``classes__1`` INT64 [-1], ``scores__2`` FP32
+    [-1], ``dims__3`` INT64 [1, 2] (input H, W).  GPU: ResNet-50-FPN + head on
+    the fused MFMA convs, decode / per-level top-k / merge / NMS kernels."""
+
+    platform = "pytorch_libtorch"
+
+    def __init__(self, name: str = "test_model", arch: str = "retinanet", hw=(640, 480), nc: int = 80,
+                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 300.0):
+        from ..config.detectron import DetectronConfig
+
+        super().__init__(name)
+        self.cfg = DetectronConfig(arch=arch, input_hw=tuple(hw), num_classes=nc)
+        self.device = _device(device)
+        self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+
+    def inputs(self):
+        H, W = self.cfg.input_hw
+        return [tensor_spec("input__00", "FP32", [3, H, W], fmt="NCHW")]
+
+    def outputs(self):
+        return [tensor_spec("bboxex__0", "FP32", [-1, 4], output=True),
+                tensor_spec("classes__1", "INT64", [-1], output=True),
+                tensor_spec("scores__2", "FP32", [-1], output=True),
+                tensor_spec("dims__3", "INT64", [1, 2], output=True)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_GPU if self.device.type == "cuda" else mc.ModelInstanceGroup.KIND_CPU
+
+    def load(self):
+        from ..models.common import fuse_model
+        from ..models.detectron import build_detectron
+
+        model = build_detectron(self.cfg, self.seed)
+        if self.weights:
+            model.load_state_dict(torch.load(self.weights, map_location="cpu", weights_only=True))
+        if self.device.type == "cuda":
+            from ..pipelines.detectron import DetectronPipeline
+            from ..utils.synthetic import camera_frame
+
+            H, W = self.cfg.input_hw
+            self.pipe = DetectronPipeline(model, batch=1, src_hw=(H, W), device=self.device, mode="stretch")
+            if not self.weights:
+                self.pipe.frames[0].copy_(torch.from_numpy(camera_frame(H, W, self.seed)))
+                self.pipe.calibrate_detection_density(self.calibrate_target)
+            self.model = self.pipe.model
+        else:
+            self.model = fuse_model(model.eval())
+        self.ready = True
+
+    @torch.no_grad()
+    def execute(self, inputs, requested):
+        H, W = self.cfg.input_hw
+        x = np.require(inputs["input__00"], np.float32, ["C", "W"]).reshape(1, 3, H, W)
+        if self.device.type == "cuda":
+            p = self.pipe
+            f = p.fast or p.build_fast()
+            xt = torch.from_numpy(x).to(self.device, non_blocking=True)
+            mean = torch.tensor(self.cfg.pixel_mean, device=self.device).view(1, 3, 1, 1)
+            std = torch.tensor(self.cfg.pixel_std, device=self.device).view(1, 3, 1, 1)
+            f.x.t.zero_()
+            f.x.t[..., :3].copy_(((xt - mean) / std).permute(0, 2, 3, 1))
+            res = p.post(f.forward()).per_image()[0]
+        else:
+            from ..models.detectron import decode_reference
+
+            bx, sc, cl = decode_reference(self.model(torch.from_numpy(x)), self.cfg)[0]
+            res = {"box": bx, "score": sc, "cls": cl}
+        return {"bboxex__0": np.asarray(res["box"], np.float32).reshape(-1, 4),
+                "classes__1": np.asarray(res["cls"]).astype(np.int64),
+                "scores__2": np.asarray(res["score"], np.float32),
+                "dims__3": np.array([[H, W]], np.int64)}

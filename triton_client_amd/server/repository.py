@@ -54,6 +54,13 @@ def _centerpoint(name):
     return f
 
 
+def _detectron(name, arch, nc=80):
+    def f(device="auto", **kw):
+        from .models import DetectronModel
+        return DetectronModel(name, arch=arch, nc=nc, device=device, **kw)
+    return f
+
+
 FACTORIES: Dict[str, Factory] = {
     "YOLOv5nCOCO": _yolo("YOLOv5nCOCO", "n", 80, 640),
     "YOLOv5n": _yolo("YOLOv5n", "n", 80, 640),
@@ -62,6 +69,10 @@ FACTORIES: Dict[str, Factory] = {
     "pointpillar_kitti": _pointpillars("pointpillar_kitti"),
     "pointpillar_python": _pointpillars("pointpillar_python"),
     "centerpoint_pp": _centerpoint("centerpoint_pp"),
+    "test_model": _detectron("test_model", "retinanet"),  # examples/RetinaNet_detectron/config.pbtxt
+    "RetinaNet_detectron": _detectron("RetinaNet_detectron", "retinanet"),
+    "FCOS_detectron": _detectron("FCOS_detectron", "fcos"),
+    "fcos_weed_detector": _detectron("fcos_weed_detector", "fcos", 2),  # main.py:75 (weeds, maize)
     "centerpoint": _centerpoint("centerpoint"),
     "echo": lambda device="auto", **kw: EchoModel("echo"),
 }
