@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
     ap.add_argument("--only", choices=["both", "camera", "lidar"], default="both")
-    ap.add_argument("--camera-model", choices=["yolov5n", "retinanet", "fcos"], default="yolov5n",
+    ap.add_argument("--camera-model", choices=["yolov5n", "yolov4", "retinanet", "fcos"], default="yolov5n",
                     help="2D detector: YOLOv5n-640 (headline) or Detectron2 RetinaNet / FCOS R50-FPN at 800x1344")
     ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint"], default="pointpillars",
                     help="3D detector: PointPillars KITTI (headline) or CenterPoint-PP nuScenes")
@@ -89,8 +89,11 @@ def main():
     use_lid = args.only in ("both", "lidar")
 
     torch.manual_seed(0)
-    det2 = args.camera_model != "yolov5n"
-    if use_cam and det2:
+    det2 = args.camera_model in ("retinanet", "fcos")
+    if use_cam and args.camera_model == "yolov4":
+        from triton_client_amd.pipelines import Yolov4Pipeline
+        cam = Yolov4Pipeline(batch=B, src_hw=(H0, W0), img=512, device=dev)
+    elif use_cam and det2:
         from triton_client_amd.config.detectron import DetectronConfig
         from triton_client_amd.pipelines import DetectronPipeline
         cam = DetectronPipeline(batch=B, src_hw=(H0, W0), cfg=DetectronConfig(arch=args.camera_model), device=dev)
@@ -280,7 +283,8 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(info, elapsed)
 
-    cam_name = {"yolov5n": "YOLOv5n-640 (COCO, 80 cls)", "retinanet": "RetinaNet R50-FPN 800x1344 (COCO)",
+    cam_name = {"yolov5n": "YOLOv5n-640 (COCO, 80 cls)", "yolov4": "YOLOv4-512 (COCO, 80 cls)",
+                "retinanet": "RetinaNet R50-FPN 800x1344 (COCO)",
                 "fcos": "FCOS R50-FPN 800x1344 (COCO)"}[args.camera_model]
     if info.is_main:
         frames = info.world * B * args.steps

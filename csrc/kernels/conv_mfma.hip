@@ -45,7 +45,7 @@ struct ConvArgs {
   int Ho, Wo, KH, KW, S, P;
   int N, K, Kp;
   int ldo, co_off, ldr, r_off;
-  int act;          // 0 none, 1 relu, 2 silu, 3 leaky(0.1)
+  int act;          // 0 none, 1 relu, 2 silu, 3 leaky(0.1), 4 mish; | 16: act after the residual add
   int shuffle;      // >0: transpose-conv pixel shuffle factor s (N = s*s*Cout_real)
   int M;            // B*Ho*Wo
 };
@@ -55,6 +55,11 @@ __device__ __forceinline__ float act_fn(float v, int act) {
     case 1: return fmaxf(v, 0.f);
     case 2: return v / (1.f + __expf(-v));
     case 3: return v > 0.f ? v : 0.1f * v;
+    case 4: {  // mish: v * tanh(softplus(v)); tanh(log(1+e^v)) = (e^2v + 2e^v) / (e^2v + 2e^v + 2)
+      if (v > 20.f) return v;
+      const float e = __expf(v), n = e * (e + 2.f);
+      return v * n / (n + 2.f);
+    }
     default: return v;
   }
 }

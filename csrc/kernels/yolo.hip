@@ -183,3 +183,119 @@ TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const v
   }
   TCA_LAUNCH_CHECK();
 }
+
+// ============================================================================
+// K5 — YOLOv4 head decode (reference tools/yolo_layer.py:148-288,
+// yolo_forward_dynamic) fused with the post-processing filter
+// (tools/utils.py:166-233: max/argmax over conf = sigmoid(cls) * sigmoid(obj),
+// conf > thresh).  One thread per (image, row) with rows anchor-major (a, y, x)
+// per level, levels at strides 8/16/32 — the [B, N, ...] order of the
+// reference's ONNX outputs.  Writes:
+//   * optional full outputs: boxes [B, N, 4] normalised x1y1x2y2 and confs
+//     [B, N, nc] (examples/YOLOv4/config.pbtxt outputs `boxes` / `confs`);
+//   * candidates (max conf > thresh) in model-input pixels, compacted per image.
+// ============================================================================
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) yolov4_decode_kernel(YoloHeads hd, int batch, int nc, float sxy,
+                                                            float conf_thres, int img_h, int img_w,
+                                                            float* __restrict__ out_boxes, float* __restrict__ out_confs,
+                                                            float* __restrict__ cand_box, float* __restrict__ cand_score,
+                                                            int* __restrict__ cand_cls, uint64_t* __restrict__ cand_key,
+                                                            int* __restrict__ cand_count, int cap) {
+  __shared__ int s_cnt, s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n0 = 3 * hd.h[0] * hd.w[0], n1 = n0 + 3 * hd.h[1] * hd.w[1], N = n1 + 3 * hd.h[2] * hd.w[2];
+  bool pass = false;
+  float best = 0.f, box[4];
+  int best_c = 0;
+  if (n < N) {
+    const int l = n < n0 ? 0 : (n < n1 ? 1 : 2);
+    const int r = n - (l == 0 ? 0 : (l == 1 ? n0 : n1));
+    const int H = hd.h[l], W = hd.w[l], HW = H * W;
+    const int a = r / HW, yx = r - a * HW, y = yx / W, x = yx - y * W;
+    const T* hp = reinterpret_cast<const T*>(hd.head[l]) + ((long)b * HW + yx) * hd.ldc[l] + a * (5 + nc);
+    const float bx = (sigmoidf_(to_f32(hp[0])) * sxy - 0.5f * (sxy - 1.f) + (float)x) / (float)W;
+    const float by = (sigmoidf_(to_f32(hp[1])) * sxy - 0.5f * (sxy - 1.f) + (float)y) / (float)H;
+    const float bw = __expf(to_f32(hp[2])) * hd.anchor[l][a][0] / (float)W;
+    const float bh = __expf(to_f32(hp[3])) * hd.anchor[l][a][1] / (float)H;
+    box[0] = bx - 0.5f * bw;
+    box[1] = by - 0.5f * bh;
+    box[2] = box[0] + bw;
+    box[3] = box[1] + bh;
+    const float obj = sigmoidf_(to_f32(hp[4]));
+    const long row = (long)b * N + n;
+    if (out_boxes) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) out_boxes[row * 4 + k] = box[k];
+    }
+    float m = -INFINITY;
+    for (int c = 0; c < nc; ++c) {
+      const float v = to_f32(hp[5 + c]);
+      if (out_confs) out_confs[row * nc + c] = sigmoidf_(v) * obj;
+      if (v > m) { m = v; best_c = c; }
+    }
+    best = sigmoidf_(m) * obj;
+    pass = best > conf_thres;
+  }
+  int my = -1;
+  if (pass) my = atomicAdd(&s_cnt, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&cand_count[b], s_cnt) : 0;
+  __syncthreads();
+  if (pass) {
+    const int slot = s_base + my;
+    if (slot < cap) {
+      const long o = (long)b * cap + slot;
+      cand_box[o * 4 + 0] = box[0] * img_w; cand_box[o * 4 + 1] = box[1] * img_h;
+      cand_box[o * 4 + 2] = box[2] * img_w; cand_box[o * 4 + 3] = box[3] * img_h;
+      cand_score[o] = best;
+      cand_cls[o] = best_c;
+      cand_key[o] = make_score_key(best, (uint32_t)n);
+    }
+  }
+}
+
+}  // namespace
+
+// heads: three NHWC slices with channel strides ldc[3] (>= 3*(5+nc)); anchors [3][3][2]
+// already divided by the level stride (masked anchors / stride, yolo_layer.py:318).
+TCA_API int tca_yolov4_decode(const void* head0, const void* head1, const void* head2, int dtype, int batch, int nc,
+                              const int* hw /*[6]*/, const int* ldc /*[3]*/, const float* anchors /*[3][3][2]*/,
+                              float scale_x_y, float conf_thres, int img_h, int img_w, float* out_boxes,
+                              float* out_confs, float* cand_box, float* cand_score, int* cand_cls, uint64_t* cand_key,
+                              int* cand_count, int cap, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  YoloHeads hd;
+  hd.head[0] = head0; hd.head[1] = head1; hd.head[2] = head2;
+  for (int l = 0; l < 3; ++l) {
+    hd.h[l] = hw[2 * l]; hd.w[l] = hw[2 * l + 1]; hd.stride[l] = 0; hd.ldc[l] = ldc[l];
+    for (int a = 0; a < 4; ++a) {
+      hd.anchor[l][a][0] = a < 3 ? anchors[(l * 3 + a) * 2] : 0.f;
+      hd.anchor[l][a][1] = a < 3 ? anchors[(l * 3 + a) * 2 + 1] : 0.f;
+    }
+  }
+  int e = zero_i32_async(cand_count, batch, stream);
+  if (e) return e;
+  long N = 0;
+  for (int l = 0; l < 3; ++l) N += 3L * hd.h[l] * hd.w[l];
+  dim3 grid((unsigned)((N + 255) / 256), (unsigned)batch);
+  switch (dtype) {
+    case kF32:
+      yolov4_decode_kernel<float><<<grid, 256, 0, stream>>>(hd, batch, nc, scale_x_y, conf_thres, img_h, img_w,
+                                                            out_boxes, out_confs, cand_box, cand_score, cand_cls,
+                                                            cand_key, cand_count, cap);
+      break;
+    case kBF16:
+      yolov4_decode_kernel<__hip_bfloat16><<<grid, 256, 0, stream>>>(hd, batch, nc, scale_x_y, conf_thres, img_h,
+                                                                     img_w, out_boxes, out_confs, cand_box, cand_score,
+                                                                     cand_cls, cand_key, cand_count, cap);
+      break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  TCA_LAUNCH_CHECK();
+}

@@ -164,3 +164,33 @@ def test_detectron_served_contract(cuda):
         d = eng.detect([camera_frame(480, 640, 3)])[0]
         assert d.shape[1] == 6 and len(d) > 0
         ch.close()
+
+
+def test_reference_model_repository_families():
+    """Every config.pbtxt of the reference maps to a served model family with the
+    same tensor contract (no model is loaded)."""
+    import os
+    import shutil
+    import tempfile
+    from triton_client_amd.server.repository import ModelRepository
+    root = tempfile.mkdtemp()
+    try:
+        for d, f in (("YOLOv5nCROP", "examples/YOLOv5/config.pbtxt"), ("YOLOv4", "examples/YOLOv4/config.pbtxt"),
+                     ("test_model", "examples/RetinaNet_detectron/config.pbtxt"),
+                     ("pointpillar_kitti", "examples/pointpillar_kitti/config.pbtxt")):
+            src = os.path.join("/root/reference", f)
+            if not os.path.exists(src):
+                pytest.skip("reference configs not mounted")
+            os.makedirs(os.path.join(root, d))
+            shutil.copy(src, os.path.join(root, d, "config.pbtxt"))
+        repo = ModelRepository.from_directory(root, device="cpu", load=False)
+        by = {m.name: m for m in repo.models()}
+        assert type(by["YOLOv4"]).__name__ == "YoloV4Model"
+        assert [o.name for o in by["YOLOv4"].config().output] == ["confs", "boxes"]
+        assert list(by["YOLOv4"].config().output[0].dims) == [1, 16128, 80]
+        assert type(by["test_model"]).__name__ == "DetectronModel"
+        assert list(by["test_model"].config().input[0].dims) == [3, 640, 480]
+        assert [o.name for o in by["test_model"].config().output] == ["bboxex__0", "classes__1", "scores__2", "dims__3"]
+        assert type(by["pointpillar_kitti"]).__name__ == "PointPillarsModel"
+    finally:
+        shutil.rmtree(root)

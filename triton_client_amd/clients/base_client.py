@@ -65,5 +65,8 @@ def client_for_model(model_name: str, model_config=None) -> Client:
     if "fcos" in n or "retina" in n or "detectron" in n or n == "test_model" or outs == 4:
         from .detectron_client import FCOS_client
         return FCOS_client()
+    if "yolov4" in n or outs == 2:
+        from .yolov4_client import Yolov4client
+        return Yolov4client()
     from .yolov5_client import Yolov5client
     return Yolov5client()

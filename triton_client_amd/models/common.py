@@ -21,8 +21,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-ACT_NONE, ACT_RELU, ACT_SILU, ACT_LEAKY = 0, 1, 2, 3
-_ACT_NAMES = {"none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU, "leaky": ACT_LEAKY}
+ACT_NONE, ACT_RELU, ACT_SILU, ACT_LEAKY, ACT_MISH = 0, 1, 2, 3, 4
+_ACT_NAMES = {"none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU, "leaky": ACT_LEAKY, "mish": ACT_MISH,
+              "linear": ACT_NONE}
 
 
 def seed_everything(seed: int = 0) -> None:
@@ -36,6 +37,8 @@ def apply_act(x: torch.Tensor, act: int) -> torch.Tensor:
         return F.silu(x)
     if act == ACT_LEAKY:
         return F.leaky_relu(x, 0.1)
+    if act == ACT_MISH:
+        return F.mish(x)
     return x
 
 

@@ -17,7 +17,7 @@ neck's three up-sampled scales), so no concat kernel ever runs.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
@@ -475,3 +475,132 @@ class FastDetectron:
                 outs.append((NHWC(lv["cls"].t, 0, self.cfg.num_anchors * self.cfg.num_classes),
                              NHWC(lv["box"].t, 0, self.cfg.num_anchors * 4)))
         return outs
+
+
+class FastGraph:
+    """A darknet-style layer graph (``model.spec``: conv / route / add / maxpool /
+    upsample, e.g. :data:`~.yolov4.YOLOV4_SPEC`) on the fused NHWC convs.
+
+    * route (concat) buffers are allocated once and each source writes straight
+      into its channel slice (a source feeding a second route is copied);
+    * ``add`` of a conv output that nothing else reads is fused into that conv's
+      epilogue (residual), so residual blocks cost one launch per conv;
+    * maxpool / upsample read and write channel slices.
+    Input: ``x`` [B, H, W, 8] (RGB + zero pad, written by K1).
+    """
+
+    IN_CHANNELS = 8
+
+    def __init__(self, model, batch: int, img_hw, device="cuda", outputs: Sequence[str] = ()):
+        from ..ops.conv import FusedConv
+
+        self.device = torch.device(device)
+        B = self.B = batch
+        H, W = img_hw
+        spec, layers = model.spec, model.layers
+        bufs = self.bufs = _Buffers(self.device)
+        shape = {"input": (H, W)}
+        chan = {"input": self.IN_CHANNELS}
+        consumers: dict = {}
+        for name, op, a in spec:
+            srcs = a["srcs"] if op == "route" else ([a["a"], a["b"]] if op == "add" else [a["src"]])
+            for s in srcs:
+                consumers.setdefault(s, []).append(name)
+            if op == "conv":
+                k, st = a["k"], a["s"]
+                h, w = shape[a["src"]]
+                shape[name] = ((h + 2 * (k // 2) - k) // st + 1, (w + 2 * (k // 2) - k) // st + 1)
+                chan[name] = _ceil8(a["c"])
+            elif op == "route":
+                shape[name] = shape[a["srcs"][0]]
+                chan[name] = sum(chan[s] for s in a["srcs"])
+            elif op == "add":
+                shape[name], chan[name] = shape[a["a"]], chan[a["a"]]
+            elif op == "upsample":
+                h, w = shape[a["src"]]
+                shape[name], chan[name] = (2 * h, 2 * w), chan[a["src"]]
+            else:
+                shape[name], chan[name] = shape[a["src"]], chan[a["src"]]
+        # fused adds: conv output read only by the add → the conv writes the add's value
+        fused_add = {}
+        for name, op, a in spec:
+            if op == "add":
+                c = next((x for x in spec if x[0] == a["a"]), None)
+                if c is not None and c[1] == "conv" and consumers.get(a["a"]) == [name]:
+                    fused_add[a["a"]] = (name, a["b"])
+        # buffers: route slices first
+        self.view = {"input": None}
+        slot = {}
+        for name, op, a in spec:
+            if op == "route":
+                h, w = shape[name]
+                rb = bufs.new(B, h, w, chan[name])
+                self.view[name] = rb
+                off = 0
+                for s in a["srcs"]:
+                    src_name = s
+                    if s not in slot:
+                        slot[s] = NHWC(rb.t, off, chan[s])
+                    else:
+                        slot[(name, s)] = NHWC(rb.t, off, chan[s])  # needs a copy
+                    off += chan[s]
+        self.x = bufs.new(B, H, W, self.IN_CHANNELS)
+        self.view["input"] = self.x
+        self.ops = []
+        for name, op, a in spec:
+            if op == "route":
+                for s in a["srcs"]:
+                    if (name, s) in slot:
+                        self.ops.append(("copy", (name, s), s))
+                continue
+            target = name
+            if op == "conv" and name in fused_add:
+                target = fused_add[name][0]
+            if op == "add" and name in [v[0] for v in fused_add.values()]:
+                continue  # produced by its conv
+            if target not in self.view:
+                h, w = shape[target]
+                self.view[target] = slot.get(target) or bufs.new(B, h, w, chan[target])
+            if op == "conv":
+                m = layers[name]
+                assert m.fused, "call fuse_model() first"
+                fc = FusedConv(m.conv, act=m.act, device=device,
+                               cin_pad=self.IN_CHANNELS if a["src"] == "input" else None)
+                res = fused_add[name][1] if name in fused_add else None
+                self.ops.append(("conv", fc, a["src"], target, res))
+            elif op == "add":
+                self.ops.append(("add", a["a"], a["b"], name))
+            elif op == "maxpool":
+                self.ops.append(("maxpool", a["src"], name, a["k"]))
+            elif op == "upsample":
+                self.ops.append(("upsample", a["src"], name))
+        for k, v in list(slot.items()):
+            if isinstance(k, tuple):
+                self.view[k] = v
+        self.outputs = list(outputs)
+
+    def input_view(self) -> torch.Tensor:
+        return self.x.t.permute(0, 3, 1, 2)
+
+    def forward(self):
+        from ..ops.conv import maxpool_nhwc, upsample2x_nhwc
+
+        v = self.view
+        for op in self.ops:
+            kind = op[0]
+            if kind == "conv":
+                _, fc, src, dst, res = op
+                fc(v[src], out=v[dst], res=v[res] if res is not None else None)
+            elif kind == "maxpool":
+                maxpool_nhwc(v[op[1]], v[op[2]], op[3])
+            elif kind == "upsample":
+                upsample2x_nhwc(v[op[1]], v[op[2]])
+            elif kind == "add":
+                v[op[3]].tensor().copy_(v[op[1]].tensor() + v[op[2]].tensor())
+            elif kind == "copy":
+                v[op[1]].tensor().copy_(v[op[2]].tensor())
+        return [v[n] for n in self.outputs]
+
+
+def _ceil8(c):
+    return (c + 7) // 8 * 8

@@ -5,3 +5,4 @@ from .lidar import LidarPipeline  # noqa: F401
 from .graph import GraphRunner  # noqa: F401
 from .centerpoint import CenterPointPipeline  # noqa: F401,E402
 from .detectron import DetectronPipeline  # noqa: F401,E402
+from .yolov4 import Yolov4Pipeline  # noqa: F401,E402

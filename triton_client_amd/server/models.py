@@ -386,3 +386,70 @@ class DetectronModel(ServedModel):
                 "classes__1": np.asarray(res["cls"]).astype(np.int64),
                 "scores__2": np.asarray(res["score"], np.float32),
                 "dims__3": np.array([[H, W]], np.int64)}
+
+
+class YoloV4Model(ServedModel):
+    """``YOLOv4`` (examples/YOLOv4/config.pbtxt): input ``input`` FP32 NCHW
+    [3, 512, 512] (reshape [1, 3, 512, 512], RGB / 255); outputs ``confs`` FP32
+    [1, N, 80] and ``boxes`` FP32 [1, N, 1, 4] (normalised x1y1x2y2) with
+    N = 16128 — what the reference's ONNX export (decode inside) returns.  GPU:
+    CSPDarknet53-SPP-PANet on the fused convs + the K5 decode kernel."""
+
+    platform = "onnxruntime_onnx"
+
+    def __init__(self, name: str = "YOLOv4", nc: int = 80, img: int = 512, device="auto",
+                 weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0):
+        super().__init__(name)
+        self.nc, self.img = nc, img
+        self.device = _device(device)
+        self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+        from ..models.yolov4 import YoloV4Config
+        self.N = YoloV4Config(nc=nc, img=(img, img)).num_predictions()
+
+    def inputs(self):
+        return [tensor_spec("input", "FP32", [3, self.img, self.img], fmt="NCHW", reshape=[1, 3, self.img, self.img])]
+
+    def outputs(self):
+        return [tensor_spec("confs", "FP32", [1, self.N, self.nc], output=True),
+                tensor_spec("boxes", "FP32", [1, self.N, 1, 4], output=True)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_GPU if self.device.type == "cuda" else mc.ModelInstanceGroup.KIND_CPU
+
+    def load(self):
+        from ..models.common import fuse_model
+        from ..models.yolov4 import build_yolov4
+
+        model = build_yolov4(self.nc, self.img, self.seed)
+        if self.weights:
+            model.load_state_dict(torch.load(self.weights, map_location="cpu", weights_only=True))
+        if self.device.type == "cuda":
+            from ..pipelines.yolov4 import Yolov4Pipeline
+            from ..utils.synthetic import camera_frame
+
+            self.pipe = Yolov4Pipeline(model, batch=1, src_hw=(self.img, self.img), img=self.img, nc=self.nc,
+                                       device=self.device)
+            if not self.weights:
+                self.pipe.frames[0].copy_(torch.from_numpy(camera_frame(self.img, self.img, self.seed)))
+                self.pipe.calibrate_detection_density(self.calibrate_target)
+            self.model = self.pipe.model
+        else:
+            self.model = fuse_model(model.eval())
+        self.ready = True
+
+    @torch.no_grad()
+    def execute(self, inputs, requested):
+        x = np.require(inputs["input"], np.float32, ["C", "W"]).reshape(1, 3, self.img, self.img)
+        if self.device.type == "cuda":
+            p = self.pipe
+            f = p.fast or p.build_fast()
+            f.x.t.zero_()
+            f.x.t[..., :3].copy_(torch.from_numpy(x).to(self.device).permute(0, 2, 3, 1))
+            _, boxes, confs = p.post(f.forward(), full=True)
+            boxes, confs = boxes.cpu().numpy(), confs.cpu().numpy()
+        else:
+            from ..models.yolov4 import decode_reference
+
+            b, c = decode_reference(self.model(torch.from_numpy(x)), self.nc)
+            boxes, confs = b.numpy(), c.numpy()
+        return {"confs": confs.astype(np.float32, copy=False), "boxes": boxes.astype(np.float32, copy=False)}

@@ -34,6 +34,8 @@ def _pointpillars(name):
 
 def _family(name: str) -> Optional[str]:
     n = name.lower()
+    if "yolov4" in n:
+        return "yolov4"
     if "yolo" in n or "weed" in n:
         return "yolo"
     if "pointpillar" in n or "pillar" in n:
@@ -61,6 +63,13 @@ def _detectron(name, arch, nc=80):
     return f
 
 
+def _yolov4(name, nc=80, img=512):
+    def f(device="auto", **kw):
+        from .models import YoloV4Model
+        return YoloV4Model(name, nc, img, device=device, **kw)
+    return f
+
+
 FACTORIES: Dict[str, Factory] = {
     "YOLOv5nCOCO": _yolo("YOLOv5nCOCO", "n", 80, 640),
     "YOLOv5n": _yolo("YOLOv5n", "n", 80, 640),
@@ -69,6 +78,7 @@ FACTORIES: Dict[str, Factory] = {
     "pointpillar_kitti": _pointpillars("pointpillar_kitti"),
     "pointpillar_python": _pointpillars("pointpillar_python"),
     "centerpoint_pp": _centerpoint("centerpoint_pp"),
+    "YOLOv4": _yolov4("YOLOv4"),  # examples/YOLOv4/config.pbtxt
     "test_model": _detectron("test_model", "retinanet"),  # examples/RetinaNet_detectron/config.pbtxt
     "RetinaNet_detectron": _detectron("RetinaNet_detectron", "retinanet"),
     "FCOS_detectron": _detectron("FCOS_detectron", "fcos"),
@@ -155,9 +165,22 @@ class ModelRepository:
                 out = list(cfg.output[0].dims)
                 from .models import YoloV5Model
                 m = YoloV5Model(name, "n", out[-1] - 5, dims[-1], device=device)
+            elif fam == "yolov4" or (len(cfg.output) == 2 and {o.name for o in cfg.output} == {"confs", "boxes"}):
+                from .models import YoloV4Model
+                dims = list(cfg.input[0].dims)
+                nc = int(list(cfg.output[0].dims)[-1]) if cfg.output[0].name == "confs" else 80
+                m = YoloV4Model(name, nc, dims[-1], device=device)
+            elif fam == "detectron" or len(cfg.output) == 4:
+                from .models import DetectronModel
+                dims = list(cfg.input[0].dims)
+                m = DetectronModel(name, "fcos" if "fcos" in name.lower() else "retinanet", tuple(dims[-2:]),
+                                   device=device)
             elif fam == "pointpillars":
                 from .models import PointPillarsModel
                 m = PointPillarsModel(name, device=device)
+            elif fam == "centerpoint":
+                from .models import CenterPointModel
+                m = CenterPointModel(name, device=device)
             else:
                 continue
             repo.add(m, load=load)
