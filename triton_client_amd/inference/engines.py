@@ -397,8 +397,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         # model declares an explicit batch dimension
         self.batch_dim = len(self.model_metadata.inputs[0].shape) == 4
         # the reference requests all 4 outputs of a Detectron model, else the first one
-        # (ros_inference.py:70-87)
-        self.requested = list(self.output_names) if len(self.output_names) == 4 else list(self.output_names[:1])
+        # (ros_inference.py:70-87); YOLOv4's two outputs (confs, boxes) are both needed
+        self.requested = list(self.output_names)
         ch = channel
         if ch.input is not None:
             ch.input.name, ch.input.datatype = self.input_name, self.dtype
