@@ -1,0 +1,325 @@
+// K15 — fused BEV neck + anchor head (PointPillars / SECOND BaseBEVBackbone
+// deblocks + AnchorHeadSingle's three 1x1 convs; reference config
+// data/pointpillar.yaml:48-72 — UPSAMPLE_STRIDES [1, 2, 4], NUM_UPSAMPLE_FILTERS
+// [128, 128, 128]; head conv_cls / conv_box / conv_dir on the 384-channel concat).
+//
+// Unfused, the three transpose convs write a [B, H, W, 384] bf16 concat
+// (658 MB at batch 16 on the KITTI canvas) and the head reads it back: ~1.3 GB
+// of HBM traffic and four launches.  Here one workgroup owns 128 output pixels
+// that share a sub-pixel class (y mod S, x mod S), S = the largest upsample
+// stride.  Every branch's transpose conv is then ONE GEMM with a single weight
+// block (rows (y mod s_i, x mod s_i) of the k = s_i, stride s_i kernel) over
+// the branch input pixel (y / s_i, x / s_i); its ReLU'd accumulators are fed
+// straight back into the head GEMM as MFMA operands, never leaving registers:
+//
+//   acc1[i][j] (mfma 16x16x32 D layout) holds, in lane l, pixel (l & 15) and
+//   branch channels 16j + 4(l >> 4) + r.  A 32-deep operand fragment needs
+//   8 k values per lane group g = l >> 4; taking (acc1[2t][0..3], acc1[2t+1][0..3])
+//   gives channels {32t + 4g + r, 32t + 16 + 4g + r}.  The head weights are
+//   stored with each 32-channel chunk permuted the same way on the host
+//   (perm(8g + e) = e < 4 ? 4g + e : 16 + 4g + e - 4), so the contraction
+//   pairs matching channels.
+//
+// Persistent: one 512-thread workgroup per CU walks a contiguous range of
+// 256-pixel tiles (ranges split per XCD so the 16 class tiles of one pixel
+// panel share an L2); each of the 8 waves owns 32 pixels x all 128 channels of
+// a branch and its own 32 x 80 head tile (no cross-wave reduction).  Operands
+// are staged by global_load_lds in 64-channel K steps through two LDS stages;
+// the pipeline runs straight across tile boundaries (step g+1 of the flat
+// (tile, step) sequence is in flight while step g computes, one barrier per
+// step).  Each stage also carries the step's 128 deconv biases (so the K loop
+// issues no ordinary global load, which would make hipcc drain the DMA queue);
+// head weights and bias are loaded once per workgroup and stay in LDS.
+#include "tca_common.h"
+
+using namespace tca;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int MAXBR = 3;
+constexpr int CB = 128;   // output channels per branch
+constexpr int BM = 256;   // pixels per tile
+constexpr int NH = 80;    // head rows (72 padded to a multiple of 16)
+constexpr int NW = 8, NT = NW * 64;
+constexpr int ROWB = 128;  // 64 bf16 channels per staged row
+constexpr int A_BYTES = BM * ROWB, B_BYTES = CB * ROWB, BIAS_BYTES = CB * 4;
+constexpr int STAGE = A_BYTES + B_BYTES + BIAS_BYTES;
+constexpr int A_INS = BM / (8 * NW), B_INS = CB / (8 * NW);
+constexpr int NL = A_INS + B_INS + 1;  // glds per wave per step (+1: a 64-B piece of the biases)
+constexpr int WH_OFF = 2 * STAGE;
+constexpr int WH_BYTES = NH * ROWB * 2 * MAXBR;  // up to 6 64-channel blocks
+constexpr int BH_OFF = WH_OFF + WH_BYTES;
+constexpr int LDS_BYTES = BH_OFF + NH * 4;
+
+struct NeckArgs {
+  const __hip_bfloat16* x[MAXBR];  // branch inputs [B, H/s, W/s, ldx] (channels [offx, offx + cin))
+  int ldx[MAXBR], offx[MAXBR], cin[MAXBR], s[MAXBR];
+  const __hip_bfloat16* w[MAXBR];  // [s*s*CB, cin]: row (sy*s + sx)*CB + co
+  const float* bias[MAXBR];        // [s*s*CB]
+  const __hip_bfloat16* wh;        // [NH, nbr*CB], 32-chunk K-permuted
+  const float* bh;                 // [NH]
+  __hip_bfloat16* out;             // [B, H, W, ldo] (channels [0, nh))
+  int ldo, nh;
+  int B, H, W, S, nbr, nsteps, ntiles;
+};
+
+__device__ uint4 g_neck_zero_page[64];
+
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) void* gbl_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t)g, (lds_void_t)l, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+__device__ __forceinline__ int swz2(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
+  bf16x8 v;
+  v[0] = (__bf16)lo[0]; v[1] = (__bf16)lo[1]; v[2] = (__bf16)lo[2]; v[3] = (__bf16)lo[3];
+  v[4] = (__bf16)hi[0]; v[5] = (__bf16)hi[1]; v[6] = (__bf16)hi[2]; v[7] = (__bf16)hi[3];
+  return v;
+}
+
+struct Tile {
+  int b, cy, cx, q0;
+};
+
+__device__ __forceinline__ Tile tile_of(const NeckArgs& a, int t, int nqt) {
+  const int ncls = a.S * a.S;
+  const int cls = t % ncls, rest = t / ncls;
+  Tile r;
+  r.b = rest / nqt;
+  r.q0 = (rest - r.b * nqt) * BM;
+  r.cy = cls / a.S;
+  r.cx = cls - r.cy * a.S;
+  return r;
+}
+
+__global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, lslot = lane & 7;
+
+  const int S = a.S;
+  const int Wq = a.W / S, nq = (a.H / S) * Wq;
+  const int nqt = (nq + BM - 1) / BM;
+
+  // this workgroup's tiles: XCD x gets the contiguous range [T*x/8, T*(x+1)/8),
+  // walked by the XCD's G/8 workgroups with stride G/8
+  const int G = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = G >> 3;
+  const int t_lo = (int)((long)a.ntiles * xcd / 8), t_hi = (int)((long)a.ntiles * (xcd + 1) / 8);
+  const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + nslot - 1) / nslot : 0;
+  const int total = my_tiles * a.nsteps;
+
+  // resident head weights (64-channel blocks [NH rows][128 B], swizzled) + head bias
+  {
+    const int nins = a.nbr * 2 * (NH / 8);
+    const int ldw = a.nbr * CB;
+    for (int ins = wid; ins < nins; ins += NW) {
+      const int kb = ins / (NH / 8), r8 = ins - kb * (NH / 8);
+      const int row = r8 * 8 + lrow;
+      glds16(a.wh + (long)row * ldw + kb * 64 + (lslot ^ swz2(row)) * 8, smem + WH_OFF + kb * NH * ROWB + r8 * 1024);
+    }
+    if (wid == 0 && lane < NH / 4) glds16(a.bh + lane * 4, smem + BH_OFF);
+  }
+
+  // flat step g -> (tile, branch, chunk); the issue side walks it incrementally
+  int i_k = 0, i_br = 0, i_kc = 0;
+  Tile it = tile_of(a, t_lo + slot, nqt);
+  auto issue = [&](int buf) {
+    unsigned char* sa = smem + buf * STAGE;
+    unsigned char* sb = sa + A_BYTES;
+    unsigned char* sbias = sb + B_BYTES;
+    const int s = a.s[i_br], f = S / s;
+    const int Hi = a.H / s, Wi = a.W / s;
+    const int sy = it.cy / s, sx = it.cx / s;
+    const int ci0 = i_kc * 64;
+    const __hip_bfloat16* xb = a.x[i_br] + a.offx[i_br] + ci0;
+    const int ldx = a.ldx[i_br];
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int row = (wid * A_INS + j) * 8 + lrow;
+      const int q = it.q0 + row;
+      const void* g = g_neck_zero_page;
+      if (q < nq) {
+        const int Y = q / Wq, X = q - Y * Wq;
+        g = xb + (((long)it.b * Hi + Y * f + sy) * Wi + X * f + sx) * ldx + (lslot ^ swz2(row)) * 8;
+      }
+      glds16(g, sa + (wid * A_INS + j) * 1024);
+    }
+    const int sub = (it.cy % s) * s + (it.cx % s);
+    const __hip_bfloat16* wb = a.w[i_br] + (long)sub * CB * a.cin[i_br] + ci0;
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int row = (wid * B_INS + j) * 8 + lrow;
+      glds16(wb + (long)row * a.cin[i_br] + (lslot ^ swz2(row)) * 8, sb + (wid * B_INS + j) * 1024);
+    }
+    // biases: wave w stages floats [16w, 16w + 16) with lanes 0..3
+    if (lane < 4) glds16(a.bias[i_br] + sub * CB + wid * 16 + lane * 4, sbias + wid * 64);
+    if (++i_kc * 64 == a.cin[i_br]) {
+      i_kc = 0;
+      if (++i_br == a.nbr) {
+        i_br = 0;
+        ++i_k;
+        it = tile_of(a, t_lo + slot + i_k * nslot, nqt);
+      }
+    }
+  };
+
+  f32x4 acc1[2][8], acc2[2][NH / 16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  if (total > 0) issue(0);
+  int c_k = 0, c_br = 0, c_kc = 0;  // compute side
+  Tile ct = tile_of(a, t_lo + slot, nqt);
+  for (int g = 0; g < total; ++g) {
+    const int cur = g & 1;
+    wait_vmcnt0();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage g landed for every wave; every wave is done with g-1's buffer
+    asm volatile("" ::: "memory");
+    if (g + 1 < total) issue(cur ^ 1);
+
+    const unsigned char* sa = smem + cur * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[2], bfg[8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wid * 32 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = j * 16 + fr;
+        bfg[j] = *reinterpret_cast<const bf16x8*>(sb + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc1[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+
+    if (++c_kc * 64 != a.cin[c_br]) continue;
+    // ---- branch done: bias + ReLU, repack as operand fragments, head GEMM
+    c_kc = 0;
+    {
+      const float* bias = reinterpret_cast<const float*>(sb + B_BYTES);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc1[i][j][0] = fmaxf(acc1[i][j][0] + bv.x, 0.f);
+          acc1[i][j][1] = fmaxf(acc1[i][j][1] + bv.y, 0.f);
+          acc1[i][j][2] = fmaxf(acc1[i][j][2] + bv.z, 0.f);
+          acc1[i][j][3] = fmaxf(acc1[i][j][3] + bv.w, 0.f);
+        }
+      }
+      const unsigned char* wh = smem + WH_OFF + c_br * 2 * NH * ROWB;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        bf16x8 xf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) xf[i] = pack8(acc1[i][2 * t], acc1[i][2 * t + 1]);
+        const unsigned char* whb = wh + (t >> 1) * NH * ROWB;
+#pragma unroll
+        for (int u = 0; u < NH / 16; ++u) {
+          const int h = u * 16 + fr;
+          const bf16x8 wf = *reinterpret_cast<const bf16x8*>(whb + h * ROWB + ((((t & 1) * 4 + fq) ^ swz2(h)) << 4));
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc2[i][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[i], acc2[i][u], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (++c_br != a.nbr) continue;
+    // ---- tile done: head bias, bf16, store (lane: pixel fr, channels 16u + 4fq .. +3)
+    c_br = 0;
+    {
+      const float* bh = reinterpret_cast<const float*>(smem + BH_OFF);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = ct.q0 + wid * 32 + i * 16 + fr;
+        if (q < nq) {
+          const int Y = q / Wq, X = q - Y * Wq;
+          __hip_bfloat16* op = a.out + (((long)ct.b * a.H + Y * S + ct.cy) * a.W + X * S + ct.cx) * a.ldo;
+#pragma unroll
+          for (int u = 0; u < NH / 16; ++u) {
+            const int h = u * 16 + fq * 4;
+            if (h < a.nh) {
+              const float4 bv = *reinterpret_cast<const float4*>(bh + h);
+              __hip_bfloat16 o[4] = {__float2bfloat16(acc2[i][u][0] + bv.x), __float2bfloat16(acc2[i][u][1] + bv.y),
+                                     __float2bfloat16(acc2[i][u][2] + bv.z), __float2bfloat16(acc2[i][u][3] + bv.w)};
+              *reinterpret_cast<uint2*>(op + h) = *reinterpret_cast<uint2*>(o);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    ++c_k;
+    ct = tile_of(a, t_lo + slot + c_k * nslot, nqt);
+  }
+  wait_vmcnt0();  // no LDS DMA may outlive the workgroup (a tile-less workgroup still loaded the head)
+}
+
+}  // namespace
+
+// Branch i: input x[i] [B, H/s_i, W/s_i, ldx[i]] channels [offx[i], offx[i]+cin[i]),
+// weights w[i] [s_i*s_i*128, cin[i]] (FusedConv's transpose-conv GEMM layout),
+// bias[i] [s_i*s_i*128].  wh: [80, nbr*128] head weights, 32-chunk permuted
+// (see the header comment); bh [80].  out: [B, H, W, ldo], channels [0, nh).
+// grid: workgroups to launch (a multiple of 8; one per CU is the design point).
+TCA_API int tca_bev_neck_head(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
+                              const int* s, const void* const* w, const float* const* bias, const void* wh,
+                              const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
+                              hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
+    return (int)hipErrorInvalidValue;
+  NeckArgs a;
+  int S = 1, nsteps = 0;
+  for (int i = 0; i < nbr; ++i) {
+    if (s[i] < 1 || (cin[i] & 63) || (ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;
+    S = s[i] > S ? s[i] : S;
+  }
+  for (int i = 0; i < nbr; ++i) {
+    if (S % s[i]) return (int)hipErrorInvalidValue;
+    a.x[i] = (const __hip_bfloat16*)x[i]; a.ldx[i] = ldx[i]; a.offx[i] = offx[i]; a.cin[i] = cin[i]; a.s[i] = s[i];
+    a.w[i] = (const __hip_bfloat16*)w[i]; a.bias[i] = bias[i];
+    nsteps += cin[i] / 64;
+  }
+  for (int i = nbr; i < MAXBR; ++i) {
+    a.x[i] = nullptr; a.ldx[i] = a.offx[i] = a.cin[i] = 0; a.s[i] = 1; a.w[i] = nullptr; a.bias[i] = nullptr;
+  }
+  if ((H % S) || (W % S)) return (int)hipErrorInvalidValue;
+  a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.out = (__hip_bfloat16*)out; a.ldo = ldo; a.nh = nh;
+  a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
+  const int nq = (H / S) * (W / S);
+  a.ntiles = B * ((nq + BM - 1) / BM) * S * S;
+  bev_neck_head_kernel<<<grid, NT, 0, stream>>>(a);
+  TCA_LAUNCH_CHECK();
+}

@@ -279,7 +279,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 __device__ __forceinline__ int swz2(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+// ONEBAR = true: one barrier per K step.  Iteration kt waits for its own
+// stage (counted vmcnt), passes ONE barrier (which also proves every wave has
+// finished reading stage kt-1), then restages buffer (kt-1) % STAGES with
+// K step kt+STAGES-1 and runs the MFMAs of stage kt; the DMAs of up to
+// STAGES-1 future steps stay in flight under them (cdna_hip_programming.md
+// T3/T4 "minimum 2-phase" form generalised to STAGES buffers).
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONEBAR = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_glds_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64, ROWB = 128;
@@ -376,6 +382,52 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_kernel(ConvArgs a) {
       advance();
     }
   const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (ONEBAR) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt % STAGES;
+      // stages issued and not yet waited for, after kt: kt+1 .. min(kt+STAGES-2, nk-1)
+      const int after = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+      if (STAGES >= 4 && after >= 2) wait_vmcnt<(STAGES >= 4 ? 2 : 0) * NL>();
+      else if (STAGES >= 3 && after >= 1) wait_vmcnt<(STAGES >= 3 ? 1 : 0) * NL>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int nx = kt + STAGES - 1;
+      if (nx < nk) {
+        issue(nx, nx % STAGES, ky, kx, ci0);
+        advance();
+      }
+      const unsigned char* sa = smem + cur * STAGE;
+      const unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], bfg[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r = wm * TM + i * 16 + fr;
+          af[i] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int r = wn * TN + j * 16 + fr;
+          bfg[j] = *reinterpret_cast<const bf16x8*>(sb + r * ROWB + (((ks * 4 + fq) ^ swz2(r)) << 4));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the epilogue reuses the staging LDS
+    asm volatile("" ::: "memory");
+    epilogue<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+    return;
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt % STAGES;
     const int nx = kt + STAGES - 1;
@@ -418,10 +470,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_kernel(ConvArgs a) {
   epilogue<BM, BN, WM, WN>(a, acc, smem, m0, n0);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES = 2>
+template <int BM, int BN, int WM, int WN, int STAGES = 2, bool ONEBAR = false>
 int launch_glds(const ConvArgs& a, hipStream_t stream) {
+  static_assert(!ONEBAR || (STAGES >= 2 && STAGES <= 4), "one-barrier pipeline: 2..4 stages");
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  conv_glds_kernel<BM, BN, WM, WN, STAGES><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_glds_kernel<BM, BN, WM, WN, STAGES, ONEBAR><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -477,6 +530,21 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
     case 25: return launch_glds<128, 128, 2, 4>(a, stream);      // 8 waves, 64x32 per wave
     case 26: return launch_glds<256, 64, 4, 2>(a, stream);       // 8 waves, 64x32 per wave
     case 27: return launch_glds<128, 256, 2, 4>(a, stream);      // 8 waves, 64x64 per wave
+    // one barrier per K step, STAGES-deep glds pipeline
+    case 31: return launch_glds<128, 128, 4, 2, 2, true>(a, stream);
+    case 32: return launch_glds<128, 128, 4, 2, 3, true>(a, stream);
+    case 33: return launch_glds<128, 64, 4, 2, 3, true>(a, stream);
+    case 34: return launch_glds<128, 64, 4, 2, 4, true>(a, stream);
+    case 35: return launch_glds<256, 128, 4, 2, 2, true>(a, stream);
+    case 36: return launch_glds<256, 128, 4, 2, 3, true>(a, stream);
+    case 37: return launch_glds<64, 128, 2, 4, 3, true>(a, stream);
+    case 38: return launch_glds<256, 64, 4, 2, 3, true>(a, stream);
+    case 39: return launch_glds<128, 256, 2, 4, 3, true>(a, stream);
+    case 40: return launch_glds<256, 256, 2, 4, 2, true>(a, stream);
+    case 41: return launch_glds<128, 64, 4, 2, 2, true>(a, stream);
+    case 42: return launch_glds<64, 128, 2, 4, 2, true>(a, stream);
+    case 43: return launch_glds<128, 128, 2, 2, 3, true>(a, stream);   // 4 waves
+    case 44: return launch_glds<128, 64, 2, 2, 3, true>(a, stream);    // 4 waves
     case 1: return launch<128, 32, 4, 1>(a, stream);
     case 2: return launch<128, 64, 4, 1>(a, stream);
     case 3: return launch<128, 128, 2, 2>(a, stream);

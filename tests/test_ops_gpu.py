@@ -272,7 +272,7 @@ def test_fused_conv_slices_residual_and_transpose(cuda):
         assert (y.tensor().float().cpu() - ref).abs().max().item() < 0.05
 
 
-@pytest.mark.parametrize("tile", [11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("tile", [11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44])
 def test_fused_conv_glds_tiles(cuda, tile):
     """v2 (global_load_lds, BK=64) tiles: Cin % 64 == 0 shapes with stride, channel
     slices, residual, M/N tails and a pixel-shuffle transpose conv, vs fp32."""
@@ -280,7 +280,7 @@ def test_fused_conv_glds_tiles(cuda, tile):
     from triton_client_amd.ops.conv import NHWC, FusedConv
     torch.manual_seed(tile)
     B, H, W = 2, 23, 31  # M tail: 2*23*31 = 1426 (not a multiple of any BM)
-    for cin, cout, k, s, act in ((64, 64, 3, 1, 1), (128, 72, 3, 2, 2), (192, 256, 1, 1, 0)):
+    for cin, cout, k, s, act in ((64, 64, 3, 1, 1), (128, 72, 3, 2, 2), (192, 256, 1, 1, 0), (64, 128, 1, 1, 1)):
         conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=True)
         fc = FusedConv(conv, act=act, device=cuda)
         buf = torch.randn(B, H, W, cin + 64).to(cuda, torch.bfloat16)

@@ -197,11 +197,20 @@ class _BEVBackbonePlan:
             self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device), off, c))
             off += c
 
-    def forward(self, canvas: NHWC) -> NHWC:
-        x = canvas
-        for (convs, pp, H, W), (up, off, c) in zip(self.blocks, self.ups):
+    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
+        """The down blocks only: each block's output (the deblocks' inputs)."""
+        x, outs = canvas, []
+        for convs, pp, H, W in self.blocks:
             for i, cv in enumerate(convs):
                 x = cv(x, out=pp[i % 2])
+            outs.append(x)
+        return outs
+
+    def up_strides(self, bb) -> List[float]:
+        return [float(u.s) for u in bb.deblocks]
+
+    def forward(self, canvas: NHWC) -> NHWC:
+        for x, (up, off, c) in zip(self.forward_blocks(canvas), self.ups):
             up(x, out=NHWC(self.cat.t, off, c))
         return self.cat
 
@@ -209,7 +218,7 @@ class _BEVBackbonePlan:
 class FastBEV:
     """PointPillars BEV backbone + anchor head on fused convs."""
 
-    def __init__(self, model, batch: int, device="cuda"):
+    def __init__(self, model, batch: int, device="cuda", fused_neck: bool = True):
         self.device = torch.device(device)
         cfg = model.cfg
         nx, ny, _ = cfg.voxel.grid_size
@@ -228,9 +237,23 @@ class FastBEV:
         self.n_cls, self.n_box, self.n_dir = (hd.conv_cls.out_channels, hd.conv_box.out_channels,
                                               hd.conv_dir.out_channels)
         self.hout = bufs.new(B, H0, W0, self.head.N)
+        # deblocks + head as one kernel (K15) when the shapes fit its contract
+        self.neck = None
+        strides = self.bb.up_strides(model.backbone)
+        if self.device.type == "cuda" and fused_neck and all(s >= 1 and float(s).is_integer() for s in strides):
+            from ..ops.neck import FusedNeckHead, neck_head_supported
+
+            ups = [u for u, _, _ in self.ups]
+            si = [int(s) for s in strides]
+            cins = [blk[0][-1].N for blk in self.blocks]
+            if neck_head_supported(ups, si, cins, self.head, H0, W0):
+                self.neck = FusedNeckHead(ups, si, self.head, self.device)
 
     def forward(self, canvas: NHWC):
-        self.head(self.bb.forward(canvas), out=self.hout)
+        if self.neck is not None:
+            self.neck(self.bb.forward_blocks(canvas), self.hout)
+        else:
+            self.head(self.bb.forward(canvas), out=self.hout)
         t = self.hout.t
         return (NHWC(t, 0, self.n_cls), NHWC(t, self.n_cls, self.n_box),
                 NHWC(t, self.n_cls + self.n_box, self.n_dir))

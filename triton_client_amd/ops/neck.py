@@ -1,0 +1,95 @@
+"""Fused BEV neck + anchor head (HIP kernel K15, ``csrc/kernels/bev_neck.hip``).
+
+Replaces BaseBEVBackbone's deblocks (transpose convs k = s, stride s, + BN +
+ReLU, 128 channels each) and AnchorHeadSingle's merged 1x1 head with one
+launch; the 384-channel concat is never written (reference config:
+``data/pointpillar.yaml:48-72``).  :func:`neck_head_supported` says whether
+a plan qualifies; :class:`FusedNeckHead` falls back to nothing — callers keep
+the unfused plan for shapes outside the contract.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Sequence
+
+import torch
+
+from .. import _native
+from .conv import NHWC, FusedConv
+
+CB = 128
+NH_PAD = 80
+
+
+def chunk32_perm() -> List[int]:
+    """Position p in a 32-channel chunk -> source channel, matching the
+    register layout the kernel repacks its deconv accumulators into."""
+    out = []
+    for g in range(4):
+        for e in range(8):
+            out.append(4 * g + e if e < 4 else 16 + 4 * g + (e - 4))
+    return out
+
+
+def permute_head_weight(w: torch.Tensor) -> torch.Tensor:
+    """[nh, K] (K % 32 == 0) -> [80, K] zero-padded rows, columns permuted per 32-chunk."""
+    nh, K = w.shape
+    assert K % 32 == 0 and nh <= NH_PAD
+    idx = torch.tensor([c * 32 + p for c in range(K // 32) for p in chunk32_perm()], dtype=torch.long)
+    out = torch.zeros(NH_PAD, K, dtype=w.dtype)
+    out[:nh] = w[:, idx]
+    return out
+
+
+def neck_head_supported(ups: Sequence[FusedConv], strides: Sequence[int], cins: Sequence[int], head: FusedConv,
+                        H: int, W: int) -> bool:
+    if not 1 <= len(ups) <= 3:
+        return False
+    S = max(strides)
+    for u, s, c in zip(ups, strides, cins):
+        if s < 1 or S % s or c % 64 or u.cout_real != CB or u.Kp != c:
+            return False
+        if u.transpose and u.shuffle != s:
+            return False
+        if not u.transpose and (u.k != 1 or s != 1):
+            return False
+    return (head.k == 1 and head.N <= NH_PAD and head.N % 8 == 0 and head.Kp == CB * len(ups)
+            and H % S == 0 and W % S == 0)
+
+
+class FusedNeckHead:
+    """out[b, y, x, :nh] = head(cat_i relu(deconv_i(x_i)))[b, y, x]."""
+
+    def __init__(self, ups: Sequence[FusedConv], strides: Sequence[int], head: FusedConv, device,
+                 grid: int = 0):
+        self.ups, self.strides = list(ups), [int(s) for s in strides]
+        self.nbr = len(self.ups)
+        self.nh = head.N
+        # persistent kernel: one workgroup per CU (a multiple of 8: tiles are split per XCD)
+        if grid <= 0:
+            grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+        self.grid = max(8, grid // 8 * 8)
+        wh = head.w_gemm.float().cpu()[:, : head.Kp]
+        self.wh = permute_head_weight(wh).to(device, torch.bfloat16).contiguous()
+        bh = torch.zeros(NH_PAD)
+        bh[: head.N] = head.b_gemm.float().cpu()
+        self.bh = bh.to(device).contiguous()
+        n = self.nbr
+        self._w = (ctypes.c_void_p * n)(*[u.w_gemm.data_ptr() for u in self.ups])
+        self._b = (ctypes.c_void_p * n)(*[u.b_gemm.data_ptr() for u in self.ups])
+        self._s = (ctypes.c_int * n)(*self.strides)
+        self._cin = (ctypes.c_int * n)(*[u.Kp for u in self.ups])
+
+    def __call__(self, xs: Sequence[NHWC], out: NHWC, stream=None) -> NHWC:
+        n = self.nbr
+        B, H, W, _ = out.shape
+        for x, s in zip(xs, self.strides):
+            assert x.shape[0] == B and x.shape[1] * s == H and x.shape[2] * s == W, (x.shape, s, out.shape)
+        assert out.off == 0 and out.t.dtype == torch.bfloat16
+        ptrs = (ctypes.c_void_p * n)(*[x.t.data_ptr() for x in xs])
+        ldx = (ctypes.c_int * n)(*[x.t.shape[-1] for x in xs])
+        offx = (ctypes.c_int * n)(*[x.off for x in xs])
+        _native.call("tca_bev_neck_head", n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
+                     _native.ptr(self.wh), _native.ptr(self.bh), self.nh, _native.ptr(out.t), out.t.shape[-1],
+                     B, H, W, self.grid, _native.stream_ptr(stream))
+        return out
