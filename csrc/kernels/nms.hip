@@ -133,13 +133,20 @@ __device__ __forceinline__ float iou_aa(const float* a, const float* c) {
 __device__ __forceinline__ float cross2(float ax, float ay, float bx, float by) { return ax * by - ay * bx; }
 
 // ca/sa, cb/sb: cos/sin of each box's heading (computed once per box).
-__device__ float rotated_overlap(const float* A, const float* B, float ca, float sa, float cb, float sb) {
+__device__ __forceinline__ float rotated_overlap(const float* A, const float* B, float ca, float sa, float cb, float sb) {
   const float ra = 0.5f * sqrtf(A[3] * A[3] + A[4] * A[4]), rb = 0.5f * sqrtf(B[3] * B[3] + B[4] * B[4]);
   const float ddx = B[0] - A[0], ddy = B[1] - A[1];
   if (ddx * ddx + ddy * ddy > (ra + rb) * (ra + rb)) return 0.f;
   const float cr = cb * ca + sb * sa, sr = sb * ca - cb * sa;  // rotation of B relative to A
   const float bx = ca * ddx + sa * ddy, by = -sa * ddx + ca * ddy;
   const float ahx = 0.5f * A[3], ahy = 0.5f * A[4], bhx = 0.5f * B[3], bhy = 0.5f * B[4];
+  {  // separating-axis test on the four box axes: a strict separation means zero overlap (exact early-out)
+    const float acr = fabsf(cr), asr = fabsf(sr);
+    const float dxb = cb * ddx + sb * ddy, dyb = -sb * ddx + cb * ddy;
+    if (fabsf(bx) > ahx + bhx * acr + bhy * asr || fabsf(by) > ahy + bhx * asr + bhy * acr ||
+        fabsf(dxb) > bhx + ahx * acr + ahy * asr || fabsf(dyb) > bhy + ahx * asr + ahy * acr)
+      return 0.f;
+  }
   // B's corners in A's frame, CCW
   float qx[4], qy[4];
   {
@@ -165,7 +172,7 @@ __device__ float rotated_overlap(const float* A, const float* B, float ca, float
       if (pp[j] == 0.f) {
         if (qq[j] <= 0.f) empty = true;
       } else {
-        const float r = qq[j] / pp[j];
+        const float r = __fdividef(qq[j], pp[j]);
         if (pp[j] < 0.f) t0 = fmaxf(t0, r);
         else t1 = fminf(t1, r);
       }
@@ -190,8 +197,8 @@ __device__ float rotated_overlap(const float* A, const float* B, float ca, float
         // collinear with B's edge j: part of A∩B's boundary only if both edges
         // run the same way (A, B on the same side); touching from outside -> 0
         if (ex * (qx2 - px) + ey * (qy2 - py) < 0.f) empty = true;
-      } else if (sp < 0.f) t0 = fmaxf(t0, sp / (sp - sq));
-      else if (sq < 0.f) t1 = fminf(t1, sp / (sp - sq));
+      } else if (sp < 0.f) t0 = fmaxf(t0, __fdividef(sp, sp - sq));
+      else if (sq < 0.f) t1 = fminf(t1, __fdividef(sp, sp - sq));
     }
     if (!empty && t0 < t1) {
       const float dx = qx2 - px, dy = qy2 - py;
@@ -303,79 +310,199 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ 
   }
 }
 
+// ---- rotated BEV mask, v2 ----------------------------------------------------
+// A prepass writes each sorted candidate once, packed: P0 = (x, y, aabb
+// half-extents ex, ey), P1 = (w, l, cos, sin), and its class, so the tile
+// kernel's loads are coalesced and no tile recomputes a sincos or chases
+// order -> box.  One wave per upper-triangle 64x64 tile: lane = row; each
+// column is one broadcast ds_read_b128 and an AABB-overlap test (~8 VALU),
+// ballot-compacted in quarters of 16 columns into an LDS pair list; only the
+// surviving pairs run the exact rotated IoU (itself SAT-gated).
+// soa layout per image (st = pre_max rounded up to 4): float4 P0[st], float4 P1[st], int cls[st].
+__global__ void __launch_bounds__(256) nms_prep_rot_kernel(const float* __restrict__ boxes, int box_dim,
+                                                           const int* __restrict__ cls, const int* __restrict__ order,
+                                                           const int* __restrict__ sorted_n, int cap, int pre_max,
+                                                           int st, float* __restrict__ soa) {
+  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= sorted_n[b]) return;
+  const int s = order[(long)b * pre_max + i];
+  const float* bx = boxes + ((long)b * cap + s) * box_dim;
+  float* base = soa + (long)b * 9 * st;
+  const float w = bx[3], l = bx[4];
+  float sn, cs;
+  sincosf(bx[6], &sn, &cs);
+  reinterpret_cast<float4*>(base)[i] =
+      make_float4(bx[0], bx[1], 0.5f * (fabsf(cs) * w + fabsf(sn) * l), 0.5f * (fabsf(sn) * w + fabsf(cs) * l));
+  reinterpret_cast<float4*>(base + 4 * st)[i] = make_float4(w, l, cs, sn);
+  reinterpret_cast<int*>(base + 8 * st)[i] = cls[(long)b * cap + s];
+}
+
+template <bool AGN>
+__global__ void __launch_bounds__(256) nms_mask_rot_kernel(const float* __restrict__ soa,
+                                                           const int* __restrict__ sorted_n, int pre_max, int st,
+                                                           int mask_words, float thr, uint64_t* __restrict__ mask) {
+  __shared__ float4 s_r0[4][64], s_r1[4][64], s_c0[4][64], s_c1[4][64];
+  __shared__ int s_ccls[4][64];
+  __shared__ unsigned short s_pairs[4][64 * 16];
+  __shared__ unsigned long long s_bits[4][64];
+  const int b = blockIdx.y, wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = sorted_n[b], nb = (n + 63) >> 6;
+  const int t = blockIdx.x * 4 + wid;
+  if (t >= nb * (nb + 1) / 2) return;  // wave-uniform; the kernel has no block-wide barrier
+  int rb = 0, rem = t;
+  while (rem >= nb - rb) { rem -= nb - rb; ++rb; }
+  const int cbk = rb + rem;
+  const float* base = soa + (long)b * 9 * st;
+  const float4* P0 = reinterpret_cast<const float4*>(base);
+  const float4* P1 = reinterpret_cast<const float4*>(base + 4 * st);
+  const int* PC = reinterpret_cast<const int*>(base + 8 * st);
+  const int i = rb * 64 + lane, j = cbk * 64 + lane;
+  const bool rok = i < n;
+  // (branches, not selects: `c ? p[i] : zero` makes hipcc spill the zero and select a pointer)
+  float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, c0 = r0, c1 = r0;
+  int rcls = -1, ccls = -2;
+  if (rok) { r0 = P0[i]; r1 = P1[i]; rcls = PC[i]; }
+  if (j < n) { c0 = P0[j]; c1 = P1[j]; ccls = PC[j]; }
+  s_r0[wid][lane] = r0;
+  s_r1[wid][lane] = r1;
+  s_c0[wid][lane] = c0;
+  s_c1[wid][lane] = c1;
+  if (!AGN) s_ccls[wid][lane] = ccls;
+  s_bits[wid][lane] = 0ull;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  const int jmax = min(64, n - cbk * 64);
+  const int jlo = cbk == rb ? lane : -1;  // diagonal tile: only columns after the row
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  unsigned short* pairs = s_pairs[wid];
+  const float4* C0 = s_c0[wid];
+  for (int q0 = 0; q0 < jmax; q0 += 16) {
+    int cnt = 0;  // wave-uniform
+    const int qe = min(q0 + 16, jmax);
+    for (int jj = q0; jj < qe; ++jj) {
+      const float4 c = C0[jj];
+      bool hit = rok && jj > jlo && fabsf(c.x - r0.x) < c.z + r0.z && fabsf(c.y - r0.y) < c.w + r0.w;
+      if (!AGN) hit = hit && s_ccls[wid][jj] == rcls;
+      const unsigned long long bal = __ballot(hit);
+      if (hit) pairs[cnt + __popcll(bal & lt)] = (unsigned short)((lane << 6) | jj);
+      cnt += __popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int p = lane; p < cnt; p += 64) {
+      const int r = pairs[p] >> 6, cc = pairs[p] & 63;
+      const float4 a0 = s_r0[wid][r], a1 = s_r1[wid][r], b0 = C0[cc], b1 = s_c1[wid][cc];
+      const float A[5] = {a0.x, a0.y, 0.f, a1.x, a1.y};
+      const float Bx[5] = {b0.x, b0.y, 0.f, b1.x, b1.y};
+      const float ov = rotated_overlap(A, Bx, a1.z, a1.w, b1.z, b1.w);
+      if (ov > 0.f && ov / fmaxf(a1.x * a1.y + b1.x * b1.y - ov, 1e-8f) > thr) atomicOr(&s_bits[wid][r], 1ull << cc);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (rok) mask[((long)b * pre_max + i) * mask_words + cbk] = s_bits[wid][lane];
+}
+
 struct OutXform {  // 2D: x' = (x - pad_x) / gain_x, clamp to [0, clip_w]
   float gain_x, gain_y, pad_x, pad_y, clip_w, clip_h;
   int enable;
 };
 
-__global__ void __launch_bounds__(256) nms_reduce_kernel(const int* __restrict__ order, const int* __restrict__ sorted_n,
-                                                         const uint64_t* __restrict__ mask, int pre_max, int mask_words,
-                                                         const float* __restrict__ boxes, int box_dim,
-                                                         const float* __restrict__ scores, const int* __restrict__ cls,
-                                                         int cap, int max_out, OutXform xf,
-                                                         float* __restrict__ out_box, float* __restrict__ out_score,
-                                                         int* __restrict__ out_cls, int* __restrict__ out_count) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint64_t* removed = (uint64_t*)smem;         // mask_words
-  uint64_t* diag = removed + mask_words;       // 64
-  int* kept = (int*)(diag + 64);               // 64
-  int* s_cnt = kept + 64;
-  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  const int n = sorted_n[b];
-  const int nb = (n + 63) >> 6;
-  const int* ob = order + (long)b * pre_max;
-  const uint64_t* mb = mask + (long)b * pre_max * mask_words;
-  for (int w = tid; w < mask_words; w += nt) removed[w] = 0;
-  __syncthreads();
-  int nkeep = 0;
-  for (int rb = 0; rb < nb && nkeep < max_out; ++rb) {
-    if (tid < 64) {
-      const int i = rb * 64 + tid;
-      diag[tid] = i < n ? mb[(long)i * mask_words + rb] : 0ull;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      uint64_t word = removed[rb];
-      int c = 0;
-      const int lim = min(64, n - rb * 64);
-      for (int k = 0; k < lim && nkeep + c < max_out; ++k) {
-        if (!((word >> k) & 1ull)) {
-          kept[c++] = rb * 64 + k;
-          word |= diag[k];
-        }
-      }
-      *s_cnt = c;
-    }
-    __syncthreads();
-    const int c = *s_cnt;
-    if (tid < c) {
-      const int s = ob[kept[tid]];
-      const long src = (long)b * cap + s;
-      const long dst = (long)b * max_out + nkeep + tid;
-      const float* bx = boxes + src * box_dim;
-      float* ox = out_box + dst * box_dim;
-      for (int d = 0; d < box_dim; ++d) ox[d] = bx[d];
-      if (xf.enable) {
-        ox[0] = fminf(fmaxf((bx[0] - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
-        ox[1] = fminf(fmaxf((bx[1] - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
-        ox[2] = fminf(fmaxf((bx[2] - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
-        ox[3] = fminf(fmaxf((bx[3] - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
-      }
-      out_score[dst] = scores[src];
-      out_cls[dst] = cls[src];
-    }
-    // OR the kept rows' masks into the removed set: all (row, word) loads in
-    // flight at once, combined with LDS 64-bit atomics.
-    const int words_left = nb - rb - 1;
-    for (int t = tid; t < c * words_left; t += nt) {
-      const int k = t / words_left, w = rb + 1 + t % words_left;
-      const uint64_t v = mb[(long)kept[k] * mask_words + w];
-      if (v) atomicOr((unsigned long long*)&removed[w], (unsigned long long)v);
-    }
-    nkeep += c;
-    __syncthreads();
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int k) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, k);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), k);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, o), hi = __shfl_xor((int)(uint32_t)(v >> 32), o);
+    v |= ((uint64_t)hi << 32) | lo;
   }
-  if (tid == 0) out_count[b] = nkeep;
+  return v;
+}
+
+// Greedy reduce over the suppression bitmask, one wave per image, RB 64-row
+// blocks per memory round.  Round r loads (a) for each of its RB row blocks,
+// the rows' own words of the round's blocks (lane k = row k of the block;
+// upper triangle only) and (b) the round's words of every row kept so far,
+// OR-reduced over the wave.  The blocks are then resolved in order entirely
+// in registers: the next kept row is ctz(~removed), and its suppression words
+// for the rest of the round come from its lane by readlane.  One dependent
+// memory round per RB*64 candidates instead of one per 64 with block barriers.
+template <int RB>
+__global__ void __launch_bounds__(64) nms_reduce_wave_kernel(const int* __restrict__ order,
+                                                             const int* __restrict__ sorted_n,
+                                                             const uint64_t* __restrict__ mask, int pre_max,
+                                                             int mask_words, const float* __restrict__ boxes,
+                                                             int box_dim, const float* __restrict__ scores,
+                                                             const int* __restrict__ cls, int cap, int max_out,
+                                                             OutXform xf, float* __restrict__ out_box,
+                                                             float* __restrict__ out_score, int* __restrict__ out_cls,
+                                                             int* __restrict__ out_count) {
+  __shared__ int s_kept[kSortCap];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int n = sorted_n[b], nb = (n + 63) >> 6;
+  const uint64_t* mb = mask + (long)b * pre_max * mask_words;
+  int nkeep = 0;
+  for (int rb0 = 0; rb0 < nb && nkeep < max_out; rb0 += RB) {
+    uint64_t M[RB][RB], P[RB];
+#pragma unroll
+    for (int c = 0; c < RB; ++c) {
+      P[c] = 0ull;
+      const int row = (rb0 + c) * 64 + lane;
+#pragma unroll
+      for (int w = 0; w < RB; ++w) {
+        M[c][w] = 0ull;
+        if (w >= c && rb0 + w < nb && row < n) M[c][w] = mb[(long)row * mask_words + rb0 + w];
+      }
+    }
+    for (int j = lane; j < nkeep; j += 64) {
+      const long row = s_kept[j];
+#pragma unroll
+      for (int w = 0; w < RB; ++w)
+        if (rb0 + w < nb) P[w] |= mb[row * mask_words + rb0 + w];
+    }
+#pragma unroll
+    for (int w = 0; w < RB; ++w) P[w] = wave_or64(P[w]);
+#pragma unroll
+    for (int c = 0; c < RB; ++c) {
+      if (rb0 + c >= nb || nkeep >= max_out) break;
+      const int lim = min(64, n - (rb0 + c) * 64);
+      const uint64_t valid = lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+      uint64_t word = P[c];
+      uint64_t avail = ~word & valid;
+      while (avail != 0ull && nkeep < max_out) {
+        const int k = __builtin_amdgcn_readfirstlane(__builtin_ctzll(avail));
+        if (lane == 0) s_kept[nkeep] = (rb0 + c) * 64 + k;
+        ++nkeep;
+        word |= readlane64(M[c][c], k) | (1ull << k);
+#pragma unroll
+        for (int w = c + 1; w < RB; ++w) P[w] |= readlane64(M[c][w], k);
+        avail = ~word & valid;
+      }
+    }
+    __syncthreads();  // s_kept (lane 0's writes) visible to the next round's loads
+  }
+  __syncthreads();
+  for (int t = lane; t < nkeep; t += 64) {
+    const int s = order[(long)b * pre_max + s_kept[t]];
+    const long src = (long)b * cap + s;
+    const long dst = (long)b * max_out + t;
+    const float* bx = boxes + src * box_dim;
+    float* ox = out_box + dst * box_dim;
+    for (int d = 0; d < box_dim; ++d) ox[d] = bx[d];
+    if (xf.enable) {
+      ox[0] = fminf(fmaxf((bx[0] - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
+      ox[1] = fminf(fmaxf((bx[1] - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
+      ox[2] = fminf(fmaxf((bx[2] - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
+      ox[3] = fminf(fmaxf((bx[3] - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
+    }
+    out_score[dst] = scores[src];
+    out_cls[dst] = cls[src];
+  }
+  if (lane == 0) out_count[b] = nkeep;
 }
 
 }  // namespace
@@ -404,6 +531,23 @@ TCA_API int tca_nms_mask(int mode, const float* boxes, int box_dim, const int* c
   TCA_LAUNCH_CHECK();
 }
 
+// Rotated-BEV suppression mask, v2: soa is scratch [batch, 9, ceil4(pre_max)] fp32 (16-B aligned).
+TCA_API int tca_nms_mask_rot(const float* boxes, int box_dim, const int* cls, const int* order, const int* sorted_n,
+                             int batch, int cap, int pre_max, float thr, int agnostic, float* soa, uint64_t* mask,
+                             hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (box_dim < 7) return (int)hipErrorInvalidValue;
+  const int mask_words = (pre_max + 63) / 64;
+  const int st = (pre_max + 3) & ~3;
+  nms_prep_rot_kernel<<<dim3((pre_max + 255) / 256, batch), 256, 0, stream>>>(boxes, box_dim, cls, order, sorted_n,
+                                                                             cap, pre_max, st, soa);
+  const int tiles = mask_words * (mask_words + 1) / 2;
+  const dim3 grid((tiles + 3) / 4, batch);
+  if (agnostic) nms_mask_rot_kernel<true><<<grid, 256, 0, stream>>>(soa, sorted_n, pre_max, st, mask_words, thr, mask);
+  else nms_mask_rot_kernel<false><<<grid, 256, 0, stream>>>(soa, sorted_n, pre_max, st, mask_words, thr, mask);
+  TCA_LAUNCH_CHECK();
+}
+
 TCA_API int tca_nms_reduce(const int* order, const int* sorted_n, const uint64_t* mask, int batch, int pre_max,
                            const float* boxes, int box_dim, const float* scores, const int* cls, int cap, int max_out,
                            const float* xform /*host [6] or null*/, float* out_box, float* out_score, int* out_cls,
@@ -412,9 +556,10 @@ TCA_API int tca_nms_reduce(const int* order, const int* sorted_n, const uint64_t
   const int mask_words = (pre_max + 63) / 64;
   OutXform xf{1.f, 1.f, 0.f, 0.f, 0.f, 0.f, 0};
   if (xform) { xf = OutXform{xform[0], xform[1], xform[2], xform[3], xform[4], xform[5], 1}; }
-  const size_t lds = sizeof(uint64_t) * (mask_words + 64) + sizeof(int) * (64 + 4);
-  nms_reduce_kernel<<<batch, 256, lds, stream>>>(order, sorted_n, mask, pre_max, mask_words, boxes, box_dim, scores, cls,
-                                                 cap, max_out, xf, out_box, out_score, out_cls, out_count);
+  if (max_out > kSortCap) return (int)hipErrorInvalidValue;
+  nms_reduce_wave_kernel<4><<<batch, 64, 0, stream>>>(order, sorted_n, mask, pre_max, mask_words, boxes, box_dim,
+                                                      scores, cls, cap, max_out, xf, out_box, out_score, out_cls,
+                                                      out_count);
   TCA_LAUNCH_CHECK();
 }
 

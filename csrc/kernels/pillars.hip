@@ -151,21 +151,19 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
   }
 }
 
+// Zero exactly the cells the previous frame scattered: one thread per 16-B
+// chunk of a pillar's C bf16 channels (C % 8 == 0), frame per grid row.
 __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict__ coords,
-                                                           const int* __restrict__ voxel_count, int batch,
-                                                           int max_voxels, int nx, int ny, int C,
-                                                           __hip_bfloat16* __restrict__ canvas) {
-  const int lane = threadIdx.x & 63;
-  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-  const long nv = (long)batch * max_voxels;
-  for (long v = wave; v < nv; v += nwaves) {
-    const int b = (int)(v / max_voxels), vid = (int)(v - (long)b * max_voxels);
-    if (vid >= voxel_count[b]) continue;
-    const int* co = coords + v * 4;
-    const long cell = ((long)b * ny + co[2]) * nx + co[3];
-    for (int c = lane; c < C; c += 64) canvas[cell * C + c] = __float2bfloat16(0.f);
-  }
+                                                           const int* __restrict__ voxel_count, int max_voxels, int nx,
+                                                           int ny, int C, __hip_bfloat16* __restrict__ canvas) {
+  const int b = blockIdx.y;
+  const int cpp = C >> 3;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int vid = t / cpp, c = t - vid * cpp;
+  if (vid >= voxel_count[b]) return;
+  const int* co = coords + ((long)b * max_voxels + vid) * 4;
+  const long cell = ((long)b * ny + co[2]) * nx + co[3];
+  reinterpret_cast<uint4*>(canvas + cell * C)[c] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 }  // namespace
@@ -201,7 +199,8 @@ TCA_API int tca_pillar_vfe_voxels(const float* voxels, const int* num_points, co
 TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
                                     int ny, int C, void* canvas, hipStream_t stream) {
   if (batch <= 0) return 0;
-  canvas_clear_kernel<<<1024, 256, 0, stream>>>(coords, voxel_count, batch, max_voxels, nx, ny, C,
-                                                (__hip_bfloat16*)canvas);
+  if (C & 7) return (int)hipErrorInvalidValue;
+  canvas_clear_kernel<<<dim3((max_voxels * (C / 8) + 255) / 256, batch), 256, 0, stream>>>(
+      coords, voxel_count, max_voxels, nx, ny, C, (__hip_bfloat16*)canvas);
   TCA_LAUNCH_CHECK();
 }

@@ -212,6 +212,37 @@ __global__ void __launch_bounds__(256) vox_gather_reset_kernel(
   }
 }
 
+// Reset pass of the fused path (no gather), split for memory-level
+// parallelism: one thread per 16-B chunk of a voxel's slot row (P % 4 == 0)
+// instead of a wave per voxel writing 4-B slots, and one thread per point for
+// the cell tables.
+__global__ void __launch_bounds__(256) vox_slot_reset_kernel(int max_voxels, int P, const int* __restrict__ voxel_count,
+                                                             int* __restrict__ vcount, int* __restrict__ slots,
+                                                             int* __restrict__ num_points) {
+  const int b = blockIdx.y;
+  const int cpv = P >> 2;  // 16-B chunks per voxel
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int vid = t / cpv, c = t - vid * cpv;
+  if (vid >= voxel_count[b]) return;
+  const long g = (long)b * max_voxels + vid;
+  reinterpret_cast<int4*>(slots + g * P)[c] = make_int4(kEmpty, kEmpty, kEmpty, kEmpty);
+  if (c == 0) {
+    num_points[g] = min(vcount[g], P);
+    vcount[g] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const int* __restrict__ npts,
+                                                             const int* __restrict__ point_cell, long cells,
+                                                             int* __restrict__ cell_first, int* __restrict__ cell_vid) {
+  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npts[b]) return;
+  const int c = point_cell[(long)b * max_pts + i];
+  if (c < 0) return;
+  cell_first[(long)b * cells + c] = kEmpty;
+  cell_vid[(long)b * cells + c] = -1;
+}
+
 VoxGeom make_geom(const float* range, const float* vsize, const int* grid) {
   VoxGeom g;
   g.r0 = range[0]; g.r1 = range[1]; g.r2 = range[2];
@@ -251,7 +282,11 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
     vox_insert_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g.cells, cell_vid, max_voxels, P,
                                                     vcount, slots);
   }
-  if (mode & 2) {
+  if ((mode & 2) && !gather && (P & 3) == 0) {
+    vox_slot_reset_kernel<<<dim3((max_voxels * (P / 4) + 255) / 256, batch), 256, 0, stream>>>(
+        max_voxels, P, voxel_count, vcount, slots, num_points);
+    vox_cell_reset_kernel<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid);
+  } else if (mode & 2) {
     vox_gather_reset_kernel<<<1024, 256, 0, stream>>>(pts, pstride, max_points, npts, nfeat, batch,
                                                                max_voxels, P, voxel_count, vcount, slots, voxels,
                                                                num_points, point_cell, g.cells, cell_first, cell_vid,

@@ -68,9 +68,9 @@ def _random_candidates(B, cap, n, D, rotated, seed):
     return box, score, cls, key, count
 
 
-@pytest.mark.parametrize("rotated", [False, True])
+@pytest.mark.parametrize("rotated,agnostic", [(False, False), (True, True), (True, False)])
 @pytest.mark.parametrize("pre_max", [64, 1000, 4096])
-def test_sort_nms_gpu_vs_golden(cuda, rotated, pre_max):
+def test_sort_nms_gpu_vs_golden(cuda, rotated, agnostic, pre_max):
     B, cap, D = 3, 6000, 7 if rotated else 4
     n = [0, 700, 5000] if pre_max > 64 else [10, 63, 200]
     box, score, cls, key, count = _random_candidates(B, cap, n, D, rotated, seed=pre_max + rotated)
@@ -80,14 +80,14 @@ def test_sort_nms_gpu_vs_golden(cuda, rotated, pre_max):
                       torch.from_numpy(count).to(cuda))
     thr = 0.1 if rotated else 0.45
     max_out = 300
-    res = sort_and_nms(ws, cand, int(rotated), thr, pre_max, max_out, agnostic=rotated)
+    res = sort_and_nms(ws, cand, int(rotated), thr, pre_max, max_out, agnostic=agnostic)
     torch.cuda.synchronize()
     got = res.per_image()
     for b in range(B):
         m = count[b]
         tie = (np.uint64(0xFFFFFFFF) - (key[b, :m] & np.uint64(0xFFFFFFFF))).astype(np.int64)
         keep = sort_and_nms_cpu(box[b, :m], score[b, :m], cls[b, :m], tie, int(rotated), thr, pre_max, max_out,
-                                rotated)
+                                agnostic)
         ref_box = box[b, keep]
         g = got[b]
         if rotated:  # rotated IoU: allow a borderline flip or two from fp32 clipping order

@@ -69,8 +69,14 @@ def sort_and_nms(ws: Workspace, cand: Candidates, mode: int, iou_thr: float, pre
     s = _native.stream_ptr(stream)
     _native.call("tca_topk_sort", _native.ptr(cand.key), _native.ptr(cand.count), B, cap, pre_max,
                  _native.ptr(order), _native.ptr(nsorted), s)
-    _native.call("tca_nms_mask", mode, _native.ptr(cand.box), D, _native.ptr(cand.cls), _native.ptr(order),
-                 _native.ptr(nsorted), B, cap, pre_max, float(iou_thr), int(agnostic), _native.ptr(mask), 0, s)
+    if mode == 1:
+        soa = ws.get(prefix + "soa", (B, 9, (pre_max + 3) // 4 * 4), torch.float32)
+        _native.call("tca_nms_mask_rot", _native.ptr(cand.box), D, _native.ptr(cand.cls), _native.ptr(order),
+                     _native.ptr(nsorted), B, cap, pre_max, float(iou_thr), int(agnostic), _native.ptr(soa),
+                     _native.ptr(mask), s)
+    else:
+        _native.call("tca_nms_mask", mode, _native.ptr(cand.box), D, _native.ptr(cand.cls), _native.ptr(order),
+                     _native.ptr(nsorted), B, cap, pre_max, float(iou_thr), int(agnostic), _native.ptr(mask), 0, s)
     xf_arr = None
     if xform is not None:
         import ctypes
