@@ -254,7 +254,9 @@ def main():
         r2, r3 = runner()
         src = outputs(r2, r3)
         if gather_dst is None and info.is_main:
-            gather_dst = [[torch.empty_like(t) for t in src] for _ in range(info.world)]
+            # rank 0's own detections are D2H-copied straight from the graph's result
+            # buffers (stream order keeps the next replay behind that copy)
+            gather_dst = [list(src)] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)]
             host_out = [[[torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in src] for _ in range(info.world)]
                         for _ in range(2)]
         ex.gather(src, gather_dst if info.is_main else None)

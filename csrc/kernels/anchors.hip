@@ -20,84 +20,127 @@ struct AnchorTable {
   float v[8][6];  // dxa, dya, dza, za(centre), rot, diag
 };
 
+constexpr int kAnchorsPerBlock = 4096;  // 16 per thread
+constexpr int kStage = 2048;            // LDS-staged passing anchors per block
+
+template <typename T>
+__device__ __forceinline__ float head_at(const T* base, int layout, int b, int H, int W, int nch, int ld, int y, int x,
+                                         int ch) {
+  const long off = layout == 0 ? (((long)b * nch + ch) * H + y) * W + x : (((long)b * H + y) * W + x) * ld + ch;
+  return to_f32(base[off]);
+}
+
+// Decode one passing anchor (ResidualCoder + direction classifier) into candidate slot o.
+template <typename T>
+__device__ void decode_write(const T* __restrict__ box, const T* __restrict__ dir, int layout, int H, int W, int A,
+                             int bins, int ld_box, int ld_dir, const AnchorTable& tb, float x0, float xs, float y0,
+                             float ys, float dir_offset, float dir_limit_offset, int b, int aidx, float score,
+                             int label, long o, float* __restrict__ cand_box, float* __restrict__ cand_score,
+                             int* __restrict__ cand_label, uint64_t* __restrict__ cand_key) {
+  const int a = aidx % A, yx = aidx / A, y = yx / W, x = yx - y * W;
+  const float* t = tb.v[a];
+  const float xa = x0 + x * xs, ya = y0 + y * ys, za = t[3];
+  const float dxa = t[0], dya = t[1], dza = t[2], ra = t[4], diag = t[5];
+  float e[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) e[q] = head_at(box, layout, b, H, W, A * 7, ld_box, y, x, a * 7 + q);
+  float out[7];
+  out[0] = e[0] * diag + xa;
+  out[1] = e[1] * diag + ya;
+  out[2] = e[2] * dza + za;
+  out[3] = __expf(e[3]) * dxa;
+  out[4] = __expf(e[4]) * dya;
+  out[5] = __expf(e[5]) * dza;
+  float rg = e[6] + ra;
+  if (dir && bins > 0) {
+    float bd = -INFINITY;
+    int dl = 0;
+    for (int d = 0; d < bins; ++d) {
+      const float v = head_at(dir, layout, b, H, W, A * bins, ld_dir, y, x, a * bins + d);
+      if (v > bd) { bd = v; dl = d; }
+    }
+    const float period = 2.f * 3.14159265358979f / (float)bins;
+    const float val = rg - dir_offset;
+    const float lim = val - floorf(val / period + dir_limit_offset) * period;
+    rg = lim + dir_offset + period * (float)dl;
+  }
+  out[6] = rg;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) cand_box[o * 7 + q] = out[q];
+  cand_score[o] = score;
+  cand_label[o] = label;
+  cand_key[o] = make_score_key(score, (uint32_t)aidx);
+}
+
+// One block covers kAnchorsPerBlock consecutive anchors of one frame: the
+// class max / sigmoid / threshold runs over all of them (loads of 4
+// iterations in flight per thread), passing anchors are staged in LDS, and
+// the block takes ONE global slot range (a single atomic per block instead of
+// one per 256 anchors), then decodes the staged boxes in parallel.
 template <typename T>
 __global__ void __launch_bounds__(256) anchor_decode_kernel(
     const T* __restrict__ cls, const T* __restrict__ box, const T* __restrict__ dir, int layout, int H, int W, int A,
-    int C, int bins, int ld_cls, int ld_box, int ld_dir, AnchorTable tb, float x0, float xs, float y0, float ys, float dir_offset, float dir_limit_offset,
-    float score_thresh, float* __restrict__ cand_box, float* __restrict__ cand_score, int* __restrict__ cand_label,
-    uint64_t* __restrict__ cand_key, int* __restrict__ cand_count, int cap) {
+    int C, int bins, int ld_cls, int ld_box, int ld_dir, AnchorTable tb, float x0, float xs, float y0, float ys,
+    float dir_offset, float dir_limit_offset, float score_thresh, float* __restrict__ cand_box,
+    float* __restrict__ cand_score, int* __restrict__ cand_label, uint64_t* __restrict__ cand_key,
+    int* __restrict__ cand_count, int cap) {
+  __shared__ int s_idx[kStage];
+  __shared__ float s_score[kStage];
+  __shared__ int s_label[kStage];
   __shared__ int s_cnt, s_base;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const int b = blockIdx.y;
-  const int aidx = blockIdx.x * blockDim.x + threadIdx.x;
   const int total = H * W * A;
-  bool pass = false;
-  float score = 0.f;
-  int label = 0;
-  float out[7];
-  if (aidx < total) {
-    const int a = aidx % A;
-    const int yx = aidx / A;
-    const int y = yx / W, x = yx - y * W;
-    // NCHW: nch channels; NHWC: channel stride ld (a slice of a wider tensor)
-    auto at = [&](const T* base, int nch, int ld, int ch) -> float {
-      long off = layout == 0 ? (((long)b * nch + ch) * H + y) * W + x : (((long)b * H + y) * W + x) * ld + ch;
-      return to_f32(base[off]);
-    };
-    float best = -INFINITY;
-    int bc = 0;
-    for (int c = 0; c < C; ++c) {
-      const float v = at(cls, A * C, ld_cls, a * C + c);
-      if (v > best) { best = v; bc = c; }
-    }
-    score = sigmoidf_(best);
-    label = bc + 1;
-    if (score >= score_thresh) {
-      pass = true;
-      const float* t = tb.v[a];
-      const float xa = x0 + x * xs, ya = y0 + y * ys, za = t[3];
-      const float dxa = t[0], dya = t[1], dza = t[2], ra = t[4], diag = t[5];
-      float e[7];
+  const int a0 = blockIdx.x * kAnchorsPerBlock;
+  const int a1 = min(a0 + kAnchorsPerBlock, total);
+  for (int base = a0 + threadIdx.x; base < a1; base += 4 * 256) {
+    float best[4];
+    int bc[4];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) e[k] = at(box, A * 7, ld_box, a * 7 + k);
-      out[0] = e[0] * diag + xa;
-      out[1] = e[1] * diag + ya;
-      out[2] = e[2] * dza + za;
-      out[3] = __expf(e[3]) * dxa;
-      out[4] = __expf(e[4]) * dya;
-      out[5] = __expf(e[5]) * dza;
-      float rg = e[6] + ra;
-      if (dir && bins > 0) {
-        float bd = -INFINITY;
-        int dl = 0;
-        for (int d = 0; d < bins; ++d) {
-          const float v = at(dir, A * bins, ld_dir, a * bins + d);
-          if (v > bd) { bd = v; dl = d; }
+    for (int u = 0; u < 4; ++u) {
+      const int aidx = base + u * 256;
+      best[u] = -INFINITY;
+      bc[u] = 0;
+      if (aidx < a1) {
+        const int a = aidx % A, yx = aidx / A, y = yx / W, x = yx - y * W;
+        for (int c = 0; c < C; ++c) {
+          const float v = head_at(cls, layout, b, H, W, A * C, ld_cls, y, x, a * C + c);
+          if (v > best[u]) { best[u] = v; bc[u] = c; }
         }
-        const float period = 2.f * 3.14159265358979f / (float)bins;
-        const float val = rg - dir_offset;
-        const float lim = val - floorf(val / period + dir_limit_offset) * period;
-        rg = lim + dir_offset + period * (float)dl;
       }
-      out[6] = rg;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int aidx = base + u * 256;
+      if (aidx >= a1) continue;
+      const float score = sigmoidf_(best[u]);
+      if (score < score_thresh) continue;
+      const int slot = atomicAdd(&s_cnt, 1);
+      if (slot < kStage) {
+        s_idx[slot] = aidx;
+        s_score[slot] = score;
+        s_label[slot] = bc[u] + 1;
+      } else {  // stage full (a dense block): take a global slot directly
+        const int g = atomicAdd(&cand_count[b], 1);
+        if (g < cap)
+          decode_write(box, dir, layout, H, W, A, bins, ld_box, ld_dir, tb, x0, xs, y0, ys, dir_offset,
+                       dir_limit_offset, b, aidx, score, bc[u] + 1, (long)b * cap + g, cand_box, cand_score,
+                       cand_label, cand_key);
+      }
     }
   }
-  int my = -1;
-  if (pass) my = atomicAdd(&s_cnt, 1);
   __syncthreads();
-  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&cand_count[b], s_cnt) : 0;
+  const int n = min(s_cnt, kStage);
+  if (threadIdx.x == 0) s_base = n ? atomicAdd(&cand_count[b], n) : 0;
   __syncthreads();
-  if (pass) {
-    const int slot = s_base + my;
-    if (slot < cap) {
-      const long o = (long)b * cap + slot;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) cand_box[o * 7 + k] = out[k];
-      cand_score[o] = score;
-      cand_label[o] = label;
-      cand_key[o] = make_score_key(score, (uint32_t)aidx);
-    }
+  const int base_slot = s_base;
+  for (int k = threadIdx.x; k < n; k += 256) {
+    const int slot = base_slot + k;
+    if (slot >= cap) break;
+    decode_write(box, dir, layout, H, W, A, bins, ld_box, ld_dir, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset,
+                 b, s_idx[k], s_score[k], s_label[k], (long)b * cap + slot, cand_box, cand_score, cand_label,
+                 cand_key);
   }
 }
 
@@ -117,7 +160,7 @@ TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const voi
     for (int k = 0; k < 6; ++k) tb.v[a][k] = a < A ? table[a * 6 + k] : 0.f;
   int e = zero_i32_async(cand_count, batch, stream);
   if (e) return e;
-  dim3 grid((H * W * A + 255) / 256, batch);
+  dim3 grid((H * W * A + kAnchorsPerBlock - 1) / kAnchorsPerBlock, batch);
 #define LAUNCH(T)                                                                                              \
   anchor_decode_kernel<T><<<grid, 256, 0, stream>>>((const T*)cls, (const T*)box, (const T*)dir, layout, H, W, A, C, \
                                                     bins, ld_cls > 0 ? ld_cls : A * C, ld_box > 0 ? ld_box : A * 7,  \

@@ -79,9 +79,9 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
   const float bias1 = b1[r];
   const float bias2_0 = b2[r], bias2_1 = b2[32 + r];
 
-  const long nv = (long)batch * max_voxels;
-  for (long v = wave; v < nv; v += nwaves) {
-    const int b = (int)(v / max_voxels), vid = (int)(v - (long)b * max_voxels);
+  const int nv = batch * max_voxels;  // 32-bit: 64-bit div/mod is ~150 VALU per use
+  for (int v = (int)wave; v < nv; v += (int)nwaves) {
+    const int b = (int)((unsigned)v / (unsigned)max_voxels), vid = v - b * max_voxels;
     if (vid >= voxel_count[b]) continue;
     int n;
     float p[5] = {0.f, 0.f, 0.f, 0.f, 0.f};

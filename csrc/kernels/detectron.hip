@@ -235,14 +235,14 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const __hip_bfloat16* __r
                                                        int ldc, int c_off, int G, const float* __restrict__ stats,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        int relu, __hip_bfloat16* __restrict__ y, int ldy, int y_off) {
-  const int c8 = C / 8;
-  const long total = (long)B * HW * c8;
+  const unsigned c8 = C / 8;
+  const unsigned total = (unsigned)B * HW * c8;  // < 2^31 (host-checked); 32-bit div/mod
   const int cg = C / G;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int cv = (int)(t % c8);
-    const long pix = t / c8;
-    const int b = (int)(pix / HW);
-    uint4 v = *reinterpret_cast<const uint4*>(x + pix * ldc + c_off + cv * 8);
+    const unsigned pix = t / c8;
+    const int b = (int)(pix / (unsigned)HW);
+    uint4 v = *reinterpret_cast<const uint4*>(x + (long)pix * ldc + c_off + cv * 8);
     __hip_bfloat16* e = reinterpret_cast<__hip_bfloat16*>(&v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const __hip_bfloat16* __r
       if (relu) f = fmaxf(f, 0.f);
       e[k] = __float2bfloat16(f);
     }
-    *reinterpret_cast<uint4*>(y + pix * ldy + y_off + cv * 8) = v;
+    *reinterpret_cast<uint4*>(y + (long)pix * ldy + y_off + cv * 8) = v;
   }
 }
 
@@ -329,6 +329,7 @@ TCA_API int tca_group_norm_nhwc(const void* x, int B, int HW, int C, int ldc, in
                                 int y_off, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((C % G) || (C & 7) || (ldc & 7) || (c_off & 7) || (ldy & 7) || (y_off & 7)) return (int)hipErrorInvalidValue;
+  if ((long)B * HW * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
   gn_stats_kernel<<<dim3(G, B), 256, 0, stream>>>((const __hip_bfloat16*)x, HW, C, ldc, c_off, G, eps, stats);
   const long work = (long)B * HW * (C / 8);
   gn_apply_kernel<<<(int)min((work + 255) / 256, (long)8192), 256, 0, stream>>>(

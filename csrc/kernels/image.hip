@@ -42,12 +42,14 @@ template <typename T>
 __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ src, T* __restrict__ dst, PrepParams p,
                                                    int batch) {
   const int qw = (p.dst_w + 3) >> 2;
-  long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)batch * p.dst_h * qw;
+  // 32-bit index math (total < 2^31, host-checked): 64-bit div/mod is ~150 VALU each
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned total = (unsigned)batch * p.dst_h * qw;
   if (gid >= total) return;
-  const int q = (int)(gid % qw);
-  const int y = (int)((gid / qw) % p.dst_h);
-  const int b = (int)(gid / ((long)qw * p.dst_h));
+  const unsigned row = gid / (unsigned)qw;
+  const int q = (int)(gid - row * qw);
+  const int b = (int)(row / (unsigned)p.dst_h);
+  const int y = (int)(row - (unsigned)b * p.dst_h);
   const uint8_t* s = src + (long)b * p.src_batch_stride;
   const float sx_scale = (float)p.src_w / (float)p.reg_w;
   const float sy_scale = (float)p.src_h / (float)p.reg_h;
@@ -162,6 +164,7 @@ TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src
   PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
                reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
   const long total = (long)batch * dst_h * ((dst_w + 3) / 4);
+  if (total >= (1L << 31)) return (int)hipErrorInvalidValue;  // the kernel's 32-bit index math
   const int bs = 256;
   dim3 grid((unsigned)((total + bs - 1) / bs));
   const uint8_t* s = (const uint8_t*)src;

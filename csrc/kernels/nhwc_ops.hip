@@ -19,12 +19,14 @@ __device__ __forceinline__ void bf16x8_max(uint4& acc, const uint4& v) {
 __global__ void __launch_bounds__(256) maxpool_kernel(const __hip_bfloat16* __restrict__ in, int B, int H, int W,
                                                       int C, int ldi, int ci_off, int k, int s, int p, int Ho, int Wo,
                                                       __hip_bfloat16* __restrict__ out, int ldo, int co_off) {
-  const int c8 = C / 8;
-  const long total = (long)B * Ho * Wo * c8;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  // 32-bit index math (host guarantees total < 2^31): 64-bit div/mod is ~150 VALU each
+  const unsigned c8 = C / 8;
+  const unsigned total = (unsigned)B * Ho * Wo * c8;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int cv = (int)(t % c8);
-    const long pix = t / c8;
-    const int x = (int)(pix % Wo), y = (int)((pix / Wo) % Ho), b = (int)(pix / ((long)Wo * Ho));
+    const unsigned pix = t / c8;
+    const unsigned yx = pix % ((unsigned)Wo * Ho);
+    const int x = (int)(yx % (unsigned)Wo), y = (int)(yx / (unsigned)Wo), b = (int)(pix / ((unsigned)Wo * Ho));
     uint4 acc = make_uint4(0, 0, 0, 0);
     bool first = true;
     for (int dy = 0; dy < k; ++dy) {
@@ -37,22 +39,23 @@ __global__ void __launch_bounds__(256) maxpool_kernel(const __hip_bfloat16* __re
         if (first) { acc = v; first = false; } else bf16x8_max(acc, v);
       }
     }
-    *reinterpret_cast<uint4*>(out + pix * ldo + co_off + cv * 8) = acc;
+    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * 8) = acc;
   }
 }
 
 __global__ void __launch_bounds__(256) upsample2x_kernel(const __hip_bfloat16* __restrict__ in, int B, int H, int W,
                                                          int C, int ldi, int ci_off,
                                                          __hip_bfloat16* __restrict__ out, int ldo, int co_off) {
-  const int c8 = C / 8;
+  const unsigned c8 = C / 8;
   const int Ho = 2 * H, Wo = 2 * W;
-  const long total = (long)B * Ho * Wo * c8;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const unsigned total = (unsigned)B * Ho * Wo * c8;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int cv = (int)(t % c8);
-    const long pix = t / c8;
-    const int x = (int)(pix % Wo), y = (int)((pix / Wo) % Ho), b = (int)(pix / ((long)Wo * Ho));
+    const unsigned pix = t / c8;
+    const unsigned yx = pix % ((unsigned)Wo * Ho);
+    const int x = (int)(yx % (unsigned)Wo), y = (int)(yx / (unsigned)Wo), b = (int)(pix / ((unsigned)Wo * Ho));
     const uint4 v = *reinterpret_cast<const uint4*>(in + (((long)b * H + y / 2) * W + x / 2) * ldi + ci_off + cv * 8);
-    *reinterpret_cast<uint4*>(out + pix * ldo + co_off + cv * 8) = v;
+    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * 8) = v;
   }
 }
 
@@ -64,6 +67,7 @@ TCA_API int tca_maxpool_nhwc(const void* in, int B, int H, int W, int C, int ldi
                              int ldo, int co_off, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
+  if ((long)B * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
   maxpool_kernel<<<grid_for((long)B * H * W * (C / 8)), 256, 0, stream>>>(
       (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, k, 1, k / 2, H, W, (__hip_bfloat16*)out, ldo, co_off);
   TCA_LAUNCH_CHECK();
@@ -74,6 +78,7 @@ TCA_API int tca_maxpool2d_nhwc(const void* in, int B, int H, int W, int C, int l
                                void* out, int Ho, int Wo, int ldo, int co_off, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7) || s < 1 || k < 1) return (int)hipErrorInvalidValue;
+  if ((long)B * Ho * Wo * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
   maxpool_kernel<<<grid_for((long)B * Ho * Wo * (C / 8)), 256, 0, stream>>>(
       (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, k, s, p, Ho, Wo, (__hip_bfloat16*)out, ldo, co_off);
   TCA_LAUNCH_CHECK();
@@ -83,6 +88,7 @@ TCA_API int tca_upsample2x_nhwc(const void* in, int B, int H, int W, int C, int 
                                 int co_off, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
+  if ((long)B * 4 * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
   upsample2x_kernel<<<grid_for((long)B * 4 * H * W * (C / 8)), 256, 0, stream>>>(
       (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, (__hip_bfloat16*)out, ldo, co_off);
   TCA_LAUNCH_CHECK();

@@ -71,26 +71,58 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
   }
   const float b_my0 = bias[r], b_my1 = bias[32 + r];
 
-  const long nv = (long)batch * max_voxels;
-  for (long v = wave; v < nv; v += nwaves) {
-    const int b = (int)(v / max_voxels), vid = (int)(v - (long)b * max_voxels);
-    if (vid >= voxel_count[b]) continue;
-    int n;
-    float p[4] = {0.f, 0.f, 0.f, 0.f};
-    if (FROM_SLOTS) {
-      n = min(vcount[v], P);
-      if (r < n) {
-        const int idx = slots[v * P + r];
-        const float* src = pts + ((long)b * max_pts + idx) * pstride;
-        p[0] = src[0]; p[1] = src[1]; p[2] = src[2]; p[3] = src[3];
-      }
-    } else {
-      n = min(num_points[v], P);
-      if (r < n) {
-        const float* src = voxels + (v * P + r) * 4;
-        p[0] = src[0]; p[1] = src[1]; p[2] = src[2]; p[3] = src[3];
-      }
+  // 32-bit pillar indices (B * max_voxels < 2^31): 64-bit div/mod is ~150 VALU.
+  // The pillar walk is wave-uniform (readfirstlane), so counts, coords and the
+  // frame's voxel_count are scalar loads, and the two per-lane vector loads
+  // (slot row, point) are issued unconditionally from clamped addresses: hipcc
+  // can then wait for just the current point (vmcnt(1)) while the next
+  // pillar's slot row is in flight, instead of draining with vmcnt(0).
+  const int nv = batch * max_voxels;
+  const int step = __builtin_amdgcn_readfirstlane((int)nwaves);
+  auto next_valid = [&](int vv) {
+    while (vv < nv) {
+      const int bb = (unsigned)vv / (unsigned)max_voxels;
+      if (vv - bb * max_voxels < voxel_count[bb]) break;
+      vv += step;
     }
+    return vv;
+  };
+  const bool vec4 = (pstride & 3) == 0;
+  const int rs = min(r, P - 1);
+  // Two-deep pipeline: slot rows are loaded two pillars ahead and points one
+  // pillar ahead, so both dependent loads have a whole pillar of compute to land.
+  auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[(long)min(vv, nv - 1) * P + rs] : 0; };
+  auto gather = [&](int vv, int id, float (&q)[4]) {
+    const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
+    const bool real_ = r < min(vc_, P);
+    const int bb = (unsigned)min(vv, nv - 1) / (unsigned)max_voxels;
+    const float* src = FROM_SLOTS ? pts + ((long)bb * max_pts + (real_ ? id : 0)) * pstride
+                                  : voxels + ((long)min(vv, nv - 1) * P + rs) * 4;
+    if (!FROM_SLOTS || vec4) {
+      const float4 t = *reinterpret_cast<const float4*>(src);
+      q[0] = t.x; q[1] = t.y; q[2] = t.z; q[3] = t.w;
+    } else {
+      q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
+    }
+  };
+  int v = next_valid(__builtin_amdgcn_readfirstlane((int)wave));
+  int vn = v < nv ? next_valid(v + step) : nv;
+  float pc[4];
+  gather(v, slot_of(v), pc);
+  int idx_n = slot_of(vn);
+  while (v < nv) {
+    const int b = (unsigned)v / (unsigned)max_voxels;
+    const int vc = FROM_SLOTS ? vcount[v] : num_points[v];
+    const int4 co = *reinterpret_cast<const int4*>(coords + (long)v * 4);
+    const int n = min(vc, P);
+    const bool real = r < n;
+    const int vnn = vn < nv ? next_valid(vn + step) : nv;
+    const int idx_nn = slot_of(vnn);  // two ahead
+    float pn[4];
+    gather(vn, idx_n, pn);            // one ahead
+    float p[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = real ? pc[k] : 0.f;
     // pillar mean over the n real points (sum within each 32-lane half)
     float sx = p[0], sy = p[1], sz = p[2];
 #pragma unroll
@@ -101,12 +133,10 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     }
     const float inv_n = 1.f / (float)max(n, 1);
     const float mx = sx * inv_n, my = sy * inv_n, mz = sz * inv_n;
-    const int* co = coords + v * 4;
-    const float xc = (float)co[3] * g.vx + (g.vx * 0.5f + g.r0);
-    const float yc = (float)co[2] * g.vy + (g.vy * 0.5f + g.r1);
-    const float zc = (float)co[1] * g.vz + (g.vz * 0.5f + g.r2);
+    const float xc = (float)co.w * g.vx + (g.vx * 0.5f + g.r0);
+    const float yc = (float)co.z * g.vy + (g.vy * 0.5f + g.r1);
+    const float zc = (float)co.y * g.vz + (g.vz * 0.5f + g.r2);
     float f[8];
-    const bool real = r < n;
     if (h == 0) {
       f[0] = p[0]; f[1] = p[1]; f[2] = p[2]; f[3] = p[3];
       f[4] = p[0] - mx; f[5] = p[1] - my; f[6] = p[2] - mz; f[7] = p[0] - xc;
@@ -144,10 +174,15 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const float val = fmaxf((h == 0 ? m[0] + b_my0 : m[1] + b_my1), 0.f);
     const int ch = 32 * h + r;
     if (canvas) {
-      const long cell = ((long)b * g.ny + co[2]) * g.nx + co[3];
+      const long cell = ((long)b * g.ny + co.z) * g.nx + co.w;
       canvas[cell * 64 + ch] = __float2bfloat16(val);
     }
-    if (feat_out) feat_out[v * 64 + ch] = val;
+    if (feat_out) feat_out[(long)v * 64 + ch] = val;
+    v = vn;
+    vn = vnn;
+    idx_n = idx_nn;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pc[k] = pn[k];
   }
 }
 

@@ -157,7 +157,18 @@ __global__ void __launch_bounds__(kBlock) vox_insert_kernel(const int* __restric
   atomicAdd(&vcount[v], 1);
   int* s = slots + v * P;
   int val = i;
-  for (int k = 0; k < P; ++k) {
+  // Slot values only ever decrease and the list stays sorted, so a slot seen
+  // holding a smaller index holds one forever: binary-search the first slot
+  // not yet known to be smaller (log2 P dependent loads instead of a walk of
+  // up to P), and leave at once when even the last slot is smaller (the point
+  // is not among its voxel's first P).
+  int lo = 0, hi = P;  // invariant: s[0 .. lo) < val was observed
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (__hip_atomic_load(&s[mid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < val) lo = mid + 1;
+    else hi = mid;
+  }
+  for (int k = lo; k < P; ++k) {
     const int cur = __hip_atomic_load(&s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur < val) continue;  // slot already (permanently) holds a smaller index
     const int old = atomicMin(&s[k], val);
@@ -209,6 +220,154 @@ __global__ void __launch_bounds__(256) vox_gather_reset_kernel(
     if (c < 0) continue;
     cell_first[(long)b * cells + c] = kEmpty;
     cell_vid[(long)b * cells + c] = -1;
+  }
+}
+
+// ---- stage c, CSR form -------------------------------------------------------
+// Sorted first-P slot lists without the atomicMin carry chain.  The chain
+// makes each point walk its voxel's slots with dependent device-scope atomics
+// (resolved at the memory side on this part, ~1-2 us each), so one dense
+// pillar's chain sets the kernel time.  Instead, a counting sort:
+//  c1) per point: vcount[vid]++ (no-return atomic)
+//  c2) per frame: exclusive scan of vcount -> offs, cursor = offs
+//  c3) per point: csr[atomicAdd(cursor[vid], 1)] = i (one round trip)
+//  c4) per voxel: count <= 8 (~95% of pillars) -> 8-wide sorting network in
+//      registers; denser voxels are listed and
+//  c5) one wave per dense voxel keeps the smallest min(count, P) indices by
+//      64-lane bitonic sort + merge over 64-index chunks.
+__global__ void __launch_bounds__(kBlock) vox_count_kernel(const int* __restrict__ point_cell, int max_pts,
+                                                           const int* __restrict__ npts, long cells,
+                                                           const int* __restrict__ cell_vid, int max_voxels,
+                                                           int* __restrict__ vcount) {
+  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npts[b] || i >= max_pts) return;
+  const int c = point_cell[(long)b * max_pts + i];
+  if (c < 0) return;
+  const int vid = cell_vid[(long)b * cells + c];
+  if (vid >= 0) atomicAdd(&vcount[(long)b * max_voxels + vid], 1);
+}
+
+constexpr int kScanT = 1024;
+
+__global__ void __launch_bounds__(kScanT) vox_scan_kernel(const int* __restrict__ voxel_count, int max_voxels,
+                                                          const int* __restrict__ vcount, int* __restrict__ offs,
+                                                          int* __restrict__ cursor, int* __restrict__ dense_count) {
+  __shared__ int s_w[kScanT / 64];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int n = voxel_count[b];
+  const int per = (n + kScanT - 1) / kScanT;
+  const int lo = min(t * per, n), hi = min(lo + per, n);
+  const int* vc = vcount + (long)b * max_voxels;
+  int sum = 0;
+  for (int v = lo; v < hi; ++v) sum += vc[v];
+  const int incl = wave_incl_sum(sum);
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  int wbase = 0;
+  for (int w = 0; w < wid; ++w) wbase += s_w[w];
+  int run = wbase + incl - sum;
+  int* ob = offs + (long)b * (max_voxels + 1);
+  int* cb = cursor + (long)b * max_voxels;
+  for (int v = lo; v < hi; ++v) {
+    ob[v] = run;
+    cb[v] = run;
+    run += vc[v];
+  }
+  if (t == kScanT - 1) ob[n] = run;
+  if (t == 0) dense_count[b] = 0;
+}
+
+__global__ void __launch_bounds__(kBlock) vox_fill_kernel(const int* __restrict__ point_cell, int max_pts,
+                                                          const int* __restrict__ npts, long cells,
+                                                          const int* __restrict__ cell_vid, int max_voxels,
+                                                          int* __restrict__ cursor, int* __restrict__ csr) {
+  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npts[b] || i >= max_pts) return;
+  const int c = point_cell[(long)b * max_pts + i];
+  if (c < 0) return;
+  const int vid = cell_vid[(long)b * cells + c];
+  if (vid < 0) return;
+  const int pos = atomicAdd(&cursor[(long)b * max_voxels + vid], 1);
+  csr[(long)b * max_pts + pos] = i;
+}
+
+__device__ __forceinline__ void cswap(int& a, int& b) {
+  const int lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
+__global__ void __launch_bounds__(kBlock) vox_sort_small_kernel(int max_voxels, int max_pts, int P,
+                                                                const int* __restrict__ voxel_count,
+                                                                const int* __restrict__ vcount,
+                                                                const int* __restrict__ offs,
+                                                                const int* __restrict__ csr, int* __restrict__ slots,
+                                                                int* __restrict__ dense, int* __restrict__ dense_count) {
+  const int b = blockIdx.y, vid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (vid >= voxel_count[b]) return;
+  const long g = (long)b * max_voxels + vid;
+  const int c = vcount[g];
+  if (c > 8) {
+    dense[(long)b * max_voxels + atomicAdd(&dense_count[b], 1)] = vid;
+    return;
+  }
+  const int* src = csr + (long)b * max_pts + offs[(long)b * (max_voxels + 1) + vid];
+  int a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = k < c ? src[k] : kEmpty;
+  // Batcher odd-even merge sort, 19 comparators (static indices: registers only)
+  cswap(a[0], a[1]); cswap(a[2], a[3]); cswap(a[4], a[5]); cswap(a[6], a[7]);
+  cswap(a[0], a[2]); cswap(a[1], a[3]); cswap(a[4], a[6]); cswap(a[5], a[7]);
+  cswap(a[1], a[2]); cswap(a[5], a[6]); cswap(a[0], a[4]); cswap(a[3], a[7]);
+  cswap(a[1], a[5]); cswap(a[2], a[6]); cswap(a[1], a[4]); cswap(a[3], a[6]);
+  cswap(a[2], a[4]); cswap(a[3], a[5]); cswap(a[3], a[4]);
+  int* s = slots + g * P;
+  const int m = min(c, P);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < m) s[k] = a[k];
+}
+
+__device__ __forceinline__ int bitonic_sort64(int v, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int o = __shfl_xor(v, j, 64);
+      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+      v = (lower == up) ? min(v, o) : max(v, o);
+    }
+  return v;
+}
+
+__global__ void __launch_bounds__(256) vox_sort_dense_kernel(int max_voxels, int max_pts, int P,
+                                                             const int* __restrict__ vcount,
+                                                             const int* __restrict__ offs,
+                                                             const int* __restrict__ csr, const int* __restrict__ dense,
+                                                             const int* __restrict__ dense_count,
+                                                             int* __restrict__ slots) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int nd = dense_count[b];
+  for (int d = wave; d < nd; d += nwaves) {
+    const int vid = dense[(long)b * max_voxels + d];
+    const long g = (long)b * max_voxels + vid;
+    const int c = vcount[g];
+    const int* src = csr + (long)b * max_pts + offs[(long)b * (max_voxels + 1) + vid];
+    int best = kEmpty;  // ascending across lanes: the 64 smallest so far
+    for (int base = 0; base < c; base += 64) {
+      int v = base + lane < c ? src[base + lane] : kEmpty;
+      v = bitonic_sort64(v, lane);
+      // smallest 64 of two ascending runs: min(best[l], v[63 - l]) is bitonic; clean it
+      int m = min(best, __shfl(v, 63 - lane, 64));
+#pragma unroll
+      for (int j = 32; j > 0; j >>= 1) {
+        const int o = __shfl_xor(m, j, 64);
+        m = (lane & j) == 0 ? min(m, o) : max(m, o);
+      }
+      best = m;
+    }
+    if (lane < min(c, P)) slots[g * P + lane] = best;
   }
 }
 
@@ -279,8 +438,9 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
                                                          block_count);
     vox_assign_kernel<<<sgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g, cell_first, bpf, block_count,
                                                     max_voxels, cell_vid, coords, voxel_count);
-    vox_insert_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g.cells, cell_vid, max_voxels, P,
-                                                    vcount, slots);
+    if (!(mode & 4))
+      vox_insert_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g.cells, cell_vid, max_voxels, P,
+                                                      vcount, slots);
   }
   if ((mode & 2) && !gather && (P & 3) == 0) {
     vox_slot_reset_kernel<<<dim3((max_voxels * (P / 4) + 255) / 256, batch), 256, 0, stream>>>(
@@ -292,5 +452,27 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
                                                                num_points, point_cell, g.cells, cell_first, cell_vid,
                                                                gather);
   }
+  TCA_LAUNCH_CHECK();
+}
+
+// Stage c in CSR form (see vox_count_kernel): run after tca_voxelize(mode 1 | 4).
+// Scratch: offs int[B*(V+1)], cursor int[B*V], csr int[B*max_points],
+// dense int[B*V], dense_count int[B].  Requires P <= 64.
+TCA_API int tca_vox_slots_csr(const int* point_cell, int max_points, const int* npts, int batch, const int* grid,
+                              const int* cell_vid, int max_voxels, int P, const int* voxel_count, int* vcount,
+                              int* offs, int* cursor, int* csr, int* dense, int* dense_count, int* slots,
+                              hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (P > 64 || P < 1) return (int)hipErrorInvalidValue;
+  const long cells = (long)grid[0] * grid[1] * grid[2];
+  dim3 pgrid((max_points + kBlock - 1) / kBlock, batch);
+  vox_count_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, cells, cell_vid, max_voxels, vcount);
+  vox_scan_kernel<<<batch, kScanT, 0, stream>>>(voxel_count, max_voxels, vcount, offs, cursor, dense_count);
+  vox_fill_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, cells, cell_vid, max_voxels, cursor,
+                                                csr);
+  vox_sort_small_kernel<<<dim3((max_voxels + kBlock - 1) / kBlock, batch), kBlock, 0, stream>>>(
+      max_voxels, max_points, P, voxel_count, vcount, offs, csr, slots, dense, dense_count);
+  vox_sort_dense_kernel<<<dim3(64, batch), 256, 0, stream>>>(max_voxels, max_points, P, vcount, offs, csr, dense,
+                                                             dense_count, slots);
   TCA_LAUNCH_CHECK();
 }

@@ -166,6 +166,43 @@ def test_voxelize_gpu_exact(cuda, vcfg):
             np.testing.assert_array_equal(v[b, :k].cpu().numpy(), rv)
 
 
+@pytest.mark.parametrize("vcfg", [KITTI_PILLARS, KITTI_SECOND_VOXELS])
+def test_voxelize_gpu_dense_voxels(cuda, vcfg):
+    """Clustered clouds: voxels with 9..300 points exercise the dense-voxel
+    (wave bitonic top-P) path of the CSR slot sort; slot order must still be
+    the first P points in point order (spconv)."""
+    cfg = dataclasses.replace(vcfg, max_voxels=3000)
+    rng = np.random.default_rng(7)
+    r = np.asarray(cfg.point_cloud_range, np.float32)
+    vs = np.asarray(cfg.voxel_size, np.float32)
+    B, N = 2, 6000
+    nf = cfg.num_point_features
+    pts = np.zeros((B, N, nf), np.float32)
+    for b in range(B):
+        p = rng.uniform(r[:3], r[3:], size=(N, 3)).astype(np.float32)
+        # pile points into a few voxels: 300, 130, 65, 20, 9 points
+        start = 0
+        for k, m in enumerate((300, 130, 65, 20, 9)):
+            centre = r[:3] + vs * (np.array([10 + 7 * k, 12 + 3 * b, 0]) + 0.5)
+            p[start:start + m] = centre + rng.uniform(-0.4, 0.4, size=(m, 3)).astype(np.float32) * vs
+            start += m
+        perm = rng.permutation(N)
+        pts[b, :, :3] = p[perm]
+        pts[b, :, 3] = rng.uniform(0, 1, N)
+    cnt = np.array([N, N - 1000], np.int32)
+    vox = Voxelizer(cfg, B, N, device=cuda, nfeat=nf)
+    for rep in range(2):
+        v, c, n, vc = vox(torch.from_numpy(pts).to(cuda), torch.from_numpy(cnt).to(cuda))
+        torch.cuda.synchronize()
+        for b in range(B):
+            rv, rcoord, rn, _ = voxelize_np(pts[b, :cnt[b]], cfg, nf)
+            k = int(vc[b])
+            assert k == len(rn) and rn.max() == cfg.max_points_per_voxel
+            np.testing.assert_array_equal(c[b, :k, 1:].cpu().numpy(), rcoord)
+            np.testing.assert_array_equal(n[b, :k].cpu().numpy(), rn)
+            np.testing.assert_array_equal(v[b, :k].cpu().numpy(), rv)
+
+
 def test_pillar_vfe_gpu_vs_fp32(cuda):
     cfg = dataclasses.replace(KITTI_PILLARS, max_voxels=6000)
     B, N = 2, 30000

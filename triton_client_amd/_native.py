@@ -55,6 +55,7 @@ _KERNEL_SIGS = {
     "tca_yolov4_decode": [P, P, P, I, I, I, P, P, P, F, F, I, I, P, P, P, P, P, P, P, I, P],
     "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, P],
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, P],
+    "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, P],
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
 }
 

@@ -149,11 +149,32 @@ class Voxelizer:
             self.coords = g("coords", (batch, V, 4), torch.int32, init=0)
             self.num_points = g("num_points", (batch, V), torch.int32, init=0)
             self.voxel_count = g("voxel_count", (batch,), torch.int32, init=0)
+            # stage c as a counting sort (tca_vox_slots_csr) when P <= 64
+            self.csr_slots = P <= 64
+            if self.csr_slots:
+                self.offs = g("offs", (batch, V + 1), torch.int32)
+                self.cursor = g("cursor", (batch, V), torch.int32)
+                self.csr = g("csr", (batch, max_points), torch.int32)
+                self.dense = g("dense", (batch, V), torch.int32)
+                self.dense_count = g("dense_count", (batch,), torch.int32)
             self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
             self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
             self._grid = _carr(ctypes.c_int, cfg.grid_size)
 
     def _launch(self, points, npts, mode, gather, stream):
+        if (mode & 1) and self.csr_slots:
+            self._launch_raw(points, npts, 1 | 4, False, stream)  # a, b1, b2 only
+            P = _native.ptr
+            _native.call("tca_vox_slots_csr", P(self.point_cell), self.max_points, P(npts), points.shape[0],
+                         self._grid, P(self.cell_vid), self.cfg.max_voxels, self.cfg.max_points_per_voxel,
+                         P(self.voxel_count), P(self.vcount), P(self.offs), P(self.cursor), P(self.csr),
+                         P(self.dense), P(self.dense_count), P(self.slots), _native.stream_ptr(stream))
+            mode &= ~1
+            if not mode:
+                return
+        self._launch_raw(points, npts, mode, gather, stream)
+
+    def _launch_raw(self, points, npts, mode, gather, stream):
         cfg = self.cfg
         _native.call("tca_voxelize", _native.ptr(points), points.shape[-1], self.max_points, _native.ptr(npts),
                      points.shape[0], self._range, self._vsize, self._grid, cfg.max_points_per_voxel,
