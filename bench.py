@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
+    ap.add_argument("--graph-mode", choices=["split", "fork"], default="fork",
+                    help="split: one hipGraph per branch, replayed on two streams; fork: one graph with two "
+                         "forked branches")
     ap.add_argument("--only", choices=["both", "camera", "lidar"], default="both")
     ap.add_argument("--camera-model", choices=["yolov5n", "yolov4", "retinanet", "fcos"], default="yolov5n",
                     help="2D detector: YOLOv5n-640 (headline) or Detectron2 RetinaNet / FCOS R50-FPN at 800x1344")
@@ -183,7 +186,29 @@ def main():
         main.wait_stream(side)
         return r2, r3
 
-    runner = GraphRunner(pipeline_step, enabled=not args.no_graph)
+    if side is not None and args.graph_mode == "split" and not args.no_graph:
+        # one graph per branch, each replayed on its own stream (its own HW queue):
+        # the overlap no longer depends on how the runtime maps a forked graph's
+        # branches onto queues
+        cam_runner = GraphRunner(cam.step)
+        lid_runner = GraphRunner(lid.step)
+
+        def split_step():
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                r3 = lid_runner()
+            r2 = cam_runner()
+            main.wait_stream(side)
+            return r2, r3
+
+        class _Split:
+            def __call__(self):
+                return split_step()
+
+        runner = _Split()
+    else:
+        runner = GraphRunner(pipeline_step, enabled=not args.no_graph)
     ex = FrameExchange(info)
 
     dsts = [t for t in ((cam.frames,) if use_cam else ()) + ((lid.data, lid.frame_n) if use_lid else ())]
@@ -326,6 +351,7 @@ def main():
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,
                 "branch_streams": 2 if side is not None else 1,
+                "graph_mode": args.graph_mode if side is not None else "single",
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "avg_2d_dets_per_frame": det2,
                 "avg_3d_dets_per_frame": det3,

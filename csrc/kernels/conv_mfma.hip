@@ -510,7 +510,7 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   // auto tile (measured on MI355X, tools/bench_conv.py -> profiles/conv_tiles_r1.md):
   // v2 (glds, 8 waves): 128x64 for N <= 64; 128x128 (4x2 waves) for wide-M layers,
   // 64x128 (2x4 waves) when M is small; v1 (register staging) when Cin % 64 != 0
-  if (tile == 0) tile = N <= 32 ? 1 : v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 64 ? 2 : 5);
+  if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 64 ? 2 : 5);
   if (tile >= 10 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 11: return launch_glds<128, 64, 4, 1>(a, stream);
@@ -546,6 +546,8 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
     case 43: return launch_glds<128, 128, 2, 2, 3, true>(a, stream);   // 4 waves
     case 44: return launch_glds<128, 64, 2, 2, 3, true>(a, stream);    // 4 waves
     case 1: return launch<128, 32, 4, 1>(a, stream);
+    case 6: return launch<128, 16, 4, 1>(a, stream);  // N <= 16 (YOLOv5n stem / C3 inner convs)
+    case 7: return launch<256, 16, 4, 1>(a, stream);
     case 2: return launch<128, 64, 4, 1>(a, stream);
     case 3: return launch<128, 128, 2, 2>(a, stream);
     case 4: return launch<256, 64, 4, 1>(a, stream);

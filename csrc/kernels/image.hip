@@ -149,6 +149,66 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
   }
 }
 
+// One resized / letterboxed / quantised RGB sample of destination pixel (y, x)
+// (before the affine), channel order of the source (swap handled by the caller).
+__device__ __forceinline__ void sample_px(const PrepParams& p, const uint8_t* s, int y, int x, float (&o)[3]) {
+  const int ly = y - p.reg_top, lx = x - p.reg_left;
+  if (ly < 0 || ly >= p.reg_h || lx < 0 || lx >= p.reg_w) {
+    o[0] = o[1] = o[2] = p.pad_value;
+    return;
+  }
+  int y0, y1, x0, x1;
+  float ay, ax;
+  coord((float)ly, (float)p.src_h / (float)p.reg_h, p.src_h, y0, y1, ay);
+  coord((float)lx, (float)p.src_w / (float)p.reg_w, p.src_w, x0, x1, ax);
+  const uint8_t* r0 = s + (long)y0 * p.src_row_stride;
+  const uint8_t* r1 = s + (long)y1 * p.src_row_stride;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v00 = r0[x0 * p.src_c + c], v01 = r0[x1 * p.src_c + c];
+    const float v10 = r1[x0 * p.src_c + c], v11 = r1[x1 * p.src_c + c];
+    const float top = v00 + ax * (v01 - v00);
+    const float bot = v10 + ax * (v11 - v10);
+    float v = top + ay * (bot - top);
+    if (p.quantize_u8) v = fminf(fmaxf(rintf(v), 0.f), 255.f);
+    o[c] = v;
+  }
+}
+
+// Layout 2: space-to-depth 2x2, bf16 [B, H/2, W/2, 16]: channel (dy*2 + dx)*3 + c
+// holds pixel (2Y + dy, 2X + dx), channels 12..15 zero.  A k=6 s=2 p=2 stem
+// conv (YOLOv5 v6+) is exactly a 3x3 s=1 p=1 conv over this tensor with
+// rearranged weights (models/fast.py), with 12 of 16 input channels real
+// instead of 3 of 8 and half the input bytes.  One thread per 2x2 block,
+// two 16-B stores.
+__global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict__ src,
+                                                       __hip_bfloat16* __restrict__ dst, PrepParams p, int batch) {
+  const int h2 = p.dst_h >> 1, w2 = p.dst_w >> 1;
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned total = (unsigned)batch * h2 * w2;
+  if (gid >= total) return;
+  const unsigned row = gid / (unsigned)w2;
+  const int X = (int)(gid - row * w2);
+  const int b = (int)(row / (unsigned)h2);
+  const int Y = (int)(row - (unsigned)b * h2);
+  const uint8_t* s = src + (long)b * p.src_batch_stride;
+  const float sc[3] = {p.sc0, p.sc1, p.sc2};
+  const float bi[3] = {p.b0, p.b1, p.b2};
+  __hip_bfloat16 px[16];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    float o[3];
+    sample_px(p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) px[d * 3 + c] = __float2bfloat16(o[p.swap_rb ? 2 - c : c] * sc[c] + bi[c]);
+  }
+#pragma unroll
+  for (int c = 12; c < 16; ++c) px[c] = __float2bfloat16(0.f);
+  uint4* o = reinterpret_cast<uint4*>(dst + (long)gid * 16);
+  o[0] = reinterpret_cast<uint4*>(px)[0];
+  o[1] = reinterpret_cast<uint4*>(px)[1];
+}
+
 }  // namespace
 
 // Preprocess `batch` frames of identical geometry.
@@ -158,11 +218,20 @@ TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src
                                  float pad_value, int quantize_u8, float sc0, float sc1, float sc2, float b0,
                                  float b1, float b2, hipStream_t stream) {
   if (batch <= 0) return 0;
+  PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
+               reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
+  if (dst_layout == 2) {  // space-to-depth 2x2, bf16, 16 channels
+    if (src_c < 3 || dst_c != 16 || dst_dtype != kBF16 || (dst_h & 1) || (dst_w & 1) || reg_h <= 0 || reg_w <= 0)
+      return (int)hipErrorInvalidValue;
+    const long t2 = (long)batch * (dst_h / 2) * (dst_w / 2);
+    if (t2 >= (1L << 31)) return (int)hipErrorInvalidValue;
+    prep_s2d_kernel<<<(unsigned)((t2 + 255) / 256), 256, 0, stream>>>((const uint8_t*)src, (__hip_bfloat16*)dst, p,
+                                                                     batch);
+    TCA_LAUNCH_CHECK();
+  }
   if (src_c < 3 || (dst_c != 3 && dst_c != 4 && !(dst_c == 8 && dst_layout == 1 && dst_dtype != kF32)) || reg_h <= 0 ||
       reg_w <= 0)
     return (int)hipErrorInvalidValue;
-  PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
-               reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
   const long total = (long)batch * dst_h * ((dst_w + 3) / 4);
   if (total >= (1L << 31)) return (int)hipErrorInvalidValue;  // the kernel's 32-bit index math
   const int bs = 256;

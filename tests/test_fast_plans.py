@@ -26,7 +26,7 @@ def test_fast_yolo_cpu_matches_module():
     with torch.no_grad():
         ref = m(x)
     f = FastYOLOv5(m, 2, (64, 64), device="cpu")
-    f.input_view()[:, :3].copy_(x)
+    f.set_input(x)
     with torch.no_grad():
         outs = f.forward()
     for r, o in zip(ref, outs):
@@ -61,7 +61,7 @@ def test_fast_plans_gpu_vs_fp32(cuda):
     with torch.no_grad():
         ref = m(x)
     f = FastYOLOv5(m, 2, (128, 128), device=cuda)
-    f.input_view()[:, :3].copy_(x.to(cuda))
+    f.set_input(x.to(cuda))
     outs = f.forward()
     torch.cuda.synchronize()
     for r, o in zip(ref, outs):

@@ -68,6 +68,19 @@ def _random_candidates(B, cap, n, D, rotated, seed):
     return box, score, cls, key, count
 
 
+@pytest.mark.parametrize("mode", ["letterbox", "stretch"])
+def test_preprocess_s2d_gpu(cuda, mode):
+    """Space-to-depth output = space_to_depth2 of the plain NHWC output, bit-exact."""
+    from triton_client_amd.ops.image import space_to_depth2
+    rng = np.random.default_rng(3)
+    frames = torch.from_numpy(rng.integers(0, 256, size=(2, 180, 322, 3), dtype=np.uint8)).to(cuda)
+    ref, _ = preprocess(frames, (96, 128), mode, "COCO", torch.bfloat16, "NHWC", 3, swap_rb=True)
+    got, _ = preprocess(frames, (96, 128), mode, "COCO", torch.bfloat16, "S2D", swap_rb=True)
+    torch.cuda.synchronize()
+    exp = space_to_depth2(ref.permute(0, 2, 3, 1).contiguous())
+    assert torch.equal(got.cpu(), exp.cpu())
+
+
 @pytest.mark.parametrize("rotated,agnostic", [(False, False), (True, True), (True, False)])
 @pytest.mark.parametrize("pre_max", [64, 1000, 4096])
 def test_sort_nms_gpu_vs_golden(cuda, rotated, agnostic, pre_max):
@@ -278,6 +291,23 @@ def test_fused_conv_vs_fp32(cuda, cin, cout, k, s, p, act):
     r = ref.tensor()[..., :cout]
     err = (got[..., :cout] - r).abs().max().item()
     assert err < 0.02 * max(1.0, r.abs().max().item()), err
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7])
+def test_fused_conv_v1_tiles(cuda, tile):
+    """v1 (register-staged) tiles incl. the N=16 ones, with N / M tails and Cin % 32 != 0."""
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(tile)
+    for cin, cout, k, s in ((16, 16, 3, 1), (24, 40, 3, 2), (16, 72, 1, 1)):
+        conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=True)
+        fc = FusedConv(conv, act=2, device=cuda)
+        x = torch.randn(2, 23, 31, cin)
+        y = fc(NHWC(x.to(cuda, torch.bfloat16)), tile=tile)
+        torch.cuda.synchronize()
+        ref = torch.nn.functional.silu(conv(x.to(torch.bfloat16).float().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
+        err = (y.tensor().float().cpu()[..., :cout] - ref).abs().max().item()
+        assert err < 0.03 * max(1.0, ref.abs().max().item()), (cin, cout, err)
 
 
 def test_fused_conv_slices_residual_and_transpose(cuda):

@@ -21,6 +21,7 @@ SHAPES = [
     ("pp.b3.conv", 16, 62, 54, 256, 256, 3, 1, 1),
     ("pp.head", 16, 248, 216, 384, 72, 1, 1, 0),
     ("pp.de1", 16, 248, 216, 64, 128, 1, 1, 1),
+    ("y.stem_s2d", 16, 320, 320, 16, 16, 3, 1, 2),
     ("y.b1", 16, 320, 320, 16, 32, 3, 2, 2),
     ("y.c3.3x3", 16, 160, 160, 16, 16, 3, 1, 2),
     ("y.b3", 16, 160, 160, 32, 64, 3, 2, 2),
@@ -43,7 +44,7 @@ def timeit(fn, iters=20):
 
 def main():
     dev = torch.device("cuda")
-    tiles = [int(t) for t in sys.argv[1].split(',')] if len(sys.argv) > 1 else [1, 2, 5, 20, 22, 24, 25] + list(range(31, 45))
+    tiles = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 2, 5, 6, 7, 20, 22, 24, 25, 31, 41, 42]
     for name, B, H, W, ci, co, k, s, act in SHAPES:
         conv = nn.Conv2d(ci, co, k, s, k // 2, bias=True).to(dev)
         fc = FusedConv(conv, act=act, device=dev)

@@ -74,16 +74,35 @@ class _C3Plan:
 
 
 class FastYOLOv5:
+    """``s2d`` (default): the input is the 2x2 space-to-depth image
+    [B, H/2, W/2, 16] that the preprocess kernel writes directly, and the k=6
+    s=2 p=2 stem runs as the equivalent 3x3 s=1 conv over it
+    (:func:`~..ops.image.s2d_stem_weight`): 12 of 16 input channels real
+    instead of 3 of 8, half the input bytes, half the stem's MACs."""
     IN_CHANNELS = 8
 
-    def __init__(self, model, batch: int, img_hw: Tuple[int, int] = (640, 640), device="cuda"):
+    def __init__(self, model, batch: int, img_hw: Tuple[int, int] = (640, 640), device="cuda", s2d: bool = True):
         self.device = torch.device(device)
         H, W = img_hw
         B = batch
         bufs = self.bufs = _Buffers(self.device)
         m = model
-        self.x = bufs.new(B, H, W, self.IN_CHANNELS)
-        self.b0 = _fc(m.b0, device, cin_pad=self.IN_CHANNELS)
+        self.s2d = s2d and H % 2 == 0 and W % 2 == 0 and m.b0.conv.kernel_size == (6, 6) \
+            and m.b0.conv.stride == (2, 2) and m.b0.conv.padding == (2, 2)
+        if self.s2d:
+            from ..ops.image import s2d_stem_weight
+
+            assert m.b0.fused, "call fuse_model() first"
+            c0 = m.b0.conv
+            stem = nn.Conv2d(16, c0.out_channels, 3, 1, 1, bias=True)
+            with torch.no_grad():
+                stem.weight.copy_(s2d_stem_weight(c0.weight.detach().float()))
+                stem.bias.copy_(c0.bias.detach().float() if c0.bias is not None else torch.zeros(c0.out_channels))
+            self.x = bufs.new(B, H // 2, W // 2, 16)
+            self.b0 = FusedConv(stem, act=m.b0.act, device=device)
+        else:
+            self.x = bufs.new(B, H, W, self.IN_CHANNELS)
+            self.b0 = _fc(m.b0, device, cin_pad=self.IN_CHANNELS)
         self.b1, self.b3, self.b5, self.b7 = (_fc(getattr(m, n), device) for n in ("b1", "b3", "b5", "b7"))
         h2, w2 = H // 2, W // 2
         s4, s8, s16, s32 = (H // 4, W // 4), (H // 8, W // 8), (H // 16, W // 16), (H // 32, W // 32)
@@ -132,8 +151,21 @@ class FastYOLOv5:
 
     def input_view(self) -> torch.Tensor:
         """[B, 3, H, W] channels_last view of the RGB part of the input buffer
-        (what the preprocess kernel writes; channels 3..7 stay zero)."""
+        (what the preprocess kernel writes; channels 3..7 stay zero).  Not
+        available in the space-to-depth layout: use :meth:`set_input`."""
+        if self.s2d:
+            raise RuntimeError("space-to-depth input: use set_input()")
         return self.x.t.permute(0, 3, 1, 2)
+
+    def set_input(self, x: torch.Tensor) -> None:
+        """x: [B, 3, H, W] normalised image -> the plan's input buffer."""
+        if self.s2d:
+            from ..ops.image import space_to_depth2
+
+            self.x.t.copy_(space_to_depth2(x.permute(0, 2, 3, 1).to(self.x.t.device)).to(self.x.t.dtype))
+        else:
+            self.x.t.zero_()
+            self.x.t[..., :3].copy_(x.permute(0, 2, 3, 1))
 
     def forward(self) -> List[NHWC]:
         t = self.b0(self.x, out=self.t0)

@@ -65,7 +65,8 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
     """frames: [B, H, W, C>=3] uint8 (or [H, W, C]). Returns (tensor, FrameXform).
 
     layout "NCHW" → [B, C, H, W] contiguous; "NHWC" → [B, C, H, W] view of a
-    channels_last buffer (C = out_channels, 3 or 4; the 4th channel is 0).
+    channels_last buffer (C = out_channels, 3 or 4; the 4th channel is 0);
+    "S2D" → [B, H/2, W/2, 16] bf16 space-to-depth (see :func:`space_to_depth2`).
     """
     if frames.dim() == 3:
         frames = frames.unsqueeze(0)
@@ -73,6 +74,9 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
     H, W = dst_hw
     scale, bias = SCALING_PRESETS[scaling.upper()] if isinstance(scaling, str) else scaling
     xf, (top, left, nh, nw) = frame_xform((h0, w0), (H, W), mode)
+    if layout == "S2D":
+        return _preprocess_s2d(frames, (H, W), mode, scale, bias, swap_rb, pad_value, quantize_u8, out, stream,
+                               xf, (top, left, nh, nw))
     if frames.device.type == "cuda":
         frames = frames.contiguous()
         if out is None:
@@ -103,3 +107,43 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
         out.copy_(t)
         return out, xf
     return t, xf
+
+
+def space_to_depth2(x: torch.Tensor) -> torch.Tensor:
+    """[B, H, W, 3] -> [B, H/2, W/2, 16]: channel (dy*2 + dx)*3 + c = x[2Y+dy, 2X+dx, c];
+    channels 12..15 are zero.  A k=6, s=2, p=2 conv over x equals a 3x3, s=1,
+    p=1 conv over this tensor (weights: :func:`s2d_stem_weight`)."""
+    B, H, W, C = x.shape
+    assert C == 3 and H % 2 == 0 and W % 2 == 0
+    y = x.view(B, H // 2, 2, W // 2, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, H // 2, W // 2, 12)
+    return torch.cat([y, y.new_zeros(B, H // 2, W // 2, 4)], -1)
+
+
+def s2d_stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 3, 6, 6] (stride 2, pad 2) -> [Cout, 16, 3, 3] (stride 1, pad 1) over space_to_depth2 input:
+    W'[o, (dy*2+dx)*3 + c, a, b] = W[o, c, 2a + dy, 2b + dx]."""
+    co, ci, kh, kw = w.shape
+    assert ci == 3 and kh == 6 and kw == 6
+    v = w.view(co, 3, 3, 2, 3, 2)                # o, c, a, dy, b, dx
+    v = v.permute(0, 3, 5, 1, 2, 4).reshape(co, 12, 3, 3)  # o, (dy, dx, c), a, b
+    return torch.cat([v, v.new_zeros(co, 4, 3, 3)], 1)
+
+
+def _preprocess_s2d(frames, dst_hw, mode, scale, bias, swap_rb, pad_value, quantize_u8, out, stream, xf, region):
+    B, h0, w0, c0 = frames.shape
+    H, W = dst_hw
+    top, left, nh, nw = region
+    if out is None:
+        out = torch.zeros((B, H // 2, W // 2, 16), dtype=torch.bfloat16, device=frames.device)
+    if frames.device.type == "cuda":
+        frames = frames.contiguous()
+        _native.call(
+            "tca_image_preprocess", _native.ptr(frames), h0 * w0 * c0, h0, w0, w0 * c0, c0, int(swap_rb),
+            _native.ptr(out), DTYPE_CODE[torch.bfloat16], 2, 16, H, W, B, top, left, nh, nw, float(pad_value),
+            int(quantize_u8), float(scale[0]), float(scale[1]), float(scale[2]), float(bias[0]), float(bias[1]),
+            float(bias[2]), _native.stream_ptr(stream))
+        return out, xf
+    res = [golden.preprocess_image(frames[b].numpy(), (H, W), mode, scale, bias, swap_rb, pad_value, "NHWC")
+           for b in range(B)]
+    out.copy_(space_to_depth2(torch.from_numpy(np.stack(res))).to(out.dtype))
+    return out, xf

@@ -94,8 +94,12 @@ class CameraPipeline:
         """Capture-safe: reads ``self.frames``, returns the NmsResult buffers."""
         if self.use_fast:
             f = self.fast or self.build_fast()
-            preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", f.IN_CHANNELS,
-                       swap_rb=self.swap_rb, out=f.x.t.permute(0, 3, 1, 2))
+            if f.s2d:
+                preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "S2D",
+                           swap_rb=self.swap_rb, out=f.x.t)
+            else:
+                preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", f.IN_CHANNELS,
+                           swap_rb=self.swap_rb, out=f.x.t.permute(0, 3, 1, 2))
             return self.post(f.forward(), self.xform)
         preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", 3, swap_rb=self.swap_rb,
                    out=self.inp)
