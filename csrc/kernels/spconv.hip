@@ -1,0 +1,607 @@
+// Sparse 3D convolution for SECOND-IoU's VoxelBackBone8x (reference
+// examples/second_iou/1/second_iou.yaml:10-18: MeanVFE, VoxelBackBone8x,
+// HeightCompression; OpenPCDet runs them on spconv), plus SECONDHead's RoI
+// grid pooling (second_iou.yaml:109-112) and IoU rescoring.
+//
+// Data model — all frames of a batch share one row space per level:
+//   feats  [cap, C] bf16 rows; coords int4 (b, z, y, x) per row;
+//   grid   dense int32 [B, Z, Y, X] site -> row (-1 = inactive).  288 GB of
+//          HBM makes dense grids the cheap option (one load per neighbour
+//          probe, no hash walk); they are reset in O(rows) from the coord
+//          lists, never cleared densely;
+//   count  device int per level, read by every consumer kernel; grids of
+//          the launches are sized for the capacity (static shapes, graph
+//          capturable); capacities are worst-case bounds, so rows never drop.
+// Rulebook = output-stationary neighbour table nbr[row][tap] (input row or
+// -1), built once per (level, kernel) and shared by a level's SubM layers
+// (spconv's indice_key), plus one 32-bit tap mask per 64-row tile.
+// GEMM = implicit gather-GEMM on MFMA 16x16x32 bf16: K = taps x Cin, A rows
+// gathered through the staged neighbour table (zero for -1), K steps whose
+// taps are empty for the whole tile are skipped, BN folded, ReLU fused,
+// persistent tile loop over the device row count.  The last layer's
+// epilogue scatters straight into the NHWC BEV map (HeightCompression) at
+// channel z*Cout + c (the 2D backbone's first conv is permuted to match), so
+// the dense [B, C, D, H, W] tensor never exists.
+#include "tca_common.h"
+
+using namespace tca;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+struct Dims {
+  int z, y, x;
+};
+struct Ksp {  // kernel / stride / padding per (z, y, x)
+  int kz, ky, kx, sz, sy, sx, pz, py, px;
+};
+
+__device__ __forceinline__ long site(const int4& c, const Dims& d) {
+  return (((long)c.x * d.z + c.y) * d.y + c.z) * d.x + c.w;
+}
+
+// ---- level 0: MeanVFE + coords + grid ------------------------------------------
+__global__ void sp_offsets_kernel(const int* __restrict__ voxel_count, int batch, int* __restrict__ off,
+                                  int* __restrict__ total) {
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int b = 0; b < batch; ++b) {
+      off[b] = s;
+      s += voxel_count[b];
+    }
+    *total = s;
+  }
+}
+
+// From the voxeliser's sorted slot lists (pipeline path: the [V, P, F] voxel
+// tensor is never materialised).  One thread per (frame, voxel).
+__global__ void __launch_bounds__(256) sp_vfe_slots_kernel(
+    const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ slots,
+    const int* __restrict__ vcount, int P, const int* __restrict__ vox_coords, const int* __restrict__ voxel_count,
+    int max_voxels, const int* __restrict__ off, Dims g0, __hip_bfloat16* __restrict__ feats,
+    int4* __restrict__ coords0, int* __restrict__ grid0) {
+  const int b = blockIdx.y, vid = blockIdx.x * 256 + threadIdx.x;
+  if (vid >= voxel_count[b]) return;
+  const long g = (long)b * max_voxels + vid;
+  const int m = min(vcount[g], P);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int k = 0; k < m; ++k) {
+    const float4 p = *reinterpret_cast<const float4*>(pts + ((long)b * max_pts + slots[g * P + k]) * pstride);
+    s0 += p.x; s1 += p.y; s2 += p.z; s3 += p.w;
+  }
+  const float inv = 1.f / (float)max(m, 1);
+  const int row = off[b] + vid;
+  __hip_bfloat16 f[8];
+  f[0] = __float2bfloat16(s0 * inv); f[1] = __float2bfloat16(s1 * inv);
+  f[2] = __float2bfloat16(s2 * inv); f[3] = __float2bfloat16(s3 * inv);
+#pragma unroll
+  for (int k = 4; k < 8; ++k) f[k] = __float2bfloat16(0.f);
+  *reinterpret_cast<uint4*>(feats + (long)row * 8) = *reinterpret_cast<const uint4*>(f);
+  const int4 c = *reinterpret_cast<const int4*>(vox_coords + g * 4);
+  coords0[row] = c;
+  grid0[site(c, g0)] = row;
+}
+
+// From materialised voxels [V, P, F] (served-model path; OpenPCDet MeanVFE sums
+// all P slots, the padding is zero).  Batch index taken from the coords.
+__global__ void __launch_bounds__(256) sp_vfe_voxels_kernel(const float* __restrict__ voxels, int P, int F,
+                                                            const int* __restrict__ num_points,
+                                                            const int* __restrict__ coords, const int* __restrict__ n_p,
+                                                            Dims g0, __hip_bfloat16* __restrict__ feats,
+                                                            int4* __restrict__ coords0, int* __restrict__ grid0) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= *n_p) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < P; ++k)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) s[f] += voxels[((long)v * P + k) * F + f];
+  const float inv = 1.f / fmaxf((float)num_points[v], 1.f);
+  __hip_bfloat16 o[8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) o[f] = __float2bfloat16(s[f] * inv);
+#pragma unroll
+  for (int f = 4; f < 8; ++f) o[f] = __float2bfloat16(0.f);
+  *reinterpret_cast<uint4*>(feats + (long)v * 8) = *reinterpret_cast<const uint4*>(o);
+  const int4 c = *reinterpret_cast<const int4*>(coords + (long)v * 4);
+  coords0[v] = c;
+  grid0[site(c, g0)] = v;
+}
+
+// ---- output sites of a strided SparseConv3d ------------------------------------
+// Each input row proposes the sites it reaches; the first proposer of a site
+// claims it (atomicCAS -1 -> -2) and the wave's claims take one contiguous
+// row range with a single atomicAdd (ballot + popcount ranks).  Row order
+// depends on timing, values do not (each output row's sum runs over taps in
+// a fixed order), so results are run-to-run identical.
+__global__ void __launch_bounds__(256) sp_claim_kernel(const int4* __restrict__ coords_in, const int* __restrict__ n_in_p,
+                                                       int cap_in, Ksp k, Dims od, int* __restrict__ grid_out,
+                                                       int4* __restrict__ coords_out, int* __restrict__ n_out,
+                                                       int cap_out) {
+  const int n = min(*n_in_p, cap_in);
+  const int lane = threadIdx.x & 63;
+  for (int base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+    const int r = base + threadIdx.x;
+    const bool act = r < n;
+    const int4 c = act ? coords_in[r] : make_int4(0, 0, 0, 0);
+    for (int kz = 0; kz < k.kz; ++kz) {
+      const int zn = c.y + k.pz - kz;
+      const int oz = zn / k.sz;
+      const bool vz = act && zn >= 0 && oz * k.sz == zn && oz < od.z;
+      for (int ky = 0; ky < k.ky; ++ky) {
+        const int yn = c.z + k.py - ky;
+        const int oy = yn / k.sy;
+        const bool vy = vz && yn >= 0 && oy * k.sy == yn && oy < od.y;
+        for (int kx = 0; kx < k.kx; ++kx) {
+          const int xn = c.w + k.px - kx;
+          const int ox = xn / k.sx;
+          const bool v = vy && xn >= 0 && ox * k.sx == xn && ox < od.x;
+          long cell = 0;
+          bool claimed = false;
+          if (v) {
+            cell = (((long)c.x * od.z + oz) * od.y + oy) * od.x + ox;
+            claimed = atomicCAS(&grid_out[cell], -1, -2) == -1;
+          }
+          const unsigned long long m = __ballot(claimed);
+          if (m) {
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            int b0 = 0;
+            if (lane == leader) b0 = atomicAdd(n_out, __popcll(m));
+            b0 = __shfl(b0, leader, 64);
+            if (claimed) {
+              const int row = b0 + __popcll(m & ((1ull << lane) - 1ull));
+              if (row < cap_out) {
+                grid_out[cell] = row;
+                coords_out[row] = make_int4(c.x, oz, oy, ox);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- neighbour table + tap masks -------------------------------------------------
+// One thread per output row; a wave is exactly one 64-row tile (base is a
+// multiple of 256), so the tile's tap mask is a wave OR-reduction.
+__global__ void __launch_bounds__(256) sp_rulebook_kernel(const int4* __restrict__ coords, const int* __restrict__ n_p,
+                                                          int cap, Ksp k, Dims id, const int* __restrict__ grid_in,
+                                                          int* __restrict__ nbr, unsigned* __restrict__ tapmask) {
+  const int n = min(*n_p, cap);
+  const int KT = k.kz * k.ky * k.kx;
+  for (int base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+    const int o = base + threadIdx.x;
+    unsigned bits = 0;
+    if (o < n) {
+      const int4 c = coords[o];
+      int* dst = nbr + (long)o * KT;
+      int t = 0;
+      for (int kz = 0; kz < k.kz; ++kz) {
+        const int iz = c.y * k.sz - k.pz + kz;
+        for (int ky = 0; ky < k.ky; ++ky) {
+          const int iy = c.z * k.sy - k.py + ky;
+          for (int kx = 0; kx < k.kx; ++kx, ++t) {
+            const int ix = c.w * k.sx - k.px + kx;
+            int r = -1;
+            if ((unsigned)iz < (unsigned)id.z && (unsigned)iy < (unsigned)id.y && (unsigned)ix < (unsigned)id.x)
+              r = grid_in[(((long)c.x * id.z + iz) * id.y + iy) * id.x + ix];
+            dst[t] = r;
+            if (r >= 0) bits |= 1u << t;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) bits |= (unsigned)__shfl_xor((int)bits, s, 64);
+    if ((threadIdx.x & 63) == 0 && o < n) tapmask[o >> 6] = bits;
+  }
+}
+
+// ---- resets ------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sp_grid_reset_kernel(const int4* __restrict__ coords, const int* __restrict__ n_p,
+                                                            int cap, Dims d, int* __restrict__ grid) {
+  const int n = min(*n_p, cap);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) grid[site(coords[i], d)] = -1;
+}
+
+__global__ void __launch_bounds__(256) sp_bev_clear_kernel(const int4* __restrict__ coords, const int* __restrict__ n_p,
+                                                           int cap, int nch, __hip_bfloat16* __restrict__ bev, int H,
+                                                           int W, int C) {
+  const int n = min(*n_p, cap);
+  const int q = nch >> 3;
+  for (long i = blockIdx.x * 256 + threadIdx.x; i < (long)n * q; i += gridDim.x * 256) {
+    const int row = (int)(i / q), j = (int)(i - (long)row * q);
+    const int4 c = coords[row];
+    *reinterpret_cast<uint4*>(bev + (((long)c.x * H + c.z) * W + c.w) * C + c.y * nch + j * 8) =
+        make_uint4(0, 0, 0, 0);
+  }
+}
+
+// ---- gather GEMM on MFMA ---------------------------------------------------------
+constexpr int SBK = 32;
+constexpr int kMaxTaps = 27;
+constexpr int kMaxSteps = 64;
+
+struct SpGemmArgs {
+  const __hip_bfloat16* in;  // input rows [*, Cin]
+  int cin_log2;
+  const int* nbr;            // [cap, KT]
+  int kt;
+  const unsigned* tapmask;   // [ceil(cap / 64)]
+  const __hip_bfloat16* w;   // [N, Kp], k = tap * Cin + ci, zero-padded
+  const float* bias;         // [N]
+  int n, kp;
+  const int* m_count;
+  int cap;
+  __hip_bfloat16* out;       // [cap, N] rows (when bev == null)
+  const int4* coords;        // BEV scatter: (b, z, y, x) per output row
+  __hip_bfloat16* bev;       // [B, H, W, C] NHWC, channel z * N + n
+  int bev_h, bev_w, bev_c;
+  int act;                   // 0 none, 1 relu
+};
+
+// 16-B chunk c (0..3) of row r in a [rows][64 B] tile, XOR-swizzled so the
+// ds_read_b128 fragment reads are bank-conflict free.
+__device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 3)) << 4); }
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) sp_gemm_kernel(SpGemmArgs a) {
+  static_assert(WM * WN == 4 && BM == 64, "4 waves, one tap-mask word per tile");
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_CHUNKS = BM * 4, B_CHUNKS = BN * 4;
+  constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
+  constexpr int EPI = BM * (BN + 8) * 2;
+  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  __shared__ int s_nbr[BM * kMaxTaps];
+  __shared__ int s_steps[kMaxSteps];
+  __shared__ int s_nsteps;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = min(*a.m_count, a.cap);
+  const int nk = a.kp / SBK;
+  const int KT = a.kt;
+  const int cmask = (1 << a.cin_log2) - 1;
+
+  for (int tile = blockIdx.x; tile * BM < M; tile += gridDim.x) {
+    const int m0 = tile * BM;
+    const int rows = min(BM, M - m0);
+    for (int i = tid; i < BM * KT; i += 256) s_nbr[i] = i < rows * KT ? a.nbr[(long)m0 * KT + i] : -1;
+    if (tid == 0) {
+      const unsigned msk = a.tapmask[tile];
+      int ns = 0;
+      for (int s = 0; s < nk; ++s) {
+        const int t0 = (s * SBK) >> a.cin_log2;
+        if (t0 >= KT) break;
+        const int t1 = min((s * SBK + SBK - 1) >> a.cin_log2, KT - 1);
+        const int w = t1 - t0 + 1;
+        const unsigned sm = (w >= 32 ? 0xffffffffu : ((1u << w) - 1u)) << t0;
+        if (msk & sm) s_steps[ns++] = s;
+      }
+      s_nsteps = ns;
+    }
+    __syncthreads();
+    const int ns = s_nsteps;
+
+    uint4 ra[A_PER_T], rb[B_PER_T];
+    auto load_tiles = [&](int s) {
+#pragma unroll
+      for (int t = 0; t < A_PER_T; ++t) {
+        const int id = tid + t * 256;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < A_CHUNKS) {
+          const int row = id >> 2, k0 = s * SBK + (id & 3) * 8;
+          const int tap = k0 >> a.cin_log2;
+          if (tap < KT) {
+            const int r = s_nbr[row * KT + tap];
+            if (r >= 0) v = *reinterpret_cast<const uint4*>(a.in + ((long)r << a.cin_log2) + (k0 & cmask));
+          }
+        }
+        ra[t] = v;
+      }
+#pragma unroll
+      for (int t = 0; t < B_PER_T; ++t) {
+        const int id = tid + t * 256;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < B_CHUNKS) {
+          const int nn = id >> 2;
+          if (nn < a.n) v = *reinterpret_cast<const uint4*>(a.w + (long)nn * a.kp + s * SBK + (id & 3) * 8);
+        }
+        rb[t] = v;
+      }
+    };
+    auto store_tiles = [&](int buf) {
+      unsigned char* sa = smem + buf * STAGE;
+      unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+      for (int t = 0; t < A_PER_T; ++t) {
+        const int id = tid + t * 256;
+        if (id < A_CHUNKS) *reinterpret_cast<uint4*>(sa + swz(id >> 2, id & 3)) = ra[t];
+      }
+#pragma unroll
+      for (int t = 0; t < B_PER_T; ++t) {
+        const int id = tid + t * 256;
+        if (id < B_CHUNKS) *reinterpret_cast<uint4*>(sb + swz(id >> 2, id & 3)) = rb[t];
+      }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (ns > 0) {
+      load_tiles(s_steps[0]);
+      store_tiles(0);
+    }
+    __syncthreads();
+    for (int i = 0; i < ns; ++i) {
+      const int cur = i & 1;
+      if (i + 1 < ns) load_tiles(s_steps[i + 1]);  // issue early: hides under this step's MFMAs
+      const unsigned char* sa = smem + cur * STAGE;
+      const unsigned char* sb = sa + A_BYTES;
+      bf16x8 af[FM], bfg[FN];
+#pragma unroll
+      for (int x = 0; x < FM; ++x) af[x] = *reinterpret_cast<const bf16x8*>(sa + swz(wm * TM + x * 16 + fr, fq));
+#pragma unroll
+      for (int y = 0; y < FN; ++y) bfg[y] = *reinterpret_cast<const bf16x8*>(sb + swz(wn * TN + y * 16 + fr, fq));
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[y], af[x], acc[x][y], 0, 0, 0);
+      if (i + 1 < ns) store_tiles(cur ^ 1);
+      __syncthreads();
+    }
+
+    // epilogue: acc[x][y] col (lane & 15) -> m, rows (lane >> 4) * 4 + r -> n
+    constexpr int LD = BN + 8;
+    __hip_bfloat16* st = reinterpret_cast<__hip_bfloat16*>(smem);
+#pragma unroll
+    for (int x = 0; x < FM; ++x) {
+      const int ml = wm * TM + x * 16 + fr;
+#pragma unroll
+      for (int y = 0; y < FN; ++y) {
+        const int nl = wn * TN + y * 16 + fq * 4;
+        __hip_bfloat16 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nn = nl + r;
+          float v = acc[x][y][r];
+          if (nn < a.n) v += a.bias[nn];
+          if (a.act == 1) v = fmaxf(v, 0.f);
+          q[r] = __float2bfloat16(v);
+        }
+        *reinterpret_cast<uint2*>(st + ml * LD + nl) = *reinterpret_cast<const uint2*>(q);
+      }
+    }
+    __syncthreads();
+    constexpr int VPR = BN / 8;
+    for (int id = tid; id < BM * VPR; id += 256) {
+      const int ml = id / VPR, c8 = (id % VPR) * 8;
+      if (ml >= rows || c8 >= a.n) continue;
+      const int m = m0 + ml;
+      const uint4 v = *reinterpret_cast<const uint4*>(st + ml * LD + c8);
+      long o;
+      if (a.bev) {
+        const int4 c = a.coords[m];
+        o = (((long)c.x * a.bev_h + c.z) * a.bev_w + c.w) * a.bev_c + (long)c.y * a.n + c8;
+      } else {
+        o = (long)m * a.n + c8;
+      }
+      *reinterpret_cast<uint4*>((a.bev ? a.bev : a.out) + o) = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- SECONDHead RoI grid pool ------------------------------------------------------
+// One block per RoI; affine_grid + grid_sample(bilinear, zeros,
+// align_corners=False) exactly as PyTorch evaluates them; a lane handles 8
+// channels of one grid point (16-B corner loads, a wave reads 1 KiB of
+// contiguous NHWC channels per corner).  Output row = (gy, gx, c).
+__global__ void __launch_bounds__(256) roi_grid_pool_kernel(const __hip_bfloat16* __restrict__ feat, int H, int W,
+                                                            int C, int ldc, int coff, const float* __restrict__ rois,
+                                                            int rdim, const int* __restrict__ roi_count, int R,
+                                                            float min_x, float min_y, float cell_x, float cell_y, int G,
+                                                            __hip_bfloat16* __restrict__ out) {
+  const int b = blockIdx.y, r = blockIdx.x;
+  const int q = C >> 3;
+  __hip_bfloat16* dst = out + ((long)b * R + r) * G * G * C;
+  if (r >= roi_count[b]) {
+    for (int i = threadIdx.x; i < G * G * q; i += 256) reinterpret_cast<uint4*>(dst)[i] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const float* ro = rois + ((long)b * R + r) * rdim;
+  const float x1 = (ro[0] - ro[3] * 0.5f - min_x) / cell_x, x2 = (ro[0] + ro[3] * 0.5f - min_x) / cell_x;
+  const float y1 = (ro[1] - ro[4] * 0.5f - min_y) / cell_y, y2 = (ro[1] + ro[4] * 0.5f - min_y) / cell_y;
+  float sa, ca;
+  sincosf(ro[6], &sa, &ca);
+  const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+  const float t00 = (x2 - x1) / wm1 * ca, t01 = (x2 - x1) / wm1 * (-sa), t02 = (x1 + x2 - wm1) / wm1;
+  const float t10 = (y2 - y1) / hm1 * sa, t11 = (y2 - y1) / hm1 * ca, t12 = (y1 + y2 - hm1) / hm1;
+  const __hip_bfloat16* fb = feat + (long)b * H * W * ldc + coff;
+  for (int i = threadIdx.x; i < G * G * q; i += 256) {
+    const int p = i / q, c8 = (i - p * q) * 8;
+    const int gy = p / G, gx = p - gy * G;
+    const float xb = (2.f * gx + 1.f) / G - 1.f, yb = (2.f * gy + 1.f) / G - 1.f;
+    const float gxn = t00 * xb + t01 * yb + t02, gyn = t10 * xb + t11 * yb + t12;
+    const float ix = ((gxn + 1.f) * W - 1.f) * 0.5f, iy = ((gyn + 1.f) * H - 1.f) * 0.5f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float wx1 = ix - fx0, wy1 = iy - fy0, wx0 = 1.f - wx1, wy0 = 1.f - wy1;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+      for (int cx = 0; cx < 2; ++cx) {
+        const int xx = x0 + cx, yy = y0 + cy;
+        if ((unsigned)xx >= (unsigned)W || (unsigned)yy >= (unsigned)H) continue;
+        const float wgt = (cx ? wx1 : wx0) * (cy ? wy1 : wy0);
+        const uint4 v = *reinterpret_cast<const uint4*>(fb + ((long)yy * W + xx) * ldc + c8);
+        const __hip_bfloat16* e = reinterpret_cast<const __hip_bfloat16*>(&v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += wgt * __bfloat162float(e[k]);
+      }
+    __hip_bfloat16 o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = __float2bfloat16(acc[k]);
+    *reinterpret_cast<uint4*>(dst + (long)p * C + c8) = *reinterpret_cast<const uint4*>(o);
+  }
+}
+
+// ---- IoU rescoring -> NMS candidates -------------------------------------------
+// One block per frame: score = sigmoid(IoU logit), keep >= thresh, compact in
+// RoI order (deterministic) into the candidate buffers of the rotated NMS.
+__global__ void __launch_bounds__(256) roi_rescore_kernel(const float* __restrict__ logit, const float* __restrict__ rois,
+                                                          int rdim, const int* __restrict__ roi_cls,
+                                                          const int* __restrict__ roi_count, int R, float thresh,
+                                                          float* __restrict__ cand_box, float* __restrict__ cand_score,
+                                                          int* __restrict__ cand_cls, uint64_t* __restrict__ cand_key,
+                                                          int* __restrict__ cand_count) {
+  __shared__ int s_scan[256 / 64 + 1];
+  const int b = blockIdx.x;
+  const int n = roi_count[b];
+  int base = 0;
+  for (int r0 = 0; r0 < R; r0 += 256) {
+    const int r = r0 + threadIdx.x;
+    float s = 0.f;
+    bool keep = false;
+    if (r < n && r < R) {
+      s = sigmoidf_(logit[(long)b * R + r]);
+      keep = s >= thresh;
+    }
+    int total;
+    const int slot = block_excl_scan(keep ? 1 : 0, s_scan, &total) + base;
+    if (keep) {
+      const long o = (long)b * R + slot;
+      const float* src = rois + ((long)b * R + r) * rdim;
+      for (int d = 0; d < rdim; ++d) cand_box[o * rdim + d] = src[d];
+      cand_score[o] = s;
+      cand_cls[o] = roi_cls[(long)b * R + r];
+      cand_key[o] = make_score_key(s, (uint32_t)r);
+    }
+    base += total;
+  }
+  if (threadIdx.x == 0) cand_count[b] = base;
+}
+
+inline int grid_for(long items, int per_block, int max_blocks) {
+  long g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (int)(g < max_blocks ? g : max_blocks);
+}
+
+inline Ksp make_ksp(const int* v) { return Ksp{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]}; }
+inline Dims make_dims(const int* v) { return Dims{v[0], v[1], v[2]}; }
+
+}  // namespace
+
+TCA_API int tca_sp_offsets(const int* voxel_count, int batch, int* off, int* total, hipStream_t stream) {
+  sp_offsets_kernel<<<1, 64, 0, stream>>>(voxel_count, batch, off, total);
+  TCA_LAUNCH_CHECK();
+}
+
+// dims0: (z, y, x) of the level-0 grid.  feats: [cap0, 8] bf16 (x, y, z, i, 0, 0, 0, 0).
+TCA_API int tca_sp_vfe_slots(const float* pts, int pstride, int max_points, const int* slots, const int* vcount, int P,
+                             const int* vox_coords, const int* voxel_count, int batch, int max_voxels, const int* off,
+                             const int* dims0, void* feats, int* coords0, int* grid0, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (pstride < 4 || (pstride & 3)) return (int)hipErrorInvalidValue;
+  sp_vfe_slots_kernel<<<dim3((max_voxels + 255) / 256, batch), 256, 0, stream>>>(
+      pts, pstride, max_points, slots, vcount, P, vox_coords, voxel_count, max_voxels, off, make_dims(dims0),
+      (__hip_bfloat16*)feats, (int4*)coords0, grid0);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_sp_vfe_voxels(const float* voxels, int cap, int P, int F, const int* num_points, const int* coords,
+                              const int* n, const int* dims0, void* feats, int* coords0, int* grid0,
+                              hipStream_t stream) {
+  if (F < 4) return (int)hipErrorInvalidValue;
+  sp_vfe_voxels_kernel<<<grid_for(cap, 256, 1 << 20), 256, 0, stream>>>(
+      voxels, P, F, num_points, coords, n, make_dims(dims0), (__hip_bfloat16*)feats, (int4*)coords0, grid0);
+  TCA_LAUNCH_CHECK();
+}
+
+// ksp: [kz, ky, kx, sz, sy, sx, pz, py, px]; odims: output (z, y, x).
+TCA_API int tca_sp_claim(const int* coords_in, const int* n_in, int cap_in, const int* ksp, const int* odims,
+                         int* grid_out, int* coords_out, int* n_out, int cap_out, hipStream_t stream) {
+  sp_claim_kernel<<<grid_for(cap_in, 256, 2048), 256, 0, stream>>>((const int4*)coords_in, n_in, cap_in,
+                                                                   make_ksp(ksp), make_dims(odims), grid_out,
+                                                                   (int4*)coords_out, n_out, cap_out);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_sp_rulebook(const int* coords, const int* n, int cap, const int* ksp, const int* idims,
+                            const int* grid_in, int* nbr, unsigned* tapmask, hipStream_t stream) {
+  const Ksp k = make_ksp(ksp);
+  if (k.kz * k.ky * k.kx > 32) return (int)hipErrorInvalidValue;
+  sp_rulebook_kernel<<<grid_for(cap, 256, 2048), 256, 0, stream>>>((const int4*)coords, n, cap, k, make_dims(idims),
+                                                                   grid_in, nbr, tapmask);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_sp_grid_reset(const int* coords, const int* n, int cap, const int* dims, int* grid,
+                              hipStream_t stream) {
+  sp_grid_reset_kernel<<<grid_for(cap, 256, 2048), 256, 0, stream>>>((const int4*)coords, n, cap, make_dims(dims),
+                                                                     grid);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_sp_bev_clear(const int* coords, const int* n, int cap, int nch, void* bev, int H, int W, int C,
+                             hipStream_t stream) {
+  if (nch & 7) return (int)hipErrorInvalidValue;
+  sp_bev_clear_kernel<<<grid_for((long)cap * (nch / 8), 256, 4096), 256, 0, stream>>>(
+      (const int4*)coords, n, cap, nch, (__hip_bfloat16*)bev, H, W, C);
+  TCA_LAUNCH_CHECK();
+}
+
+// out = relu?(gather(in, nbr) @ W^T + bias) over the device row count.
+// Contract: Cin a power of two >= 8, KT <= 27, Kp % 32 == 0, Kp / 32 <= 64,
+// N % 8 == 0 and N <= 128; bev != null -> scatter rows into the NHWC map.
+TCA_API int tca_sp_gemm(const void* in, int cin, const int* nbr, int kt, const unsigned* tapmask, const void* w,
+                        const float* bias, int n, int kp, const int* m_count, int cap, void* out, const int* coords,
+                        void* bev, int bev_h, int bev_w, int bev_c, int act, hipStream_t stream) {
+  int lg = 0;
+  while ((1 << lg) < cin) ++lg;
+  if ((1 << lg) != cin || cin < 8 || kt > kMaxTaps || (kp % SBK) || kp / SBK > kMaxSteps || (n & 7) || n > 128 ||
+      kp < kt * cin)
+    return (int)hipErrorInvalidValue;
+  SpGemmArgs a{(const __hip_bfloat16*)in, lg, nbr, kt, tapmask, (const __hip_bfloat16*)w, bias, n, kp, m_count, cap,
+               (__hip_bfloat16*)out, (const int4*)coords, (__hip_bfloat16*)bev, bev_h, bev_w, bev_c, act};
+  const int grid = grid_for(cap, 64, 1024);
+  if (n <= 16) sp_gemm_kernel<64, 16, 4, 1><<<grid, 256, 0, stream>>>(a);
+  else if (n <= 32) sp_gemm_kernel<64, 32, 4, 1><<<grid, 256, 0, stream>>>(a);
+  else if (n <= 64) sp_gemm_kernel<64, 64, 2, 2><<<grid, 256, 0, stream>>>(a);
+  else sp_gemm_kernel<64, 128, 2, 2><<<grid, 256, 0, stream>>>(a);
+  TCA_LAUNCH_CHECK();
+}
+
+// feat: NHWC [B, H, W, ldc], channels [coff, coff + C); rois [B, R, rdim]
+// (x, y, z, dx, dy, dz, yaw, ...); out [B * R, G * G * C] bf16 in (gy, gx, c) order.
+TCA_API int tca_roi_grid_pool(const void* feat, int batch, int H, int W, int C, int ldc, int coff, const float* rois,
+                              int rdim, const int* roi_count, int R, float min_x, float min_y, float cell_x,
+                              float cell_y, int G, void* out, hipStream_t stream) {
+  if (batch <= 0 || R <= 0) return 0;
+  if ((C & 7) || (ldc & 7) || (coff & 7) || rdim < 7) return (int)hipErrorInvalidValue;
+  roi_grid_pool_kernel<<<dim3(R, batch), 256, 0, stream>>>((const __hip_bfloat16*)feat, H, W, C, ldc, coff, rois, rdim,
+                                                           roi_count, R, min_x, min_y, cell_x, cell_y, G,
+                                                           (__hip_bfloat16*)out);
+  TCA_LAUNCH_CHECK();
+}
+
+// Candidate buffers have capacity R per frame.
+TCA_API int tca_roi_rescore(const float* logit, const float* rois, int rdim, const int* roi_cls, const int* roi_count,
+                            int batch, int R, float thresh, float* cand_box, float* cand_score, int* cand_cls,
+                            uint64_t* cand_key, int* cand_count, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  roi_rescore_kernel<<<batch, 256, 0, stream>>>(logit, rois, rdim, roi_cls, roi_count, R, thresh, cand_box, cand_score,
+                                                cand_cls, cand_key, cand_count);
+  TCA_LAUNCH_CHECK();
+}

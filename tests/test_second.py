@@ -1,0 +1,242 @@
+"""SECOND-IoU (OpenPCDet SECONDNetIoU, reference examples/second_iou): sparse
+3D conv semantics, RoI grid pooling, the fp32 model, and the HIP kernels /
+GPU pipeline against the fp32 PyTorch reference."""
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from triton_client_amd.config.lidar import KITTI_SECOND_VOXELS, SecondIoUConfig, SparseConvSpec
+from triton_client_amd.models.common import fuse_model, randomize_bn
+from triton_client_amd.models.second import (SparseConv3d, bev_channel_permutation, build_second_iou,
+                                             height_compression, mean_vfe, postprocess_reference,
+                                             roi_grid_pool_reference)
+from triton_client_amd.ops.lidar import voxelize_np
+from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+
+def _small_cfg(**kw):
+    v = dataclasses.replace(KITTI_SECOND_VOXELS, point_cloud_range=(0.0, -12.8, -3.0, 25.6, 12.8, 1.0),
+                            max_voxels=16000)
+    return SecondIoUConfig(voxel=v, **kw)
+
+
+def _voxels(cfg, seeds=(0,)):
+    vs, ns, cs = [], [], []
+    for b, s in enumerate(seeds):
+        p = lidar_sweep(LidarSpec(rings=16, azimuth_steps=768, sensor_height=1.73), s)
+        p = p[~np.isnan(p).any(1)]
+        v, zyx, num, _ = voxelize_np(p, cfg.voxel, 4)
+        vs.append(v)
+        ns.append(num)
+        cs.append(np.concatenate([np.full((len(zyx), 1), b, np.int32), zyx], 1))
+    return (torch.from_numpy(np.concatenate(vs)), torch.from_numpy(np.concatenate(ns).astype(np.int64)),
+            torch.from_numpy(np.concatenate(cs)))
+
+
+def _model(cfg, seed=0):
+    m = build_second_iou(cfg, seed)
+    randomize_bn(m, 3)
+    for layer in m.backbone3d.layers:  # non-trivial BN statistics for the sparse layers too
+        c = layer.spec.cout
+        with torch.no_grad():
+            layer.bn.running_mean.copy_(torch.randn(c) * 0.1)
+            layer.bn.running_var.copy_(torch.rand(c) * 0.5 + 0.75)
+    return fuse_model(m.eval())
+
+
+def test_config_level_shapes():
+    cfg = SecondIoUConfig()
+    sh = cfg.level_shapes()
+    assert sh[0] == (41, 1600, 1408)
+    assert sh[3] == (21, 800, 704) and sh[6] == (11, 400, 352) and sh[9] == (5, 200, 176)
+    assert sh[-1] == (2, 200, 176)
+    assert cfg.bev_shape == (256, 200, 176)
+    assert cfg.feature_map_size == (200, 176)
+    assert cfg.num_anchors_per_loc == 6 and cfg.proposal_post_max == 100
+
+
+@pytest.mark.parametrize("spec", [SparseConvSpec(8, 16), SparseConvSpec(8, 16, False, stride=(2, 2, 2)),
+                                  SparseConvSpec(8, 16, False, stride=(2, 2, 2), padding=(0, 1, 1)),
+                                  SparseConvSpec(8, 16, False, kernel=(3, 1, 1), stride=(2, 1, 1),
+                                                 padding=(0, 0, 0))])
+def test_sparse_conv_matches_dense_conv3d(spec):
+    """Sparse conv on a random site subset == dense conv3d of the zero-filled
+    grid, at the sparse layer's output sites; and no output site is missed."""
+    torch.manual_seed(0)
+    B, shape = 2, (7, 9, 10)
+    dense_mask = torch.rand(B, *shape) < 0.15
+    coords = torch.nonzero(dense_mask).int()
+    feats = torch.randn(len(coords), spec.cin)
+    layer = SparseConv3d(spec).eval()
+    layer.fuse_bn()
+    with torch.no_grad():
+        y, co, shp = layer(feats, coords, shape)
+        dense = torch.zeros(B, spec.cin, *shape)
+        c = coords.long()
+        dense[c[:, 0], :, c[:, 1], c[:, 2], c[:, 3]] = feats
+        w = layer.weight.permute(0, 4, 1, 2, 3)
+        ref = F.conv3d(dense, w, layer.bias, stride=spec.stride, padding=spec.padding)
+        ref = F.relu(ref)
+        cc = co.long()
+        got_dense = ref[cc[:, 0], :, cc[:, 1], cc[:, 2], cc[:, 3]]
+    assert ref.shape[2:] == torch.Size(shp)
+    torch.testing.assert_close(y, got_dense, rtol=1e-4, atol=1e-4)
+    # output set: subm keeps the input sites; strided = every site whose window holds an input site
+    if spec.subm:
+        assert torch.equal(co, coords)
+    else:
+        reach = F.conv3d(dense_mask.float().unsqueeze(1), torch.ones(1, 1, *spec.kernel), stride=spec.stride,
+                         padding=spec.padding)[:, 0] > 0
+        assert reach.sum().item() == len(co)
+        assert reach[cc[:, 0], cc[:, 1], cc[:, 2], cc[:, 3]].all()
+
+
+def test_height_compression_and_bev_permutation():
+    cfg = _small_cfg()
+    D, H, W = cfg.level_shapes()[-1]
+    C = cfg.sparse[-1].cout
+    coords = torch.tensor([[0, 1, 2, 3], [1, 0, 4, 5]], dtype=torch.int32)
+    feats = torch.arange(2 * C, dtype=torch.float32).view(2, C)
+    bev = height_compression(feats, coords, (D, H, W), 2)
+    assert bev.shape == (2, C * D, H, W)
+    assert bev[0, 5 * D + 1, 2, 3] == feats[0, 5] and bev[1, 7 * D + 0, 4, 5] == feats[1, 7]
+    perm = bev_channel_permutation(cfg)
+    # GPU layout: channel z*C + c holds HeightCompression channel c*D + z
+    assert perm[1 * C + 5] == 5 * D + 1 and sorted(perm.tolist()) == list(range(C * D))
+
+
+def test_roi_grid_pool_reference_constant_and_axis_aligned():
+    cfg = _small_cfg()
+    H, W = 64, 80
+    feat = torch.full((1, 3, H, W), 2.0)
+    # RoI well inside the map: every bilinear sample sees the constant
+    rois = torch.tensor([[[10.0, 0.0, -1.0, 4.0, 3.0, 1.5, 0.3]]])
+    p = roi_grid_pool_reference(feat, rois, cfg)
+    assert p.shape == (1, 3, cfg.roi_grid, cfg.roi_grid)
+    torch.testing.assert_close(p, torch.full_like(p, 2.0))
+
+
+def test_second_model_cpu_forward_and_postprocess():
+    cfg = _small_cfg()
+    m = _model(cfg)
+    vox, num, coords = _voxels(cfg, (0, 1))
+    with torch.no_grad():
+        bev = m.sparse_forward(vox, num, coords, 2)
+        C, Hb, Wb = cfg.bev_shape
+        assert bev.shape == (2, C, Hb, Wb)
+        assert (bev != 0).any()
+        sf, cls, box, dir_ = m.bev_forward(bev)
+        H, W = cfg.feature_map_size
+        assert sf.shape == (2, 512, H, W) and cls.shape == (2, 18, H, W) and box.shape == (2, 42, H, W)
+        from triton_client_amd.models.second import proposal_config
+        from triton_client_amd.ops.lidar import AnchorPostprocess
+        props = AnchorPostprocess(proposal_config(cfg), 2, device="cpu").cpu(cls, box, dir_)
+        assert (props.count == cfg.proposal_post_max).all()
+        logits = m.roi_iou(sf, props.box)
+        assert logits.shape == (2, cfg.proposal_post_max) and torch.isfinite(logits).all()
+        out = postprocess_reference(props.box, props.cls, props.count, logits + 3.0, cfg)
+    for bx, sc, lb in out:
+        assert bx.shape[1] == 7 and len(sc) <= cfg.nms_post_max
+        assert (sc >= cfg.score_thresh).all() and set(np.unique(lb)) <= {1, 2, 3}
+
+
+def test_mean_vfe():
+    v = torch.zeros(2, 5, 4)
+    v[0, :2] = torch.tensor([[1.0, 2, 3, 4], [3.0, 4, 5, 6]])
+    v[1, :1] = torch.tensor([[7.0, 8, 9, 1]])
+    out = mean_vfe(v, torch.tensor([2, 1]))
+    torch.testing.assert_close(out, torch.tensor([[2.0, 3, 4, 5], [7.0, 8, 9, 1]]))
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp(min=1e-6)).item()
+
+
+@pytest.mark.gpu
+def test_sparse_backbone_gpu_matches_fp32(cuda):
+    from triton_client_amd.ops.spconv import SparseBackbone
+    cfg = _small_cfg()
+    m = _model(cfg)
+    vox, num, coords = _voxels(cfg, (0, 1))
+    with torch.no_grad():
+        ref = m.sparse_forward(vox, num, coords, 2)  # [2, 256, H, W]
+    sp = SparseBackbone(cfg, [l.to(cuda) for l in m.to(cuda).backbone3d.layers], 2, cuda)
+    V = len(vox)
+    cap = sp.levels[0].cap
+    vg = torch.zeros((cap, 5, 4), device=cuda)
+    vg[:V] = vox.to(cuda)
+    ng = torch.zeros((cap,), dtype=torch.int32, device=cuda)
+    ng[:V] = num.to(cuda)
+    cg = torch.zeros((cap, 4), dtype=torch.int32, device=cuda)
+    cg[:V] = coords.to(cuda)
+    n = torch.tensor([V], dtype=torch.int32, device=cuda)
+    for _ in range(2):  # the second run exercises the reset of the first
+        sp.reset()
+        sp.encode_from_voxels(vg, ng, cg, n)
+        bev = sp.forward()
+    torch.cuda.synchronize()
+    perm = bev_channel_permutation(cfg)
+    got = bev.float().cpu()[..., torch.argsort(perm)].permute(0, 3, 1, 2)
+    rows = sp.level_rows()
+    assert rows[0] == V and all(r > 0 for r in rows)
+    assert _rel(got, ref) < 0.03, _rel(got, ref)
+    # the active BEV sites agree exactly
+    assert torch.equal((got.abs().sum(1) > 0), (ref.abs().sum(1) > 0))
+
+
+@pytest.mark.gpu
+def test_roi_grid_pool_kernel_matches_reference(cuda):
+    from triton_client_amd import _native
+    cfg = _small_cfg()
+    torch.manual_seed(0)
+    B, H, W, C, R = 2, 64, 64, 64, 100
+    feat = torch.randn(B, H, W, C).to(torch.bfloat16)
+    rois = torch.zeros(B, R, 7)
+    rois[..., 0] = torch.rand(B, R) * 25.6
+    rois[..., 1] = torch.rand(B, R) * 25.6 - 12.8
+    rois[..., 3:6] = torch.rand(B, R, 3) * 4 + 0.5
+    rois[..., 6] = (torch.rand(B, R) - 0.5) * 6.3
+    count = torch.tensor([R, 37], dtype=torch.int32)
+    out = torch.empty(B * R, 49 * C, dtype=torch.bfloat16, device=cuda)
+    G = 7
+    ds = cfg.feature_map_stride
+    v = cfg.voxel
+    _native.call("tca_roi_grid_pool", _native.ptr(fg := feat.to(cuda)), B, H, W, C, C, 0,
+                 _native.ptr(rg := rois.to(cuda)), 7, _native.ptr(cc := count.to(cuda)), R,
+                 float(v.point_cloud_range[0]), float(v.point_cloud_range[1]), float(v.voxel_size[0] * ds),
+                 float(v.voxel_size[1] * ds), G, _native.ptr(out), _native.stream_ptr())
+    torch.cuda.synchronize()
+    ref = roi_grid_pool_reference(feat.float().permute(0, 3, 1, 2), rois, cfg)  # [B*R, C, G, G]
+    got = out.float().cpu().view(B * R, G, G, C).permute(0, 3, 1, 2)
+    valid = torch.cat([torch.arange(R) < int(c) for c in count])
+    assert _rel(got[valid], ref[valid]) < 0.01
+    assert (got[~valid] == 0).all()
+    del fg, rg, cc
+
+
+@pytest.mark.gpu
+def test_second_pipeline_graph(cuda):
+    from triton_client_amd.pipelines import GraphRunner, SecondPipeline
+    cfg = _small_cfg()
+    pipe = SecondPipeline(batch=2, max_points=16384, device=cuda, cfg=cfg, z_offset=0.0)
+    for b in range(2):
+        c = lidar_sweep(LidarSpec(rings=16, azimuth_steps=768, sensor_height=1.73), b)
+        raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+        pipe.data[b * pipe.frame_bytes: b * pipe.frame_bytes + raw.numel()].copy_(raw)
+        pipe.frame_n[b] = c.shape[0]
+    d = pipe.calibrate_detection_density(30.0)
+    assert -30 < d < 30
+    eager = pipe.step().per_image()
+    torch.cuda.synchronize()
+    run = GraphRunner(pipe.step)
+    g = run().per_image()
+    g2 = run().per_image()
+    assert any(len(x["score"]) > 0 for x in eager)
+    for a, b, c in zip(eager, g, g2):
+        np.testing.assert_array_equal(b["box"], c["box"])
+        assert a["box"].shape[1] == 7 and len(a["score"]) <= cfg.nms_post_max
+        assert (a["score"] >= cfg.score_thresh).all()

@@ -57,6 +57,17 @@ _KERNEL_SIGS = {
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, P],
     "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, P],
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
+    # SECOND-IoU: sparse 3D backbone + RoI head (spconv.hip)
+    "tca_sp_offsets": [P, I, P, P, P],
+    "tca_sp_vfe_slots": [P, I, I, P, P, I, P, P, I, I, P, P, P, P, P, P],
+    "tca_sp_vfe_voxels": [P, I, I, I, P, P, P, P, P, P, P, P],
+    "tca_sp_claim": [P, P, I, P, P, P, P, P, I, P],
+    "tca_sp_rulebook": [P, P, I, P, P, P, P, P, P],
+    "tca_sp_grid_reset": [P, P, I, P, P, P],
+    "tca_sp_bev_clear": [P, P, I, I, P, I, I, I, P],
+    "tca_sp_gemm": [P, I, P, I, P, P, P, I, I, P, I, P, P, P, I, I, I, I, P],
+    "tca_roi_grid_pool": [P, I, I, I, I, I, I, P, I, P, I, F, F, F, F, I, P, P],
+    "tca_roi_rescore": [P, P, I, P, P, I, I, F, P, P, P, P, P, P],
 }
 
 

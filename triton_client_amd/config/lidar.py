@@ -140,6 +140,94 @@ class PointPillarsConfig:
 
 
 @dataclass
+class SparseConvSpec:
+    """One layer of the VoxelBackBone8x sparse 3D CNN (OpenPCDet
+    ``backbones_3d/spconv_backbone.py``, named by ``second_iou.yaml:13-14``):
+    ``subm`` = SubMConv3d (output sites = input sites, 3x3x3, pad 1);
+    otherwise SparseConv3d with per-(z, y, x) kernel / stride / padding.
+    Every layer is conv (no bias) + BatchNorm1d(eps 1e-3) + ReLU."""
+    cin: int
+    cout: int
+    subm: bool = True
+    kernel: Tuple[int, int, int] = (3, 3, 3)
+    stride: Tuple[int, int, int] = (1, 1, 1)
+    padding: Tuple[int, int, int] = (1, 1, 1)
+
+    @property
+    def taps(self) -> int:
+        return self.kernel[0] * self.kernel[1] * self.kernel[2]
+
+
+def voxel_backbone_8x(c_in: int = 4) -> Tuple[SparseConvSpec, ...]:
+    """VoxelBackBone8x: conv_input + conv1 at 1x, conv2 at 2x, conv3 at 4x,
+    conv4 at 8x (z padding 0), conv_out (3,1,1)/(2,1,1): 16, 16, 32, 64, 64,
+    128 channels."""
+    S = SparseConvSpec
+    return (
+        S(c_in, 16), S(16, 16),                                                       # conv_input, conv1
+        S(16, 32, False, stride=(2, 2, 2)), S(32, 32), S(32, 32),                       # conv2
+        S(32, 64, False, stride=(2, 2, 2)), S(64, 64), S(64, 64),                       # conv3
+        S(64, 64, False, stride=(2, 2, 2), padding=(0, 1, 1)), S(64, 64), S(64, 64),    # conv4
+        S(64, 128, False, kernel=(3, 1, 1), stride=(2, 1, 1), padding=(0, 0, 0)),       # conv_out
+    )
+
+
+@dataclass
+class SecondIoUConfig(PointPillarsConfig):
+    """OpenPCDet SECONDNetIoU (reference ``examples/second_iou/1/second_iou.yaml``)
+    on the client's KITTI voxels (``data/kitti_dataset.yaml:4,64-70``):
+    MeanVFE → VoxelBackBone8x → HeightCompression (256) → BaseBEVBackbone
+    [5,5] / [1,2] / [128,256] / up [1,2] / [256,256] → AnchorHeadSingle
+    (stride 8) → proposal NMS (pre 1024, post 100, IoU 0.7) → SECONDHead
+    (7x7 RoI grid pool on the 512-channel BEV map, shared FC [256,256], IoU FC
+    [256,256]) → rotated NMS on sigmoid(IoU) (score 0.1, IoU 0.01, 4096 → 500)."""
+    voxel: VoxelConfig = field(default_factory=lambda: KITTI_SECOND_VOXELS)
+    sparse: Tuple[SparseConvSpec, ...] = field(default_factory=voxel_backbone_8x)  # second_iou.yaml:13-14
+    bev_features: int = 256  # :16-18 (HeightCompression: 128 channels x 2 z-levels)
+    layer_nums: Tuple[int, ...] = (5, 5)  # :20-27
+    layer_strides: Tuple[int, ...] = (1, 2)
+    num_filters: Tuple[int, ...] = (128, 256)
+    upsample_strides: Tuple[float, ...] = (1, 2)
+    num_upsample_filters: Tuple[int, ...] = (256, 256)
+    feature_map_stride: int = 8  # :45
+    # ROI_HEAD (:87-112)
+    roi_grid: int = 7
+    roi_shared_fc: Tuple[int, ...] = (256, 256)
+    roi_iou_fc: Tuple[int, ...] = (256, 256)
+    proposal_nms_thresh: float = 0.7
+    proposal_pre_max: int = 1024
+    proposal_post_max: int = 100
+    # POST_PROCESSING (:136-148) = the inherited score 0.1, NMS 0.01, 4096 → 500
+
+    @property
+    def sparse_shape(self) -> Tuple[int, int, int]:
+        """spconv input shape (z, y, x) = grid[::-1] + [1, 0, 0]."""
+        nx, ny, nz = self.voxel.grid_size
+        return nz + 1, ny, nx
+
+    def level_shapes(self) -> List[Tuple[int, int, int]]:
+        """(z, y, x) shape of the input and of every sparse layer's output."""
+        shp = [self.sparse_shape]
+        for s in self.sparse:
+            z = shp[-1]
+            shp.append(z if s.subm else
+                       tuple((z[d] + 2 * s.padding[d] - s.kernel[d]) // s.stride[d] + 1 for d in range(3)))
+        return shp
+
+    @property
+    def bev_shape(self) -> Tuple[int, int, int]:
+        """(channels, ny, nx) of HeightCompression's output."""
+        z, y, x = self.level_shapes()[-1]
+        return self.sparse[-1].cout * z, y, x
+
+    @property
+    def feature_map_size(self) -> Tuple[int, int]:
+        _, y, x = self.bev_shape
+        s = self.layer_strides[0]
+        return y // s, x // s
+
+
+@dataclass
 class CenterPointTask:
     class_names: Tuple[str, ...]
 

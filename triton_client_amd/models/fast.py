@@ -250,10 +250,16 @@ class _BEVBackbonePlan:
 class FastBEV:
     """PointPillars BEV backbone + anchor head on fused convs."""
 
-    def __init__(self, model, batch: int, device="cuda", fused_neck: bool = True):
+    def __init__(self, model, batch: int, device="cuda", fused_neck: bool = True,
+                 bev_hw: Optional[Tuple[int, int]] = None):
+        """bev_hw: (ny, nx) of the backbone input when it is not the voxel grid
+        (SECOND: the 8x-downsampled HeightCompression map)."""
         self.device = torch.device(device)
         cfg = model.cfg
-        nx, ny, _ = cfg.voxel.grid_size
+        if bev_hw is not None:
+            ny, nx = bev_hw
+        else:
+            nx, ny, _ = cfg.voxel.grid_size
         B = batch
         bufs = self.bufs = _Buffers(self.device)
         self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)

@@ -6,3 +6,4 @@ from .graph import GraphRunner  # noqa: F401
 from .centerpoint import CenterPointPipeline  # noqa: F401,E402
 from .detectron import DetectronPipeline  # noqa: F401,E402
 from .yolov4 import Yolov4Pipeline  # noqa: F401,E402
+from .second import SecondPipeline  # noqa: F401,E402
