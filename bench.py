@@ -63,8 +63,9 @@ def parse():
     ap.add_argument("--only", choices=["both", "camera", "lidar"], default="both")
     ap.add_argument("--camera-model", choices=["yolov5n", "yolov4", "retinanet", "fcos"], default="yolov5n",
                     help="2D detector: YOLOv5n-640 (headline) or Detectron2 RetinaNet / FCOS R50-FPN at 800x1344")
-    ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint"], default="pointpillars",
-                    help="3D detector: PointPillars KITTI (headline) or CenterPoint-PP nuScenes")
+    ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint", "second_iou"], default="pointpillars",
+                    help="3D detector: PointPillars KITTI (headline), CenterPoint-PP nuScenes or SECOND-IoU KITTI "
+                         "(sparse 3D conv backbone + RoI head)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--target-2d", type=float, default=100.0, help="candidates/frame reaching 2D NMS (calibration)")
     ap.add_argument("--target-3d", type=float, default=2000.0, help="anchors/frame reaching 3D NMS (calibration)")
@@ -102,9 +103,13 @@ def main():
         cam = DetectronPipeline(batch=B, src_hw=(H0, W0), cfg=DetectronConfig(arch=args.camera_model), device=dev)
     else:
         cam = CameraPipeline(batch=B, src_hw=(H0, W0), device=dev) if use_cam else None
+    sec = args.lidar_model == "second_iou"
     if use_lid and cp:
         from triton_client_amd.pipelines import CenterPointPipeline
         lid = CenterPointPipeline(batch=B, max_points=max_points, device=dev)
+    elif use_lid and sec:
+        from triton_client_amd.pipelines import SecondPipeline
+        lid = SecondPipeline(batch=B, max_points=max_points, device=dev, z_offset=1.5)
     else:
         lid = LidarPipeline(batch=B, max_points=max_points, device=dev, z_offset=1.5) if use_lid else None
 
@@ -157,8 +162,9 @@ def main():
             calib["detectron_logit_shift" if det2 else "yolo_logit_shift"] = cam.calibrate_detection_density(
                 min(args.target_2d, 300.0) if det2 else args.target_2d)
         if use_lid:
-            key = "centerpoint_hm_shift" if cp else "pp_logit_shift"
-            calib[key] = lid.calibrate_detection_density(args.target_3d)
+            key = "centerpoint_hm_shift" if cp else ("second_iou_shift" if sec else "pp_logit_shift")
+            # SECOND-IoU: the target is RoIs (of the 100 proposals) passing the final score threshold
+            calib[key] = lid.calibrate_detection_density(min(args.target_3d, 60.0) if sec else args.target_3d)
     if info.world > 1:
         # every GPU must run the same model: rank 0's calibrated weights win
         from triton_client_amd.models.common import broadcast_parameters
@@ -342,7 +348,8 @@ def main():
             "config": {
                 "model": ({"both": cam_name + " + ", "camera": cam_name, "lidar": ""}[args.only]
                           + ("" if args.only == "camera" else
-                             ("CenterPoint-PP (nuScenes, 10 cls)" if cp else "PointPillars (KITTI, 3 cls)"))),
+                             ("CenterPoint-PP (nuScenes, 10 cls)" if cp else
+                              ("SECOND-IoU (KITTI, 3 cls)" if sec else "PointPillars (KITTI, 3 cls)")))),
                 "global_batch": info.world * B,
                 "seq_len": None,
                 "parallelism": f"dp{info.world}",

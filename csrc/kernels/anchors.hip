@@ -81,9 +81,9 @@ template <typename T>
 __global__ void __launch_bounds__(256) anchor_decode_kernel(
     const T* __restrict__ cls, const T* __restrict__ box, const T* __restrict__ dir, int layout, int H, int W, int A,
     int C, int bins, int ld_cls, int ld_box, int ld_dir, AnchorTable tb, float x0, float xs, float y0, float ys,
-    float dir_offset, float dir_limit_offset, float score_thresh, float* __restrict__ cand_box,
-    float* __restrict__ cand_score, int* __restrict__ cand_label, uint64_t* __restrict__ cand_key,
-    int* __restrict__ cand_count, int cap) {
+    float dir_offset, float dir_limit_offset, float score_thresh, const uint32_t* __restrict__ key_thr,
+    float* __restrict__ cand_box, float* __restrict__ cand_score, int* __restrict__ cand_label,
+    uint64_t* __restrict__ cand_key, int* __restrict__ cand_count, int cap) {
   __shared__ int s_idx[kStage];
   __shared__ float s_score[kStage];
   __shared__ int s_label[kStage];
@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
   __syncthreads();
   const int b = blockIdx.y;
   const int total = H * W * A;
+  const uint32_t kthr = key_thr ? key_thr[2 * b + 1] : 0u;  // sel layout [B][2]
   const int a0 = blockIdx.x * kAnchorsPerBlock;
   const int a1 = min(a0 + kAnchorsPerBlock, total);
   for (int base = a0 + threadIdx.x; base < a1; base += 4 * 256) {
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
       const int aidx = base + u * 256;
       if (aidx >= a1) continue;
       const float score = sigmoidf_(best[u]);
-      if (score < score_thresh) continue;
+      if (key_thr ? float_to_ordered(best[u]) < kthr : score < score_thresh) continue;
       const int slot = atomicAdd(&s_cnt, 1);
       if (slot < kStage) {
         s_idx[slot] = aidx;
@@ -144,15 +145,149 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
   }
 }
 
+// ---- exact top-k threshold over all anchors (proposal layers) -------------------
+// SECONDHead's proposal layer keeps the top NMS_PRE_MAXSIZE (1024) of all
+// 211,200 anchors by max class logit, with no score threshold.  Decoding and
+// radix-selecting every anchor (one block per frame) cost ~0.9 ms per batch;
+// instead two histogram passes over the ordered-u32 max-logit key (12 bits,
+// then the next 12 bits inside the boundary bin) find a per-frame key
+// threshold that admits the top k plus at most one 256-key bucket, and the
+// decode kernel compacts only those.  Histograms are LDS-privatised per
+// block, with the wave's dominant bins aggregated (the high bits of a
+// narrow score band are all equal), and self-resetting.
+constexpr int kHistBins = 4096;
+
+template <typename T>
+__global__ void __launch_bounds__(256) anchor_hist_kernel(const T* __restrict__ cls, int layout, int H, int W, int A,
+                                                          int C, int ld_cls, int level, const uint32_t* __restrict__ sel,
+                                                          unsigned* __restrict__ hist) {
+  __shared__ unsigned sh[kHistBins];
+  for (int i = threadIdx.x; i < kHistBins; i += 256) sh[i] = 0;
+  __syncthreads();
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int total = H * W * A;
+  const int a0 = blockIdx.x * kAnchorsPerBlock, a1 = min(a0 + kAnchorsPerBlock, total);
+  const uint32_t pre = level == 2 ? sel[b * 2] : 0u;
+  if (level == 2 && pre == 0xffffffffu) return;  // fewer than k anchors: nothing to refine
+  for (int aidx = a0 + threadIdx.x; aidx < a0 + kAnchorsPerBlock; aidx += 256) {
+    bool m = false;
+    int d = 0;
+    if (aidx < a1) {
+      const int a = aidx % A, yx = aidx / A, y = yx / W, x = yx - y * W;
+      float best = -INFINITY;
+      for (int c = 0; c < C; ++c) best = fmaxf(best, head_at(cls, layout, b, H, W, A * C, ld_cls, y, x, a * C + c));
+      const uint32_t u = float_to_ordered(best);
+      if (level == 1) {
+        m = true;
+        d = (int)(u >> 20);
+      } else {
+        m = (u >> 20) == pre;
+        d = (int)((u >> 8) & (kHistBins - 1));
+      }
+    }
+    for (int round = 0; round < 2; ++round) {
+      const unsigned long long mm = __ballot(m);
+      if (!mm) break;
+      const int leader = __ffsll(mm) - 1;
+      const int dl = __shfl(d, leader, 64);
+      const unsigned long long same = __ballot(m && d == dl);
+      if (lane == leader) atomicAdd(&sh[dl], (unsigned)__popcll(same));
+      if (d == dl) m = false;
+    }
+    if (m) atomicAdd(&sh[d], 1u);
+  }
+  __syncthreads();
+  unsigned* hb = hist + (long)b * kHistBins;
+  for (int i = threadIdx.x; i < kHistBins; i += 256)
+    if (sh[i]) atomicAdd(&hb[i], sh[i]);
+}
+
+// One block per frame.  Level 1: sel[2b] = boundary bin (0xffffffff: all
+// anchors pass), sel[2b+1] = count strictly above it.  Level 2: sel[2b+1] =
+// the final ordered-key threshold.  Each level zeroes the histogram it read.
+__global__ void __launch_bounds__(256) anchor_select_kernel(unsigned* __restrict__ hist, int level, int k,
+                                                            uint32_t* __restrict__ sel) {
+  __shared__ unsigned s_sum[256];
+  __shared__ int s_pick;
+  const int b = blockIdx.x, t = threadIdx.x;
+  unsigned* hb = hist + (long)b * kHistBins;
+  constexpr int PER = kHistBins / 256;  // 16 bins per thread, thread 0 owns the top bins
+  unsigned v[PER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = hb[kHistBins - 1 - (t * PER + j)];
+    sum += v[j];
+  }
+  s_sum[t] = sum;
+  if (t == 0) s_pick = -1;
+  __syncthreads();
+  const bool all = level == 2 && sel[b * 2] == 0xffffffffu;
+  const unsigned need = level == 1 ? (unsigned)k : (unsigned)k - sel[b * 2 + 1];
+  if (t == 0 && !all) {  // 256 partial sums, serial from the top
+    unsigned cum = 0;
+    for (int i = 0; i < 256; ++i) {
+      if (cum + s_sum[i] >= need) { s_pick = i; break; }
+      cum += s_sum[i];
+    }
+    s_sum[0] = cum;  // count above the picked thread's range (thread 0 re-reads it below)
+  }
+  __syncthreads();
+  const int pick = s_pick;
+  if (t == pick) {
+    unsigned cum = s_sum[0];  // count above this thread's bins (written by thread 0's scan)
+    int bin = 0;
+    for (int j = 0; j < PER; ++j) {
+      if (cum + v[j] >= need) { bin = kHistBins - 1 - (t * PER + j); break; }
+      cum += v[j];
+    }
+    if (level == 1) {
+      sel[b * 2] = (uint32_t)bin;
+      sel[b * 2 + 1] = cum;
+    } else {
+      sel[b * 2 + 1] = (sel[b * 2] << 20) | ((uint32_t)bin << 8);
+    }
+  }
+  if (t == 0 && (pick < 0 || all)) {  // fewer than k keys: every anchor passes
+    if (level == 1) { sel[b * 2] = 0xffffffffu; sel[b * 2 + 1] = 0; }
+    else sel[b * 2 + 1] = 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) hb[kHistBins - 1 - (t * PER + j)] = 0;
+}
+
 }  // namespace
 
+// sel: [B][2] uint32 scratch, hist: [B][4096] uint32 zero-initialised once
+// (self-resetting).  On return sel[b][1] is frame b's ordered max-logit key
+// threshold admitting its top k anchors (pass it to tca_anchor_decode_filter_keyed).
+TCA_API int tca_anchor_topk_threshold(const void* cls, int dtype, int layout, int batch, int H, int W, int A, int C,
+                                      int ld_cls, int k, unsigned* hist, uint32_t* sel, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  dim3 grid((H * W * A + kAnchorsPerBlock - 1) / kAnchorsPerBlock, batch);
+  const int ldc = ld_cls > 0 ? ld_cls : A * C;
+  for (int level = 1; level <= 2; ++level) {
+    switch (dtype) {
+      case kF32: anchor_hist_kernel<float><<<grid, 256, 0, stream>>>((const float*)cls, layout, H, W, A, C, ldc, level,
+                                                                      sel, hist); break;
+      case kF16: anchor_hist_kernel<__half><<<grid, 256, 0, stream>>>((const __half*)cls, layout, H, W, A, C, ldc,
+                                                                       level, sel, hist); break;
+      case kBF16: anchor_hist_kernel<__hip_bfloat16><<<grid, 256, 0, stream>>>((const __hip_bfloat16*)cls, layout, H,
+                                                                               W, A, C, ldc, level, sel, hist); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    anchor_select_kernel<<<batch, 256, 0, stream>>>(hist, level, k, sel);
+  }
+  TCA_LAUNCH_CHECK();
+}
+
 // table: host [A][6] (dxa, dya, dza, za, rot, diag).
-TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const void* dir, int dtype, int layout, int batch,
-                                     int H, int W, int A, int C, int bins, int ld_cls, int ld_box, int ld_dir,
-                                     const float* table, float x0, float xs,
-                                     float y0, float ys, float dir_offset, float dir_limit_offset, float score_thresh,
-                                     float* cand_box, float* cand_score, int* cand_label, uint64_t* cand_key,
-                                     int* cand_count, int cap, hipStream_t stream) {
+static int anchor_decode_launch(const void* cls, const void* box, const void* dir, int dtype, int layout, int batch,
+                                int H, int W, int A, int C, int bins, int ld_cls, int ld_box, int ld_dir,
+                                const float* table, float x0, float xs, float y0, float ys, float dir_offset,
+                                float dir_limit_offset, float score_thresh, const uint32_t* key_thr, float* cand_box,
+                                float* cand_score, int* cand_label, uint64_t* cand_key, int* cand_count, int cap,
+                                hipStream_t stream) {
   if (batch <= 0) return 0;
   if (A > 8) return (int)hipErrorInvalidValue;
   AnchorTable tb;
@@ -165,7 +300,7 @@ TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const voi
   anchor_decode_kernel<T><<<grid, 256, 0, stream>>>((const T*)cls, (const T*)box, (const T*)dir, layout, H, W, A, C, \
                                                     bins, ld_cls > 0 ? ld_cls : A * C, ld_box > 0 ? ld_box : A * 7,  \
                                                     ld_dir > 0 ? ld_dir : A * bins, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset,          \
-                                                    score_thresh, cand_box, cand_score, cand_label, cand_key,        \
+                                                    score_thresh, key_thr, cand_box, cand_score, cand_label, cand_key, \
                                                     cand_count, cap)
   switch (dtype) {
     case kF32: LAUNCH(float); break;
@@ -175,4 +310,28 @@ TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const voi
   }
 #undef LAUNCH
   TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_anchor_decode_filter(const void* cls, const void* box, const void* dir, int dtype, int layout, int batch,
+                                     int H, int W, int A, int C, int bins, int ld_cls, int ld_box, int ld_dir,
+                                     const float* table, float x0, float xs,
+                                     float y0, float ys, float dir_offset, float dir_limit_offset, float score_thresh,
+                                     float* cand_box, float* cand_score, int* cand_label, uint64_t* cand_key,
+                                     int* cand_count, int cap, hipStream_t stream) {
+  return anchor_decode_launch(cls, box, dir, dtype, layout, batch, H, W, A, C, bins, ld_cls, ld_box, ld_dir, table, x0,
+                              xs, y0, ys, dir_offset, dir_limit_offset, score_thresh, nullptr, cand_box, cand_score,
+                              cand_label, cand_key, cand_count, cap, stream);
+}
+
+// Same, but an anchor passes iff its ordered max-logit key >= key_thr[b]
+// (device array from tca_anchor_topk_threshold; sel + 1 with stride 2).
+TCA_API int tca_anchor_decode_filter_keyed(const void* cls, const void* box, const void* dir, int dtype, int layout,
+                                           int batch, int H, int W, int A, int C, int bins, int ld_cls, int ld_box,
+                                           int ld_dir, const float* table, float x0, float xs, float y0, float ys,
+                                           float dir_offset, float dir_limit_offset, const uint32_t* sel,
+                                           float* cand_box, float* cand_score, int* cand_label, uint64_t* cand_key,
+                                           int* cand_count, int cap, hipStream_t stream) {
+  return anchor_decode_launch(cls, box, dir, dtype, layout, batch, H, W, A, C, bins, ld_cls, ld_box, ld_dir, table, x0,
+                              xs, y0, ys, dir_offset, dir_limit_offset, 0.f, sel, cand_box, cand_score, cand_label,
+                              cand_key, cand_count, cap, stream);
 }

@@ -51,9 +51,29 @@ __global__ void __launch_bounds__(1024) topk_sort_kernel(const uint64_t* __restr
       const int shift = 56 - 8 * pass;
       for (int i = tid; i < 256; i += nt) hist[i] = 0;
       __syncthreads();
-      for (int i = tid; i < n; i += nt) {
-        uint64_t key = kb[i];
-        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1);
+      // In the high passes nearly every key shares one digit (scores in a
+      // narrow band), and 64 lanes adding to one LDS word serialise: fold each
+      // wave's dominant digits into one atomic each, the rest go direct.
+      const int lane = tid & 63;
+      for (int i0 = 0; i0 < n; i0 += nt) {  // uniform trip count: every lane reaches the ballots
+        const int i = i0 + tid;
+        bool m = false;
+        int d = 0;
+        if (i < n) {
+          const uint64_t key = kb[i];
+          m = (key & pmask) == prefix;
+          d = (int)((key >> shift) & 255);
+        }
+        for (int round = 0; round < 2; ++round) {
+          const unsigned long long mm = __ballot(m);
+          if (!mm) break;
+          const int leader = __ffsll(mm) - 1;
+          const int dl = __shfl(d, leader, 64);
+          const unsigned long long same = __ballot(m && d == dl);
+          if (lane == leader) atomicAdd(&hist[dl], __popcll(same));
+          if (d == dl) m = false;
+        }
+        if (m) atomicAdd(&hist[d], 1);
       }
       __syncthreads();
       if (tid == 0) {

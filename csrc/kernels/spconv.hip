@@ -111,61 +111,78 @@ __global__ void __launch_bounds__(256) sp_vfe_voxels_kernel(const float* __restr
 
 // ---- output sites of a strided SparseConv3d ------------------------------------
 // Each input row proposes the sites it reaches; the first proposer of a site
-// claims it (atomicCAS -1 -> -2) and the wave's claims take one contiguous
-// row range with a single atomicAdd (ballot + popcount ranks).  Row order
-// depends on timing, values do not (each output row's sum runs over taps in
-// a fixed order), so results are run-to-run identical.
+// claims it (atomicCAS -1 -> -2; a plain load first skips sites already
+// claimed — most are: a site is proposed by ~7 inputs; a stale load can only
+// read -1, which just costs the CAS).  A thread records its claims as a tap
+// bitmask, the block scans the claim counts and takes ONE contiguous row
+// range with a single atomicAdd (the first version's per-tap wave atomic on
+// one counter serialised at the L2 channel), then each thread re-derives its
+// claimed sites from the mask and writes rows + coords.  Row order depends
+// on timing, values do not (each output row's sum runs over taps in a fixed
+// order), so results are run-to-run identical.
 __global__ void __launch_bounds__(256) sp_claim_kernel(const int4* __restrict__ coords_in, const int* __restrict__ n_in_p,
                                                        int cap_in, Ksp k, Dims od, int* __restrict__ grid_out,
                                                        int4* __restrict__ coords_out, int* __restrict__ n_out,
                                                        int cap_out) {
+  __shared__ int s_scan[256 / 64 + 1];
+  __shared__ int s_base;
   const int n = min(*n_in_p, cap_in);
-  const int lane = threadIdx.x & 63;
+  const int kyx = k.ky * k.kx;
   for (int base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
     const int r = base + threadIdx.x;
     const bool act = r < n;
     const int4 c = act ? coords_in[r] : make_int4(0, 0, 0, 0);
-    for (int kz = 0; kz < k.kz; ++kz) {
-      const int zn = c.y + k.pz - kz;
-      const int oz = zn / k.sz;
-      const bool vz = act && zn >= 0 && oz * k.sz == zn && oz < od.z;
-      for (int ky = 0; ky < k.ky; ++ky) {
-        const int yn = c.z + k.py - ky;
-        const int oy = yn / k.sy;
-        const bool vy = vz && yn >= 0 && oy * k.sy == yn && oy < od.y;
-        for (int kx = 0; kx < k.kx; ++kx) {
-          const int xn = c.w + k.px - kx;
-          const int ox = xn / k.sx;
-          const bool v = vy && xn >= 0 && ox * k.sx == xn && ox < od.x;
-          long cell = 0;
-          bool claimed = false;
-          if (v) {
-            cell = (((long)c.x * od.z + oz) * od.y + oy) * od.x + ox;
-            claimed = atomicCAS(&grid_out[cell], -1, -2) == -1;
-          }
-          const unsigned long long m = __ballot(claimed);
-          if (m) {
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            int b0 = 0;
-            if (lane == leader) b0 = atomicAdd(n_out, __popcll(m));
-            b0 = __shfl(b0, leader, 64);
-            if (claimed) {
-              const int row = b0 + __popcll(m & ((1ull << lane) - 1ull));
-              if (row < cap_out) {
-                grid_out[cell] = row;
-                coords_out[row] = make_int4(c.x, oz, oy, ox);
-              }
+    unsigned cm = 0;
+    int cnt = 0;
+    if (act) {
+      int t = 0;
+      for (int kz = 0; kz < k.kz; ++kz) {
+        const int zn = c.y + k.pz - kz;
+        const int oz = zn / k.sz;
+        const bool vz = zn >= 0 && oz * k.sz == zn && oz < od.z;
+        for (int ky = 0; ky < k.ky; ++ky) {
+          const int yn = c.z + k.py - ky;
+          const int oy = yn / k.sy;
+          const bool vy = vz && yn >= 0 && oy * k.sy == yn && oy < od.y;
+          for (int kx = 0; kx < k.kx; ++kx, ++t) {
+            const int xn = c.w + k.px - kx;
+            const int ox = xn / k.sx;
+            if (!(vy && xn >= 0 && ox * k.sx == xn && ox < od.x)) continue;
+            int* g = grid_out + ((((long)c.x * od.z + oz) * od.y + oy) * od.x + ox);
+            if (*g != -1) continue;
+            if (atomicCAS(g, -1, -2) == -1) {
+              cm |= 1u << t;
+              ++cnt;
             }
           }
         }
       }
     }
+    int total;
+    int row = block_excl_scan(cnt, s_scan, &total);
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, total) : 0;
+    __syncthreads();
+    row += s_base;
+    while (cm) {
+      const int t = __ffs(cm) - 1;
+      cm &= cm - 1;
+      const int kz = t / kyx, ky = (t - kz * kyx) / k.kx, kx = t - kz * kyx - ky * k.kx;
+      const int oz = (c.y + k.pz - kz) / k.sz, oy = (c.z + k.py - ky) / k.sy, ox = (c.w + k.px - kx) / k.sx;
+      if (row < cap_out) {
+        grid_out[(((long)c.x * od.z + oz) * od.y + oy) * od.x + ox] = row;
+        coords_out[row] = make_int4(c.x, oz, oy, ox);
+      }
+      ++row;
+    }
+    __syncthreads();  // s_base / s_scan are reused by the next iteration
   }
 }
 
 // ---- neighbour table + tap masks -------------------------------------------------
 // One thread per output row; a wave is exactly one 64-row tile (base is a
-// multiple of 256), so the tile's tap mask is a wave OR-reduction.
+// multiple of 256), so the tile's tap mask is a wave OR-reduction.  Layout
+// nbr[tile][tap][64]: the 64 lanes' stores of one tap are one contiguous
+// 256-B run, and the GEMM stages a tile's table with one contiguous copy.
 __global__ void __launch_bounds__(256) sp_rulebook_kernel(const int4* __restrict__ coords, const int* __restrict__ n_p,
                                                           int cap, Ksp k, Dims id, const int* __restrict__ grid_in,
                                                           int* __restrict__ nbr, unsigned* __restrict__ tapmask) {
@@ -176,7 +193,7 @@ __global__ void __launch_bounds__(256) sp_rulebook_kernel(const int4* __restrict
     unsigned bits = 0;
     if (o < n) {
       const int4 c = coords[o];
-      int* dst = nbr + (long)o * KT;
+      int* dst = nbr + (long)(o >> 6) * KT * 64 + (o & 63);  // [tile][tap][64 rows]: coalesced per tap
       int t = 0;
       for (int kz = 0; kz < k.kz; ++kz) {
         const int iz = c.y * k.sz - k.pz + kz;
@@ -187,7 +204,7 @@ __global__ void __launch_bounds__(256) sp_rulebook_kernel(const int4* __restrict
             int r = -1;
             if ((unsigned)iz < (unsigned)id.z && (unsigned)iy < (unsigned)id.y && (unsigned)ix < (unsigned)id.x)
               r = grid_in[(((long)c.x * id.z + iz) * id.y + iy) * id.x + ix];
-            dst[t] = r;
+            dst[t * 64] = r;
             if (r >= 0) bits |= 1u << t;
           }
         }
@@ -227,7 +244,7 @@ constexpr int kMaxSteps = 64;
 struct SpGemmArgs {
   const __hip_bfloat16* in;  // input rows [*, Cin]
   int cin_log2;
-  const int* nbr;            // [cap, KT]
+  const int* nbr;            // [ceil(cap/64)][KT][64]
   int kt;
   const unsigned* tapmask;   // [ceil(cap / 64)]
   const __hip_bfloat16* w;   // [N, Kp], k = tap * Cin + ci, zero-padded
@@ -271,7 +288,7 @@ __global__ void __launch_bounds__(256) sp_gemm_kernel(SpGemmArgs a) {
   for (int tile = blockIdx.x; tile * BM < M; tile += gridDim.x) {
     const int m0 = tile * BM;
     const int rows = min(BM, M - m0);
-    for (int i = tid; i < BM * KT; i += 256) s_nbr[i] = i < rows * KT ? a.nbr[(long)m0 * KT + i] : -1;
+    for (int i = tid; i < BM * KT; i += 256) s_nbr[i] = (i & 63) < rows ? a.nbr[(long)tile * KT * 64 + i] : -1;
     if (tid == 0) {
       const unsigned msk = a.tapmask[tile];
       int ns = 0;
@@ -298,7 +315,7 @@ __global__ void __launch_bounds__(256) sp_gemm_kernel(SpGemmArgs a) {
           const int row = id >> 2, k0 = s * SBK + (id & 3) * 8;
           const int tap = k0 >> a.cin_log2;
           if (tap < KT) {
-            const int r = s_nbr[row * KT + tap];
+            const int r = s_nbr[tap * 64 + row];
             if (r >= 0) v = *reinterpret_cast<const uint4*>(a.in + ((long)r << a.cin_log2) + (k0 & cmask));
           }
         }
@@ -532,6 +549,7 @@ TCA_API int tca_sp_vfe_voxels(const float* voxels, int cap, int P, int F, const 
 // ksp: [kz, ky, kx, sz, sy, sx, pz, py, px]; odims: output (z, y, x).
 TCA_API int tca_sp_claim(const int* coords_in, const int* n_in, int cap_in, const int* ksp, const int* odims,
                          int* grid_out, int* coords_out, int* n_out, int cap_out, hipStream_t stream) {
+  if (ksp[0] * ksp[1] * ksp[2] > 32) return (int)hipErrorInvalidValue;
   sp_claim_kernel<<<grid_for(cap_in, 256, 2048), 256, 0, stream>>>((const int4*)coords_in, n_in, cap_in,
                                                                    make_ksp(ksp), make_dims(odims), grid_out,
                                                                    (int4*)coords_out, n_out, cap_out);

@@ -240,3 +240,30 @@ def test_second_pipeline_graph(cuda):
         np.testing.assert_array_equal(b["box"], c["box"])
         assert a["box"].shape[1] == 7 and len(a["score"]) <= cfg.nms_post_max
         assert (a["score"] >= cfg.score_thresh).all()
+
+
+@pytest.mark.gpu
+def test_proposal_topk_preselection_matches_full_decode(cuda):
+    """Exact top-k key threshold (tca_anchor_topk_threshold) + keyed decode
+    selects the same proposals as decoding and radix-selecting every anchor."""
+    from triton_client_amd.models.second import proposal_config
+    from triton_client_amd.ops.lidar import AnchorPostprocess
+    cfg = proposal_config(_small_cfg())
+    H, W = cfg.feature_map_size
+    torch.manual_seed(0)
+    cls = (torch.randn(2, 18, H, W) * 2).to(cuda)
+    cls[1, :, :4] = 3.0  # ties at the top
+    box = (torch.randn(2, 42, H, W) * 0.2).to(cuda)
+    dir_ = torch.randn(2, 12, H, W).to(cuda)
+    fast = AnchorPostprocess(cfg, 2, device=cuda)
+    assert fast.topk_select
+    full = AnchorPostprocess(cfg, 2, device=cuda)
+    full.topk_select = False
+    a = fast(cls, box, dir_)
+    b = full(cls, box, dir_)
+    torch.cuda.synchronize()
+    assert torch.equal(a.count, b.count) and (a.count == cfg.proposal_post_max).all()
+    for k in range(2):
+        n = int(a.count[k])
+        torch.testing.assert_close(a.box[k, :n], b.box[k, :n])
+        torch.testing.assert_close(a.score[k, :n], b.score[k, :n])

@@ -289,6 +289,9 @@ class AnchorPostprocess:
         self.A = cfg.num_anchors_per_loc
         self.C = cfg.num_classes
         self.cap = min(self.H * self.W * self.A, 1 << 20)
+        # exact top-k preselection (tca_anchor_topk_threshold) when every anchor would
+        # pass the score filter and only pre_max of them reach the NMS
+        self.topk_select = cfg.score_thresh <= 0.0 and cfg.nms_pre_max < self.H * self.W * self.A
         if self.device.type == "cuda":
             self.ws = Workspace(self.device)
 
@@ -315,13 +318,30 @@ class AnchorPostprocess:
             lds = (0, 0, 0)
             dt, B = dtype_code(c), c.shape[0]
         cfg = self.cfg
+        s = _native.stream_ptr(stream)
+        if self.topk_select:
+            # no score threshold and pre_max << anchors (SECONDHead proposals): find each
+            # frame's exact top-k key threshold first, decode only those anchors
+            hist = self.ws.get("anc_hist", (B, 4096), torch.int32, init=0)
+            sel = self.ws.get("anc_sel", (B, 2), torch.int32)
+            _native.call("tca_anchor_topk_threshold", pc, dt, lay, B, self.H, self.W, self.A, self.C, lds[0],
+                         int(cfg.nms_pre_max), _native.ptr(hist), _native.ptr(sel), s)
+            cand = Candidates.alloc(self.ws, "anc_", B, self.cap, 7)
+            _native.call("tca_anchor_decode_filter_keyed", pc, pb, pd, dt, lay,
+                         B, self.H, self.W, self.A, self.C, cfg.num_dir_bins, *lds, self._table, float(self.x0),
+                         float(self.xs), float(self.y0), float(self.ys), float(cfg.dir_offset),
+                         float(cfg.dir_limit_offset), _native.ptr(sel), _native.ptr(cand.box),
+                         _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key),
+                         _native.ptr(cand.count), self.cap, s)
+            return sort_and_nms(self.ws, cand, 1, cfg.nms_thresh, cfg.nms_pre_max, cfg.nms_post_max, True, None,
+                                prefix="anc_nms_", stream=stream)
         cand = Candidates.alloc(self.ws, "anc_", B, self.cap, 7)
         _native.call("tca_anchor_decode_filter", pc, pb, pd, dt, lay,
                      B, self.H, self.W, self.A, self.C, cfg.num_dir_bins, *lds, self._table, float(self.x0),
                      float(self.xs), float(self.y0), float(self.ys), float(cfg.dir_offset),
                      float(cfg.dir_limit_offset), float(cfg.score_thresh), _native.ptr(cand.box),
                      _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count),
-                     self.cap, _native.stream_ptr(stream))
+                     self.cap, s)
         return sort_and_nms(self.ws, cand, 1, cfg.nms_thresh, cfg.nms_pre_max, cfg.nms_post_max, True, None,
                             prefix="anc_nms_", stream=stream)
 

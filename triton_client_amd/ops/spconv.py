@@ -131,11 +131,11 @@ class SparseBackbone:
                        bias.to(self.device).contiguous(), kp, ksp)
             if spec.subm:
                 if lev.subm_nbr is None:
-                    lev.subm_nbr = ws.get(f"sp_nbr_s{cur}", (lev.cap, 27), torch.int32)
+                    lev.subm_nbr = ws.get(f"sp_nbr_s{cur}", (_ceil(lev.cap, 64), 27), torch.int32)
                     lev.subm_mask = ws.get(f"sp_mask_s{cur}", ((lev.cap + 63) // 64,), torch.int32)
                 L.nbr, L.mask = lev.subm_nbr, lev.subm_mask
             else:
-                L.nbr = ws.get(f"sp_nbr_d{i}", (lev.cap, T), torch.int32)
+                L.nbr = ws.get(f"sp_nbr_d{i}", (_ceil(lev.cap, 64), T), torch.int32)
                 L.mask = ws.get(f"sp_mask_d{i}", ((lev.cap + 63) // 64,), torch.int32)
             assert x.shape[1] == cin_p, (i, x.shape, cin_p)
             L.inp = x
