@@ -287,3 +287,24 @@ def test_centerpoint_served_over_kserve():
         q = m.detections[0].bbox.center.orientation
         assert abs(q.z - np.sin(p["pred_boxes"][0, 8] / 2)) < 1e-5
         ch.close()
+
+
+def test_second_iou_served_over_kserve():
+    """second_iou contract (examples/second_iou/config.pbtxt): the client voxelises
+    with the served SECOND geometry (5 points per voxel, 0.05 m x 0.05 m x 0.1 m),
+    the server runs the sparse 3D backbone + RoI IoU head, 7-d boxes come back."""
+    from triton_client_amd.config.lidar import KITTI_SECOND_VOXELS, SecondIoUConfig
+    from triton_client_amd.server.models import SecondIoUModel
+    v = dataclasses.replace(KITTI_SECOND_VOXELS, point_cloud_range=(0.0, -12.8, -3.0, 25.6, 12.8, 1.0),
+                            max_voxels=16000)
+    cfg = SecondIoUConfig(voxel=v, score_thresh=0.0)
+    repo = ModelRepository("cpu")
+    repo.add(SecondIoUModel("second_iou", cfg=cfg, device="cpu"))
+    with KServeServer(repo, "127.0.0.1:0") as srv:
+        ch = GRPCChannel({"grpc_channel": srv.target}, Flags("second_iou"))
+        eng = RemoteDetector3D(ch, Pointpillars_client(), z_offset=0.0)
+        assert eng.pre.cfg == v and eng.pre.cfg.max_points_per_voxel == 5
+        p = eng.detect([_cloud(2)])[0]
+        assert p["pred_boxes"].shape[1] == 7 and 0 < len(p["pred_scores"]) <= cfg.nms_post_max
+        assert set(np.unique(p["pred_labels"])) <= {1, 2, 3}
+        ch.close()

@@ -267,3 +267,22 @@ def test_proposal_topk_preselection_matches_full_decode(cuda):
         n = int(a.count[k])
         torch.testing.assert_close(a.box[k, :n], b.box[k, :n])
         torch.testing.assert_close(a.score[k, :n], b.score[k, :n])
+
+
+@pytest.mark.gpu
+def test_second_iou_served_model_gpu(cuda):
+    """The served second_iou model on the GPU path (run_voxels on received voxels)."""
+    from triton_client_amd.server.models import SecondIoUModel
+    m = SecondIoUModel("second_iou", device="cuda")
+    m.load()
+    cfg = m.cfg
+    p = lidar_sweep(LidarSpec(sensor_height=3.23), 7)
+    p = p[~np.isnan(p).any(1)]
+    p[:, 2] += 1.5
+    v, zyx, num, _ = voxelize_np(p, cfg.voxel, 4)
+    coords = np.concatenate([np.zeros((len(zyx), 1), np.int32), zyx], 1)
+    out = m.execute({"voxels": v, "voxel_coords": coords, "voxel_num_points": num.astype(np.int32)}, None)
+    assert out["pred_boxes"].shape[1] == 7 and 0 < len(out["pred_scores"]) <= cfg.nms_post_max
+    assert out["pred_labels"].dtype == np.int64 and np.isfinite(out["pred_boxes"]).all()
+    out2 = m.execute({"voxels": v, "voxel_coords": coords, "voxel_num_points": num.astype(np.int32)}, None)
+    np.testing.assert_array_equal(out["pred_boxes"], out2["pred_boxes"])

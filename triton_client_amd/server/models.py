@@ -6,6 +6,7 @@
   [1,3,H,W]), output ``output`` FP32 [1, N, 5+nc] decoded rows — what the
   reference's ONNX export returns.  On MI355X: bf16 channels_last network +
   the HIP decode kernel writing the decoded tensor.
+* :class:`SecondIoUModel` — ``second_iou`` (sparse 3D conv backbone + RoI IoU head).
 * :class:`PointPillarsModel` — ``pointpillar_kitti``
   (``examples/pointpillar_kitti/config.pbtxt``): inputs ``voxels`` [-1,P,4],
   ``voxel_coords`` INT32 [-1,4] (b,z,y,x), ``voxel_num_points`` INT32 [-1];
@@ -193,6 +194,111 @@ class PointPillarsModel(ServedModel):
         return {"pred_boxes": res.box[0, :k].cpu().numpy().astype(np.float32),
                 "pred_scores": res.score[0, :k].cpu().numpy().astype(np.float32),
                 "pred_labels": res.cls[0, :k].cpu().numpy().astype(np.int64)}
+
+
+class SecondIoUModel(ServedModel):
+    """``second_iou`` — OpenPCDet SECONDNetIoU (``examples/second_iou/config.pbtxt``,
+    KIND_GPU; ``examples/second_iou/1/model.py``): inputs ``voxels`` FP32
+    [-1, 5, 4], ``voxel_coords`` INT32 [-1, 4] (b, z, y, x), ``voxel_num_points``
+    INT32 [-1] — the client's KITTI voxels (``data/kitti_dataset.yaml``); outputs
+    ``pred_boxes`` FP32 [-1, 7], ``pred_scores`` FP32 [-1] (sigmoid IoU),
+    ``pred_labels`` INT64 [-1] (1-based).  GPU: MeanVFE + sparse 3D backbone
+    (spconv.hip gather-GEMMs) from the received voxels, fused BEV convs,
+    proposal top-k + rotated NMS, RoI grid pool + FC IoU head, final NMS."""
+
+    def __init__(self, name: str = "second_iou", cfg=None, device="auto", weights: Optional[str] = None,
+                 seed: int = 0, calibrate_target: float = 60.0):
+        from ..config.lidar import SecondIoUConfig
+
+        super().__init__(name)
+        self.cfg = cfg or SecondIoUConfig()
+        self.device = _device(device)
+        self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+        self.P = self.cfg.voxel.max_points_per_voxel
+
+    def inputs(self):
+        return [tensor_spec("voxels", "FP32", [-1, self.P, 4]), tensor_spec("voxel_coords", "INT32", [-1, 4]),
+                tensor_spec("voxel_num_points", "INT32", [-1])]
+
+    def outputs(self):
+        return [tensor_spec("pred_boxes", "FP32", [-1, 7], output=True),
+                tensor_spec("pred_scores", "FP32", [-1], output=True),
+                tensor_spec("pred_labels", "INT64", [-1], output=True)]
+
+    def instance_kind(self):
+        return mc.ModelInstanceGroup.KIND_GPU if self.device.type == "cuda" else mc.ModelInstanceGroup.KIND_CPU
+
+    def config(self):
+        c = super().config()
+        v = self.cfg.voxel
+        for k, val in (("point_cloud_range", list(v.point_cloud_range)), ("voxel_size", list(v.voxel_size)),
+                       ("max_points_per_voxel", v.max_points_per_voxel), ("max_voxels", v.max_voxels),
+                       ("class_names", list(self.cfg.class_names))):
+            c.parameters[k].string_value = json.dumps(val)
+        return c
+
+    def load(self):
+        from ..models.common import fuse_model
+        from ..models.second import build_second_iou
+
+        model = build_second_iou(self.cfg, self.seed)
+        if self.weights:
+            model.load_state_dict(torch.load(self.weights, map_location="cpu", weights_only=True))
+        if self.device.type == "cuda":
+            from ..pipelines.second import SecondPipeline
+            from ..utils.synthetic import LidarSpec, lidar_sweep
+
+            spec = LidarSpec(sensor_height=3.23)
+            maxp = ((spec.points_per_sweep + 1023) // 1024) * 1024
+            self.pipe = SecondPipeline(model, batch=1, max_points=maxp, device=self.device, z_offset=1.5)
+            if not self.weights:
+                c = lidar_sweep(spec, self.seed)
+                raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+                self.pipe.data[: raw.numel()].copy_(raw)
+                self.pipe.frame_n.fill_(c.shape[0])
+                self.pipe.calibrate_detection_density(self.calibrate_target)
+            V = self.cfg.voxel.max_voxels
+            self.voxels = torch.zeros((V, self.P, 4), dtype=torch.float32, device=self.device)
+            self.coords = torch.zeros((V, 4), dtype=torch.int32, device=self.device)
+            self.nump = torch.zeros((V,), dtype=torch.int32, device=self.device)
+            self.vcount = torch.zeros((1,), dtype=torch.int32, device=self.device)
+            self.model = self.pipe.model
+        else:
+            self.model = fuse_model(model.eval())
+        self.ready = True
+
+    @torch.no_grad()
+    def execute(self, inputs, requested):
+        vox, co, n = inputs["voxels"], inputs["voxel_coords"], inputs["voxel_num_points"]
+        V = vox.shape[0]
+        if vox.shape[1] != self.P or vox.shape[2] < 4:
+            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
+        if V > self.cfg.voxel.max_voxels:
+            raise InferError(f"{V} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+        v = torch.from_numpy(np.require(vox[..., :4], np.float32, ['C', 'W']))
+        c = torch.from_numpy(np.require(co, np.int32, ['C', 'W'])).clone()
+        c[:, 0] = 0
+        nn_ = torch.from_numpy(np.require(n, np.int32, ['C', 'W']))
+        if self.device.type == "cuda":
+            self.voxels[:V].copy_(v)
+            self.coords[:V].copy_(c)
+            self.nump[:V].copy_(nn_)
+            self.vcount.fill_(V)
+            res = self.pipe.run_voxels(self.voxels, self.nump, self.coords, self.vcount)
+            k = int(res.count[0])
+            return {"pred_boxes": res.box[0, :k].cpu().numpy().astype(np.float32),
+                    "pred_scores": res.score[0, :k].cpu().numpy().astype(np.float32),
+                    "pred_labels": res.cls[0, :k].cpu().numpy().astype(np.int64)}
+        from ..models.second import postprocess_reference, proposal_config
+        from ..ops.lidar import AnchorPostprocess
+        m = self.model
+        bev = m.sparse_forward(v, nn_.long(), c, 1)
+        sf, cls, box, dr = m.bev_forward(bev)
+        props = AnchorPostprocess(proposal_config(self.cfg), 1, device="cpu").cpu(cls, box, dr)
+        logits = m.roi_iou(sf, props.box)
+        bx, sc, lb = postprocess_reference(props.box, props.cls, props.count, logits, self.cfg)[0]
+        return {"pred_boxes": bx.astype(np.float32), "pred_scores": sc.astype(np.float32),
+                "pred_labels": lb.astype(np.int64)}
 
 
 class CenterPointModel(ServedModel):

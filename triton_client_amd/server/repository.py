@@ -44,9 +44,18 @@ def _family(name: str) -> Optional[str]:
         return "detectron"
     if "centerpoint" in n:
         return "centerpoint"
+    if "second" in n:
+        return "second_iou"
     if "echo" in n:
         return "echo"
     return None
+
+
+def _second(name):
+    def f(device="auto", **kw):
+        from .models import SecondIoUModel
+        return SecondIoUModel(name, device=device, **kw)
+    return f
 
 
 def _centerpoint(name):
@@ -78,6 +87,7 @@ FACTORIES: Dict[str, Factory] = {
     "pointpillar_kitti": _pointpillars("pointpillar_kitti"),
     "pointpillar_python": _pointpillars("pointpillar_python"),
     "centerpoint_pp": _centerpoint("centerpoint_pp"),
+    "second_iou": _second("second_iou"),  # examples/second_iou/config.pbtxt
     "YOLOv4": _yolov4("YOLOv4"),  # examples/YOLOv4/config.pbtxt
     "test_model": _detectron("test_model", "retinanet"),  # examples/RetinaNet_detectron/config.pbtxt
     "RetinaNet_detectron": _detectron("RetinaNet_detectron", "retinanet"),
@@ -181,6 +191,9 @@ class ModelRepository:
             elif fam == "centerpoint":
                 from .models import CenterPointModel
                 m = CenterPointModel(name, device=device)
+            elif fam == "second_iou":
+                from .models import SecondIoUModel
+                m = SecondIoUModel(name, device=device)
             else:
                 continue
             repo.add(m, load=load)
