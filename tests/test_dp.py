@@ -122,3 +122,67 @@ def test_dp_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert all(v == "ok" for v in res.values()), res
+
+
+def _fault_worker(rank, world, port, q):
+    """Rank 2 serves one batch, then its process dies without any cleanup; rank
+    0's HealthMonitor notices the stalled heartbeat and the next batches are
+    re-sharded over ranks {0, 1} with unchanged results."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import faulthandler
+    import time
+    faulthandler.dump_traceback_later(150, exit=True)
+    try:
+        from triton_client_amd.parallel.dp import DataParallelDetector2D, HealthMonitor, init_distributed
+
+        info = init_distributed("gloo")
+        mon = HealthMonitor(info, interval=0.1, timeout=1.0)
+        dp = DataParallelDetector2D(FakeDetector(), info, max_det=8, monitor=mon)
+        frames = [np.full((8, 12, 3), 7 * i, np.uint8) for i in range(9)]
+        want = FakeDetector().detect(frames)
+        if info.is_main:
+            got = dp.detect(frames)
+            assert all(np.array_equal(a, b) for a, b in zip(got, want))
+            assert mon.alive() == [0, 1, 2]
+            q.put((2, "wait"))  # let rank 2 die before the next batch
+            time.sleep(2.5)
+            for _ in range(2):
+                got = dp.detect(frames)
+                assert all(np.array_equal(a, b) for a, b in zip(got, want))
+            assert mon.alive() == [0, 1] and mon.dead == {2}
+            dp.close()
+            q.put((0, "ok"))
+        elif rank == 1:
+            assert dp.serve() == 3
+            q.put((1, "ok"))
+        else:
+            hdr = dp._recv_header()
+            dp._step(hdr, None)
+            mon.stop()
+            os._exit(0)  # simulated crash: no close, no heartbeat, sockets drop
+        mon.stop()
+        q.close()
+        q.join_thread()  # flush the result before the hard exit
+        os._exit(0)
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        q.close()
+        q.join_thread()
+        os._exit(1)
+
+
+def test_dp_rank_failure_resharding():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert res == {0: "ok", 1: "ok", 2: "wait"}, res

@@ -73,5 +73,14 @@ def maybe_data_parallel(engine, three_d: bool = False):
         from ..models.common import broadcast_parameters
 
         broadcast_parameters(engine.model)  # every replica runs rank 0's weights
-    wrap = DataParallelDetector3D(engine, info) if three_d else DataParallelDetector2D(engine, info)
+    # rank-failure detection: heartbeats over the c10d store; a dead rank's
+    # shards are re-split over the survivors (TCA_DP_HEARTBEAT=0 disables)
+    monitor = None
+    if os.environ.get("TCA_DP_HEARTBEAT", "1") != "0":
+        from ..parallel.dp import HealthMonitor
+
+        monitor = HealthMonitor(info, timeout=float(os.environ.get("TCA_DP_HEARTBEAT_TIMEOUT", "5")))
+    box_dim = 9 if getattr(engine, "family", "") == "centerpoint" else 7
+    wrap = (DataParallelDetector3D(engine, info, box_dim=box_dim, monitor=monitor) if three_d
+            else DataParallelDetector2D(engine, info, monitor=monitor))
     return wrap, info

@@ -76,6 +76,8 @@ class PFNLayer(nn.Module):
 
     @torch.no_grad()
     def fuse_bn(self) -> None:
+        if self.fused_weight is not None:  # idempotent: a shared model is fused (fp32) once
+            return
         s = self.norm.weight / torch.sqrt(self.norm.running_var + self.norm.eps)
         self.fused_weight = (self.linear.weight * s.view(-1, 1)).detach().clone()
         self.fused_bias = (self.norm.bias - self.norm.running_mean * s).detach().clone()

@@ -69,6 +69,8 @@ class PillarVFE(nn.Module):
 
     @torch.no_grad()
     def fuse_bn(self) -> None:
+        if self.fused_weight is not None:  # idempotent: a shared model is fused (fp32) once
+            return
         scale = self.norm.weight / torch.sqrt(self.norm.running_var + self.norm.eps)
         self.fused_weight = (self.linear.weight * scale.view(-1, 1)).contiguous()
         self.fused_bias = (self.norm.bias - self.norm.running_mean * scale).contiguous()

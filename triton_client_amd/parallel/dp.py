@@ -73,20 +73,23 @@ class FrameExchange:
         self.info = info
         self.group = group
 
-    def scatter(self, src: Optional[Sequence[Sequence[torch.Tensor]]], dst: Sequence[torch.Tensor]) -> None:
-        """src (rank 0 only): src[r][k] is the k-th tensor for rank r; dst[k]
-        receives this rank's share.  Async w.r.t. the host; ordered on the
-        current stream."""
+    def scatter(self, src: Optional[Sequence[Sequence[torch.Tensor]]], dst: Sequence[torch.Tensor],
+                peers: Optional[Sequence[int]] = None) -> None:
+        """src (rank 0 only): src[i][k] is the k-th tensor for rank peers[i]
+        (peers defaults to every rank; peers[0] is rank 0); dst[k] receives
+        this rank's share.  Async w.r.t. the host; ordered on the current
+        stream."""
         info = self.info
         if info.world == 1:
             for d, s in zip(dst, src[0]):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
             return
+        peers = list(peers) if peers is not None else list(range(info.world))
         ops = []
         if info.rank == 0:
-            for r in range(1, info.world):
-                for s in src[r]:
+            for i, r in enumerate(peers[1:], 1):
+                for s in src[i]:
                     ops.append(dist.P2POp(dist.isend, s, r, self.group))
             for d, s in zip(dst, src[0]):
                 if d.data_ptr() != s.data_ptr():
@@ -98,18 +101,21 @@ class FrameExchange:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
 
-    def gather(self, src: Sequence[torch.Tensor], dst: Optional[Sequence[Sequence[torch.Tensor]]]) -> None:
-        """src: this rank's tensors; dst (rank 0 only): dst[r][k] receives rank r's k-th tensor."""
+    def gather(self, src: Sequence[torch.Tensor], dst: Optional[Sequence[Sequence[torch.Tensor]]],
+               peers: Optional[Sequence[int]] = None) -> None:
+        """src: this rank's tensors; dst (rank 0 only): dst[i][k] receives rank
+        peers[i]'s k-th tensor (peers defaults to every rank)."""
         info = self.info
         if info.world == 1:
             for d, s in zip(dst[0], src):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
             return
+        peers = list(peers) if peers is not None else list(range(info.world))
         ops = []
         if info.rank == 0:
-            for r in range(1, info.world):
-                for d in dst[r]:
+            for i, r in enumerate(peers[1:], 1):
+                for d in dst[i]:
                     ops.append(dist.P2POp(dist.irecv, d, r, self.group))
             for d, s in zip(dst[0], src):
                 if d.data_ptr() != s.data_ptr():
@@ -147,37 +153,136 @@ def shutdown(info: DistInfo) -> None:
 _STOP = -1
 
 
-def _bcast_ints(info: DistInfo, vals: Optional[Sequence[int]], n: int) -> List[int]:
-    t = torch.zeros(n, dtype=torch.int64, device=info.device)
-    if info.is_main:
-        t[: len(vals)] = torch.tensor(list(vals), dtype=torch.int64)
-    dist.broadcast(t, 0)
-    return [int(v) for v in t.tolist()]
+class HealthMonitor:
+    """Rank-failure detection for the host-level DP detectors.
+
+    Every rank's background thread bumps a heartbeat counter in the c10d
+    TCPStore (its own client connection, independent of the RCCL / gloo data
+    plane, so a wedged communicator does not hide liveness).  Rank 0 declares a
+    rank dead when its counter has not moved for ``timeout`` seconds of rank
+    0's own monotonic clock (no cross-host clock comparison).  Detects crashed
+    or killed processes; a rank whose process lives but whose serve loop hangs
+    keeps beating (the per-step exception path below covers broken links)."""
+
+    PREFIX = "tca_hb/"
+
+    def __init__(self, info: DistInfo, interval: float = 0.25, timeout: float = 2.0, store=None):
+        import threading
+        import time
+
+        self.info, self.interval, self.timeout = info, interval, timeout
+        self._time = time
+        host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500"))
+        self.store = store or dist.TCPStore(host, port, info.world, is_master=False,
+                                            timeout=datetime.timedelta(seconds=30), wait_for_workers=False)
+        self.dead: set = set()
+        self._seen = {}  # rank -> (counter, monotonic time it last changed)
+        self._beats = 0
+        self._stop = threading.Event()
+        self.store.set(self._key(info.rank), "0")
+        self._thread = threading.Thread(target=self._run, name="tca-heartbeat", daemon=True)
+        self._thread.start()
+
+    def _key(self, r: int) -> str:
+        return f"{self.PREFIX}{r}"
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.interval):
+            self._beats += 1
+            try:
+                self.store.set(self._key(self.info.rank), str(self._beats))
+            except Exception:  # store gone (rank 0 exited): stop beating
+                return
+
+    def alive(self) -> List[int]:
+        """Rank 0: the ranks currently considered alive (always includes 0)."""
+        now = self._time.monotonic()
+        for r in range(1, self.info.world):
+            if r in self.dead:
+                continue
+            try:
+                v = int(self.store.get(self._key(r))) if self.store.check([self._key(r)]) else -1
+            except Exception:
+                v = -1
+            last = self._seen.get(r)
+            if last is None or v != last[0]:
+                self._seen[r] = (v, now)
+            elif now - last[1] > self.timeout:
+                self.dead.add(r)
+        return [0] + [r for r in range(1, self.info.world) if r not in self.dead]
+
+    def wait_for_change(self, before: Sequence[int]) -> List[int]:
+        """After a failed step: poll until some participant is declared dead
+        (up to 2x timeout); returns the new live set (unchanged if none died)."""
+        t_end = self._time.monotonic() + 2 * self.timeout + self.interval
+        while self._time.monotonic() < t_end:
+            now = self.alive()
+            if len(now) < len(before):
+                return now
+            self._time.sleep(self.interval)
+        return self.alive()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=2 * self.interval + 1)
+
+
+_HDR = 16  # header ints; the last slot carries the participant bitmask
 
 
 class _DPBase:
     """Rank 0 calls ``detect(items)``; every other rank calls ``serve()``,
     which runs until rank 0 calls ``close()``.  Work is split into
-    contiguous equal shards (padded), scattered with grouped p2p, run by each
-    rank's local engine, and gathered back as fixed-size padded buffers."""
+    contiguous equal shards (padded) over the participating ranks, scattered
+    with grouped p2p, run by each rank's local engine, and gathered back as
+    fixed-size padded buffers.  Headers go point-to-point, so a dead rank is
+    simply left out: with a :class:`HealthMonitor` the shards are re-split over
+    the survivors (rank 0 alone runs everything as the last resort), and a
+    step that fails mid-flight (broken peer link) is retried on the new live
+    set."""
 
-    def __init__(self, local, info: DistInfo):
+    def __init__(self, local, info: DistInfo, monitor: Optional[HealthMonitor] = None):
         self.local, self.info = local, info
         self.ex = FrameExchange(info)
         self.names = getattr(local, "names", [])
+        self.monitor = monitor
+        self.retries = 0
+
+    def _participants(self) -> List[int]:
+        return self.monitor.alive() if self.monitor is not None else list(range(self.info.world))
 
     def close(self) -> None:
         if self.info.world > 1 and self.info.is_main:
-            self._header([_STOP])
+            self._send_header([_STOP], self._participants())
 
-    def _header(self, vals):
-        return _bcast_ints(self.info, vals, 16)
+    def _send_header(self, vals, parts: Sequence[int]) -> List[int]:
+        mask = 0
+        for r in parts:
+            mask |= 1 << r
+        v = list(vals) + [0] * (_HDR - len(vals))
+        v[_HDR - 1] = mask
+        t = torch.tensor(v, dtype=torch.int64, device=self.info.device)
+        for r in parts:
+            if r != 0:
+                dist.send(t, r)
+        return v
+
+    def _recv_header(self) -> List[int]:
+        t = torch.zeros(_HDR, dtype=torch.int64, device=self.info.device)
+        dist.recv(t, 0)
+        return [int(x) for x in t.tolist()]
+
+    @staticmethod
+    def _workers(hdr) -> List[int]:
+        mask = hdr[_HDR - 1]
+        return [r for r in range(63) if (mask >> r) & 1]
 
     def serve(self) -> int:
         """Non-main ranks: process shards until rank 0 closes.  Returns shards done."""
         n = 0
         while True:
-            hdr = self._header(None)
+            hdr = self._recv_header()
             if hdr[0] == _STOP:
                 return n
             self._step(hdr, None)
@@ -188,14 +293,23 @@ class _DPBase:
             return self.local.detect(items)
         if not items:
             return []
-        return self._step(self._header(self._make_header(items)), items)
+        while True:
+            parts = self._participants()
+            if parts == [0]:
+                return self.local.detect(items)  # every peer is gone: degrade to rank 0 alone
+            try:
+                return self._step(self._send_header(self._make_header(items), parts), items)
+            except RuntimeError:
+                if self.monitor is None or len(self.monitor.wait_for_change(parts)) == len(parts):
+                    raise
+                self.retries += 1
 
 
 class DataParallelDetector2D(_DPBase):
     """Frames (HxWx3 uint8, one size per call) → per-frame [n, 6] detections."""
 
-    def __init__(self, local, info: DistInfo, max_det: int = 300):
-        super().__init__(local, info)
+    def __init__(self, local, info: DistInfo, max_det: int = 300, monitor: Optional[HealthMonitor] = None):
+        super().__init__(local, info, monitor)
         self.max_det = max_det
 
     def _make_header(self, frames):
@@ -210,18 +324,20 @@ class DataParallelDetector2D(_DPBase):
     def _step(self, hdr, frames):
         info = self.info
         n, H, W = hdr[:3]
-        per = (n + info.world - 1) // info.world
+        wk = self._workers(hdr)
+        nw, me = len(wk), wk.index(info.rank)
+        per = (n + nw - 1) // nw
         dev = info.device
         src = None
         if info.is_main:
-            buf = torch.zeros((info.world, per, H, W, 3), dtype=torch.uint8)
+            buf = torch.zeros((nw, per, H, W, 3), dtype=torch.uint8)
             for i, f in enumerate(frames):
                 buf[i // per, i % per] = torch.from_numpy(np.ascontiguousarray(f[..., :3]))
             buf = buf.to(dev)
-            src = [[buf[r]] for r in range(info.world)]
+            src = [[buf[r]] for r in range(nw)]
         mine = torch.empty((per, H, W, 3), dtype=torch.uint8, device=dev)
-        self.ex.scatter(src, [mine])
-        valid = max(0, min(per, n - info.rank * per))
+        self.ex.scatter(src, [mine], wk)
+        valid = max(0, min(per, n - me * per))
         host = mine[:valid].cpu().numpy()
         dets = self.local.detect([host[i] for i in range(valid)]) if valid else []
         pad = torch.zeros((per, self.max_det, 6), dtype=torch.float32)
@@ -233,8 +349,8 @@ class DataParallelDetector2D(_DPBase):
         pad, cnt = pad.to(dev), cnt.to(dev)
         dst = None
         if info.is_main:
-            dst = [[torch.empty_like(pad), torch.empty_like(cnt)] for _ in range(info.world)]
-        self.ex.gather([pad, cnt], dst)
+            dst = [[torch.empty_like(pad), torch.empty_like(cnt)] for _ in range(nw)]
+        self.ex.gather([pad, cnt], dst, wk)
         if not info.is_main:
             return None
         out = []
@@ -248,8 +364,9 @@ class DataParallelDetector2D(_DPBase):
 class DataParallelDetector3D(_DPBase):
     """PointCloud2 messages (same field layout per call) → per-cloud dicts."""
 
-    def __init__(self, local, info: DistInfo, max_out: int = 500, box_dim: int = 7):
-        super().__init__(local, info)
+    def __init__(self, local, info: DistInfo, max_out: int = 500, box_dim: int = 7,
+                 monitor: Optional[HealthMonitor] = None):
+        super().__init__(local, info, monitor)
         self.max_out, self.box_dim = max_out, box_dim
 
     def _make_header(self, clouds):
@@ -267,22 +384,24 @@ class DataParallelDetector3D(_DPBase):
         info = self.info
         n, step, maxb = hdr[:3]
         offs, dts = hdr[3:7], hdr[7:11]
-        per = (n + info.world - 1) // info.world
+        wk = self._workers(hdr)
+        nw, me = len(wk), wk.index(info.rank)
+        per = (n + nw - 1) // nw
         dev = info.device
         src = None
         if info.is_main:
-            buf = torch.zeros((info.world, per, maxb), dtype=torch.uint8)
-            npts = torch.zeros((info.world, per), dtype=torch.int64)
+            buf = torch.zeros((nw, per, maxb), dtype=torch.uint8)
+            npts = torch.zeros((nw, per), dtype=torch.int64)
             for i, c in enumerate(clouds):
                 raw = np.frombuffer(c.data, np.uint8)
                 buf[i // per, i % per, : raw.size] = torch.from_numpy(raw.copy())
                 npts[i // per, i % per] = c.width * c.height
             buf, npts = buf.to(dev), npts.to(dev)
-            src = [[buf[r], npts[r]] for r in range(info.world)]
+            src = [[buf[r], npts[r]] for r in range(nw)]
         mine = torch.empty((per, maxb), dtype=torch.uint8, device=dev)
         mine_n = torch.empty((per,), dtype=torch.int64, device=dev)
-        self.ex.scatter(src, [mine, mine_n])
-        valid = max(0, min(per, n - info.rank * per))
+        self.ex.scatter(src, [mine, mine_n], wk)
+        valid = max(0, min(per, n - me * per))
         fields = [msgs.PointField(k, o, d, 1) for k, o, d in zip(("x", "y", "z", "intensity"), offs, dts)]
         hb, hn = mine.cpu().numpy(), mine_n.cpu().numpy()
         local = [msgs.PointCloud2(height=1, width=int(hn[i]), fields=fields, point_step=step,
@@ -301,8 +420,8 @@ class DataParallelDetector3D(_DPBase):
             lab[i, :k] = torch.from_numpy(np.asarray(p["pred_labels"][:k], np.int64))
             cnt[i] = k
         mine_out = [t.to(dev) for t in (box, score, lab, cnt)]
-        dst = [[torch.empty_like(t) for t in mine_out] for _ in range(info.world)] if info.is_main else None
-        self.ex.gather(mine_out, dst)
+        dst = [[torch.empty_like(t) for t in mine_out] for _ in range(nw)] if info.is_main else None
+        self.ex.gather(mine_out, dst, wk)
         if not info.is_main:
             return None
         out = []
