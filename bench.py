@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--columns", type=int, default=1875)
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic frames per rank")
     ap.add_argument("--ingest", choices=["local", "rccl"], default="local")
+    ap.add_argument("--comm", choices=["torch", "native"], default="torch",
+                    help="DP scatter/gather: torch batch_isend_irecv or the C++ RCCL communicator")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
@@ -255,7 +257,12 @@ def main():
         runner = _Split()
     else:
         runner = GraphRunner(pipeline_step, enabled=not args.no_graph)
-    ex = FrameExchange(info)
+    native = None
+    if args.comm == "native" and info.world > 1:
+        from triton_client_amd.parallel.rccl import NativeComm
+
+        native = NativeComm.from_info(info)
+    ex = FrameExchange(info, native=native)
 
     dsts = [t for t in ((cam.frames,) if use_cam else ()) + ((lid.data, lid.frame_n) if use_lid else ())]
     # ---------------- ingest: local mode prefetches step t+1's frames (H2D on a copy
@@ -401,6 +408,7 @@ def main():
                 "parallelism": f"dp{info.world}",
                 "frames_per_gpu_per_step": B,
                 "ingest": args.ingest,
+                "comm": args.comm,
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,
                 "branch_streams": 2 if side is not None else 1,

@@ -1,0 +1,71 @@
+"""Native RCCL communicator (csrc/runtime/rccl_comm.cpp, parallel/rccl.py).
+
+CPU: the runtime library exports the communicator ABI with declared argtypes.
+GPU (world 1 — a one-GPU box cannot hold two ranks of one RCCL communicator):
+grouped send/recv to self, MAX all-reduce, broadcast, async-error polling and
+the FrameExchange plumbing through the native path."""
+import pytest
+import torch
+
+from triton_client_amd import _native
+
+SYMS = ("tca_rccl_unique_id_bytes", "tca_rccl_get_unique_id", "tca_rccl_comm_init", "tca_rccl_comm_destroy",
+        "tca_rccl_comm_abort", "tca_rccl_async_error", "tca_rccl_error_string", "tca_rccl_group_p2p",
+        "tca_rccl_allreduce_max_f64", "tca_rccl_broadcast")
+
+
+def test_runtime_exports_rccl_abi():
+    lib = _native.runtime()
+    for s in SYMS:
+        assert getattr(lib, s).argtypes is not None, s
+    assert lib.tca_rccl_unique_id_bytes() == 128
+    assert b"success" in lib.tca_rccl_error_string(0).lower()
+
+
+@pytest.mark.gpu
+def test_native_comm_world1():
+    from triton_client_amd.parallel.rccl import RECV, SEND, NativeComm
+
+    torch.cuda.set_device(0)
+    comm = NativeComm(0, 1)
+    try:
+        assert comm.async_error() is None
+        a = torch.arange(1000, dtype=torch.float32, device="cuda")
+        b = torch.empty_like(a)
+        odd_src = torch.arange(7, dtype=torch.uint8, device="cuda")  # byte path (7 B)
+        odd_dst = torch.zeros_like(odd_src)
+        comm.group_p2p([(SEND, a, 0), (RECV, b, 0), (SEND, odd_src, 0), (RECV, odd_dst, 0)])
+        torch.cuda.synchronize()
+        assert torch.equal(a, b) and torch.equal(odd_src, odd_dst)
+        t = torch.tensor([3.5, -1.0], dtype=torch.float64, device="cuda")
+        comm.allreduce_max_(t)
+        x = torch.randn(33, device="cuda")
+        y = x.clone()
+        comm.broadcast_(y, 0)
+        torch.cuda.synchronize()
+        assert t.tolist() == [3.5, -1.0] and torch.equal(x, y)
+        with pytest.raises(ValueError):
+            comm.group_p2p([(SEND, a.cpu(), 0)])
+        with pytest.raises(ValueError):
+            comm.group_p2p([(SEND, a, 1)])
+        assert comm.async_error() is None
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
+def test_frame_exchange_native_ops():
+    """FrameExchange's op list through the native group on one rank."""
+    from triton_client_amd.parallel.dp import DistInfo, FrameExchange
+    from triton_client_amd.parallel.rccl import NativeComm
+
+    comm = NativeComm(0, 1)
+    try:
+        ex = FrameExchange(DistInfo(0, 1, 0, torch.device("cuda", 0)), native=comm)
+        src = torch.randint(0, 255, (3, 64, 64, 3), dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+        ex._run([(0, src, 0), (1, dst, 0)])
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+    finally:
+        comm.close()

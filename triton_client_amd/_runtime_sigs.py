@@ -11,6 +11,17 @@ SIGS = {
     "tca_kserve_request_size": (L, [CP, CP, CP, I, PP, PP, P, P, P, I, PP]),
     "tca_kserve_encode_request": (L, [CP, CP, CP, I, PP, PP, P, P, P, P, I, PP, P, L]),
     "tca_kserve_parse_response": (I, [P, L, I, P, P, I, P, P]),
+    # native RCCL communicator (csrc/runtime/rccl_comm.cpp)
+    "tca_rccl_unique_id_bytes": (I, []),
+    "tca_rccl_get_unique_id": (I, [P]),
+    "tca_rccl_comm_init": (I, [ctypes.POINTER(P), I, P, I]),
+    "tca_rccl_comm_destroy": (I, [P]),
+    "tca_rccl_comm_abort": (I, [P]),
+    "tca_rccl_async_error": (I, [P]),
+    "tca_rccl_error_string": (CP, [I]),
+    "tca_rccl_group_p2p": (I, [P, I, P, P, P, P, P]),
+    "tca_rccl_allreduce_max_f64": (I, [P, P, ctypes.c_int64, P]),
+    "tca_rccl_broadcast": (I, [P, P, ctypes.c_int64, I, P]),
 }
 
 

@@ -67,11 +67,27 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Dis
 
 
 class FrameExchange:
-    """Grouped p2p scatter/gather of fixed-shape tensor sets."""
+    """Grouped p2p scatter/gather of fixed-shape tensor sets.
 
-    def __init__(self, info: DistInfo, group=None):
+    ``native``: a :class:`~triton_client_amd.parallel.rccl.NativeComm`; the
+    plan is then issued as one C++ RCCL group on the current stream instead of
+    through ``batch_isend_irecv`` (GPU tensors only)."""
+
+    def __init__(self, info: DistInfo, group=None, native=None):
         self.info = info
         self.group = group
+        self.native = native
+
+    def _run(self, ops) -> None:
+        """ops: (0 send | 1 recv, tensor, peer)."""
+        if not ops:
+            return
+        if self.native is not None:
+            self.native.group_p2p(ops)
+            return
+        p2p = [dist.P2POp(dist.isend if k == 0 else dist.irecv, t, p, self.group) for k, t, p in ops]
+        for w in dist.batch_isend_irecv(p2p):
+            w.wait()
 
     def scatter(self, src: Optional[Sequence[Sequence[torch.Tensor]]], dst: Sequence[torch.Tensor],
                 peers: Optional[Sequence[int]] = None) -> None:
@@ -89,17 +105,13 @@ class FrameExchange:
         ops = []
         if info.rank == 0:
             for i, r in enumerate(peers[1:], 1):
-                for s in src[i]:
-                    ops.append(dist.P2POp(dist.isend, s, r, self.group))
+                ops += [(0, s, r) for s in src[i]]
             for d, s in zip(dst, src[0]):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
         else:
-            for d in dst:
-                ops.append(dist.P2POp(dist.irecv, d, 0, self.group))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            ops += [(1, d, 0) for d in dst]
+        self._run(ops)
 
     def gather(self, src: Sequence[torch.Tensor], dst: Optional[Sequence[Sequence[torch.Tensor]]],
                peers: Optional[Sequence[int]] = None) -> None:
@@ -115,17 +127,13 @@ class FrameExchange:
         ops = []
         if info.rank == 0:
             for i, r in enumerate(peers[1:], 1):
-                for d in dst[i]:
-                    ops.append(dist.P2POp(dist.irecv, d, r, self.group))
+                ops += [(1, d, r) for d in dst[i]]
             for d, s in zip(dst[0], src):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
         else:
-            for s in src:
-                ops.append(dist.P2POp(dist.isend, s, 0, self.group))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            ops += [(0, s, 0) for s in src]
+        self._run(ops)
 
 
 def barrier(info: DistInfo) -> None:
