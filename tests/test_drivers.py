@@ -287,6 +287,11 @@ def test_centerpoint_served_over_kserve():
         q = m.detections[0].bbox.center.orientation
         assert abs(q.z - np.sin(p["pred_boxes"][0, 8] / 2)) < 1e-5
         ch.close()
+    # the in-process engine (same seed, same voxeliser) returns the served result
+    local = LocalDetector3D(cfg=cfg, device="cpu", family="centerpoint", z_offset=0.0)
+    assert local.family == "centerpoint" and local.box_dim == 9
+    lp = local.detect([_cloud(3)])[0]
+    np.testing.assert_allclose(np.sort(lp["pred_scores"]), np.sort(p["pred_scores"]), rtol=1e-5, atol=1e-6)
 
 
 def test_second_iou_served_over_kserve():
@@ -308,3 +313,10 @@ def test_second_iou_served_over_kserve():
         assert p["pred_boxes"].shape[1] == 7 and 0 < len(p["pred_scores"]) <= cfg.nms_post_max
         assert set(np.unique(p["pred_labels"])) <= {1, 2, 3}
         ch.close()
+    local = LocalDetector3D(cfg=cfg, device="cpu", family="second_iou", z_offset=0.0)
+    lp = local.detect([_cloud(2)])[0]
+    assert lp["pred_boxes"].shape == p["pred_boxes"].shape
+    np.testing.assert_allclose(np.sort(lp["pred_scores"]), np.sort(p["pred_scores"]), rtol=1e-5, atol=1e-6)
+    from triton_client_amd.cli.engines import lidar_family
+    assert [lidar_family(n) for n in ("second_iou", "pointpillar_kitti", "centerpoint_pp")] == [
+        "second_iou", "pointpillars", "centerpoint"]

@@ -45,6 +45,24 @@ def test_local_3d_engine_gpu(cuda):
         assert (p["pred_scores"] >= 0.1 - 1e-6).all()
 
 
+@pytest.mark.parametrize("family,labels,dim", [("second_iou", {1, 2, 3}, 7), ("centerpoint", set(range(10)), 9)])
+def test_local_3d_engine_families_gpu(cuda, family, labels, dim):
+    """main3d.py -m second_iou / centerpoint_pp --engine local: the family's
+    graph-captured pipeline behind the same Detector3D interface."""
+    from triton_client_amd.inference import LocalDetector3D
+
+    eng = LocalDetector3D(batch=2, device=cuda, family=family)
+    clouds = [_cloud(s, 64, 1875) for s in range(3)]
+    a = eng.detect(clouds)
+    b = eng.detect(clouds[::-1])[::-1]
+    assert len(a) == 3 and all(len(p["pred_scores"]) > 0 for p in a)
+    for x, y in zip(a, b):  # micro-batch position must not matter
+        np.testing.assert_array_equal(x["pred_boxes"], y["pred_boxes"])
+    for p in a:
+        assert p["pred_boxes"].shape[1] == dim and np.isfinite(p["pred_boxes"]).all()
+        assert set(np.unique(p["pred_labels"])) <= labels
+
+
 def test_gpu_server_models_over_kserve(cuda):
     from triton_client_amd.channel.grpc_channel import GRPCChannel
     from triton_client_amd.clients import Pointpillars_client, Yolov5client

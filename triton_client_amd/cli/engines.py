@@ -41,12 +41,23 @@ def engine_2d(flags, params, letterbox=None, conf_thres=None):
     return eng, ch, client
 
 
+def lidar_family(model_name: str) -> str:
+    """Model family of a served 3D model name (the reference's ``-m`` values:
+    ``second_iou`` by default in .vscode/launch.json, ``pointpillar_kitti``)."""
+    n = model_name.lower()
+    if "second" in n:
+        return "second_iou"
+    if "centerpoint" in n or "nusc" in n:
+        return "centerpoint"
+    return "pointpillars"
+
+
 def engine_3d(flags, params):
     if flags.engine == "local":
         from ..inference import LocalDetector3D
 
         eng = LocalDetector3D(batch=max(1, flags.frames_per_step), device=flags.device, weights=flags.weights,
-                              z_offset=flags.z_offset)
+                              z_offset=flags.z_offset, family=lidar_family(flags.model_name))
         return eng, None, None
     from ..inference import RemoteDetector3D
 

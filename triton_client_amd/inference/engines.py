@@ -52,8 +52,8 @@ def _empty2d() -> np.ndarray:
     return np.zeros((0, 6), np.float32)
 
 
-def _empty3d() -> dict:
-    return {"pred_boxes": np.zeros((0, 7), np.float32), "pred_scores": np.zeros((0,), np.float32),
+def _empty3d(box_dim: int = 7) -> dict:
+    return {"pred_boxes": np.zeros((0, box_dim), np.float32), "pred_scores": np.zeros((0,), np.float32),
             "pred_labels": np.zeros((0,), np.int64)}
 
 
@@ -148,25 +148,54 @@ class LocalDetector2D(Detector2D):
 
 
 class LocalDetector3D(Detector3D):
-    """PointPillars on this GPU through :class:`~triton_client_amd.pipelines.LidarPipeline`
-    (PointCloud2 payload bytes in, boxes out).  On a GPU-less host the same
-    semantics run on the CPU (vectorised voxeliser + module forward)."""
+    """A LiDAR detector on this GPU (PointCloud2 payload bytes in, boxes out):
+
+    * ``family="pointpillars"`` — :class:`~triton_client_amd.pipelines.LidarPipeline`
+      (KITTI PointPillars, the served ``pointpillar_kitti``);
+    * ``"second_iou"`` — :class:`~triton_client_amd.pipelines.SecondPipeline`
+      (the reference's default 3D model, ``main3d.py -m second_iou``);
+    * ``"centerpoint"`` — :class:`~triton_client_amd.pipelines.centerpoint.CenterPointPipeline`
+      (nuScenes, 9-d boxes with yaw at index 8, 0-based labels).
+
+    On a GPU-less host the same semantics run on the CPU (vectorised
+    voxeliser + the fp32 reference modules)."""
+
+    FAMILIES = {"pointpillars": 2000.0, "second_iou": 60.0, "centerpoint": 1000.0}  # default calibration targets
+    Z_OFFSET = {"pointpillars": 1.5, "second_iou": 1.5, "centerpoint": 0.0}
 
     def __init__(self, cfg=None, batch: int = 1, device="auto", graph: bool = True, weights: Optional[str] = None,
-                 calibrate_target: Optional[float] = 2000.0, z_offset: float = 1.5, normalize_intensity: bool = True,
-                 seed: int = 0, max_points: int = 131072):
-        from ..config.lidar import PointPillarsConfig
-        from ..models.pointpillars import build_pointpillars
-
+                 calibrate_target="auto", z_offset: Optional[float] = None, normalize_intensity: bool = True,
+                 seed: int = 0, max_points: int = 131072, family: str = "pointpillars"):
+        if family not in self.FAMILIES:
+            raise ValueError(f"family {family!r}: one of {sorted(self.FAMILIES)}")
+        self.family = family
         self.device = _device(device)
-        self.cfg = cfg or PointPillarsConfig()
-        self.B, self.z_offset, self.normalize = batch, z_offset, normalize_intensity
+        if family == "pointpillars":
+            from ..config.lidar import PointPillarsConfig
+            from ..models.pointpillars import build_pointpillars
+
+            self.cfg = cfg or PointPillarsConfig()
+            self.model = build_pointpillars(self.cfg, seed)
+        elif family == "second_iou":
+            from ..config.lidar import SecondIoUConfig
+            from ..models.second import build_second_iou
+
+            self.cfg = cfg or SecondIoUConfig()
+            self.model = build_second_iou(self.cfg, seed)
+        else:
+            from ..config.lidar import CenterPointConfig
+            from ..models.centerpoint import build_centerpoint
+
+            self.cfg = cfg or CenterPointConfig()
+            self.model = build_centerpoint(self.cfg, seed)
+        self.box_dim = 9 if family == "centerpoint" else 7
+        self.B, self.normalize = batch, normalize_intensity
+        self.z_offset = self.Z_OFFSET[family] if z_offset is None else z_offset
         self.graph = graph and self.device.type == "cuda"
-        self.model = build_pointpillars(self.cfg, seed)
         if weights:
             self.model.load_state_dict(torch.load(weights, map_location="cpu", weights_only=True))
             calibrate_target = None
-        self.calibrate_target = calibrate_target
+        self.calibrate_target = self.FAMILIES[family] if calibrate_target == "auto" else calibrate_target
         self.max_points = max_points
         self.names = list(self.cfg.class_names)
         self._pipes: Dict[tuple, tuple] = {}
@@ -174,8 +203,18 @@ class LocalDetector3D(Detector3D):
         self._cpu = None
 
     # ----------------------------------------------------------------- GPU path
+    def _pipeline_cls(self):
+        if self.family == "second_iou":
+            from ..pipelines import SecondPipeline
+            return SecondPipeline
+        if self.family == "centerpoint":
+            from ..pipelines.centerpoint import CenterPointPipeline
+            return CenterPointPipeline
+        from ..pipelines import LidarPipeline
+        return LidarPipeline
+
     def _pipe(self, layout, npts: int, sample: msgs.PointCloud2):
-        from ..pipelines import GraphRunner, LidarPipeline
+        from ..pipelines import GraphRunner
 
         maxp = self.max_points
         while maxp < npts:
@@ -184,8 +223,8 @@ class LocalDetector3D(Detector3D):
         ent = self._pipes.get(key)
         if ent is not None and ent[0].max_points >= npts:
             return ent
-        p = LidarPipeline(self.model, batch=self.B, max_points=maxp, layout=layout, z_offset=self.z_offset,
-                          normalize_intensity=self.normalize, device=self.device)
+        p = self._pipeline_cls()(self.model, batch=self.B, max_points=maxp, layout=layout, z_offset=self.z_offset,
+                                 normalize_intensity=self.normalize, device=self.device)
         if self.calibrate_target is not None:
             raw = torch.frombuffer(bytearray(sample.data), dtype=torch.uint8)
             for b in range(self.B):
@@ -199,19 +238,42 @@ class LocalDetector3D(Detector3D):
         self._pipes[key] = ent
         return ent
 
+    def _sample_cloud(self, seed: int):
+        from ..ros.compat import create_cloud_xyzi
+        from ..utils.synthetic import LidarSpec, lidar_sweep
+
+        spec = (LidarSpec(rings=32, azimuth_steps=1800, sensor_height=1.8) if self.family == "centerpoint"
+                else LidarSpec(sensor_height=3.23))
+        pts = lidar_sweep(spec, seed)
+        return create_cloud_xyzi(np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4))
+
     def calibrate_synthetic(self, seed: int = 0) -> None:
         """Set the random-init head prior from a synthetic sweep (rank-independent)."""
         if self.calibrate_target is None:
             return
-        from ..ros.compat import cloud_layout, create_cloud_xyzi
-        from ..utils.synthetic import LidarSpec, lidar_sweep
+        from ..ros.compat import cloud_layout
 
-        pts = lidar_sweep(LidarSpec(sensor_height=3.23), seed)
-        cloud = create_cloud_xyzi(np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4))
+        cloud = self._sample_cloud(seed)
         if self.device.type == "cuda":
             self._pipe(cloud_layout(cloud), cloud.width, cloud)
         else:
             self._detect_cpu(cloud)
+
+    def _frames_out(self, res) -> List[dict]:
+        """Pipeline result → per-frame dicts in the sensor frame (z offset removed)."""
+        if self.family == "centerpoint":
+            per = res.per_image()
+            for d in per:
+                d["pred_boxes"] = d["pred_boxes"].copy()
+                d["pred_boxes"][:, 2] -= self.z_offset
+            return per
+        out = []
+        for d in res.per_image():
+            box = d["box"].astype(np.float32).copy()
+            box[:, 2] -= self.z_offset
+            out.append({"pred_boxes": box, "pred_scores": d["score"].astype(np.float32),
+                        "pred_labels": d["cls"].astype(np.int64)})
+        return out
 
     @torch.no_grad()
     def detect(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
@@ -244,14 +306,9 @@ class LocalDetector3D(Detector3D):
                     p.data.copy_(pinned, non_blocking=True)
                     p.frame_n.copy_(nh, non_blocking=True)
                     with trace_range("lidar_graph"):
-                        res = run()
-                        per = res.per_image()
+                        per = self._frames_out(run())
                     for j, i in enumerate(chunk):
-                        d = per[j]
-                        box = d["box"].astype(np.float32).copy()
-                        box[:, 2] -= self.z_offset
-                        out[i] = {"pred_boxes": box, "pred_scores": d["score"].astype(np.float32),
-                                  "pred_labels": d["cls"].astype(np.int64)}
+                        out[i] = per[j]
         return out
 
     # ----------------------------------------------------------------- CPU path
@@ -261,6 +318,8 @@ class LocalDetector3D(Detector3D):
         from ..ops.lidar import AnchorPostprocess, voxelize_np
         from ..ros.compat import cloud_to_numpy
 
+        if self.family != "pointpillars":
+            return self._detect_cpu_voxels(cloud)
         if self._cpu is None:
             self.model = fuse_model(self.model.eval()).float()
             self._cpu = AnchorPostprocess(self.cfg, 1, device="cpu")
@@ -281,6 +340,33 @@ class LocalDetector3D(Detector3D):
         box[:, 2] -= self.z_offset
         return {"pred_boxes": box, "pred_scores": np.asarray(res.score[0, :k], np.float32),
                 "pred_labels": np.asarray(res.cls[0, :k]).astype(np.int64)}
+
+    def _detect_cpu_voxels(self, cloud: msgs.PointCloud2) -> dict:
+        """SECOND-IoU / CenterPoint on the CPU: the client-side voxeliser, then
+        the served model's CPU path (same code as the KServe ``second_iou`` /
+        ``centerpoint_pp`` models).  Random-init heads are not calibrated here."""
+        from ..models.common import fuse_model
+        from ..ops.lidar import voxelize_np
+        from ..ros.compat import cloud_to_numpy
+
+        if self._cpu is None:
+            from ..server.models import CenterPointModel, SecondIoUModel
+
+            m = (SecondIoUModel if self.family == "second_iou" else CenterPointModel)(cfg=self.cfg, device="cpu")
+            self.model = m.model = fuse_model(self.model.eval()).float()
+            m.ready = True
+            self._cpu = m
+            self.calibrate_target = None
+        pts = cloud_to_numpy(cloud, normalize_intensity=self.normalize, z_offset=self.z_offset)
+        v, zyx, num, _ = voxelize_np(pts, self.cfg.voxel, 4)
+        if len(v) == 0:
+            return _empty3d(self.box_dim)
+        coords = np.pad(zyx, ((0, 0), (1, 0))).astype(np.int32)
+        out = self._cpu.execute({"voxels": v, "voxel_coords": coords, "voxel_num_points": num.astype(np.int32)}, None)
+        out = dict(out)
+        out["pred_boxes"] = np.asarray(out["pred_boxes"], np.float32).copy()
+        out["pred_boxes"][:, 2] -= self.z_offset
+        return out
 
     def _calibrate_cpu(self, feats, coords):
         """CPU twin of LidarPipeline.calibrate_detection_density (bias shift only)."""
