@@ -125,7 +125,21 @@ class LocalDetector2D(Detector2D):
 
     @torch.no_grad()
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
+        return self._run(frames, annotate=False)[0]
+
+    @torch.no_grad()
+    def detect_annotated(self, frames: Sequence[np.ndarray], thickness: int = 2):
+        """→ (annotated frames, detections).  The rectangles are drawn on the
+        GPU into the pipeline's resident frame buffer (K15, ``ops.image.draw_boxes_``)
+        and come back in the one D2H copy the publisher needs; only the label
+        text is left to the host."""
+        return self._run(frames, annotate=True, thickness=thickness)
+
+    def _run(self, frames, annotate: bool, thickness: int = 2):
+        from ..ops.image import draw_boxes_
+
         out: List[Optional[np.ndarray]] = [None] * len(frames)
+        imgs: List[Optional[np.ndarray]] = [None] * len(frames)
         groups: Dict[Tuple[int, int], List[int]] = {}
         for i, f in enumerate(frames):
             groups.setdefault(tuple(f.shape[:2]), []).append(i)
@@ -139,12 +153,17 @@ class LocalDetector2D(Detector2D):
                     p.frames.copy_(pinned, non_blocking=True)
                     with trace_range("camera_graph"):
                         res = run()
+                        if annotate:
+                            draw_boxes_(p.frames, res.box, res.cls, res.count, thickness)
+                            host = p.frames[:len(chunk)].cpu().numpy()
                         per = res.per_image()
                     for j, i in enumerate(chunk):
                         d = per[j]
                         out[i] = np.concatenate([d["box"], d["score"][:, None],
                                                  d["cls"][:, None].astype(np.float32)], 1).astype(np.float32)
-        return out
+                        if annotate:
+                            imgs[i] = host[j]
+        return out, imgs
 
 
 class LocalDetector3D(Detector3D):

@@ -81,12 +81,19 @@ class RosInference(BaseInference):
         timer = StageTimer(self.metrics)
         with timer("decode"):
             rgb = [decode_image_msg(m) for m in images]
+        gpu_draw = self.draw and hasattr(self.engine, "detect_annotated") and \
+            getattr(getattr(self.engine, "device", None), "type", "cpu") == "cuda"
         with timer("detect"):
-            dets = self.engine.detect(rgb)
+            if gpu_draw:  # rectangles drawn on the GPU (K15), labels below
+                dets, drawn = self.engine.detect_annotated(rgb)
+            else:
+                dets, drawn = self.engine.detect(rgb), None
         out = []
         with timer("draw_publish"):
-            for m, img, d in zip(images, rgb, dets):
-                if self.draw:
+            for j, (m, img, d) in enumerate(zip(images, rgb, dets)):
+                if drawn is not None:
+                    img = draw_detections(drawn[j], d, self.class_names, rects=False)
+                elif self.draw:
                     img = draw_detections(img.copy(), d, self.class_names)
                 im = compat.numpy_to_imgmsg(img, "rgb8", header=m.header)
                 out.append((im, detections_to_msg(d, m.header), d))

@@ -147,3 +147,35 @@ def _preprocess_s2d(frames, dst_hw, mode, scale, bias, swap_rb, pad_value, quant
            for b in range(B)]
     out.copy_(space_to_depth2(torch.from_numpy(np.stack(res))).to(out.dtype))
     return out, xf
+
+
+def draw_boxes_(frames: torch.Tensor, box: torch.Tensor, cls: torch.Tensor, count: torch.Tensor,
+                thickness: int = 2, stream=None) -> torch.Tensor:
+    """K15: draw result boxes onto uint8 frames in place (``csrc/kernels/draw.hip``).
+
+    frames [B, H, W, 3] uint8 (row-contiguous), box [B, K, D>=4] fp32 x1,y1,x2,y2
+    in frame pixels, cls [B, K] int32, count [B] int32.  Boxes 0..count-1 are
+    drawn in order (a later box wins where boxes overlap), pixel-identical to
+    :func:`triton_client_amd.utils.draw.draw_rect` with ``class_color``
+    (reference ``ros_inference.py:149-169``)."""
+    B, H, W, C = frames.shape
+    if C != 3 or frames.dtype != torch.uint8 or frames.stride(2) != 3 or frames.stride(1) != 3 * W:
+        raise ValueError("frames must be [B, H, W, 3] uint8 with contiguous rows")
+    if box.dim() != 3 or box.shape[0] != B or box.shape[2] < 4 or not box.is_contiguous():
+        raise ValueError("box must be contiguous [B, K, >=4]")
+    if tuple(cls.shape) != tuple(box.shape[:2]) or cls.dtype != torch.int32 or count.dtype != torch.int32:
+        raise ValueError("cls [B, K] int32 and count [B] int32")
+    if frames.is_cuda:
+        _native.call("tca_draw_boxes", _native.ptr(frames), frames.stride(0), B, H, W, frames.stride(1),
+                     _native.ptr(box), box.shape[1], box.shape[2], _native.ptr(cls.contiguous()),
+                     _native.ptr(count), thickness, _native.stream_ptr(stream))
+        return frames
+    from ..utils.draw import class_color, draw_rect
+
+    cnt = count.numpy()
+    for b in range(B):
+        img = frames[b].numpy()
+        for k in range(min(int(cnt[b]), box.shape[1])):
+            x = box[b, k].tolist()
+            draw_rect(img, x[0], x[1], x[2], x[3], class_color(int(cls[b, k])), thickness)
+    return frames

@@ -32,11 +32,12 @@ def draw_rect(img: np.ndarray, x1: float, y1: float, x2: float, y2: float, color
 
 
 def draw_detections(img: np.ndarray, dets: np.ndarray, names: Optional[Sequence[str]] = None,
-                    thickness: int = 2, labels: bool = True) -> np.ndarray:
+                    thickness: int = 2, labels: bool = True, rects: bool = True) -> np.ndarray:
     """img HxWx3 uint8 (modified in place and returned); dets [n, 6] x1,y1,x2,y2,conf,cls
-    in img pixels."""
+    in img pixels.  rects=False: only the labels (the rectangles were drawn on
+    the GPU by ``ops.image.draw_boxes_``)."""
     dets = np.asarray(dets).reshape(-1, 6)
-    for d in dets:
+    for d in dets if rects else ():
         draw_rect(img, d[0], d[1], d[2], d[3], class_color(int(d[5])), thickness)
     if labels and len(dets):
         try:
