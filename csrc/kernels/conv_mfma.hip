@@ -25,6 +25,8 @@
 // stores are 16-B vectors, coalesced along channels.
 #include "tca_common.h"
 
+#include <cstdlib>
+
 using namespace tca;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -470,6 +472,203 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_kernel(ConvArgs a) {
   epilogue<BM, BN, WM, WN>(a, acc, smem, m0, n0);
 }
 
+// ============================================================================
+// v3 "halo": 3x3 / stride 1 / pad 1, Cin = N = 64 (PointPillars BEV block 1,
+// CenterPoint RPN block 1: the layers v2 runs at ~0.5 PF/s).  There the
+// implicit GEMM re-reads every input pixel once per tap (9x the tensor
+// through L2 for a K of only 576), which is what bounds v2.  Here:
+//   * persistent workgroups, one per CU; all 9 taps x 64 x 64 of the weights
+//     (72 KiB) are staged into LDS once per workgroup;
+//   * the output tile is a 16 x 16 pixel block; its 18 x 18 x 64 input halo
+//     (41 KiB) is staged once and every tap's A fragments are read from it at
+//     (row + ky, col + kx): the input crosses L2 ~1.3x instead of 9x;
+//   * two halo buffers: tile i+1's halo DMAs run under tile i's MFMAs;
+//   * wave w owns output rows 4w..4w+3 (16 pixels each) x all 64 channels
+//     (64x64 per wave, 16 accumulators), so per 32-deep K sub-step a wave
+//     issues 8 ds_read_b128 for 16 MFMAs;
+//   * the epilogue stores bias+act straight from the accumulators (8 B per
+//     lane, 4 channels); those stores drain under the next tile's MFMAs.
+// LDS: 2 x 352 halo pixels x 128 B + 9 x 64 x 128 B = 163,840 B (all of it).
+// Measured (pp.b1.conv, B 16, 248 x 216): MFMAs + halo loads alone 67 us
+// (~940 TFLOP/s); with the epilogue 127-130 us, because one wave per SIMD
+// cannot overlap its LDS-staged stores with MFMAs (deferring the stores into
+// the next tile's K loop measured slower: in-order vmcnt then waits on them).
+// Bias values are held in registers: a per-tile global bias load exposed a
+// full memory round trip per tile (189 us).
+// Swizzle: 16-B slot ^= row & 7 for both images (swz_h).
+// ============================================================================
+constexpr int HT = 16;                       // output tile edge
+// 16-B slot swizzle of a 128-B row: slot ^= row & 7.  A ds_read_b128 lane group
+// reads 16 consecutive rows starting at ANY row (the halo taps shift by kx,
+// ky); row & 7 keeps all 16 on distinct (bank-row half, slot) pairs for every
+// start, where (row >> 1) & 7 is 2-way for unaligned starts.
+__device__ __forceinline__ int swz_h(int row) { return row & 7; }
+constexpr int HH = HT + 2;                   // halo edge
+constexpr int H_INS = 11;                    // halo glds per wave: 4 x 11 x 8 = 352 >= 18 x 18 pixels
+constexpr int H_BYTES = 4 * H_INS * 1024;    // 45,056
+constexpr int W_INS = 18;                    // weight glds per wave: 4 x 18 x 1 KiB = 72 KiB
+constexpr int W_BYTES = 4 * W_INS * 1024;    // 73,728
+
+__global__ void __launch_bounds__(256) conv_halo_kernel(ConvArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * H_BYTES + W_BYTES];
+  unsigned char* const wl = smem + 2 * H_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const int ntx = (a.Wo + HT - 1) / HT, nty = (a.Ho + HT - 1) / HT;
+
+  // weights once: slot s -> (tap, n, chunk'), source chunk = chunk' ^ swz_h(n)
+#pragma unroll
+  for (int j = 0; j < W_INS; ++j) {
+    const int r8 = wid * W_INS + j;          // 1-KiB piece = 8 rows (tap, n..n+7)
+    const int t = r8 >> 3, n = (r8 & 7) * 8 + lrow;
+    glds16(a.w + (long)n * a.Kp + t * 64 + (lslot ^ swz_h(n)) * 8, wl + r8 * 1024);
+  }
+
+  auto issue_halo = [&](int tile, unsigned char* hb) {
+    const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
+    const int iy0 = (rem / ntx) * HT - 1, ix0 = (rem % ntx) * HT - 1;
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j) {
+      const int r8 = wid * H_INS + j;
+      const int p = r8 * 8 + lrow;           // halo pixel of this lane
+      const int hy = p / HH, hx = p - hy * HH;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = p < HH * HH && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const void* g = ok ? (const void*)(a.in + (((long)b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off +
+                                         (lslot ^ swz_h(p)) * 8)
+                         : (const void*)g_conv_zero_page;
+      glds16(g, hb + r8 * 1024);
+    }
+  };
+
+  // workgroup w walks tiles [w*per, (w+1)*per): consecutive tiles are x-neighbours
+  // whose halos overlap (L2 hits); measured ~3% faster than a grid stride
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t_begin = blockIdx.x * per, t_end = min(ntiles, t_begin + per);
+  int tile = t_begin;
+  if (tile < t_end) issue_halo(tile, smem);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int act = a.act & 15;
+  // this lane's 16 bias values, loaded once: a global load in the per-tile
+  // epilogue would expose a full memory round trip per tile (measured 2.6x)
+  float bias_r[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias_r[j][r] = a.bias ? a.bias[j * 16 + fq * 4 + r] : 0.f;
+  for (int it = 0; tile < t_end; ++it, ++tile) {
+    unsigned char* hb = smem + (it & 1) * H_BYTES;
+    const int nxt = tile + 1;
+    if (nxt < t_end) issue_halo(nxt, smem + ((it + 1) & 1) * H_BYTES);
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - ky * 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + fq;
+        bf16x8 af[4], bfg[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = (wid * 4 + i + ky) * HH + fr + kx;
+          af[i] = *reinterpret_cast<const bf16x8*>(hb + p * 128 + ((c ^ swz_h(p)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = j * 16 + fr;
+          bfg[j] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + n) * 128 + ((c ^ swz_h(n)) << 4));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // the next tile's halo has landed (and every wave is done with this one)
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // epilogue, staged through this tile's (now free) halo buffer so the global
+    // stores are whole 128-B pixel lines (8 B per lane straight from the
+    // accumulators would write 32-B pieces of each line).
+    // lane (fr, fq) holds pixel fr of output row 4*wid + i, channels j*16 + fq*4 + 0..3
+    constexpr int LDE = 72;  // staged pixel stride in bf16 (+16 B: conflict-free 8-B writes)
+    __hip_bfloat16* st = reinterpret_cast<__hip_bfloat16*>(hb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ml = (wid * 4 + i) * HT + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = j * 16 + fq * 4;
+        __hip_bfloat16 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          q[r] = __float2bfloat16(act_fn(acc[i][j][r] + bias_r[j][r], act));
+        }
+        *reinterpret_cast<uint2*>(st + ml * LDE + n) = *reinterpret_cast<uint2*>(q);
+      }
+    }
+    // LDS-only barriers: __syncthreads() would also wait for vmcnt(0), i.e. for
+    // the global stores still in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
+    const int ty0 = (rem / ntx) * HT, tx0 = (rem % ntx) * HT;
+#pragma unroll
+    for (int k = 0; k < HT * HT * 8 / 256; ++k) {
+      const int id = tid + k * 256, ml = id >> 3, c8 = (id & 7) * 8;
+      const int oy = ty0 + (ml >> 4), ox = tx0 + (ml & 15);
+      if (oy < a.Ho && ox < a.Wo)
+        *reinterpret_cast<uint4*>(a.out + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + c8) =
+            *reinterpret_cast<const uint4*>(st + ml * LDE + c8);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done: the buffer receives
+    __builtin_amdgcn_s_barrier();                        // tile it+2's halo next
+    asm volatile("" ::: "memory");
+  }
+}
+
+int g_num_cus = 0;
+
+bool halo_ok(const ConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.S == 1 && a.P == 1 && a.Cin == 64 && a.N == 64 && a.Kp == 576 && !a.res &&
+         a.shuffle == 0 && a.Ho == a.H && a.Wo == a.W;
+}
+
+int launch_halo(const ConvArgs& a, hipStream_t stream) {
+  if (!halo_ok(a)) return (int)hipErrorInvalidValue;
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+      g_num_cus = 256;
+  }
+  const int ntiles = a.B * ((a.Ho + HT - 1) / HT) * ((a.Wo + HT - 1) / HT);
+  static const int grid_cap = [] {
+    const char* e = getenv("TCA_HALO_GRID");  // experiment hook: override the persistent grid size
+    return e ? atoi(e) : 0;
+  }();
+  const int cap = grid_cap > 0 ? grid_cap : g_num_cus;
+  const int grid = ntiles < cap ? ntiles : cap;
+  conv_halo_kernel<<<grid, 256, 0, stream>>>(a, ntiles);
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES = 2, bool ONEBAR = false>
 int launch_glds(const ConvArgs& a, hipStream_t stream) {
   static_assert(!ONEBAR || (STAGES >= 2 && STAGES <= 4), "one-barrier pipeline: 2..4 stages");
@@ -511,8 +710,12 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   // v2 (glds, 8 waves): 128x64 for N <= 64; 128x128 (4x2 waves) for wide-M layers,
   // 64x128 (2x4 waves) when M is small; v1 (register staging) when Cin % 64 != 0
   if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 64 ? 2 : 5);
+  // the persistent halo kernel (tile 50) is opt-in: 130 vs 137 us alone on
+  // pp.b1.conv, but it holds all of a CU's LDS, and inside the camera || LiDAR
+  // step it measured no gain (profiles/conv_tiles_r1.md)
   if (tile >= 10 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
+    case 50: return launch_halo(a, stream);  // 3x3 s1 Cin = N = 64, persistent + LDS halo
     case 11: return launch_glds<128, 64, 4, 1>(a, stream);
     case 12: return launch_glds<128, 128, 2, 2>(a, stream);
     case 13: return launch_glds<256, 64, 4, 1>(a, stream);

@@ -371,3 +371,29 @@ def test_fused_conv_glds_tiles(cuda, tile):
     torch.cuda.synchronize()
     ref = torch.relu(ct(x.to(torch.bfloat16).float().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
     assert (y.tensor().float().cpu() - ref).abs().max().item() < 0.05
+
+
+def test_fused_conv_halo_tile(cuda):
+    """v3 halo kernel (tile 50: 3x3 s1, Cin = N = 64, persistent, LDS-resident
+    weights + 18x18 input halo): partial edge tiles (H, W not multiples of 16),
+    input/output channel slices, more tiles than CUs and fewer, vs fp32."""
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(50)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=True)
+    fc = FusedConv(conv, act=1, device=cuda)
+    for B, H, W in ((2, 23, 31), (3, 16, 16), (16, 70, 54), (1, 5, 3)):
+        buf = torch.randn(B, H, W, 96).to(cuda, torch.bfloat16)
+        xin = NHWC(buf, 16, 64)  # channels [16, 80)
+        out = torch.zeros(B, H, W, 80, dtype=torch.bfloat16, device=cuda)
+        fc(xin, out=NHWC(out, 8, 64), tile=50)
+        torch.cuda.synchronize()
+        x32 = buf[..., 16:80].float().permute(0, 3, 1, 2).cpu()
+        ref = torch.relu(conv(x32))
+        got = out[..., 8:72].float().permute(0, 3, 1, 2).cpu()
+        err = (got - ref).abs().max().item()
+        assert err < 0.03 * max(1.0, ref.abs().max().item()), (B, H, W, err)
+        assert out[..., :8].abs().sum().item() == 0 and out[..., 72:].abs().sum().item() == 0
+    with pytest.raises(Exception):  # outside the contract (stride 2) is refused, not run
+        fc2 = FusedConv(nn.Conv2d(64, 64, 3, 2, 1), act=1, device=cuda)
+        fc2(NHWC(torch.randn(1, 8, 8, 64).to(cuda, torch.bfloat16)), tile=50)
