@@ -48,10 +48,17 @@ class DistInfo:
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> DistInfo:
+    """One process per GPU.  ``TCA_DIST_BACKEND=gloo`` (rehearsal only) runs the
+    GPU path with host-staged gloo transfers, so several ranks can share one
+    GPU (RCCL refuses two ranks on one device): it exercises every DP code path
+    of the bench and drivers except RCCL itself."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    backend = backend or os.environ.get("TCA_DIST_BACKEND") or None
     if torch.cuda.is_available():
+        if backend == "gloo":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -85,9 +92,22 @@ class FrameExchange:
         if self.native is not None:
             self.native.group_p2p(ops)
             return
+        staged = []
+        if dist.get_backend(self.group) == "gloo":  # gloo moves host tensors: stage device ones
+            host = []
+            for k, t, p in ops:
+                if t.is_cuda:
+                    h = t.cpu() if k == 0 else torch.empty(t.shape, dtype=t.dtype)
+                    if k == 1:
+                        staged.append((h, t))
+                    t = h
+                host.append((k, t, p))
+            ops = host
         p2p = [dist.P2POp(dist.isend if k == 0 else dist.irecv, t, p, self.group) for k, t, p in ops]
         for w in dist.batch_isend_irecv(p2p):
             w.wait()
+        for h, t in staged:
+            t.copy_(h)
 
     def scatter(self, src: Optional[Sequence[Sequence[torch.Tensor]]], dst: Sequence[torch.Tensor],
                 peers: Optional[Sequence[int]] = None) -> None:
@@ -138,7 +158,7 @@ class FrameExchange:
 
 def barrier(info: DistInfo) -> None:
     if info.world > 1:
-        if info.device.type == "cuda":
+        if info.device.type == "cuda" and dist.get_backend() != "gloo":
             dist.barrier(device_ids=[info.device.index])
         else:
             dist.barrier()
@@ -147,7 +167,8 @@ def barrier(info: DistInfo) -> None:
 def allreduce_max(info: DistInfo, value: float) -> float:
     if info.world == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=info.device)
+    dev = "cpu" if dist.get_backend() == "gloo" else info.device
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -264,20 +285,23 @@ class _DPBase:
         if self.info.world > 1 and self.info.is_main:
             self._send_header([_STOP], self._participants())
 
+    def _hdr_dev(self):
+        return "cpu" if dist.get_backend() == "gloo" else self.info.device
+
     def _send_header(self, vals, parts: Sequence[int]) -> List[int]:
         mask = 0
         for r in parts:
             mask |= 1 << r
         v = list(vals) + [0] * (_HDR - len(vals))
         v[_HDR - 1] = mask
-        t = torch.tensor(v, dtype=torch.int64, device=self.info.device)
+        t = torch.tensor(v, dtype=torch.int64, device=self._hdr_dev())
         for r in parts:
             if r != 0:
                 dist.send(t, r)
         return v
 
     def _recv_header(self) -> List[int]:
-        t = torch.zeros(_HDR, dtype=torch.int64, device=self.info.device)
+        t = torch.zeros(_HDR, dtype=torch.int64, device=self._hdr_dev())
         dist.recv(t, 0)
         return [int(x) for x in t.tolist()]
 
