@@ -25,8 +25,6 @@
 // stores are 16-B vectors, coalesced along channels.
 #include "tca_common.h"
 
-#include <cstdlib>
-
 using namespace tca;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -654,17 +652,12 @@ int launch_halo(const ConvArgs& a, hipStream_t stream) {
   if (!halo_ok(a)) return (int)hipErrorInvalidValue;
   if (g_num_cus == 0) {
     int dev = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
       g_num_cus = 256;
   }
   const int ntiles = a.B * ((a.Ho + HT - 1) / HT) * ((a.Wo + HT - 1) / HT);
-  static const int grid_cap = [] {
-    const char* e = getenv("TCA_HALO_GRID");  // experiment hook: override the persistent grid size
-    return e ? atoi(e) : 0;
-  }();
-  const int cap = grid_cap > 0 ? grid_cap : g_num_cus;
-  const int grid = ntiles < cap ? ntiles : cap;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
   conv_halo_kernel<<<grid, 256, 0, stream>>>(a, ntiles);
   return (int)hipGetLastError();
 }
