@@ -641,6 +641,155 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(ConvArgs a, int ntiles) 
   }
 }
 
+// ============================================================================
+// v4 "small halo": 3x3, pad 1, stride 1 or 2, Cin and N in {16, 32} (the
+// YOLOv5n stem / stage-1 / C3-bottleneck 3x3s).  At these widths the v1 tile
+// moves 32-64 B per pixel per tap through L2 in 16-B pieces, 9 taps over,
+// and runs 5-7x off the HBM roofline.  Here one 16x16 output tile per
+// workgroup: its input halo ((15*S+3)^2 pixels x Cin) is staged into LDS once
+// by global_load_lds, the packed weights (N x Kp, rows padded by 16 B so the
+// 16 rows of a ds_read_b128 lane group hit distinct banks) next to it, and
+// every K step's A fragments are read from the halo at the tap's offset.
+// K is packed across taps (Cin 16: one 32-deep MFMA step covers two taps).
+// Small LDS (11-46 KiB) keeps several workgroups per CU, so one tile's
+// stores overlap another's MFMAs.  Epilogue straight from the accumulators:
+// 4 lanes write a pixel's 16 channels as 32 contiguous bytes, with bias, act
+// and the Bottleneck residual as in v1/v2.
+// ============================================================================
+template <int CIN, int NOUT, int S>
+__global__ void __launch_bounds__(256) conv_small_halo_kernel(ConvArgs a) {
+  constexpr int TT = 16;
+  constexpr int HW_ = (TT - 1) * S + 3;            // halo edge
+  constexpr int NPX = HW_ * HW_;
+  constexpr int PB = CIN * 2, CPP = CIN / 8;       // bytes / 16-B chunks per halo pixel
+  constexpr int INS = (NPX * CPP + 255) / 256;     // halo glds per wave
+  constexpr int H_BYTES = INS * 4 * 1024;
+  constexpr int KP = (9 * CIN + 31) / 32 * 32, KS = KP / 32;
+  constexpr int WRS = KP * 2 + 16;                 // padded weight row (bytes)
+  constexpr int FN = NOUT / 16;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[H_BYTES + NOUT * WRS];
+  unsigned char* const wl = smem + H_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int ntx = (a.Wo + TT - 1) / TT, nty = (a.Ho + TT - 1) / TT;
+  const int tile = blockIdx.x;
+  const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
+  const int ty0 = (rem / ntx) * TT, tx0 = (rem % ntx) * TT;
+  const int iy0 = ty0 * S - 1, ix0 = tx0 * S - 1;
+
+  // halo: lane-linear 16-B chunks, chunk g = (pixel g / CPP, part g % CPP)
+#pragma unroll
+  for (int j = 0; j < INS; ++j) {
+    const int g = (wid * INS + j) * 64 + lane;
+    const int p = g / CPP, c = g - p * CPP;
+    const int hy = p / HW_, hx = p - hy * HW_;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = p < NPX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    const void* src = ok ? (const void*)(a.in + (((long)b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + c * 8)
+                         : (const void*)g_conv_zero_page;
+    glds16(src, smem + (wid * INS + j) * 1024);
+  }
+  // weights: plain 16-B loads into the padded rows
+  for (int g = tid; g < NOUT * KP / 8; g += 256) {
+    const int n = g / (KP / 8), c = g - n * (KP / 8);
+    *reinterpret_cast<uint4*>(wl + n * WRS + c * 16) = *reinterpret_cast<const uint4*>(a.w + (long)n * a.Kp + c * 8);
+  }
+  float bias_r[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias_r[j][r] = a.bias ? a.bias[j * 16 + fq * 4 + r] : 0.f;
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  f32x4 acc[4][FN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = s * 32 + fq * 8;                  // this lane's 8-deep K chunk
+    const int tap = k0 / CIN, ci0 = k0 - tap * CIN;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    bf16x8 af[4], bfg[FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = ((wid * 4 + i) * S + ky) * HW_ + fr * S + kx;
+      af[i] = tap < 9 ? *reinterpret_cast<const bf16x8*>(smem + p * PB + ci0 * 2) : bf16x8{};
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfg[j] = *reinterpret_cast<const bf16x8*>(wl + (j * 16 + fr) * WRS + k0 * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+  }
+
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res != nullptr;
+  const int ox = tx0 + fr;
+  if (ox >= a.Wo) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = ty0 + wid * 4 + i;
+    if (oy >= a.Ho) break;
+    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = j * 16 + fq * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias_r[j][r];
+      if (a.res) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(a.res + pix * a.ldr + a.r_off + n);
+        const __hip_bfloat16* rv = reinterpret_cast<const __hip_bfloat16*>(&rr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = post_res ? act_fn(v[r] + __bfloat162float(rv[r]), act)
+                          : __bfloat162float(__float2bfloat16(act_fn(v[r], act))) + __bfloat162float(rv[r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      }
+      __hip_bfloat16 q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[r] = __float2bfloat16(v[r]);
+      *reinterpret_cast<uint2*>(a.out + pix * a.ldo + a.co_off + n) = *reinterpret_cast<uint2*>(q);
+    }
+  }
+}
+
+bool small_halo_ok(const ConvArgs& a) {
+  const bool cin = a.Cin == 16 || a.Cin == 32, n = a.N == 16 || a.N == 32;
+  return cin && n && a.KH == 3 && a.KW == 3 && a.P == 1 && (a.S == 1 || a.S == 2) && a.shuffle == 0 &&
+         a.Kp == (9 * a.Cin + 31) / 32 * 32 && a.Ho == (a.H - 1) / a.S + 1 && a.Wo == (a.W - 1) / a.S + 1;
+}
+
+template <int CIN, int NOUT, int S>
+int launch_small_halo_t(const ConvArgs& a, hipStream_t stream) {
+  const int ntiles = a.B * ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16);
+  conv_small_halo_kernel<CIN, NOUT, S><<<ntiles, 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+int launch_small_halo(const ConvArgs& a, hipStream_t stream) {
+  if (!small_halo_ok(a)) return (int)hipErrorInvalidValue;
+  const int key = (a.Cin == 32) * 4 + (a.N == 32) * 2 + (a.S == 2);
+  switch (key) {
+    case 0: return launch_small_halo_t<16, 16, 1>(a, stream);
+    case 1: return launch_small_halo_t<16, 16, 2>(a, stream);
+    case 2: return launch_small_halo_t<16, 32, 1>(a, stream);
+    case 3: return launch_small_halo_t<16, 32, 2>(a, stream);
+    case 4: return launch_small_halo_t<32, 16, 1>(a, stream);
+    case 5: return launch_small_halo_t<32, 16, 2>(a, stream);
+    case 6: return launch_small_halo_t<32, 32, 1>(a, stream);
+    default: return launch_small_halo_t<32, 32, 2>(a, stream);
+  }
+}
+
 int g_num_cus = 0;
 
 bool halo_ok(const ConvArgs& a) {
@@ -702,13 +851,17 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   // auto tile (measured on MI355X, tools/bench_conv.py -> profiles/conv_tiles_r1.md):
   // v2 (glds, 8 waves): 128x64 for N <= 64; 128x128 (4x2 waves) for wide-M layers,
   // 64x128 (2x4 waves) when M is small; v1 (register staging) when Cin % 64 != 0
+  // v4 small-halo for 3x3 Cin, N in {16, 32} (tools/bench_conv.py: YOLOv5n stem 90 -> 35 us,
+  // C3 3x3 30 -> 13 us, stage-1 downsample 39 -> 33 us)
+  if (tile == 0 && small_halo_ok(a)) tile = 60;
   if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 64 ? 2 : 5);
   // the persistent halo kernel (tile 50) is opt-in: 130 vs 137 us alone on
   // pp.b1.conv, but it holds all of a CU's LDS, and inside the camera || LiDAR
   // step it measured no gain (profiles/conv_tiles_r1.md)
-  if (tile >= 10 && !v2ok) return (int)hipErrorInvalidValue;
+  if (tile >= 10 && tile < 60 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 50: return launch_halo(a, stream);  // 3x3 s1 Cin = N = 64, persistent + LDS halo
+    case 60: return launch_small_halo(a, stream);  // 3x3 s1/s2, Cin, N in {16, 32}, LDS halo
     case 11: return launch_glds<128, 64, 4, 1>(a, stream);
     case 12: return launch_glds<128, 128, 2, 2>(a, stream);
     case 13: return launch_glds<256, 64, 4, 1>(a, stream);

@@ -397,3 +397,31 @@ def test_fused_conv_halo_tile(cuda):
     with pytest.raises(Exception):  # outside the contract (stride 2) is refused, not run
         fc2 = FusedConv(nn.Conv2d(64, 64, 3, 2, 1), act=1, device=cuda)
         fc2(NHWC(torch.randn(1, 8, 8, 64).to(cuda, torch.bfloat16)), tile=50)
+
+
+@pytest.mark.parametrize("cin,cout,s", [(16, 16, 1), (16, 32, 2), (32, 32, 1), (16, 32, 1), (32, 16, 2), (16, 16, 2)])
+def test_fused_conv_small_halo(cuda, cin, cout, s):
+    """v4 small-halo kernel (tile 60: 3x3, Cin, N in {16, 32}, stride 1/2): edge
+    tiles, channel slices, SiLU, the Bottleneck residual (both orders) vs fp32."""
+    import torch.nn as nn
+    from triton_client_amd.ops.conv import NHWC, FusedConv
+    torch.manual_seed(60 + cin + cout + s)
+    conv = nn.Conv2d(cin, cout, 3, s, 1, bias=True)
+    for B, H, W in ((2, 23, 31), (1, 40, 17)):
+        for post in (False, True):
+            fc = FusedConv(conv, act=2, device=cuda, post_res=post)
+            buf = torch.randn(B, H, W, cin + 16).to(cuda, torch.bfloat16)
+            xin = NHWC(buf, 8, cin)  # channels [8, 8+cin)
+            Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+            res = torch.randn(B, Ho, Wo, cout + 8).to(cuda, torch.bfloat16)
+            out = torch.zeros(B, Ho, Wo, cout + 16, dtype=torch.bfloat16, device=cuda)
+            fc(xin, out=NHWC(out, 8, cout), res=NHWC(res, 8, cout), tile=60)
+            torch.cuda.synchronize()
+            x32 = buf[..., 8:8 + cin].float().permute(0, 3, 1, 2).cpu()
+            r32 = res[..., 8:8 + cout].float().permute(0, 3, 1, 2).cpu()
+            y = conv(x32)
+            ref = torch.nn.functional.silu(y + r32) if post else torch.nn.functional.silu(y) + r32
+            got = out[..., 8:8 + cout].float().permute(0, 3, 1, 2).cpu()
+            err = (got - ref).abs().max().item()
+            assert err < 0.03 * max(1.0, ref.abs().max().item()), (B, H, W, post, err)
+            assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
