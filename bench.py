@@ -46,8 +46,8 @@ REFERENCE_EQUIVALENT_FPS = 3.2319
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=16, help="frames per GPU per step")
     ap.add_argument("--cam", default="720x1280", help="camera HxW")
     ap.add_argument("--rings", type=int, default=64)
