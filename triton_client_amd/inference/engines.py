@@ -40,6 +40,7 @@ import torch
 from ..ops.image import frame_xform, preprocess
 from ..ros import msgs
 from ..utils.trace import trace_range
+from ..utils.model_store import load_state_dict
 
 
 def _device(device) -> torch.device:
@@ -90,7 +91,7 @@ class LocalDetector2D(Detector2D):
         self.graph = graph and self.device.type == "cuda"
         self.model = build_yolov5(variant, nc, self.img, seed)
         if weights:
-            self.model.load_state_dict(torch.load(weights, map_location="cpu", weights_only=True))
+            self.model.load_state_dict(load_state_dict(weights))
             calibrate_target = None
         self.calibrate_target = calibrate_target
         self.names = list(names) if names is not None else [str(i) for i in range(nc)]
@@ -212,7 +213,7 @@ class LocalDetector3D(Detector3D):
         self.z_offset = self.Z_OFFSET[family] if z_offset is None else z_offset
         self.graph = graph and self.device.type == "cuda"
         if weights:
-            self.model.load_state_dict(torch.load(weights, map_location="cpu", weights_only=True))
+            self.model.load_state_dict(load_state_dict(weights))
             calibrate_target = None
         self.calibrate_target = self.FAMILIES[family] if calibrate_target == "auto" else calibrate_target
         self.max_points = max_points

@@ -14,8 +14,19 @@ def main(argv=None):
     ap.add_argument("--metrics-port", type=int, default=8002)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--export-repository", default=None, metavar="DIR",
+                    help="write a Triton-layout repository for --models into DIR and exit")
+    ap.add_argument("--weights", action="append", default=[], metavar="MODEL=URI",
+                    help="with --export-repository: weights for MODEL (path, file/http(s)/s3 URI); repeatable")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    if args.export_repository:
+        from .repository import export_repository
+
+        w = dict(kv.split("=", 1) for kv in args.weights)
+        for d in export_repository(filter(None, (m.strip() for m in args.models.split(","))), args.export_repository, w):
+            print(d)
+        return
     if args.model_repository:
         repo = ModelRepository.from_directory(args.model_repository, args.device)
     else:

@@ -102,6 +102,21 @@ def register_factory(name: str, factory: Factory) -> None:
     FACTORIES[name] = factory
 
 
+def _weights_for(model_dir: str, cfg) -> Optional[str]:
+    """Weights of one repository entry: ``parameters { key: "weights" }`` (path or
+    file/http(s)/s3 URI, see ``utils/model_store.py``), else the highest numeric
+    version directory holding ``model.pt`` (Triton's ``<model>/<version>/`` layout)."""
+    if "weights" in cfg.parameters and cfg.parameters["weights"].string_value:
+        w = cfg.parameters["weights"].string_value
+        return w if "://" in w or os.path.isabs(w) else os.path.join(model_dir, w)
+    versions = sorted((int(v) for v in os.listdir(model_dir) if v.isdigit()), reverse=True)
+    for v in versions:
+        f = os.path.join(model_dir, str(v), "model.pt")
+        if os.path.isfile(f):
+            return f
+    return None
+
+
 class ModelRepository:
     def __init__(self, device="auto"):
         self.device = device
@@ -196,5 +211,41 @@ class ModelRepository:
                 m = SecondIoUModel(name, device=device)
             else:
                 continue
+            weights = _weights_for(os.path.join(path, entry), cfg)
+            if weights and hasattr(m, "weights"):
+                m.weights = weights
             repo.add(m, load=load)
         return repo
+
+
+def export_repository(names: Iterable[str], out_dir: str, weights: Optional[Dict[str, str]] = None) -> List[str]:
+    """Write a Triton-layout model repository (``<name>/config.pbtxt`` plus
+    ``<name>/1/model.pt`` when weights are given) for the named served models.
+
+    This is the deploy step of the reference's ``deploy.sh:1-65`` (export the
+    model, write its ``config.pbtxt`` into the server's repository), minus the
+    ONNX export: the server here runs the native MI355X pipelines, so the
+    repository holds the KServe contract and, optionally, a state_dict.
+    ``from_directory`` reads it back."""
+    import shutil
+
+    from google.protobuf import text_format
+
+    written = []
+    for name in names:
+        if name not in FACTORIES:
+            raise KeyError(f"no factory for model '{name}'")
+        m = FACTORIES[name](device="cpu")
+        d = os.path.join(out_dir, name)
+        os.makedirs(os.path.join(d, "1"), exist_ok=True)
+        with open(os.path.join(d, "config.pbtxt"), "w") as f:
+            f.write(text_format.MessageToString(m.config()))
+        w = (weights or {}).get(name)
+        if w:
+            if "://" in w:  # remote: reference it, the server fetches it at load time
+                with open(os.path.join(d, "config.pbtxt"), "a") as f:
+                    f.write(f'parameters {{\n  key: "weights"\n  value {{\n    string_value: "{w}"\n  }}\n}}\n')
+            else:
+                shutil.copyfile(w, os.path.join(d, "1", "model.pt"))
+        written.append(d)
+    return written
