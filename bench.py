@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint", "second_iou"], default="pointpillars",
                     help="3D detector: PointPillars KITTI (headline), CenterPoint-PP nuScenes or SECOND-IoU KITTI "
                          "(sparse 3D conv backbone + RoI head)")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32 (default): the reference's serving precision — fp32 activations, split-product "
+                         "MFMA convs; bf16: bf16 activations (secondary, labelled)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--target-2d", type=float, default=100.0, help="candidates/frame reaching 2D NMS (calibration)")
     ap.add_argument("--target-3d", type=float, default=2000.0, help="anchors/frame reaching 3D NMS (calibration)")
@@ -115,7 +118,7 @@ def main():
                                      device=dev)
     else:
         def make_cam(b, m):
-            return CameraPipeline(model=m, batch=b, src_hw=(H0, W0), device=dev)
+            return CameraPipeline(model=m, batch=b, src_hw=(H0, W0), device=dev, precision=args.precision)
     sec = args.lidar_model == "second_iou"
     if use_lid and cp:
         from triton_client_amd.pipelines import CenterPointPipeline
@@ -129,7 +132,8 @@ def main():
             return SecondPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5)
     else:
         def make_lid(b, m):
-            return LidarPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5)
+            return LidarPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5,
+                                 precision=args.precision)
     if S > 1:
         from triton_client_amd.pipelines.multistream import SubBatched
         cam = SubBatched(make_cam, B, S) if use_cam else None
@@ -394,7 +398,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(fps / REFERENCE_EQUIVALENT_FPS, 2) if REFERENCE_EQUIVALENT_FPS else None),
-            "dtype": "bf16",
+            "dtype": args.precision if (args.camera_model == "yolov5n" and args.lidar_model == "pointpillars")
+            else "bf16",
             "data": (f"synthetic: {W0}x{H0} uint8 RGB camera frames + {spec.rings}x{spec.azimuth_steps} LiDAR sweeps "
                      f"(PointCloud2 16 B/pt, ~2% NaN dropouts); random-init weights (He-normal + LSUV rescaling on "
                      f"sample frames), detection-head bias offset calibrated so ~{args.target_2d:g} 2D / ~{args.target_3d:g} 3D candidates per frame reach NMS"),

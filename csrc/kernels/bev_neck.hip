@@ -90,14 +90,14 @@ struct Tile {
   int b, cy, cx, q0;
 };
 
-__device__ __forceinline__ Tile tile_of(const NeckArgs& a, int t, int nqt) {
-  const int ncls = a.S * a.S;
+__device__ __forceinline__ Tile tile_of(int S, int t, int nqt, int bm = BM) {
+  const int ncls = S * S;
   const int cls = t % ncls, rest = t / ncls;
   Tile r;
   r.b = rest / nqt;
-  r.q0 = (rest - r.b * nqt) * BM;
-  r.cy = cls / a.S;
-  r.cx = cls - r.cy * a.S;
+  r.q0 = (rest - r.b * nqt) * bm;
+  r.cy = cls / S;
+  r.cx = cls - r.cy * S;
   return r;
 }
 
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
 
   // flat step g -> (tile, branch, chunk); the issue side walks it incrementally
   int i_k = 0, i_br = 0, i_kc = 0;
-  Tile it = tile_of(a, t_lo + slot, nqt);
+  Tile it = tile_of(a.S, t_lo + slot, nqt);
   auto issue = [&](int buf) {
     unsigned char* sa = smem + buf * STAGE;
     unsigned char* sb = sa + A_BYTES;
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
       if (++i_br == a.nbr) {
         i_br = 0;
         ++i_k;
-        it = tile_of(a, t_lo + slot + i_k * nslot, nqt);
+        it = tile_of(a.S, t_lo + slot + i_k * nslot, nqt);
       }
     }
   };
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
 
   if (total > 0) issue(0);
   int c_k = 0, c_br = 0, c_kc = 0;  // compute side
-  Tile ct = tile_of(a, t_lo + slot, nqt);
+  Tile ct = tile_of(a.S, t_lo + slot, nqt);
   for (int g = 0; g < total; ++g) {
     const int cur = g & 1;
     wait_vmcnt0();
@@ -281,9 +281,265 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
       }
     }
     ++c_k;
-    ct = tile_of(a, t_lo + slot + c_k * nslot, nqt);
+    ct = tile_of(a.S, t_lo + slot + c_k * nslot, nqt);
   }
   wait_vmcnt0();  // no LDS DMA may outlive the workgroup (a tile-less workgroup still loaded the head)
+}
+
+// ============================================================================
+// fp32 mode ("x3", see conv_mfma.hip): fp32 branch inputs and output, split
+// weights (deconv [s*s*CB, cin/8, {hi 8, lo 8}], head [NH, nbr*CB/8, {hi, lo}]
+// with the same 32-chunk permutation), three MFMAs per fragment pair.  The
+// split head weights (2 x 60 KiB) do not fit in LDS next to the fp32
+// staging, so they are streamed through the ring instead: each branch's
+// flat step sequence is its cin/32 deconv K steps followed by 4 head steps
+// whose B slot carries the 80 x 32 split head weights of one 32-channel chunk
+// of that branch (A slot unused); the head GEMM consumes the branch's ReLU'd
+// accumulators chunk by chunk (split to hi/lo in registers).
+// LDS rows are 128 B; slot swizzle s ^ ((r ^ (r >> 3)) & 7) (conv_mfma.hip swz3).
+// ============================================================================
+constexpr int X_BM = 128;                         // pixels per tile: 16 per wave (register budget)
+constexpr int X_FM = X_BM / (16 * NW);            // 16-pixel fragments per wave
+constexpr int X_ROWB = 128;                       // 32 fp32 channels / 4 x {hi 8, lo 8}
+constexpr int X_A_BYTES = X_BM * X_ROWB;          // 16 KiB
+constexpr int X_B_BYTES = CB * X_ROWB;            // 16 KiB (head steps use 80 rows of it)
+constexpr int X_STAGE = X_A_BYTES + X_B_BYTES + BIAS_BYTES;
+constexpr int X_BH_OFF = 2 * X_STAGE;
+constexpr int X_LDS_BYTES = X_BH_OFF + NH * 4;
+constexpr int X_A_INS = X_BM / (8 * NW), X_B_INS = CB / (8 * NW);
+
+__device__ __forceinline__ int swz3(int row) { return (row ^ (row >> 3)) & 7; }
+
+__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8& hi, bf16x8& lo) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    hi[e] = h;
+    lo[e] = (__bf16)(v[e] - (float)h);
+  }
+}
+
+__device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
+                                      const bf16x8& al) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+}
+
+struct NeckArgsX3 {
+  const float* x[MAXBR];
+  int ldx[MAXBR], offx[MAXBR], cin[MAXBR], s[MAXBR];
+  const __hip_bfloat16* w[MAXBR];  // split [s*s*CB, 2*cin]
+  const float* bias[MAXBR];
+  const __hip_bfloat16* wh;        // split [NH, 2*nbr*CB], 32-chunk permuted
+  const float* bh;
+  float* out;
+  int ldo, nh;
+  int B, H, W, S, nbr, nsteps, ntiles;
+};
+
+__global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[X_LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, lslot = lane & 7;
+
+  const int S = a.S;
+  const int Wq = a.W / S, nq = (a.H / S) * Wq;
+  const int nqt = (nq + X_BM - 1) / X_BM;
+  const int G = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = G >> 3;
+  const int t_lo = (int)((long)a.ntiles * xcd / 8), t_hi = (int)((long)a.ntiles * (xcd + 1) / 8);
+  const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + nslot - 1) / nslot : 0;
+  const int total = my_tiles * a.nsteps;
+  const int ldwh = 2 * a.nbr * CB;  // bf16 per split head-weight row
+
+  if (wid == 0 && lane < NH / 4) glds16(a.bh + lane * 4, smem + X_BH_OFF);
+
+  // issue side: (tile, branch, chunk) with chunk < cin/32 a deconv step, else head step chunk - cin/32
+  int i_k = 0, i_br = 0, i_kc = 0;
+  Tile it = tile_of(a.S, t_lo + slot, nqt, X_BM);
+  auto issue = [&](int buf) {
+    unsigned char* sa = smem + buf * X_STAGE;
+    unsigned char* sb = sa + X_A_BYTES;
+    unsigned char* sbias = sb + X_B_BYTES;
+    const int nkc = a.cin[i_br] / 32;
+    if (i_kc < nkc) {
+      const int s = a.s[i_br], f = S / s;
+      const int Hi = a.H / s, Wi = a.W / s;
+      const int sy = it.cy / s, sx = it.cx / s;
+      const int ci0 = i_kc * 32;
+      const float* xb = a.x[i_br] + a.offx[i_br] + ci0;
+      const int ldx = a.ldx[i_br];
+#pragma unroll
+      for (int j = 0; j < X_A_INS; ++j) {
+        const int row = (wid * X_A_INS + j) * 8 + lrow;
+        const int q = it.q0 + row;
+        const void* g = g_neck_zero_page;
+        if (q < nq) {
+          const int Y = q / Wq, X = q - Y * Wq;
+          g = xb + (((long)it.b * Hi + Y * f + sy) * Wi + X * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
+        }
+        glds16(g, sa + (wid * X_A_INS + j) * 1024);
+      }
+      const int sub = (it.cy % s) * s + (it.cx % s);
+      const int cin2 = 2 * a.cin[i_br];
+      const __hip_bfloat16* wb = a.w[i_br] + (long)sub * CB * cin2 + ci0 * 2;
+#pragma unroll
+      for (int j = 0; j < X_B_INS; ++j) {
+        const int row = (wid * X_B_INS + j) * 8 + lrow;
+        glds16(wb + (long)row * cin2 + (lslot ^ swz3(row)) * 8, sb + (wid * X_B_INS + j) * 1024);
+      }
+      if (lane < 4) glds16(a.bias[i_br] + sub * CB + wid * 16 + lane * 4, sbias + wid * 64);
+    } else {
+      // head step t: rows h < 80 of the split head weights, channels [br*CB + 32t, +32)
+      const int t = i_kc - nkc;
+      const __hip_bfloat16* whb = a.wh + (i_br * CB + 32 * t) * 2;
+      for (int r8 = wid; r8 < NH / 8; r8 += NW) {
+        const int h = r8 * 8 + lrow;
+        glds16(whb + (long)h * ldwh + (lslot ^ swz3(h)) * 8, sb + r8 * 1024);
+      }
+    }
+    if (++i_kc == nkc + 4) {
+      i_kc = 0;
+      if (++i_br == a.nbr) {
+        i_br = 0;
+        ++i_k;
+        it = tile_of(a.S, t_lo + slot + i_k * nslot, nqt, X_BM);
+      }
+    }
+  };
+
+  f32x4 acc1[X_FM][8], acc2[X_FM][NH / 16];
+#pragma unroll
+  for (int i = 0; i < X_FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  if (total > 0) issue(0);
+  int c_k = 0, c_br = 0, c_kc = 0;
+  Tile ct = tile_of(a.S, t_lo + slot, nqt, X_BM);
+  for (int g = 0; g < total; ++g) {
+    const int cur = g & 1;
+    wait_vmcnt0();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (g + 1 < total) issue(cur ^ 1);
+
+    const unsigned char* sa = smem + cur * X_STAGE;
+    const unsigned char* sb = sa + X_A_BYTES;
+    const int nkc = a.cin[c_br] / 32;
+    if (c_kc < nkc) {
+      // ---- deconv K step: 2 x 8 fragment pairs, three MFMAs each
+      bf16x8 ah[X_FM], al[X_FM];
+#pragma unroll
+      for (int i = 0; i < X_FM; ++i) {
+        const int r = wid * 16 * X_FM + i * 16 + fr;
+        const float4 x0 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+        const float4 x1 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+        split8(x0, x1, ah[i], al[i]);
+      }
+      __builtin_amdgcn_s_setprio(1);
+      // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the
+      // VGPRs) to half the tile; the scheduler may not move reads across the barrier
+#pragma unroll
+      for (int jh = 0; jh < 2; ++jh) {
+        bf16x8 wh_[4], wl_[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = (jh * 4 + jj) * 16 + fr;
+          wh_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+          wl_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int i = 0; i < X_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (c_kc == nkc - 1) {  // branch GEMM done: bias + ReLU (this stage carries the biases)
+        const float* bias = reinterpret_cast<const float*>(sb + X_B_BYTES);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
+#pragma unroll
+          for (int i = 0; i < X_FM; ++i) {
+            acc1[i][j][0] = fmaxf(acc1[i][j][0] + bv.x, 0.f);
+            acc1[i][j][1] = fmaxf(acc1[i][j][1] + bv.y, 0.f);
+            acc1[i][j][2] = fmaxf(acc1[i][j][2] + bv.z, 0.f);
+            acc1[i][j][3] = fmaxf(acc1[i][j][3] + bv.w, 0.f);
+          }
+        }
+      }
+      ++c_kc;
+      continue;
+    }
+    // ---- head step t: 32 of the branch's channels (acc1[.][2t], acc1[.][2t+1]) x 80 head rows
+    const int t = c_kc - nkc;
+    bf16x8 xh[X_FM], xl[X_FM];
+    auto take = [&](int q) {
+#pragma unroll
+      for (int i = 0; i < X_FM; ++i) {
+        const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];
+        split8(make_float4(p0[0], p0[1], p0[2], p0[3]), make_float4(p1[0], p1[1], p1[2], p1[3]), xh[i], xl[i]);
+      }
+    };
+    switch (t) {  // static register indices per case (a runtime index would put acc1 in scratch)
+      case 0: take(0); break;
+      case 1: take(1); break;
+      case 2: take(2); break;
+      default: take(3); break;
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int u = 0; u < NH / 16; ++u) {
+      const int h = u * 16 + fr;
+      const bf16x8 wh_ = *reinterpret_cast<const bf16x8*>(sb + h * X_ROWB + (((2 * fq) ^ swz3(h)) << 4));
+      const bf16x8 wl_ = *reinterpret_cast<const bf16x8*>(sb + h * X_ROWB + (((2 * fq + 1) ^ swz3(h)) << 4));
+#pragma unroll
+      for (int i = 0; i < X_FM; ++i) mfma3(acc2[i][u], wh_, wl_, xh[i], xl[i]);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (++c_kc != nkc + 4) continue;
+    c_kc = 0;
+#pragma unroll
+    for (int i = 0; i < X_FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (++c_br != a.nbr) continue;
+    c_br = 0;
+    {
+      const float* bh = reinterpret_cast<const float*>(smem + X_BH_OFF);
+#pragma unroll
+      for (int i = 0; i < X_FM; ++i) {
+        const int q = ct.q0 + wid * 16 * X_FM + i * 16 + fr;
+        if (q < nq) {
+          const int Y = q / Wq, X = q - Y * Wq;
+          float* op = a.out + (((long)ct.b * a.H + Y * S + ct.cy) * a.W + X * S + ct.cx) * a.ldo;
+#pragma unroll
+          for (int u = 0; u < NH / 16; ++u) {
+            const int h = u * 16 + fq * 4;
+            if (h < a.nh) {
+              const float4 bv = *reinterpret_cast<const float4*>(bh + h);
+              *reinterpret_cast<float4*>(op + h) = make_float4(acc2[i][u][0] + bv.x, acc2[i][u][1] + bv.y,
+                                                               acc2[i][u][2] + bv.z, acc2[i][u][3] + bv.w);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    ++c_k;
+    ct = tile_of(a.S, t_lo + slot + c_k * nslot, nqt, X_BM);
+  }
+  wait_vmcnt0();
 }
 
 }  // namespace
@@ -321,5 +577,38 @@ TCA_API int tca_bev_neck_head(int nbr, const void* const* x, const int* ldx, con
   const int nq = (H / S) * (W / S);
   a.ntiles = B * ((nq + BM - 1) / BM) * S * S;
   bev_neck_head_kernel<<<grid, NT, 0, stream>>>(a);
+  TCA_LAUNCH_CHECK();
+}
+
+// fp32 mode: x[i] fp32, w[i] split [s_i*s_i*128, 2*cin[i]] bf16, wh split [80, 2*nbr*128]
+// (32-chunk permuted, then split), out fp32 [B, H, W, ldo].  Other arguments as tca_bev_neck_head.
+TCA_API int tca_bev_neck_head_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
+                                 const int* s, const void* const* w, const float* const* bias, const void* wh,
+                                 const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
+                                 hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
+    return (int)hipErrorInvalidValue;
+  NeckArgsX3 a;
+  int S = 1, nsteps = 0;
+  for (int i = 0; i < nbr; ++i) {
+    if (s[i] < 1 || (cin[i] & 31) || (ldx[i] & 3) || (offx[i] & 3)) return (int)hipErrorInvalidValue;
+    S = s[i] > S ? s[i] : S;
+  }
+  for (int i = 0; i < nbr; ++i) {
+    if (S % s[i]) return (int)hipErrorInvalidValue;
+    a.x[i] = (const float*)x[i]; a.ldx[i] = ldx[i]; a.offx[i] = offx[i]; a.cin[i] = cin[i]; a.s[i] = s[i];
+    a.w[i] = (const __hip_bfloat16*)w[i]; a.bias[i] = bias[i];
+    nsteps += cin[i] / 32 + 4;
+  }
+  for (int i = nbr; i < MAXBR; ++i) {
+    a.x[i] = nullptr; a.ldx[i] = a.offx[i] = a.cin[i] = 0; a.s[i] = 1; a.w[i] = nullptr; a.bias[i] = nullptr;
+  }
+  if ((H % S) || (W % S)) return (int)hipErrorInvalidValue;
+  a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.out = (float*)out; a.ldo = ldo; a.nh = nh;
+  a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
+  const int nq = (H / S) * (W / S);
+  a.ntiles = B * ((nq + X_BM - 1) / X_BM) * S * S;
+  bev_neck_head_x3_kernel<<<grid, NT, 0, stream>>>(a);
   TCA_LAUNCH_CHECK();
 }

@@ -48,6 +48,11 @@ struct ConvArgs {
   int act;          // 0 none, 1 relu, 2 silu, 3 leaky(0.1), 4 mish; | 16: act after the residual add
   int shuffle;      // >0: transpose-conv pixel shuffle factor s (N = s*s*Cout_real)
   int M;            // B*Ho*Wo
+  // fp32 mode (tca_conv_nhwc_x3): activations are fp32 and `w` is the split
+  // weight [N, Kp/8, {hi[8], lo[8]}] (row stride 2*Kp bf16); in/res/out above are unused
+  const float* in_f;
+  const float* res_f;
+  float* out_f;
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -826,6 +831,541 @@ int launch(const ConvArgs& a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// ============================================================================
+// fp32 mode ("x3"): fp32 activations, fp32-accurate products on the bf16 MFMA.
+//
+// The reference serves fp32 models (examples/YOLOv5/config.pbtxt:7,16,
+// examples/pointpillar_kitti/config.pbtxt:33,54).  gfx950 has no xf32 and its
+// f32-input MFMA runs at 1/16 of the bf16 rate, so every product is split:
+//   x = xh + xl,  xh = bf16_rne(x),  xl = bf16_rne(x - xh)   (|x - xh - xl| <= 2^-17 |x|)
+//   x * w ~= xh*wh + xh*wl + xl*wh                        (dropped xl*wl <= 2^-16 |x w|)
+// three mfma_f32_16x16x32_bf16 per fragment pair with fp32 accumulation:
+// ~16 significant bits per product, 3x the bf16 MFMA work (vs 16x for f32 MFMA).
+// Weights are split once on the host into [N][Kp/8][hi 8 | lo 8] (one 32-B
+// row chunk per 8 channels); activations stay fp32 in HBM and are split in
+// registers — at LDS staging (v1, small halo) or at the fragment read (v2,
+// whose operands go global -> LDS by DMA).  Epilogues compute in fp32 and
+// store fp32, residuals are fp32.
+// ============================================================================
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8& hi, bf16x8& lo) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    hi[e] = h;
+    lo[e] = (__bf16)(v[e] - (float)h);
+  }
+}
+
+__device__ __forceinline__ void split4(const float4& x, uint2& hi, uint2& lo) {
+  const float v[4] = {x.x, x.y, x.z, x.w};
+  __bf16 h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  hi = *reinterpret_cast<const uint2*>(h);
+  lo = *reinterpret_cast<const uint2*>(l);
+}
+
+__device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
+                                      const bf16x8& al) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+}
+
+// fp32 epilogue: bias/act into an fp32 LDS tile, then 16-B (4-channel) coalesced
+// stores with residual and pixel-shuffle addressing as in the bf16 epilogue.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue_f32(const ConvArgs& a, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                             unsigned char* smem, int m0, int n0) {
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int NT = WM * WN * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
+  constexpr int LD = BN + 4;
+  float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = wm * TM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int nl = wn * TN + j * 16 + fq * 4;
+      float4 q;
+      float* qv = reinterpret_cast<float*>(&q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + nl + r;
+        float v = acc[i][j][r];
+        if (a.bias && n < a.N) v += a.bias[n];
+        qv[r] = post_res ? v : act_fn(v, act);
+      }
+      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+    }
+  }
+  __syncthreads();
+  constexpr int VEC_PER_ROW = BN / 4;
+  for (int id = tid; id < BM * VEC_PER_ROW; id += NT) {
+    const int ml = id / VEC_PER_ROW, c4 = (id % VEC_PER_ROW) * 4;
+    const int m = m0 + ml, n = n0 + c4;
+    if (m >= a.M || n >= a.N) continue;
+    float4 v = *reinterpret_cast<const float4*>(st + ml * LD + c4);
+    const int ox = m % a.Wo, oy = (m / a.Wo) % a.Ho, b = m / (a.Wo * a.Ho);
+    long o;
+    if (a.shuffle > 0) {
+      const int s = a.shuffle, coutr = a.N / (s * s);
+      const int sy = n / (s * coutr), sx = (n / coutr) % s, co = n % coutr;
+      o = (((long)b * a.Ho * s + oy * s + sy) * (a.Wo * s) + ox * s + sx) * a.ldo + a.co_off + co;
+    } else {
+      o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n;
+    }
+    if (a.res_f) {
+      const float4 r = *reinterpret_cast<const float4*>(a.res_f + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldr +
+                                                        a.r_off + n);
+      if (post_res) {
+        v.x = act_fn(v.x + r.x, act); v.y = act_fn(v.y + r.y, act);
+        v.z = act_fn(v.z + r.z, act); v.w = act_fn(v.w + r.w, act);
+      } else {
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+      }
+    }
+    *reinterpret_cast<float4*>(a.out_f + o) = v;
+  }
+}
+
+// ---- x3 v1: register staging (any Cin % 8 == 0).  A chunk = 8 channels of one
+// pixel (two 16-B fp32 loads, split into hi / lo bf16x8); LDS holds hi and lo
+// images of A and B in the bf16 kernel's [rows][64 B] swizzled layout.
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) conv_nhwc_x3_kernel(ConvArgs a) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_CHUNKS = BM * 4, B_CHUNKS = BN * 4;
+  constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64;
+  constexpr int STAGE = 2 * (A_BYTES + B_BYTES);  // A hi, A lo, B hi, B lo
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+
+  int a_row[A_PER_T], a_c[A_PER_T], a_b[A_PER_T], a_iy0[A_PER_T], a_ix0[A_PER_T];
+  bool a_ok[A_PER_T];
+#pragma unroll
+  for (int t = 0; t < A_PER_T; ++t) {
+    const int id = tid + t * 256;
+    a_row[t] = id >> 2;
+    a_c[t] = id & 3;
+    const int m = m0 + a_row[t];
+    a_ok[t] = id < A_CHUNKS && m < a.M;
+    const int mm = a_ok[t] ? m : 0;
+    const int ox = mm % a.Wo, oy = (mm / a.Wo) % a.Ho, b = mm / (a.Wo * a.Ho);
+    a_b[t] = b;
+    a_iy0[t] = oy * a.S - a.P;
+    a_ix0[t] = ox * a.S - a.P;
+  }
+  const long ldw = 2L * a.Kp;
+
+  uint4 rah[A_PER_T], ral[A_PER_T], rbh[B_PER_T], rbl[B_PER_T];
+  auto load_tiles = [&](int kt) {
+#pragma unroll
+    for (int t = 0; t < A_PER_T; ++t) {
+      float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+      const int k0 = kt * BK + a_c[t] * 8;
+      if (a_ok[t] && k0 < a.K) {
+        const int tap = k0 / a.Cin, ci = k0 - tap * a.Cin;
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
+        const int iy = a_iy0[t] + ky, ix = a_ix0[t] + kx;
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+          const float* p = a.in_f + (((long)a_b[t] * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + ci;
+          x0 = *reinterpret_cast<const float4*>(p);
+          x1 = *reinterpret_cast<const float4*>(p + 4);
+        }
+      }
+      bf16x8 h, l;
+      split8(x0, x1, h, l);
+      rah[t] = *reinterpret_cast<uint4*>(&h);
+      ral[t] = *reinterpret_cast<uint4*>(&l);
+    }
+#pragma unroll
+    for (int t = 0; t < B_PER_T; ++t) {
+      const int id = tid + t * 256;
+      uint4 h = make_uint4(0, 0, 0, 0), l = h;
+      if (id < B_CHUNKS) {
+        const int n = n0 + (id >> 2);
+        if (n < a.N) {
+          const __hip_bfloat16* p = a.w + (long)n * ldw + (kt * BK + (id & 3) * 8) * 2;
+          h = *reinterpret_cast<const uint4*>(p);
+          l = *reinterpret_cast<const uint4*>(p + 8);
+        }
+      }
+      rbh[t] = h;
+      rbl[t] = l;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    unsigned char* sah = smem + buf * STAGE;
+    unsigned char* sal = sah + A_BYTES;
+    unsigned char* sbh = sal + A_BYTES;
+    unsigned char* sbl = sbh + B_BYTES;
+#pragma unroll
+    for (int t = 0; t < A_PER_T; ++t)
+      if (tid + t * 256 < A_CHUNKS) {
+        *reinterpret_cast<uint4*>(sah + swz(a_row[t], a_c[t])) = rah[t];
+        *reinterpret_cast<uint4*>(sal + swz(a_row[t], a_c[t])) = ral[t];
+      }
+#pragma unroll
+    for (int t = 0; t < B_PER_T; ++t) {
+      const int id = tid + t * 256;
+      if (id < B_CHUNKS) {
+        *reinterpret_cast<uint4*>(sbh + swz(id >> 2, id & 3)) = rbh[t];
+        *reinterpret_cast<uint4*>(sbl + swz(id >> 2, id & 3)) = rbl[t];
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kp / BK;
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles(kt + 1);
+    const unsigned char* sah = smem + cur * STAGE;
+    const unsigned char* sal = sah + A_BYTES;
+    const unsigned char* sbh = sal + A_BYTES;
+    const unsigned char* sbl = sbh + B_BYTES;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * TM + i * 16 + fr;
+      ah[i] = *reinterpret_cast<const bf16x8*>(sah + swz(r, fq));
+      al[i] = *reinterpret_cast<const bf16x8*>(sal + swz(r, fq));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int r = wn * TN + j * 16 + fr;
+      bh[j] = *reinterpret_cast<const bf16x8*>(sbh + swz(r, fq));
+      bl[j] = *reinterpret_cast<const bf16x8*>(sbl + swz(r, fq));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+  epilogue_f32<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+}
+
+// ---- x3 v2: global_load_lds staging, Cin % 32 == 0 (a 32-channel K step never
+// straddles a tap).  LDS rows are 128 B for both operands: A = 32 fp32
+// channels (slot s = channels 4s..4s+3), B = 4 x {hi 8, lo 8}.  A lane group
+// fq reads slots 2fq and 2fq+1 of its 16 rows; the slot swizzle
+// s ^ ((r ^ (r >> 3)) & 7) keeps every ds_read_b128 lane group on 16 distinct
+// (bank-row half, slot) pairs for that pattern (exhaustive check over the four
+// gfx950 b128 lane groups, rows at any 16-row fragment base).
+__device__ __forceinline__ int swz3(int row) { return (row ^ (row >> 3)) & 7; }
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN;
+  constexpr int BKC = 32, ROWB = 128;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split over the waves' 8-row DMAs");
+  constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);
+  constexpr int NL = A_INS + B_INS;
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nmt = (a.M + BM - 1) / BM, nnt = (a.N + BN - 1) / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int lrow = lane >> 3, lslot = lane & 7;
+  long a_base[A_INS];
+  int a_iy0[A_INS], a_ix0[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wid * A_INS + j) * 8 + lrow;
+    const int m = m0 + row;
+    const int c = lslot ^ swz3(row);
+    if (m < a.M) {
+      const int ox = m % a.Wo, t = m / a.Wo, oy = t % a.Ho, b = t / a.Ho;
+      a_iy0[j] = oy * a.S - a.P;
+      a_ix0[j] = ox * a.S - a.P;
+      a_base[j] = (((long)b * a.H + a_iy0[j]) * a.W + a_ix0[j]) * a.ldi + a.ci_off + c * 4;
+    } else {
+      a_iy0[j] = -(1 << 28);
+      a_ix0[j] = 0;
+      a_base[j] = 0;
+    }
+  }
+  const __hip_bfloat16* b_ptr[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wid * B_INS + j) * 8 + lrow;
+    const int n = n0 + row;
+    b_ptr[j] = n < a.N ? a.w + (long)n * 2 * a.Kp + (lslot ^ swz3(row)) * 8 : nullptr;
+  }
+  const long tap_stride_x = a.ldi, tap_stride_y = (long)a.W * a.ldi;
+
+  auto issue = [&](int kt, int buf, int ky, int kx, int ci0) {
+    unsigned char* sa = smem + buf * STAGE;
+    unsigned char* sb = sa + A_BYTES;
+    const long toff = ky * tap_stride_y + kx * tap_stride_x + ci0;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      const void* g = ok ? (const void*)(a.in_f + a_base[j] + toff) : (const void*)g_conv_zero_page;
+      glds16(g, sa + (wid * A_INS + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const void* g = b_ptr[j] ? (const void*)(b_ptr[j] + kt * BKC * 2) : (const void*)g_conv_zero_page;
+      glds16(g, sb + (wid * B_INS + j) * 1024);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kp / BKC;
+  int ky = 0, kx = 0, ci0 = 0;
+  auto advance = [&]() {
+    ci0 += BKC;
+    if (ci0 == a.Cin) {
+      ci0 = 0;
+      if (++kx == a.KW) { kx = 0; ++ky; }
+    }
+  };
+  issue(0, 0, ky, kx, ci0);
+  advance();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, cur ^ 1, ky, kx, ci0);
+      advance();
+      wait_vmcnt<NL>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const unsigned char* sa = smem + cur * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int r = wn * TN + j * 16 + fr;
+      bh[j] = *reinterpret_cast<const bf16x8*>(sb + r * ROWB + (((2 * fq) ^ swz3(r)) << 4));
+      bl[j] = *reinterpret_cast<const bf16x8*>(sb + r * ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * TM + i * 16 + fr;
+      const float4 x0 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq) ^ swz3(r)) << 4));
+      const float4 x1 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+      split8(x0, x1, ah[i], al[i]);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is restaged
+    asm volatile("" ::: "memory");
+  }
+  epilogue_f32<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+}
+
+// ---- x3 small halo: 3x3, pad 1, stride 1/2, Cin and N in {16, 32}.  The fp32
+// halo is split once while staging (register path: every halo pixel is read by
+// 9 taps, so splitting at the fragment read would cost 9x the VALU); hi and lo
+// halo images and hi / lo weight rows sit side by side in LDS.
+template <int CIN, int NOUT, int S>
+struct SmallHaloX3 {
+  static constexpr int TT = 16, HW_ = (TT - 1) * S + 3, NPX = HW_ * HW_;
+  static constexpr int PB = CIN * 2;                      // bytes per pixel per image
+  static constexpr int H_BYTES = (NPX * PB + 15) / 16 * 16;
+  static constexpr int KP = (9 * CIN + 31) / 32 * 32, KS = KP / 32;
+  static constexpr int WRS = KP * 2 + 16;
+  static constexpr int LDS = 2 * H_BYTES + 2 * NOUT * WRS;
+};
+
+template <int CIN, int NOUT, int S>
+__global__ void __launch_bounds__(256) conv_small_halo_x3_kernel(ConvArgs a) {
+  using G = SmallHaloX3<CIN, NOUT, S>;
+  constexpr int TT = G::TT, HW_ = G::HW_, NPX = G::NPX, PB = G::PB, KP = G::KP, KS = G::KS, WRS = G::WRS;
+  constexpr int FN = NOUT / 16, CPP = CIN / 4;  // 16-B fp32 chunks per pixel
+  static_assert(G::LDS <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
+  unsigned char* const himg = smem;
+  unsigned char* const limg = smem + G::H_BYTES;
+  unsigned char* const wlh = smem + 2 * G::H_BYTES;
+  unsigned char* const wll = wlh + NOUT * WRS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int ntx = (a.Wo + TT - 1) / TT, nty = (a.Ho + TT - 1) / TT;
+  const int tile = blockIdx.x;
+  const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
+  const int ty0 = (rem / ntx) * TT, tx0 = (rem % ntx) * TT;
+  const int iy0 = ty0 * S - 1, ix0 = tx0 * S - 1;
+
+  for (int g = tid; g < NPX * CPP; g += 256) {
+    const int p = g / CPP, c = g - p * CPP;
+    const int hy = p / HW_, hx = p - hy * HW_;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+      v = *reinterpret_cast<const float4*>(a.in_f + (((long)b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + c * 4);
+    uint2 h, l;
+    split4(v, h, l);
+    *reinterpret_cast<uint2*>(himg + p * PB + c * 8) = h;
+    *reinterpret_cast<uint2*>(limg + p * PB + c * 8) = l;
+  }
+  for (int g = tid; g < NOUT * KP / 8; g += 256) {
+    const int n = g / (KP / 8), c = g - n * (KP / 8);
+    const __hip_bfloat16* src = a.w + (long)n * 2 * a.Kp + c * 16;
+    *reinterpret_cast<uint4*>(wlh + n * WRS + c * 16) = *reinterpret_cast<const uint4*>(src);
+    *reinterpret_cast<uint4*>(wll + n * WRS + c * 16) = *reinterpret_cast<const uint4*>(src + 8);
+  }
+  float bias_r[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias_r[j][r] = a.bias ? a.bias[j * 16 + fq * 4 + r] : 0.f;
+  __syncthreads();
+
+  f32x4 acc[4][FN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = s * 32 + fq * 8;
+    const int tap = k0 / CIN, ci0 = k0 - tap * CIN;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    bf16x8 ah[4], al[4], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = ((wid * 4 + i) * S + ky) * HW_ + fr * S + kx;
+      ah[i] = tap < 9 ? *reinterpret_cast<const bf16x8*>(himg + p * PB + ci0 * 2) : bf16x8{};
+      al[i] = tap < 9 ? *reinterpret_cast<const bf16x8*>(limg + p * PB + ci0 * 2) : bf16x8{};
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(wlh + (j * 16 + fr) * WRS + k0 * 2);
+      bl[j] = *reinterpret_cast<const bf16x8*>(wll + (j * 16 + fr) * WRS + k0 * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+  }
+
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
+  const int ox = tx0 + fr;
+  if (ox >= a.Wo) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = ty0 + wid * 4 + i;
+    if (oy >= a.Ho) break;
+    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = j * 16 + fq * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias_r[j][r];
+      if (a.res_f) {
+        const float4 rr = *reinterpret_cast<const float4*>(a.res_f + pix * a.ldr + a.r_off + n);
+        const float rv[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = post_res ? act_fn(v[r] + rv[r], act) : act_fn(v[r], act) + rv[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      }
+      *reinterpret_cast<float4*>(a.out_f + pix * a.ldo + a.co_off + n) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+template <int CIN, int NOUT, int S>
+int launch_small_halo_x3_t(const ConvArgs& a, hipStream_t stream) {
+  const int ntiles = a.B * ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16);
+  conv_small_halo_x3_kernel<CIN, NOUT, S><<<ntiles, 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// (Cin 32, stride 2) needs a 33 x 33 x 32 halo (2 x 70 KiB): not instantiated, v1 takes it
+bool small_halo_x3_ok(const ConvArgs& a) { return small_halo_ok(a) && !(a.Cin == 32 && a.S == 2); }
+
+int launch_small_halo_x3(const ConvArgs& a, hipStream_t stream) {
+  if (!small_halo_x3_ok(a)) return (int)hipErrorInvalidValue;
+  const int key = (a.Cin == 32) * 4 + (a.N == 32) * 2 + (a.S == 2);
+  switch (key) {
+    case 0: return launch_small_halo_x3_t<16, 16, 1>(a, stream);
+    case 1: return launch_small_halo_x3_t<16, 16, 2>(a, stream);
+    case 2: return launch_small_halo_x3_t<16, 32, 1>(a, stream);
+    case 3: return launch_small_halo_x3_t<16, 32, 2>(a, stream);
+    case 4: return launch_small_halo_x3_t<32, 16, 1>(a, stream);
+    case 6: return launch_small_halo_x3_t<32, 32, 1>(a, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  conv_glds_x3_kernel<BM, BN, WM, WN><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_x3(const ConvArgs& a, hipStream_t stream) {
+  dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN);
+  conv_nhwc_x3_kernel<BM, BN, WM, WN><<<grid, 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // Returns hipErrorInvalidValue when the shape is outside the kernel's
@@ -844,6 +1384,7 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
   a.N = N; a.K = KH * KW * Cin; a.Kp = Kp; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off;
   a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
+  a.in_f = nullptr; a.res_f = nullptr; a.out_f = nullptr;
   if (a.K > Kp) return (int)hipErrorInvalidValue;
   // tile: 0 = auto
   // measured on MI355X (tools/bench_conv.py): 128x32 for N<=32, 128x64 for N<=64, 64x128 above
@@ -901,6 +1442,45 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
     case 3: return launch<128, 128, 2, 2>(a, stream);
     case 4: return launch<256, 64, 4, 1>(a, stream);
     case 5: return launch<64, 128, 1, 4>(a, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// fp32 mode: fp32 NHWC activations (in / res / out), split weights w
+// [N, Kp/8, {hi 8, lo 8}] bf16 (2*Kp per row), fp32 bias.  Same slice / residual /
+// pixel-shuffle contract as tca_conv_nhwc.  tile: 0 auto, 1 v1 128x16 ... (see switch).
+TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
+                             const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
+                             int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
+                             int tile, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((Cin & 7) || (ldi & 7) || (ci_off & 7) || (N & 7) || (ldo & 7) || (co_off & 7) || (Kp & 31)) return (int)hipErrorInvalidValue;
+  if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
+  ConvArgs a;
+  a.in = nullptr; a.res = nullptr; a.out = nullptr;
+  a.in_f = in; a.res_f = res; a.out_f = out;
+  a.w = (const __hip_bfloat16*)w; a.bias = bias;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off;
+  a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
+  a.N = N; a.K = KH * KW * Cin; a.Kp = Kp; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off;
+  a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
+  if (a.K > Kp) return (int)hipErrorInvalidValue;
+  const bool v2ok = (Cin % 32) == 0 && Kp == a.K;
+  if (tile == 0 && small_halo_x3_ok(a)) tile = 60;
+  if (tile == 0) tile = v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 16 ? 6 : N <= 32 ? 1 : N <= 64 ? 2 : 5);
+  if (tile >= 10 && tile < 60 && !v2ok) return (int)hipErrorInvalidValue;
+  switch (tile) {
+    case 60: return launch_small_halo_x3(a, stream);
+    case 20: return launch_glds_x3<128, 128, 4, 2>(a, stream);
+    case 22: return launch_glds_x3<128, 64, 4, 2>(a, stream);
+    case 24: return launch_glds_x3<64, 128, 2, 4>(a, stream);
+    case 25: return launch_glds_x3<128, 128, 2, 4>(a, stream);
+    case 26: return launch_glds_x3<256, 64, 4, 2>(a, stream);
+    case 27: return launch_glds_x3<128, 256, 2, 4>(a, stream);
+    case 1: return launch_x3<128, 32, 4, 1>(a, stream);
+    case 2: return launch_x3<128, 64, 4, 1>(a, stream);
+    case 5: return launch_x3<64, 128, 1, 4>(a, stream);
+    case 6: return launch_x3<128, 16, 4, 1>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

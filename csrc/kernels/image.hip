@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
       for (int k = 0; k < 4; ++k)
         if (q * 4 + k < p.dst_w) o[k] = from_f32<T>(0.f);
     }
-  } else if (p.dst_c == 8 && sizeof(T) == 2) {  // NHWC, 3 channels + 5 zero pad: one 16-B store per pixel
+  } else if (p.dst_c == 8) {  // NHWC, 3 channels + 5 zero pad: 16-B stores per pixel
     const long base = (((long)b * p.dst_h + y) * p.dst_w + q * 4) * 8;
     for (int k = 0; k < 4; ++k) {
       if (q * 4 + k >= p.dst_w) break;
@@ -126,7 +126,9 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
       }
 #pragma unroll
       for (int c = 3; c < 8; ++c) px[c] = from_f32<T>(0.f);
-      *reinterpret_cast<uint4*>(d + base + (long)k * 8) = *reinterpret_cast<uint4*>(px);
+#pragma unroll
+      for (int v = 0; v < (int)(8 * sizeof(T) / 16); ++v)
+        reinterpret_cast<uint4*>(d + base + (long)k * 8)[v] = reinterpret_cast<uint4*>(px)[v];
     }
   } else {  // NHWC with dst_c in {3, 4}
     const long base = (((long)b * p.dst_h + y) * p.dst_w + q * 4) * p.dst_c;
@@ -175,14 +177,15 @@ __device__ __forceinline__ void sample_px(const PrepParams& p, const uint8_t* s,
   }
 }
 
-// Layout 2: space-to-depth 2x2, bf16 [B, H/2, W/2, 16]: channel (dy*2 + dx)*3 + c
-// holds pixel (2Y + dy, 2X + dx), channels 12..15 zero.  A k=6 s=2 p=2 stem
-// conv (YOLOv5 v6+) is exactly a 3x3 s=1 p=1 conv over this tensor with
-// rearranged weights (models/fast.py), with 12 of 16 input channels real
-// instead of 3 of 8 and half the input bytes.  One thread per 2x2 block,
-// two 16-B stores.
-__global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict__ src,
-                                                       __hip_bfloat16* __restrict__ dst, PrepParams p, int batch) {
+// Layout 2: space-to-depth 2x2, bf16 or fp32 [B, H/2, W/2, 16]: channel
+// (dy*2 + dx)*3 + c holds pixel (2Y + dy, 2X + dx), channels 12..15 zero.  A
+// k=6 s=2 p=2 stem conv (YOLOv5 v6+) is exactly a 3x3 s=1 p=1 conv over this
+// tensor with rearranged weights (models/fast.py), with 12 of 16 input
+// channels real instead of 3 of 8 and half the input bytes.  One thread per
+// 2x2 block, 32 B (bf16) or 64 B (fp32) of 16-B stores.
+template <typename T>
+__global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict__ src, T* __restrict__ dst,
+                                                       PrepParams p, int batch) {
   const int h2 = p.dst_h >> 1, w2 = p.dst_w >> 1;
   const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned total = (unsigned)batch * h2 * w2;
@@ -194,19 +197,20 @@ __global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict
   const uint8_t* s = src + (long)b * p.src_batch_stride;
   const float sc[3] = {p.sc0, p.sc1, p.sc2};
   const float bi[3] = {p.b0, p.b1, p.b2};
-  __hip_bfloat16 px[16];
+  T px[16];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     float o[3];
     sample_px(p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) px[d * 3 + c] = __float2bfloat16(o[p.swap_rb ? 2 - c : c] * sc[c] + bi[c]);
+    for (int c = 0; c < 3; ++c) px[d * 3 + c] = from_f32<T>(o[p.swap_rb ? 2 - c : c] * sc[c] + bi[c]);
   }
 #pragma unroll
-  for (int c = 12; c < 16; ++c) px[c] = __float2bfloat16(0.f);
+  for (int c = 12; c < 16; ++c) px[c] = from_f32<T>(0.f);
+  constexpr int NV = 16 * sizeof(T) / 16;
   uint4* o = reinterpret_cast<uint4*>(dst + (long)gid * 16);
-  o[0] = reinterpret_cast<uint4*>(px)[0];
-  o[1] = reinterpret_cast<uint4*>(px)[1];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) o[v] = reinterpret_cast<uint4*>(px)[v];
 }
 
 }  // namespace
@@ -220,16 +224,20 @@ TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src
   if (batch <= 0) return 0;
   PrepParams p{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, dst_c, dst_layout,
                reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
-  if (dst_layout == 2) {  // space-to-depth 2x2, bf16, 16 channels
-    if (src_c < 3 || dst_c != 16 || dst_dtype != kBF16 || (dst_h & 1) || (dst_w & 1) || reg_h <= 0 || reg_w <= 0)
+  if (dst_layout == 2) {  // space-to-depth 2x2, bf16 or fp32, 16 channels
+    if (src_c < 3 || dst_c != 16 || (dst_dtype != kBF16 && dst_dtype != kF32) || (dst_h & 1) || (dst_w & 1) ||
+        reg_h <= 0 || reg_w <= 0)
       return (int)hipErrorInvalidValue;
     const long t2 = (long)batch * (dst_h / 2) * (dst_w / 2);
     if (t2 >= (1L << 31)) return (int)hipErrorInvalidValue;
-    prep_s2d_kernel<<<(unsigned)((t2 + 255) / 256), 256, 0, stream>>>((const uint8_t*)src, (__hip_bfloat16*)dst, p,
-                                                                     batch);
+    const unsigned g = (unsigned)((t2 + 255) / 256);
+    if (dst_dtype == kF32)
+      prep_s2d_kernel<float><<<g, 256, 0, stream>>>((const uint8_t*)src, (float*)dst, p, batch);
+    else
+      prep_s2d_kernel<__hip_bfloat16><<<g, 256, 0, stream>>>((const uint8_t*)src, (__hip_bfloat16*)dst, p, batch);
     TCA_LAUNCH_CHECK();
   }
-  if (src_c < 3 || (dst_c != 3 && dst_c != 4 && !(dst_c == 8 && dst_layout == 1 && dst_dtype != kF32)) || reg_h <= 0 ||
+  if (src_c < 3 || (dst_c != 3 && dst_c != 4 && !(dst_c == 8 && dst_layout == 1)) || reg_h <= 0 ||
       reg_w <= 0)
     return (int)hipErrorInvalidValue;
   const long total = (long)batch * dst_h * ((dst_w + 3) / 4);

@@ -1,30 +1,35 @@
-// Small NHWC bf16 data-movement kernels for the concat-free detector plans:
+// Small NHWC data-movement kernels for the concat-free detector plans, bf16 or
+// fp32 activations (dtype kBF16 / kF32):
 //  * max-pool k x k, stride 1, pad k/2 (YOLOv5 SPPF) or strided (ResNet stem), slice in -> slice out
 //  * nearest 2x upsample (YOLOv5 PANet), channel slice in -> slice out
-// Both move 16 B (8 channels) per thread; slices are ci_off/ldi, co_off/ldo.
+// Both move 16 B per thread (8 bf16 or 4 fp32 channels); slices are ci_off/ldi, co_off/ldo.
 #include "tca_common.h"
 
 using namespace tca;
 
 namespace {
 
-__device__ __forceinline__ void bf16x8_max(uint4& acc, const uint4& v) {
-  __hip_bfloat16* a = reinterpret_cast<__hip_bfloat16*>(&acc);
-  const __hip_bfloat16* b = reinterpret_cast<const __hip_bfloat16*>(&v);
+template <typename T>
+__device__ __forceinline__ void vec_max(uint4& acc, const uint4& v) {
+  constexpr int E = 16 / sizeof(T);
+  T* a = reinterpret_cast<T*>(&acc);
+  const T* b = reinterpret_cast<const T*>(&v);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = __float2bfloat16(fmaxf(__bfloat162float(a[e]), __bfloat162float(b[e])));
+  for (int e = 0; e < E; ++e) a[e] = from_f32<T>(fmaxf(to_f32(a[e]), to_f32(b[e])));
 }
 
 // k x k max-pool, stride s, pad p (out-of-image taps ignored, as nn.MaxPool2d's -inf padding)
-__global__ void __launch_bounds__(256) maxpool_kernel(const __hip_bfloat16* __restrict__ in, int B, int H, int W,
-                                                      int C, int ldi, int ci_off, int k, int s, int p, int Ho, int Wo,
-                                                      __hip_bfloat16* __restrict__ out, int ldo, int co_off) {
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_kernel(const T* __restrict__ in, int B, int H, int W, int C, int ldi,
+                                                      int ci_off, int k, int s, int p, int Ho, int Wo,
+                                                      T* __restrict__ out, int ldo, int co_off) {
+  constexpr int E = 16 / sizeof(T);
   // 32-bit index math (host guarantees total < 2^31): 64-bit div/mod is ~150 VALU each
-  const unsigned c8 = C / 8;
-  const unsigned total = (unsigned)B * Ho * Wo * c8;
+  const unsigned cv_n = C / E;
+  const unsigned total = (unsigned)B * Ho * Wo * cv_n;
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int cv = (int)(t % c8);
-    const unsigned pix = t / c8;
+    const int cv = (int)(t % cv_n);
+    const unsigned pix = t / cv_n;
     const unsigned yx = pix % ((unsigned)Wo * Ho);
     const int x = (int)(yx % (unsigned)Wo), y = (int)(yx / (unsigned)Wo), b = (int)(pix / ((unsigned)Wo * Ho));
     uint4 acc = make_uint4(0, 0, 0, 0);
@@ -35,61 +40,83 @@ __global__ void __launch_bounds__(256) maxpool_kernel(const __hip_bfloat16* __re
       for (int dx = 0; dx < k; ++dx) {
         const int xx = x * s - p + dx;
         if (xx < 0 || xx >= W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(in + (((long)b * H + yy) * W + xx) * ldi + ci_off + cv * 8);
-        if (first) { acc = v; first = false; } else bf16x8_max(acc, v);
+        const uint4 v = *reinterpret_cast<const uint4*>(in + (((long)b * H + yy) * W + xx) * ldi + ci_off + cv * E);
+        if (first) { acc = v; first = false; } else vec_max<T>(acc, v);
       }
     }
-    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * 8) = acc;
+    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * E) = acc;
   }
 }
 
-__global__ void __launch_bounds__(256) upsample2x_kernel(const __hip_bfloat16* __restrict__ in, int B, int H, int W,
-                                                         int C, int ldi, int ci_off,
-                                                         __hip_bfloat16* __restrict__ out, int ldo, int co_off) {
-  const unsigned c8 = C / 8;
+template <typename T>
+__global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ in, int B, int H, int W, int C, int ldi,
+                                                         int ci_off, T* __restrict__ out, int ldo, int co_off) {
+  constexpr int E = 16 / sizeof(T);
+  const unsigned cv_n = C / E;
   const int Ho = 2 * H, Wo = 2 * W;
-  const unsigned total = (unsigned)B * Ho * Wo * c8;
+  const unsigned total = (unsigned)B * Ho * Wo * cv_n;
   for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int cv = (int)(t % c8);
-    const unsigned pix = t / c8;
+    const int cv = (int)(t % cv_n);
+    const unsigned pix = t / cv_n;
     const unsigned yx = pix % ((unsigned)Wo * Ho);
     const int x = (int)(yx % (unsigned)Wo), y = (int)(yx / (unsigned)Wo), b = (int)(pix / ((unsigned)Wo * Ho));
-    const uint4 v = *reinterpret_cast<const uint4*>(in + (((long)b * H + y / 2) * W + x / 2) * ldi + ci_off + cv * 8);
-    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * 8) = v;
+    const uint4 v = *reinterpret_cast<const uint4*>(in + (((long)b * H + y / 2) * W + x / 2) * ldi + ci_off + cv * E);
+    *reinterpret_cast<uint4*>(out + (long)pix * ldo + co_off + cv * E) = v;
   }
 }
 
 int grid_for(long work) { return (int)min((work + 255) / 256, (long)4096); }
 
+bool slices_ok(int C, int ldi, int ci_off, int ldo, int co_off, int dtype) {
+  if (dtype != kBF16 && dtype != kF32) return false;
+  const int e = dtype == kF32 ? 3 : 7;  // channels per 16-B vector - 1
+  return !((C & e) || (ldi & e) || (ci_off & e) || (ldo & e) || (co_off & e));
+}
+
+int launch_pool(const void* in, int B, int H, int W, int C, int ldi, int ci_off, int k, int s, int p, void* out,
+                int Ho, int Wo, int ldo, int co_off, int dtype, hipStream_t stream) {
+  const int E = dtype == kF32 ? 4 : 8;
+  const int g = grid_for((long)B * Ho * Wo * (C / E));
+  if (dtype == kF32)
+    maxpool_kernel<float><<<g, 256, 0, stream>>>((const float*)in, B, H, W, C, ldi, ci_off, k, s, p, Ho, Wo,
+                                                 (float*)out, ldo, co_off);
+  else
+    maxpool_kernel<__hip_bfloat16><<<g, 256, 0, stream>>>((const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, k, s,
+                                                          p, Ho, Wo, (__hip_bfloat16*)out, ldo, co_off);
+  TCA_LAUNCH_CHECK();
+}
+
 }  // namespace
 
 TCA_API int tca_maxpool_nhwc(const void* in, int B, int H, int W, int C, int ldi, int ci_off, int k, void* out,
-                             int ldo, int co_off, hipStream_t stream) {
+                             int ldo, int co_off, int dtype, hipStream_t stream) {
   if (B <= 0) return 0;
-  if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
-  if ((long)B * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
-  maxpool_kernel<<<grid_for((long)B * H * W * (C / 8)), 256, 0, stream>>>(
-      (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, k, 1, k / 2, H, W, (__hip_bfloat16*)out, ldo, co_off);
-  TCA_LAUNCH_CHECK();
+  if (!slices_ok(C, ldi, ci_off, ldo, co_off, dtype)) return (int)hipErrorInvalidValue;
+  if ((long)B * H * W * C >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
+  return launch_pool(in, B, H, W, C, ldi, ci_off, k, 1, k / 2, out, H, W, ldo, co_off, dtype, stream);
 }
 
 // strided max-pool (ResNet stem: k 3, s 2, p 1); output Ho x Wo given by the caller
 TCA_API int tca_maxpool2d_nhwc(const void* in, int B, int H, int W, int C, int ldi, int ci_off, int k, int s, int p,
-                               void* out, int Ho, int Wo, int ldo, int co_off, hipStream_t stream) {
+                               void* out, int Ho, int Wo, int ldo, int co_off, int dtype, hipStream_t stream) {
   if (B <= 0) return 0;
-  if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7) || s < 1 || k < 1) return (int)hipErrorInvalidValue;
-  if ((long)B * Ho * Wo * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
-  maxpool_kernel<<<grid_for((long)B * Ho * Wo * (C / 8)), 256, 0, stream>>>(
-      (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, k, s, p, Ho, Wo, (__hip_bfloat16*)out, ldo, co_off);
-  TCA_LAUNCH_CHECK();
+  if (!slices_ok(C, ldi, ci_off, ldo, co_off, dtype) || s < 1 || k < 1) return (int)hipErrorInvalidValue;
+  if ((long)B * Ho * Wo * C >= (1L << 31)) return (int)hipErrorInvalidValue;
+  return launch_pool(in, B, H, W, C, ldi, ci_off, k, s, p, out, Ho, Wo, ldo, co_off, dtype, stream);
 }
 
 TCA_API int tca_upsample2x_nhwc(const void* in, int B, int H, int W, int C, int ldi, int ci_off, void* out, int ldo,
-                                int co_off, hipStream_t stream) {
+                                int co_off, int dtype, hipStream_t stream) {
   if (B <= 0) return 0;
-  if ((C & 7) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
-  if ((long)B * 4 * H * W * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
-  upsample2x_kernel<<<grid_for((long)B * 4 * H * W * (C / 8)), 256, 0, stream>>>(
-      (const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off, (__hip_bfloat16*)out, ldo, co_off);
+  if (!slices_ok(C, ldi, ci_off, ldo, co_off, dtype)) return (int)hipErrorInvalidValue;
+  if ((long)B * 4 * H * W * C >= (1L << 31)) return (int)hipErrorInvalidValue;
+  const int E = dtype == kF32 ? 4 : 8;
+  const int g = grid_for((long)B * 4 * H * W * (C / E));
+  if (dtype == kF32)
+    upsample2x_kernel<float><<<g, 256, 0, stream>>>((const float*)in, B, H, W, C, ldi, ci_off, (float*)out, ldo,
+                                                    co_off);
+  else
+    upsample2x_kernel<__hip_bfloat16><<<g, 256, 0, stream>>>((const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off,
+                                                             (__hip_bfloat16*)out, ldo, co_off);
   TCA_LAUNCH_CHECK();
 }

@@ -18,8 +18,9 @@
 //     pillar;
 //   * max over slots: 16 accumulator registers, then lane l <-> l+32;
 //     relu(max + bias) == max(relu(x + bias));
-//   * scatter: lanes write the 64 bf16 channels of canvas[b][y][x][:] as one
-//     128-byte line (NHWC canvas, the layout the BEV convs consume).
+//   * scatter: lanes write the 64 channels of canvas[b][y][x][:] as one
+//     128-byte (bf16) or 256-byte (fp32 mode) line (NHWC canvas, the layout
+//     the BEV convs consume).
 // tca_pillar_canvas_clear zeroes exactly the cells the previous frame wrote,
 // so the 27 MB/frame canvas is never memset.
 #include "tca_common.h"
@@ -41,14 +42,14 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
-template <bool FROM_SLOTS>
+template <bool FROM_SLOTS, typename CT>
 __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const float* __restrict__ pts, int pstride, int max_pts,               // FROM_SLOTS source
     const int* __restrict__ slots, const int* __restrict__ vcount,        // FROM_SLOTS source
     const float* __restrict__ voxels, const int* __restrict__ num_points,  // materialised source [V][P][4]
     const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P,
     const float* __restrict__ W /*[64][10]*/, const float* __restrict__ bias /*[64]*/, PillarGeom g,
-    __hip_bfloat16* __restrict__ canvas, float* __restrict__ feat_out) {
+    CT* __restrict__ canvas, float* __restrict__ feat_out) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const int ch = 32 * h + r;
     if (canvas) {
       const long cell = ((long)b * g.ny + co.z) * g.nx + co.w;
-      canvas[cell * 64 + ch] = __float2bfloat16(val);
+      canvas[cell * 64 + ch] = from_f32<CT>(val);
     }
     if (feat_out) feat_out[(long)v * 64 + ch] = val;
     v = vn;
@@ -187,18 +188,18 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
 }
 
 // Zero exactly the cells the previous frame scattered: one thread per 16-B
-// chunk of a pillar's C bf16 channels (C % 8 == 0), frame per grid row.
+// chunk of a pillar's C channels (C * esize % 16 == 0), frame per grid row.
 __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict__ coords,
                                                            const int* __restrict__ voxel_count, int max_voxels, int nx,
-                                                           int ny, int C, __hip_bfloat16* __restrict__ canvas) {
+                                                           int ny, int C, int esize, uint4* __restrict__ canvas) {
   const int b = blockIdx.y;
-  const int cpp = C >> 3;
+  const int cpp = C * esize >> 4;
   const int t = blockIdx.x * 256 + threadIdx.x;
   const int vid = t / cpp, c = t - vid * cpp;
   if (vid >= voxel_count[b]) return;
   const int* co = coords + ((long)b * max_voxels + vid) * 4;
   const long cell = ((long)b * ny + co[2]) * nx + co[3];
-  reinterpret_cast<uint4*>(canvas + cell * C)[c] = make_uint4(0u, 0u, 0u, 0u);
+  canvas[cell * cpp + c] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 }  // namespace
@@ -207,13 +208,18 @@ __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict
 TCA_API int tca_pillar_vfe_slots(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount,
                                  const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                                  const float* W, const float* bias, const float* range, const float* vsize, int nx,
-                                 int ny, void* canvas, float* feat_out, hipStream_t stream) {
+                                 int ny, void* canvas, float* feat_out, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (P > 32) return (int)hipErrorInvalidValue;
+  if (P > 32 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
-  pillar_vfe_kernel<true><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords,
-                                                    voxel_count, batch, max_voxels, P, W, bias, g,
-                                                    (__hip_bfloat16*)canvas, feat_out);
+  if (canvas_dtype == kF32)
+    pillar_vfe_kernel<true, float><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr,
+                                                             coords, voxel_count, batch, max_voxels, P, W, bias, g,
+                                                             (float*)canvas, feat_out);
+  else
+    pillar_vfe_kernel<true, __hip_bfloat16><<<2048, 256, 0, stream>>>(
+        pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords, voxel_count, batch, max_voxels, P, W, bias, g,
+        (__hip_bfloat16*)canvas, feat_out);
   TCA_LAUNCH_CHECK();
 }
 
@@ -221,21 +227,27 @@ TCA_API int tca_pillar_vfe_slots(const float* pts, int pstride, int max_pts, con
 TCA_API int tca_pillar_vfe_voxels(const float* voxels, const int* num_points, const int* coords,
                                   const int* voxel_count, int batch, int max_voxels, int P, const float* W,
                                   const float* bias, const float* range, const float* vsize, int nx, int ny,
-                                  void* canvas, float* feat_out, hipStream_t stream) {
+                                  void* canvas, float* feat_out, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (P > 32) return (int)hipErrorInvalidValue;
+  if (P > 32 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
-  pillar_vfe_kernel<false><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords,
-                                                     voxel_count, batch, max_voxels, P, W, bias, g,
-                                                     (__hip_bfloat16*)canvas, feat_out);
+  if (canvas_dtype == kF32)
+    pillar_vfe_kernel<false, float><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points,
+                                                              coords, voxel_count, batch, max_voxels, P, W, bias, g,
+                                                              (float*)canvas, feat_out);
+  else
+    pillar_vfe_kernel<false, __hip_bfloat16><<<2048, 256, 0, stream>>>(
+        nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias, g,
+        (__hip_bfloat16*)canvas, feat_out);
   TCA_LAUNCH_CHECK();
 }
 
 TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
-                                    int ny, int C, void* canvas, hipStream_t stream) {
+                                    int ny, int C, void* canvas, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (C & 7) return (int)hipErrorInvalidValue;
-  canvas_clear_kernel<<<dim3((max_voxels * (C / 8) + 255) / 256, batch), 256, 0, stream>>>(
-      coords, voxel_count, max_voxels, nx, ny, C, (__hip_bfloat16*)canvas);
+  const int esize = canvas_dtype == kF32 ? 4 : 2;
+  if ((C * esize) & 15 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
+  canvas_clear_kernel<<<dim3((max_voxels * (C * esize / 16) + 255) / 256, batch), 256, 0, stream>>>(
+      coords, voxel_count, max_voxels, nx, ny, C, esize, (uint4*)canvas);
   TCA_LAUNCH_CHECK();
 }

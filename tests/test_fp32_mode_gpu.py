@@ -1,0 +1,293 @@
+"""fp32 precision mode (split-product MFMA kernels) vs fp32 PyTorch references.
+
+The reference serves its detectors in fp32 (``examples/YOLOv5/config.pbtxt:7,16``,
+``examples/pointpillar_kitti/config.pbtxt:33,54``).  The fp32 mode keeps fp32
+activations and computes every conv product as ``xh*wh + xh*wl + xl*wh`` on the
+bf16 MFMA (~16 significant bits per product, fp32 accumulation).  These gates
+are relative-L2 bounds two orders of magnitude below what the bf16 mode
+reaches (bf16: ~3e-3), plus end-to-end kept-set parity of both pipelines
+against the fp32 PyTorch modules followed by the CPU reference postprocess.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from triton_client_amd.ops.conv import NHWC, FusedConv, maxpool_nhwc, upsample2x_nhwc
+
+pytestmark = pytest.mark.gpu
+
+ACTS = {0: lambda t: t, 1: torch.relu, 2: F.silu}
+# fp32 mode: per-output relative L2 error bound (measured ~1e-6..1e-5; bf16 mode ~3e-3)
+REL_L2_FP32 = 5e-5
+
+
+def rel_l2(got: torch.Tensor, ref: torch.Tensor) -> float:
+    got, ref = got.double(), ref.double()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+def _conv_case(cuda, cin, cout, k, s, act, tile, transpose=False, post=False, res_on=True, seed=0):
+    torch.manual_seed(seed)
+    B, H, W = 2, 23, 31
+    if transpose:
+        conv = nn.ConvTranspose2d(cin, cout, k, stride=k, bias=True).double()
+    else:
+        conv = nn.Conv2d(cin, cout, k, s, k // 2, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=act, device=cuda, precision="fp32", post_res=post)
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    xin = buf[..., 8:8 + cin]
+    if transpose:
+        Ho, Wo = H * k, W * k
+    else:
+        Ho, Wo = (H + 2 * (k // 2) - k) // s + 1, (W + 2 * (k // 2) - k) // s + 1
+    n_out = fc.out_channels()
+    res = torch.randn(B, Ho, Wo, n_out + 8, dtype=torch.float64) if res_on else None
+    out = torch.zeros(B, Ho, Wo, n_out + 16, dtype=torch.float32, device=cuda)
+    fc(NHWC(buf.float().to(cuda), 8, cin), out=NHWC(out, 8, n_out),
+       res=NHWC(res.float().to(cuda), 8, n_out) if res_on else None, tile=tile)
+    torch.cuda.synchronize()
+    x64 = xin.permute(0, 3, 1, 2)
+    y = conv(x64)
+    r64 = res[..., 8:8 + cout].permute(0, 3, 1, 2) if res_on else 0.0
+    ref = ACTS[act](y + r64) if post else ACTS[act](y) + r64
+    got = out[..., 8:8 + cout].permute(0, 3, 1, 2).cpu()
+    assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + n_out:].abs().sum().item() == 0
+    return rel_l2(got, ref)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 5, 6])
+def test_conv_x3_v1_tiles(cuda, tile):
+    """register-staged x3 kernel: Cin % 32 != 0, N / M tails, residual."""
+    for i, (cin, cout, k, s, act) in enumerate(((16, 16, 3, 1, 2), (24, 40, 3, 2, 1), (16, 72, 1, 1, 0),
+                                                (8, 16, 6, 2, 2))):
+        e = _conv_case(cuda, cin, cout, k, s, act, tile, seed=tile * 10 + i)
+        assert e < REL_L2_FP32, (cin, cout, k, s, e)
+
+
+@pytest.mark.parametrize("tile", [20, 22, 24, 25, 26, 27])
+def test_conv_x3_glds_tiles(cuda, tile):
+    """global_load_lds x3 kernel (Cin % 32 == 0): strides, slices, residual, tails."""
+    for i, (cin, cout, k, s, act) in enumerate(((64, 64, 3, 1, 1), (128, 72, 3, 2, 2), (32, 256, 1, 1, 0),
+                                                (96, 128, 3, 1, 1))):
+        e = _conv_case(cuda, cin, cout, k, s, act, tile, seed=tile * 10 + i)
+        assert e < REL_L2_FP32, (cin, cout, k, s, e)
+    e = _conv_case(cuda, 128, 64, 2, 2, 1, tile, transpose=True, res_on=False, seed=tile)
+    assert e < REL_L2_FP32, e
+
+
+@pytest.mark.parametrize("cin,cout,s", [(16, 16, 1), (16, 32, 2), (32, 32, 1), (16, 32, 1), (16, 16, 2), (32, 16, 1)])
+def test_conv_x3_small_halo(cuda, cin, cout, s):
+    for post in (False, True):
+        e = _conv_case(cuda, cin, cout, 3, s, 2, 60, post=post, seed=cin + cout + s)
+        assert e < REL_L2_FP32, (post, e)
+
+
+def test_conv_x3_auto_and_bf16_gap(cuda):
+    """auto tile selection over the detectors' shapes; the same layer in bf16
+    mode is two orders of magnitude less accurate (the gate discriminates)."""
+    for cin, cout, k, s in ((16, 32, 3, 2), (32, 16, 1, 1), (64, 64, 3, 2), (256, 128, 3, 1), (384, 72, 1, 1)):
+        assert _conv_case(cuda, cin, cout, k, s, 1, 0) < REL_L2_FP32
+    torch.manual_seed(3)
+    conv = nn.Conv2d(64, 64, 3, 1, 1)
+    x = torch.randn(2, 19, 21, 64)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), conv.weight.double(), conv.bias.double(), padding=1)
+    e32 = rel_l2(FusedConv(conv, device=cuda, precision="fp32")(NHWC(x.to(cuda))).nchw().cpu(), ref)
+    e16 = rel_l2(FusedConv(conv, device=cuda, precision="bf16")(NHWC(x.to(cuda, torch.bfloat16))).nchw().float().cpu(),
+                 ref)
+    assert e32 < REL_L2_FP32 and e16 > 20 * e32, (e32, e16)
+
+
+def test_conv_x3_rejects_bf16_buffers(cuda):
+    fc = FusedConv(nn.Conv2d(32, 32, 1), device=cuda, precision="fp32")
+    with pytest.raises(TypeError):
+        fc(NHWC(torch.zeros(1, 4, 4, 32, device=cuda, dtype=torch.bfloat16)))
+
+
+def test_nhwc_ops_fp32(cuda):
+    torch.manual_seed(4)
+    x = torch.randn(2, 13, 11, 40)
+    out = torch.zeros(2, 13, 11, 48, device=cuda)
+    maxpool_nhwc(NHWC(x.to(cuda), 8, 32), NHWC(out, 4, 32), 5)
+    ref = F.max_pool2d(x[..., 8:40].permute(0, 3, 1, 2), 5, 1, 2).permute(0, 2, 3, 1)
+    assert torch.equal(out[..., 4:36].cpu(), ref)
+    up = torch.zeros(2, 26, 22, 36, device=cuda)
+    upsample2x_nhwc(NHWC(x.to(cuda), 4, 32), NHWC(up, 4, 32))
+    ref = F.interpolate(x[..., 4:36].permute(0, 3, 1, 2), scale_factor=2.0).permute(0, 2, 3, 1)
+    assert torch.equal(up[..., 4:36].cpu(), ref)
+
+
+def test_preprocess_s2d_fp32(cuda):
+    from triton_client_amd.ops.image import preprocess, space_to_depth2
+    from triton_client_amd.ops.golden import preprocess_image
+    from triton_client_amd.utils.synthetic import camera_frame
+
+    frames = np.stack([camera_frame(360, 640, s) for s in (0, 1)])
+    out = torch.zeros(2, 320, 320, 16, device=cuda)
+    preprocess(torch.from_numpy(frames).to(cuda), (640, 640), "letterbox", "COCO", torch.float32, "S2D", out=out)
+    torch.cuda.synchronize()
+    ref = np.stack([preprocess_image(f, (640, 640), "letterbox", layout="NHWC") for f in frames])
+    ref = space_to_depth2(torch.from_numpy(ref))
+    assert (out.cpu() - ref).abs().max().item() <= 1.0 / 255 + 1e-6  # one u8 LSB at most (bilinear rounding)
+    assert (out.cpu() - ref).abs().mean().item() < 1e-4
+
+
+def test_fused_neck_x3_vs_unfused(cuda):
+    """fp32 fused deconv + head (streamed split head weights) == the fp32 module."""
+    from triton_client_amd.models.fast import FastBEV
+    from test_fast_plans import _small_pp
+
+    pm = _small_pp()
+    nx, ny, _ = pm.cfg.voxel.grid_size
+    canvas = torch.zeros(2, ny, nx, 64)
+    canvas[:, ::3, ::2] = torch.rand(2, (ny + 2) // 3, (nx + 1) // 2, 64)
+    with torch.no_grad():
+        ref = copy.deepcopy(pm).double().bev_forward(canvas.double().permute(0, 3, 1, 2))
+    fb = FastBEV(pm, 2, device=cuda, precision="fp32")
+    assert fb.neck is not None
+    outs = fb.forward(NHWC(canvas.to(cuda)))
+    torch.cuda.synchronize()
+    for r, o in zip(ref, outs):
+        assert rel_l2(o.nchw().cpu(), r) < 2e-4
+
+
+def test_fast_yolo_fp32_vs_module(cuda):
+    from triton_client_amd.models.fast import FastYOLOv5
+    from test_fast_plans import _yolo
+
+    m = _yolo(128)
+    x = torch.rand(2, 3, 128, 128)
+    with torch.no_grad():
+        ref = copy.deepcopy(m).double()(x.double())
+    f = FastYOLOv5(m, 2, (128, 128), device=cuda, precision="fp32")
+    f.set_input(x.to(cuda))
+    outs = f.forward()
+    torch.cuda.synchronize()
+    for r, o in zip(ref, outs):
+        assert rel_l2(o.nchw().cpu(), r) < 2e-4
+
+
+# ------------------------------------------------------------------ end to end
+# A kept box "matches" a reference box of the same class if IoU > 0.99 or, for the
+# near-degenerate boxes random-init heads produce (heights of 1e-3 px, where
+# IoU is ill-conditioned), every coordinate agrees within 0.05 px / 0.02 m.
+# Counts are aggregated over the batch: a candidate whose score sits within
+# ~1e-6 of a threshold may legitimately flip, so the gates are fractions of
+# all kept boxes (>= 99% matched, totals within 1%).
+def _match_2d(ref, got, b, iou_min=0.99, tol=0.05):
+    from triton_client_amd.ops.golden import box_iou_np
+    n_r, n_g = int(ref.count[b]), int(got.count[b])
+    if n_r == 0 or n_g == 0:
+        return 0, n_r, n_g
+    rb, gb = np.asarray(ref.box[b, :n_r]), got.box[b, :n_g].cpu().numpy()
+    rc, gc = np.asarray(ref.cls[b, :n_r]), got.cls[b, :n_g].cpu().numpy()
+    same = rc[:, None] == gc[None, :]
+    iou = np.nan_to_num(box_iou_np(rb, gb)) * same
+    close = (np.abs(rb[:, None, :] - gb[None, :, :]).max(-1) < tol) & same
+    return int(((iou > iou_min) | close).any(1).sum()), n_r, n_g
+
+
+def _camera_parity(cuda, precision, B=4, iou_min=0.99, tol=0.05):
+    from triton_client_amd.ops.golden import preprocess_image
+    from triton_client_amd.pipelines import CameraPipeline
+    from triton_client_amd.utils.synthetic import camera_frame
+
+    cam = CameraPipeline(batch=B, src_hw=(360, 640), device=cuda, precision=precision)
+    frames = [camera_frame(360, 640, 10 + b) for b in range(B)]
+    for b in range(B):
+        cam.frames[b].copy_(torch.from_numpy(frames[b]))
+    cam.calibrate_detection_density(100.0)
+    got = cam.step()
+    torch.cuda.synchronize()
+    # reference: CPU golden letterbox -> fp32 PyTorch module -> CPU reference postprocess
+    x = torch.from_numpy(np.stack([preprocess_image(f, (640, 640), "letterbox") for f in frames]))
+    model = copy.deepcopy(cam.model).float().to(memory_format=torch.contiguous_format)
+    with torch.no_grad():
+        heads = model(x.to(cuda))
+    ref = cam.post.cpu([h.float().cpu() for h in heads], cam.xform)
+    return [_match_2d(ref, got, b, iou_min, tol) for b in range(B)]
+
+
+def _lidar_parity(cuda, precision, B=2, iou_min=0.99, tol=0.02):
+    from triton_client_amd.models.pointpillars import pillar_point_features, scatter_to_bev
+    from triton_client_amd.ops.lidar import AnchorPostprocess, PointLayout, Voxelizer, pc2_unpack
+    from triton_client_amd.ops.golden import rotated_iou_bev
+    from triton_client_amd.pipelines import LidarPipeline
+    from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    lid = LidarPipeline(batch=B, max_points=32768, device=cuda, precision=precision)
+    clouds = [lidar_sweep(spec, 20 + b) for b in range(B)]
+    for b, c in enumerate(clouds):
+        raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+        lid.data[b * lid.frame_bytes: b * lid.frame_bytes + raw.numel()].copy_(raw)
+        lid.frame_n[b] = c.shape[0]
+    lid.calibrate_detection_density(1000.0)
+    got = lid.step()
+    torch.cuda.synchronize()
+    # reference: CPU unpack + CPU voxeliser (spconv order) -> fp32 PyTorch PointPillars -> CPU postprocess
+    data, off, n = lid.data.cpu(), lid.frame_off.cpu(), lid.frame_n.cpu()
+    pts, cnt = pc2_unpack(None, data, off, n, PointLayout.xyzi_f32(), lid.max_points, True, 1.5)
+    vox = Voxelizer(lid.cfg.voxel, B, lid.max_points, device="cpu")
+    v, c, npts, vc = vox(pts, cnt)
+    model = copy.deepcopy(lid.model).float().to(memory_format=torch.contiguous_format)
+    nx, ny, _ = lid.cfg.voxel.grid_size
+    canvases = []
+    with torch.no_grad():
+        for b in range(B):
+            k = int(vc[b])
+            co = c[b, :k].clone()
+            co[:, 0] = 0
+            feats = pillar_point_features(v[b, :k].to(cuda), npts[b, :k].to(cuda).long(), co.to(cuda), lid.cfg.voxel)
+            canvases.append(scatter_to_bev(model.vfe(feats), co.to(cuda), 1, ny, nx, channels_last=False))
+        cls, box, dr = model.bev_forward(torch.cat(canvases))
+    ref = AnchorPostprocess(lid.cfg, B, device="cpu").cpu(cls.float().cpu(), box.float().cpu(), dr.float().cpu())
+    stats = []
+    for b in range(B):
+        n_r, n_g = int(ref.count[b]), int(got.count[b])
+        rb, gb = np.asarray(ref.box[b, :n_r]), got.box[b, :n_g].cpu().numpy()
+        rc, gc = np.asarray(ref.cls[b, :n_r]), got.cls[b, :n_g].cpu().numpy()
+        ok = 0
+        for i in range(n_r):
+            same = np.nonzero(gc == rc[i])[0]
+            if len(same) == 0:
+                continue
+            j = same[np.argmin(np.linalg.norm(gb[same, :3] - rb[i, :3], axis=1))]
+            dyaw = abs((gb[j, 6] - rb[i, 6] + np.pi) % (2 * np.pi) - np.pi)
+            close = np.abs(gb[j, :6] - rb[i, :6]).max() < tol and dyaw < tol / 2
+            ok += bool(close or rotated_iou_bev(rb[i], gb[j][None])[0] > iou_min)
+        stats.append((ok, n_r, n_g))
+    return stats
+
+
+def _totals(stats):
+    ok, n_r, n_g = (sum(s[i] for s in stats) for i in range(3))
+    return ok / max(n_r, 1), n_r, n_g
+
+
+@pytest.mark.parametrize("branch", ["camera", "lidar"])
+def test_pipeline_fp32_detection_parity(cuda, branch):
+    """fp32 mode vs the fp32 modules + CPU reference post: >= 99% of the kept
+    boxes matched, kept totals within 1%."""
+    stats = (_camera_parity if branch == "camera" else _lidar_parity)(cuda, "fp32")
+    frac, n_r, n_g = _totals(stats)
+    print(branch, "fp32", stats, f"matched {frac:.4f}")
+    assert all(s[1] > 10 for s in stats), stats
+    assert frac >= 0.99 and abs(n_r - n_g) <= max(1, n_r // 100), stats
+
+
+@pytest.mark.parametrize("branch", ["camera", "lidar"])
+def test_pipeline_bf16_detection_parity(cuda, branch):
+    """bf16 mode (secondary, labelled bf16 in the bench) is NOT detection-equivalent
+    to the fp32 model on these random-init detectors (MI355X: 32% of camera
+    boxes within 0.05 px; at IoU > 0.5 same class, 73% of camera and 55% of
+    LiDAR boxes).  This is a regression guard at those measured levels, not an
+    equivalence claim (docs/precision.md)."""
+    floor = {"camera": 0.6, "lidar": 0.45}[branch]
+    fn = _camera_parity if branch == "camera" else _lidar_parity
+    frac, n_r, n_g = _totals(fn(cuda, "bf16", iou_min=0.5, tol=0.0))
+    print(branch, "bf16 @IoU0.5", f"matched {frac:.4f}", n_r, n_g)
+    assert frac >= floor and abs(n_r - n_g) <= max(3, n_r // 5), (frac, n_r, n_g)

@@ -39,10 +39,11 @@ _KERNEL_SIGS = {
     "tca_pc2_blocks_per_frame": [I],
     "tca_vox_blocks_per_frame": [I],
     "tca_voxelize": [P, I, I, P, I, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P],
-    "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
-    "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, P],
-    "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, P],
+    "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
+    "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
+    "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, I, P],
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
+    "tca_conv_nhwc_x3": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_zero_i32": [P, I, P],
     "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
     "tca_anchor_decode_filter_keyed": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, P, P, P, P, P, P, I,
@@ -51,16 +52,17 @@ _KERNEL_SIGS = {
     "tca_pfn2_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
     "tca_pfn2_voxels": [P, I, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
     "tca_centerhead_decode": [P, I, I, I, I, I, I, P, P, I, F, P, P, I, P, P, P, P, P, P, I, P],
-    "tca_maxpool2d_nhwc": [P, I, I, I, I, I, I, I, I, I, P, I, I, I, I, P],
+    "tca_maxpool2d_nhwc": [P, I, I, I, I, I, I, I, I, I, P, I, I, I, I, I, P],
     "tca_retina_decode": [P, P, I, I, I, I, I, I, I, I, I, P, F, F, F, F, I, I, P, P, P, P, P, I, I, P],
     "tca_fcos_decode": [P, P, P, I, I, I, I, I, I, I, I, I, F, F, F, I, I, P, P, P, P, P, I, I, P],
     "tca_segment_merge": [P, P, P, P, I, I, P, P, I, I, I, P, P, P, P, P, I, P],
     "tca_group_norm_nhwc": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, P],
     "tca_yolov4_decode": [P, P, P, I, I, I, P, P, P, F, F, I, I, P, P, P, P, P, P, P, I, P],
-    "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, P],
-    "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, P],
+    "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, I, P],
+    "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, I, P],
     "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, P],
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
+    "tca_bev_neck_head_x3": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     # SECOND-IoU: sparse 3D backbone + RoI head (spconv.hip)
     "tca_sp_offsets": [P, I, P, P, P],
     "tca_sp_vfe_slots": [P, I, I, P, P, I, P, P, I, I, P, P, P, P, P, P],

@@ -81,10 +81,11 @@ class LocalDetector2D(Detector2D):
     def __init__(self, variant: str = "n", nc: int = 80, img: int = 640, batch: int = 1, letterbox: bool = True,
                  conf_thres: float = 0.3, iou_thres: float = 0.45, max_det: int = 300, device="auto",
                  graph: bool = True, weights: Optional[str] = None, calibrate_target: Optional[float] = 100.0,
-                 seed: int = 0, names: Optional[Sequence[str]] = None):
+                 seed: int = 0, names: Optional[Sequence[str]] = None, precision: str = "fp32"):
         from ..models.yolov5 import build_yolov5
 
         self.device = _device(device)
+        self.precision = precision
         self.B, self.img = batch, (img, img) if isinstance(img, int) else tuple(img)
         self.mode = "letterbox" if letterbox else "stretch"
         self.conf_thres, self.iou_thres, self.max_det = conf_thres, iou_thres, max_det
@@ -105,7 +106,7 @@ class LocalDetector2D(Detector2D):
 
         p = CameraPipeline(self.model, batch=self.B, src_hw=hw, img_hw=self.img, mode=self.mode,
                            conf_thres=self.conf_thres, iou_thres=self.iou_thres, max_det=self.max_det,
-                           device=self.device, dtype=torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+                           device=self.device, precision=self.precision)
         if self.calibrate_target is not None:  # random-init weights: set the head prior once
             p.frames.copy_(torch.from_numpy(np.array(sample, np.uint8)).to(p.frames.device).expand_as(p.frames))
             p.calibrate_detection_density(self.calibrate_target)

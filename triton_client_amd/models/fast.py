@@ -1,6 +1,8 @@
 """Concat-free NHWC execution plans of the detectors on the fused MFMA conv.
 
-Every activation is an NHWC bf16 buffer allocated once per batch size (so a
+Every activation is an NHWC buffer (fp32 in the ``precision="fp32"`` mode:
+split-product MFMA convs, the reference's serving precision; bf16 in the
+``"bf16"`` mode) allocated once per batch size (so a
 whole forward is hipGraph-capturable with stable addresses); a layer whose
 output feeds a concatenation writes straight into its channel slice of the
 concat buffer (C3's two branches, SPPF's pyramid, PANet's skip joins, the BEV
@@ -22,20 +24,21 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from ..ops.conv import NHWC, FusedConv, maxpool_nhwc, upsample2x_nhwc
+from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, upsample2x_nhwc
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 
-def _fc(m: ConvBNAct, device, **kw) -> FusedConv:
+def _fc(m: ConvBNAct, device, precision: str = "bf16", **kw) -> FusedConv:
     assert m.fused, "call fuse_model() first"
-    return FusedConv(m.conv, act=m.act, device=device, **kw)
+    return FusedConv(m.conv, act=m.act, device=device, precision=precision, **kw)
 
 
 class _Buffers:
-    def __init__(self, device, dtype=None):
+    def __init__(self, device, precision: str = "bf16"):
         self.device = torch.device(device)
-        # bf16 on the GPU; fp32 on the CPU reference path (exact comparisons in tests)
-        self.dtype = dtype or (torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.precision = precision
+        # the precision's activation dtype on the GPU; fp32 on the CPU reference path
+        self.dtype = act_dtype(precision) if self.device.type == "cuda" else torch.float32
         self.bufs = []
 
     def new(self, B, H, W, C) -> NHWC:
@@ -51,8 +54,9 @@ class _C3Plan:
     """C3: cv3(cat(m(cv1(x)), cv2(x))) with the cat buffer written in place."""
 
     def __init__(self, c3, B, H, W, bufs: _Buffers, device):
-        self.cv1, self.cv2, self.cv3 = _fc(c3.cv1, device), _fc(c3.cv2, device), _fc(c3.cv3, device)
-        self.m = [(_fc(b.cv1, device), _fc(b.cv2, device), b.add) for b in c3.m]
+        pr = bufs.precision
+        self.cv1, self.cv2, self.cv3 = _fc(c3.cv1, device, pr), _fc(c3.cv2, device, pr), _fc(c3.cv3, device, pr)
+        self.m = [(_fc(b.cv1, device, pr), _fc(b.cv2, device, pr), b.add) for b in c3.m]
         c_ = self.cv1.N
         self.c_ = c_
         self.cat = bufs.new(B, H, W, 2 * c_)
@@ -81,11 +85,13 @@ class FastYOLOv5:
     instead of 3 of 8, half the input bytes, half the stem's MACs."""
     IN_CHANNELS = 8
 
-    def __init__(self, model, batch: int, img_hw: Tuple[int, int] = (640, 640), device="cuda", s2d: bool = True):
+    def __init__(self, model, batch: int, img_hw: Tuple[int, int] = (640, 640), device="cuda", s2d: bool = True,
+                 precision: str = "bf16"):
         self.device = torch.device(device)
+        self.precision = pr = precision
         H, W = img_hw
         B = batch
-        bufs = self.bufs = _Buffers(self.device)
+        bufs = self.bufs = _Buffers(self.device, precision)
         m = model
         self.s2d = s2d and H % 2 == 0 and W % 2 == 0 and m.b0.conv.kernel_size == (6, 6) \
             and m.b0.conv.stride == (2, 2) and m.b0.conv.padding == (2, 2)
@@ -99,11 +105,11 @@ class FastYOLOv5:
                 stem.weight.copy_(s2d_stem_weight(c0.weight.detach().float()))
                 stem.bias.copy_(c0.bias.detach().float() if c0.bias is not None else torch.zeros(c0.out_channels))
             self.x = bufs.new(B, H // 2, W // 2, 16)
-            self.b0 = FusedConv(stem, act=m.b0.act, device=device)
+            self.b0 = FusedConv(stem, act=m.b0.act, device=device, precision=pr)
         else:
             self.x = bufs.new(B, H, W, self.IN_CHANNELS)
-            self.b0 = _fc(m.b0, device, cin_pad=self.IN_CHANNELS)
-        self.b1, self.b3, self.b5, self.b7 = (_fc(getattr(m, n), device) for n in ("b1", "b3", "b5", "b7"))
+            self.b0 = _fc(m.b0, device, pr, cin_pad=self.IN_CHANNELS)
+        self.b1, self.b3, self.b5, self.b7 = (_fc(getattr(m, n), device, pr) for n in ("b1", "b3", "b5", "b7"))
         h2, w2 = H // 2, W // 2
         s4, s8, s16, s32 = (H // 4, W // 4), (H // 8, W // 8), (H // 16, W // 16), (H // 32, W // 32)
         self.t0 = bufs.new(B, h2, w2, self.b0.N)
@@ -113,26 +119,26 @@ class FastYOLOv5:
         self.t3 = bufs.new(B, *s8, self.b3.N)
         self.c3_4 = _C3Plan(m.b4, B, *s8, bufs, device)
         c_p3 = self.c3_4.out_c
-        self.h14 = _fc(m.h14, device)
+        self.h14 = _fc(m.h14, device, pr)
         self.cat17 = bufs.new(B, *s8, self.h14.N + c_p3)  # [up(h14) | p3]
         self.p3 = NHWC(self.cat17.t, self.h14.N, c_p3)
         self.t5 = bufs.new(B, *s16, self.b5.N)
         self.c3_6 = _C3Plan(m.b6, B, *s16, bufs, device)
         c_p4 = self.c3_6.out_c
-        self.h10 = _fc(m.h10, device)
+        self.h10 = _fc(m.h10, device, pr)
         self.cat13 = bufs.new(B, *s16, self.h10.N + c_p4)  # [up(h10) | p4]
         self.p4 = NHWC(self.cat13.t, self.h10.N, c_p4)
         self.t7 = bufs.new(B, *s32, self.b7.N)
         self.c3_8 = _C3Plan(m.b8, B, *s32, bufs, device)
         self.t8 = bufs.new(B, *s32, self.c3_8.out_c)
         # SPPF
-        self.sp1, self.sp2 = _fc(m.b9.cv1, device), _fc(m.b9.cv2, device)
+        self.sp1, self.sp2 = _fc(m.b9.cv1, device, pr), _fc(m.b9.cv2, device, pr)
         cs = self.sp1.N
         self.spcat = bufs.new(B, *s32, 4 * cs)
         self.t9 = bufs.new(B, *s32, self.sp2.N)
         self.k = m.b9.k
         # head
-        self.h18, self.h21 = _fc(m.h18, device), _fc(m.h21, device)
+        self.h18, self.h21 = _fc(m.h18, device, pr), _fc(m.h21, device, pr)
         self.cat23 = bufs.new(B, *s32, self.h21.N + self.h10.N)  # [h21 | h10]
         self.h10_out = NHWC(self.cat23.t, self.h21.N, self.h10.N)
         self.c3_13 = _C3Plan(m.h13, B, *s16, bufs, device)
@@ -145,7 +151,7 @@ class FastYOLOv5:
         self.o4 = bufs.new(B, *s16, self.c3_20.out_c)
         self.c3_23 = _C3Plan(m.h23, B, *s32, bufs, device)
         self.o5 = bufs.new(B, *s32, self.c3_23.out_c)
-        self.det = [FusedConv(c, act=ACT_NONE, device=device) for c in m.detect]
+        self.det = [FusedConv(c, act=ACT_NONE, device=device, precision=pr) for c in m.detect]
         self.dout = [bufs.new(B, *s, d.N) for s, d in zip((s8, s16, s32), self.det)]
         self.no_real = m.detect[0].out_channels
 
@@ -207,8 +213,9 @@ class _BEVBackbonePlan:
     def __init__(self, bb, B: int, ny: int, nx: int, bufs: _Buffers, device):
         self.blocks = []
         H, W = ny, nx
+        pr = bufs.precision
         for blk in bb.blocks:
-            convs = [_fc(c, device) for c in blk]
+            convs = [_fc(c, device, pr) for c in blk]
             s = convs[0].s
             H, W = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
             pp = [bufs.new(B, H, W, convs[0].N), bufs.new(B, H, W, convs[0].N)]
@@ -226,7 +233,7 @@ class _BEVBackbonePlan:
         off = 0
         for u, c in zip(bb.deblocks, up_c):
             assert u.fused, "call fuse_model() first"
-            self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device), off, c))
+            self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device, precision=pr), off, c))
             off += c
 
     def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
@@ -251,17 +258,18 @@ class FastBEV:
     """PointPillars BEV backbone + anchor head on fused convs."""
 
     def __init__(self, model, batch: int, device="cuda", fused_neck: bool = True,
-                 bev_hw: Optional[Tuple[int, int]] = None):
+                 bev_hw: Optional[Tuple[int, int]] = None, precision: str = "bf16"):
         """bev_hw: (ny, nx) of the backbone input when it is not the voxel grid
         (SECOND: the 8x-downsampled HeightCompression map)."""
         self.device = torch.device(device)
+        self.precision = precision
         cfg = model.cfg
         if bev_hw is not None:
             ny, nx = bev_hw
         else:
             nx, ny, _ = cfg.voxel.grid_size
         B = batch
-        bufs = self.bufs = _Buffers(self.device)
+        bufs = self.bufs = _Buffers(self.device, precision)
         self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)
         self.blocks, self.ups, self.cat, self.out_hw = self.bb.blocks, self.bb.ups, self.bb.cat, self.bb.out_hw
         H0, W0 = self.out_hw
@@ -271,7 +279,7 @@ class FastBEV:
         with torch.no_grad():
             merged.weight.copy_(torch.cat([hd.conv_cls.weight, hd.conv_box.weight, hd.conv_dir.weight]).float())
             merged.bias.copy_(torch.cat([hd.conv_cls.bias, hd.conv_box.bias, hd.conv_dir.bias]).float())
-        self.head = FusedConv(merged, act=ACT_NONE, device=device)
+        self.head = FusedConv(merged, act=ACT_NONE, device=device, precision=precision)
         self.n_cls, self.n_box, self.n_dir = (hd.conv_cls.out_channels, hd.conv_box.out_channels,
                                               hd.conv_dir.out_channels)
         self.hout = bufs.new(B, H0, W0, self.head.N)

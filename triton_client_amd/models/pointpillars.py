@@ -77,7 +77,7 @@ class PillarVFE(nn.Module):
 
     def forward(self, feats: torch.Tensor) -> torch.Tensor:  # [V, P, in] → [V, C]
         if self.fused_weight is not None:
-            x = feats @ self.fused_weight.t().to(feats.dtype) + self.fused_bias.to(feats.dtype)
+            x = feats @ self.fused_weight.t().to(feats) + self.fused_bias.to(feats)
         else:
             x = self.linear(feats)
             x = self.norm(x.permute(0, 2, 1)).permute(0, 2, 1)

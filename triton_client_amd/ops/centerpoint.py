@@ -50,7 +50,7 @@ class PFNEncoder:
 
     def clear_coords(self, coords: torch.Tensor, voxel_count: torch.Tensor, stream=None) -> None:
         _native.call("tca_pillar_canvas_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
-                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), _native.stream_ptr(stream))
+                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), 2, _native.stream_ptr(stream))
 
     def clear(self, vox: Voxelizer, stream=None) -> None:
         self.clear_coords(vox.coords, vox.voxel_count, stream)

@@ -1,11 +1,21 @@
-"""Fused NHWC bf16 convolution (``csrc/kernels/conv_mfma.hip``).
+"""Fused NHWC convolution (``csrc/kernels/conv_mfma.hip``), bf16 or fp32.
 
 :class:`FusedConv` packs a (BN-folded) ``Conv2d`` / ``ConvTranspose2d``
 (k == stride) into the kernel's GEMM layout once and runs
 ``act(conv(x) + bias) (+ residual)`` in one launch, reading and writing
 channel slices of wider NHWC buffers (:class:`NHWC`), so the detectors'
-concatenations are free.  CPU tensors take an fp32 PyTorch path with the
-same semantics (used for tests on the GPU-less host).
+concatenations are free.
+
+Precision (``precision=``):
+
+* ``"fp32"`` — fp32 activations; every product on the bf16 MFMA as three
+  split terms (``xh*wh + xh*wl + xl*wh``, fp32 accumulate, see
+  ``tca_conv_nhwc_x3``): the reference's fp32 serving precision
+  (``examples/YOLOv5/config.pbtxt:7,16``) at 3x the bf16 MFMA work.
+* ``"bf16"`` — bf16 activations and weights, fp32 accumulation.
+
+CPU tensors take an fp32 PyTorch path with the same semantics (used for tests
+on the GPU-less host).
 """
 from __future__ import annotations
 
@@ -46,15 +56,52 @@ def _ceil(x, m):
     return (x + m - 1) // m * m
 
 
+PRECISIONS = ("fp32", "bf16")
+
+
+def act_dtype(precision: str) -> torch.dtype:
+    """Activation dtype of a precision mode."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
+    return torch.float32 if precision == "fp32" else torch.bfloat16
+
+
+def split_bf16(w: torch.Tensor):
+    """fp32 -> (hi, lo) bf16 with hi = rne(w), lo = rne(w - hi)."""
+    w = w.float()
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    return hi, lo
+
+
+def split_pairs(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] fp32 (K % 8 == 0) -> [N, 2K] bf16: per 8 columns, 8 hi then 8 lo —
+    the split-weight layout of the fp32-mode kernels."""
+    N, K = w.shape
+    assert K % 8 == 0, K
+    hi, lo = split_bf16(w)
+    return torch.stack([hi.reshape(N, K // 8, 8), lo.reshape(N, K // 8, 8)], 2).reshape(N, 2 * K).contiguous()
+
+
+def nhwc_dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 2
+    raise TypeError(f"NHWC activations must be fp32 or bf16, got {t.dtype}")
+
+
 class FusedConv:
     def __init__(self, conv: nn.Module, act: int = ACT_NONE, device="cuda", cin_pad: Optional[int] = None,
-                 cout_pad: Optional[int] = None, post_res: bool = False):
+                 cout_pad: Optional[int] = None, post_res: bool = False, precision: str = "bf16"):
         w = conv.weight.detach().float()
         b = conv.bias.detach().float() if conv.bias is not None else None
         self.transpose = isinstance(conv, nn.ConvTranspose2d)
         self.device = torch.device(device)
         self.act = act
         self.post_res = post_res  # act(conv + residual): ResNet bottleneck output
+        self.precision = precision
+        self.dtype = act_dtype(precision)
         if self.transpose:
             cin, cout, kh, kw = w.shape
             s = conv.stride[0]
@@ -92,7 +139,11 @@ class FusedConv:
         self.bias = torch.zeros(self.N)
         if bias is not None:
             self.bias[:N] = bias
-        self.w_gemm = W.to(self.device, torch.bfloat16).contiguous()
+        self.w_f32_gemm = W  # [N, Kp] fp32 (host): the fused neck re-packs from it
+        if precision == "fp32":
+            self.w_gemm = split_pairs(W).to(self.device)  # [N, 2*Kp] bf16 hi/lo
+        else:
+            self.w_gemm = W.to(self.device, torch.bfloat16).contiguous()
         self.b_gemm = self.bias.to(self.device).contiguous()
         # fp32 copies for the CPU path
         self.w_f32, self.b_f32 = w, b
@@ -110,12 +161,16 @@ class FusedConv:
         B, H, W, C = x.shape
         Ho, Wo = self.out_hw(H, W)
         if out is None:
-            out = NHWC(torch.empty((B, Ho, Wo, self.out_channels()), dtype=torch.bfloat16, device=x.t.device))
+            out = NHWC(torch.empty((B, Ho, Wo, self.out_channels()), dtype=self.dtype, device=x.t.device))
         if x.t.device.type != "cuda":
             return self._cpu(x, out, res)
         assert C == self.cin_p, (C, self.cin_p)
+        for t in (x.t, out.t) + ((res.t,) if res is not None else ()):
+            if t.dtype != self.dtype:
+                raise TypeError(f"{self.precision} conv needs {self.dtype} activations, got {t.dtype}")
         gh, gw = (H, W) if self.transpose else (Ho, Wo)
-        _native.call("tca_conv_nhwc", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+        fn = "tca_conv_nhwc_x3" if self.precision == "fp32" else "tca_conv_nhwc"
+        _native.call(fn, _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                      _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
                      self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off,
                      self.act | (16 if (self.post_res and res is not None) else 0),
@@ -147,7 +202,7 @@ def maxpool_nhwc(x: NHWC, out: NHWC, k: int = 5, stream=None) -> NHWC:
         out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
         return out
     _native.call("tca_maxpool_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, k, _native.ptr(out.t),
-                 out.t.shape[-1], out.off, _native.stream_ptr(stream))
+                 out.t.shape[-1], out.off, nhwc_dtype_code(x.t), _native.stream_ptr(stream))
     return out
 
 
@@ -160,7 +215,7 @@ def maxpool2d_nhwc(x: NHWC, out: NHWC, k: int = 3, s: int = 2, p: int = 1, strea
         out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
         return out
     _native.call("tca_maxpool2d_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, k, s, p,
-                 _native.ptr(out.t), Ho, Wo, out.t.shape[-1], out.off, _native.stream_ptr(stream))
+                 _native.ptr(out.t), Ho, Wo, out.t.shape[-1], out.off, nhwc_dtype_code(x.t), _native.stream_ptr(stream))
     return out
 
 
@@ -172,5 +227,5 @@ def upsample2x_nhwc(x: NHWC, out: NHWC, stream=None) -> NHWC:
         out.tensor().copy_(y.permute(0, 2, 3, 1).to(out.t.dtype))
         return out
     _native.call("tca_upsample2x_nhwc", _native.ptr(x.t), B, H, W, C, x.t.shape[-1], x.off, _native.ptr(out.t),
-                 out.t.shape[-1], out.off, _native.stream_ptr(stream))
+                 out.t.shape[-1], out.off, nhwc_dtype_code(x.t), _native.stream_ptr(stream))
     return out

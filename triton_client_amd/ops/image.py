@@ -66,7 +66,7 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
 
     layout "NCHW" → [B, C, H, W] contiguous; "NHWC" → [B, C, H, W] view of a
     channels_last buffer (C = out_channels, 3 or 4; the 4th channel is 0);
-    "S2D" → [B, H/2, W/2, 16] bf16 space-to-depth (see :func:`space_to_depth2`).
+    "S2D" → [B, H/2, W/2, 16] space-to-depth (bf16 or fp32, see :func:`space_to_depth2`).
     """
     if frames.dim() == 3:
         frames = frames.unsqueeze(0)
@@ -76,7 +76,7 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
     xf, (top, left, nh, nw) = frame_xform((h0, w0), (H, W), mode)
     if layout == "S2D":
         return _preprocess_s2d(frames, (H, W), mode, scale, bias, swap_rb, pad_value, quantize_u8, out, stream,
-                               xf, (top, left, nh, nw))
+                               xf, (top, left, nh, nw), dtype)
     if frames.device.type == "cuda":
         frames = frames.contiguous()
         if out is None:
@@ -129,17 +129,18 @@ def s2d_stem_weight(w: torch.Tensor) -> torch.Tensor:
     return torch.cat([v, v.new_zeros(co, 4, 3, 3)], 1)
 
 
-def _preprocess_s2d(frames, dst_hw, mode, scale, bias, swap_rb, pad_value, quantize_u8, out, stream, xf, region):
+def _preprocess_s2d(frames, dst_hw, mode, scale, bias, swap_rb, pad_value, quantize_u8, out, stream, xf, region,
+                    dtype=torch.bfloat16):
     B, h0, w0, c0 = frames.shape
     H, W = dst_hw
     top, left, nh, nw = region
     if out is None:
-        out = torch.zeros((B, H // 2, W // 2, 16), dtype=torch.bfloat16, device=frames.device)
+        out = torch.zeros((B, H // 2, W // 2, 16), dtype=dtype, device=frames.device)
     if frames.device.type == "cuda":
         frames = frames.contiguous()
         _native.call(
             "tca_image_preprocess", _native.ptr(frames), h0 * w0 * c0, h0, w0, w0 * c0, c0, int(swap_rb),
-            _native.ptr(out), DTYPE_CODE[torch.bfloat16], 2, 16, H, W, B, top, left, nh, nw, float(pad_value),
+            _native.ptr(out), DTYPE_CODE[out.dtype], 2, 16, H, W, B, top, left, nh, nw, float(pad_value),
             int(quantize_u8), float(scale[0]), float(scale[1]), float(scale[2]), float(bias[0]), float(bias[1]),
             float(bias[2]), _native.stream_ptr(stream))
         return out, xf

@@ -218,11 +218,15 @@ class Voxelizer:
 
 # ----------------------------------------------------------------------------- K8/K9
 class PillarEncoder:
-    """Fused PillarVFE (BN folded) + scatter into an NHWC bf16 BEV canvas."""
+    """Fused PillarVFE (BN folded) + scatter into an NHWC BEV canvas (bf16, or
+    fp32 for the fp32 precision mode)."""
 
     def __init__(self, cfg: VoxelConfig, weight: torch.Tensor, bias: torch.Tensor, batch: int, device="cuda",
-                 channels: int = 64):
+                 channels: int = 64, dtype: torch.dtype = torch.bfloat16):
         self.cfg, self.B, self.C = cfg, batch, channels
+        assert dtype in (torch.bfloat16, torch.float32), dtype
+        self.dtype = dtype
+        self._dt = 0 if dtype == torch.float32 else 2
         self.device = torch.device(device)
         self.W = weight.detach().float().contiguous().to(self.device)  # [64, 10]
         self.b = bias.detach().float().contiguous().to(self.device)
@@ -231,7 +235,7 @@ class PillarEncoder:
         if self.device.type == "cuda":
             self.ws = Workspace(self.device)
             # NHWC canvas, zero-initialised once; cleared per frame by cell list
-            self.canvas = self.ws.get("canvas", (batch, ny, nx, channels), torch.bfloat16, init=0)
+            self.canvas = self.ws.get("canvas", (batch, ny, nx, channels), dtype, init=0)
             self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
             self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
 
@@ -246,7 +250,8 @@ class PillarEncoder:
     def clear_coords(self, coords: torch.Tensor, voxel_count: torch.Tensor, stream=None) -> None:
         """coords [B, V, 4] (b, z, y, x), voxel_count [B]."""
         _native.call("tca_pillar_canvas_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
-                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), _native.stream_ptr(stream))
+                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), self._dt,
+                     _native.stream_ptr(stream))
 
     def encode_from_slots(self, points: torch.Tensor, vox: Voxelizer, feat_out: Optional[torch.Tensor] = None,
                           stream=None) -> torch.Tensor:
@@ -254,7 +259,7 @@ class PillarEncoder:
                      _native.ptr(vox.slots), _native.ptr(vox.vcount), _native.ptr(vox.coords),
                      _native.ptr(vox.voxel_count), self.B, self.cfg.max_voxels, self.cfg.max_points_per_voxel,
                      _native.ptr(self.W), _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny,
-                     _native.ptr(self.canvas), _native.ptr(feat_out), _native.stream_ptr(stream))
+                     _native.ptr(self.canvas), _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
         return self.canvas_nchw()
 
     def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
@@ -262,7 +267,7 @@ class PillarEncoder:
         _native.call("tca_pillar_vfe_voxels", _native.ptr(voxels), _native.ptr(num_points), _native.ptr(coords),
                      _native.ptr(voxel_count), voxels.shape[0], voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
                      _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas),
-                     _native.ptr(feat_out), _native.stream_ptr(stream))
+                     _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
         return self.canvas_nchw()
 
 

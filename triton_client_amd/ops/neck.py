@@ -15,7 +15,7 @@ from typing import List, Sequence
 import torch
 
 from .. import _native
-from .conv import NHWC, FusedConv
+from .conv import NHWC, FusedConv, split_pairs
 
 CB = 128
 NH_PAD = 80
@@ -47,7 +47,7 @@ def neck_head_supported(ups: Sequence[FusedConv], strides: Sequence[int], cins: 
         return False
     S = max(strides)
     for u, s, c in zip(ups, strides, cins):
-        if s < 1 or S % s or c % 64 or u.cout_real != CB or u.Kp != c:
+        if s < 1 or S % s or c % (32 if head.precision == "fp32" else 64) or u.cout_real != CB or u.Kp != c:
             return False
         if u.transpose and u.shuffle != s:
             return False
@@ -58,19 +58,28 @@ def neck_head_supported(ups: Sequence[FusedConv], strides: Sequence[int], cins: 
 
 
 class FusedNeckHead:
-    """out[b, y, x, :nh] = head(cat_i relu(deconv_i(x_i)))[b, y, x]."""
+    """out[b, y, x, :nh] = head(cat_i relu(deconv_i(x_i)))[b, y, x].
+
+    Precision follows the convs: bf16 (``tca_bev_neck_head``) or fp32 split
+    products (``tca_bev_neck_head_x3``, fp32 activations, split weights)."""
 
     def __init__(self, ups: Sequence[FusedConv], strides: Sequence[int], head: FusedConv, device,
                  grid: int = 0):
         self.ups, self.strides = list(ups), [int(s) for s in strides]
+        self.precision = head.precision
+        assert all(u.precision == self.precision for u in self.ups)
+        self.dtype = head.dtype
         self.nbr = len(self.ups)
         self.nh = head.N
         # persistent kernel: one workgroup per CU (a multiple of 8: tiles are split per XCD)
         if grid <= 0:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
-        wh = head.w_gemm.float().cpu()[:, : head.Kp]
-        self.wh = permute_head_weight(wh).to(device, torch.bfloat16).contiguous()
+        wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
+        if self.precision == "fp32":
+            self.wh = split_pairs(wh).to(device)
+        else:
+            self.wh = wh.to(device, torch.bfloat16).contiguous()
         bh = torch.zeros(NH_PAD)
         bh[: head.N] = head.b_gemm.float().cpu()
         self.bh = bh.to(device).contiguous()
@@ -85,11 +94,11 @@ class FusedNeckHead:
         B, H, W, _ = out.shape
         for x, s in zip(xs, self.strides):
             assert x.shape[0] == B and x.shape[1] * s == H and x.shape[2] * s == W, (x.shape, s, out.shape)
-        assert out.off == 0 and out.t.dtype == torch.bfloat16
+        assert out.off == 0 and out.t.dtype == self.dtype and all(x.t.dtype == self.dtype for x in xs)
         ptrs = (ctypes.c_void_p * n)(*[x.t.data_ptr() for x in xs])
         ldx = (ctypes.c_int * n)(*[x.t.shape[-1] for x in xs])
         offx = (ctypes.c_int * n)(*[x.off for x in xs])
-        _native.call("tca_bev_neck_head", n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
+        _native.call("tca_bev_neck_head_x3" if self.precision == "fp32" else "tca_bev_neck_head", n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
                      _native.ptr(self.wh), _native.ptr(self.bh), self.nh, _native.ptr(out.t), out.t.shape[-1],
                      B, H, W, self.grid, _native.stream_ptr(stream))
         return out

@@ -1,8 +1,12 @@
 """2D camera pipeline on one GPU: raw uint8 frames → detections.
 
-    frames u8 [B,H0,W0,3] ─K1→ NHWC bf16 [B,640,640,3] ─YOLOv5n (BN folded,
-    channels_last, bf16)→ 3 head maps ─K3 decode+filter→ candidates ─K4
+    frames u8 [B,H0,W0,3] ─K1→ NHWC [B,640,640,3] ─YOLOv5n (BN folded,
+    channels_last)→ 3 head maps ─K3 decode+filter→ candidates ─K4
     sort/NMS + letterbox undo→ boxes [B,300,4], scores, classes, counts
+
+``precision="fp32"`` (default, the reference's serving precision —
+``examples/YOLOv5/config.pbtxt:7,16`` TYPE_FP32): fp32 activations, split-
+product MFMA convs (``ops/conv.py``); ``"bf16"``: bf16 activations.
 
 Replaces the reference's per-frame CPU chain (``communicator/ros_inference.py:117-175``:
 cv2 decode/resize, ``image_adjust``, gRPC ``ModelInfer``, 500 ms struct-unpack
@@ -17,16 +21,19 @@ import torch
 
 from ..models.common import fuse_model, lsuv_rescale
 from ..models.yolov5 import YOLOv5, build_yolov5
+from ..ops.conv import act_dtype
 from ..ops.image import frame_xform, preprocess
 from ..ops.yolo import YoloPostprocess
 
 
 class CameraPipeline:
     def __init__(self, model: Optional[YOLOv5] = None, batch: int = 16, src_hw: Tuple[int, int] = (720, 1280),
-                 img_hw: Tuple[int, int] = (640, 640), mode: str = "letterbox", dtype: torch.dtype = torch.bfloat16,
+                 img_hw: Tuple[int, int] = (640, 640), mode: str = "letterbox", precision: str = "fp32",
                  conf_thres: float = 0.3, iou_thres: float = 0.45, max_det: int = 300, device="cuda",
                  variant: str = "n", nc: int = 80, seed: int = 0, swap_rb: bool = False, fast: bool = True):
         self.device = torch.device(device)
+        self.precision = precision
+        dtype = act_dtype(precision)
         self.B, self.src_hw, self.img_hw, self.mode, self.dtype = batch, tuple(src_hw), tuple(img_hw), mode, dtype
         self.swap_rb = swap_rb
         if model is None:
@@ -47,7 +54,7 @@ class CameraPipeline:
 
     def build_fast(self):
         from ..models.fast import FastYOLOv5
-        self.fast = FastYOLOv5(self.model, self.B, self.img_hw, self.device)
+        self.fast = FastYOLOv5(self.model, self.B, self.img_hw, self.device, precision=self.precision)
         return self.fast
 
     @torch.no_grad()
@@ -95,10 +102,10 @@ class CameraPipeline:
         if self.use_fast:
             f = self.fast or self.build_fast()
             if f.s2d:
-                preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "S2D",
+                preprocess(self.frames, self.img_hw, self.mode, "COCO", f.x.t.dtype, "S2D",
                            swap_rb=self.swap_rb, out=f.x.t)
             else:
-                preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", f.IN_CHANNELS,
+                preprocess(self.frames, self.img_hw, self.mode, "COCO", f.x.t.dtype, "NHWC", f.IN_CHANNELS,
                            swap_rb=self.swap_rb, out=f.x.t.permute(0, 3, 1, 2))
             return self.post(f.forward(), self.xform)
         preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", 3, swap_rb=self.swap_rb,

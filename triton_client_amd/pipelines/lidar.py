@@ -2,9 +2,13 @@
 
     PointCloud2 bytes ─K6 unpack (skip NaN, i/=max, z+=offset)→ points
     ─K7 voxelise (spconv order)→ sorted slot lists ─K8/K9 MFMA PillarVFE +
-    scatter→ NHWC bf16 BEV canvas ─BEV backbone + anchor head (bf16,
-    channels_last)→ cls/box/dir maps ─K11 decode/filter→ candidates ─K10
-    top-4096 + rotated-IoU NMS→ boxes [B,500,7], scores, labels, counts
+    scatter→ NHWC BEV canvas ─BEV backbone + anchor head (channels_last)→
+    cls/box/dir maps ─K11 decode/filter→ candidates ─K10 top-4096 +
+    rotated-IoU NMS→ boxes [B,500,7], scores, labels, counts
+
+``precision="fp32"`` (default; the reference serves PointPillars in fp32,
+``examples/pointpillar_kitti/config.pbtxt:33,54``): fp32 canvas and
+activations, split-product MFMA convs and fused neck; ``"bf16"``: bf16.
 
 The reference splits this across a client (``communicator/ros_inference3d.py:120-213``:
 138 ms Python ``read_points``, OpenPCDet/spconv CPU voxeliser, three
@@ -23,15 +27,18 @@ from ..config.lidar import PointPillarsConfig
 from ..models.common import fuse_model, lsuv_rescale
 from ..models.pointpillars import PointPillars, build_pointpillars
 from ..ops._ws import Workspace
+from ..ops.conv import act_dtype
 from ..ops.lidar import AnchorPostprocess, PillarEncoder, PointLayout, Voxelizer, pc2_unpack
 
 
 class LidarPipeline:
     def __init__(self, model: Optional[PointPillars] = None, batch: int = 16, max_points: int = 131072,
                  layout: Optional[PointLayout] = None, z_offset: float = 1.5, normalize_intensity: bool = True,
-                 dtype: torch.dtype = torch.bfloat16, device="cuda", cfg: Optional[PointPillarsConfig] = None,
+                 precision: str = "fp32", device="cuda", cfg: Optional[PointPillarsConfig] = None,
                  seed: int = 0, fast: bool = True):
         self.device = torch.device(device)
+        self.precision = precision
+        dtype = act_dtype(precision)
         self.B, self.max_points, self.dtype = batch, max_points, dtype
         self.layout = layout or PointLayout.xyzi_f32()
         self.z_offset, self.normalize = z_offset, normalize_intensity
@@ -49,14 +56,14 @@ class LidarPipeline:
         v = self.cfg.voxel
         self.vox = Voxelizer(v, batch, max_points, device=self.device, materialize=False)
         self.enc = PillarEncoder(v, model.vfe.fused_weight.float(), model.vfe.fused_bias.float(), batch,
-                                 device=self.device, channels=self.cfg.vfe_filters)
+                                 device=self.device, channels=self.cfg.vfe_filters, dtype=dtype)
         self.post = AnchorPostprocess(self.cfg, batch, device=self.device)
         self.use_fast = fast and self.device.type == "cuda"
         self.fast = None
 
     def build_fast(self):
         from ..models.fast import FastBEV
-        self.fast = FastBEV(self.model, self.B, self.device)
+        self.fast = FastBEV(self.model, self.B, self.device, precision=self.precision)
         return self.fast
 
     @torch.no_grad()

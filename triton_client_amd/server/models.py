@@ -74,7 +74,7 @@ class YoloV5Model(ServedModel):
                 self.pipe.frames[0].copy_(torch.from_numpy(camera_frame(self.img, self.img, self.seed)))
                 self.pipe.calibrate_detection_density(self.calibrate_target)
             self.model = self.pipe.model
-            self.x = torch.empty((1, self.img, self.img, 3), dtype=torch.bfloat16, device=self.device).permute(0, 3, 1, 2)
+            self.x = torch.empty((1, self.img, self.img, 3), dtype=self.pipe.dtype, device=self.device).permute(0, 3, 1, 2)
         else:
             from ..models.common import fuse_model
             self.model = fuse_model(model.eval())
