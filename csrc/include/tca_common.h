@@ -46,6 +46,21 @@ __device__ __forceinline__ float load_any(const void* p, long i, int dtype) {
   }
 }
 
+// 16-B global -> LDS DMA (global_load_lds_dwordx4) issued from inline asm, so
+// hipcc neither counts it nor inserts the conservative vmcnt(0) it places in
+// front of any ds_read that might alias an in-flight LDS DMA: the caller waits
+// with its own counted s_waitcnt vmcnt(N) and a barrier before reading the
+// destination (cdna_hip_programming.md §5.7 item 1).  l: the wave's LDS
+// destination base (wave-uniform); lane i writes l + 16 * i.
+__device__ __forceinline__ void glds16_asm(const void* g, const void* l) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);  // flat -> LDS offset (low 32 bits)
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Order-preserving float <-> uint mapping (for atomicMax on floats and for

@@ -1084,8 +1084,25 @@ __global__ void __launch_bounds__(256) conv_nhwc_x3_kernel(ConvArgs a) {
 // gfx950 b128 lane groups, rows at any 16-row fragment base).
 __device__ __forceinline__ int swz3(int row) { return (row ^ (row >> 3)) & 7; }
 
-template <int BM, int BN, int WM, int WN>
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_upto(int k) {  // vmcnt(k * N), k in [0, 3]
+  if (k >= 3) wait_vmcnt<3 * N>();
+  else if (k == 2) wait_vmcnt<2 * N>();
+  else if (k == 1) wait_vmcnt<N>();
+  else wait_vmcnt<0>();
+}
+
+// STAGES-deep LDS ring, one barrier per K step (the bf16 kernel's ONEBAR form):
+// iteration kt waits for its own stage with a counted vmcnt that leaves the
+// STAGES-2 younger stages in flight, passes one barrier (which also proves
+// every wave is done with stage kt-1), refills that buffer with K step
+// kt+STAGES-1 and runs stage kt's MFMAs.  With 3 MFMAs per fragment pair a
+// 32-deep K step is ~770 cycles of matrix work per SIMD, shorter than an HBM
+// round trip, so 2 stages (one step in flight) leave the MFMAs waiting on the
+// DMA; 3-4 stages hide it.
+template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) {
+  static_assert(STAGES >= 2 && STAGES <= 5, "stages");
   constexpr int NW = WM * WN;
   constexpr int BKC = 32, ROWB = 128;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -1094,7 +1111,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
   constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);
   constexpr int NL = A_INS + B_INS;
   constexpr int EPI = BM * (BN + 4) * 4;
-  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  constexpr int LDS = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1145,12 +1162,12 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
       const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
       const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
       const void* g = ok ? (const void*)(a.in_f + a_base[j] + toff) : (const void*)g_conv_zero_page;
-      glds16(g, sa + (wid * A_INS + j) * 1024);
+      glds16_asm(g, sa + (wid * A_INS + j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const void* g = b_ptr[j] ? (const void*)(b_ptr[j] + kt * BKC * 2) : (const void*)g_conv_zero_page;
-      glds16(g, sb + (wid * B_INS + j) * 1024);
+      glds16_asm(g, sb + (wid * B_INS + j) * 1024);
     }
   };
 
@@ -1169,20 +1186,25 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
       if (++kx == a.KW) { kx = 0; ++ky; }
     }
   };
-  issue(0, 0, ky, kx, ci0);
-  advance();
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nk) {
+      issue(st, st, ky, kx, ci0);
+      advance();
+    }
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      issue(kt + 1, cur ^ 1, ky, kx, ci0);
-      advance();
-      wait_vmcnt<NL>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    const int cur = kt % STAGES;
+    const int after = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    wait_vmcnt_upto<NL>(after);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    const int nx = kt + STAGES - 1;
+    if (nx < nk) {
+      issue(nx, nx % STAGES, ky, kx, ci0);
+      advance();
+    }
     const unsigned char* sa = smem + cur * STAGE;
     const unsigned char* sb = sa + A_BYTES;
     bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
@@ -1205,10 +1227,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
 #pragma unroll
       for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
     __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is restaged
-    asm volatile("" ::: "memory");
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the staging LDS
+  asm volatile("" ::: "memory");
   epilogue_f32<BM, BN, WM, WN>(a, acc, smem, m0, n0);
 }
 
@@ -1352,10 +1374,10 @@ int launch_small_halo_x3(const ConvArgs& a, hipStream_t stream) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGES = 2>
 int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  conv_glds_x3_kernel<BM, BN, WM, WN><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_glds_x3_kernel<BM, BN, WM, WN, STAGES><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -1477,6 +1499,26 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
     case 25: return launch_glds_x3<128, 128, 2, 4>(a, stream);
     case 26: return launch_glds_x3<256, 64, 4, 2>(a, stream);
     case 27: return launch_glds_x3<128, 256, 2, 4>(a, stream);
+    // deeper rings (3 / 4 stages)
+    case 30: return launch_glds_x3<128, 128, 4, 2, 3>(a, stream);
+    case 31: return launch_glds_x3<128, 128, 4, 2, 4>(a, stream);
+    case 32: return launch_glds_x3<128, 64, 4, 2, 3>(a, stream);
+    case 33: return launch_glds_x3<128, 64, 4, 2, 4>(a, stream);
+    case 34: return launch_glds_x3<64, 128, 2, 4, 4>(a, stream);
+    case 35: return launch_glds_x3<256, 64, 4, 2, 3>(a, stream);
+    case 36: return launch_glds_x3<128, 256, 2, 4, 3>(a, stream);
+    case 37: return launch_glds_x3<256, 128, 4, 2, 2>(a, stream);
+    case 38: return launch_glds_x3<128, 128, 2, 4, 4>(a, stream);
+    case 39: return launch_glds_x3<256, 64, 4, 2, 4>(a, stream);
+    // one wave column (WN = 1): every A fragment is split once per K step per tile
+    case 40: return launch_glds_x3<128, 128, 8, 1>(a, stream);
+    case 41: return launch_glds_x3<128, 64, 8, 1>(a, stream);
+    case 42: return launch_glds_x3<256, 64, 8, 1>(a, stream);
+    case 43: return launch_glds_x3<256, 128, 8, 1>(a, stream);
+    case 44: return launch_glds_x3<128, 128, 8, 1, 3>(a, stream);
+    case 45: return launch_glds_x3<256, 64, 8, 1, 3>(a, stream);
+    case 46: return launch_glds_x3<64, 128, 4, 1>(a, stream);
+    case 47: return launch_glds_x3<64, 64, 4, 1>(a, stream);
     case 1: return launch_x3<128, 32, 4, 1>(a, stream);
     case 2: return launch_x3<128, 64, 4, 1>(a, stream);
     case 5: return launch_x3<64, 128, 1, 4>(a, stream);
