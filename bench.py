@@ -17,13 +17,25 @@ rank 0 over RCCL and copied to its host.  Weak scaling: B frames per GPU per
 step.  Data: synthetic sensors, random-init weights (no datasets/checkpoints
 reachable); compute dtype bf16 with fp32 accumulation.
 
-Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (the script
+starts N rank processes itself, before any GPU call) or ``torchrun
+--nproc-per-node N bench.py --gpus N``.  The run fails — it never silently
+measures fewer GPUs — when the ranks that come up, the visible devices or the
+ranks RCCL built its communicator over differ from ``--gpus``.
+
+Precision: ``--precision fp32`` (default) is the reference's serving precision
+(``examples/YOLOv5/config.pbtxt:7,16``, ``examples/pointpillar_kitti/config.pbtxt:33,54``
+TYPE_FP32): fp32 activations, split-product MFMA convs, detection parity with
+the fp32 models gated in ``tests/test_fp32_mode_gpu.py``.  ``--precision bf16``
+is a secondary, labelled number.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -54,8 +66,8 @@ def parse():
     ap.add_argument("--columns", type=int, default=1875)
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic frames per rank")
     ap.add_argument("--ingest", choices=["local", "rccl"], default="local")
-    ap.add_argument("--comm", choices=["torch", "native"], default="torch",
-                    help="DP scatter/gather: torch batch_isend_irecv or the C++ RCCL communicator")
+    ap.add_argument("--comm", choices=["torch", "native"], default="native",
+                    help="DP scatter/gather: the C++ RCCL communicator (default) or torch batch_isend_irecv")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
@@ -75,16 +87,76 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 (default): the reference's serving precision — fp32 activations, split-product "
                          "MFMA convs; bf16: bf16 activations (secondary, labelled)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launch/rendezvous check only: every rank joins, the ranks are counted with an all-reduce, "
+                         "rank 0 prints them (no GPU work; used by the CPU tests with TCA_DIST_BACKEND=gloo)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--target-2d", type=float, default=100.0, help="candidates/frame reaching 2D NMS (calibration)")
     ap.add_argument("--target-3d", type=float, default=2000.0, help="anchors/frame reaching 3D NMS (calibration)")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and
+    return the worst exit code.  Runs before anything initialises the GPU in
+    this process (spawned children, never an exec)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TCA_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait()
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # one rank failed: the others would block in a collective
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world_env} rank(s): refusing to report a "
+                         f"number under the wrong GPU count")
+    gloo_rehearsal = os.environ.get("TCA_DIST_BACKEND") == "gloo"
+    if args.gpus > 1 and not gloo_rehearsal and torch.cuda.device_count() < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) are visible")
     info = init_distributed()
     dev = info.device
+    if info.world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but {info.world} ranks joined the process group")
+    if args.check_launch:
+        import torch.distributed as dist
+        seen = torch.zeros(args.gpus, dtype=torch.int64)
+        seen[info.rank] = 1
+        if info.world > 1:
+            dist.all_reduce(seen)
+        if info.is_main:
+            print(json.dumps({"check_launch": True, "world": info.world, "ranks_seen": int(seen.sum()),
+                              "self_launched": os.environ.get("TCA_SELF_LAUNCHED") == "1"}), flush=True)
+        shutdown(info)
+        return
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
     from triton_client_amd.pipelines import CameraPipeline, GraphRunner, LidarPipeline
@@ -262,10 +334,19 @@ def main():
     else:
         runner = GraphRunner(pipeline_step, enabled=not args.no_graph)
     native = None
-    if args.comm == "native" and info.world > 1:
+    comm_used = "torch" if info.world > 1 else "none"
+    rccl_ranks = 1
+    if args.comm == "native" and info.world > 1 and not gloo_rehearsal:
         from triton_client_amd.parallel.rccl import NativeComm
 
         native = NativeComm.from_info(info)
+        rccl_ranks = native.count()
+        comm_used = "native"
+    elif info.world > 1:
+        import torch.distributed as dist
+        rccl_ranks = dist.get_world_size() if dist.get_backend() == "nccl" else 0
+    if info.world > 1 and not gloo_rehearsal and rccl_ranks != args.gpus:
+        raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
     ex = FrameExchange(info, native=native)
 
     dsts = [t for t in ((cam.frames,) if use_cam else ()) + ((lid.data, lid.frame_n) if use_lid else ())]
@@ -397,10 +478,12 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(fps / REFERENCE_EQUIVALENT_FPS, 2) if REFERENCE_EQUIVALENT_FPS else None),
+            # BASELINE.json publishes no reference number: nothing to divide by
+            "vs_baseline": None,
             "dtype": args.precision if (args.camera_model == "yolov5n" and args.lidar_model == "pointpillars")
             else "bf16",
-            "data": (f"synthetic: {W0}x{H0} uint8 RGB camera frames + {spec.rings}x{spec.azimuth_steps} LiDAR sweeps "
+            "data": (f"synthetic: {nd} distinct {W0}x{H0} uint8 RGB camera frames + {nd} distinct "
+                     f"{spec.rings}x{spec.azimuth_steps} LiDAR sweeps per rank, re-sent every step "
                      f"(PointCloud2 16 B/pt, ~2% NaN dropouts); random-init weights (He-normal + LSUV rescaling on "
                      f"sample frames), detection-head bias offset calibrated so ~{args.target_2d:g} 2D / ~{args.target_3d:g} 3D candidates per frame reach NMS"),
             "config": {
@@ -412,8 +495,12 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{info.world}",
                 "frames_per_gpu_per_step": B,
+                "precision": args.precision,
+                "distinct_frames_per_rank": nd,
+                "rccl_ranks": rccl_ranks,
+                "vs_reference_equivalent_emulation": round(fps / REFERENCE_EQUIVALENT_FPS, 2),
                 "ingest": args.ingest,
-                "comm": args.comm,
+                "comm": comm_used,
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,
                 "branch_streams": 2 if side is not None else 1,

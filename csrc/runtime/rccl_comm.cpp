@@ -54,6 +54,12 @@ int tca_rccl_async_error(void* comm) {
     return r != ncclSuccess ? (int)r : (int)e;
 }
 
+// Ranks the communicator was built over (ncclCommCount): what the bench reports as n_gpus.
+int tca_rccl_comm_count(void* comm, int* count) {
+  if (!comm || !count) return (int)ncclInvalidArgument;
+  return (int)ncclCommCount((ncclComm_t)comm, count);
+}
+
 const char* tca_rccl_error_string(int code) { return ncclGetErrorString((ncclResult_t)code); }
 
 // One grouped p2p plan: n ops; op i moves bytes[i] bytes of buf[i] to

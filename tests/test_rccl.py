@@ -11,7 +11,7 @@ from triton_client_amd import _native
 
 SYMS = ("tca_rccl_unique_id_bytes", "tca_rccl_get_unique_id", "tca_rccl_comm_init", "tca_rccl_comm_destroy",
         "tca_rccl_comm_abort", "tca_rccl_async_error", "tca_rccl_error_string", "tca_rccl_group_p2p",
-        "tca_rccl_allreduce_max_f64", "tca_rccl_broadcast")
+        "tca_rccl_allreduce_max_f64", "tca_rccl_broadcast", "tca_rccl_comm_count")
 
 
 def test_runtime_exports_rccl_abi():
@@ -30,6 +30,7 @@ def test_native_comm_world1():
     comm = NativeComm(0, 1)
     try:
         assert comm.async_error() is None
+        assert comm.count() == 1
         a = torch.arange(1000, dtype=torch.float32, device="cuda")
         b = torch.empty_like(a)
         odd_src = torch.arange(7, dtype=torch.uint8, device="cuda")  # byte path (7 B)
@@ -69,3 +70,36 @@ def test_frame_exchange_native_ops():
         assert torch.equal(src, dst)
     finally:
         comm.close()
+
+
+@pytest.mark.gpu
+def test_native_p2p_plan_graph_capture():
+    """The grouped p2p plan is plain stream work: it can be captured into a
+    hipGraph with the pipeline step and replayed (the bench's in-graph gather)."""
+    from triton_client_amd.parallel.rccl import RECV, SEND, NativeComm
+
+    torch.cuda.set_device(0)
+    comm = NativeComm(0, 1)
+    try:
+        a = torch.arange(4096, dtype=torch.float32, device="cuda")
+        b = torch.zeros_like(a)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            comm.group_p2p([(SEND, a, 0), (RECV, b, 0)])  # warm-up outside capture
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            a.add_(1.0)
+            comm.group_p2p([(SEND, a, 0), (RECV, b, 0)])
+        b.zero_()
+        g.replay()
+        g.replay()
+        torch.cuda.synchronize()
+        ok = torch.equal(b, torch.arange(4096, dtype=torch.float32, device="cuda") + 2.0)
+        del g  # the graph holds RCCL work: release it before the communicator goes
+        torch.cuda.synchronize()
+        assert ok
+    finally:
+        comm.abort()  # never block on teardown of a communicator a graph has used

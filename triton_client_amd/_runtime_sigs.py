@@ -19,6 +19,7 @@ SIGS = {
     "tca_rccl_comm_abort": (I, [P]),
     "tca_rccl_async_error": (I, [P]),
     "tca_rccl_error_string": (CP, [I]),
+    "tca_rccl_comm_count": (I, [P, ctypes.POINTER(I)]),
     "tca_rccl_group_p2p": (I, [P, I, P, P, P, P, P]),
     "tca_rccl_allreduce_max_f64": (I, [P, P, ctypes.c_int64, P]),
     "tca_rccl_broadcast": (I, [P, P, ctypes.c_int64, I, P]),

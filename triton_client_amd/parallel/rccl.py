@@ -97,6 +97,12 @@ class NativeComm:
                                                 self._stream(stream)), "ncclBroadcast")
         return t
 
+    def count(self) -> int:
+        """Ranks RCCL built this communicator over (ncclCommCount)."""
+        n = ctypes.c_int(0)
+        self._check(self.lib.tca_rccl_comm_count(self._comm, ctypes.byref(n)), "ncclCommCount")
+        return int(n.value)
+
     def async_error(self) -> Optional[str]:
         """None while healthy, else the RCCL error string (a peer died, a link broke)."""
         rc = self.lib.tca_rccl_async_error(self._comm)
