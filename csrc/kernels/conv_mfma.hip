@@ -1488,8 +1488,11 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
   a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
   if (a.K > Kp) return (int)hipErrorInvalidValue;
   const bool v2ok = (Cin % 32) == 0 && Kp == a.K;
-  if (tile == 0 && small_halo_x3_ok(a)) tile = 60;
-  if (tile == 0) tile = v2ok ? (N <= 64 ? 22 : (a.M >= 40000 ? 20 : 24)) : (N <= 16 ? 6 : N <= 32 ? 1 : N <= 64 ? 2 : 5);
+  // auto tile, measured on MI355X at batch 32 (tools/bench_conv_x3.py -> profiles/r2/conv_x3_tiles.jsonl):
+  // small halo only at stride 1 (stride 2: v1 128x32 is 1.9x faster); N <= 32: v1 (a 1x1 64->32 runs 26 us
+  // vs 38 on glds); glds 128x64 with one wave column for N <= 64, 128x128 4x2 above
+  if (tile == 0 && small_halo_x3_ok(a) && a.S == 1) tile = 60;
+  if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 41 : 20) : (N <= 64 ? 2 : 5);
   if (tile >= 10 && tile < 60 && !v2ok) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 60: return launch_small_halo_x3(a, stream);

@@ -78,7 +78,7 @@ def main():
             fc(xin, out=out, tile=t)
             e = ((out.nchw() - ref).norm() / ref.norm()).item()
             if e > 1e-4:
-                res[t] = f"WRONG rel={e:.3g}"
+                res[t] = f"WRONG rel={e:.3g} {us:.1f}us"
                 continue
             res[t] = round(us, 1)
             if best is None or us < best[1]:
