@@ -186,3 +186,75 @@ def test_dp_rank_failure_resharding():
         if p.is_alive():
             p.kill()
     assert res == {0: "ok", 1: "ok", 2: "wait"}, res
+
+
+class _DiesMidStep(FakeDetector):
+    """Rank 2's engine: the process dies inside its second shard, i.e. after
+    the step's scatter and before its gather (the case a header-less protocol
+    would answer with a stale payload on retry)."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def detect(self, frames):
+        self.calls += 1
+        if self.calls == 2:
+            os._exit(0)
+        return super().detect(frames)
+
+
+def _midstep_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)
+    try:
+        from triton_client_amd.parallel.dp import DataParallelDetector2D, HealthMonitor, init_distributed
+
+        info = init_distributed("gloo")
+        mon = HealthMonitor(info, interval=0.1, timeout=1.0)
+        local = _DiesMidStep() if rank == 2 else FakeDetector()
+        dp = DataParallelDetector2D(local, info, max_det=8, monitor=mon)
+        if info.is_main:
+            for b in range(3):
+                frames = [np.full((8, 12, 3), 5 * i + 40 * b, np.uint8) for i in range(9)]
+                want = FakeDetector().detect(frames)
+                got = dp.detect(frames)
+                assert len(got) == len(want)
+                for a, w in zip(got, want):
+                    assert np.array_equal(a, w), (b, a, w)
+            assert dp.retries == 1 and mon.dead == {2}, (dp.retries, mon.dead)
+            dp.close()
+            q.put((0, "ok"))
+        else:
+            n = dp.serve()
+            q.put((rank, f"served {n}"))
+        mon.stop()
+        q.close()
+        q.join_thread()
+        os._exit(0)
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        q.close()
+        q.join_thread()
+        os._exit(1)
+
+
+def test_dp_rank_dies_between_scatter_and_gather():
+    """rank 0 drains every op of the failed step, the survivor's payload is
+    consumed in that step (so the retry cannot read it), the retry runs with a
+    new sequence number over the survivors and every batch's results are exact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_midstep_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    # rank 1: batch 0, the failed batch 1, its retry, batch 2
+    assert res == {0: "ok", 1: "served 4"}, res

@@ -93,6 +93,8 @@ def _load_hip() -> ctypes.CDLL:
         if _HIP is not None:
             _HIP.hipGetErrorString.restype = ctypes.c_char_p
             _HIP.hipGetErrorString.argtypes = [I]
+            _HIP.hipGetLastError.restype = I
+            _HIP.hipGetLastError.argtypes = []
     return _HIP
 
 
@@ -148,7 +150,15 @@ def check(rc: int, what: str) -> None:
 
 
 def call(name: str, *args) -> None:
+    """Launch through the C ABI.  The launchers report ``hipGetLastError()``
+    after their launch; a stale error left by an earlier runtime call that
+    its caller already handled (e.g. a pointer-attribute probe on pageable
+    host memory inside a framework copy) would be misreported as this
+    launch's failure, so the thread's error state is cleared first."""
     fn = getattr(kernels(), name)
+    hip = _HIP if _HIP is not None else _load_hip()
+    if hip is not None:
+        hip.hipGetLastError()
     check(fn(*args), name)
 
 

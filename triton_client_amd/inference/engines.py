@@ -130,6 +130,35 @@ class LocalDetector2D(Detector2D):
         return self._run(frames, annotate=False)[0]
 
     @torch.no_grad()
+    def detect_device(self, frames: torch.Tensor, max_det: Optional[int] = None):
+        """Device-resident detection for the data-parallel path: ``frames``
+        [n, H, W, 3] uint8 already in this GPU's memory (a DP shard) is copied
+        device-to-device into the pipeline's frame buffer; returns
+        ``(dets [n, max_det, 6] fp32, count [n] int32)`` on the device (x1, y1,
+        x2, y2, conf, cls in frame pixels).  No host transfer of frames or
+        results."""
+        if self.device.type != "cuda" or not frames.is_cuda:
+            raise ValueError("detect_device needs a GPU engine and GPU frames")
+        n, H, W = frames.shape[:3]
+        md = max_det or self.max_det
+        if self.calibrate_target is not None:
+            self.calibrate_synthetic()
+        dets = torch.zeros((n, md, 6), dtype=torch.float32, device=frames.device)
+        cnt = torch.zeros((n,), dtype=torch.int32, device=frames.device)
+        with self._lock:
+            p, run, _ = self._pipe((int(H), int(W)), None)
+            for s in range(0, n, self.B):
+                k = min(self.B, n - s)
+                p.frames[:k].copy_(frames[s:s + k, ..., :3])
+                res = run()
+                m = min(md, res.box.shape[1])
+                dets[s:s + k, :m, :4] = res.box[:k, :m]
+                dets[s:s + k, :m, 4] = res.score[:k, :m]
+                dets[s:s + k, :m, 5] = res.cls[:k, :m].float()
+                cnt[s:s + k] = res.count[:k].clamp(max=md)
+        return dets, cnt
+
+    @torch.no_grad()
     def detect_annotated(self, frames: Sequence[np.ndarray], thickness: int = 2):
         """→ (annotated frames, detections).  The rectangles are drawn on the
         GPU into the pipeline's resident frame buffer (K15, ``ops.image.draw_boxes_``)
@@ -331,6 +360,51 @@ class LocalDetector3D(Detector3D):
                     for j, i in enumerate(chunk):
                         out[i] = per[j]
         return out
+
+    @torch.no_grad()
+    def detect_device(self, data: torch.Tensor, npts: torch.Tensor, fields, point_step: int,
+                      max_out: int = 500):
+        """Device-resident detection for the data-parallel path: ``data``
+        [n, maxb] uint8 PointCloud2 payloads and ``npts`` [n] already in this
+        GPU's memory; → ``(box [n, M, D], score [n, M], label [n, M] int64,
+        count [n] int32)`` on the device, boxes in the sensor frame (z offset
+        removed).  PointPillars / SECOND-IoU (NmsResult pipelines)."""
+        from ..ops.lidar import PointLayout
+
+        if self.device.type != "cuda" or not data.is_cuda:
+            raise ValueError("detect_device needs a GPU engine and GPU payloads")
+        if self.family == "centerpoint":
+            raise NotImplementedError("centerpoint results are per-task segments: use detect()")
+        by = {f.name: f for f in fields}
+        names = ("x", "y", "z", "intensity")
+        layout = PointLayout(int(point_step), tuple(by[k].offset for k in names), tuple(by[k].datatype for k in names))
+        n, maxb = data.shape
+        if self.calibrate_target is not None:
+            self.calibrate_synthetic()
+        D = self.box_dim
+        dev = data.device
+        box = torch.zeros((n, max_out, D), dtype=torch.float32, device=dev)
+        score = torch.zeros((n, max_out), dtype=torch.float32, device=dev)
+        lab = torch.zeros((n, max_out), dtype=torch.int64, device=dev)
+        cnt = torch.zeros((n,), dtype=torch.int32, device=dev)
+        with self._lock:
+            p, run, _, _ = self._pipe(layout, max(1, maxb // max(1, int(point_step))), None)
+            if maxb > p.frame_bytes:
+                raise ValueError(f"payload of {maxb} B exceeds the pipeline's {p.frame_bytes} B frame slot")
+            slots = p.data.view(p.B, p.frame_bytes)
+            for s in range(0, n, self.B):
+                k = min(self.B, n - s)
+                slots[:k, :maxb].copy_(data[s:s + k])
+                p.frame_n[:k].copy_(npts[s:s + k].to(torch.int32))
+                res = run()
+                m = min(max_out, res.box.shape[1])
+                b = res.box[:k, :m, :D].float()
+                box[s:s + k, :m] = b
+                box[s:s + k, :m, 2] -= self.z_offset
+                score[s:s + k, :m] = res.score[:k, :m]
+                lab[s:s + k, :m] = res.cls[:k, :m].long()
+                cnt[s:s + k] = res.count[:k].clamp(max=max_out)
+        return box, score, lab, cnt
 
     # ----------------------------------------------------------------- CPU path
     def _detect_cpu(self, cloud: msgs.PointCloud2) -> dict:

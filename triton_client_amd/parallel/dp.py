@@ -85,13 +85,16 @@ class FrameExchange:
         self.group = group
         self.native = native
 
-    def _run(self, ops) -> None:
-        """ops: (0 send | 1 recv, tensor, peer)."""
+    def _run(self, ops, strict: bool = True) -> set:
+        """ops: (0 send | 1 recv, tensor, peer).  Every op is waited for, even
+        after one fails, so no operation of this call is left in flight.
+        strict: raise on the first failed peer; else return the failed peers
+        (the DP detectors' retry path)."""
         if not ops:
-            return
+            return set()
         if self.native is not None:
             self.native.group_p2p(ops)
-            return
+            return set()
         staged = []
         if dist.get_backend(self.group) == "gloo":  # gloo moves host tensors: stage device ones
             host = []
@@ -99,18 +102,27 @@ class FrameExchange:
                 if t.is_cuda:
                     h = t.cpu() if k == 0 else torch.empty(t.shape, dtype=t.dtype)
                     if k == 1:
-                        staged.append((h, t))
+                        staged.append((h, t, p))
                     t = h
                 host.append((k, t, p))
             ops = host
         p2p = [dist.P2POp(dist.isend if k == 0 else dist.irecv, t, p, self.group) for k, t, p in ops]
-        for w in dist.batch_isend_irecv(p2p):
-            w.wait()
-        for h, t in staged:
-            t.copy_(h)
+        failed, err = set(), None
+        for (k, t, p), w in zip(ops, dist.batch_isend_irecv(p2p)):
+            try:
+                w.wait()
+            except RuntimeError as e:  # a dead / unreachable peer (gloo raises; RCCL would hang: see _DPBase)
+                failed.add(p)
+                err = err or e
+        for h, t, p in staged:
+            if p not in failed:
+                t.copy_(h)
+        if failed and strict:
+            raise err
+        return failed
 
     def scatter(self, src: Optional[Sequence[Sequence[torch.Tensor]]], dst: Sequence[torch.Tensor],
-                peers: Optional[Sequence[int]] = None) -> None:
+                peers: Optional[Sequence[int]] = None, strict: bool = True) -> set:
         """src (rank 0 only): src[i][k] is the k-th tensor for rank peers[i]
         (peers defaults to every rank; peers[0] is rank 0); dst[k] receives
         this rank's share.  Async w.r.t. the host; ordered on the current
@@ -120,7 +132,7 @@ class FrameExchange:
             for d, s in zip(dst, src[0]):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
-            return
+            return set()
         peers = list(peers) if peers is not None else list(range(info.world))
         ops = []
         if info.rank == 0:
@@ -131,10 +143,10 @@ class FrameExchange:
                     d.copy_(s, non_blocking=True)
         else:
             ops += [(1, d, 0) for d in dst]
-        self._run(ops)
+        return self._run(ops, strict)
 
     def gather(self, src: Sequence[torch.Tensor], dst: Optional[Sequence[Sequence[torch.Tensor]]],
-               peers: Optional[Sequence[int]] = None) -> None:
+               peers: Optional[Sequence[int]] = None, strict: bool = True) -> set:
         """src: this rank's tensors; dst (rank 0 only): dst[i][k] receives rank
         peers[i]'s k-th tensor (peers defaults to every rank)."""
         info = self.info
@@ -142,7 +154,7 @@ class FrameExchange:
             for d, s in zip(dst[0], src):
                 if d.data_ptr() != s.data_ptr():
                     d.copy_(s, non_blocking=True)
-            return
+            return set()
         peers = list(peers) if peers is not None else list(range(info.world))
         ops = []
         if info.rank == 0:
@@ -153,7 +165,7 @@ class FrameExchange:
                     d.copy_(s, non_blocking=True)
         else:
             ops += [(0, s, 0) for s in src]
-        self._run(ops)
+        return self._run(ops, strict)
 
 
 def barrier(info: DistInfo) -> None:
@@ -257,19 +269,29 @@ class HealthMonitor:
         self._thread.join(timeout=2 * self.interval + 1)
 
 
-_HDR = 16  # header ints; the last slot carries the participant bitmask
+_HDR = 16  # header ints: [seq, payload fields..., participant bitmask]
 
 
 class _DPBase:
     """Rank 0 calls ``detect(items)``; every other rank calls ``serve()``,
     which runs until rank 0 calls ``close()``.  Work is split into
     contiguous equal shards (padded) over the participating ranks, scattered
-    with grouped p2p, run by each rank's local engine, and gathered back as
-    fixed-size padded buffers.  Headers go point-to-point, so a dead rank is
-    simply left out: with a :class:`HealthMonitor` the shards are re-split over
-    the survivors (rank 0 alone runs everything as the last resort), and a
-    step that fails mid-flight (broken peer link) is retried on the new live
-    set."""
+    with grouped p2p, run by each rank's local engine ON THE DEVICE (the
+    shard the exchange landed in GPU memory goes straight into the engine's
+    pipeline buffers: no host round trip on any rank), and gathered back as
+    fixed-size padded device buffers.
+
+    Failure handling (gloo transport; an RCCL peer that dies hangs the
+    communicator instead of raising, so under RCCL a dead rank surfaces
+    through :class:`HealthMonitor` / ``NativeComm.async_error`` and the job is
+    restarted): every step carries a sequence number in its header, every
+    peer echoes it in its gather payload and rank 0 checks it; rank 0 waits
+    for EVERY scatter / gather operation of a step even after one peer has
+    failed, so a failed step leaves no operation in flight and no stale
+    payload queued (each survivor has consumed its shard and delivered its
+    detections); then the shards are re-split over the survivors the
+    :class:`HealthMonitor` reports and the step is retried with a new
+    sequence number."""
 
     def __init__(self, local, info: DistInfo, monitor: Optional[HealthMonitor] = None):
         self.local, self.info = local, info
@@ -277,6 +299,7 @@ class _DPBase:
         self.names = getattr(local, "names", [])
         self.monitor = monitor
         self.retries = 0
+        self.seq = 0
 
     def _participants(self) -> List[int]:
         return self.monitor.alive() if self.monitor is not None else list(range(self.info.world))
@@ -329,16 +352,49 @@ class _DPBase:
             parts = self._participants()
             if parts == [0]:
                 return self.local.detect(items)  # every peer is gone: degrade to rank 0 alone
+            self.seq += 1
             try:
-                return self._step(self._send_header(self._make_header(items), parts), items)
+                return self._step(self._send_header([self.seq] + self._make_header(items), parts), items)
             except RuntimeError:
                 if self.monitor is None or len(self.monitor.wait_for_change(parts)) == len(parts):
                     raise
                 self.retries += 1
 
+    # shared step skeleton ---------------------------------------------------------------
+    def _exchange(self, hdr, src, mine, run_local, out_like):
+        """scatter ``src`` (rank 0) into ``mine``; ``run_local(valid)`` → this
+        rank's padded device outputs (the last one an int32 count vector of
+        length per + 1 whose last slot receives the step's sequence number);
+        gather them.  Rank 0 returns (gathered, workers, per)."""
+        info = self.info
+        seq = hdr[0]
+        wk = self._workers(hdr)
+        nw, me = len(wk), wk.index(info.rank)
+        n = hdr[1]
+        per = (n + nw - 1) // nw
+        strict = not info.is_main
+        failed = self.ex.scatter(src, mine, wk, strict=strict)
+        valid = max(0, min(per, n - me * per))
+        outs = run_local(valid, per)
+        outs[-1][per] = seq & 0x7FFFFFFF
+        dst = [[torch.empty_like(t) for t in outs] for _ in range(nw)] if info.is_main else None
+        failed |= self.ex.gather(outs, dst, wk, strict=strict)
+        if not info.is_main:
+            return None
+        if failed:
+            raise RuntimeError(f"DP step {seq}: ranks {sorted(failed)} failed")
+        for r, d in zip(wk, dst):
+            got = int(d[-1][per])
+            if got != seq & 0x7FFFFFFF:
+                raise RuntimeError(f"DP step {seq}: rank {r} answered for step {got}")
+        return dst, wk, per
+
 
 class DataParallelDetector2D(_DPBase):
-    """Frames (HxWx3 uint8, one size per call) → per-frame [n, 6] detections."""
+    """Frames (HxWx3 uint8, one size per call) → per-frame [n, 6] detections.
+    ``local`` must offer ``detect_device(frames [n, H, W, 3] uint8 GPU) ->
+    (dets [n, max_det, 6], count [n])`` on device (LocalDetector2D does) or,
+    for CPU engines, ``detect``."""
 
     def __init__(self, local, info: DistInfo, max_det: int = 300, monitor: Optional[HealthMonitor] = None):
         super().__init__(local, info, monitor)
@@ -353,48 +409,59 @@ class DataParallelDetector2D(_DPBase):
             return [d for f in items for d in self.detect([f])]
         return super().detect(items)
 
+    def _local_padded(self, frames_dev: torch.Tensor, valid: int, per: int):
+        dev = self.info.device
+        pad = torch.zeros((per, self.max_det, 6), dtype=torch.float32, device=dev)
+        cnt = torch.zeros((per + 1,), dtype=torch.int32, device=dev)
+        if valid == 0:
+            return [pad, cnt]
+        if hasattr(self.local, "detect_device") and frames_dev.is_cuda:
+            d, c = self.local.detect_device(frames_dev[:valid], self.max_det)
+            pad[:valid] = d
+            cnt[:valid] = c
+            return [pad, cnt]
+        dets = self.local.detect([frames_dev[i].cpu().numpy() for i in range(valid)])  # CPU engines
+        for i, d in enumerate(dets):
+            k = min(len(d), self.max_det)
+            pad[i, :k] = torch.from_numpy(np.asarray(d[:k], np.float32)).to(dev)
+            cnt[i] = k
+        return [pad, cnt]
+
     def _step(self, hdr, frames):
         info = self.info
-        n, H, W = hdr[:3]
+        n, H, W = hdr[1:4]
         wk = self._workers(hdr)
-        nw, me = len(wk), wk.index(info.rank)
+        nw = len(wk)
         per = (n + nw - 1) // nw
         dev = info.device
         src = None
         if info.is_main:
-            buf = torch.zeros((nw, per, H, W, 3), dtype=torch.uint8)
+            buf = torch.zeros((nw, per, H, W, 3), dtype=torch.uint8, pin_memory=dev.type == "cuda")
             for i, f in enumerate(frames):
-                buf[i // per, i % per] = torch.from_numpy(np.ascontiguousarray(f[..., :3]))
-            buf = buf.to(dev)
+                buf[i // per, i % per].copy_(torch.from_numpy(np.ascontiguousarray(f[..., :3])))
+            buf = buf.to(dev, non_blocking=True)
             src = [[buf[r]] for r in range(nw)]
-        mine = torch.empty((per, H, W, 3), dtype=torch.uint8, device=dev)
-        self.ex.scatter(src, [mine], wk)
-        valid = max(0, min(per, n - me * per))
-        host = mine[:valid].cpu().numpy()
-        dets = self.local.detect([host[i] for i in range(valid)]) if valid else []
-        pad = torch.zeros((per, self.max_det, 6), dtype=torch.float32)
-        cnt = torch.zeros((per,), dtype=torch.int32)
-        for i, d in enumerate(dets):
-            k = min(len(d), self.max_det)
-            pad[i, :k] = torch.from_numpy(np.asarray(d[:k], np.float32))
-            cnt[i] = k
-        pad, cnt = pad.to(dev), cnt.to(dev)
-        dst = None
-        if info.is_main:
-            dst = [[torch.empty_like(pad), torch.empty_like(cnt)] for _ in range(nw)]
-        self.ex.gather([pad, cnt], dst, wk)
-        if not info.is_main:
+            mine = [buf[0]]
+        else:
+            mine = [torch.empty((per, H, W, 3), dtype=torch.uint8, device=dev)]
+        res = self._exchange(hdr, src, mine, lambda valid, per_: self._local_padded(mine[0], valid, per_), None)
+        if res is None:
             return None
+        dst, wk, per = res
+        pads = torch.stack([d[0] for d in dst]).cpu().numpy()  # the one D2H of the step: detections only
+        cnts = torch.stack([d[1] for d in dst]).cpu().numpy()
         out = []
         for i in range(n):
             r, j = divmod(i, per)
-            k = int(dst[r][1][j])
-            out.append(dst[r][0][j, :k].cpu().numpy())
+            out.append(pads[r, j, :int(cnts[r, j])])
         return out
 
 
 class DataParallelDetector3D(_DPBase):
-    """PointCloud2 messages (same field layout per call) → per-cloud dicts."""
+    """PointCloud2 messages (same field layout per call) → per-cloud dicts.
+    ``local`` offers ``detect_device(data [n, maxb] uint8 GPU, npts [n],
+    layout, max_out) -> (box [n, M, D], score [n, M], label [n, M], count [n])``
+    (LocalDetector3D does) or, for CPU engines, ``detect``."""
 
     def __init__(self, local, info: DistInfo, max_out: int = 500, box_dim: int = 7,
                  monitor: Optional[HealthMonitor] = None):
@@ -410,56 +477,68 @@ class DataParallelDetector3D(_DPBase):
         maxb = max(len(c.data) for c in clouds)
         return [len(clouds), c0.point_step, maxb] + offs + dts
 
-    def _step(self, hdr, clouds):
+    def _local_padded(self, data, npts, valid, per, step, offs, dts):
         from ..ros import msgs
 
+        dev = self.info.device
+        D, M = self.box_dim, self.max_out
+        box = torch.zeros((per, M, D), dtype=torch.float32, device=dev)
+        score = torch.zeros((per, M), dtype=torch.float32, device=dev)
+        lab = torch.zeros((per, M), dtype=torch.int64, device=dev)
+        cnt = torch.zeros((per + 1,), dtype=torch.int32, device=dev)
+        if valid == 0:
+            return [box, score, lab, cnt]
+        fields = [msgs.PointField(k, o, d, 1) for k, o, d in zip(("x", "y", "z", "intensity"), offs, dts)]
+        if hasattr(self.local, "detect_device") and data.is_cuda:
+            b, s_, l_, c = self.local.detect_device(data[:valid], npts[:valid], fields, step, M)
+            box[:valid, :, : b.shape[-1]] = b[..., :D]
+            score[:valid], lab[:valid], cnt[:valid] = s_, l_, c
+            return [box, score, lab, cnt]
+        hb, hn = data.cpu().numpy(), npts.cpu().numpy()  # CPU engines
+        local = [msgs.PointCloud2(height=1, width=int(hn[i]), fields=fields, point_step=step,
+                                  row_step=step * int(hn[i]), data=hb[i, : int(hn[i]) * step].tobytes())
+                 for i in range(valid)]
+        for i, p in enumerate(self.local.detect(local)):
+            k = min(len(p["pred_scores"]), M)
+            box[i, :k] = torch.from_numpy(np.asarray(p["pred_boxes"][:k, :D], np.float32)).to(dev)
+            score[i, :k] = torch.from_numpy(np.asarray(p["pred_scores"][:k], np.float32)).to(dev)
+            lab[i, :k] = torch.from_numpy(np.asarray(p["pred_labels"][:k], np.int64)).to(dev)
+            cnt[i] = k
+        return [box, score, lab, cnt]
+
+    def _step(self, hdr, clouds):
         info = self.info
-        n, step, maxb = hdr[:3]
-        offs, dts = hdr[3:7], hdr[7:11]
+        n, step, maxb = hdr[1:4]
+        offs, dts = hdr[4:8], hdr[8:12]
         wk = self._workers(hdr)
-        nw, me = len(wk), wk.index(info.rank)
+        nw = len(wk)
         per = (n + nw - 1) // nw
         dev = info.device
         src = None
         if info.is_main:
-            buf = torch.zeros((nw, per, maxb), dtype=torch.uint8)
-            npts = torch.zeros((nw, per), dtype=torch.int64)
+            pin = dev.type == "cuda"
+            buf = torch.zeros((nw, per, maxb), dtype=torch.uint8, pin_memory=pin)
+            npts = torch.zeros((nw, per), dtype=torch.int64, pin_memory=pin)
             for i, c in enumerate(clouds):
                 raw = np.frombuffer(c.data, np.uint8)
-                buf[i // per, i % per, : raw.size] = torch.from_numpy(raw.copy())
+                buf[i // per, i % per, : raw.size].copy_(torch.from_numpy(raw))
                 npts[i // per, i % per] = c.width * c.height
-            buf, npts = buf.to(dev), npts.to(dev)
+            buf, npts = buf.to(dev, non_blocking=True), npts.to(dev, non_blocking=True)
             src = [[buf[r], npts[r]] for r in range(nw)]
-        mine = torch.empty((per, maxb), dtype=torch.uint8, device=dev)
-        mine_n = torch.empty((per,), dtype=torch.int64, device=dev)
-        self.ex.scatter(src, [mine, mine_n], wk)
-        valid = max(0, min(per, n - me * per))
-        fields = [msgs.PointField(k, o, d, 1) for k, o, d in zip(("x", "y", "z", "intensity"), offs, dts)]
-        hb, hn = mine.cpu().numpy(), mine_n.cpu().numpy()
-        local = [msgs.PointCloud2(height=1, width=int(hn[i]), fields=fields, point_step=step,
-                                  row_step=step * int(hn[i]), data=hb[i, : int(hn[i]) * step].tobytes())
-                 for i in range(valid)]
-        preds = self.local.detect(local) if valid else []
-        D, M = self.box_dim, self.max_out
-        box = torch.zeros((per, M, D), dtype=torch.float32)
-        score = torch.zeros((per, M), dtype=torch.float32)
-        lab = torch.zeros((per, M), dtype=torch.int64)
-        cnt = torch.zeros((per,), dtype=torch.int32)
-        for i, p in enumerate(preds):
-            k = min(len(p["pred_scores"]), M)
-            box[i, :k] = torch.from_numpy(np.asarray(p["pred_boxes"][:k, :D], np.float32))
-            score[i, :k] = torch.from_numpy(np.asarray(p["pred_scores"][:k], np.float32))
-            lab[i, :k] = torch.from_numpy(np.asarray(p["pred_labels"][:k], np.int64))
-            cnt[i] = k
-        mine_out = [t.to(dev) for t in (box, score, lab, cnt)]
-        dst = [[torch.empty_like(t) for t in mine_out] for _ in range(nw)] if info.is_main else None
-        self.ex.gather(mine_out, dst, wk)
-        if not info.is_main:
+            mine = [buf[0], npts[0]]
+        else:
+            mine = [torch.empty((per, maxb), dtype=torch.uint8, device=dev),
+                    torch.empty((per,), dtype=torch.int64, device=dev)]
+        res = self._exchange(hdr, src, mine,
+                             lambda valid, per_: self._local_padded(mine[0], mine[1], valid, per_, step, offs, dts),
+                             None)
+        if res is None:
             return None
+        dst, wk, per = res
+        hb = [torch.stack([d[k] for d in dst]).cpu().numpy() for k in range(4)]
         out = []
         for i in range(n):
             r, j = divmod(i, per)
-            k = int(dst[r][3][j])
-            out.append({"pred_boxes": dst[r][0][j, :k].cpu().numpy(), "pred_scores": dst[r][1][j, :k].cpu().numpy(),
-                        "pred_labels": dst[r][2][j, :k].cpu().numpy()})
+            k = int(hb[3][r, j])
+            out.append({"pred_boxes": hb[0][r, j, :k], "pred_scores": hb[1][r, j, :k], "pred_labels": hb[2][r, j, :k]})
         return out
