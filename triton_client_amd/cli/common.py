@@ -51,6 +51,11 @@ def add_framework_flags(p: argparse.ArgumentParser, params_default: str, three_d
     g.add_argument("--server", default=None, help="override grpc_channel host:port")
     g.add_argument("--device", default="auto", help="GPU for the local engine / preprocessing (cuda:N, cpu)")
     g.add_argument("--frames-per-step", type=int, default=8, help="micro-batch for bag replay / local engine")
+    g.add_argument("--live-batch", type=int, default=1,
+                   help="live topic: run up to N pending frames per engine call (latest-wins window, "
+                        "re-published in header.seq order); 1 = the reference's one frame per callback")
+    g.add_argument("--live-workers", type=int, default=1,
+                   help="live topic: micro-batches in flight (host work of one overlaps another's GPU work)")
     g.add_argument("--wire", choices=["raw", "proto"], default="raw",
                    help="raw: C++ zero-copy KServe codec; proto: reference-style protobuf request")
     g.add_argument("--timeout", type=float, default=None, help="per-RPC deadline (s); default none")

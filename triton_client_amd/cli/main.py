@@ -7,7 +7,7 @@ import sys
 
 from .common import (DATA, add_framework_flags, add_reference_flags, image_files, load_params, play_bag,
                      setup_logging)
-from .engines import engine_2d
+from .engines import engine_2d, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -26,18 +26,37 @@ def main(argv=None) -> int:
     compat.init_node("ros_infer_2D")
     params = load_params(flags.params, flags.server)
     engine, channel, client = engine_2d(flags, params)
+    info = None
+    if flags.engine == "local":  # under torchrun: shard every micro-batch over the node's GPUs
+        engine, info = maybe_data_parallel(engine)
+        if info is not None and not info.is_main:
+            engine.serve()
+            from ..parallel.dp import shutdown
+            shutdown(info)
+            return 0
     metrics = None
     if flags.metrics_port:
         from ..utils.metrics import ClientMetrics
         metrics = ClientMetrics(flags.metrics_port)
     bus = default_bus() if (flags.play or flags.image_src == "local" or not compat.HAVE_ROSPY) else None
     drv = RosInference(channel, client, engine=engine, params=params, bus=bus, metrics=metrics,
-                       queue_size=None if flags.play or flags.image_src == "local" else 1)
+                       queue_size=None if flags.play or flags.image_src == "local" else 1,
+                       batch=flags.live_batch, workers=flags.live_workers)
     if flags.image_src == "local":
-        return _run_local_images(drv, flags, params)
+        rc = _run_local_images(drv, flags, params)
+        if info is not None:
+            engine.close()
+            from ..parallel.dp import shutdown
+            shutdown(info)
+        return rc
     if flags.play:
         play_bag(flags.play, bus, topics=[params["sub_topic"]])
     drv.start_inference(spin=True, timeout=flags.spin_timeout)
+    drv.stop()
+    if info is not None:
+        engine.close()
+        from ..parallel.dp import shutdown
+        shutdown(info)
     print(f"processed {drv.frames} frames", file=sys.stderr)
     return 0
 

@@ -6,7 +6,7 @@ import os
 import sys
 
 from .common import DATA, add_framework_flags, add_reference_flags, labels_arg, load_params, play_bag, setup_logging
-from .engines import engine_3d
+from .engines import engine_3d, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -25,13 +25,27 @@ def main(argv=None) -> int:
     compat.init_node("ros_infer_3d")
     params = load_params(flags.params, flags.server)
     engine, channel, client = engine_3d(flags, params)
+    info = None
+    if flags.engine == "local":  # under torchrun: shard every micro-batch over the node's GPUs
+        engine, info = maybe_data_parallel(engine, three_d=True)
+        if info is not None and not info.is_main:
+            engine.serve()
+            from ..parallel.dp import shutdown
+            shutdown(info)
+            return 0
     bus = default_bus() if (flags.play or not compat.HAVE_ROSPY) else None
     drv = RosInference3D(channel, client, engine=engine, params=params, bus=bus, jsk=not flags.detection3d,
                          labels=labels_arg(flags.labels), score_thresh=flags.score_thresh,
-                         queue_size=None if flags.play else 50)
+                         queue_size=None if flags.play else 50,
+                       batch=flags.live_batch, workers=flags.live_workers)
     if flags.play:
         play_bag(flags.play, bus, topics=[params["sub_topic"]])
     drv.start_inference(spin=True, timeout=flags.spin_timeout)
+    drv.stop()
+    if info is not None:
+        engine.close()
+        from ..parallel.dp import shutdown
+        shutdown(info)
     print(f"processed {drv.frames} clouds", file=sys.stderr)
     return 0
 

@@ -6,6 +6,11 @@ server), draws the boxes and publishes an annotated ``Image`` (rgb8) carrying
 the *input* header (A4) — plus a ``vision_msgs/Detection2DArray`` on
 ``<pub_topic>/detections`` (the intent of ``utils/pred2ros_msg.py:21-52``).
 An empty detection set still publishes the frame (fixes A5).
+
+``batch > 1`` (or ``workers > 1``): the callback only enqueues; frames are
+run as micro-batches (one engine call — one graph replay, or one DP scatter
+over the node's GPUs — per batch) from a latest-wins window, and results are
+re-published in ``header.seq`` order (:mod:`.batching`).
 """
 from __future__ import annotations
 
@@ -46,7 +51,7 @@ class RosInference(BaseInference):
     def __init__(self, channel=None, client=None, engine: Optional[Detector2D] = None, params: Optional[dict] = None,
                  bus=None, letterbox: bool = False, conf_thres: float = 0.3, draw: bool = True,
                  publish_detections: bool = True, queue_size: Optional[int] = 1, metrics=None, mode: str = "sync",
-                 wire: str = "raw"):
+                 wire: str = "raw", batch: int = 1, workers: int = 1):
         super().__init__(channel, client)
         self._params = params or {}
         self.engine = engine or RemoteDetector2D(channel, client, letterbox=letterbox, conf_thres=conf_thres,
@@ -56,6 +61,8 @@ class RosInference(BaseInference):
         self.queue_size, self.metrics = queue_size, metrics
         self.frames = 0
         self.sub = self.pub = self.det_pub = None
+        self.batch, self.workers = max(1, batch), max(1, workers)
+        self.runner = None
 
     # ------------------------------------------------------------------ run
     def start_inference(self, spin: bool = True, timeout: Optional[float] = None):
@@ -64,15 +71,30 @@ class RosInference(BaseInference):
         if self.publish_detections:
             self.det_pub = compat.Publisher(p["pub_topic"] + "/detections", msgs.Detection2DArray, queue_size=10,
                                             bus=self.bus)
-        self.sub = compat.Subscriber(p["sub_topic"], msgs.CompressedImage, self._callback, queue_size=self.queue_size,
-                                     bus=self.bus)
+        cb, qs = self._callback, self.queue_size
+        if self.batch > 1 or self.workers > 1:
+            from .batching import MicroBatchRunner
+            self.runner = MicroBatchRunner(lambda ms: [(im, det) for im, det, _ in self.process(ms)], self._publish,
+                                           batch=self.batch, workers=self.workers,
+                                           capacity=max(self.queue_size or 0, 2 * self.batch * self.workers))
+            cb, qs = self.runner.push, None  # the window is the (latest-wins) queue
+        self.sub = compat.Subscriber(p["sub_topic"], msgs.CompressedImage, cb, queue_size=qs, bus=self.bus)
         if spin:
             compat.spin(self.bus, timeout)
 
-    def stop(self):
+    def stop(self, drain: bool = True):
         if self.sub is not None:
             self.sub.unregister()
             self.sub = None
+        if self.runner is not None:
+            self.runner.close(drain=drain)
+            self.runner = None
+
+    def _publish(self, item) -> None:
+        im, det = item
+        self.pub.publish(im)
+        if self.det_pub is not None:
+            self.det_pub.publish(det)
 
     # ------------------------------------------------------------------ work
     def process(self, images: Sequence) -> List[tuple]:

@@ -64,7 +64,7 @@ class RosInference3D(BaseInference):
     def __init__(self, channel=None, client=None, engine: Optional[Detector3D] = None, params: Optional[dict] = None,
                  bus=None, jsk: bool = True, labels: Optional[Sequence[int]] = (2,), score_thresh: float = 0.5,
                  z_offset: float = 1.5, queue_size: Optional[int] = 50, metrics=None, mode: str = "sync",
-                 wire: str = "raw"):
+                 wire: str = "raw", batch: int = 1, workers: int = 1):
         super().__init__(channel, client)
         self._params = params or {}
         self.engine = engine or RemoteDetector3D(channel, client, z_offset=z_offset, mode=mode, wire=wire)
@@ -72,20 +72,34 @@ class RosInference3D(BaseInference):
         self.queue_size, self.metrics = queue_size, metrics
         self.frames = 0
         self.sub = self.pub = None
+        # batch > 1: the reference's queue of 50 becomes a latest-wins window
+        # drained as micro-batches (one engine call per batch), re-published in
+        # header.seq order (see .batching)
+        self.batch, self.workers = max(1, batch), max(1, workers)
+        self.runner = None
 
     def start_inference(self, spin: bool = True, timeout: Optional[float] = None):
         p = self.params
         t = msgs.BoundingBoxArray if self.jsk else msgs.Detection3DArray
         self.pub = compat.Publisher(p["pub_topic"], t, queue_size=1, bus=self.bus)
-        self.sub = compat.Subscriber(p["sub_topic"], msgs.PointCloud2, self._pc_callback,
-                                     queue_size=self.queue_size, bus=self.bus)
+        cb, qs = self._pc_callback, self.queue_size
+        if self.batch > 1 or self.workers > 1:
+            from .batching import MicroBatchRunner
+            self.runner = MicroBatchRunner(lambda cs: [m for m, _ in self.process(cs)], self.pub.publish,
+                                           batch=self.batch, workers=self.workers,
+                                           capacity=max(self.queue_size or 0, 2 * self.batch * self.workers))
+            cb, qs = self.runner.push, None
+        self.sub = compat.Subscriber(p["sub_topic"], msgs.PointCloud2, cb, queue_size=qs, bus=self.bus)
         if spin:
             compat.spin(self.bus, timeout)
 
-    def stop(self):
+    def stop(self, drain: bool = True):
         if self.sub is not None:
             self.sub.unregister()
             self.sub = None
+        if self.runner is not None:
+            self.runner.close(drain=drain)
+            self.runner = None
 
     def to_msg(self, pred: dict, header: msgs.Header):
         idx = select_boxes(pred, self.labels, self.score_thresh)

@@ -300,6 +300,8 @@ class _DPBase:
         self.monitor = monitor
         self.retries = 0
         self.seq = 0
+        import threading
+        self._lock = threading.Lock()  # one step at a time on the p2p channel (live drivers may call from threads)
 
     def _participants(self) -> List[int]:
         return self.monitor.alive() if self.monitor is not None else list(range(self.info.world))
@@ -348,6 +350,10 @@ class _DPBase:
             return self.local.detect(items)
         if not items:
             return []
+        with self._lock:
+            return self._detect_locked(items)
+
+    def _detect_locked(self, items):
         while True:
             parts = self._participants()
             if parts == [0]:
@@ -406,7 +412,14 @@ class DataParallelDetector2D(_DPBase):
 
     def detect(self, items):
         if self.info.world > 1 and items and any(f.shape[:2] != items[0].shape[:2] for f in items):
-            return [d for f in items for d in self.detect([f])]
+            groups = {}
+            for i, f in enumerate(items):
+                groups.setdefault(f.shape[:2], []).append(i)
+            out = [None] * len(items)
+            for idx in groups.values():  # one step per frame geometry
+                for i, d in zip(idx, super().detect([items[i] for i in idx])):
+                    out[i] = d
+            return out
         return super().detect(items)
 
     def _local_padded(self, frames_dev: torch.Tensor, valid: int, per: int):
