@@ -1,13 +1,20 @@
 """Bag files: record / replay topic streams (reference: ``rosbag.Bag`` in
 ``communicator/bag_inference{2d,3d}.py``, ``tools/bag_stitch.py``).
 
-``rosbag`` is not installed, so this is a compact self-describing format
-with the same API (``Bag(path, 'r'|'w')``, ``write(topic, msg, t)``,
-``read_messages(topics=...)`` → ``(topic, msg, t)``, ``get_message_count``):
-a magic header, then length-prefixed msgpack records
-``{topic, type, t_ns, msg}`` where ``msg`` is the message's field dict
-(bytes payloads stay binary, no pickling — a bag never executes code when
-read).  Reading streams record by record (large bags are never loaded whole).
+``Bag(path, 'r'|'w')``, ``write(topic, msg, t)``, ``read_messages(topics=...)``
+→ ``(topic, msg, t)``, ``get_message_count``, ``get_type_and_topic_info`` —
+the ``rosbag.Bag`` API, over two formats:
+
+* **ROS bag v2.0** (:mod:`.rosbag_v2`, pure Python): what real recordings
+  are; read whenever the file carries the ``#ROSBAG V2.0`` magic, written for
+  paths ending in ``.bag`` (or ``fmt="rosbag"``).
+* **TCABAG1**: a compact self-describing fallback — a magic header, then
+  length-prefixed msgpack records ``{topic, type, t_ns, msg}`` where ``msg``
+  is the message's field dict (bytes payloads stay binary, no pickling — a
+  bag never executes code when read); written for other paths.
+
+Reading streams record by record / chunk by chunk (large bags are never
+loaded whole).
 """
 from __future__ import annotations
 
@@ -16,22 +23,77 @@ from typing import Iterator, Optional, Sequence, Tuple
 
 import msgpack
 
-from . import msgs
+from . import msgs, rosbag_v2
 
 MAGIC = b"TCABAG1\n"
 
 
-class Bag:
+def Bag(path: str, mode: str = "r", fmt: Optional[str] = None, compression: str = "none"):
+    """Open a bag: ROS bag v2.0 (read by magic; written for ``*.bag`` or
+    ``fmt="rosbag"``) or the TCABAG1 fallback."""
+    if mode not in ("r", "w", "a"):
+        raise ValueError("mode must be r, w or a")
+    if mode == "r":
+        return RosBag(path, "r") if rosbag_v2.is_rosbag(path) else TcaBag(path, "r")
+    fmt = fmt or ("rosbag" if path.endswith(".bag") else "tcabag")
+    if fmt == "rosbag":
+        if mode == "a":
+            raise ValueError("appending to a ROS bag is not supported")
+        return RosBag(path, "w", compression)
+    return TcaBag(path, mode)
+
+
+class RosBag:
+    """rosbag.Bag-like wrapper over :mod:`.rosbag_v2`."""
+
+    def __init__(self, path: str, mode: str = "r", compression: str = "none"):
+        self.path, self.mode = path, mode
+        self._w = rosbag_v2.RosBagWriter(path, compression) if mode == "w" else None
+        self._r = rosbag_v2.RosBagReader(path) if mode == "r" else None
+
+    def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
+        self._w.write(topic, msg, t)
+
+    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0):
+        k = 0
+        for topic, m, t in rosbag_v2.read_messages(self._r, topics):
+            k += 1
+            if k <= start_seq:
+                continue
+            yield topic, m, t
+
+    def get_message_count(self, topic_filters: Optional[Sequence[str]] = None) -> int:
+        return sum(1 for c, _, _ in self._r.raw_messages() if not topic_filters or c.topic in topic_filters)
+
+    def get_type_and_topic_info(self):
+        info = {}
+        for c, _, _ in self._r.raw_messages():
+            d = info.setdefault(c.topic, {"type": c.type, "count": 0, "md5sum": c.md5sum})
+            d["count"] += 1
+        return info
+
+    def close(self) -> None:
+        if self._w is not None:
+            self._w.close()
+        if self._r is not None:
+            self._r.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class TcaBag:
     def __init__(self, path: str, mode: str = "r"):
-        if mode not in ("r", "w", "a"):
-            raise ValueError("mode must be r, w or a")
         self.path, self.mode = path, mode
         self._f = open(path, {"r": "rb", "w": "wb", "a": "ab"}[mode])
         if mode == "w":
             self._f.write(MAGIC)
         elif mode == "r":
             if self._f.read(len(MAGIC)) != MAGIC:
-                raise ValueError(f"{path}: not a triton_client_amd bag")
+                raise ValueError(f"{path}: neither a ROS bag v2.0 nor a triton_client_amd bag")
 
     def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
         t = t or getattr(getattr(msg, "header", None), "stamp", None) or msgs.Time.now()

@@ -1,0 +1,270 @@
+"""ROS1 bag format 2.0 reader / writer, pure Python (``rosbag`` is not installed).
+
+The reference replays and records real ``.bag`` files
+(``communicator/bag_inference2d.py:34-35``, ``communicator/bag_inference3d.py:62-63,182-183``,
+``tools/bag_stitch.py:4-5``, ``tools/pc_extractor.py:30``).  Record layout (bag
+format 2.0): ``#ROSBAG V2.0\\n``, then records ``<u32 header_len><header><u32
+data_len><data>``, a header being ``<u32 len>name=value`` fields with an
+``op`` byte:
+
+* 0x03 bag header — ``index_pos`` (u64), ``conn_count``, ``chunk_count``;
+  padded to 4096 bytes;
+* 0x05 chunk — ``compression`` (none / bz2 / lz4), ``size``; its data is
+  connection + message-data records;
+* 0x07 connection — ``conn``, ``topic``; data = a field block with ``topic``,
+  ``type``, ``md5sum``, ``message_definition``;
+* 0x02 message data — ``conn``, ``time`` (u32 sec, u32 nsec); data = the
+  serialised message (:mod:`.rosmsg`);
+* 0x04 index data (per connection after each chunk: ``ver`` 1, ``conn``,
+  ``count``; data = (time, offset-in-chunk) pairs) and 0x06 chunk info (in
+  the index section: ``ver``, ``chunk_pos``, ``start_time``, ``end_time``,
+  ``count``; data = (conn, msg_count) pairs).
+
+Reading streams chunk by chunk (a bag is never loaded whole); messages of
+types without a schema come back as :class:`RawMessage`.  bz2 chunks are
+read with the stdlib; lz4 only if the ``lz4`` module is importable.
+"""
+from __future__ import annotations
+
+import bz2
+import struct
+from dataclasses import dataclass
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+from . import msgs, rosmsg
+
+MAGIC = b"#ROSBAG V2.0\n"
+OP_MSG, OP_BAG_HEADER, OP_INDEX, OP_CHUNK, OP_CHUNK_INFO, OP_CONNECTION = 0x02, 0x03, 0x04, 0x05, 0x06, 0x07
+HEADER_LEN = 4096
+CHUNK_THRESHOLD = 768 * 1024
+
+
+@dataclass
+class RawMessage:
+    type: str
+    md5sum: str
+    data: bytes
+
+
+@dataclass
+class Connection:
+    id: int
+    topic: str
+    type: str
+    md5sum: str
+    definition: str
+
+
+def _fields(d: Dict[str, bytes]) -> bytes:
+    out = bytearray()
+    for k, v in d.items():
+        f = k.encode() + b"=" + v
+        out += struct.pack("<I", len(f)) + f
+    return bytes(out)
+
+
+def _parse_fields(b: bytes) -> Dict[str, bytes]:
+    d, off = {}, 0
+    while off < len(b):
+        (n,) = struct.unpack_from("<I", b, off)
+        f = b[off + 4: off + 4 + n]
+        k, _, v = f.partition(b"=")
+        d[k.decode()] = v
+        off += 4 + n
+    return d
+
+
+def _record(header: Dict[str, bytes], data: bytes) -> bytes:
+    h = _fields(header)
+    return struct.pack("<I", len(h)) + h + struct.pack("<I", len(data)) + data
+
+
+def _u32(v: int) -> bytes:
+    return struct.pack("<I", v)
+
+
+def _time(t: msgs.Time) -> bytes:
+    return struct.pack("<II", t.secs, t.nsecs)
+
+
+def _read_time(b: bytes) -> msgs.Time:
+    s, ns = struct.unpack("<II", b)
+    return msgs.Time(s, ns)
+
+
+class RosBagWriter:
+    def __init__(self, path: str, compression: str = "none", chunk_threshold: int = CHUNK_THRESHOLD):
+        if compression not in ("none", "bz2"):
+            raise ValueError("compression: none or bz2")
+        self.f = open(path, "wb")
+        self.compression, self.threshold = compression, chunk_threshold
+        self.conns: Dict[Tuple[str, str], Connection] = {}
+        self.chunk_infos: List[Tuple[int, msgs.Time, msgs.Time, Dict[int, int]]] = []
+        self._chunk = bytearray()
+        self._chunk_conns: set = set()
+        self._index: Dict[int, List[Tuple[msgs.Time, int]]] = {}
+        self._t0 = self._t1 = None
+        self.f.write(MAGIC)
+        self._write_bag_header(0, 0, 0)
+
+    def _write_bag_header(self, index_pos: int, conn_count: int, chunk_count: int) -> None:
+        h = _fields({"op": bytes([OP_BAG_HEADER]), "index_pos": struct.pack("<Q", index_pos),
+                     "conn_count": _u32(conn_count), "chunk_count": _u32(chunk_count)})
+        pad = HEADER_LEN - 4 - len(h) - 4
+        self.f.write(struct.pack("<I", len(h)) + h + struct.pack("<I", pad) + b" " * pad)
+
+    def _conn_record(self, c: Connection) -> bytes:
+        data = _fields({"topic": c.topic.encode(), "type": c.type.encode(), "md5sum": c.md5sum.encode(),
+                        "message_definition": c.definition.encode()})
+        return _record({"op": bytes([OP_CONNECTION]), "conn": _u32(c.id), "topic": c.topic.encode()}, data)
+
+    def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
+        t = t or getattr(getattr(msg, "header", None), "stamp", None) or msgs.Time.now()
+        if isinstance(msg, RawMessage):
+            mtype, md5, data, definition = msg.type, msg.md5sum, msg.data, ""
+        else:
+            mtype = rosmsg.TYPE_OF[type(msg)]
+            md5, data, definition = rosmsg.md5sum(mtype), rosmsg.serialize(msg, mtype), rosmsg.full_definition(mtype)
+        key = (topic, mtype)
+        c = self.conns.get(key)
+        if c is None:
+            c = self.conns[key] = Connection(len(self.conns), topic, mtype, md5, definition)
+        if c.id not in self._chunk_conns:
+            self._chunk += self._conn_record(c)
+            self._chunk_conns.add(c.id)
+        self._index.setdefault(c.id, []).append((t, len(self._chunk)))
+        self._chunk += _record({"op": bytes([OP_MSG]), "conn": _u32(c.id), "time": _time(t)}, data)
+        ns = t.to_nsec()
+        self._t0 = t if self._t0 is None or ns < self._t0.to_nsec() else self._t0
+        self._t1 = t if self._t1 is None or ns > self._t1.to_nsec() else self._t1
+        if len(self._chunk) >= self.threshold:
+            self._flush_chunk()
+
+    def _flush_chunk(self) -> None:
+        if not self._chunk:
+            return
+        raw = bytes(self._chunk)
+        data = bz2.compress(raw) if self.compression == "bz2" else raw
+        pos = self.f.tell()
+        self.f.write(_record({"op": bytes([OP_CHUNK]), "compression": self.compression.encode(),
+                              "size": _u32(len(raw))}, data))
+        counts = {}
+        for cid, entries in sorted(self._index.items()):
+            body = b"".join(_time(t) + _u32(off) for t, off in entries)
+            self.f.write(_record({"op": bytes([OP_INDEX]), "ver": _u32(1), "conn": _u32(cid),
+                                  "count": _u32(len(entries))}, body))
+            counts[cid] = len(entries)
+        self.chunk_infos.append((pos, self._t0, self._t1, counts))
+        self._chunk, self._chunk_conns, self._index = bytearray(), set(), {}
+        self._t0 = self._t1 = None
+
+    def close(self) -> None:
+        if self.f.closed:
+            return
+        self._flush_chunk()
+        index_pos = self.f.tell()
+        for c in sorted(self.conns.values(), key=lambda c: c.id):
+            self.f.write(self._conn_record(c))
+        for pos, t0, t1, counts in self.chunk_infos:
+            body = b"".join(_u32(cid) + _u32(n) for cid, n in sorted(counts.items()))
+            self.f.write(_record({"op": bytes([OP_CHUNK_INFO]), "ver": _u32(1), "chunk_pos": struct.pack("<Q", pos),
+                                  "start_time": _time(t0), "end_time": _time(t1), "count": _u32(len(counts))},
+                                 body))
+        self.f.seek(len(MAGIC))
+        self._write_bag_header(index_pos, len(self.conns), len(self.chunk_infos))
+        self.f.close()
+
+
+class RosBagReader:
+    def __init__(self, path: str):
+        self.f = open(path, "rb")
+        if self.f.read(len(MAGIC)) != MAGIC:
+            raise ValueError(f"{path}: not a ROS bag v2.0")
+        self.conns: Dict[int, Connection] = {}
+
+    def _read_record(self, f) -> Optional[Tuple[Dict[str, bytes], bytes]]:
+        b = f.read(4)
+        if len(b) < 4:
+            return None
+        (hl,) = struct.unpack("<I", b)
+        h = _parse_fields(f.read(hl))
+        (dl,) = struct.unpack("<I", f.read(4))
+        return h, f.read(dl)
+
+    def _conn(self, h, data) -> Connection:
+        d = _parse_fields(data)
+        cid = struct.unpack("<I", h["conn"])[0]
+        c = Connection(cid, h["topic"].decode(), d["type"].decode(), d.get("md5sum", b"*").decode(),
+                       d.get("message_definition", b"").decode("utf-8", "replace"))
+        self.conns[cid] = c
+        return c
+
+    @staticmethod
+    def _decompress(kind: str, data: bytes) -> bytes:
+        if kind == "none":
+            return data
+        if kind == "bz2":
+            return bz2.decompress(data)
+        if kind == "lz4":
+            try:
+                import lz4.frame  # noqa: F401
+            except ImportError as e:
+                raise RuntimeError("lz4-compressed bag chunk and the lz4 module is not installed") from e
+            import lz4.frame
+            return lz4.frame.decompress(data)
+        raise ValueError(f"unknown chunk compression {kind!r}")
+
+    def _iter_payload(self, blob: bytes) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
+        off = 0
+        n = len(blob)
+        while off + 8 <= n:
+            (hl,) = struct.unpack_from("<I", blob, off)
+            h = _parse_fields(blob[off + 4: off + 4 + hl])
+            (dl,) = struct.unpack_from("<I", blob, off + 4 + hl)
+            data = blob[off + 8 + hl: off + 8 + hl + dl]
+            off += 8 + hl + dl
+            op = h["op"][0]
+            if op == OP_CONNECTION:
+                self._conn(h, data)
+            elif op == OP_MSG:
+                cid = struct.unpack("<I", h["conn"])[0]
+                yield self.conns[cid], _read_time(h["time"]), data
+
+    def raw_messages(self) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
+        """(connection, time, serialised bytes) in file order."""
+        self.f.seek(len(MAGIC))
+        while True:
+            rec = self._read_record(self.f)
+            if rec is None:
+                return
+            h, data = rec
+            op = h["op"][0]
+            if op == OP_CHUNK:
+                yield from self._iter_payload(self._decompress(h["compression"].decode(), data))
+            elif op == OP_CONNECTION:
+                self._conn(h, data)
+            elif op == OP_MSG:
+                cid = struct.unpack("<I", h["conn"])[0]
+                yield self.conns[cid], _read_time(h["time"]), data
+            # bag header, index data, chunk info: nothing to replay
+
+    @staticmethod
+    def decode(conn: Connection, data: bytes):
+        if conn.type in rosmsg.DEFS:
+            return rosmsg.deserialize(data, conn.type)
+        return RawMessage(conn.type, conn.md5sum, data)
+
+    def close(self) -> None:
+        self.f.close()
+
+
+def is_rosbag(path: str) -> bool:
+    with open(path, "rb") as f:
+        return f.read(len(MAGIC)) == MAGIC
+
+
+def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None):
+    for c, t, data in reader.raw_messages():
+        if topics and c.topic not in topics:
+            continue
+        yield c.topic, reader.decode(c, data), t
