@@ -95,46 +95,50 @@ struct Reader {
 
 }  // namespace
 
-// Size of the encoded request (for allocating the output buffer).
-TCA_API long tca_kserve_request_size(const char* model_name, const char* model_version, const char* id, int n_in,
-                                     const char** in_names, const char** in_dtypes, const int64_t* shapes,
-                                     const int* ndims, const long* in_nbytes, int n_out, const char** out_names) {
-  long n = 0;
-  if (model_name && *model_name) n += bytes_field_len(1, strlen(model_name));
-  if (model_version && *model_version) n += bytes_field_len(2, strlen(model_version));
-  if (id && *id) n += bytes_field_len(3, strlen(id));
+namespace {
+
+// ModelInferRequest and ModelInferResponse share their layout up to the field
+// numbers: 1 model_name, 2 model_version, 3 id, then the tensor descriptors
+// (request field 5 InferInputTensor / response field 5 InferOutputTensor:
+// {1 name, 2 datatype, 3 packed shape}), the requested outputs (request
+// field 6, {1 name}) and the raw contents (request 7, response 6).
+long msg_size(const char* model_name, const char* model_version, const char* id, int n, const char** names,
+              const char** dtypes, const int64_t* shapes, const int* ndims, const long* nbytes, int n_req,
+              const char** req_names, int req_field, int raw_field) {
+  long sz = 0;
+  if (model_name && *model_name) sz += bytes_field_len(1, strlen(model_name));
+  if (model_version && *model_version) sz += bytes_field_len(2, strlen(model_version));
+  if (id && *id) sz += bytes_field_len(3, strlen(id));
   const int64_t* sh = shapes;
-  for (int i = 0; i < n_in; ++i) {
+  for (int i = 0; i < n; ++i) {
     long sp;
-    long t = input_tensor_len(in_names[i], in_dtypes[i], sh, ndims[i], &sp);
+    long t = input_tensor_len(names[i], dtypes[i], sh, ndims[i], &sp);
     sh += ndims[i];
-    n += bytes_field_len(5, t);
+    sz += bytes_field_len(5, t);
   }
-  for (int i = 0; i < n_out; ++i) n += bytes_field_len(6, bytes_field_len(1, strlen(out_names[i])));
-  for (int i = 0; i < n_in; ++i) n += bytes_field_len(7, in_nbytes[i]);
-  return n;
+  for (int i = 0; i < n_req; ++i) sz += bytes_field_len(req_field, bytes_field_len(1, strlen(req_names[i])));
+  for (int i = 0; i < n; ++i) sz += bytes_field_len(raw_field, nbytes[i]);
+  return sz;
 }
 
-// Encode; returns bytes written, or -(required size) if cap is too small.
-TCA_API long tca_kserve_encode_request(const char* model_name, const char* model_version, const char* id, int n_in,
-                                       const char** in_names, const char** in_dtypes, const int64_t* shapes,
-                                       const int* ndims, const void** in_data, const long* in_nbytes, int n_out,
-                                       const char** out_names, uint8_t* out, long cap) {
-  const long need = tca_kserve_request_size(model_name, model_version, id, n_in, in_names, in_dtypes, shapes, ndims,
-                                            in_nbytes, n_out, out_names);
+long msg_encode(const char* model_name, const char* model_version, const char* id, int n, const char** names,
+                const char** dtypes, const int64_t* shapes, const int* ndims, const void** data, const long* nbytes,
+                int n_req, const char** req_names, int req_field, int raw_field, uint8_t* out, long cap) {
+  const long need = msg_size(model_name, model_version, id, n, names, dtypes, shapes, ndims, nbytes, n_req,
+                             req_names, req_field, raw_field);
   if (need > cap) return -need;
   uint8_t* p = out;
   if (model_name && *model_name) p = put_bytes(p, 1, model_name, strlen(model_name));
   if (model_version && *model_version) p = put_bytes(p, 2, model_version, strlen(model_version));
   if (id && *id) p = put_bytes(p, 3, id, strlen(id));
   const int64_t* sh = shapes;
-  for (int i = 0; i < n_in; ++i) {
+  for (int i = 0; i < n; ++i) {
     long sp;
-    const long t = input_tensor_len(in_names[i], in_dtypes[i], sh, ndims[i], &sp);
+    const long t = input_tensor_len(names[i], dtypes[i], sh, ndims[i], &sp);
     p = put_tag(p, 5, 2);
     p = put_varint(p, t);
-    p = put_bytes(p, 1, in_names[i], strlen(in_names[i]));
-    p = put_bytes(p, 2, in_dtypes[i], strlen(in_dtypes[i]));
+    p = put_bytes(p, 1, names[i], strlen(names[i]));
+    p = put_bytes(p, 2, dtypes[i], strlen(dtypes[i]));
     if (ndims[i] > 0) {
       p = put_tag(p, 3, 2);
       p = put_varint(p, sp);
@@ -142,14 +146,163 @@ TCA_API long tca_kserve_encode_request(const char* model_name, const char* model
     }
     sh += ndims[i];
   }
-  for (int i = 0; i < n_out; ++i) {
-    const long l = strlen(out_names[i]);
-    p = put_tag(p, 6, 2);
+  for (int i = 0; i < n_req; ++i) {
+    const long l = strlen(req_names[i]);
+    p = put_tag(p, req_field, 2);
     p = put_varint(p, bytes_field_len(1, l));
-    p = put_bytes(p, 1, out_names[i], l);
+    p = put_bytes(p, 1, req_names[i], l);
   }
-  for (int i = 0; i < n_in; ++i) p = put_bytes(p, 7, in_data[i], in_nbytes[i]);
+  for (int i = 0; i < n; ++i) p = put_bytes(p, raw_field, data[i], nbytes[i]);
   return (long)(p - out);
+}
+
+// Tensor descriptor (field 5 payload) -> meta[0..5]: name off/len, dtype off/len, ndim, shape index.
+bool parse_tensor(const uint8_t* buf, const uint8_t* s, uint64_t l, long* m, int64_t* shapes, int max_dims,
+                  int* nd_total, int* err) {
+  Reader t{s, s + l};
+  m[0] = m[1] = m[2] = m[3] = 0;
+  m[4] = 0;
+  m[5] = *nd_total;
+  while (t.p < t.end && t.ok) {
+    const uint64_t tt = t.varint();
+    if (!t.ok) break;
+    const int f = (int)(tt >> 3), w = (int)(tt & 7);
+    if ((f == 1 || f == 2) && w == 2) {
+      uint64_t sl;
+      const uint8_t* q = t.take(&sl);
+      if (!t.ok) break;
+      m[f == 1 ? 0 : 2] = q - buf;
+      m[f == 1 ? 1 : 3] = (long)sl;
+    } else if (f == 3 && w == 2) {
+      uint64_t sl;
+      const uint8_t* q = t.take(&sl);
+      if (!t.ok) break;
+      Reader sr{q, q + sl};
+      while (sr.p < sr.end && sr.ok) {
+        const uint64_t d = sr.varint();
+        if (!sr.ok) { *err = -1; return false; }
+        if (*nd_total >= max_dims) { *err = -2; return false; }
+        shapes[(*nd_total)++] = (int64_t)d;
+        ++m[4];
+      }
+    } else if (f == 3 && w == 0) {
+      const uint64_t d = t.varint();
+      if (!t.ok) break;
+      if (*nd_total >= max_dims) { *err = -2; return false; }
+      shapes[(*nd_total)++] = (int64_t)d;
+      ++m[4];
+    } else if (!t.skip(w)) {
+      *err = -1;
+      return false;
+    }
+  }
+  if (!t.ok) { *err = -1; return false; }
+  return true;
+}
+
+}  // namespace
+
+// Size of the encoded request (for allocating the output buffer).
+TCA_API long tca_kserve_request_size(const char* model_name, const char* model_version, const char* id, int n_in,
+                                     const char** in_names, const char** in_dtypes, const int64_t* shapes,
+                                     const int* ndims, const long* in_nbytes, int n_out, const char** out_names) {
+  return msg_size(model_name, model_version, id, n_in, in_names, in_dtypes, shapes, ndims, in_nbytes, n_out,
+                  out_names, 6, 7);
+}
+
+// Encode; returns bytes written, or -(required size) if cap is too small.
+TCA_API long tca_kserve_encode_request(const char* model_name, const char* model_version, const char* id, int n_in,
+                                       const char** in_names, const char** in_dtypes, const int64_t* shapes,
+                                       const int* ndims, const void** in_data, const long* in_nbytes, int n_out,
+                                       const char** out_names, uint8_t* out, long cap) {
+  return msg_encode(model_name, model_version, id, n_in, in_names, in_dtypes, shapes, ndims, in_data, in_nbytes,
+                    n_out, out_names, 6, 7, out, cap);
+}
+
+// The server side: a ModelInferResponse straight from the output tensors'
+// memory (pinned staging the device results were copied into).
+TCA_API long tca_kserve_response_size(const char* model_name, const char* model_version, const char* id, int n,
+                                      const char** names, const char** dtypes, const int64_t* shapes,
+                                      const int* ndims, const long* nbytes) {
+  return msg_size(model_name, model_version, id, n, names, dtypes, shapes, ndims, nbytes, 0, nullptr, 6, 6);
+}
+
+TCA_API long tca_kserve_encode_response(const char* model_name, const char* model_version, const char* id, int n,
+                                        const char** names, const char** dtypes, const int64_t* shapes,
+                                        const int* ndims, const void** data, const long* nbytes, uint8_t* out,
+                                        long cap) {
+  return msg_encode(model_name, model_version, id, n, names, dtypes, shapes, ndims, data, nbytes, 0, nullptr, 6, 6,
+                    out, cap);
+}
+
+// Parse a serialized ModelInferRequest (the server's zero-copy decode).
+//   meta[k*8 + 0..5] input k: name off/len, dtype off/len, ndim, shape index; shapes[...] its dims
+//   raw[k*2 + 0..1]  raw_input_contents[k] offset/length
+//   req[k*2 + 0..1]  requested output k name offset/length
+//   counts[0..8]     n_inputs, n_raw, n_requested, model_name off/len, model_version off/len, id off/len
+// Returns 0, -1 malformed, -2 capacity exceeded.
+TCA_API int tca_kserve_parse_request(const uint8_t* buf, long len, int max_t, long* meta, int64_t* shapes,
+                                     int max_dims, long* raw, long* req, long* counts) {
+  if (!buf || len < 0 || max_t < 0 || max_dims < 0) return -1;
+  Reader r{buf, buf + len};
+  int n_in = 0, n_raw = 0, n_req = 0, nd_total = 0, err = 0;
+  for (int i = 0; i < 9; ++i) counts[i] = 0;
+  while (r.p < r.end && r.ok) {
+    const uint64_t tag = r.varint();
+    const int field = (int)(tag >> 3), wire = (int)(tag & 7);
+    if (!r.ok) break;
+    if ((field == 1 || field == 2 || field == 3) && wire == 2) {
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
+      counts[3 + 2 * (field - 1)] = s - buf;
+      counts[4 + 2 * (field - 1)] = (long)l;
+    } else if (field == 5 && wire == 2) {
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
+      if (n_in >= max_t) return -2;
+      if (!parse_tensor(buf, s, l, meta + n_in * 8, shapes, max_dims, &nd_total, &err)) return err;
+      ++n_in;
+    } else if (field == 6 && wire == 2) {
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
+      if (n_req >= max_t) return -2;
+      Reader t{s, s + l};
+      req[n_req * 2] = req[n_req * 2 + 1] = 0;
+      while (t.p < t.end && t.ok) {
+        const uint64_t tt = t.varint();
+        if (!t.ok) break;
+        if ((tt >> 3) == 1 && (tt & 7) == 2) {
+          uint64_t sl;
+          const uint8_t* q = t.take(&sl);
+          if (!t.ok) break;
+          req[n_req * 2] = q - buf;
+          req[n_req * 2 + 1] = (long)sl;
+        } else if (!t.skip((int)(tt & 7))) {
+          return -1;
+        }
+      }
+      if (!t.ok) return -1;
+      ++n_req;
+    } else if (field == 7 && wire == 2) {
+      uint64_t l;
+      const uint8_t* s = r.take(&l);
+      if (!r.ok) return -1;
+      if (n_raw >= max_t) return -2;
+      raw[n_raw * 2] = s - buf;
+      raw[n_raw * 2 + 1] = (long)l;
+      ++n_raw;
+    } else if (!r.skip(wire)) {
+      return -1;
+    }
+  }
+  if (!r.ok) return -1;
+  counts[0] = n_in;
+  counts[1] = n_raw;
+  counts[2] = n_req;
+  return 0;
 }
 
 // Parse a serialized ModelInferResponse.  For output k (< max_out):

@@ -63,15 +63,22 @@ def test_local_3d_engine_families_gpu(cuda, family, labels, dim):
         assert set(np.unique(p["pred_labels"])) <= labels
 
 
-def test_gpu_server_models_over_kserve(cuda):
+def test_served_path_matches_local_engines(cuda):
+    """The zero-copy served path (client GPU preprocess / voxelise -> pinned
+    staging -> C++ encoder -> KServe -> GPU model -> C++ encoder) keeps the
+    same detections as the local engines running the same weights."""
     from triton_client_amd.channel.grpc_channel import GRPCChannel
-    from triton_client_amd.clients import Pointpillars_client, Yolov5client
-    from triton_client_amd.inference import RemoteDetector2D, RemoteDetector3D
+    from triton_client_amd.clients import Yolov5client, client_for_model
+    from triton_client_amd.inference import LocalDetector2D, LocalDetector3D, RemoteDetector2D, RemoteDetector3D
+    from triton_client_amd.ops.golden import box_iou_np
     from triton_client_amd.server import KServeServer, ModelRepository
 
     repo = ModelRepository("cuda")
     repo.load("YOLOv5nCOCO")
     repo.load("pointpillar_kitti")
+    s2, s3 = repo.get("YOLOv5nCOCO"), repo.get("pointpillar_kitti")
+    frames = [camera_frame(480, 640, s) for s in (1, 2, 3)]
+    clouds = [_cloud(s, 64, 1875) for s in (4, 5)]
     with KServeServer(repo, "127.0.0.1:0") as srv:
         class F:
             model_version, batch_size = "", 1
@@ -80,11 +87,29 @@ def test_gpu_server_models_over_kserve(cuda):
         f2.model_name, f3.model_name = "YOLOv5nCOCO", "pointpillar_kitti"
         p = {"grpc_channel": srv.target}
         ch2, ch3 = GRPCChannel(p, f2), GRPCChannel(p, f3)
-        d2 = RemoteDetector2D(ch2, Yolov5client(), device=cuda).detect([camera_frame(480, 640, 1)])
-        assert len(d2) == 1 and d2[0].shape[1] == 6 and len(d2[0]) > 0
-        d3 = RemoteDetector3D(ch3, Pointpillars_client()).detect([_cloud(4, 64, 1875)])
-        assert len(d3[0]["pred_scores"]) > 0
+        r2 = RemoteDetector2D(ch2, Yolov5client(), device=cuda, mode="async").detect(frames)
+        cfg3 = ch3.get_metadata()["config_response"]
+        rem3 = RemoteDetector3D(ch3, client_for_model("pointpillar_kitti", getattr(cfg3, "config", cfg3)), device=cuda)
+        r3 = rem3.detect(clouds)
         st = ch3.model_statistics("pointpillar_kitti")
-        assert st.model_stats[0].inference_count >= 1
+        assert st.model_stats[0].inference_count >= 2
         ch2.close()
         ch3.close()
+    loc2 = LocalDetector2D(batch=1, device=cuda, letterbox=False, calibrate_target=None)
+    loc2.model = s2.model  # the served weights (calibrated head prior included)
+    l2 = loc2.detect(frames)
+    ok = tot_r = tot_l = 0
+    for a, b in zip(r2, l2):
+        tot_r, tot_l = tot_r + len(a), tot_l + len(b)
+        if len(a) and len(b):
+            iou = box_iou_np(a[:, :4], b[:, :4]) * (a[:, 5:6] == b[None, :, 5])
+            ok += int((iou.max(1) > 0.95).sum())
+    assert tot_r > 10 and ok >= 0.95 * tot_r and abs(tot_r - tot_l) <= max(2, tot_r // 30), (ok, tot_r, tot_l)
+    loc3 = LocalDetector3D(batch=1, device=cuda, calibrate_target=None)
+    loc3.model, loc3.cfg = s3.model, s3.cfg
+    l3 = loc3.detect(clouds)
+    for a, b in zip(r3, l3):
+        na, nb = len(a["pred_scores"]), len(b["pred_scores"])
+        assert na > 0 and abs(na - nb) <= max(2, na // 50), (na, nb)
+        np.testing.assert_allclose(np.sort(a["pred_scores"])[-20:], np.sort(b["pred_scores"])[-20:], rtol=1e-4,
+                                   atol=1e-5)

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Served-path throughput: the reference's architecture (client → KServe-v2
+gRPC → server → client), with this framework's zero-copy served path.
+
+Client (``inference/engines.py`` RemoteDetector2D/3D, ``--device cuda``):
+camera frame → pinned → GPU K1 preprocess → pinned staging → C++ encoder
+writes the request bytes directly (one host copy of the tensor); LiDAR
+PointCloud2 bytes → GPU unpack + spconv-order voxeliser → pinned staging →
+C++ encoder.  Requests go as a window of gRPC futures (``-a``).
+Server (``server/kserve_server.py`` ModelInferBytes): the C++ codec parses
+the request bytes into views, the model copies them once into pinned
+staging → DMA → captured GPU pipeline → pinned output staging → the C++
+encoder writes the response.  Client parses the response into views.
+
+Camera and LiDAR clients run concurrently (two threads: the reference runs
+them as two ROS nodes) against one in-process server on 127.0.0.1; one
+frame pair = one camera frame + one LiDAR sweep.  Prints one JSON line with
+frame pairs/s and per-stage milliseconds; ``--reference`` also runs
+tools/reference_equivalent.py's per-frame protocol for the ratio.
+
+    python tools/served_bench.py --frames 64 [--window 8] [--device cuda]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from types import SimpleNamespace
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--window", type=int, default=8, help="requests in flight per client")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--cam", default="720x1280")
+    ap.add_argument("--rings", type=int, default=64)
+    ap.add_argument("--columns", type=int, default=1875)
+    ap.add_argument("--workers", type=int, default=8, help="server threads")
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+    from triton_client_amd.clients import Yolov5client, client_for_model
+    from triton_client_amd.inference.engines import RemoteDetector2D, RemoteDetector3D
+    from triton_client_amd.ros import compat
+    from triton_client_amd.server import KServeServer, ModelRepository
+    from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+
+    H0, W0 = (int(v) for v in a.cam.split("x"))
+    repo = ModelRepository(a.device)
+    repo.load("YOLOv5nCOCO")
+    repo.load("pointpillar_kitti")
+    srv = KServeServer(repo, "127.0.0.1:0", max_workers=a.workers).start()
+
+    def channel(model):
+        flags = SimpleNamespace(model_name=model, model_version="", batch_size=64, verbose=False)
+        return GRPCChannel({"grpc_channel": srv.target}, flags)
+
+    ch2, ch3 = channel("YOLOv5nCOCO"), channel("pointpillar_kitti")
+    cr3 = ch3.get_metadata()["config_response"]
+    det2 = RemoteDetector2D(ch2, Yolov5client(), letterbox=False, conf_thres=0.3, mode="async", wire="raw",
+                            device=a.device)
+    det3 = RemoteDetector3D(ch3, client_for_model("pointpillar_kitti", getattr(cr3, "config", cr3)), z_offset=1.5,
+                            mode="async", wire="raw", device=a.device)
+    det2.window = det3.window = a.window
+    n = a.frames + a.warmup
+    frames = [camera_frame(H0, W0, s) for s in range(8)]
+    spec = LidarSpec(rings=a.rings, azimuth_steps=a.columns, sensor_height=3.23)
+    clouds = [compat.create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, 500 + s).tobytes(), np.float32).reshape(-1, 4))
+              for s in range(8)]
+
+    def run(det, items, count, out):
+        done = 0
+        while done < count:
+            k = min(a.window, count - done)
+            res = det.detect([items[(done + i) % len(items)] for i in range(k)])
+            done += k
+            out.append(res)
+
+    # warm-up (graph capture, calibration, connection setup), then timed
+    run(det2, frames, a.warmup, [])
+    run(det3, clouds, a.warmup, [])
+    det2.timer, det3.timer = {}, {}
+    r2, r3 = [], []
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=(det2, frames, a.frames, r2)),
+          threading.Thread(target=run, args=(det3, clouds, a.frames, r3))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    srv.stop()
+    stats = {m: repo.get(m).stats for m in ("YOLOv5nCOCO", "pointpillar_kitti")}
+
+    def ms(timer):
+        return {k: round(1e3 * float(np.sum(v)) / a.frames, 3) for k, v in timer.items()}
+
+    n2 = float(np.mean([len(d) for res in r2 for d in res]))
+    n3 = float(np.mean([len(d["pred_scores"]) for res in r3 for d in res]))
+    line = {"metric": "served-path frame pairs/s (camera + LiDAR over KServe gRPC, localhost)",
+            "value": round(a.frames / wall, 2), "unit": "frame pairs/s", "frames": a.frames, "window": a.window,
+            "wall_s": round(wall, 3), "device": a.device,
+            "client_ms_per_frame": {"camera": ms(det2.timer), "lidar": ms(det3.timer)},
+            "server_compute_ms_per_request": {m: round(s.compute_ns / max(1, s.inference_count) / 1e6, 3)
+                                              for m, s in stats.items()},
+            "avg_dets_per_frame": {"2d": round(n2, 1), "3d": round(n3, 1)},
+            "path": "GPU preprocess/voxelise -> pinned staging -> C++ KServe encoder -> gRPC -> C++ parse -> pinned "
+                    "-> GPU model -> pinned -> C++ encoder -> gRPC -> zero-copy response views"}
+    print(json.dumps(line), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(json.dumps(line) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

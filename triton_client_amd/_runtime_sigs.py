@@ -11,6 +11,9 @@ SIGS = {
     "tca_kserve_request_size": (L, [CP, CP, CP, I, PP, PP, P, P, P, I, PP]),
     "tca_kserve_encode_request": (L, [CP, CP, CP, I, PP, PP, P, P, P, P, I, PP, P, L]),
     "tca_kserve_parse_response": (I, [P, L, I, P, P, I, P, P]),
+    "tca_kserve_response_size": (L, [CP, CP, CP, I, PP, PP, P, P, P]),
+    "tca_kserve_encode_response": (L, [CP, CP, CP, I, PP, PP, P, P, P, P, P, L]),
+    "tca_kserve_parse_request": (I, [P, L, I, P, P, I, P, P, P]),
     # native RCCL communicator (csrc/runtime/rccl_comm.cpp)
     "tca_rccl_unique_id_bytes": (I, []),
     "tca_rccl_get_unique_id": (I, [P]),

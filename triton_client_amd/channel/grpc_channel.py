@@ -153,6 +153,14 @@ class GRPCChannel(BaseChannel):
         data = self._call(self._grpc_stub.ModelInferRaw, raw)
         return parse_response(data)
 
+    def send_raw(self, raw: bytes) -> ParsedResponse:
+        """One pre-encoded request (see channel.wire.encode_request) → parsed response."""
+        return parse_response(self._call(self._grpc_stub.ModelInferRaw, raw))
+
+    def send_raw_async(self, raw: bytes):
+        """grpc future of a pre-encoded request (``.result()`` → response bytes)."""
+        return self._grpc_stub.ModelInferRaw.future(raw, timeout=self.timeout_s)
+
     def server_metadata(self):
         return self._grpc_stub.ServerMetadata(pb.ServerMetadataRequest(), timeout=self.timeout_s)
 

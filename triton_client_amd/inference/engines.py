@@ -484,6 +484,23 @@ class LocalDetector3D(Detector3D):
 
 
 # =============================================================================== remote
+class _stage:
+    """Optional per-stage wall time: ``timer`` is a dict name -> [seconds]."""
+
+    def __init__(self, timer, name):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        if self.timer is not None:
+            import time as _t
+            self.t0 = _t.perf_counter()
+
+    def __exit__(self, *exc):
+        if self.timer is not None:
+            import time as _t
+            self.timer.setdefault(self.name, []).append(_t.perf_counter() - self.t0)
+
+
 _NP_OF = {"FP32": np.float32, "FP16": np.float16, "UINT8": np.uint8, "INT8": np.int8, "FP64": np.float64,
           "INT32": np.int32, "INT64": np.int64}
 
@@ -508,6 +525,31 @@ class _RemoteBase:
         cfg = md["config_response"]
         self.model_metadata = md["metadata_response"]
         self.model_config = cfg.config if hasattr(cfg, "config") else cfg
+
+    def _encode(self, inputs, outputs: Sequence[str], rid: str = "") -> bytes:
+        """Raw wire: the request bytes, each tensor (numpy or pinned CPU torch
+        staging) copied once by the C++ encoder."""
+        from ..channel.wire import encode_request
+
+        return encode_request(self.channel.model_name, [(n, a) for n, _, a in inputs], outputs,
+                              self.channel.model_version, rid, [d for _, d, _ in inputs])
+
+    def _send(self, raws: List[bytes]) -> list:
+        """Pre-encoded requests → ParsedResponses (sync, or a window of futures)."""
+        from ..channel.wire import parse_response
+
+        ch = self.channel
+        if self.mode != "async":
+            return [ch.send_raw(r) for r in raws]
+        res, fl = [None] * len(raws), []
+        for i, r in enumerate(raws):
+            fl.append((i, ch.send_raw_async(r)))
+            if len(fl) >= self.window:
+                j, f = fl.pop(0)
+                res[j] = parse_response(f.result())
+        for j, f in fl:
+            res[j] = parse_response(f.result())
+        return res
 
     def _request(self, inputs: Sequence[Tuple[str, str, np.ndarray]], outputs: Sequence[str], rid: str = ""):
         from ..proto import service_pb2 as pb
@@ -594,17 +636,47 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         self.device = _device(device)
         self.names = self.post.load_class_names(names_file) if names_file else self.post.load_class_names()
 
+    _TORCH_OF = {"FP32": torch.float32, "FP16": torch.float16, "UINT8": torch.uint8}
+
+    def _gpu_staging(self, hw):
+        """Per source geometry: pinned frame upload buffer, device input, and
+        the pinned staging the model input lands in (one D2H DMA)."""
+        st = getattr(self, "_st", None)
+        if st is None or st[0] != hw:
+            H0, W0 = hw
+            tdt = self._TORCH_OF.get(self.dtype, torch.float32)
+            shape = (self.h, self.w, 3) if self.nhwc else (3, self.h, self.w)
+            st = (hw, torch.empty((1, H0, W0, 3), dtype=torch.uint8).pin_memory(),
+                  torch.empty((1, H0, W0, 3), dtype=torch.uint8, device=self.device),
+                  torch.empty(((1,) if self.batch_dim else ()) + shape, dtype=tdt).pin_memory(), tdt)
+            self._st = st
+        return st
+
     def _prep(self, frame: np.ndarray):
-        t = torch.from_numpy(np.array(frame[..., :3], np.uint8))
+        """→ (model input, xform).  GPU: frame → pinned → device → K1 preprocess
+        → pinned staging (returned as a CPU torch tensor the wire encoder reads
+        directly: no NumPy round trip, no intermediate host copy)."""
         if self.device.type == "cuda":
-            t = t.to(self.device, non_blocking=True)
+            _, pin_in, dev_in, pin_out, tdt = self._gpu_staging(tuple(frame.shape[:2]))
+            pin_in[0].numpy()[...] = frame[..., :3]
+            dev_in.copy_(pin_in, non_blocking=True)
+            x, xf = preprocess(dev_in, (self.h, self.w), self.mode2d, self.scaling, torch.float32,
+                               "NHWC" if self.nhwc else "NCHW")
+            if self.nhwc:
+                x = x.permute(0, 2, 3, 1)
+            if not self.batch_dim:
+                x = x[0]
+            pin_out.copy_(x.to(tdt), non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return pin_out, xf
+        t = torch.from_numpy(np.array(frame[..., :3], np.uint8))
         x, xf = preprocess(t, (self.h, self.w), self.mode2d, self.scaling, torch.float32,
                            "NHWC" if self.nhwc else "NCHW")
         if self.nhwc:
             x = x.permute(0, 2, 3, 1)
         if not self.batch_dim:
             x = x[0]
-        a = x.cpu().numpy()
+        a = x.numpy()
         a = np.ascontiguousarray(a.astype(_NP_OF.get(self.dtype, np.float32), copy=False))
         return a, xf
 
@@ -618,10 +690,26 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
 
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
         from ..utils.trace import trace_range
-        with trace_range("preprocess"):
-            preps = [self._prep(f) for f in frames]
-        with trace_range("rpc"):
-            resps = self._run([[(self.input_name, self.dtype, a)] for a, _ in preps], self.requested)
+        timer = getattr(self, "timer", None)
+        if self.wire == "raw" and self.mode != "stream":
+            # prepare + encode frame by frame: the staging buffer is reused, each
+            # request's bytes are complete before the next frame is prepared
+            xfs, raws = [], []
+            for i, f in enumerate(frames):
+                with trace_range("preprocess"), _stage(timer, "preprocess"):
+                    a, xf = self._prep(f)
+                with _stage(timer, "encode"):
+                    raws.append(self._encode([(self.input_name, self.dtype, a)], self.requested, str(i)))
+                xfs.append(xf)
+            with trace_range("rpc"), _stage(timer, "rpc"):
+                resps = self._send(raws)
+            preps = [(None, xf) for xf in xfs]
+        else:
+            with trace_range("preprocess"):
+                preps = [self._prep(f) for f in frames]
+            preps = [(a.numpy() if isinstance(a, torch.Tensor) else a, xf) for a, xf in preps]
+            with trace_range("rpc"):
+                resps = self._run([[(self.input_name, self.dtype, a)] for a, _ in preps], self.requested)
         out = []
         for (a, xf), r in zip(preps, resps):
             d = self._extract(r)
@@ -658,6 +746,11 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
 
             self.pre = type(self.pre)(client.voxel_cfg, device) if isinstance(self.pre, PointpillarPreprocess) \
                 else self.pre
+        else:
+            from ..clients.detector_3d_client import PointpillarPreprocess
+
+            if isinstance(self.pre, PointpillarPreprocess) and str(device) != "cpu":
+                self.pre = type(self.pre)(self.pre.cfg, device)
         self.names = self.post.load_class_names()
         self.z_offset, self.normalize = z_offset, normalize_intensity
         self.out_names = [o["name"] for o in self.outputs]
@@ -665,9 +758,33 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
         if ch.input is not None:
             _set_outputs(ch, self.out_names)
 
+    def _detect_gpu_raw(self, clouds) -> List[dict]:
+        """GPU unpack + voxelise into pinned staging, one C++-encoded request per
+        cloud (no NumPy round trip of points or voxels)."""
+        timer = getattr(self, "timer", None)
+        keys = [_voxel_key(spec["name"], k) for k, spec in enumerate(self.inputs)]
+        dts = {key: spec["dtype"] for key, spec in zip(keys, self.inputs)}
+        raws, keep = [], []
+        for i, c in enumerate(clouds):
+            with _stage(timer, "preprocess"):
+                d = self.pre.filter_cloud_gpu(c, self.normalize, self.z_offset, dts)
+            if d["voxels"].shape[0] == 0:
+                continue
+            with _stage(timer, "encode"):
+                raws.append(self._encode([(spec["name"], spec["dtype"], d[key]) for key, spec in zip(keys, self.inputs)],
+                                         self.out_names, str(i)))
+            keep.append(i)
+        with _stage(timer, "rpc"):
+            resps = self._send(raws)
+        return keep, resps
+
     def detect(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
         from ..ros.compat import cloud_to_numpy
 
+        if (self.wire == "raw" and self.mode != "stream" and getattr(self.pre, "device", None) is not None
+                and self.pre.device.type == "cuda" and hasattr(self.pre, "filter_cloud_gpu")):
+            keep, resps = self._detect_gpu_raw(clouds)
+            return self._outputs(clouds, keep, resps)
         batches, empty = [], []
         for c in clouds:
             pts = cloud_to_numpy(c, normalize_intensity=self.normalize, z_offset=self.z_offset)
@@ -678,6 +795,9 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
                             for k, spec in enumerate(self.inputs)])
         keep = [i for i, e in enumerate(empty) if not e]
         resps = self._run([batches[i] for i in keep], self.out_names)
+        return self._outputs(clouds, keep, resps)
+
+    def _outputs(self, clouds, keep, resps) -> List[dict]:
         out = [_empty3d() for _ in clouds]
         for i, r in zip(keep, resps):
             d = self.post.extract_boxes(r)

@@ -88,7 +88,8 @@ def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], cor
     for n in names:
         if n not in outputs:
             raise InferError(f"unknown output '{n}' for model '{model.name}'")
-        a = np.ascontiguousarray(outputs[n])
+        a = outputs[n]
+        a = np.ascontiguousarray(a.numpy() if hasattr(a, "numpy") and not isinstance(a, np.ndarray) else a)
         t = resp.outputs.add(name=n, datatype=_kserve_dtype(a))
         t.shape.extend(a.shape)
         b = a.tobytes()
@@ -178,8 +179,9 @@ class GRPCInferenceServicer:
             ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
         try:
             inputs = decode_inputs(req)
-            outputs = m(inputs, [o.name for o in req.outputs])
-            resp = encode_response(m, req, outputs, corrupt=self.fault.roll(self.fault.corrupt_rate))
+            corrupt = self.fault.roll(self.fault.corrupt_rate)
+            resp = m(inputs, [o.name for o in req.outputs],
+                     encode=lambda outputs: encode_response(m, req, outputs, corrupt=corrupt))
         except InferError as e:
             if self.metrics:
                 self.metrics.request(m.name, False, time.perf_counter() - t0)
@@ -190,6 +192,46 @@ class GRPCInferenceServicer:
 
     def ModelInfer(self, req, ctx):
         return self._infer(req, ctx)
+
+    def ModelInferBytes(self, data: bytes, ctx) -> bytes:
+        """ModelInfer on the raw wire bytes through the C++ codec: inputs are
+        views into the request (no protobuf objects, no tensor copies until
+        the model stages them for the device), the response is written
+        straight from the output tensors."""
+        from ..channel.wire import encode_response, parse_request
+
+        t0 = time.perf_counter()
+        try:
+            req = parse_request(data)
+        except ValueError as e:
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        m = self._model(req.model_name, req.model_version, ctx)
+        if self.fault.delay_s:
+            time.sleep(self.fault.delay_s)
+        if self.fault.roll(self.fault.drop_rate):
+            ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
+        try:
+            for name, a in req.inputs.items():
+                if a.size == 0 and 0 not in a.shape:
+                    raise InferError(f"input '{name}': no raw contents")
+            corrupt = self.fault.roll(self.fault.corrupt_rate)
+
+            def encode(outputs):
+                names = req.outputs or list(outputs.keys())
+                for n in names:
+                    if n not in outputs:
+                        raise InferError(f"unknown output '{n}' for model '{m.name}'")
+                outs = [(n, np.zeros(tuple(outputs[n].shape), np.asarray(outputs[n]).dtype) if corrupt else outputs[n])
+                        for n in names]
+                return encode_response(m.name, outs, m.version, req.id)
+            resp = m(req.inputs, req.outputs, encode=encode)
+        except InferError as e:
+            if self.metrics:
+                self.metrics.request(m.name, False, time.perf_counter() - t0)
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        if self.metrics:
+            self.metrics.request(m.name, True, time.perf_counter() - t0)
+        return resp
 
     def ModelStreamInfer(self, req_iter, ctx):
         for req in req_iter:
@@ -214,10 +256,14 @@ class _StreamCtx:
         raise _StreamAbort(details)
 
 
-def _handlers(servicer: GRPCInferenceServicer):
+def _handlers(servicer: GRPCInferenceServicer, raw_infer: bool = True):
     from ..proto import SERVICE_METHODS
     h = {}
     for rpc, req, resp, cs, ss in SERVICE_METHODS:
+        if rpc == "ModelInfer" and raw_infer:  # bytes in, bytes out through the C++ codec
+            h[rpc] = grpc.unary_unary_rpc_method_handler(servicer.ModelInferBytes, request_deserializer=None,
+                                                         response_serializer=None)
+            continue
         fn = getattr(servicer, rpc)
         de = getattr(pb, req).FromString
         ser = getattr(pb, resp).SerializeToString
@@ -231,7 +277,9 @@ def _handlers(servicer: GRPCInferenceServicer):
 class KServeServer:
     def __init__(self, repo: ModelRepository, address: str = "127.0.0.1:8001", max_workers: int = 8,
                  max_message_bytes: int = 512 << 20, fault: Optional[FaultInjector] = None,
-                 metrics_port: Optional[int] = None):
+                 metrics_port: Optional[int] = None, raw_infer: bool = True):
+        """raw_infer: serve ModelInfer through the C++ codec on the wire bytes
+        (False: the protobuf runtime, as a Triton-like reference path)."""
         self.repo = repo
         self.address = address
         metrics = None
@@ -242,7 +290,7 @@ class KServeServer:
         opts = [("grpc.max_send_message_length", max_message_bytes),
                 ("grpc.max_receive_message_length", max_message_bytes)]
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers), options=opts)
-        self.server.add_generic_rpc_handlers((_handlers(self.servicer),))
+        self.server.add_generic_rpc_handlers((_handlers(self.servicer, raw_infer),))
         self.port = self.server.add_insecure_port(address)
         if self.port == 0:
             raise RuntimeError(f"could not bind {address}")

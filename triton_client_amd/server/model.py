@@ -121,12 +121,17 @@ class ServedModel(ABC):
                 if d != -1 and d != s:
                     raise InferError(f"input '{spec.name}': shape {list(a.shape)} does not match {ref}")
 
-    def __call__(self, inputs: Dict[str, np.ndarray], requested: Sequence[str]) -> Dict[str, np.ndarray]:
+    def __call__(self, inputs: Dict[str, np.ndarray], requested: Sequence[str], encode=None):
+        """Run the model; ``encode(outputs)`` (the response serialiser) runs
+        under the model lock too, because GPU models return their reusable
+        pinned output staging, which the next request overwrites."""
         t0 = time.perf_counter_ns()
         try:
             self.validate(inputs)
             with self._lock:
                 out = self.execute(inputs, requested)
+                if encode is not None:
+                    out = encode(out)
         except Exception:
             with self.stats.lock:
                 self.stats.fail_count += 1
