@@ -5,22 +5,24 @@
 # runs the in-tree HIP pipelines; the repository carries each model's KServe
 # contract and, optionally, its state_dict (path or file/http(s)/s3 URI).
 #
-#   ./deploy.sh [-m MODELS] [-w MODEL=URI]... [-r user@host] [-d REMOTE_DIR] [OUT_DIR]
+#   ./deploy.sh [-m MODELS] [-w MODEL=URI]... [-s MODEL=SHA256]... [-r user@host] [-d REMOTE_DIR] [OUT_DIR]
 #
 # No credentials are read or written here; s3:// weights are fetched by the
-# server at load time with env-provided keys (utils/model_store.py).
+# server at load time with env-provided keys (utils/model_store.py) and
+# checked against the -s sha256 (local files get theirs recorded automatically).
 set -euo pipefail
 MODELS="YOLOv5nCOCO,pointpillar_kitti"
 REMOTE=""
 REMOTE_DIR="/models"
 WEIGHTS=()
-while getopts "m:w:r:d:h" opt; do
+while getopts "m:w:s:r:d:h" opt; do
   case "$opt" in
     m) MODELS="$OPTARG" ;;
     w) WEIGHTS+=(--weights "$OPTARG") ;;
+    s) WEIGHTS+=(--weights-sha256 "$OPTARG") ;;
     r) REMOTE="$OPTARG" ;;
     d) REMOTE_DIR="$OPTARG" ;;
-    *) sed -n '2,11p' "$0"; exit 0 ;;
+    *) sed -n '2,12p' "$0"; exit 0 ;;
   esac
 done
 shift $((OPTIND - 1))

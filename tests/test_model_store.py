@@ -8,6 +8,7 @@ import io
 import json
 import threading
 import urllib.parse
+import urllib.request
 
 import pytest
 import torch
@@ -27,6 +28,7 @@ def _state_bytes():
 class _Mock(http.server.BaseHTTPRequestHandler):
     blob = b""
     log = []
+    redirect_to = ""
 
     def log_message(self, *a):
         pass
@@ -53,6 +55,15 @@ class _Mock(http.server.BaseHTTPRequestHandler):
         self._send(403, b"denied")
 
     def do_GET(self):
+        if self.path.startswith("/redirect/"):  # -> the other server (another host:port)
+            self.send_response(302)
+            self.send_header("Location", self.redirect_to + "/open/w.pt")
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+            return None
+        if self.path.startswith("/open/"):
+            self.log.append(("open", self.headers.get("Authorization"), self.headers.get("x-amz-security-token")))
+            return self._send(200, self.blob)
         if self.path.startswith("/http/"):
             if self.headers.get("Authorization") != "Bearer tok-1":
                 return self._send(401, b"no")
@@ -79,8 +90,10 @@ def server(tmp_path, monkeypatch):
     t = threading.Thread(target=srv.serve_forever, daemon=True)
     t.start()
     monkeypatch.setenv("TCA_MODEL_CACHE", str(tmp_path / "cache"))
-    for k in ("AWS_ACCESS_KEY_ID", "AWS_SECRET_ACCESS_KEY", "AWS_SESSION_TOKEN", "TCA_MODEL_STORE_TOKEN"):
+    for k in ("AWS_ACCESS_KEY_ID", "AWS_SECRET_ACCESS_KEY", "AWS_SESSION_TOKEN", "TCA_MODEL_STORE_TOKEN",
+              "TCA_MODEL_STORE_TOKEN_HOSTS"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("TCA_MODEL_STORE_ALLOW_HTTP", "1")  # the mocks speak plain http
     yield f"http://127.0.0.1:{srv.server_address[1]}", sd, blob
     srv.shutdown()
     srv.server_close()
@@ -107,9 +120,52 @@ def test_local_and_file_uri(tmp_path):
 def test_http_bearer_and_cache(server, monkeypatch):
     base, sd, blob = server
     monkeypatch.setenv("TCA_MODEL_STORE_TOKEN", "tok-1")
+    monkeypatch.setenv("TCA_MODEL_STORE_TOKEN_HOSTS", base.split("//", 1)[1])
     _same(ms.load_state_dict(base + "/http/w.pt", sha256=hashlib.sha256(blob).hexdigest()), sd)
-    ms.load_state_dict(base + "/http/w.pt")  # cached: no second GET
+    ms.load_state_dict(base + "/http/w.pt")  # cached (sidecar sha matches): no second GET
     assert _Mock.log == [("http",)]
+    p = ms.resolve(base + "/http/w.pt")
+    p.write_bytes(b"tampered")  # a cache entry that no longer matches its sidecar is fetched again
+    _same(ms.load_state_dict(base + "/http/w.pt"), sd)
+    ms.resolve(base + "/http/w.pt", refresh=True)
+    assert _Mock.log == [("http",)] * 3
+    with pytest.raises(ms.ModelStoreError, match="sha256 mismatch"):
+        ms.resolve(base + "/http/w.pt", sha256="0" * 64)
+
+
+def test_token_only_to_allowlisted_https(server, monkeypatch):
+    base, _, _ = server
+    monkeypatch.setenv("TCA_MODEL_STORE_TOKEN", "tok-1")
+    with pytest.raises(Exception, match="401"):  # host not allow-listed: no token sent
+        ms.resolve(base + "/http/w.pt")
+    monkeypatch.setenv("TCA_MODEL_STORE_TOKEN_HOSTS", base.split("//", 1)[1])
+    monkeypatch.delenv("TCA_MODEL_STORE_ALLOW_HTTP")
+    with pytest.raises(ms.ModelStoreError, match="refusing to send"):
+        ms.resolve(base + "/http/w.pt")
+    monkeypatch.setenv("TCA_S3_ENDPOINT", base)
+    with pytest.raises(ms.ModelStoreError, match="not https"):
+        ms.resolve("s3://models/pp/weights.pt")
+
+
+def test_redirect_strips_credentials(server, monkeypatch):
+    """urllib copies headers onto a redirected request; the store's opener drops
+    Authorization and x-amz-* before following a redirect to another host."""
+    base, sd, blob = server
+    other = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _Mock)
+    threading.Thread(target=other.serve_forever, daemon=True).start()
+    try:
+        _Mock.redirect_to = f"http://127.0.0.1:{other.server_address[1]}"
+        monkeypatch.setenv("TCA_MODEL_STORE_TOKEN", "tok-1")
+        monkeypatch.setenv("TCA_MODEL_STORE_TOKEN_HOSTS", base.split("//", 1)[1])
+        _same(ms.load_state_dict(base + "/redirect/w.pt"), sd)
+        assert _Mock.log == [("open", None, None)]
+        req = urllib.request.Request(base + "/redirect/x", headers={"Authorization": "AWS4 x", "x-amz-security-token": "s"})
+        with ms._open(req, 10) as r:
+            assert r.read() == blob
+        assert _Mock.log[-1] == ("open", None, None)
+    finally:
+        other.shutdown()
+        other.server_close()
 
 
 def test_s3_oidc_sts_sigv4(server, monkeypatch):
@@ -161,6 +217,7 @@ def test_repository_export_roundtrip_with_weights(tmp_path):
     assert (tmp_path / "repo" / "YOLOv5nCOCO" / "1" / "model.pt").is_file()
     lazy = ModelRepository.from_directory(str(tmp_path / "repo"), "cpu", load=False)
     assert lazy.get("pointpillar_kitti").weights == "s3://models/pp.pt"
+    assert lazy.get("YOLOv5nCOCO").weights_sha256 == hashlib.sha256(wpath.read_bytes()).hexdigest()
     repo = ModelRepository.from_directory(str(tmp_path / "repo"), "cpu", load=False)
     m = repo.load("YOLOv5nCOCO")
     ref = YoloV5Model("YOLOv5nCOCO", "n", 80, 640, device="cpu", seed=123)
@@ -169,6 +226,20 @@ def test_repository_export_roundtrip_with_weights(tmp_path):
     with torch.no_grad():
         for a, b in zip(m.model(x), ref.model(x)):
             assert torch.equal(a, b)
+    # a swapped weights file no longer matches the recorded sha256: refused at load
+    torch.save(build_yolov5("n", 80, 640, 7).state_dict(), tmp_path / "repo" / "YOLOv5nCOCO" / "1" / "model.pt")
+    bad = ModelRepository.from_directory(str(tmp_path / "repo"), "cpu", load=False)
+    with pytest.raises(ms.ModelStoreError, match="sha256"):
+        bad.load("YOLOv5nCOCO")
+
+
+def test_export_escapes_uri_and_records_sha(tmp_path):
+    from triton_client_amd.server.repository import ModelRepository, export_repository
+
+    uri = 'https://store.example/a"b\\c\n}.pt'
+    export_repository(["second_iou"], str(tmp_path / "r"), {"second_iou": uri}, {"second_iou": "AB" * 32})
+    m = ModelRepository.from_directory(str(tmp_path / "r"), "cpu", load=False).get("second_iou")
+    assert m.weights == uri and m.weights_sha256 == "ab" * 32
 
 
 def test_deploy_script_writes_repository(tmp_path):

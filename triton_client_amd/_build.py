@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import json
 import os
 import shutil
 import subprocess
@@ -56,8 +57,28 @@ def _compile(src: str, obj: str, flags: List[str]) -> str:
     return obj
 
 
+def _stamp_changed(name: str, flags: List[str], link: List[str]) -> bool:
+    """mtimes alone would reuse objects built for another arch / flag set (e.g.
+    host objects copied into an image): the compiler, arch and flags of the
+    last build are kept in a stamp next to the objects; any change rebuilds."""
+    want = json.dumps({"hipcc": HIPCC, "arch": ARCH, "common": COMMON_FLAGS, "flags": flags, "link": link},
+                      sort_keys=True)
+    stamp = os.path.join(BUILDDIR, name + ".stamp")
+    try:
+        with open(stamp) as f:
+            same = f.read() == want
+    except OSError:
+        same = False
+    if not same:
+        os.makedirs(BUILDDIR, exist_ok=True)
+        with open(stamp, "w") as f:
+            f.write(want)
+    return not same
+
+
 def _build_lib(name: str, sources: List[str], flags: List[str], link: List[str], jobs: int, force: bool) -> str:
     out = os.path.join(LIBDIR, name)
+    force = _stamp_changed(name, flags, link) or force
     hdrs = _headers()
     objs = []
     todo = []

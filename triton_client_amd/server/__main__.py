@@ -18,13 +18,17 @@ def main(argv=None):
                     help="write a Triton-layout repository for --models into DIR and exit")
     ap.add_argument("--weights", action="append", default=[], metavar="MODEL=URI",
                     help="with --export-repository: weights for MODEL (path, file/http(s)/s3 URI); repeatable")
+    ap.add_argument("--weights-sha256", action="append", default=[], metavar="MODEL=HEX",
+                    help="with --export-repository: expected sha256 of MODEL's weights (written into config.pbtxt)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     if args.export_repository:
         from .repository import export_repository
 
         w = dict(kv.split("=", 1) for kv in args.weights)
-        for d in export_repository(filter(None, (m.strip() for m in args.models.split(","))), args.export_repository, w):
+        sha = dict(kv.split("=", 1) for kv in args.weights_sha256)
+        names = filter(None, (m.strip() for m in args.models.split(",")))
+        for d in export_repository(names, args.export_repository, w, sha):
             print(d)
         return
     if args.model_repository:

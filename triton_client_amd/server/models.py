@@ -66,7 +66,7 @@ class YoloV5Model(ServedModel):
 
         model = build_yolov5(self.variant, self.nc, self.img, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             self.pipe = CameraPipeline(model, batch=1, src_hw=(self.img, self.img), img_hw=(self.img, self.img),
                                        mode="stretch", device=self.device)
@@ -146,7 +146,7 @@ class PointPillarsModel(ServedModel):
         from ..models.pointpillars import build_pointpillars
         model = build_pointpillars(self.cfg, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             from ..pipelines.lidar import LidarPipeline
             from ..ops.lidar import PillarEncoder
@@ -270,7 +270,7 @@ class SecondIoUModel(ServedModel):
 
         model = build_second_iou(self.cfg, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             from ..pipelines.second import SecondPipeline
             from ..utils.synthetic import LidarSpec, lidar_sweep
@@ -376,7 +376,7 @@ class CenterPointModel(ServedModel):
 
         model = build_centerpoint(self.cfg, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             from ..pipelines.centerpoint import CenterPointPipeline
             from ..utils.synthetic import LidarSpec, lidar_sweep
@@ -482,7 +482,7 @@ class DetectronModel(ServedModel):
 
         model = build_detectron(self.cfg, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             from ..pipelines.detectron import DetectronPipeline
             from ..utils.synthetic import camera_frame
@@ -555,7 +555,7 @@ class YoloV4Model(ServedModel):
 
         model = build_yolov4(self.nc, self.img, self.seed)
         if self.weights:
-            model.load_state_dict(load_state_dict(self.weights))
+            model.load_state_dict(load_state_dict(self.weights, getattr(self, "weights_sha256", None)))
         if self.device.type == "cuda":
             from ..pipelines.yolov4 import Yolov4Pipeline
             from ..utils.synthetic import camera_frame

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import os
 import threading
+from pathlib import Path
 from typing import Callable, Dict, Iterable, List, Optional, Tuple
 
 from .model import EchoModel, ServedModel
@@ -102,19 +103,24 @@ def register_factory(name: str, factory: Factory) -> None:
     FACTORIES[name] = factory
 
 
-def _weights_for(model_dir: str, cfg) -> Optional[str]:
-    """Weights of one repository entry: ``parameters { key: "weights" }`` (path or
-    file/http(s)/s3 URI, see ``utils/model_store.py``), else the highest numeric
-    version directory holding ``model.pt`` (Triton's ``<model>/<version>/`` layout)."""
+def _weights_for(model_dir: str, cfg) -> Tuple[Optional[str], Optional[str]]:
+    """(weights, sha256) of one repository entry.  Weights: ``parameters { key:
+    "weights" }`` (path or file/http(s)/s3 URI, see ``utils/model_store.py``), else
+    the highest numeric version directory holding ``model.pt`` (Triton's
+    ``<model>/<version>/`` layout).  sha256: ``parameters { key: "weights_sha256" }``
+    — checked by the model store before the file is loaded (and before a cached
+    download is reused)."""
+    sha = cfg.parameters["weights_sha256"].string_value if "weights_sha256" in cfg.parameters else ""
+    sha = sha or None
     if "weights" in cfg.parameters and cfg.parameters["weights"].string_value:
         w = cfg.parameters["weights"].string_value
-        return w if "://" in w or os.path.isabs(w) else os.path.join(model_dir, w)
+        return (w if "://" in w or os.path.isabs(w) else os.path.join(model_dir, w)), sha
     versions = sorted((int(v) for v in os.listdir(model_dir) if v.isdigit()), reverse=True)
     for v in versions:
         f = os.path.join(model_dir, str(v), "model.pt")
         if os.path.isfile(f):
-            return f
-    return None
+            return f, sha
+    return None, sha
 
 
 class ModelRepository:
@@ -211,16 +217,21 @@ class ModelRepository:
                 m = SecondIoUModel(name, device=device)
             else:
                 continue
-            weights = _weights_for(os.path.join(path, entry), cfg)
+            weights, sha = _weights_for(os.path.join(path, entry), cfg)
             if weights and hasattr(m, "weights"):
-                m.weights = weights
+                m.weights, m.weights_sha256 = weights, sha
             repo.add(m, load=load)
         return repo
 
 
-def export_repository(names: Iterable[str], out_dir: str, weights: Optional[Dict[str, str]] = None) -> List[str]:
+def export_repository(names: Iterable[str], out_dir: str, weights: Optional[Dict[str, str]] = None,
+                      weights_sha256: Optional[Dict[str, str]] = None) -> List[str]:
     """Write a Triton-layout model repository (``<name>/config.pbtxt`` plus
     ``<name>/1/model.pt`` when weights are given) for the named served models.
+    A local weights file is copied and its sha256 recorded as the
+    ``weights_sha256`` parameter; a remote URI is referenced with the sha256
+    given in ``weights_sha256`` (strongly advised: without it the server trusts
+    whatever the URI serves).
 
     This is the deploy step of the reference's ``deploy.sh:1-65`` (export the
     model, write its ``config.pbtxt`` into the server's repository), minus the
@@ -235,17 +246,27 @@ def export_repository(names: Iterable[str], out_dir: str, weights: Optional[Dict
     for name in names:
         if name not in FACTORIES:
             raise KeyError(f"no factory for model '{name}'")
+        from ..utils.model_store import _sha256_file
+
         m = FACTORIES[name](device="cpu")
         d = os.path.join(out_dir, name)
         os.makedirs(os.path.join(d, "1"), exist_ok=True)
-        with open(os.path.join(d, "config.pbtxt"), "w") as f:
-            f.write(text_format.MessageToString(m.config()))
+        cfg = m.config()
         w = (weights or {}).get(name)
+        sha = (weights_sha256 or {}).get(name)
         if w:
             if "://" in w:  # remote: reference it, the server fetches it at load time
-                with open(os.path.join(d, "config.pbtxt"), "a") as f:
-                    f.write(f'parameters {{\n  key: "weights"\n  value {{\n    string_value: "{w}"\n  }}\n}}\n')
+                cfg.parameters["weights"].string_value = w  # text_format escapes it
             else:
-                shutil.copyfile(w, os.path.join(d, "1", "model.pt"))
+                dst = os.path.join(d, "1", "model.pt")
+                shutil.copyfile(w, dst)
+                got = _sha256_file(Path(dst))
+                if sha and sha.lower() != got:
+                    raise ValueError(f"{w}: sha256 {got} != expected {sha}")
+                sha = got
+            if sha:
+                cfg.parameters["weights_sha256"].string_value = sha.lower()
+        with open(os.path.join(d, "config.pbtxt"), "w") as f:
+            f.write(text_format.MessageToString(cfg))
         written.append(d)
     return written

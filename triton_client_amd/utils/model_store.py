@@ -15,9 +15,10 @@ URI                        how it is fetched
 =========================  ====================================================
 ``/path`` / ``file://``    used in place
 ``http(s)://…``            GET; ``Authorization: Bearer $TCA_MODEL_STORE_TOKEN``
-                           when that variable is set
+                           only to hosts listed in ``$TCA_MODEL_STORE_TOKEN_HOSTS``
+                           (comma-separated ``host[:port]``) and only over https
 ``s3://bucket/key``        SigV4-signed GET against ``$TCA_S3_ENDPOINT``
-                           (path-style, MinIO-compatible).  Credentials:
+                           (path-style, MinIO-compatible; https).  Credentials:
                            ``AWS_ACCESS_KEY_ID`` / ``AWS_SECRET_ACCESS_KEY`` /
                            ``AWS_SESSION_TOKEN``, or — when ``TCA_OIDC_TOKEN_URL``
                            is set — an OIDC token (client-credentials grant, or
@@ -25,9 +26,17 @@ URI                        how it is fetched
                            exchanged at the endpoint's STS for temporary keys.
 =========================  ====================================================
 
+Credentials never follow a redirect: every fetch goes through an opener whose
+redirect handler drops ``Authorization`` and ``x-amz-*`` headers and refuses an
+https → http downgrade.  Plain-http token / SigV4 traffic (a MinIO on a private
+network) needs ``TCA_MODEL_STORE_ALLOW_HTTP=1``.
+
 Downloads land in a content cache (``$TCA_MODEL_CACHE`` or
-``~/.cache/triton_client_amd/models``) via write-to-temp + atomic rename, and
-are checked against an optional sha256.  ``load_state_dict`` only ever calls
+``~/.cache/triton_client_amd/models``) via write-to-temp + atomic rename, with
+a ``.sha256`` sidecar written at download time.  A cached copy is reused only
+if it still matches the expected sha256 (when one is given — the model
+repository carries it as the ``weights_sha256`` parameter) or its sidecar;
+``refresh=True`` always fetches again.  ``load_state_dict`` only ever calls
 ``torch.load(..., weights_only=True)``.
 """
 from __future__ import annotations
@@ -74,16 +83,67 @@ def _sha256_file(path: Path) -> str:
     return h.hexdigest()
 
 
-def _download(req: urllib.request.Request, dest: Path, timeout: float) -> None:
+_SECRET_HEADERS = ("authorization", "x-amz-")
+
+
+class _NoCredentialRedirect(urllib.request.HTTPRedirectHandler):
+    """urllib copies every header but Content-Length/-Type onto a redirected
+    request; this one strips credentials and refuses an https → http hop."""
+
+    def redirect_request(self, req, fp, code, msg, headers, newurl):
+        new = super().redirect_request(req, fp, code, msg, headers, newurl)
+        if new is None:
+            return None
+        if urllib.parse.urlsplit(req.full_url).scheme == "https" and urllib.parse.urlsplit(newurl).scheme != "https":
+            raise ModelStoreError(f"refusing https -> {urllib.parse.urlsplit(newurl).scheme} redirect to {newurl}")
+        for k in list(new.headers):
+            if k.lower().startswith(_SECRET_HEADERS):
+                del new.headers[k]
+        for k in list(new.unredirected_hdrs):
+            if k.lower().startswith(_SECRET_HEADERS):
+                del new.unredirected_hdrs[k]
+        return new
+
+
+_OPENER = urllib.request.build_opener(_NoCredentialRedirect)
+
+
+def _open(req: urllib.request.Request, timeout: float):
+    return _OPENER.open(req, timeout=timeout)
+
+
+def _allow_plain_http() -> bool:
+    return os.environ.get("TCA_MODEL_STORE_ALLOW_HTTP", "") == "1"
+
+
+def _token_for(parts: urllib.parse.SplitResult) -> Optional[str]:
+    """The bearer token, if this URL may receive it (allow-listed host, https)."""
+    tok = os.environ.get("TCA_MODEL_STORE_TOKEN")
+    if not tok:
+        return None
+    hosts = {h.strip().lower() for h in os.environ.get("TCA_MODEL_STORE_TOKEN_HOSTS", "").split(",") if h.strip()}
+    if parts.netloc.lower() not in hosts and (parts.hostname or "").lower() not in hosts:
+        return None
+    if parts.scheme != "https" and not _allow_plain_http():
+        raise ModelStoreError(f"refusing to send TCA_MODEL_STORE_TOKEN over {parts.scheme}:// "
+                              "(set TCA_MODEL_STORE_ALLOW_HTTP=1 for a private-network store)")
+    return tok
+
+
+def _download(req: urllib.request.Request, dest: Path, timeout: float) -> str:
+    """Stream ``req`` into ``dest`` (atomic rename); returns the sha256."""
     fd, tmp = tempfile.mkstemp(dir=dest.parent, prefix=".part-")
+    h = hashlib.sha256()
     try:
-        with os.fdopen(fd, "wb") as out, urllib.request.urlopen(req, timeout=timeout) as r:
+        with os.fdopen(fd, "wb") as out, _open(req, timeout) as r:
             while True:
                 blk = r.read(1 << 20)
                 if not blk:
                     break
+                h.update(blk)
                 out.write(blk)
         os.replace(tmp, dest)
+        return h.hexdigest()
     except BaseException:
         try:
             os.unlink(tmp)
@@ -135,7 +195,7 @@ def oidc_token(token_url: str, client_id: str, client_secret: Optional[str] = No
         form["grant_type"] = "client_credentials"
     req = urllib.request.Request(token_url, data=urllib.parse.urlencode(form).encode(), method="POST",
                                  headers={"Content-Type": "application/x-www-form-urlencoded"})
-    with urllib.request.urlopen(req, timeout=timeout) as r:
+    with _open(req, timeout) as r:
         body = json.loads(r.read())
     tok = body.get("access_token") or body.get("id_token")
     if not tok:
@@ -149,7 +209,7 @@ def sts_web_identity(endpoint: str, token: str, duration_s: int = 3600, timeout:
             "WebIdentityToken": token, "DurationSeconds": str(duration_s)}
     req = urllib.request.Request(endpoint, data=urllib.parse.urlencode(form).encode(), method="POST",
                                  headers={"Content-Type": "application/x-www-form-urlencoded"})
-    with urllib.request.urlopen(req, timeout=timeout) as r:
+    with _open(req, timeout) as r:
         root = ET.fromstring(r.read())
     found = {el.tag.rsplit("}", 1)[-1]: (el.text or "") for el in root.iter()}
     try:
@@ -170,7 +230,17 @@ def _s3_credentials(endpoint: str) -> S3Credentials:
 
 
 # ------------------------------------------------------------------ public
-def resolve(uri: str, sha256: Optional[str] = None, timeout: float = 120.0) -> Path:
+def _cached_ok(path: Path, sha256: Optional[str]) -> bool:
+    if not path.is_file():
+        return False
+    want = sha256.lower() if sha256 else None
+    if want is None:
+        side = path.with_name(path.name + ".sha256")
+        want = side.read_text().strip() if side.is_file() else None
+    return want is not None and _sha256_file(path) == want
+
+
+def resolve(uri: str, sha256: Optional[str] = None, timeout: float = 120.0, refresh: bool = False) -> Path:
     """Return a local path holding the object named by ``uri`` (downloading it if remote)."""
     parts = urllib.parse.urlsplit(uri)
     if parts.scheme in ("", "file"):
@@ -180,22 +250,27 @@ def resolve(uri: str, sha256: Optional[str] = None, timeout: float = 120.0) -> P
     else:
         name = hashlib.sha256(uri.encode()).hexdigest()[:16] + "-" + (Path(parts.path).name or "object")
         path = _cache_dir() / name
-        if not path.is_file() or (sha256 and _sha256_file(path) != sha256.lower()):
+        if refresh or not _cached_ok(path, sha256):
             if parts.scheme in ("http", "https"):
-                hdrs = {}
-                if os.environ.get("TCA_MODEL_STORE_TOKEN"):
-                    hdrs["Authorization"] = "Bearer " + os.environ["TCA_MODEL_STORE_TOKEN"]
-                req = urllib.request.Request(uri, headers=hdrs)
+                tok = _token_for(parts)
+                req = urllib.request.Request(uri, headers={"Authorization": "Bearer " + tok} if tok else {})
             elif parts.scheme == "s3":
                 endpoint = os.environ.get("TCA_S3_ENDPOINT")
                 if not endpoint:
-                    raise ModelStoreError("s3:// URI needs TCA_S3_ENDPOINT (e.g. http://minio:9000)")
+                    raise ModelStoreError("s3:// URI needs TCA_S3_ENDPOINT (e.g. https://minio:9000)")
+                if urllib.parse.urlsplit(endpoint).scheme != "https" and not _allow_plain_http():
+                    raise ModelStoreError(f"TCA_S3_ENDPOINT {endpoint} is not https "
+                                          "(set TCA_MODEL_STORE_ALLOW_HTTP=1 for a private-network MinIO)")
                 url = endpoint.rstrip("/") + "/" + parts.netloc + "/" + parts.path.lstrip("/")
                 hdrs = sigv4_headers("GET", url, _s3_credentials(endpoint), os.environ.get("TCA_S3_REGION", "us-east-1"))
                 req = urllib.request.Request(url, headers=hdrs)
             else:
                 raise ModelStoreError(f"unsupported weights URI scheme: {parts.scheme!r}")
-            _download(req, path, timeout)
+            digest = _download(req, path, timeout)
+            path.with_name(path.name + ".sha256").write_text(digest + "\n")
+            if sha256 and digest != sha256.lower():
+                raise ModelStoreError(f"sha256 mismatch for {uri}")
+            return path
     if sha256 and _sha256_file(path) != sha256.lower():
         raise ModelStoreError(f"sha256 mismatch for {uri}")
     return path
