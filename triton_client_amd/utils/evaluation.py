@@ -6,9 +6,10 @@ Same definitions as the reference evaluator:
   of the 10 IoU thresholds 0.5:0.05:0.95 when it overlaps a same-class GT box;
   every GT and every prediction is matched at most once, highest IoU first
   (``evaluate_inference.py:411-425``).
-* ``compute_ap`` — precision envelope + 101-point interpolated area (COCO).
-* ``ap_per_class`` — per-class PR curves over confidence, AP per IoU
-  threshold, precision / recall / F1 at the confidence maximising mean F1.
+* ``compute_ap`` / ``ap_per_class`` — COCO 101-point AP of each class's PR
+  curve at each IoU threshold, and precision / recall / F1 at the confidence
+  maximising mean F1; all classes and thresholds in one vectorised pass
+  (segmented cumsum / envelope / interpolation, no per-class loop).
 
 Differences: predictions and ground truth are joined by
 ``header.seq`` (the reference zips two lists filled by independent
@@ -59,43 +60,123 @@ def match_predictions(gt: np.ndarray, pred: np.ndarray, iouv: np.ndarray = IOU_T
     return correct
 
 
+def _segmented_reverse_cummax(v: np.ndarray, seg: np.ndarray) -> np.ndarray:
+    """Running max from the right within each segment of ``v`` (values in
+    [0, 1], ``seg`` non-decreasing ints).  One ``maximum.accumulate`` over the
+    reversed array: lowering segment s by 2*s puts every segment above all
+    segments after it, so the max carried out of a later segment never wins
+    in an earlier one."""
+    lift = -2.0 * seg
+    return np.maximum.accumulate((v + lift)[::-1])[::-1] - lift
+
+
+def _segmented_interp(x: np.ndarray, xseg: np.ndarray, xp: np.ndarray, fp: np.ndarray, pseg: np.ndarray,
+                      span: float) -> np.ndarray:
+    """``np.interp`` of every query against its own segment's (xp, fp) in a
+    single call: segments are laid side by side on the x axis (offset
+    ``span`` * segment id, span > the width of any segment), so the sorted
+    concatenation stays sorted and a query never reaches a neighbour's
+    points as long as it lies inside its own segment's x range."""
+    return np.interp(x + span * xseg, xp + span * pseg, fp)
+
+
 def compute_ap(recall: np.ndarray, precision: np.ndarray) -> Tuple[float, np.ndarray, np.ndarray]:
-    """101-point interpolated AP (COCO).  Returns (ap, envelope, recall axis)."""
-    mrec = np.concatenate(([0.0], recall, [1.0]))
-    mpre = np.concatenate(([1.0], precision, [0.0]))
-    mpre = np.flip(np.maximum.accumulate(np.flip(mpre)))
-    x = np.linspace(0, 1, 101)
-    ap = float(np.trapezoid(np.interp(x, mrec, mpre), x))
-    return ap, mpre, mrec
+    """COCO 101-point AP of one PR curve.  Returns (ap, envelope, recall axis)
+    with the (0, 1) / (1, 0) end points included."""
+    ap, env, rec = _ap_segments(np.asarray(recall, np.float64)[None], np.asarray(precision, np.float64)[None])
+    return float(ap[0]), env[0], rec[0]
+
+
+_AP_GRID = np.linspace(0.0, 1.0, 101)
+
+
+def _ap_segments(recall: np.ndarray, precision: np.ndarray):
+    """AP of S PR curves at once: recall/precision [S, n] (each row one curve
+    over the confidence-sorted predictions).  Every curve gets the end points
+    recall 0 -> precision 1 and recall 1 -> precision 0, its precision is
+    replaced by the best precision at any higher recall (the envelope), and
+    the envelope is sampled on 101 recall points and integrated (trapezoid)."""
+    S, n = recall.shape
+    rec = np.concatenate([np.zeros((S, 1)), recall, np.ones((S, 1))], 1)
+    pre = np.concatenate([np.ones((S, 1)), precision, np.zeros((S, 1))], 1)
+    seg = np.repeat(np.arange(S), n + 2)
+    env = _segmented_reverse_cummax(pre.ravel(), seg).reshape(S, n + 2)
+    g = len(_AP_GRID)
+    span = 1.0 + max(1.0, float(rec.max()))  # recall <= 1 when each GT is matched at most once
+    samples = _segmented_interp(np.tile(_AP_GRID, S), np.repeat(np.arange(S), g), rec.ravel(), env.ravel(), seg,
+                                span=span).reshape(S, g)
+    ap = np.trapezoid(samples, _AP_GRID, axis=1)
+    return ap, env, rec
 
 
 def ap_per_class(tp: np.ndarray, conf: np.ndarray, pred_cls: np.ndarray, target_cls: np.ndarray):
-    """Returns (p, r, ap [nc, n_iou], f1, classes) like the reference :158-218."""
-    tp = np.asarray(tp).reshape(len(conf), -1)
-    i = np.argsort(-np.asarray(conf), kind="stable")
-    tp, conf, pred_cls = tp[i], np.asarray(conf)[i], np.asarray(pred_cls)[i]
+    """Per-class PR statistics over a whole run: returns (p, r, ap [nc, n_iou],
+    f1, classes) — the metric of the reference's evaluator
+    (``communicator/evaluate_inference.py:131-218``, itself YOLOv5's), computed
+    for all classes and IoU thresholds at once.
+
+    * Predictions are ordered by class, then by descending confidence; running
+      TP / FP counts restart at each class (segmented cumsum).
+    * recall = TP / #GT of the class, precision = TP / (TP + FP); AP per
+      (class, IoU threshold) from :func:`_ap_segments`.
+    * p / r / f1 are read at one confidence threshold shared by all classes:
+      each class's precision and recall (IoU 0.5) are interpolated linearly
+      over confidence on a 1000-point grid (above the class's top confidence:
+      recall 0, precision 1; below its lowest: its last value), and the grid
+      point with the best class-mean F1 is taken.
+    Classes are those present in the ground truth; a class without
+    predictions scores 0."""
+    conf = np.asarray(conf, np.float64).reshape(-1)
+    tp = np.asarray(tp, np.float64)
+    tp = tp.reshape(len(conf), tp.shape[-1] if tp.ndim == 2 else -1) if len(conf) else tp.reshape(0, max(tp.shape[-1:] or [1]))
+    pred_cls = np.asarray(pred_cls).reshape(-1)
+    target_cls = np.asarray(target_cls).reshape(-1)
     classes = np.unique(target_cls)
-    nc = classes.shape[0]
-    px = np.linspace(0, 1, 1000)
-    ap = np.zeros((nc, tp.shape[1]))
-    p, r = np.zeros((nc, 1000)), np.zeros((nc, 1000))
-    for ci, c in enumerate(classes):
-        sel = pred_cls == c
-        n_l = int((target_cls == c).sum())
-        n_p = int(sel.sum())
-        if n_p == 0 or n_l == 0:
-            continue
-        fpc = (1 - tp[sel]).cumsum(0)
-        tpc = tp[sel].cumsum(0)
-        recall = tpc / (n_l + 1e-16)
-        r[ci] = np.interp(-px, -conf[sel], recall[:, 0], left=0)
-        precision = tpc / (tpc + fpc)
-        p[ci] = np.interp(-px, -conf[sel], precision[:, 0], left=1)
-        for j in range(tp.shape[1]):
-            ap[ci, j] = compute_ap(recall[:, j], precision[:, j])[0]
-    f1 = 2 * p * r / (p + r + 1e-16)
-    k = int(f1.mean(0).argmax()) if nc else 0
-    return p[:, k], r[:, k], ap, f1[:, k], classes.astype(np.int32)
+    nc, nt = len(classes), tp.shape[1]
+    grid = np.linspace(0.0, 1.0, 1000)
+    ap = np.zeros((nc, nt))
+    p_curve = np.zeros((nc, len(grid)))
+    r_curve = np.zeros((nc, len(grid)))
+    # class index of each prediction; predictions of classes absent from the GT drop out
+    ci = np.searchsorted(classes, pred_cls)
+    keep = (ci < nc) & (classes[np.minimum(ci, max(nc - 1, 0))] == pred_cls) if nc else np.zeros(len(conf), bool)
+    ci, cf, hits = ci[keep], conf[keep], tp[keep]
+    if len(ci):
+        order = np.lexsort((-cf, ci))  # by class, then confidence high -> low
+        ci, cf, hits = ci[order], cf[order], hits[order]
+        n_gt = np.bincount(np.searchsorted(classes, target_cls), minlength=nc).astype(np.float64)
+        first = np.r_[0, np.flatnonzero(np.diff(ci)) + 1]  # start of each class run
+        count = np.diff(np.r_[first, len(ci)])
+        cum_tp = np.cumsum(hits, 0)
+        base = np.repeat(np.r_[np.zeros((1, nt)), cum_tp[first[1:] - 1]], count, 0)
+        tps = cum_tp - base  # TP among this class's predictions so far
+        rank = np.arange(len(ci)) - np.repeat(first, count) + 1.0  # predictions so far
+        recall = tps / n_gt[ci][:, None]
+        precision = tps / rank[:, None]
+        present = ci[first]
+        # AP: one curve per (class run, IoU threshold), padded to the longest run
+        # by repeating each run's last point (adds no area: same recall, same precision).
+        L = int(count.max())
+        pos = first[:, None] + np.minimum(np.arange(L)[None], count[:, None] - 1)  # [runs, L]
+        R = recall[pos].transpose(0, 2, 1).reshape(-1, L)
+        P = precision[pos].transpose(0, 2, 1).reshape(-1, L)
+        ap[present] = _ap_segments(R, P)[0].reshape(len(present), nt)
+        # p / r at each grid confidence, per class run, linear in confidence
+        runs = len(present)
+        q = np.tile(-grid, runs)
+        qseg = np.repeat(np.arange(runs), len(grid))
+        pseg = np.repeat(np.arange(runs), count)
+        r_all = _segmented_interp(q, qseg, -cf, recall[:, 0], pseg, span=4.0).reshape(runs, -1)
+        p_all = _segmented_interp(q, qseg, -cf, precision[:, 0], pseg, span=4.0).reshape(runs, -1)
+        top = cf[first][:, None]
+        low = cf[first + count - 1][:, None]
+        above, below = grid[None] > top, grid[None] < low
+        r_all = np.where(above, 0.0, np.where(below, recall[first + count - 1, 0][:, None], r_all))
+        p_all = np.where(above, 1.0, np.where(below, precision[first + count - 1, 0][:, None], p_all))
+        r_curve[present], p_curve[present] = r_all, p_all
+    f1 = 2 * p_curve * r_curve / (p_curve + r_curve + 1e-16)
+    k = int(np.argmax(f1.mean(0))) if nc else 0
+    return p_curve[:, k], r_curve[:, k], ap, f1[:, k], classes.astype(np.int32)
 
 
 @dataclass
