@@ -87,6 +87,12 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 (default): the reference's serving precision — fp32 activations, split-product "
                          "MFMA convs; bf16: bf16 activations (secondary, labelled)")
+    ap.add_argument("--camera-input", choices=["raw", "jpeg"], default="raw",
+                    help="raw: uint8 RGB frames (sensor_msgs/Image); jpeg: CompressedImage JPEGs decoded every step "
+                         "(C++ Huffman decode into pinned staging on --decode-threads host threads, overlapped with "
+                         "the previous step's GPU work; IDCT + upsample + colour on the GPU)")
+    ap.add_argument("--decode-threads", type=int, default=16, help="host threads of the JPEG entropy decoder")
+    ap.add_argument("--jpeg-quality", type=int, default=90)
     ap.add_argument("--check-launch", action="store_true",
                     help="launch/rendezvous check only: every rank joins, the ranks are counted with an all-reduce, "
                          "rank 0 prints them (no GPU work; used by the CPU tests with TCA_DIST_BACKEND=gloo)")
@@ -223,6 +229,16 @@ def main():
         seed0 = 1000 * info.rank
         cams = [camera_frame(H0, W0, seed0 + i) for i in range(nd)] if use_cam else []
         clouds = [lidar_sweep(spec, seed0 + 500 + i) for i in range(nd)] if use_lid else []
+        jpegs = None
+        if use_cam and args.camera_input == "jpeg":
+            import io
+
+            from PIL import Image
+            jpegs = []
+            for f in cams:
+                buf = io.BytesIO()
+                Image.fromarray(f).save(buf, format="JPEG", quality=args.jpeg_quality)
+                jpegs.append(buf.getvalue())
         if use_cam:
             cam_host = torch.empty((shards, B, H0, W0, 3), dtype=torch.uint8).pin_memory()
             for s in range(shards):
@@ -349,14 +365,33 @@ def main():
         raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
     ex = FrameExchange(info, native=native)
 
-    dsts = [t for t in ((cam.frames,) if use_cam else ()) + ((lid.data, lid.frame_n) if use_lid else ())]
+    jdec = None
+    if use_cam and args.camera_input == "jpeg":
+        if args.ingest != "local" or S > 1:
+            raise SystemExit("--camera-input jpeg needs --ingest local and --sub-batches 1")
+        from triton_client_amd.ops.jpeg import JpegBatchDecoder
+        jdec = JpegBatchDecoder(B, dev, threads=args.decode_threads)
+        jpeg_copy = torch.cuda.Stream()
+        jstep = [0]
+
+        def stage_next_jpegs():
+            """Host entropy decode of the next step's B JPEGs (C++ threads),
+            then their H2D on a copy stream — runs while the GPU computes."""
+            j0 = jstep[0]
+            jstep[0] += 1
+            jdec.upload(jdec.stage([jpegs[(j0 * B + b) % nd] for b in range(B)]), jpeg_copy)
+
+        stage_next_jpegs()
+    dsts = [t for t in ((cam.frames,) if use_cam and jdec is None else ()) +
+            ((lid.data, lid.frame_n) if use_lid else ())]
     # ---------------- ingest: local mode prefetches step t+1's frames (H2D on a copy
     # stream into landing buffers) while step t computes
     prefetch = args.ingest == "local" and not args.no_prefetch
     if prefetch:
         copy_stream = torch.cuda.Stream()
         landing = [torch.empty_like(t) for t in dsts]
-        host_src = [t for t in ((cam_host[0],) if use_cam else ()) + ((pc_host[0], n_host[0]) if use_lid else ())]
+        host_src = [t for t in ((cam_host[0],) if use_cam and jdec is None else ()) +
+                    ((pc_host[0], n_host[0]) if use_lid else ())]
         h2d_done = torch.cuda.Event()
         consumed = torch.cuda.Event()
 
@@ -371,6 +406,8 @@ def main():
         issue_h2d()
 
     def ingest():
+        if jdec is not None:
+            jdec.reconstruct(cam.frames)  # this step's JPEGs, staged during the previous step
         if prefetch:
             cur = torch.cuda.current_stream()
             cur.wait_event(h2d_done)
@@ -380,7 +417,7 @@ def main():
             issue_h2d()  # next step's frames stream in while this step computes
             return
         if args.ingest == "local":
-            if use_cam:
+            if use_cam and jdec is None:
                 cam.frames.copy_(cam_host[0], non_blocking=True)
             if use_lid:
                 lid.data.copy_(pc_host[0], non_blocking=True)
@@ -419,6 +456,8 @@ def main():
         nonlocal gather_dst, host_out
         ingest()
         r2, r3 = runner()
+        if jdec is not None:
+            stage_next_jpegs()  # host decode overlaps this step's GPU work
         src = outputs(r2, r3)
         if gather_dst is None and info.is_main:
             # rank 0's own detections are D2H-copied straight from the graph's result
@@ -444,6 +483,8 @@ def main():
         step()
     barrier(info)
     torch.cuda.synchronize()
+    if jdec is not None:
+        jdec.stats.update(frames=0, host_s=0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -451,6 +492,24 @@ def main():
     barrier(info)
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(info, elapsed)
+    jpeg_info = None
+    if jdec is not None:
+        host_us = jdec.host_us_per_frame()
+        # GPU half alone (IDCT + colour kernels), timed after the run
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        reps = 10
+        e0.record()
+        for _ in range(reps):
+            jdec.pending = 0
+            jdec.reconstruct(cam.frames)
+        e1.record()
+        torch.cuda.synchronize()
+        jpeg_info = {"decode_threads": args.decode_threads, "quality": args.jpeg_quality,
+                     "avg_jpeg_bytes": int(np.mean([len(j) for j in jpegs])),
+                     "host_entropy_decode_wall_us_per_frame": round(host_us, 1),
+                     "gpu_idct_color_us_per_frame": round(1e3 * e0.elapsed_time(e1) / reps / B, 2),
+                     "fallback_frames": jdec.stats["fallback"]}
 
     cam_name = {"yolov5n": "YOLOv5n-640 (COCO, 80 cls)", "yolov4": "YOLOv4-512 (COCO, 80 cls)",
                 "retinanet": "RetinaNet R50-FPN 800x1344 (COCO)",
@@ -482,7 +541,9 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision if (args.camera_model == "yolov5n" and args.lidar_model == "pointpillars")
             else "bf16",
-            "data": (f"synthetic: {nd} distinct {W0}x{H0} uint8 RGB camera frames + {nd} distinct "
+            "data": (f"synthetic: {nd} distinct {W0}x{H0} "
+                     + (f"JPEG (q{args.jpeg_quality}, decoded every step)" if jdec is not None else "uint8 RGB")
+                     + f" camera frames + {nd} distinct "
                      f"{spec.rings}x{spec.azimuth_steps} LiDAR sweeps per rank, re-sent every step "
                      f"(PointCloud2 16 B/pt, ~2% NaN dropouts); random-init weights (He-normal + LSUV rescaling on "
                      f"sample frames), detection-head bias offset calibrated so ~{args.target_2d:g} 2D / ~{args.target_3d:g} 3D candidates per frame reach NMS"),
@@ -500,6 +561,8 @@ def main():
                 "rccl_ranks": rccl_ranks,
                 "vs_reference_equivalent_emulation": round(fps / REFERENCE_EQUIVALENT_FPS, 2),
                 "ingest": args.ingest,
+                "camera_input": args.camera_input if use_cam else None,
+                "jpeg": jpeg_info,
                 "comm": comm_used,
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,

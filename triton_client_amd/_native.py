@@ -28,6 +28,9 @@ F = ctypes.c_float
 # name -> argtypes (restype is always int = hipError_t)
 _KERNEL_SIGS = {
     "tca_draw_boxes": [P, L, I, I, I, I, P, I, I, P, P, I, P],
+    # JPEG pixel reconstruction (csrc/kernels/jpeg.hip)
+    "tca_jpeg_idct": [P, P, P, P, L, L, I, P],
+    "tca_jpeg_color": [P, P, P, L, L, I, P],
     "tca_image_preprocess": [P, L, I, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P],
     "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
     "tca_topk_sort": [P, P, I, I, I, P, P, P],

@@ -14,6 +14,10 @@ SIGS = {
     "tca_kserve_response_size": (L, [CP, CP, CP, I, PP, PP, P, P, P]),
     "tca_kserve_encode_response": (L, [CP, CP, CP, I, PP, PP, P, P, P, P, P, L]),
     "tca_kserve_parse_request": (I, [P, L, I, P, P, I, P, P, P]),
+    # baseline JPEG entropy decoder (csrc/runtime/jpeg_entropy.cpp)
+    "tca_jpeg_probe": (I, [P, ctypes.c_int64, P]),
+    "tca_jpeg_decode_coefs": (I, [P, ctypes.c_int64, P, ctypes.c_int64, P, P]),
+    "tca_jpeg_decode_batch": (I, [P, P, I, P, ctypes.c_int64, P, P, P, I]),
     # native RCCL communicator (csrc/runtime/rccl_comm.cpp)
     "tca_rccl_unique_id_bytes": (I, []),
     "tca_rccl_get_unique_id": (I, [P]),
