@@ -90,7 +90,13 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
             nh, nw, float(pad_value), int(quantize_u8), float(scale[0]), float(scale[1]), float(scale[2]),
             float(bias[0]), float(bias[1]), float(bias[2]), _native.stream_ptr(stream))
         return out, xf
-    # CPU path (config 1 / GPU-less host)
+    # CPU path (config 1 / GPU-less host): the C++ preprocess when the runtime
+    # library is built, else the NumPy golden (bit-identical results)
+    if out_channels == 3 and frames.dtype == torch.uint8 and dtype == torch.float32 and layout in ("NCHW", "NHWC"):
+        rt = _cpu_runtime()
+        if rt is not None:
+            return _preprocess_cpu_native(rt, frames, (H, W), layout, swap_rb, pad_value, quantize_u8, scale, bias,
+                                          (top, left, nh, nw), out, xf)
     res = []
     for b in range(B):
         img = frames[b].numpy()
@@ -103,6 +109,36 @@ def preprocess(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str = "stret
         t = arr.permute(0, 3, 1, 2).contiguous()
     else:
         t = arr.permute(0, 3, 1, 2)
+    if out is not None:
+        out.copy_(t)
+        return out, xf
+    return t, xf
+
+
+def _cpu_runtime():
+    try:
+        return _native.runtime()
+    except _native.NativeError:
+        return None
+
+
+def _preprocess_cpu_native(rt, frames, dst_hw, layout, swap_rb, pad_value, quantize_u8, scale, bias, region, out, xf):
+    import ctypes
+    import os
+
+    B, h0, w0, c0 = frames.shape
+    H, W = dst_hw
+    top, left, nh, nw = region
+    frames = frames.contiguous()
+    res = torch.empty((B, 3, H, W) if layout == "NCHW" else (B, H, W, 3), dtype=torch.float32)
+    sc = (ctypes.c_float * 3)(*[float(v) for v in scale])
+    bi = (ctypes.c_float * 3)(*[float(v) for v in bias])
+    threads = min(8, os.cpu_count() or 1)
+    for b in range(B):
+        rt.tca_cpu_preprocess(frames[b].data_ptr(), h0, w0, c0, int(swap_rb), res[b].data_ptr(),
+                              0 if layout == "NCHW" else 1, H, W, top, left, nh, nw, float(pad_value),
+                              int(quantize_u8), sc, bi, threads)
+    t = res if layout == "NCHW" else res.permute(0, 3, 1, 2)
     if out is not None:
         out.copy_(t)
         return out, xf

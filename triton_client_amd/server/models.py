@@ -90,6 +90,12 @@ class YoloV5Model(ServedModel):
             self.runner = GraphRunner(step)
         else:
             from ..models.common import fuse_model
+            if not self.weights:  # same head prior as the GPU path (random init)
+                pipe = CameraPipeline(model, batch=1, src_hw=(self.img, self.img), img_hw=(self.img, self.img),
+                                      mode="stretch", device="cpu")
+                pipe.frames[0].copy_(torch.from_numpy(camera_frame(self.img, self.img, self.seed)))
+                pipe.calibrate_detection_density(self.calibrate_target)
+                model = pipe.model
             self.model = fuse_model(model.eval())
         self.ready = True
 
