@@ -24,7 +24,12 @@ namespace tca {
 
 constexpr int kWave = 64;
 
-enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2, kU8 = 3, kI32 = 4 };
+enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2, kU8 = 3, kI32 = 4, kPair = 5 };
+
+// fp32-mode "pair" activation storage: per 8 channels {hi bf16 x 8 | lo bf16 x 8}
+// (32 B, the footprint of 8 fp32), x = hi + lo to 2^-17 relative; consumers feed
+// the halves to MFMA as stored.  Tag type for kernels templated on storage.
+struct PairTag {};
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(__half x) { return __half2float(x); }

@@ -339,6 +339,9 @@ struct NeckArgsX3 {
   int B, H, W, S, nbr, nsteps, ntiles;
 };
 
+// PAIR: branch inputs in pair storage ({hi 8 | lo 8} per 8 channels, see
+// conv_mfma.hip pair_split8): the A fragments are read as stored, no split.
+template <bool PAIR>
 __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[X_LDS_BYTES];
 
@@ -440,9 +443,14 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
 #pragma unroll
       for (int i = 0; i < X_FM; ++i) {
         const int r = wid * 16 * X_FM + i * 16 + fr;
-        const float4 x0 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
-        const float4 x1 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
-        split8(x0, x1, ah[i], al[i]);
+        if constexpr (PAIR) {
+          ah[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+          al[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+        } else {
+          const float4 x0 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+          const float4 x1 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+          split8(x0, x1, ah[i], al[i]);
+        }
       }
       __builtin_amdgcn_s_setprio(1);
       // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the
@@ -582,10 +590,10 @@ TCA_API int tca_bev_neck_head(int nbr, const void* const* x, const int* ldx, con
 
 // fp32 mode: x[i] fp32, w[i] split [s_i*s_i*128, 2*cin[i]] bf16, wh split [80, 2*nbr*128]
 // (32-chunk permuted, then split), out fp32 [B, H, W, ldo].  Other arguments as tca_bev_neck_head.
-TCA_API int tca_bev_neck_head_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
-                                 const int* s, const void* const* w, const float* const* bias, const void* wh,
-                                 const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
-                                 hipStream_t stream) {
+namespace {
+int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin, const int* s,
+            const void* const* w, const float* const* bias, const void* wh, const float* bh, int nh, void* out,
+            int ldo, int B, int H, int W, int grid, bool pair, hipStream_t stream) {
   if (B <= 0) return 0;
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
@@ -609,6 +617,28 @@ TCA_API int tca_bev_neck_head_x3(int nbr, const void* const* x, const int* ldx, 
   a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
   const int nq = (H / S) * (W / S);
   a.ntiles = B * ((nq + X_BM - 1) / X_BM) * S * S;
-  bev_neck_head_x3_kernel<<<grid, NT, 0, stream>>>(a);
+  if (pair) {
+    for (int i = 0; i < nbr; ++i)
+      if ((ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;
+    bev_neck_head_x3_kernel<true><<<grid, NT, 0, stream>>>(a);
+  } else {
+    bev_neck_head_x3_kernel<false><<<grid, NT, 0, stream>>>(a);
+  }
   TCA_LAUNCH_CHECK();
+}
+}  // namespace
+
+TCA_API int tca_bev_neck_head_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
+                                 const int* s, const void* const* w, const float* const* bias, const void* wh,
+                                 const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
+                                 hipStream_t stream) {
+  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, false, stream);
+}
+
+// Same, branch inputs x[i] in pair storage.
+TCA_API int tca_bev_neck_head_x3p(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
+                                  const int* s, const void* const* w, const float* const* bias, const void* wh,
+                                  const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
+                                  hipStream_t stream) {
+  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, true, stream);
 }

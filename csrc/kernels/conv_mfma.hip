@@ -880,7 +880,31 @@ __device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8
 
 // fp32 epilogue: bias/act into an fp32 LDS tile, then 16-B (4-channel) coalesced
 // stores with residual and pixel-shuffle addressing as in the bf16 epilogue.
-template <int BM, int BN, int WM, int WN>
+// "pair" activations (fp32 mode's storage for BEV chains): 8 channels as
+// {hi bf16 x 8 | lo bf16 x 8} = 32 B, the same bytes and element offsets as 8
+// fp32 values.  x == float(hi) + float(lo) to 2^-17 relative, and a consumer's
+// MFMA fragments are the two 16-B halves as stored: no VALU split on the read.
+__device__ __forceinline__ void pair_split8(const float* v, uint4& hi, uint4& lo) {
+  __bf16 h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  hi = *reinterpret_cast<const uint4*>(h);
+  lo = *reinterpret_cast<const uint4*>(l);
+}
+
+__device__ __forceinline__ void pair_join8(const float* p, float* v) {
+  const uint4 hq = *reinterpret_cast<const uint4*>(p);
+  const uint4 lq = *reinterpret_cast<const uint4*>(p + 4);
+  const __bf16* h = reinterpret_cast<const __bf16*>(&hq);
+  const __bf16* l = reinterpret_cast<const __bf16*>(&lq);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
+}
+
+template <int BM, int BN, int WM, int WN, bool PAIR_OUT = false>
 __device__ __forceinline__ void epilogue_f32(const ConvArgs& a, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                              unsigned char* smem, int m0, int n0) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -911,6 +935,39 @@ __device__ __forceinline__ void epilogue_f32(const ConvArgs& a, const f32x4 (&ac
     }
   }
   __syncthreads();
+  if constexpr (PAIR_OUT) {
+    // pair storage: 8 channels per store (residual read as pairs too)
+    constexpr int V8 = BN / 8;
+    for (int id = tid; id < BM * V8; id += NT) {
+      const int ml = id / V8, c8 = (id % V8) * 8;
+      const int m = m0 + ml, n = n0 + c8;
+      if (m >= a.M || n >= a.N) continue;
+      float v[8];
+      const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+      const int ox = m % a.Wo, oy = (m / a.Wo) % a.Ho, b = m / (a.Wo * a.Ho);
+      long o;
+      if (a.shuffle > 0) {
+        const int s = a.shuffle, coutr = a.N / (s * s);
+        const int sy = n / (s * coutr), sx = (n / coutr) % s, co = n % coutr;
+        o = (((long)b * a.Ho * s + oy * s + sy) * (a.Wo * s) + ox * s + sx) * a.ldo + a.co_off + co;
+      } else {
+        o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n;
+      }
+      if (a.res_f) {
+        float r[8];
+        pair_join8(a.res_f + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldr + a.r_off + n, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
+      }
+      uint4 hi, lo;
+      pair_split8(v, hi, lo);
+      *reinterpret_cast<uint4*>(a.out_f + o) = hi;
+      *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+    }
+    return;
+  }
   constexpr int VEC_PER_ROW = BN / 4;
   for (int id = tid; id < BM * VEC_PER_ROW; id += NT) {
     const int ml = id / VEC_PER_ROW, c4 = (id % VEC_PER_ROW) * 4;
@@ -1100,7 +1157,7 @@ __device__ __forceinline__ void wait_vmcnt_upto(int k) {  // vmcnt(k * N), k in 
 // 32-deep K step is ~770 cycles of matrix work per SIMD, shorter than an HBM
 // round trip, so 2 stages (one step in flight) leave the MFMAs waiting on the
 // DMA; 3-4 stages hide it.
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_IN = false, bool PAIR_OUT = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) {
   static_assert(STAGES >= 2 && STAGES <= 5, "stages");
   constexpr int NW = WM * WN;
@@ -1217,9 +1274,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int r = wm * TM + i * 16 + fr;
-      const float4 x0 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq) ^ swz3(r)) << 4));
-      const float4 x1 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
-      split8(x0, x1, ah[i], al[i]);
+      if constexpr (PAIR_IN) {  // slots 2fq / 2fq+1 already hold hi / lo of channels 8fq..8fq+7
+        ah[i] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + (((2 * fq) ^ swz3(r)) << 4));
+        al[i] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+      } else {
+        const float4 x0 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq) ^ swz3(r)) << 4));
+        const float4 x1 = *reinterpret_cast<const float4*>(sa + r * ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+        split8(x0, x1, ah[i], al[i]);
+      }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1231,7 +1293,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // the epilogue reuses the staging LDS
   asm volatile("" ::: "memory");
-  epilogue_f32<BM, BN, WM, WN>(a, acc, smem, m0, n0);
+  epilogue_f32<BM, BN, WM, WN, PAIR_OUT>(a, acc, smem, m0, n0);
 }
 
 // ---- x3 small halo: 3x3, pad 1, stride 1/2, Cin and N in {16, 32}.  The fp32
@@ -1374,11 +1436,23 @@ int launch_small_halo_x3(const ConvArgs& a, hipStream_t stream) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES = 2>
+template <int BM, int BN, int WM, int WN, int STAGES = 2, bool PAIR_IN = false, bool PAIR_OUT = false>
 int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  conv_glds_x3_kernel<BM, BN, WM, WN, STAGES><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_glds_x3_kernel<BM, BN, WM, WN, STAGES, PAIR_IN, PAIR_OUT><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
+}
+
+template <bool PAIR_OUT>
+int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
+  switch (tile) {
+    case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
+    case 22: return launch_glds_x3<128, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
+    case 24: return launch_glds_x3<64, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
+    case 25: return launch_glds_x3<128, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
+    case 41: return launch_glds_x3<128, 64, 8, 1, 2, true, PAIR_OUT>(a, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1528,4 +1602,29 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
     case 6: return launch_x3<128, 16, 4, 1>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// fp32 mode, pair activations: `in` (and `res`) hold pairs (see pair_split8),
+// `out` pairs when out_pair, else fp32.  Same slice / residual / pixel-shuffle
+// contract as tca_conv_nhwc_x3; the global_load_lds kernels only (Cin % 32 == 0,
+// Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 41.
+TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
+                              const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
+                              int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
+                              int tile, int out_pair, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((Cin & 7) || (ldi & 7) || (ci_off & 7) || (N & 7) || (ldo & 7) || (co_off & 7) || (Kp & 31)) return (int)hipErrorInvalidValue;
+  if (res && ((ldr & 7) || (r_off & 7) || !out_pair)) return (int)hipErrorInvalidValue;
+  if (shuffle > 0 && ((N / (shuffle * shuffle)) & 7)) return (int)hipErrorInvalidValue;
+  ConvArgs a;
+  a.in = nullptr; a.res = nullptr; a.out = nullptr;
+  a.in_f = in; a.res_f = res; a.out_f = out;
+  a.w = (const __hip_bfloat16*)w; a.bias = bias;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off;
+  a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
+  a.N = N; a.K = KH * KW * Cin; a.Kp = Kp; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off;
+  a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
+  if (a.K > Kp || (Cin % 32) != 0 || Kp != a.K) return (int)hipErrorInvalidValue;
+  if (tile == 0) tile = N <= 64 ? 41 : 20;
+  return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
 }

@@ -23,6 +23,8 @@
 //     the BEV convs consume).
 // tca_pillar_canvas_clear zeroes exactly the cells the previous frame wrote,
 // so the 27 MB/frame canvas is never memset.
+#include <type_traits>
+
 #include "tca_common.h"
 
 using namespace tca;
@@ -176,7 +178,15 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const int ch = 32 * h + r;
     if (canvas) {
       const long cell = ((long)b * g.ny + co.z) * g.nx + co.w;
-      canvas[cell * 64 + ch] = from_f32<CT>(val);
+      if constexpr (std::is_same<CT, PairTag>::value) {
+        // pair storage: channel ch -> hi at 16*(ch/8) + ch%8, lo 8 bf16 later
+        __bf16* c2 = reinterpret_cast<__bf16*>(canvas) + cell * 128 + (ch >> 3) * 16 + (ch & 7);
+        const __bf16 h = (__bf16)val;
+        c2[0] = h;
+        c2[8] = (__bf16)(val - (float)h);
+      } else {
+        canvas[cell * 64 + ch] = from_f32<CT>(val);
+      }
     }
     if (feat_out) feat_out[(long)v * 64 + ch] = val;
     v = vn;
@@ -204,23 +214,40 @@ __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict
 
 }  // namespace
 
-// Fused path: source = voxeliser slots + unpacked points.
+namespace {
+template <bool FROM_SLOTS>
+int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
+               const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
+               const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
+               hipStream_t stream) {
+  if (P > 32 || (dt != kBF16 && dt != kF32 && dt != kPair)) return (int)hipErrorInvalidValue;
+  if (dt == kF32)
+    pillar_vfe_kernel<FROM_SLOTS, float><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
+                                                                   num_points, coords, voxel_count, batch, max_voxels,
+                                                                   P, W, bias, g, (float*)canvas, feat_out);
+  else if (dt == kPair)
+    pillar_vfe_kernel<FROM_SLOTS, PairTag><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
+                                                                     num_points, coords, voxel_count, batch,
+                                                                     max_voxels, P, W, bias, g, (PairTag*)canvas,
+                                                                     feat_out);
+  else
+    pillar_vfe_kernel<FROM_SLOTS, __hip_bfloat16><<<2048, 256, 0, stream>>>(
+        pts, pstride, max_pts, slots, vcount, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias,
+        g, (__hip_bfloat16*)canvas, feat_out);
+  TCA_LAUNCH_CHECK();
+}
+}  // namespace
+
+// Fused path: source = voxeliser slots + unpacked points.  canvas_dtype: kBF16,
+// kF32 or kPair (fp32 mode's pair storage, see tca_common.h).
 TCA_API int tca_pillar_vfe_slots(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount,
                                  const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                                  const float* W, const float* bias, const float* range, const float* vsize, int nx,
                                  int ny, void* canvas, float* feat_out, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (P > 32 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
-  if (canvas_dtype == kF32)
-    pillar_vfe_kernel<true, float><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr,
-                                                             coords, voxel_count, batch, max_voxels, P, W, bias, g,
-                                                             (float*)canvas, feat_out);
-  else
-    pillar_vfe_kernel<true, __hip_bfloat16><<<2048, 256, 0, stream>>>(
-        pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords, voxel_count, batch, max_voxels, P, W, bias, g,
-        (__hip_bfloat16*)canvas, feat_out);
-  TCA_LAUNCH_CHECK();
+  return launch_vfe<true>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords, voxel_count, batch,
+                          max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, stream);
 }
 
 // Server path: source = materialised voxels [B*V][P][4] + num_points (KServe inputs).
@@ -229,24 +256,17 @@ TCA_API int tca_pillar_vfe_voxels(const float* voxels, const int* num_points, co
                                   const float* bias, const float* range, const float* vsize, int nx, int ny,
                                   void* canvas, float* feat_out, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  if (P > 32 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
-  if (canvas_dtype == kF32)
-    pillar_vfe_kernel<false, float><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points,
-                                                              coords, voxel_count, batch, max_voxels, P, W, bias, g,
-                                                              (float*)canvas, feat_out);
-  else
-    pillar_vfe_kernel<false, __hip_bfloat16><<<2048, 256, 0, stream>>>(
-        nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias, g,
-        (__hip_bfloat16*)canvas, feat_out);
-  TCA_LAUNCH_CHECK();
+  return launch_vfe<false>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords, voxel_count, batch,
+                           max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, stream);
 }
 
 TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
                                     int ny, int C, void* canvas, int canvas_dtype, hipStream_t stream) {
   if (batch <= 0) return 0;
-  const int esize = canvas_dtype == kF32 ? 4 : 2;
-  if ((C * esize) & 15 || (canvas_dtype != kBF16 && canvas_dtype != kF32)) return (int)hipErrorInvalidValue;
+  const int esize = (canvas_dtype == kF32 || canvas_dtype == kPair) ? 4 : 2;
+  if ((C * esize) & 15 || (canvas_dtype != kBF16 && canvas_dtype != kF32 && canvas_dtype != kPair))
+    return (int)hipErrorInvalidValue;
   canvas_clear_kernel<<<dim3((max_voxels * (C * esize / 16) + 255) / 256, batch), 256, 0, stream>>>(
       coords, voxel_count, max_voxels, nx, ny, C, esize, (uint4*)canvas);
   TCA_LAUNCH_CHECK();

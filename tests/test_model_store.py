@@ -207,7 +207,6 @@ def test_repository_export_roundtrip_with_weights(tmp_path):
     version-dir state_dict and the remote-URI parameter; loaded weights win over
     the seeded random init."""
     from triton_client_amd.models.yolov5 import build_yolov5
-    from triton_client_amd.server.models import YoloV5Model
     from triton_client_amd.server.repository import ModelRepository, export_repository
 
     wpath = tmp_path / "y.pt"
@@ -220,11 +219,12 @@ def test_repository_export_roundtrip_with_weights(tmp_path):
     assert lazy.get("YOLOv5nCOCO").weights_sha256 == hashlib.sha256(wpath.read_bytes()).hexdigest()
     repo = ModelRepository.from_directory(str(tmp_path / "repo"), "cpu", load=False)
     m = repo.load("YOLOv5nCOCO")
-    ref = YoloV5Model("YOLOv5nCOCO", "n", 80, 640, device="cpu", seed=123)
-    ref.load()
+    from triton_client_amd.models.common import fuse_model
+
+    ref = fuse_model(build_yolov5("n", 80, 640, 123).eval())  # the saved weights, uncalibrated
     x = torch.rand(1, 3, 640, 640)
     with torch.no_grad():
-        for a, b in zip(m.model(x), ref.model(x)):
+        for a, b in zip(m.model(x), ref(x)):
             assert torch.equal(a, b)
     # a swapped weights file no longer matches the recorded sha256: refused at load
     torch.save(build_yolov5("n", 80, 640, 7).state_dict(), tmp_path / "repo" / "YOLOv5nCOCO" / "1" / "model.pt")

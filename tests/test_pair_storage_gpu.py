@@ -1,0 +1,119 @@
+"""fp32 mode's pair activation storage ({hi | lo} bf16 halves per 8 channels,
+read by the split-product kernels as MFMA fragments without a VALU split):
+the pair conv / neck kernels vs fp64 references, and a pair-storage BEV plan
+bit-identical to the plain-fp32 plan (same hi / lo operands, same tiles)."""
+import copy
+import dataclasses
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from triton_client_amd.ops.conv import NHWC, FusedConv, from_pairs, to_pairs
+
+pytestmark = pytest.mark.gpu
+
+ACTS = {0: lambda t: t, 1: torch.relu}
+
+
+def rel_l2(got, ref):
+    got, ref = got.double().cpu(), ref.double().cpu()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+def test_pairs_roundtrip_cpu():
+    x = torch.randn(2, 3, 5, 64)
+    p = to_pairs(x)
+    assert p.dtype == torch.float32 and p.shape == x.shape
+    assert ((from_pairs(p) - x).abs() <= x.abs() * 2 ** -16).all()
+
+
+@pytest.mark.parametrize("tile", [0, 20, 22, 24, 25, 41])
+@pytest.mark.parametrize("out_pair", [True, False])
+def test_conv_pair_vs_fp64(cuda, tile, out_pair):
+    torch.manual_seed(tile)
+    B, H, W, cin, cout = 2, 23, 31, 64, 128
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    xin = buf[..., 8:8 + cin]
+    out = torch.zeros(B, H, W, cout + 16, dtype=torch.float32, device=cuda)
+    fc(NHWC(to_pairs(buf.float()).to(cuda), 8, cin, pair=True), out=NHWC(out, 8, cout, pair=out_pair), tile=tile)
+    torch.cuda.synchronize()
+    ref = torch.relu(conv(xin.permute(0, 3, 1, 2)))
+    got = NHWC(out, 8, cout, pair=out_pair).nchw()
+    assert rel_l2(got, ref) < 5e-5
+    assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
+
+
+def test_conv_pair_residual_and_deconv_shuffle(cuda):
+    torch.manual_seed(1)
+    B, H, W = 2, 12, 10
+    conv = nn.Conv2d(64, 64, 3, 1, 1).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32", post_res=True)
+    x = torch.randn(B, H, W, 64, dtype=torch.float64)
+    r = torch.randn(B, H, W, 64, dtype=torch.float64)
+    out = NHWC(torch.zeros(B, H, W, 64, device=cuda), pair=True)
+    fc(NHWC(to_pairs(x.float()).to(cuda), pair=True), out=out, res=NHWC(to_pairs(r.float()).to(cuda), pair=True))
+    ref = torch.relu(conv(x.permute(0, 3, 1, 2)) + r.permute(0, 3, 1, 2))
+    assert rel_l2(out.nchw(), ref) < 5e-5
+    up = nn.ConvTranspose2d(64, 128, 2, stride=2).double()
+    fu = FusedConv(copy.deepcopy(up).float(), act=1, device=cuda, precision="fp32")
+    o2 = NHWC(torch.zeros(B, 2 * H, 2 * W, 128 + 64, device=cuda), 64, 128, pair=True)
+    fu(NHWC(to_pairs(x.float()).to(cuda), pair=True), out=o2)
+    ref2 = torch.relu(up(x.permute(0, 3, 1, 2)))
+    assert rel_l2(o2.nchw(), ref2) < 5e-5
+
+
+def test_bev_plan_pair_equals_fp32_plan(cuda):
+    """Pair storage feeds the MFMAs the same hi / lo halves the fp32 plan splits
+    at its fragment reads: the head outputs match bit for bit."""
+    from triton_client_amd.config.lidar import KITTI_PILLARS, PointPillarsConfig
+    from triton_client_amd.models.common import fuse_model, randomize_bn
+    from triton_client_amd.models.fast import FastBEV
+    from triton_client_amd.models.pointpillars import build_pointpillars
+
+    v = dataclasses.replace(KITTI_PILLARS, point_cloud_range=(0.0, -10.24, -3.0, 20.48, 10.24, 1.0))
+    m = build_pointpillars(PointPillarsConfig(voxel=v))
+    randomize_bn(m, 2)
+    m = fuse_model(m.eval())
+    nx, ny, _ = m.cfg.voxel.grid_size
+    canvas = torch.zeros(2, ny, nx, 64)
+    canvas[:, ::3, ::2] = torch.rand(2, (ny + 2) // 3, (nx + 1) // 2, 64)
+    fp = FastBEV(m, 2, device=cuda, precision="fp32", pair=True)
+    f32 = FastBEV(m, 2, device=cuda, precision="fp32", pair=False)
+    assert fp.pair and not f32.pair and fp.neck is not None
+    a = [o.values().clone() for o in fp.forward(NHWC(to_pairs(canvas).to(cuda), pair=True))]
+    b = [o.values().clone() for o in f32.forward(NHWC(canvas.to(cuda)))]
+    c = [o.values().clone() for o in fp.forward(NHWC(canvas.to(cuda)))]  # plain canvas: converted on entry
+    torch.cuda.synchronize()
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x, y) and torch.equal(x, z)
+    with torch.no_grad():
+        ref = m.double().bev_forward(canvas.double().permute(0, 3, 1, 2))
+    m.float()
+    for o, r in zip(a, ref):
+        assert rel_l2(o.permute(0, 3, 1, 2), r) < 2e-4
+
+
+def test_lidar_pipeline_uses_pair_canvas(cuda):
+    import numpy as np
+
+    from triton_client_amd.pipelines import LidarPipeline
+    from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    lid = LidarPipeline(batch=2, max_points=32768, device=cuda, z_offset=1.5, precision="fp32")
+    for b in range(2):
+        c = lidar_sweep(spec, b)
+        raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+        lid.data[b * lid.frame_bytes: b * lid.frame_bytes + raw.numel()].copy_(raw)
+        lid.frame_n[b] = c.shape[0]
+    lid.calibrate_detection_density(500.0)
+    r1 = lid.step()
+    n1 = r1.count.clone()
+    assert lid.enc.pair and lid.fast.pair
+    r2 = lid.step()  # pair canvas from the scatter, cleared by cell list
+    torch.cuda.synchronize()
+    assert torch.equal(n1, r2.count) and int(n1.min()) > 0

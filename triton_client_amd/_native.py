@@ -47,6 +47,7 @@ _KERNEL_SIGS = {
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, I, P],
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
+    "tca_conv_nhwc_x3p": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P],
     "tca_zero_i32": [P, I, P],
     "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
     "tca_anchor_decode_filter_keyed": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, P, P, P, P, P, P, I,
@@ -66,6 +67,7 @@ _KERNEL_SIGS = {
     "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, P],
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     "tca_bev_neck_head_x3": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
+    "tca_bev_neck_head_x3p": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     # SECOND-IoU: sparse 3D backbone + RoI head (spconv.hip)
     "tca_sp_offsets": [P, I, P, P, P],
     "tca_sp_vfe_slots": [P, I, I, P, P, I, P, P, I, I, P, P, P, P, P, P],

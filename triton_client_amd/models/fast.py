@@ -24,7 +24,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, upsample2x_nhwc
+from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, to_pairs, upsample2x_nhwc
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 
@@ -41,10 +41,10 @@ class _Buffers:
         self.dtype = act_dtype(precision) if self.device.type == "cuda" else torch.float32
         self.bufs = []
 
-    def new(self, B, H, W, C) -> NHWC:
+    def new(self, B, H, W, C, pair: bool = False) -> NHWC:
         t = torch.zeros((B, H, W, C), dtype=self.dtype, device=self.device)
         self.bufs.append(t)
-        return NHWC(t)
+        return NHWC(t, pair=pair)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in self.bufs)
@@ -210,15 +210,19 @@ class _BEVBackbonePlan:
     """BaseBEVBackbone / det3d RPN: down blocks (ping-pong buffers) and deblocks
     writing straight into their channel slices of the concat buffer."""
 
-    def __init__(self, bb, B: int, ny: int, nx: int, bufs: _Buffers, device):
+    def __init__(self, bb, B: int, ny: int, nx: int, bufs: _Buffers, device, pair: bool = False):
         self.blocks = []
         H, W = ny, nx
         pr = bufs.precision
-        for blk in bb.blocks:
-            convs = [_fc(c, device, pr) for c in blk]
+        convs_all = [[_fc(c, device, pr) for c in blk] for blk in bb.blocks]
+        ups_all = [FusedConv(u.conv, act=ACT_RELU, device=device, precision=pr) for u in bb.deblocks]
+        # pair storage (fp32 mode): every conv must take it (global_load_lds kernels)
+        self.pair = pair and torch.device(device).type == "cuda" and all(
+            c.pair_ok() for c in [cv for blk in convs_all for cv in blk] + ups_all)
+        for convs in convs_all:
             s = convs[0].s
             H, W = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
-            pp = [bufs.new(B, H, W, convs[0].N), bufs.new(B, H, W, convs[0].N)]
+            pp = [bufs.new(B, H, W, convs[0].N, self.pair), bufs.new(B, H, W, convs[0].N, self.pair)]
             self.blocks.append((convs, pp, H, W))
         self.ups = []
         up_c = [u.conv.out_channels for u in bb.deblocks]
@@ -229,11 +233,11 @@ class _BEVBackbonePlan:
         else:
             H0, W0 = self.blocks[0][2] * int(round(s0)), self.blocks[0][3] * int(round(s0))
         self.out_hw = (H0, W0)
-        self.cat = bufs.new(B, H0, W0, sum(up_c))
+        self.cat = bufs.new(B, H0, W0, sum(up_c), self.pair)
         off = 0
-        for u, c in zip(bb.deblocks, up_c):
+        for u, fc, c in zip(bb.deblocks, ups_all, up_c):
             assert u.fused, "call fuse_model() first"
-            self.ups.append((FusedConv(u.conv, act=ACT_RELU, device=device, precision=pr), off, c))
+            self.ups.append((fc, off, c))
             off += c
 
     def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
@@ -250,7 +254,7 @@ class _BEVBackbonePlan:
 
     def forward(self, canvas: NHWC) -> NHWC:
         for x, (up, off, c) in zip(self.forward_blocks(canvas), self.ups):
-            up(x, out=NHWC(self.cat.t, off, c))
+            up(x, out=self.cat.slice(off, c))
         return self.cat
 
 
@@ -258,7 +262,7 @@ class FastBEV:
     """PointPillars BEV backbone + anchor head on fused convs."""
 
     def __init__(self, model, batch: int, device="cuda", fused_neck: bool = True,
-                 bev_hw: Optional[Tuple[int, int]] = None, precision: str = "bf16"):
+                 bev_hw: Optional[Tuple[int, int]] = None, precision: str = "bf16", pair: bool = True):
         """bev_hw: (ny, nx) of the backbone input when it is not the voxel grid
         (SECOND: the 8x-downsampled HeightCompression map)."""
         self.device = torch.device(device)
@@ -270,7 +274,11 @@ class FastBEV:
             nx, ny, _ = cfg.voxel.grid_size
         B = batch
         bufs = self.bufs = _Buffers(self.device, precision)
-        self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)
+        # fp32 mode keeps the BEV chain in pair storage (hi / lo bf16 halves as the
+        # MFMA fragments read them): no split on any operand read
+        self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device, pair=pair and precision == "fp32")
+        self.pair = self.bb.pair
+        self.canvas_pairs = None  # conversion buffer for callers that hand in a plain fp32 canvas
         self.blocks, self.ups, self.cat, self.out_hw = self.bb.blocks, self.bb.ups, self.bb.cat, self.bb.out_hw
         H0, W0 = self.out_hw
         hd = model.head
@@ -283,6 +291,8 @@ class FastBEV:
         self.n_cls, self.n_box, self.n_dir = (hd.conv_cls.out_channels, hd.conv_box.out_channels,
                                               hd.conv_dir.out_channels)
         self.hout = bufs.new(B, H0, W0, self.head.N)
+        if self.pair and not self.head.pair_ok():
+            raise ValueError("pair storage: the head conv must take the global_load_lds kernels")
         # deblocks + head as one kernel (K15) when the shapes fit its contract
         self.neck = None
         strides = self.bb.up_strides(model.backbone)
@@ -296,6 +306,13 @@ class FastBEV:
                 self.neck = FusedNeckHead(ups, si, self.head, self.device)
 
     def forward(self, canvas: NHWC):
+        if self.pair and not canvas.pair:
+            if self.canvas_pairs is None or self.canvas_pairs.t.shape != canvas.tensor().shape:
+                self.canvas_pairs = NHWC(torch.empty_like(canvas.tensor(), dtype=torch.float32), pair=True)
+            self.canvas_pairs.t.copy_(to_pairs(canvas.tensor()))
+            canvas = self.canvas_pairs
+        elif canvas.pair and not self.pair:
+            raise TypeError("pair canvas handed to a plan built without pair storage")
         if self.neck is not None:
             self.neck(self.bb.forward_blocks(canvas), self.hout)
         else:

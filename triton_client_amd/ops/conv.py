@@ -32,14 +32,23 @@ from ..models.common import ACT_LEAKY, ACT_NONE, ACT_RELU, ACT_SILU, apply_act
 
 @dataclass
 class NHWC:
-    """A channel slice [off, off + c) of an NHWC buffer ``t`` [B, H, W, C]."""
+    """A channel slice [off, off + c) of an NHWC buffer ``t`` [B, H, W, C].
+
+    ``pair``: the fp32 buffer holds fp32-mode *pair* storage — per 8
+    channels {hi bf16 x 8 | lo bf16 x 8}, the bytes of 8 fp32 (see
+    :func:`to_pairs`); the split-product kernels read its halves as MFMA
+    fragments directly.  ``tensor()`` is then the raw storage; ``values()``
+    / ``nchw()`` decode it."""
     t: torch.Tensor
     off: int = 0
     c: Optional[int] = None
+    pair: bool = False
 
     def __post_init__(self):
         if self.c is None:
             self.c = self.t.shape[-1] - self.off
+        if self.pair:
+            assert self.t.dtype == torch.float32 and self.off % 8 == 0 and self.c % 8 == 0, (self.off, self.c)
 
     @property
     def shape(self):
@@ -48,8 +57,34 @@ class NHWC:
     def tensor(self) -> torch.Tensor:
         return self.t[..., self.off:self.off + self.c]
 
+    def slice(self, off: int, c: int) -> "NHWC":
+        return NHWC(self.t, self.off + off, c, self.pair)
+
+    def values(self) -> torch.Tensor:
+        """NHWC fp32 / bf16 values of the slice (pairs decoded)."""
+        return from_pairs(self.tensor()) if self.pair else self.tensor()
+
     def nchw(self) -> torch.Tensor:
-        return self.tensor().permute(0, 3, 1, 2)
+        return self.values().permute(0, 3, 1, 2)
+
+
+def to_pairs(x: torch.Tensor) -> torch.Tensor:
+    """[..., C] fp32 values (C % 8 == 0) -> [..., C] fp32 *storage* holding, per
+    8 channels, hi = bf16(x) then lo = bf16(x - hi)."""
+    *lead, C = x.shape
+    assert C % 8 == 0, C
+    v = x.float().reshape(*lead, C // 8, 1, 8)
+    hi = v.to(torch.bfloat16)
+    lo = (v - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, lo], -2).reshape(*lead, 2 * C).view(torch.float32)
+
+
+def from_pairs(p: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`to_pairs`: pair storage -> fp32 values (hi + lo)."""
+    *lead, C = p.shape
+    assert C % 8 == 0, C
+    h = p.contiguous().view(torch.bfloat16).reshape(*lead, C // 8, 2, 8).float()
+    return (h[..., 0, :] + h[..., 1, :]).reshape(*lead, C)
 
 
 def _ceil(x, m):
@@ -169,14 +204,28 @@ class FusedConv:
             if t.dtype != self.dtype:
                 raise TypeError(f"{self.precision} conv needs {self.dtype} activations, got {t.dtype}")
         gh, gw = (H, W) if self.transpose else (Ho, Wo)
+        act = self.act | (16 if (self.post_res and res is not None) else 0)
+        rp = (_native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
+              res.off if res is not None else 0)
+        if x.pair or out.pair:
+            # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
+            if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
+                raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
+            _native.call("tca_conv_nhwc_x3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                         _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
+                         self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, act, *rp, self.shuffle,
+                         tile if tile in (20, 22, 24, 25, 41) else 0, int(out.pair), _native.stream_ptr(stream))
+            return out
         fn = "tca_conv_nhwc_x3" if self.precision == "fp32" else "tca_conv_nhwc"
         _native.call(fn, _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                      _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
-                     self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off,
-                     self.act | (16 if (self.post_res and res is not None) else 0),
-                     _native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
-                     res.off if res is not None else 0, self.shuffle, tile, _native.stream_ptr(stream))
+                     self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, act, *rp, self.shuffle, tile,
+                     _native.stream_ptr(stream))
         return out
+
+    def pair_ok(self) -> bool:
+        """The pair-storage kernels take this conv (Cin % 32, K == Kp)."""
+        return self.precision == "fp32" and self.cin_p % 32 == 0 and self.K == self.Kp
 
     def _cpu(self, x: NHWC, out: NHWC, res: Optional[NHWC]) -> NHWC:
         xi = x.nchw().float()[:, : self.cin]

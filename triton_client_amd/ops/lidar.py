@@ -227,6 +227,7 @@ class PillarEncoder:
         assert dtype in (torch.bfloat16, torch.float32), dtype
         self.dtype = dtype
         self._dt = 0 if dtype == torch.float32 else 2
+        self.pair = False  # fp32 canvas written as pair storage (ops/conv.py to_pairs)
         self.device = torch.device(device)
         self.W = weight.detach().float().contiguous().to(self.device)  # [64, 10]
         self.b = bias.detach().float().contiguous().to(self.device)
@@ -239,7 +240,23 @@ class PillarEncoder:
             self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
             self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
 
+    def set_pair(self, pair: bool) -> None:
+        """fp32 canvas only: write the scatter in pair storage (what a pair-storage
+        BEV plan reads).  Zero bytes are zero in both forms, so the per-frame
+        clear-by-cell-list stays valid across a switch."""
+        if pair and self.dtype != torch.float32:
+            raise ValueError("pair storage needs the fp32 canvas")
+        self.pair = bool(pair)
+        self._dt = 5 if pair else (0 if self.dtype == torch.float32 else 2)
+
+    def canvas_nhwc(self):
+        from .conv import NHWC
+        return NHWC(self.canvas, pair=self.pair)
+
     def canvas_nchw(self) -> torch.Tensor:
+        if self.pair:
+            from .conv import from_pairs
+            return from_pairs(self.canvas).permute(0, 3, 1, 2)
         return self.canvas.permute(0, 3, 1, 2)  # channels_last view
 
     def clear(self, vox: Voxelizer, stream=None) -> None:

@@ -95,10 +95,15 @@ class FusedNeckHead:
         for x, s in zip(xs, self.strides):
             assert x.shape[0] == B and x.shape[1] * s == H and x.shape[2] * s == W, (x.shape, s, out.shape)
         assert out.off == 0 and out.t.dtype == self.dtype and all(x.t.dtype == self.dtype for x in xs)
+        pair = xs[0].pair
+        if any(x.pair != pair for x in xs) or (pair and self.precision != "fp32") or out.pair:
+            raise TypeError("neck inputs: all pair storage (fp32 mode) or none; output fp32")
         ptrs = (ctypes.c_void_p * n)(*[x.t.data_ptr() for x in xs])
         ldx = (ctypes.c_int * n)(*[x.t.shape[-1] for x in xs])
         offx = (ctypes.c_int * n)(*[x.off for x in xs])
-        _native.call("tca_bev_neck_head_x3" if self.precision == "fp32" else "tca_bev_neck_head", n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
+        fn = ("tca_bev_neck_head_x3p" if pair else "tca_bev_neck_head_x3") if self.precision == "fp32" \
+            else "tca_bev_neck_head"
+        _native.call(fn, n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
                      _native.ptr(self.wh), _native.ptr(self.bh), self.nh, _native.ptr(out.t), out.t.shape[-1],
                      B, H, W, self.grid, _native.stream_ptr(stream))
         return out

@@ -64,6 +64,8 @@ class LidarPipeline:
     def build_fast(self):
         from ..models.fast import FastBEV
         self.fast = FastBEV(self.model, self.B, self.device, precision=self.precision)
+        # fp32 mode: the scatter writes the pair storage the plan reads
+        self.enc.set_pair(self.fast.pair)
         return self.fast
 
     @torch.no_grad()
@@ -77,8 +79,11 @@ class LidarPipeline:
                               self.normalize, self.z_offset)
         self.enc.clear(self.vox)
         self.vox.assign(pts, cnt)
+        pair = self.enc.pair
+        self.enc.set_pair(False)  # the PyTorch module reads plain fp32
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
+        self.enc.set_pair(pair)  # (the next frame's scatter; its clear zeroes these cells)
         if lsuv:
             h = self.model.head
             lsuv_rescale(self.model, lambda: self.model.bev_forward(canvas), head_modules=[h.conv_cls, h.conv_dir])
@@ -106,15 +111,14 @@ class LidarPipeline:
 
     @torch.no_grad()
     def step(self):
+        f = (self.fast or self.build_fast()) if self.use_fast else None  # sets the canvas storage first
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
         self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
-        if self.use_fast:
-            from ..ops.conv import NHWC
-            f = self.fast or self.build_fast()
-            return self.post(*f.forward(NHWC(self.enc.canvas)))
+        if f is not None:
+            return self.post(*f.forward(self.enc.canvas_nhwc()))
         cls, box, dir_ = self.model.bev_forward(canvas)
         return self.post(cls, box, dir_)

@@ -207,10 +207,9 @@ class PointPillarsModel(ServedModel):
             self.coords[0, :V, 0] = 0
             self.nump[0, :V].copy_(self.pin_n[:V], non_blocking=True)
             self.vcount.fill_(V)
+            fast = self.pipe.fast or self.pipe.build_fast()  # sets the canvas storage first
             self.enc.encode_from_voxels(self.voxels, self.nump, self.coords, self.vcount)
-            from ..ops.conv import NHWC
-            fast = self.pipe.fast or self.pipe.build_fast()
-            res = self.pipe.post(*fast.forward(NHWC(self.enc.canvas)))
+            res = self.pipe.post(*fast.forward(self.enc.canvas_nhwc()))
         else:
             from ..models.pointpillars import pillar_point_features, scatter_to_bev
             from ..ops.lidar import AnchorPostprocess
