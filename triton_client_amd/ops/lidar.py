@@ -277,7 +277,8 @@ class PillarEncoder:
                      _native.ptr(vox.voxel_count), self.B, self.cfg.max_voxels, self.cfg.max_points_per_voxel,
                      _native.ptr(self.W), _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny,
                      _native.ptr(self.canvas), _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
-        return self.canvas_nchw()
+        # pair storage: the plan reads the raw buffer; decoding it here would cost a full pass
+        return None if self.pair else self.canvas_nchw()
 
     def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
         """voxels [B, V, P, 4], num_points [B, V], coords [B, V, 4], voxel_count [B]."""
@@ -285,7 +286,8 @@ class PillarEncoder:
                      _native.ptr(voxel_count), voxels.shape[0], voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
                      _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas),
                      _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
-        return self.canvas_nchw()
+        # pair storage: the plan reads the raw buffer; decoding it here would cost a full pass
+        return None if self.pair else self.canvas_nchw()
 
 
 def pillar_features_reference(voxels: torch.Tensor, num_points: torch.Tensor, coords: torch.Tensor,
