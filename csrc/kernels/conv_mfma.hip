@@ -1450,7 +1450,13 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     case 22: return launch_glds_x3<128, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
     case 25: return launch_glds_x3<128, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
+    case 26: return launch_glds_x3<256, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
+    case 30: return launch_glds_x3<128, 128, 4, 2, 3, true, PAIR_OUT>(a, stream);
+    case 32: return launch_glds_x3<128, 64, 4, 2, 3, true, PAIR_OUT>(a, stream);
+    case 35: return launch_glds_x3<256, 64, 4, 2, 3, true, PAIR_OUT>(a, stream);
+    case 37: return launch_glds_x3<256, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 41: return launch_glds_x3<128, 64, 8, 1, 2, true, PAIR_OUT>(a, stream);
+    case 42: return launch_glds_x3<256, 64, 8, 1, 2, true, PAIR_OUT>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -1607,7 +1613,7 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
 // fp32 mode, pair activations: `in` (and `res`) hold pairs (see pair_split8),
 // `out` pairs when out_pair, else fp32.  Same slice / residual / pixel-shuffle
 // contract as tca_conv_nhwc_x3; the global_load_lds kernels only (Cin % 32 == 0,
-// Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 41.
+// Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42.
 TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
                               const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
                               int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
@@ -1625,6 +1631,9 @@ TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int
   a.N = N; a.K = KH * KW * Cin; a.Kp = Kp; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off;
   a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
   if (a.K > Kp || (Cin % 32) != 0 || Kp != a.K) return (int)hipErrorInvalidValue;
-  if (tile == 0) tile = N <= 64 ? 41 : 20;
+  // auto tile, measured on MI355X at batch 32 (tools/bench_conv_x3.py --pair ->
+  // profiles/r2/conv_x3p_tiles.jsonl): N <= 64: 256x64 (4x2 waves), 3-stage 128x64 for
+  // stride 2; wider: 128x128 4x2
+  if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 20;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
 }

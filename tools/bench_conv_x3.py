@@ -3,7 +3,10 @@ detectors' layer shapes at the headline batch (32).  One JSON line per shape:
 µs per tile, useful fp32 TFLOP/s, and the bf16-MFMA utilisation the 3 split
 products imply (3 x FLOPs / 2.5 PF).
 
-    python tools/bench_conv_x3.py [tiles,comma,separated] [layer-prefixes]
+    python tools/bench_conv_x3.py [tiles,comma,separated] [layer-prefixes] [--pair]
+
+--pair: input and output in pair storage (ops/conv.py to_pairs), the BEV
+chain's fp32-mode format.
 """
 import json
 import sys
@@ -14,7 +17,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 sys.path.insert(0, ".")
-from triton_client_amd.ops.conv import NHWC, FusedConv  # noqa: E402
+from triton_client_amd.ops.conv import NHWC, FusedConv, to_pairs  # noqa: E402
+
+PAIR = "--pair" in sys.argv
+if PAIR:
+    sys.argv.remove("--pair")
 
 B = 32
 SHAPES = [
@@ -59,8 +66,8 @@ def main():
         conv = nn.Conv2d(ci, co, k, s, k // 2, bias=True).to(dev)
         fc = FusedConv(conv, act=act, device=dev, precision="fp32")
         x = torch.randn(b, H, W, ci, device=dev)
-        xin = NHWC(x)
-        out = fc(xin)
+        xin = NHWC(to_pairs(x), pair=True) if PAIR else NHWC(x)
+        out = fc(xin, out=NHWC(torch.empty(b, *fc.out_hw(H, W), fc.N, device=dev), pair=PAIR))
         cm = conv.to(memory_format=torch.channels_last)
         xc = x.permute(0, 3, 1, 2)
         actf = {0: lambda t: t, 1: F.relu, 2: F.silu}[act]

@@ -92,6 +92,8 @@ def _ceil(x, m):
 
 
 PRECISIONS = ("fp32", "bf16")
+# global_load_lds split-product tiles with pair-storage instantiations (conv_mfma.hip launch_glds_x3p)
+PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42)
 
 
 def act_dtype(precision: str) -> torch.dtype:
@@ -214,7 +216,7 @@ class FusedConv:
             _native.call("tca_conv_nhwc_x3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                          _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
                          self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, act, *rp, self.shuffle,
-                         tile if tile in (20, 22, 24, 25, 41) else 0, int(out.pair), _native.stream_ptr(stream))
+                         tile if tile in PAIR_TILES else 0, int(out.pair), _native.stream_ptr(stream))
             return out
         fn = "tca_conv_nhwc_x3" if self.precision == "fp32" else "tca_conv_nhwc"
         _native.call(fn, _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
