@@ -363,27 +363,39 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
   // issue side: (tile, branch, chunk) with chunk < cin/32 a deconv step, else head step chunk - cin/32
   int i_k = 0, i_br = 0, i_kc = 0;
   Tile it = tile_of(a.S, t_lo + slot, nqt, X_BM);
+  // each lane's A source row for the current (tile, branch), computed once per
+  // branch (the q -> (Y, X) division is most of the loop's VALU otherwise);
+  // the K steps of the branch only add their channel offset
+  const float* a_src[X_A_INS];
+  auto row_sources = [&]() {
+    const int s = a.s[i_br], f = S / s;
+    const int Hi = a.H / s, Wi = a.W / s;
+    const int sy = it.cy / s, sx = it.cx / s;
+    const float* xb = a.x[i_br] + a.offx[i_br];
+    const int ldx = a.ldx[i_br];
+#pragma unroll
+    for (int j = 0; j < X_A_INS; ++j) {
+      const int row = (wid * X_A_INS + j) * 8 + lrow;
+      const int q = it.q0 + row;
+      a_src[j] = nullptr;
+      if (q < nq) {
+        const int Y = q / Wq, X = q - Y * Wq;
+        a_src[j] = xb + (((long)it.b * Hi + Y * f + sy) * Wi + X * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
+      }
+    }
+  };
   auto issue = [&](int buf) {
     unsigned char* sa = smem + buf * X_STAGE;
     unsigned char* sb = sa + X_A_BYTES;
     unsigned char* sbias = sb + X_B_BYTES;
     const int nkc = a.cin[i_br] / 32;
     if (i_kc < nkc) {
-      const int s = a.s[i_br], f = S / s;
-      const int Hi = a.H / s, Wi = a.W / s;
-      const int sy = it.cy / s, sx = it.cx / s;
+      const int s = a.s[i_br];
       const int ci0 = i_kc * 32;
-      const float* xb = a.x[i_br] + a.offx[i_br] + ci0;
-      const int ldx = a.ldx[i_br];
+      if (i_kc == 0) row_sources();
 #pragma unroll
       for (int j = 0; j < X_A_INS; ++j) {
-        const int row = (wid * X_A_INS + j) * 8 + lrow;
-        const int q = it.q0 + row;
-        const void* g = g_neck_zero_page;
-        if (q < nq) {
-          const int Y = q / Wq, X = q - Y * Wq;
-          g = xb + (((long)it.b * Hi + Y * f + sy) * Wi + X * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
-        }
+        const void* g = a_src[j] ? (const void*)(a_src[j] + ci0) : (const void*)g_neck_zero_page;
         glds16(g, sa + (wid * X_A_INS + j) * 1024);
       }
       const int sub = (it.cy % s) * s + (it.cx % s);

@@ -1633,7 +1633,8 @@ TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int
   if (a.K > Kp || (Cin % 32) != 0 || Kp != a.K) return (int)hipErrorInvalidValue;
   // auto tile, measured on MI355X at batch 32 (tools/bench_conv_x3.py --pair ->
   // profiles/r2/conv_x3p_tiles.jsonl): N <= 64: 256x64 (4x2 waves), 3-stage 128x64 for
-  // stride 2; wider: 128x128 4x2
-  if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 20;
+  // stride 2; wider: 128x128 2x4
+  // (4-wave 64x64-per-wave tiles measured slower on every layer)
+  if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
 }
