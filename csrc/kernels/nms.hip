@@ -601,3 +601,107 @@ TCA_API int tca_box_iou(const float* a, int n, const float* b, int m, float* out
   box_iou_kernel<<<(unsigned)((t + 255) / 256), 256, 0, stream>>>(a, n, b, m, out);
   TCA_LAUNCH_CHECK();
 }
+
+// ---- merge-NMS (K4m; reference clients/postprocess/yolov5_postprocess.py:111-117,
+// `merge = True`): every kept box becomes the score-weighted mean of all the
+// image's candidates of its class with IoU > thr (itself included), and with
+// `redundant` a kept box that overlaps no other candidate is dropped.  Applied
+// only when 1 < n < 3000 candidates, as in the reference.  Runs after
+// tca_nms_reduce (called without an output transform): one workgroup per image,
+// one wave per kept box, candidates streamed 64 at a time; kept results are then
+// compacted in score order and mapped to the original frame.
+namespace {
+constexpr int kMergeMaxKept = 1024;
+
+__global__ void __launch_bounds__(256) nms_merge_kernel(const float* __restrict__ kbox, const float* __restrict__ kscore,
+                                                        const int* __restrict__ kcls, const int* __restrict__ kcount,
+                                                        const float* __restrict__ cbox, const float* __restrict__ cscore,
+                                                        const int* __restrict__ ccls, const int* __restrict__ ccount,
+                                                        int cap, int max_out, float thr, int agnostic, int redundant,
+                                                        OutXform xf, float* __restrict__ out_box,
+                                                        float* __restrict__ out_score, int* __restrict__ out_cls,
+                                                        int* __restrict__ out_count) {
+  __shared__ float mbox[kMergeMaxKept][4];
+  __shared__ int keep_flag[kMergeMaxKept];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nk = min(kcount[b], max_out);
+  const int n = min(ccount[b], cap);
+  const bool merge = ccount[b] > 1 && ccount[b] < 3000;  // the reference's 1 < n < 3E3
+  const float* kb = kbox + (long)b * max_out * 4;
+  const float* cb = cbox + (long)b * cap * 4;
+  for (int k = wid; k < nk; k += nw) {
+    float me[4] = {kb[4 * k], kb[4 * k + 1], kb[4 * k + 2], kb[4 * k + 3]};
+    const int mc = kcls[(long)b * max_out + k];
+    float sw = 0.f, sx1 = 0.f, sy1 = 0.f, sx2 = 0.f, sy2 = 0.f;
+    int hits = 0;
+    if (merge) {
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        if (j < n && (agnostic || ccls[(long)b * cap + j] == mc)) {
+          const float* c = cb + 4 * (long)j;
+          if (iou_aa(me, c) > thr) {
+            const float w = cscore[(long)b * cap + j];
+            sw += w;
+            sx1 += w * c[0]; sy1 += w * c[1]; sx2 += w * c[2]; sy2 += w * c[3];
+            ++hits;
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        sw += __shfl_xor(sw, o); sx1 += __shfl_xor(sx1, o); sy1 += __shfl_xor(sy1, o);
+        sx2 += __shfl_xor(sx2, o); sy2 += __shfl_xor(sy2, o); hits += __shfl_xor(hits, o);
+      }
+    }
+    if (lane == 0) {
+      if (merge && sw > 0.f) {
+        me[0] = sx1 / sw; me[1] = sy1 / sw; me[2] = sx2 / sw; me[3] = sy2 / sw;
+      }
+      mbox[k][0] = me[0]; mbox[k][1] = me[1]; mbox[k][2] = me[2]; mbox[k][3] = me[3];
+      keep_flag[k] = !(merge && redundant && hits <= 1);
+    }
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  // compaction in score order: wave 0, 64 kept boxes per round, ballot prefix
+  int base = 0;
+  for (int k0 = 0; k0 < nk; k0 += 64) {
+    const int k = k0 + lane;
+    const bool f = k < nk && keep_flag[k];
+    const uint64_t bal = __ballot(f);
+    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+    if (f) {
+      float x1 = mbox[k][0], y1 = mbox[k][1], x2 = mbox[k][2], y2 = mbox[k][3];
+      if (xf.enable) {
+        x1 = fminf(fmaxf((x1 - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
+        x2 = fminf(fmaxf((x2 - xf.pad_x) / xf.gain_x, 0.f), xf.clip_w);
+        y1 = fminf(fmaxf((y1 - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
+        y2 = fminf(fmaxf((y2 - xf.pad_y) / xf.gain_y, 0.f), xf.clip_h);
+      }
+      float* o = out_box + ((long)b * max_out + pos) * 4;
+      o[0] = x1; o[1] = y1; o[2] = x2; o[3] = y2;
+      out_score[(long)b * max_out + pos] = kscore[(long)b * max_out + k];
+      out_cls[(long)b * max_out + pos] = kcls[(long)b * max_out + k];
+    }
+    base += __popcll(bal);
+  }
+  if (lane == 0) out_count[b] = base;
+}
+}  // namespace
+
+// kbox/kscore/kcls/kcount: tca_nms_reduce output (model coordinates, xform
+// null); cbox/cscore/ccls/ccount: the candidates it ran on (xyxy, box_dim 4).
+// Outputs must not alias the kept inputs.
+TCA_API int tca_nms_merge(const float* kbox, const float* kscore, const int* kcls, const int* kcount,
+                          const float* cbox, const float* cscore, const int* ccls, const int* ccount, int batch,
+                          int cap, int max_out, float thr, int agnostic, int redundant,
+                          const float* xform /*host [6] or null*/, float* out_box, float* out_score, int* out_cls,
+                          int* out_count, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (max_out > kMergeMaxKept) return (int)hipErrorInvalidValue;
+  OutXform xf{1.f, 1.f, 0.f, 0.f, 0.f, 0.f, 0};
+  if (xform) { xf = OutXform{xform[0], xform[1], xform[2], xform[3], xform[4], xform[5], 1}; }
+  nms_merge_kernel<<<batch, 256, 0, stream>>>(kbox, kscore, kcls, kcount, cbox, cscore, ccls, ccount, cap, max_out,
+                                              thr, agnostic, redundant, xf, out_box, out_score, out_cls, out_count);
+  TCA_LAUNCH_CHECK();
+}

@@ -115,3 +115,23 @@ def test_ap_per_class_classes_are_independent():
     for c in range(3):
         s = pc == c
         np.testing.assert_allclose(ap_all[c], ap_per_class(tp[s], conf[s], pc[s], tc[tc == c])[2][0], atol=1e-12)
+
+
+def test_merge_nms_hand_computed():
+    """Merge-NMS (reference yolov5_postprocess.py:111-117): A and B overlap
+    (IoU 90/110 > 0.45), NMS keeps A; merged A = (0.9 A + 0.6 B) / 1.5.  C has
+    no partner: dropped under ``redundant``, unchanged without it."""
+    from triton_client_amd.ops.yolo import merge_nms
+
+    box = np.array([[0, 0, 10, 10], [1, 0, 11, 10], [50, 50, 60, 60], [2, 0, 12, 10]], np.float32)
+    score = np.array([0.9, 0.6, 0.8, 0.7], np.float32)
+    cls = np.array([0, 0, 0, 1])  # the class-1 box overlaps A but is another class
+    keep = np.array([0, 2, 3])
+    mb, k = merge_nms(box, score, cls, keep, 0.45)
+    assert list(k) == [0]
+    np.testing.assert_allclose(mb[0], [0.4, 0.0, 10.4, 10.0], rtol=1e-6)
+    mb, k = merge_nms(box, score, cls, keep, 0.45, redundant=False)
+    assert list(k) == [0, 2, 3]
+    np.testing.assert_allclose(mb[1], box[2]) and np.testing.assert_allclose(mb[2], box[3])
+    mb, k = merge_nms(box, score, cls, np.array([0, 2]), 0.45, agnostic=True)
+    np.testing.assert_allclose(mb[0], (0.9 * box[0] + 0.6 * box[1] + 0.7 * box[3]) / 2.2, rtol=1e-6)

@@ -425,3 +425,32 @@ def test_fused_conv_small_halo(cuda, cin, cout, s):
             err = (got - ref).abs().max().item()
             assert err < 0.03 * max(1.0, ref.abs().max().item()), (B, H, W, post, err)
             assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("agnostic", [False, True])
+def test_yolo_merge_nms_gpu_matches_cpu(cuda, agnostic):
+    """tca_nms_merge (K4m) == the NumPy merge-NMS on the same decoded heads."""
+    from triton_client_amd.models.yolov5 import STRIDES
+    from triton_client_amd.ops.image import frame_xform
+    from triton_client_amd.ops.yolo import YoloPostprocess
+
+    torch.manual_seed(3)
+    nc, img = 6, (128, 160)
+    anchors = torch.tensor([[10, 13, 16, 30, 33, 23], [30, 61, 62, 45, 59, 119], [116, 90, 156, 198, 373, 326]],
+                           dtype=torch.float32).reshape(3, 3, 2)
+    heads = [torch.randn(2, 3 * (5 + nc), img[0] // s, img[1] // s) * 2.0 + 0.5 for s in STRIDES]
+    xf, _ = frame_xform((240, 320), img, "letterbox")
+    pg = YoloPostprocess(nc, anchors, img, conf_thres=0.3, iou_thres=0.45, device=cuda, merge=True, agnostic=agnostic)
+    pc = YoloPostprocess(nc, anchors, img, conf_thres=0.3, iou_thres=0.45, device="cpu", merge=True, agnostic=agnostic)
+    rg = pg([h.to(cuda) for h in heads], xf).per_image()
+    rc = pc.cpu(heads, xf).per_image()
+    merged_any = False
+    for g, c in zip(rg, rc):
+        assert len(g["score"]) == len(c["score"]) and len(c["score"]) > 0
+        np.testing.assert_array_equal(g["cls"], c["cls"])
+        np.testing.assert_allclose(g["score"], c["score"], rtol=1e-5)
+        np.testing.assert_allclose(g["box"], c["box"], rtol=1e-4, atol=2e-3)
+    plain = YoloPostprocess(nc, anchors, img, conf_thres=0.3, iou_thres=0.45, device="cpu", agnostic=agnostic)
+    for p, c in zip(plain.cpu(heads, xf).per_image(), rc):
+        merged_any |= len(p["score"]) != len(c["score"]) or not np.allclose(p["box"][:len(c["box"])], c["box"])
+    assert merged_any  # the merge changed something on these heads

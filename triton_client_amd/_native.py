@@ -38,6 +38,7 @@ _KERNEL_SIGS = {
     "tca_nms_mask_rot": [P, I, P, P, P, I, I, I, F, I, P, P, P],
     "tca_nms_reduce": [P, P, P, I, I, P, I, P, P, I, I, P, P, P, P, P, P],
     "tca_box_iou": [P, I, P, I, P, P],
+    "tca_nms_merge": [P, P, P, P, P, P, P, P, I, I, I, F, I, I, P, P, P, P, P, P],
     "tca_pc2_unpack": [P, P, P, I, I, I, P, P, I, F, P, I, P, P, P, P],
     "tca_pc2_blocks_per_frame": [I],
     "tca_vox_blocks_per_frame": [I],

@@ -7,8 +7,12 @@ Appendix A5/A10): an empty result is an empty detection set (the reference
 returns the AssertionError object); output dtypes follow the data.
 
 Deviations, documented: candidates beyond 8192 per image are cut to the top
-8192 by score before NMS (reference: 30000); merge-NMS (off by default in the
-reference, ``merge = False``) is only available on the CPU path.
+8192 by score before NMS (reference: 30000).  Merge-NMS (``merge=True``; off by
+default, as in the reference's ``merge = False``) follows
+``yolov5_postprocess.py:111-117``: each kept box becomes the score-weighted mean
+of its class's candidates with IoU > iou_thres, and with ``redundant`` (the
+reference's default) kept boxes overlapping no other candidate are dropped;
+only when 1 < n < 3000 candidates.  GPU: ``tca_nms_merge`` (csrc/kernels/nms.hip).
 """
 from __future__ import annotations
 
@@ -36,8 +40,10 @@ def _on_gpu(t) -> bool:
 class YoloPostprocess:
     def __init__(self, nc: int, anchors: torch.Tensor | Sequence, img_hw=(640, 640), conf_thres: float = 0.3,
                  iou_thres: float = 0.45, max_det: int = 300, max_nms: int = 8192, agnostic: bool = False,
-                 multi_label: bool = False, classes: Optional[Sequence[int]] = None, device="cuda"):
+                 multi_label: bool = False, classes: Optional[Sequence[int]] = None, device="cuda",
+                 merge: bool = False, redundant: bool = True):
         self.nc = nc
+        self.merge, self.redundant = merge, redundant
         a = torch.as_tensor(anchors, dtype=torch.float32).reshape(3, -1, 2)
         self.anchors = a.cpu()
         self.na = a.shape[1]
@@ -71,9 +77,26 @@ class YoloPostprocess:
         if not _on_gpu(heads[0]):
             return self.cpu(heads, xform)
         cand, decoded = self._filter(heads, decoded_out, stream)
+        xf = xform.as_list() if xform is not None else None
         res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
-                           xform.as_list() if xform is not None else None, prefix="yolo_nms_", stream=stream)
+                           None if self.merge else xf, prefix="yolo_nms_", stream=stream)
+        if self.merge:
+            res = self._merge(cand, res, xf, stream)
         return (res, decoded) if decoded_out else res
+
+    def _merge(self, cand, kept: NmsResult, xf, stream=None) -> NmsResult:
+        B, md = kept.score.shape
+        out = NmsResult(self.ws.get("yolo_merge_box", (B, md, 4), torch.float32),
+                        self.ws.get("yolo_merge_score", (B, md), torch.float32),
+                        self.ws.get("yolo_merge_cls", (B, md), torch.int32),
+                        self.ws.get("yolo_merge_count", (B,), torch.int32))
+        xf_arr = (ctypes.c_float * 6)(*[float(v) for v in xf]) if xf is not None else None
+        _native.call("tca_nms_merge", _native.ptr(kept.box), _native.ptr(kept.score), _native.ptr(kept.cls),
+                     _native.ptr(kept.count), _native.ptr(cand.box), _native.ptr(cand.score), _native.ptr(cand.cls),
+                     _native.ptr(cand.count), B, cand.box.shape[1], md, float(self.iou_thres), int(self.agnostic),
+                     int(self.redundant), xf_arr, _native.ptr(out.box), _native.ptr(out.score), _native.ptr(out.cls),
+                     _native.ptr(out.count), _native.stream_ptr(stream))
+        return out
 
     def _filter(self, heads, decoded_out: bool, stream=None):
         from .conv import NHWC
@@ -153,6 +176,8 @@ class YoloPostprocess:
             keep = sort_and_nms_cpu(bx, sc, cl.astype(np.int32), tie, 0, self.iou_thres, self.max_nms,
                                     self.max_det, self.agnostic)
             kb = bx[keep]
+            if self.merge and 1 < len(sc) < 3000 and len(keep):
+                kb, keep = merge_nms(bx, sc, cl, keep, self.iou_thres, self.agnostic, self.redundant)
             if xform is not None:
                 kb = xform.unmap_boxes(kb)
             outs.append((kb, sc[keep], cl[keep].astype(np.int32)))
@@ -165,6 +190,23 @@ class YoloPostprocess:
             n = len(ks)
             box[b, :n], score[b, :n], cls[b, :n], count[b] = kb, ks, kc, n
         return NmsResult(torch.from_numpy(box), torch.from_numpy(score), torch.from_numpy(cls), torch.from_numpy(count))
+
+
+def merge_nms(box: np.ndarray, score: np.ndarray, cls: np.ndarray, keep: np.ndarray, iou_thr: float,
+              agnostic: bool = False, redundant: bool = True):
+    """Merge-NMS of one image (reference yolov5_postprocess.py:111-117): kept
+    box i -> sum_j w_ij box_j / sum_j w_ij with w_ij = score_j [IoU(i, j) > thr,
+    same class unless agnostic] over all candidates j; with ``redundant`` a kept
+    box with no other such candidate is dropped.  Returns (merged boxes, keep)."""
+    iou = golden.box_iou_np(box[keep].astype(np.float64), box.astype(np.float64)) > iou_thr
+    if not agnostic:
+        iou &= cls[keep][:, None] == cls[None, :]
+    w = iou * score[None, :].astype(np.float64)
+    merged = (w @ box.astype(np.float64)) / w.sum(1, keepdims=True)
+    if redundant:
+        r = iou.sum(1) > 1
+        return merged[r].astype(np.float32), keep[r]
+    return merged.astype(np.float32), keep
 
 
 def detections_nx6(res: NmsResult) -> List[np.ndarray]:

@@ -30,7 +30,8 @@ class CameraPipeline:
     def __init__(self, model: Optional[YOLOv5] = None, batch: int = 16, src_hw: Tuple[int, int] = (720, 1280),
                  img_hw: Tuple[int, int] = (640, 640), mode: str = "letterbox", precision: str = "fp32",
                  conf_thres: float = 0.3, iou_thres: float = 0.45, max_det: int = 300, device="cuda",
-                 variant: str = "n", nc: int = 80, seed: int = 0, swap_rb: bool = False, fast: bool = True):
+                 variant: str = "n", nc: int = 80, seed: int = 0, swap_rb: bool = False, fast: bool = True,
+                 merge_nms: bool = False):
         self.device = torch.device(device)
         self.precision = precision
         dtype = act_dtype(precision)
@@ -45,7 +46,7 @@ class CameraPipeline:
         self.inp = torch.empty((batch, H, W, 3), dtype=dtype, device=self.device).permute(0, 3, 1, 2)
         self.xform, _ = frame_xform(self.src_hw, self.img_hw, mode)
         self.post = YoloPostprocess(model.cfg.nc, model.anchors.cpu(), img_hw, conf_thres, iou_thres, max_det,
-                                    device=self.device)
+                                    device=self.device, merge=merge_nms)
         # fused-MFMA concat-free plan (built lazily so calibration edits to the
         # module weights are picked up); the PyTorch module path stays for
         # validation and for CPU runs
