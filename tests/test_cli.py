@@ -119,9 +119,9 @@ def test_bagtools_and_bev(bags, tmp_path):
     with Bag(dst) as b:
         assert b.get_message_count() == 3
     out = str(tmp_path / "pcs")
-    assert bagtools.main(["extract-pc", pc, out, "--bev"]) == 0
+    assert bagtools.main(["extract-pc", pc, out, "--bev", "--scene"]) == 0
     files = sorted(os.listdir(out))
-    assert files == ["000000.npy", "000000.png", "000001.npy", "000001.png"]
+    assert files == ["000000.npy", "000000.png", "000000_scene.png", "000001.npy", "000001.png", "000001_scene.png"]
     pts = np.load(os.path.join(out, "000000.npy"))
     assert pts.shape[1] == 4 and np.isfinite(pts).all()
     c = boxes_to_corners_3d(np.array([[1.0, 2.0, 0.0, 4.0, 2.0, 1.5, np.pi / 2]]))

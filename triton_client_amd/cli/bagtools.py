@@ -2,7 +2,7 @@
 
     python -m triton_client_amd.cli.bagtools info BAG
     python -m triton_client_amd.cli.bagtools stitch SRC DST [-n 500] [--topics T ...]
-    python -m triton_client_amd.cli.bagtools extract-pc BAG OUT_DIR [--topic T] [--bev]
+    python -m triton_client_amd.cli.bagtools extract-pc BAG OUT_DIR [--topic T] [--bev] [--scene]
 """
 from __future__ import annotations
 
@@ -26,6 +26,8 @@ def main(argv=None) -> int:
     p.add_argument("out")
     p.add_argument("--topic", default=None, help="default: every PointCloud2 topic")
     p.add_argument("--bev", action="store_true", help="also write a bird's-eye-view PNG per cloud")
+    p.add_argument("--scene", action="store_true",
+                   help="also write a 3D scene view PNG per cloud (the reference's Open3D draw_scenes, headless)")
     a = ap.parse_args(argv)
     from ..ros import Bag, msgs
     from ..ros.bag import stitch
@@ -45,7 +47,7 @@ def main(argv=None) -> int:
     import numpy as np
 
     from ..ros.compat import cloud_to_numpy
-    from ..utils.visualize import render_bev
+    from ..utils.visualize import draw_scenes, render_bev
 
     os.makedirs(a.out, exist_ok=True)
     k = 0
@@ -57,6 +59,8 @@ def main(argv=None) -> int:
             np.save(os.path.join(a.out, f"{k:06d}.npy"), pts)
             if a.bev:
                 render_bev(pts, path=os.path.join(a.out, f"{k:06d}.png"))
+            if a.scene:
+                draw_scenes(pts, path=os.path.join(a.out, f"{k:06d}_scene.png"))
             k += 1
     print(f"extracted {k} clouds to {a.out}")
     return 0
