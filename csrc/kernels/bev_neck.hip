@@ -292,23 +292,43 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
 // with the same 32-chunk permutation), three MFMAs per fragment pair.  The
 // split head weights (2 x 60 KiB) do not fit in LDS next to the fp32
 // staging, so they are streamed through the ring instead: each branch's
-// flat step sequence is its cin/32 deconv K steps followed by 4 head steps
-// whose B slot carries the 80 x 32 split head weights of one 32-channel chunk
-// of that branch (A slot unused); the head GEMM consumes the branch's ReLU'd
-// accumulators chunk by chunk (split to hi/lo in registers).
+// flat step sequence is its cin/32 deconv K steps followed by 2 head steps
+// whose A slot carries the 80 x 64 split head weights of 64 of that branch's
+// channels; the head GEMM consumes the branch's ReLU'd accumulators chunk by
+// chunk (split to hi/lo in registers).
 // LDS rows are 128 B; slot swizzle s ^ ((r ^ (r >> 3)) & 7) (conv_mfma.hip swz3).
 // ============================================================================
-constexpr int X_BM = 128;                         // pixels per tile: 16 per wave (register budget)
-constexpr int X_FM = X_BM / (16 * NW);            // 16-pixel fragments per wave
+// v2 tiling: 256 pixels per tile (32 per wave, two 16-pixel fragments), so
+// every B fragment read from LDS feeds two fragment pairs; a 3-stage ring (two
+// steps in flight, counted vmcnt, one barrier per step; LDS DMA from inline asm
+// so hipcc inserts no vmcnt(0) in front of the fragment reads); tiles run over
+// the flat (frame, pixel) index of a sub-pixel class, so no tile is cut short at
+// a frame edge; each head step carries 64 of the branch's channels (two 32-channel
+// chunks of split head weights in the stage's A slot).
 constexpr int X_ROWB = 128;                       // 32 fp32 channels / 4 x {hi 8, lo 8}
-constexpr int X_A_BYTES = X_BM * X_ROWB;          // 16 KiB
-constexpr int X_B_BYTES = CB * X_ROWB;            // 16 KiB (head steps use 80 rows of it)
-constexpr int X_STAGE = X_A_BYTES + X_B_BYTES + BIAS_BYTES;
-constexpr int X_BH_OFF = 2 * X_STAGE;
-constexpr int X_LDS_BYTES = X_BH_OFF + NH * 4;
-constexpr int X_A_INS = X_BM / (8 * NW), X_B_INS = CB / (8 * NW);
+constexpr int Y_BM = 256;                         // pixels per tile
+constexpr int Y_FM = Y_BM / (16 * NW);            // 16-pixel fragments per wave (2)
+constexpr int Y_STAGES = 3;
+constexpr int Y_A_BYTES = Y_BM * X_ROWB;          // 32 KiB (head steps: 2 x [80 rows][128 B])
+constexpr int Y_B_BYTES = CB * X_ROWB;            // 16 KiB
+constexpr int Y_STAGE = Y_A_BYTES + Y_B_BYTES + BIAS_BYTES;
+constexpr int Y_BH_OFF = Y_STAGES * Y_STAGE;
+constexpr int Y_LDS_BYTES = Y_BH_OFF + NH * 4;
+constexpr int Y_A_INS = Y_BM / (8 * NW), Y_B_INS = CB / (8 * NW);
+constexpr int Y_DC_LOADS = Y_A_INS + Y_B_INS + 1;  // DMA pieces per wave per deconv step (+1: biases)
+constexpr int Y_HEAD_STEPS = CB / 64;              // head steps per branch
+constexpr int Y_HEAD_PIECES = 2 * (NH / 8);        // 1-KiB DMA pieces per head step
+static_assert(Y_LDS_BYTES <= 163840, "LDS budget");
+static_assert(2 * NH * X_ROWB <= Y_A_BYTES, "a head step's weights fit the A slot");
+static_assert(Y_DC_LOADS == 7 && NW == 8 && Y_HEAD_PIECES == 20, "vmcnt cases below");
 
-__device__ __forceinline__ int swz3(int row) { return (row ^ (row >> 3)) & 7; }
+template <int V> struct IC { static constexpr int value = V; };
+
+// 16-row periodic slot swizzle: conv_mfma.hip's swz3 on the row's position in
+// its 16-row fragment (conflict-free for the b128 fragment reads at any 16-row
+// base), so the fragment-read address is a per-lane base plus a constant per
+// fragment (folded into the ds_read offset instead of one VGPR per fragment)
+__device__ __forceinline__ int swz3(int row) { return ((row & 15) ^ ((row & 15) >> 3)) & 7; }
 
 __device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8& hi, bf16x8& lo) {
   const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -327,6 +347,19 @@ __device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+// all but this wave's n youngest vector-memory ops done (n = the DMA pieces of
+// the one step allowed to stay in flight; an unlisted n waits for everything)
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  if (n == Y_DC_LOADS) wait_vm<Y_DC_LOADS>();
+  else if (n == 3) wait_vm<3>();
+  else if (n == 2) wait_vm<2>();
+  else wait_vm<0>();
+}
+
 struct NeckArgsX3 {
   const float* x[MAXBR];
   int ldx[MAXBR], offx[MAXBR], cin[MAXBR], s[MAXBR];
@@ -343,118 +376,136 @@ struct NeckArgsX3 {
 // conv_mfma.hip pair_split8): the A fragments are read as stored, no split.
 template <bool PAIR>
 __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[X_LDS_BYTES];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[Y_LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int lrow = lane >> 3, lslot = lane & 7;
 
-  const int S = a.S;
+  const int S = a.S, ncls = S * S;
   const int Wq = a.W / S, nq = (a.H / S) * Wq;
-  const int nqt = (nq + X_BM - 1) / X_BM;
+  const int np = a.B * nq;  // pixels of one sub-pixel class over the batch
   const int G = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = G >> 3;
   const int t_lo = (int)((long)a.ntiles * xcd / 8), t_hi = (int)((long)a.ntiles * (xcd + 1) / 8);
   const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + nslot - 1) / nslot : 0;
   const int total = my_tiles * a.nsteps;
   const int ldwh = 2 * a.nbr * CB;  // bf16 per split head-weight row
 
-  if (wid == 0 && lane < NH / 4) glds16(a.bh + lane * 4, smem + X_BH_OFF);
+  if (wid == 0 && lane < NH / 4) glds16_asm(a.bh + lane * 4, smem + Y_BH_OFF);
 
-  // issue side: (tile, branch, chunk) with chunk < cin/32 a deconv step, else head step chunk - cin/32
-  int i_k = 0, i_br = 0, i_kc = 0;
-  Tile it = tile_of(a.S, t_lo + slot, nqt, X_BM);
-  // each lane's A source row for the current (tile, branch), computed once per
-  // branch (the q -> (Y, X) division is most of the loop's VALU otherwise);
-  // the K steps of the branch only add their channel offset
-  const float* a_src[X_A_INS];
-  auto row_sources = [&]() {
-    const int s = a.s[i_br], f = S / s;
-    const int Hi = a.H / s, Wi = a.W / s;
-    const int sy = it.cy / s, sx = it.cx / s;
-    const float* xb = a.x[i_br] + a.offx[i_br];
-    const int ldx = a.ldx[i_br];
+  // ---- issue side: (tile, branch, chunk); chunk < cin/32 a deconv step, else a head step
+  int i_k = 0, i_br = 0, i_kc = 0, i_cy = 0, i_cx = 0;
+  // this lane's A rows of the issue-side tile: (global q-row Yg = b * H/S + Y) << 16 | X, or -1.
+  // A branch of stride s reads input pixel (Yg * S/s + sy, X * S/s + sx) of its [B * H/s, W/s] map.
+  int r_yx[Y_A_INS];
+  auto tile_rows = [&](int t) {
+    const int cls = t % ncls, pt = t / ncls;
+    i_cy = cls / S;
+    i_cx = cls - i_cy * S;
 #pragma unroll
-    for (int j = 0; j < X_A_INS; ++j) {
-      const int row = (wid * X_A_INS + j) * 8 + lrow;
-      const int q = it.q0 + row;
-      a_src[j] = nullptr;
-      if (q < nq) {
-        const int Y = q / Wq, X = q - Y * Wq;
-        a_src[j] = xb + (((long)it.b * Hi + Y * f + sy) * Wi + X * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
+    for (int j = 0; j < Y_A_INS; ++j) {
+      const int p = pt * Y_BM + (wid * Y_A_INS + j) * 8 + lrow;
+      r_yx[j] = -1;
+      if (p < np) {
+        const int yg = p / Wq;
+        r_yx[j] = (yg << 16) | (p - yg * Wq);
       }
     }
   };
-  auto issue = [&](int buf) {
-    unsigned char* sa = smem + buf * X_STAGE;
-    unsigned char* sb = sa + X_A_BYTES;
-    unsigned char* sbias = sb + X_B_BYTES;
-    const int nkc = a.cin[i_br] / 32;
-    if (i_kc < nkc) {
-      const int s = a.s[i_br];
-      const int ci0 = i_kc * 32;
-      if (i_kc == 0) row_sources();
+  int a_off[Y_A_INS];  // per (tile, branch) element offsets of the lane's A rows (-1: zero page)
+  const float* a_base = nullptr;
+  auto row_sources = [&]() {  // once per (tile, branch): the K steps only add their channel offset
+    const int s = a.s[i_br], f = S / s;
+    const int Wi = a.W / s;
+    const int sy = i_cy / s, sx = i_cx / s;
+    a_base = a.x[i_br] + a.offx[i_br];
+    const int ldx = a.ldx[i_br];
 #pragma unroll
-      for (int j = 0; j < X_A_INS; ++j) {
-        const void* g = a_src[j] ? (const void*)(a_src[j] + ci0) : (const void*)g_neck_zero_page;
-        glds16(g, sa + (wid * X_A_INS + j) * 1024);
+    for (int j = 0; j < Y_A_INS; ++j) {
+      const int row = (wid * Y_A_INS + j) * 8 + lrow;
+      const int yg = r_yx[j] >> 16, x = r_yx[j] & 0xFFFF;
+      a_off[j] = r_yx[j] < 0 ? -1 : ((yg * f + sy) * Wi + x * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
+    }
+  };
+  auto issue = [&](int buf) -> int {
+    unsigned char* sa = smem + buf * Y_STAGE;
+    unsigned char* sb = sa + Y_A_BYTES;
+    unsigned char* sbias = sb + Y_B_BYTES;
+    const int nkc = a.cin[i_br] / 32;
+    int n = 0;
+    if (i_kc < nkc) {
+      if (i_kc == 0) row_sources();
+      const int ci0 = i_kc * 32;
+#pragma unroll
+      for (int j = 0; j < Y_A_INS; ++j) {
+        const void* g = a_off[j] >= 0 ? (const void*)(a_base + a_off[j] + ci0) : (const void*)g_neck_zero_page;
+        glds16_asm(g, sa + (wid * Y_A_INS + j) * 1024);
       }
-      const int sub = (it.cy % s) * s + (it.cx % s);
+      const int s = a.s[i_br];
+      const int sub = (i_cy % s) * s + (i_cx % s);
       const int cin2 = 2 * a.cin[i_br];
       const __hip_bfloat16* wb = a.w[i_br] + (long)sub * CB * cin2 + ci0 * 2;
 #pragma unroll
-      for (int j = 0; j < X_B_INS; ++j) {
-        const int row = (wid * X_B_INS + j) * 8 + lrow;
-        glds16(wb + (long)row * cin2 + (lslot ^ swz3(row)) * 8, sb + (wid * X_B_INS + j) * 1024);
+      for (int j = 0; j < Y_B_INS; ++j) {
+        const int row = (wid * Y_B_INS + j) * 8 + lrow;
+        glds16_asm(wb + (long)row * cin2 + (lslot ^ swz3(row)) * 8, sb + (wid * Y_B_INS + j) * 1024);
       }
-      if (lane < 4) glds16(a.bias[i_br] + sub * CB + wid * 16 + lane * 4, sbias + wid * 64);
+      if (lane < 4) glds16_asm(a.bias[i_br] + sub * CB + wid * 16 + lane * 4, sbias + wid * 64);
+      n = Y_DC_LOADS;
     } else {
-      // head step t: rows h < 80 of the split head weights, channels [br*CB + 32t, +32)
+      // head step t: rows h < 80 of the split head weights, channels [br*CB + 64t, +64)
+      // as two 32-channel blocks [80][128 B] in the A slot
       const int t = i_kc - nkc;
-      const __hip_bfloat16* whb = a.wh + (i_br * CB + 32 * t) * 2;
-      for (int r8 = wid; r8 < NH / 8; r8 += NW) {
-        const int h = r8 * 8 + lrow;
-        glds16(whb + (long)h * ldwh + (lslot ^ swz3(h)) * 8, sb + r8 * 1024);
+      const __hip_bfloat16* whb = a.wh + (i_br * CB + 64 * t) * 2;
+      for (int p = wid; p < Y_HEAD_PIECES; p += NW) {
+        const int c = p / (NH / 8), r8 = p - c * (NH / 8), h = r8 * 8 + lrow;
+        glds16_asm(whb + (long)h * ldwh + c * 64 + (lslot ^ swz3(h)) * 8, sa + c * NH * X_ROWB + r8 * 1024);
+        ++n;
       }
     }
-    if (++i_kc == nkc + 4) {
+    if (++i_kc == nkc + Y_HEAD_STEPS) {
       i_kc = 0;
       if (++i_br == a.nbr) {
         i_br = 0;
-        ++i_k;
-        it = tile_of(a.S, t_lo + slot + i_k * nslot, nqt, X_BM);
+        if (++i_k < my_tiles) tile_rows(t_lo + slot + i_k * nslot);
       }
     }
+    return n;
   };
 
-  f32x4 acc1[X_FM][8], acc2[X_FM][NH / 16];
+  f32x4 acc1[Y_FM][8], acc2[Y_FM][NH / 16];
 #pragma unroll
-  for (int i = 0; i < X_FM; ++i) {
+  for (int i = 0; i < Y_FM; ++i) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  if (total > 0) issue(0);
+  int nxt = 0;  // DMA pieces of the step after the current one (0: not issued)
+  if (total > 0) {
+    tile_rows(t_lo + slot);
+    issue(0);
+    if (total > 1) nxt = issue(1);
+  }
   int c_k = 0, c_br = 0, c_kc = 0;
-  Tile ct = tile_of(a.S, t_lo + slot, nqt, X_BM);
   for (int g = 0; g < total; ++g) {
-    const int cur = g & 1;
-    wait_vmcnt0();
+    const int cur = g % Y_STAGES;
+    wait_vm_rt(nxt);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();  // step g landed for every wave; every wave is done with step g-1's buffer
     asm volatile("" ::: "memory");
-    if (g + 1 < total) issue(cur ^ 1);
+    nxt = g + 2 < total ? issue((g + 2) % Y_STAGES) : 0;
 
-    const unsigned char* sa = smem + cur * X_STAGE;
-    const unsigned char* sb = sa + X_A_BYTES;
+    const unsigned char* sa = smem + cur * Y_STAGE;
+    const unsigned char* sb = sa + Y_A_BYTES;
     const int nkc = a.cin[c_br] / 32;
     if (c_kc < nkc) {
       // ---- deconv K step: 2 x 8 fragment pairs, three MFMAs each
-      bf16x8 ah[X_FM], al[X_FM];
+      bf16x8 ah[Y_FM], al[Y_FM];
 #pragma unroll
-      for (int i = 0; i < X_FM; ++i) {
-        const int r = wid * 16 * X_FM + i * 16 + fr;
+      for (int i = 0; i < Y_FM; ++i) {
+        const int r = wid * 16 * Y_FM + i * 16 + fr;
         if constexpr (PAIR) {
           ah[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
           al[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
@@ -465,8 +516,7 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
         }
       }
       __builtin_amdgcn_s_setprio(1);
-      // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the
-      // VGPRs) to half the tile; the scheduler may not move reads across the barrier
+      // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the VGPRs) to half the tile
 #pragma unroll
       for (int jh = 0; jh < 2; ++jh) {
         bf16x8 wh_[4], wl_[4];
@@ -479,17 +529,17 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-          for (int i = 0; i < X_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
+          for (int i = 0; i < Y_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_s_setprio(0);
       if (c_kc == nkc - 1) {  // branch GEMM done: bias + ReLU (this stage carries the biases)
-        const float* bias = reinterpret_cast<const float*>(sb + X_B_BYTES);
+        const float* bias = reinterpret_cast<const float*>(sb + Y_B_BYTES);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
 #pragma unroll
-          for (int i = 0; i < X_FM; ++i) {
+          for (int i = 0; i < Y_FM; ++i) {
             acc1[i][j][0] = fmaxf(acc1[i][j][0] + bv.x, 0.f);
             acc1[i][j][1] = fmaxf(acc1[i][j][1] + bv.y, 0.f);
             acc1[i][j][2] = fmaxf(acc1[i][j][2] + bv.z, 0.f);
@@ -500,53 +550,62 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
       ++c_kc;
       continue;
     }
-    // ---- head step t: 32 of the branch's channels (acc1[.][2t], acc1[.][2t+1]) x 80 head rows
-    const int t = c_kc - nkc;
-    bf16x8 xh[X_FM], xl[X_FM];
-    auto take = [&](int q) {
+    // ---- head step t: branch channels 64t..64t+63 (acc1[.][4t .. 4t+3]) x 80 head rows
+    auto head_chunk = [&](auto QC, const unsigned char* whb) {
+      constexpr int q = decltype(QC)::value;  // static register indices (a runtime index would spill acc1)
+      bf16x8 xh[Y_FM], xl[Y_FM];
 #pragma unroll
-      for (int i = 0; i < X_FM; ++i) {
+      for (int i = 0; i < Y_FM; ++i) {
         const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];
         split8(make_float4(p0[0], p0[1], p0[2], p0[3]), make_float4(p1[0], p1[1], p1[2], p1[3]), xh[i], xl[i]);
       }
+#pragma unroll
+      for (int u = 0; u < NH / 16; ++u) {
+        const int h = u * 16 + fr;
+        const bf16x8 wh_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq) ^ swz3(h)) << 4));
+        const bf16x8 wl_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq + 1) ^ swz3(h)) << 4));
+#pragma unroll
+        for (int i = 0; i < Y_FM; ++i) mfma3(acc2[i][u], wh_, wl_, xh[i], xl[i]);
+      }
     };
-    switch (t) {  // static register indices per case (a runtime index would put acc1 in scratch)
-      case 0: take(0); break;
-      case 1: take(1); break;
-      case 2: take(2); break;
-      default: take(3); break;
-    }
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int u = 0; u < NH / 16; ++u) {
-      const int h = u * 16 + fr;
-      const bf16x8 wh_ = *reinterpret_cast<const bf16x8*>(sb + h * X_ROWB + (((2 * fq) ^ swz3(h)) << 4));
-      const bf16x8 wl_ = *reinterpret_cast<const bf16x8*>(sb + h * X_ROWB + (((2 * fq + 1) ^ swz3(h)) << 4));
-#pragma unroll
-      for (int i = 0; i < X_FM; ++i) mfma3(acc2[i][u], wh_, wl_, xh[i], xl[i]);
+    if (c_kc == nkc) {
+      head_chunk(IC<0>{}, sa);
+      __builtin_amdgcn_sched_barrier(0);
+      head_chunk(IC<1>{}, sa + NH * X_ROWB);
+    } else {
+      head_chunk(IC<2>{}, sa);
+      __builtin_amdgcn_sched_barrier(0);
+      head_chunk(IC<3>{}, sa + NH * X_ROWB);
     }
     __builtin_amdgcn_s_setprio(0);
-    if (++c_kc != nkc + 4) continue;
+    if (++c_kc != nkc + Y_HEAD_STEPS) continue;
     c_kc = 0;
 #pragma unroll
-    for (int i = 0; i < X_FM; ++i)
+    for (int i = 0; i < Y_FM; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (++c_br != a.nbr) continue;
     c_br = 0;
-    {
-      const float* bh = reinterpret_cast<const float*>(smem + X_BH_OFF);
+    {  // ---- tile done: head bias, fp32 store (lane: pixel fr, head rows 16u + 4fq .. +3)
+      const int ct = t_lo + slot + c_k * nslot;
+      const int cls = ct % ncls, pt = ct / ncls, cy = cls / S, cx = cls - cy * S;
+      // lane's head-bias LDS offset, formed here (the opaque copy keeps hipcc from
+      // hoisting the five per-u addresses out of the step loop, where they spill)
+      int bofs = Y_BH_OFF + fq * 16;
+      asm volatile("" : "+v"(bofs));
+      const unsigned char* bh = smem + bofs;
 #pragma unroll
-      for (int i = 0; i < X_FM; ++i) {
-        const int q = ct.q0 + wid * 16 * X_FM + i * 16 + fr;
-        if (q < nq) {
-          const int Y = q / Wq, X = q - Y * Wq;
-          float* op = a.out + (((long)ct.b * a.H + Y * S + ct.cy) * a.W + X * S + ct.cx) * a.ldo;
+      for (int i = 0; i < Y_FM; ++i) {
+        const int p = pt * Y_BM + wid * 16 * Y_FM + i * 16 + fr;
+        if (p < np) {
+          const int b = p / nq, q = p - b * nq, Y = q / Wq, X = q - Y * Wq;
+          float* op = a.out + (((long)b * a.H + Y * S + cy) * a.W + X * S + cx) * a.ldo;
 #pragma unroll
           for (int u = 0; u < NH / 16; ++u) {
             const int h = u * 16 + fq * 4;
             if (h < a.nh) {
-              const float4 bv = *reinterpret_cast<const float4*>(bh + h);
+              const float4 bv = *reinterpret_cast<const float4*>(bh + u * 64);
               *reinterpret_cast<float4*>(op + h) = make_float4(acc2[i][u][0] + bv.x, acc2[i][u][1] + bv.y,
                                                                acc2[i][u][2] + bv.z, acc2[i][u][3] + bv.w);
             }
@@ -557,9 +616,8 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
       }
     }
     ++c_k;
-    ct = tile_of(a.S, t_lo + slot + c_k * nslot, nqt, X_BM);
   }
-  wait_vmcnt0();
+  wait_vm<0>();  // no LDS DMA may outlive the workgroup (a tile-less workgroup still loaded the head bias)
 }
 
 }  // namespace
@@ -619,16 +677,20 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
     if (S % s[i]) return (int)hipErrorInvalidValue;
     a.x[i] = (const float*)x[i]; a.ldx[i] = ldx[i]; a.offx[i] = offx[i]; a.cin[i] = cin[i]; a.s[i] = s[i];
     a.w[i] = (const __hip_bfloat16*)w[i]; a.bias[i] = bias[i];
-    nsteps += cin[i] / 32 + 4;
+    nsteps += cin[i] / 32 + Y_HEAD_STEPS;
   }
   for (int i = nbr; i < MAXBR; ++i) {
     a.x[i] = nullptr; a.ldx[i] = a.offx[i] = a.cin[i] = 0; a.s[i] = 1; a.w[i] = nullptr; a.bias[i] = nullptr;
   }
   if ((H % S) || (W % S)) return (int)hipErrorInvalidValue;
+  // the kernel packs q-grid rows as (Yg << 16 | X) and addresses branch inputs with 32-bit element offsets
+  if ((long)B * (H / S) >= 32768 || W / S >= 65536) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < nbr; ++i)
+    if ((long)B * (H / s[i]) * (W / s[i]) * ldx[i] >= (1L << 31)) return (int)hipErrorInvalidValue;
   a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.out = (float*)out; a.ldo = ldo; a.nh = nh;
   a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
   const int nq = (H / S) * (W / S);
-  a.ntiles = B * ((nq + X_BM - 1) / X_BM) * S * S;
+  a.ntiles = ((B * nq + Y_BM - 1) / Y_BM) * S * S;
   if (pair) {
     for (int i = 0; i < nbr; ++i)
       if ((ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;

@@ -5,7 +5,7 @@ import logging
 from . import KServeServer, ModelRepository
 
 
-def main(argv=None):
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="KServe-v2 (Triton protocol) server on MI355X")
     ap.add_argument("--models", default="YOLOv5nCOCO,pointpillar_kitti")
     ap.add_argument("--model-repository", default=None, help="Triton-style directory of config.pbtxt files")
@@ -20,7 +20,11 @@ def main(argv=None):
                     help="with --export-repository: weights for MODEL (path, file/http(s)/s3 URI); repeatable")
     ap.add_argument("--weights-sha256", action="append", default=[], metavar="MODEL=HEX",
                     help="with --export-repository: expected sha256 of MODEL's weights (written into config.pbtxt)")
-    args = ap.parse_args(argv)
+    return ap
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     if args.export_repository:
         from .repository import export_repository
