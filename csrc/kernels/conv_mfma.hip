@@ -1296,6 +1296,172 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
   epilogue_f32<BM, BN, WM, WN, PAIR_OUT>(a, acc, smem, m0, n0);
 }
 
+// ---- x3 pair, buffer-resource LDS DMA ("xb"): the pair-input glds kernel with
+// the K loop's VALU taken out (PMC of the glds form: 3.3 VALU per MFMA, the SIMD's
+// vector-issue port oversubscribed at 4 waves per SIMD):
+//  * operands go global -> LDS by `buffer_load_dwordx4 ... offen lds` through a
+//    buffer descriptor per tensor: each lane's 32-bit row offset is formed once
+//    per tap (A) or once per tile (B), the K step's advance is the scalar soffset,
+//    and a padding tap or a row past M / N reads zeros by the descriptor's range
+//    check (offset 0x80000000 >= num_records) instead of a select per load;
+//  * the slot swizzle is 16-row periodic (swz3 of the row within its fragment;
+//    conflict-free for the b128 fragment reads at any 16-row base), so fragment
+//    i / j of a wave is a constant offset from one per-lane base per operand half
+//    and the reads fold it into the ds_read immediate.
+// Same K order, fragments and MFMA sequence as conv_glds_x3_kernel<..., true, .>:
+// outputs are bit-identical to it.
+__device__ __forceinline__ int swzp(int row) { return swz3(row & 15); }
+
+__device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, const void* l, unsigned soff) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+               : "memory");
+}
+
+constexpr unsigned kOutOfRange = 0x80000000u;  // >= any num_records the launcher accepts (< 2^31)
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT>
+__global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
+  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+  constexpr int NW = WM * WN;
+  constexpr int BKC = 32, ROWB = 128;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split over the waves' 8-row DMAs");
+  constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);
+  constexpr int NL = A_INS + B_INS;
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int LDS = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nmt = (a.M + BM - 1) / BM, nnt = (a.N + BN - 1) / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.N * a.Kp * 4, 0x00020000);
+
+  const int lrow = lane >> 3, lslot = lane & 7;
+  int a_base[A_INS], a_iy0[A_INS], a_ix0[A_INS];  // element offset of the row's tap-(0,0) pixel + slot
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wid * A_INS + j) * 8 + lrow;
+    const int m = m0 + row;
+    if (m < a.M) {
+      const int ox = m % a.Wo, t = m / a.Wo, oy = t % a.Ho, b = t / a.Ho;
+      a_iy0[j] = oy * a.S - a.P;
+      a_ix0[j] = ox * a.S - a.P;
+      a_base[j] = ((b * a.H + a_iy0[j]) * a.W + a_ix0[j]) * a.ldi + a.ci_off + (lslot ^ swzp(row)) * 4;
+    } else {
+      a_iy0[j] = -(1 << 28);
+      a_ix0[j] = 0;
+      a_base[j] = 0;
+    }
+  }
+  unsigned b_off[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wid * B_INS + j) * 8 + lrow;
+    const int n = n0 + row;
+    b_off[j] = n < a.N ? (unsigned)(n * 2 * a.Kp + (lslot ^ swzp(row)) * 8) * 2u : kOutOfRange;
+  }
+  unsigned a_off[A_INS];
+  auto tap_offsets = [&](int ky, int kx) {
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      a_off[j] = ok ? (unsigned)(a_base[j] + (ky * a.W + kx) * a.ldi) * 4u : kOutOfRange;
+    }
+  };
+
+  unsigned char* const sbase = smem + __builtin_amdgcn_readfirstlane(wid) * (A_INS * 1024);
+  auto issue = [&](int kt, int buf, int ci0) {
+    unsigned char* sa = sbase + buf * STAGE;
+    unsigned char* sb = smem + buf * STAGE + A_BYTES + __builtin_amdgcn_readfirstlane(wid) * (B_INS * 1024);
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) bdma16(a_off[j], rin, sa + j * 1024, (unsigned)ci0 * 4u);
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) bdma16(b_off[j], rw, sb + j * 1024, (unsigned)kt * (BKC * 4));
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kp / BKC;
+  int ky = 0, kx = 0, ci0 = 0;
+  tap_offsets(0, 0);
+  auto advance = [&]() {
+    ci0 += BKC;
+    if (ci0 == a.Cin) {
+      ci0 = 0;
+      if (++kx == a.KW) { kx = 0; ++ky; }
+      if (ky < a.KH) tap_offsets(ky, kx);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nk) {
+      issue(st, st, ci0);
+      advance();
+    }
+  const int fr = lane & 15, fq = lane >> 4;
+  // per-lane fragment bases (fragment i / j: + i * 16 rows, a constant)
+  const int sw = swzp(fr);
+  const int a_hi = (wm * TM + fr) * ROWB + (((2 * fq) ^ sw) << 4), a_lo = (wm * TM + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
+  const int b_hi = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq) ^ sw) << 4);
+  const int b_lo = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % STAGES;
+    const int after = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    wait_vmcnt_upto<NL>(after);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int nx = kt + STAGES - 1;
+    if (nx < nk) {
+      issue(nx, nx % STAGES, ci0);
+      advance();
+    }
+    const unsigned char* st = smem + cur * STAGE;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(st + b_hi + j * 16 * ROWB);
+      bl[j] = *reinterpret_cast<const bf16x8*>(st + b_lo + j * 16 * ROWB);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
+      al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the staging LDS
+  asm volatile("" ::: "memory");
+  epilogue_f32<BM, BN, WM, WN, PAIR_OUT>(a, acc, smem, m0, n0);
+}
+
 // ---- x3 small halo: 3x3, pad 1, stride 1/2, Cin and N in {16, 32}.  The fp32
 // halo is split once while staging (register path: every halo pixel is read by
 // 9 taps, so splitting at the fragment read would cost 9x the VALU); hi and lo
@@ -1443,9 +1609,30 @@ int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT>
+int launch_xb(const ConvArgs& a, hipStream_t stream) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  conv_xb_kernel<BM, BN, WM, WN, STAGES, PAIR_OUT><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// the xb kernels address through 32-bit buffer offsets: tensors below 2 GiB
+bool xb_ok(const ConvArgs& a) {
+  return (long)a.B * a.H * a.W * a.ldi * 4 < (1L << 31) && (long)a.N * a.Kp * 4 < (1L << 31);
+}
+
 template <bool PAIR_OUT>
 int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
+  if (tile >= 70 && !xb_ok(a)) return (int)hipErrorInvalidValue;
   switch (tile) {
+    case 70: return launch_xb<128, 128, 2, 4, 2, PAIR_OUT>(a, stream);
+    case 71: return launch_xb<256, 64, 4, 2, 2, PAIR_OUT>(a, stream);
+    case 72: return launch_xb<128, 64, 4, 2, 3, PAIR_OUT>(a, stream);
+    case 73: return launch_xb<128, 128, 4, 2, 2, PAIR_OUT>(a, stream);
+    case 74: return launch_xb<128, 128, 2, 4, 3, PAIR_OUT>(a, stream);
+    case 75: return launch_xb<256, 64, 4, 2, 3, PAIR_OUT>(a, stream);
+    case 76: return launch_xb<256, 128, 4, 2, 2, PAIR_OUT>(a, stream);
+    case 77: return launch_xb<128, 64, 4, 2, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 22: return launch_glds_x3<128, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
@@ -1613,7 +1800,7 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
 // fp32 mode, pair activations: `in` (and `res`) hold pairs (see pair_split8),
 // `out` pairs when out_pair, else fp32.  Same slice / residual / pixel-shuffle
 // contract as tca_conv_nhwc_x3; the global_load_lds kernels only (Cin % 32 == 0,
-// Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42.
+// Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42 (glds) or 70-77 (xb).
 TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
                               const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
                               int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
@@ -1635,6 +1822,9 @@ TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int
   // profiles/r2/conv_x3p_tiles.jsonl): N <= 64: 256x64 (4x2 waves), 3-stage 128x64 for
   // stride 2; wider: 128x128 2x4
   // (4-wave 64x64-per-wave tiles measured slower on every layer)
+  // xb (buffer-descriptor DMA) twins, same bits, 8-10% faster on every PointPillars layer
+  // (profiles/r2/xb_tiles.jsonl): 256x64 / 128x64 for N <= 64 (stride 1 / 2), 128x128 2x4 / 4x2
+  if (tile == 0 && xb_ok(a)) tile = N <= 64 ? (S == 1 ? 71 : 77) : (S == 1 ? 70 : 73);
   if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
 }

@@ -29,7 +29,7 @@ def test_pairs_roundtrip_cpu():
     assert ((from_pairs(p) - x).abs() <= x.abs() * 2 ** -16).all()
 
 
-@pytest.mark.parametrize("tile", [0, 20, 22, 24, 25, 41])
+@pytest.mark.parametrize("tile", [0, 20, 22, 24, 25, 41, 70, 71, 72])
 @pytest.mark.parametrize("out_pair", [True, False])
 def test_conv_pair_vs_fp64(cuda, tile, out_pair):
     torch.manual_seed(tile)
@@ -45,6 +45,33 @@ def test_conv_pair_vs_fp64(cuda, tile, out_pair):
     got = NHWC(out, 8, cout, pair=out_pair).nchw()
     assert rel_l2(got, ref) < 5e-5
     assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
+
+
+XB_TWINS = [(70, 25), (71, 26), (72, 32), (73, 20), (74, 25), (75, 26), (76, 37), (77, 22)]
+
+
+@pytest.mark.parametrize("xb,glds", XB_TWINS)
+@pytest.mark.parametrize("shape", [(2, 23, 31, 64, 128, 3, 1, 1), (3, 17, 12, 32, 64, 3, 2, 1),
+                                   (2, 9, 14, 128, 72, 1, 1, 0), (1, 40, 33, 96, 256, 3, 1, 1)])
+def test_conv_pair_xb_bit_identical_to_glds(cuda, xb, glds, shape):
+    """The buffer-descriptor kernels (zero fill by range check, periodic swizzle)
+    run the glds kernels' K order and MFMA sequence: identical bits, including
+    padding taps, partial M / N tiles, stride 2, 1x1 and a residual."""
+    torch.manual_seed(xb)
+    B, H, W, cin, cout, k, s, pad = shape
+    conv = nn.Conv2d(cin, cout, k, s, pad, bias=True)
+    fc = FusedConv(conv, act=1, device=cuda, precision="fp32", post_res=True)
+    x = NHWC(to_pairs(torch.randn(B, H, W, cin + 8)).to(cuda), 8, cin, pair=True)
+    Ho, Wo = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+    r = NHWC(to_pairs(torch.randn(B, Ho, Wo, cout)).to(cuda), pair=True)
+    outs = []
+    for t in (xb, glds):
+        o = NHWC(torch.full((B, Ho, Wo, cout + 8), 7.0, device=cuda), 0, cout, pair=True)
+        fc(x, out=o, res=r, tile=t)
+        outs.append(o.t.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0][..., cout:] == 7.0).all()
 
 
 def test_conv_pair_residual_and_deconv_shuffle(cuda):

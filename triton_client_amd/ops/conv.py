@@ -92,8 +92,9 @@ def _ceil(x, m):
 
 
 PRECISIONS = ("fp32", "bf16")
-# global_load_lds split-product tiles with pair-storage instantiations (conv_mfma.hip launch_glds_x3p)
-PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42)
+# split-product tiles with pair-storage instantiations (conv_mfma.hip launch_glds_x3p: global_load_lds
+# kernels 20-42, buffer-descriptor DMA kernels 70-77)
+PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 70, 71, 72, 73, 74, 75, 76, 77)
 
 
 def act_dtype(precision: str) -> torch.dtype:
