@@ -1308,8 +1308,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_glds_x3_kernel(ConvArgs a) 
 //    conflict-free for the b128 fragment reads at any 16-row base), so fragment
 //    i / j of a wave is a constant offset from one per-lane base per operand half
 //    and the reads fold it into the ds_read immediate.
-// Same K order, fragments and MFMA sequence as conv_glds_x3_kernel<..., true, .>:
-// outputs are bit-identical to it.
+// Same K order, fragments and MFMA sequence as conv_glds_x3_kernel<..., PAIR_IN, .>:
+// outputs are bit-identical to it (PAIR_IN = false: fp32 input split at the fragment
+// read, the camera chain's form).
 __device__ __forceinline__ int swzp(int row) { return swz3(row & 15); }
 
 __device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, const void* l, unsigned soff) {
@@ -1323,7 +1324,7 @@ __device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsr
 
 constexpr unsigned kOutOfRange = 0x80000000u;  // >= any num_records the launcher accepts (< 2^31)
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT, bool PAIR_IN = true>
 __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
   static_assert(STAGES >= 2 && STAGES <= 4, "stages");
   constexpr int NW = WM * WN;
@@ -1446,8 +1447,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
-      al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
+      if constexpr (PAIR_IN) {  // slots hold hi / lo of 8 channels as stored
+        ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
+        al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
+      } else {  // slots hold fp32 channels 8fq..8fq+3 / +4..+7: split here
+        const float4 x0 = *reinterpret_cast<const float4*>(st + a_hi + i * 16 * ROWB);
+        const float4 x1 = *reinterpret_cast<const float4*>(st + a_lo + i * 16 * ROWB);
+        split8(x0, x1, ah[i], al[i]);
+      }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1609,10 +1616,10 @@ int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT, bool PAIR_IN = true>
 int launch_xb(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  conv_xb_kernel<BM, BN, WM, WN, STAGES, PAIR_OUT><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_xb_kernel<BM, BN, WM, WN, STAGES, PAIR_OUT, PAIR_IN><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -1759,10 +1766,23 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
   // small halo only at stride 1 (stride 2: v1 128x32 is 1.9x faster); N <= 32: v1 (a 1x1 64->32 runs 26 us
   // vs 38 on glds); glds 128x64 with one wave column for N <= 64, 128x128 4x2 above
   if (tile == 0 && small_halo_x3_ok(a) && a.S == 1) tile = 60;
+  // glds-class layers go to the xb twins (same bits; profiles/r2/xbf_tiles.jsonl at batch 32: 128x64 8x1 for
+  // N <= 64 and for small M (YOLOv5n b7 39 vs 54 us on the old glds 128x128), 128x128 4x2 above)
+  if (tile == 0 && N > 32 && v2ok && xb_ok(a)) tile = (N <= 64 || a.M < 40000) ? 81 : 80;
   if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 41 : 20) : (N <= 64 ? 2 : 5);
-  if (tile >= 10 && tile < 60 && !v2ok) return (int)hipErrorInvalidValue;
+  if (((tile >= 10 && tile < 60) || tile >= 70) && !v2ok) return (int)hipErrorInvalidValue;
+  if (tile >= 80 && !xb_ok(a)) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 60: return launch_small_halo_x3(a, stream);
+    // xb twins (buffer-descriptor DMA, split at the fragment read; same bits as the glds tile named)
+    case 80: return launch_xb<128, 128, 4, 2, 2, false, false>(a, stream);  // 20
+    case 81: return launch_xb<128, 64, 8, 1, 2, false, false>(a, stream);   // 41
+    case 82: return launch_xb<128, 128, 2, 4, 2, false, false>(a, stream);  // 25
+    case 83: return launch_xb<256, 64, 4, 2, 2, false, false>(a, stream);   // 26
+    case 84: return launch_xb<128, 64, 4, 2, 2, false, false>(a, stream);   // 22
+    case 85: return launch_xb<64, 128, 2, 4, 2, false, false>(a, stream);   // 24
+    case 86: return launch_xb<256, 64, 8, 1, 2, false, false>(a, stream);   // 42
+    case 87: return launch_xb<64, 64, 4, 1, 2, false, false>(a, stream);    // 47
     case 20: return launch_glds_x3<128, 128, 4, 2>(a, stream);
     case 22: return launch_glds_x3<128, 64, 4, 2>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4>(a, stream);

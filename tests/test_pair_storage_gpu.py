@@ -74,6 +74,32 @@ def test_conv_pair_xb_bit_identical_to_glds(cuda, xb, glds, shape):
     assert (outs[0][..., cout:] == 7.0).all()
 
 
+XB_F32_TWINS = [(80, 20), (81, 41), (82, 25), (83, 26), (84, 22), (85, 24), (86, 42), (87, 47)]
+
+
+@pytest.mark.parametrize("xb,glds", XB_F32_TWINS)
+@pytest.mark.parametrize("shape", [(2, 23, 31, 64, 128, 3, 1, 1), (3, 17, 12, 32, 64, 3, 2, 1),
+                                   (2, 9, 14, 128, 72, 1, 1, 0)])
+def test_conv_fp32_xb_bit_identical_to_glds(cuda, xb, glds, shape):
+    """fp32-input xb kernels (split at the fragment read, the camera chain's form)
+    == their glds twins, bit for bit, fp32 and SiLU with a pre-activation residual."""
+    torch.manual_seed(xb)
+    B, H, W, cin, cout, k, s, pad = shape
+    conv = nn.Conv2d(cin, cout, k, s, pad, bias=True)
+    fc = FusedConv(conv, act=2, device=cuda, precision="fp32")
+    x = NHWC(torch.randn(B, H, W, cin + 8, device=cuda), 8, cin)
+    Ho, Wo = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+    r = NHWC(torch.randn(B, Ho, Wo, cout, device=cuda))
+    outs = []
+    for t in (xb, glds):
+        o = NHWC(torch.full((B, Ho, Wo, cout + 8), 7.0, device=cuda), 8, cout)
+        fc(x, out=o, res=r, tile=t)
+        outs.append(o.t.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0][..., :8] == 7.0).all()
+
+
 def test_conv_pair_residual_and_deconv_shuffle(cuda):
     torch.manual_seed(1)
     B, H, W = 2, 12, 10
