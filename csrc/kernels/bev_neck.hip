@@ -306,21 +306,30 @@ __global__ void __launch_bounds__(NT) bev_neck_head_kernel(NeckArgs a) {
 // a frame edge; each head step carries 64 of the branch's channels (two 32-channel
 // chunks of split head weights in the stage's A slot).
 constexpr int X_ROWB = 128;                       // 32 fp32 channels / 4 x {hi 8, lo 8}
-constexpr int Y_BM = 256;                         // pixels per tile
-constexpr int Y_FM = Y_BM / (16 * NW);            // 16-pixel fragments per wave (2)
-constexpr int Y_STAGES = 3;
-constexpr int Y_A_BYTES = Y_BM * X_ROWB;          // 32 KiB (head steps: 2 x [80 rows][128 B])
-constexpr int Y_B_BYTES = CB * X_ROWB;            // 16 KiB
-constexpr int Y_STAGE = Y_A_BYTES + Y_B_BYTES + BIAS_BYTES;
-constexpr int Y_BH_OFF = Y_STAGES * Y_STAGE;
-constexpr int Y_LDS_BYTES = Y_BH_OFF + NH * 4;
-constexpr int Y_A_INS = Y_BM / (8 * NW), Y_B_INS = CB / (8 * NW);
-constexpr int Y_DC_LOADS = Y_A_INS + Y_B_INS + 1;  // DMA pieces per wave per deconv step (+1: biases)
-constexpr int Y_HEAD_STEPS = CB / 64;              // head steps per branch
-constexpr int Y_HEAD_PIECES = 2 * (NH / 8);        // 1-KiB DMA pieces per head step
-static_assert(Y_LDS_BYTES <= 163840, "LDS budget");
-static_assert(2 * NH * X_ROWB <= Y_A_BYTES, "a head step's weights fit the A slot");
-static_assert(Y_DC_LOADS == 7 && NW == 8 && Y_HEAD_PIECES == 20, "vmcnt cases below");
+// Tiling traits: NWV waves per workgroup (32 pixels each), STAGES-deep ring.
+// <8, 3>: one 512-thread workgroup per CU; <4, 2>: two independent 256-thread
+// workgroups per CU (66.5 KiB each), whose barriers do not line up, so one
+// workgroup's MFMAs fill the other's barrier / LDS-latency bubbles.
+template <int NWV, int STAGES>
+struct NeckX3 {
+  static constexpr int NWAVES = NWV, NTH = NWV * 64;
+  static constexpr int BM = 32 * NWV;                      // pixels per tile
+  static constexpr int FM = 2;                             // 16-pixel fragments per wave
+  static constexpr int A_BYTES = BM * X_ROWB;              // head steps: 2 x [80 rows][128 B]
+  static constexpr int B_BYTES = CB * X_ROWB;              // 16 KiB
+  static constexpr int STAGE = A_BYTES + B_BYTES + BIAS_BYTES;
+  static constexpr int BH_OFF = STAGES * STAGE;
+  static constexpr int LDS_BYTES = BH_OFF + NH * 4;
+  static constexpr int A_INS = BM / (8 * NWV), B_INS = CB / (8 * NWV);
+  static constexpr int BIAS_LANES = CB / 4 / NWV;          // 16-B bias pieces per wave
+  static constexpr int DC_LOADS = A_INS + B_INS + 1;       // DMA instructions per wave per deconv step
+  static constexpr int HEAD_PIECES = 2 * (NH / 8);         // 1-KiB DMA pieces per head step
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static_assert(2 * NH * X_ROWB <= A_BYTES + B_BYTES, "a head step's weights fit the stage's A + B slots");
+  static_assert(STAGES == 2 || STAGES == 3, "ring depth");
+  __device__ static int head_loads(int wid) { return (HEAD_PIECES - wid + NWV - 1) / NWV; }
+};
+constexpr int Y_HEAD_STEPS = CB / 64;  // head steps per branch (64 channels each)
 
 template <int V> struct IC { static constexpr int value = V; };
 
@@ -353,10 +362,12 @@ __device__ __forceinline__ void wait_vm() {
 }
 // all but this wave's n youngest vector-memory ops done (n = the DMA pieces of
 // the one step allowed to stay in flight; an unlisted n waits for everything)
+template <typename T>
 __device__ __forceinline__ void wait_vm_rt(int n) {
-  if (n == Y_DC_LOADS) wait_vm<Y_DC_LOADS>();
-  else if (n == 3) wait_vm<3>();
-  else if (n == 2) wait_vm<2>();
+  constexpr int H_HI = (T::HEAD_PIECES + T::NWAVES - 1) / T::NWAVES, H_LO = T::HEAD_PIECES / T::NWAVES;
+  if (n == T::DC_LOADS) wait_vm<T::DC_LOADS>();
+  else if (n == H_HI) wait_vm<H_HI>();
+  else if (n == H_LO) wait_vm<H_LO>();
   else wait_vm<0>();
 }
 
@@ -374,9 +385,13 @@ struct NeckArgsX3 {
 
 // PAIR: branch inputs in pair storage ({hi 8 | lo 8} per 8 channels, see
 // conv_mfma.hip pair_split8): the A fragments are read as stored, no split.
-template <bool PAIR>
-__global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[Y_LDS_BYTES];
+template <bool PAIR, int NWV, int STAGES>
+__global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a) {
+  using T = NeckX3<NWV, STAGES>;
+  constexpr int Y_BM = T::BM, Y_FM = T::FM, Y_STAGES = STAGES, Y_STAGE = T::STAGE, Y_A_BYTES = T::A_BYTES;
+  constexpr int Y_B_BYTES = T::B_BYTES, Y_BH_OFF = T::BH_OFF, Y_A_INS = T::A_INS, Y_B_INS = T::B_INS;
+  constexpr int Y_DC_LOADS = T::DC_LOADS, Y_HEAD_PIECES = T::HEAD_PIECES, NW = NWV;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[T::LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -450,7 +465,8 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
         const int row = (wid * Y_B_INS + j) * 8 + lrow;
         glds16_asm(wb + (long)row * cin2 + (lslot ^ swz3(row)) * 8, sb + (wid * Y_B_INS + j) * 1024);
       }
-      if (lane < 4) glds16_asm(a.bias[i_br] + sub * CB + wid * 16 + lane * 4, sbias + wid * 64);
+      if (lane < T::BIAS_LANES)
+        glds16_asm(a.bias[i_br] + sub * CB + wid * (4 * T::BIAS_LANES) + lane * 4, sbias + wid * (16 * T::BIAS_LANES));
       n = Y_DC_LOADS;
     } else {
       // head step t: rows h < 80 of the split head weights, channels [br*CB + 64t, +64)
@@ -482,20 +498,26 @@ __global__ void __launch_bounds__(NT) bev_neck_head_x3_kernel(NeckArgsX3 a) {
     for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  int nxt = 0;  // DMA pieces of the step after the current one (0: not issued)
+  int nxt = 0;  // 3 stages: DMA pieces of the step after the current one (0: not issued)
   if (total > 0) {
     tile_rows(t_lo + slot);
     issue(0);
-    if (total > 1) nxt = issue(1);
+    if (Y_STAGES == 3 && total > 1) nxt = issue(1);
   }
   int c_k = 0, c_br = 0, c_kc = 0;
   for (int g = 0; g < total; ++g) {
     const int cur = g % Y_STAGES;
-    wait_vm_rt(nxt);
+    if constexpr (Y_STAGES == 3) wait_vm_rt<T>(nxt);
+    else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // step g landed for every wave; every wave is done with step g-1's buffer
     asm volatile("" ::: "memory");
-    nxt = g + 2 < total ? issue((g + 2) % Y_STAGES) : 0;
+    if (g + Y_STAGES - 1 < total) {
+      const int n = issue((g + Y_STAGES - 1) % Y_STAGES);
+      if constexpr (Y_STAGES == 3) nxt = n;
+    } else {
+      nxt = 0;
+    }
 
     const unsigned char* sa = smem + cur * Y_STAGE;
     const unsigned char* sb = sa + Y_A_BYTES;
@@ -661,12 +683,27 @@ TCA_API int tca_bev_neck_head(int nbr, const void* const* x, const int* ldx, con
 // fp32 mode: x[i] fp32, w[i] split [s_i*s_i*128, 2*cin[i]] bf16, wh split [80, 2*nbr*128]
 // (32-chunk permuted, then split), out fp32 [B, H, W, ldo].  Other arguments as tca_bev_neck_head.
 namespace {
+// variant 1: <8 waves, 3 stages> one workgroup per CU; 2: <4 waves, 2 stages> two per CU; 3: <8, 2>
+// auto: <8, 2> (tools/bench_neck.py at batch 32 on MI355X: 1157 us vs 1348 for <8, 3> and 2000 for <4, 2>;
+// profiles/r2/neck_variants.json)
+constexpr int kNeckX3Auto = 3;
+
+template <int NWV, int STAGES>
+void launch_neck_x3(NeckArgsX3& a, long np, int grid, bool pair, hipStream_t stream) {
+  using T = NeckX3<NWV, STAGES>;
+  a.ntiles = (int)((np + T::BM - 1) / T::BM) * a.S * a.S;
+  if (pair) bev_neck_head_x3_kernel<true, NWV, STAGES><<<grid, T::NTH, 0, stream>>>(a);
+  else bev_neck_head_x3_kernel<false, NWV, STAGES><<<grid, T::NTH, 0, stream>>>(a);
+}
+
 int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin, const int* s,
             const void* const* w, const float* const* bias, const void* wh, const float* bh, int nh, void* out,
-            int ldo, int B, int H, int W, int grid, bool pair, hipStream_t stream) {
+            int ldo, int B, int H, int W, int grid, bool pair, int variant, hipStream_t stream) {
   if (B <= 0) return 0;
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
+  if (variant == 0) variant = kNeckX3Auto;
+  if (variant < 1 || variant > 3) return (int)hipErrorInvalidValue;
   NeckArgsX3 a;
   int S = 1, nsteps = 0;
   for (int i = 0; i < nbr; ++i) {
@@ -690,13 +727,14 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.out = (float*)out; a.ldo = ldo; a.nh = nh;
   a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
   const int nq = (H / S) * (W / S);
-  a.ntiles = ((B * nq + Y_BM - 1) / Y_BM) * S * S;
-  if (pair) {
+  if (pair)
     for (int i = 0; i < nbr; ++i)
       if ((ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;
-    bev_neck_head_x3_kernel<true><<<grid, NT, 0, stream>>>(a);
-  } else {
-    bev_neck_head_x3_kernel<false><<<grid, NT, 0, stream>>>(a);
+  // grid: workgroup slots of the persistent kernel for one per CU; variant 2 runs two per CU
+  switch (variant) {
+    case 1: launch_neck_x3<8, 3>(a, B * nq, grid, pair, stream); break;
+    case 2: launch_neck_x3<4, 2>(a, B * nq, 2 * grid, pair, stream); break;
+    default: launch_neck_x3<8, 2>(a, B * nq, grid, pair, stream); break;
   }
   TCA_LAUNCH_CHECK();
 }
@@ -706,7 +744,7 @@ TCA_API int tca_bev_neck_head_x3(int nbr, const void* const* x, const int* ldx, 
                                  const int* s, const void* const* w, const float* const* bias, const void* wh,
                                  const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
                                  hipStream_t stream) {
-  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, false, stream);
+  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, false, 0, stream);
 }
 
 // Same, branch inputs x[i] in pair storage.
@@ -714,5 +752,15 @@ TCA_API int tca_bev_neck_head_x3p(int nbr, const void* const* x, const int* ldx,
                                   const int* s, const void* const* w, const float* const* bias, const void* wh,
                                   const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
                                   hipStream_t stream) {
-  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, true, stream);
+  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, true, 0, stream);
+}
+
+// Same with an explicit tiling variant (0 auto, 1 <8 waves, 3 stages>, 2 <4 waves, 2 stages, two
+// workgroups per CU>, 3 <8 waves, 2 stages>) and input storage (pair != 0: pair storage).
+TCA_API int tca_bev_neck_head_x3v(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
+                                  const int* s, const void* const* w, const float* const* bias, const void* wh,
+                                  const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,
+                                  int pair, int variant, hipStream_t stream) {
+  return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, pair != 0, variant,
+                 stream);
 }

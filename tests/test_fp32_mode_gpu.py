@@ -135,8 +135,10 @@ def test_preprocess_s2d_fp32(cuda):
     assert (out.cpu() - ref).abs().mean().item() < 1e-4
 
 
-def test_fused_neck_x3_vs_unfused(cuda):
-    """fp32 fused deconv + head (streamed split head weights) == the fp32 module."""
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_fused_neck_x3_vs_unfused(cuda, variant):
+    """fp32 fused deconv + head (streamed split head weights) == the fp32 module,
+    for every tiling variant (per-pixel math is the same, so the bits are too)."""
     from triton_client_amd.models.fast import FastBEV
     from test_fast_plans import _small_pp
 
@@ -148,10 +150,13 @@ def test_fused_neck_x3_vs_unfused(cuda):
         ref = copy.deepcopy(pm).double().bev_forward(canvas.double().permute(0, 3, 1, 2))
     fb = FastBEV(pm, 2, device=cuda, precision="fp32")
     assert fb.neck is not None
-    outs = fb.forward(NHWC(canvas.to(cuda)))
+    outs = [o.values().clone() for o in fb.forward(NHWC(canvas.to(cuda)))]
+    fb.neck.variant = variant
+    outs_v = [o.values().clone() for o in fb.forward(NHWC(canvas.to(cuda)))]
     torch.cuda.synchronize()
-    for r, o in zip(ref, outs):
-        assert rel_l2(o.nchw().cpu(), r) < 2e-4
+    for r, o, ov in zip(ref, outs, outs_v):
+        assert torch.equal(o, ov)
+        assert rel_l2(o.permute(0, 3, 1, 2).cpu(), r) < 2e-4
 
 
 def test_fast_yolo_fp32_vs_module(cuda):

@@ -69,6 +69,7 @@ _KERNEL_SIGS = {
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     "tca_bev_neck_head_x3": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     "tca_bev_neck_head_x3p": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
+    "tca_bev_neck_head_x3v": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, I, I, P],
     # SECOND-IoU: sparse 3D backbone + RoI head (spconv.hip)
     "tca_sp_offsets": [P, I, P, P, P],
     "tca_sp_vfe_slots": [P, I, I, P, P, I, P, P, I, I, P, P, P, P, P, P],

@@ -75,6 +75,9 @@ class FusedNeckHead:
         if grid <= 0:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
+        # fp32 tiling variant (bev_neck.hip tca_bev_neck_head_x3v): 0 auto, 1 <8 waves, 3 stages>,
+        # 2 <4 waves, 2 stages, two workgroups per CU>, 3 <8 waves, 2 stages>
+        self.variant = 0
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
             self.wh = split_pairs(wh).to(device)
@@ -101,9 +104,10 @@ class FusedNeckHead:
         ptrs = (ctypes.c_void_p * n)(*[x.t.data_ptr() for x in xs])
         ldx = (ctypes.c_int * n)(*[x.t.shape[-1] for x in xs])
         offx = (ctypes.c_int * n)(*[x.off for x in xs])
-        fn = ("tca_bev_neck_head_x3p" if pair else "tca_bev_neck_head_x3") if self.precision == "fp32" \
-            else "tca_bev_neck_head"
-        _native.call(fn, n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b,
-                     _native.ptr(self.wh), _native.ptr(self.bh), self.nh, _native.ptr(out.t), out.t.shape[-1],
-                     B, H, W, self.grid, _native.stream_ptr(stream))
+        args = (n, ptrs, ldx, offx, self._cin, self._s, self._w, self._b, _native.ptr(self.wh),
+                _native.ptr(self.bh), self.nh, _native.ptr(out.t), out.t.shape[-1], B, H, W, self.grid)
+        if self.precision == "fp32":
+            _native.call("tca_bev_neck_head_x3v", *args, int(pair), self.variant, _native.stream_ptr(stream))
+        else:
+            _native.call("tca_bev_neck_head", *args, _native.stream_ptr(stream))
         return out
