@@ -1640,6 +1640,9 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     case 75: return launch_xb<256, 64, 4, 2, 3, PAIR_OUT>(a, stream);
     case 76: return launch_xb<256, 128, 4, 2, 2, PAIR_OUT>(a, stream);
     case 77: return launch_xb<128, 64, 4, 2, 2, PAIR_OUT>(a, stream);
+    // 4 waves of 64x64: half the LDS fragment reads per MFMA of the 8-wave tiles
+    case 78: return launch_xb<128, 128, 2, 2, 2, PAIR_OUT>(a, stream);
+    case 79: return launch_xb<256, 64, 4, 1, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 22: return launch_glds_x3<128, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);
