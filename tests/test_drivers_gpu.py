@@ -113,3 +113,35 @@ def test_served_path_matches_local_engines(cuda):
         assert na > 0 and abs(na - nb) <= max(2, na // 50), (na, nb)
         np.testing.assert_allclose(np.sort(a["pred_scores"])[-20:], np.sort(b["pred_scores"])[-20:], rtol=1e-4,
                                    atol=1e-5)
+
+
+def test_served_dynamic_batch_matches_single_requests(cuda):
+    """Server-side dynamic batching: a batch of requests through the models'
+    batch plans returns what each request gets alone."""
+    from triton_client_amd.ops.golden import preprocess_image
+    from triton_client_amd.ops.lidar import voxelize_np
+    from triton_client_amd.server import ModelRepository
+
+    repo = ModelRepository("cuda")
+    s2, s3 = repo.load("YOLOv5nCOCO"), repo.load("pointpillar_kitti")
+    assert s2.dynamic_batch > 1 and s3.dynamic_batch > 1
+    imgs = [preprocess_image(camera_frame(480, 640, s), (640, 640), "stretch", layout="NCHW")[None] for s in range(3)]
+    single = [s2.execute({"images": x}, ["output"])["output"].clone() for x in imgs]
+    batch = s2.execute_batch([{"images": x} for x in imgs], ["output"])
+    for a, b in zip(single, batch):
+        d = (a - b["output"]).abs().max().item()
+        assert d <= 1e-3 * max(1.0, a.abs().max().item()), d
+    reqs = []
+    for s in (4, 5, 6):
+        pts = lidar_sweep(LidarSpec(rings=64, azimuth_steps=1875, sensor_height=3.23), s)
+        pts = np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4)
+        vox, co, n = voxelize_np(pts, s3.cfg.voxel)[:3]
+        co4 = np.concatenate([np.zeros((len(co), 1), np.int32), co.astype(np.int32)], 1)
+        reqs.append({"voxels": vox.astype(np.float32), "voxel_coords": co4, "voxel_num_points": n.astype(np.int32)})
+    single3 = [{k: v.copy() for k, v in s3.execute(r, []).items()} for r in reqs]
+    batch3 = s3.execute_batch(reqs, [])
+    for a, b in zip(single3, batch3):
+        na, nb = len(a["pred_scores"]), len(b["pred_scores"])
+        assert na > 0 and abs(na - nb) <= max(2, na // 50), (na, nb)
+        np.testing.assert_allclose(np.sort(a["pred_scores"])[-20:], np.sort(b["pred_scores"])[-20:], rtol=1e-4,
+                                   atol=1e-5)

@@ -115,3 +115,72 @@ def test_server_errors_and_faults():
         idx = ch.fetch_channel().RepositoryIndex(pb.RepositoryIndexRequest())
         assert any(m.name == "echo" and m.state == "READY" for m in idx.models)
         ch.close()
+
+
+class _PickyEcho(EchoModel):
+    """Echo that rejects a request whose first value is negative (per-request error in a batch)."""
+
+    def execute(self, inputs, requested):
+        from triton_client_amd.server.model import InferError
+        if float(inputs["INPUT0"].reshape(-1)[0]) < 0:
+            raise InferError("negative")
+        return super().execute(inputs, requested)
+
+    def execute_batch(self, batch, requested):
+        self.sizes.append(len(batch))
+        return [self.execute(x, requested) for x in batch]
+
+
+def test_dynamic_batching_concurrent_requests_and_isolation():
+    """Concurrent batch-1 requests are executed in shared batches (fewer
+    executions than requests), every caller gets its own result, and a bad
+    request fails alone while the rest of its batch succeeds."""
+    import threading
+
+    from triton_client_amd.server.model import InferError
+
+    m = _PickyEcho("echo")
+    m.sizes = []
+    m.dynamic_batch, m.batch_delay_s = 4, 0.02
+    m.load()
+    n = 24
+    res, errs = [None] * n, [None] * n
+
+    def call(i):
+        x = np.full((3,), -1.0 if i == 5 else float(i), np.float32)
+        try:
+            res[i] = m({"INPUT0": x}, ["OUTPUT0"], encode=lambda o: o["OUTPUT0"].copy())
+        except InferError as e:
+            errs[i] = e
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(10)
+    assert isinstance(errs[5], InferError) and res[5] is None
+    for i in range(n):
+        if i != 5:
+            assert errs[i] is None and np.array_equal(res[i], np.full((3,), float(i), np.float32))
+    assert sum(m.sizes) == n and max(m.sizes) <= 4 and len(m.sizes) < n
+    assert m.stats.inference_count == n - 1 and m.stats.fail_count == 1
+    m.unload()
+    assert m._batcher is None
+
+
+def test_dynamic_batching_over_grpc():
+    import concurrent.futures as cf
+
+    repo = ModelRepository("cpu")
+    m = EchoModel("echo", n=1)
+    m.dynamic_batch, m.batch_delay_s = 8, 0.01
+    repo.add(m)
+    with KServeServer(repo, "127.0.0.1:0", max_workers=16) as srv:
+        ch = GRPCChannel({"grpc_channel": srv.target}, Flags("echo"))
+        xs = [np.arange(4, dtype=np.float32) + i for i in range(16)]
+        with cf.ThreadPoolExecutor(16) as ex:
+            outs = list(ex.map(lambda x: ch.infer_raw([("INPUT0", x)], ["OUTPUT0"]), xs))
+        for x, o in zip(xs, outs):
+            np.testing.assert_array_equal(o["OUTPUT0"], x)
+        assert m._batcher is not None and m._batcher.batches <= 16
+        ch.close()

@@ -44,8 +44,10 @@ def main(argv=None):
     ap.add_argument("--cam", default="720x1280")
     ap.add_argument("--rings", type=int, default=64)
     ap.add_argument("--columns", type=int, default=1875)
-    ap.add_argument("--workers", type=int, default=8, help="server threads")
+    ap.add_argument("--workers", type=int, default=32, help="server threads")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--server-process", action="store_true",
+                    help="run the server as its own process (the deployed topology: no GIL shared with the clients)")
     a = ap.parse_args(argv)
 
     import torch
@@ -58,14 +60,30 @@ def main(argv=None):
     from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
 
     H0, W0 = (int(v) for v in a.cam.split("x"))
-    repo = ModelRepository(a.device)
-    repo.load("YOLOv5nCOCO")
-    repo.load("pointpillar_kitti")
-    srv = KServeServer(repo, "127.0.0.1:0", max_workers=a.workers).start()
+    proc = repo = srv = None
+    if a.server_process:
+        import socket
+        import subprocess
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        target = f"127.0.0.1:{port}"
+        proc = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+                                 str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
+                                 "--models", "YOLOv5nCOCO,pointpillar_kitti"])
+    else:
+        repo = ModelRepository(a.device)
+        repo.load("YOLOv5nCOCO")
+        repo.load("pointpillar_kitti")
+        srv = KServeServer(repo, "127.0.0.1:0", max_workers=a.workers).start()
+        target = srv.target
 
     def channel(model):
         flags = SimpleNamespace(model_name=model, model_version="", batch_size=64, verbose=False)
-        return GRPCChannel({"grpc_channel": srv.target}, flags)
+        ch = GRPCChannel({"grpc_channel": target}, flags, wait_ready_s=300.0) if proc else \
+            GRPCChannel({"grpc_channel": target}, flags)
+        return ch
 
     ch2, ch3 = channel("YOLOv5nCOCO"), channel("pointpillar_kitti")
     cr3 = ch3.get_metadata()["config_response"]
@@ -101,8 +119,16 @@ def main(argv=None):
     for t in th:
         t.join()
     wall = time.perf_counter() - t0
-    srv.stop()
-    stats = {m: repo.get(m).stats for m in ("YOLOv5nCOCO", "pointpillar_kitti")}
+    stats = {}
+    for m in ("YOLOv5nCOCO", "pointpillar_kitti"):  # from the server (either topology) over the stats RPC
+        ms_ = ch2.model_statistics(m).model_stats[0]
+        stats[m] = SimpleNamespace(compute_ns=ms_.inference_stats.compute_infer.ns, inference_count=ms_.inference_count,
+                                   execution_count=ms_.execution_count)
+    if srv is not None:
+        srv.stop()
+    if proc is not None:
+        proc.terminate()
+        proc.wait(30)
 
     def ms(timer):
         return {k: round(1e3 * float(np.sum(v)) / a.frames, 3) for k, v in timer.items()}
@@ -115,6 +141,9 @@ def main(argv=None):
             "client_ms_per_frame": {"camera": ms(det2.timer), "lidar": ms(det3.timer)},
             "server_compute_ms_per_request": {m: round(s.compute_ns / max(1, s.inference_count) / 1e6, 3)
                                               for m, s in stats.items()},
+            "server_requests_per_execution": {m: round(s.inference_count / max(1, s.execution_count), 2)
+                                              for m, s in stats.items()},
+            "topology": "server process + client process" if proc else "one process",
             "avg_dets_per_frame": {"2d": round(n2, 1), "3d": round(n3, 1)},
             "path": "GPU preprocess/voxelise -> pinned staging -> C++ KServe encoder -> gRPC -> C++ parse -> pinned "
                     "-> GPU model -> pinned -> C++ encoder -> gRPC -> zero-copy response views"}

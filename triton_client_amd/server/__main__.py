@@ -13,7 +13,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--port", type=int, default=8001)
     ap.add_argument("--metrics-port", type=int, default=8002)
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--workers", type=int, default=32)
     ap.add_argument("--export-repository", default=None, metavar="DIR",
                     help="write a Triton-layout repository for --models into DIR and exit")
     ap.add_argument("--weights", action="append", default=[], metavar="MODEL=URI",

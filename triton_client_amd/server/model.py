@@ -9,6 +9,7 @@ contract the reference's clients negotiate via ``ModelMetadata`` /
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 from abc import ABC, abstractmethod
@@ -51,10 +52,106 @@ class InferError(Exception):
     """Raised by execute() for a client error (bad shape/dtype) → INVALID_ARGUMENT."""
 
 
+class _Pending:
+    __slots__ = ("inputs", "requested", "encode", "done", "result", "exc")
+
+    def __init__(self, inputs, requested, encode):
+        self.inputs, self.requested, self.encode = inputs, requested, encode
+        self.done = threading.Event()
+        self.result = None
+        self.exc: Optional[BaseException] = None
+
+
+class DynamicBatcher:
+    """Server-side dynamic batching (Triton's ``dynamic_batching``, transparent
+    to batch-1 clients: the reference's models are ``max_batch_size: 0``,
+    ``examples/YOLOv5/config.pbtxt:3``).  Request threads enqueue and wait;
+    one batcher thread takes the oldest request, waits up to ``delay_s`` for
+    more (up to ``max_batch``), runs them as ONE ``execute_batch`` under the
+    model lock and encodes every request's response from its slice before the
+    next batch reuses the staging.  A batch that fails is re-run request by
+    request so one bad request cannot fail its neighbours."""
+
+    def __init__(self, model: "ServedModel", max_batch: int, delay_s: float):
+        self.model, self.max_batch, self.delay_s = model, max_batch, delay_s
+        self.q: "collections.deque[_Pending]" = collections.deque()
+        self.cv = threading.Condition()
+        self.stopped = False
+        self.batches = 0
+        self.thread = threading.Thread(target=self._run, name=f"batcher-{model.name}", daemon=True)
+        self.thread.start()
+
+    def submit(self, inputs, requested, encode):
+        item = _Pending(inputs, requested, encode)
+        with self.cv:
+            if self.stopped:
+                raise InferError(f"model '{self.model.name}' is unloading")
+            self.q.append(item)
+            self.cv.notify()
+        item.done.wait()
+        if item.exc is not None:
+            raise item.exc
+        return item.result
+
+    def stop(self) -> None:
+        with self.cv:
+            self.stopped = True
+            self.cv.notify_all()
+        self.thread.join(timeout=5)
+
+    def _take(self):
+        with self.cv:
+            while not self.q and not self.stopped:
+                self.cv.wait()
+            if not self.q:
+                return None
+            deadline = time.perf_counter() + self.delay_s
+            while len(self.q) < self.max_batch and not self.stopped:
+                left = deadline - time.perf_counter()
+                if left <= 0:
+                    break
+                self.cv.wait(left)
+            return [self.q.popleft() for _ in range(min(self.max_batch, len(self.q)))]
+
+    def _run(self) -> None:
+        while True:
+            items = self._take()
+            if items is None:
+                return
+            self.batches += 1
+            m = self.model
+            with m._lock:
+                try:
+                    outs = m.execute_batch([it.inputs for it in items], items[0].requested)
+                    for it, o in zip(items, outs):
+                        self._finish(it, o)
+                except Exception:
+                    for it in items:  # isolate the failing request(s)
+                        if it.done.is_set():
+                            continue
+                        try:
+                            self._finish(it, m.execute(it.inputs, it.requested))
+                        except Exception as e:  # noqa: BLE001 - handed to the waiting request thread
+                            it.exc = e
+                            it.done.set()
+
+    @staticmethod
+    def _finish(it: _Pending, out) -> None:
+        try:
+            it.result = it.encode(out) if it.encode is not None else out
+        except Exception as e:  # noqa: BLE001
+            it.exc = e
+        it.done.set()
+
+
 class ServedModel(ABC):
     platform = "amd_mi355x"
     backend = "triton_client_amd"
     max_batch_size = 0
+    # server-side dynamic batching of concurrent batch-1 requests (DynamicBatcher);
+    # a model sets dynamic_batch > 1 in load() once it has an execute_batch
+    dynamic_batch = 1
+    batch_delay_s = 0.0005
 
     def __init__(self, name: str, version: str = "1"):
         self.name = name
@@ -63,6 +160,7 @@ class ServedModel(ABC):
         self.stats = ModelStats()
         self._config: Optional[mc.ModelConfig] = None
         self._lock = threading.Lock()  # one execution at a time per instance (GPU graph buffers)
+        self._batcher: Optional[DynamicBatcher] = None
 
     # ---------------------------------------------------------------- contract
     @abstractmethod
@@ -77,11 +175,21 @@ class ServedModel(ABC):
     def execute(self, inputs: Dict[str, np.ndarray], requested: Sequence[str]) -> Dict[str, np.ndarray]:
         ...
 
+    def execute_batch(self, batch: Sequence[Dict[str, np.ndarray]], requested: Sequence[str]
+                      ) -> List[Dict[str, np.ndarray]]:
+        """Run several requests as one execution (dynamic batching).  The
+        returned outputs may be views of staging that stays valid until the
+        next execution; the batcher encodes every response before that."""
+        raise NotImplementedError
+
     def load(self) -> None:
         """Allocate / build / warm up.  Sets ready."""
         self.ready = True
 
     def unload(self) -> None:
+        if self._batcher is not None:
+            self._batcher.stop()
+            self._batcher = None
         self.ready = False
 
     def instance_kind(self) -> int:
@@ -128,10 +236,17 @@ class ServedModel(ABC):
         t0 = time.perf_counter_ns()
         try:
             self.validate(inputs)
-            with self._lock:
-                out = self.execute(inputs, requested)
-                if encode is not None:
-                    out = encode(out)
+            if self.dynamic_batch > 1:
+                if self._batcher is None:
+                    with self._lock:
+                        if self._batcher is None:
+                            self._batcher = DynamicBatcher(self, self.dynamic_batch, self.batch_delay_s)
+                out = self._batcher.submit(inputs, requested, encode)
+            else:
+                with self._lock:
+                    out = self.execute(inputs, requested)
+                    if encode is not None:
+                        out = encode(out)
         except Exception:
             with self.stats.lock:
                 self.stats.fail_count += 1
@@ -139,7 +254,8 @@ class ServedModel(ABC):
         dt = time.perf_counter_ns() - t0
         with self.stats.lock:
             self.stats.inference_count += 1
-            self.stats.execution_count += 1
+            self.stats.execution_count = (self._batcher.batches if self._batcher is not None
+                                          else self.stats.execution_count + 1)
             self.stats.success_ns += dt
             self.stats.compute_ns += dt
             self.stats.last_inference_ms = int(time.time() * 1000)
@@ -164,3 +280,6 @@ class EchoModel(ServedModel):
 
     def execute(self, inputs, requested):
         return {f"OUTPUT{i}": inputs[f"INPUT{i}"] for i in range(self.n)}
+
+    def execute_batch(self, batch, requested):
+        return [self.execute(x, requested) for x in batch]

@@ -42,8 +42,10 @@ def _device(device) -> torch.device:
 
 class YoloV5Model(ServedModel):
     def __init__(self, name: str = "YOLOv5nCOCO", variant: str = "n", nc: int = 80, img: int = 640,
-                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0):
+                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0,
+                 batch: int = 8):
         super().__init__(name)
+        self.batch = batch  # dynamic batching: concurrent requests run as one captured batch-`batch` graph
         self.variant, self.nc, self.img = variant, nc, img
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -88,6 +90,21 @@ class YoloV5Model(ServedModel):
                 self.fast.set_input(self.x_dev)
                 return self.pipe.post.decode(self.fast.forward())
             self.runner = GraphRunner(step)
+            if self.batch > 1:
+                # batch plan over the same (calibrated) module, its own graph and staging
+                from ..models.fast import FastYOLOv5
+                B = self.batch
+                self.fast_b = FastYOLOv5(self.pipe.model, B, (self.img, self.img), self.device,
+                                         precision=self.pipe.precision)
+                self.xb_dev = torch.zeros((B, 3, self.img, self.img), dtype=torch.float32, device=self.device)
+                self.pin_in_b = torch.empty((B, 3, self.img, self.img), dtype=torch.float32).pin_memory()
+                self.pin_out_b = None
+
+                def step_b():
+                    self.fast_b.set_input(self.xb_dev)
+                    return self.pipe.post.decode(self.fast_b.forward())
+                self.runner_b = GraphRunner(step_b)
+                self.dynamic_batch = B
         else:
             from ..models.common import fuse_model
             if not self.weights:  # same head prior as the GPU path (random init)
@@ -117,11 +134,28 @@ class YoloV5Model(ServedModel):
             out = yolo_decode_reference(heads, self.model.anchors).numpy()
         return {"output": out.astype(np.float32, copy=False)}
 
+    @torch.no_grad()
+    def execute_batch(self, batch, requested):
+        n = len(batch)
+        if n == 1 or self.device.type != "cuda" or self.batch <= 1:
+            return [self.execute(x, requested) for x in batch]
+        for i, inp in enumerate(batch):  # request views -> pinned staging (the one host copy)
+            np.copyto(self.pin_in_b[i].numpy(), inp["images"].reshape(3, self.img, self.img), casting="same_kind")
+        self.xb_dev[:n].copy_(self.pin_in_b[:n], non_blocking=True)  # slots >= n: stale, outputs unused
+        dec = self.runner_b()
+        if self.pin_out_b is None:
+            self.pin_out_b = torch.empty(dec.shape, dtype=torch.float32).pin_memory()
+        self.pin_out_b[:n].copy_(dec[:n], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return [{"output": self.pin_out_b[i:i + 1]} for i in range(n)]
+
 
 class PointPillarsModel(ServedModel):
     def __init__(self, name: str = "pointpillar_kitti", cfg: Optional[PointPillarsConfig] = None, device="auto",
-                 weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 2000.0):
+                 weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 2000.0,
+                 batch: int = 8):
         super().__init__(name)
+        self.batch = batch  # dynamic batching: concurrent requests share one batch-`batch` pass
         self.cfg = cfg or PointPillarsConfig()
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -176,10 +210,64 @@ class PointPillarsModel(ServedModel):
             self.vcount = torch.zeros((1,), dtype=torch.int32, device=self.device)
             self.enc.clear(self.pipe.vox)  # start from an empty canvas
             self.model = self.pipe.model
+            if self.batch > 1:
+                B = self.batch
+                self.pipe_b = LidarPipeline(self.pipe.model, batch=B, max_points=1024, device=self.device)
+                self.enc_b = self.pipe_b.enc
+                self.voxels_b = torch.zeros((B, V, self.P, 4), dtype=torch.float32, device=self.device)
+                self.coords_b = torch.zeros((B, V, 4), dtype=torch.int32, device=self.device)
+                self.nump_b = torch.zeros((B, V), dtype=torch.int32, device=self.device)
+                self.vcount_b = torch.zeros((B,), dtype=torch.int32, device=self.device)
+                self.pin_vcount_b = torch.zeros((B,), dtype=torch.int32).pin_memory()
+                self.enc_b.clear(self.pipe_b.vox)
+                self.dynamic_batch = B
         else:
             from ..models.common import fuse_model
             self.model = fuse_model(model.eval())
         self.ready = True
+
+    def _check(self, vox):
+        if vox.ndim != 3 or vox.shape[1] != self.P or vox.shape[2] < 4:
+            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
+        if vox.shape[0] > self.cfg.voxel.max_voxels:
+            raise InferError(f"{vox.shape[0]} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+
+    @torch.no_grad()
+    def execute_batch(self, batch, requested):
+        n = len(batch)
+        if n == 1 or self.device.type != "cuda" or self.batch <= 1:
+            return [self.execute(x, requested) for x in batch]
+        for inp in batch:
+            self._check(inp["voxels"])
+        Vm = self.cfg.voxel.max_voxels
+        if getattr(self, "pin_vox_b", None) is None:
+            B = self.batch
+            self.pin_vox_b = torch.empty((B, Vm, self.P, 4), dtype=torch.float32).pin_memory()
+            self.pin_co_b = torch.empty((B, Vm, 4), dtype=torch.int32).pin_memory()
+            self.pin_n_b = torch.empty((B, Vm), dtype=torch.int32).pin_memory()
+        # clear the previous batch's cells (its coords / counts) before the new ones land
+        self.enc_b.clear_coords(self.coords_b, self.vcount_b)
+        self.pin_vcount_b.zero_()
+        for i, inp in enumerate(batch):
+            vox, co, nn_ = inp["voxels"], inp["voxel_coords"], inp["voxel_num_points"]
+            V = vox.shape[0]
+            np.copyto(self.pin_vox_b[i, :V].numpy(), vox[..., :4], casting="same_kind")
+            np.copyto(self.pin_co_b[i, :V].numpy(), co, casting="unsafe")
+            np.copyto(self.pin_n_b[i, :V].numpy(), nn_, casting="unsafe")
+            self.pin_co_b[i, :V, 0] = i
+            self.voxels_b[i, :V].copy_(self.pin_vox_b[i, :V], non_blocking=True)
+            self.coords_b[i, :V].copy_(self.pin_co_b[i, :V], non_blocking=True)
+            self.nump_b[i, :V].copy_(self.pin_n_b[i, :V], non_blocking=True)
+            self.pin_vcount_b[i] = V
+        self.vcount_b.copy_(self.pin_vcount_b, non_blocking=True)  # slots >= n: no voxels
+        fast = self.pipe_b.fast or self.pipe_b.build_fast()
+        self.enc_b.encode_from_voxels(self.voxels_b, self.nump_b, self.coords_b, self.vcount_b)
+        res = self.pipe_b.post(*fast.forward(self.enc_b.canvas_nhwc()))
+        cnt = res.count[:n].cpu().tolist()
+        box, score, cls = res.box[:n].cpu(), res.score[:n].cpu(), res.cls[:n].cpu()
+        return [{"pred_boxes": box[i, :k].numpy().astype(np.float32),
+                 "pred_scores": score[i, :k].numpy().astype(np.float32),
+                 "pred_labels": cls[i, :k].numpy().astype(np.int64)} for i, k in enumerate(cnt)]
 
     @torch.no_grad()
     def execute(self, inputs, requested):
@@ -187,10 +275,7 @@ class PointPillarsModel(ServedModel):
         co = inputs["voxel_coords"]
         n = inputs["voxel_num_points"]
         V = vox.shape[0]
-        if vox.shape[1] != self.P or vox.shape[2] < 4:
-            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
-        if V > self.cfg.voxel.max_voxels:
-            raise InferError(f"{V} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+        self._check(vox)
         if self.device.type == "cuda":
             if getattr(self, "pin_vox", None) is None:
                 Vm = self.cfg.voxel.max_voxels
