@@ -52,6 +52,44 @@ class InferError(Exception):
     """Raised by execute() for a client error (bad shape/dtype) → INVALID_ARGUMENT."""
 
 
+class _RWLock:
+    """Many executions (shared) or one model load (exclusive).  A load builds
+    and captures hipGraphs; a capture racing kernels that another thread
+    launches (another model serving) can record or corrupt them, so no
+    model executes while any model loads."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._readers = 0
+        self._writer = False
+
+    def acquire_shared(self):
+        with self._cv:
+            while self._writer:
+                self._cv.wait()
+            self._readers += 1
+
+    def release_shared(self):
+        with self._cv:
+            self._readers -= 1
+            if self._readers == 0:
+                self._cv.notify_all()
+
+    def acquire_exclusive(self):
+        with self._cv:
+            while self._writer or self._readers:
+                self._cv.wait()
+            self._writer = True
+
+    def release_exclusive(self):
+        with self._cv:
+            self._writer = False
+            self._cv.notify_all()
+
+
+GPU_PHASE = _RWLock()
+
+
 class _Pending:
     __slots__ = ("inputs", "requested", "encode", "done", "result", "exc")
 
@@ -120,20 +158,27 @@ class DynamicBatcher:
                 return
             self.batches += 1
             m = self.model
-            with m._lock:
-                try:
-                    outs = m.execute_batch([it.inputs for it in items], items[0].requested)
-                    for it, o in zip(items, outs):
-                        self._finish(it, o)
-                except Exception:
-                    for it in items:  # isolate the failing request(s)
-                        if it.done.is_set():
-                            continue
-                        try:
-                            self._finish(it, m.execute(it.inputs, it.requested))
-                        except Exception as e:  # noqa: BLE001 - handed to the waiting request thread
-                            it.exc = e
-                            it.done.set()
+            GPU_PHASE.acquire_shared()
+            try:
+                self._execute(m, items)
+            finally:
+                GPU_PHASE.release_shared()
+
+    def _execute(self, m: "ServedModel", items) -> None:
+        with m._lock:
+            try:
+                outs = m.execute_batch([it.inputs for it in items], items[0].requested)
+                for it, o in zip(items, outs):
+                    self._finish(it, o)
+            except Exception:
+                for it in items:  # isolate the failing request(s)
+                    if it.done.is_set():
+                        continue
+                    try:
+                        self._finish(it, m.execute(it.inputs, it.requested))
+                    except Exception as e:  # noqa: BLE001 - handed to the waiting request thread
+                        it.exc = e
+                        it.done.set()
 
     @staticmethod
     def _finish(it: _Pending, out) -> None:
@@ -243,10 +288,14 @@ class ServedModel(ABC):
                             self._batcher = DynamicBatcher(self, self.dynamic_batch, self.batch_delay_s)
                 out = self._batcher.submit(inputs, requested, encode)
             else:
-                with self._lock:
-                    out = self.execute(inputs, requested)
-                    if encode is not None:
-                        out = encode(out)
+                GPU_PHASE.acquire_shared()
+                try:
+                    with self._lock:
+                        out = self.execute(inputs, requested)
+                        if encode is not None:
+                            out = encode(out)
+                finally:
+                    GPU_PHASE.release_shared()
         except Exception:
             with self.stats.lock:
                 self.stats.fail_count += 1

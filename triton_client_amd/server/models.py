@@ -34,6 +34,24 @@ from .model import InferError, ServedModel, tensor_spec
 from ..utils.model_store import load_state_dict
 
 
+_STAGE_POOL = None
+
+
+def _stage_parallel(fn, n: int) -> None:
+    """Run fn(0..n-1) on a small shared thread pool: the per-request copies of a
+    dynamic batch into pinned staging (numpy releases the GIL inside copyto, so
+    the host memcpys of several multi-MB requests overlap)."""
+    global _STAGE_POOL
+    if n <= 1:
+        for i in range(n):
+            fn(i)
+        return
+    if _STAGE_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _STAGE_POOL = ThreadPoolExecutor(8, thread_name_prefix="stage")
+    list(_STAGE_POOL.map(fn, range(n)))
+
+
 def _device(device) -> torch.device:
     if device in (None, "auto"):
         return torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -105,6 +123,10 @@ class YoloV5Model(ServedModel):
                     return self.pipe.post.decode(self.fast_b.forward())
                 self.runner_b = GraphRunner(step_b)
                 self.dynamic_batch = B
+            # capture now (under the repository's exclusive GPU phase), never lazily while serving
+            self.runner.capture()
+            if self.batch > 1:
+                self.runner_b.capture()
         else:
             from ..models.common import fuse_model
             if not self.weights:  # same head prior as the GPU path (random init)
@@ -139,8 +161,8 @@ class YoloV5Model(ServedModel):
         n = len(batch)
         if n == 1 or self.device.type != "cuda" or self.batch <= 1:
             return [self.execute(x, requested) for x in batch]
-        for i, inp in enumerate(batch):  # request views -> pinned staging (the one host copy)
-            np.copyto(self.pin_in_b[i].numpy(), inp["images"].reshape(3, self.img, self.img), casting="same_kind")
+        _stage_parallel(lambda i: np.copyto(self.pin_in_b[i].numpy(),  # request views -> pinned (one host copy)
+                                            batch[i]["images"].reshape(3, self.img, self.img), casting="same_kind"), n)
         self.xb_dev[:n].copy_(self.pin_in_b[:n], non_blocking=True)  # slots >= n: stale, outputs unused
         dec = self.runner_b()
         if self.pin_out_b is None:
@@ -248,13 +270,17 @@ class PointPillarsModel(ServedModel):
         # clear the previous batch's cells (its coords / counts) before the new ones land
         self.enc_b.clear_coords(self.coords_b, self.vcount_b)
         self.pin_vcount_b.zero_()
-        for i, inp in enumerate(batch):
-            vox, co, nn_ = inp["voxels"], inp["voxel_coords"], inp["voxel_num_points"]
+
+        def stage(i):
+            vox, co, nn_ = batch[i]["voxels"], batch[i]["voxel_coords"], batch[i]["voxel_num_points"]
             V = vox.shape[0]
             np.copyto(self.pin_vox_b[i, :V].numpy(), vox[..., :4], casting="same_kind")
             np.copyto(self.pin_co_b[i, :V].numpy(), co, casting="unsafe")
             np.copyto(self.pin_n_b[i, :V].numpy(), nn_, casting="unsafe")
             self.pin_co_b[i, :V, 0] = i
+        _stage_parallel(stage, n)
+        for i, inp in enumerate(batch):
+            V = inp["voxels"].shape[0]
             self.voxels_b[i, :V].copy_(self.pin_vox_b[i, :V], non_blocking=True)
             self.coords_b[i, :V].copy_(self.pin_co_b[i, :V], non_blocking=True)
             self.nump_b[i, :V].copy_(self.pin_n_b[i, :V], non_blocking=True)

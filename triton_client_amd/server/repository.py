@@ -131,7 +131,12 @@ class ModelRepository:
 
     def add(self, model: ServedModel, load: bool = True) -> ServedModel:
         if load and not model.ready:
-            model.load()
+            from .model import GPU_PHASE
+            GPU_PHASE.acquire_exclusive()  # graphs are captured with no other model executing
+            try:
+                model.load()
+            finally:
+                GPU_PHASE.release_exclusive()
         with self._lock:
             self._models[model.name] = model
         return model
