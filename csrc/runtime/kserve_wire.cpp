@@ -163,6 +163,7 @@ bool parse_tensor(const uint8_t* buf, const uint8_t* s, uint64_t l, long* m, int
   m[0] = m[1] = m[2] = m[3] = 0;
   m[4] = 0;
   m[5] = *nd_total;
+  m[6] = 0;
   while (t.p < t.end && t.ok) {
     const uint64_t tt = t.varint();
     if (!t.ok) break;
@@ -191,6 +192,9 @@ bool parse_tensor(const uint8_t* buf, const uint8_t* s, uint64_t l, long* m, int
       if (*nd_total >= max_dims) { *err = -2; return false; }
       shapes[(*nd_total)++] = (int64_t)d;
       ++m[4];
+    } else if (f == 4 && w == 2) {  // parameters (e.g. shared_memory_region): flagged for the caller
+      m[6] = 1;
+      if (!t.skip(w)) { *err = -1; return false; }
     } else if (!t.skip(w)) {
       *err = -1;
       return false;
@@ -240,13 +244,16 @@ TCA_API long tca_kserve_encode_response(const char* model_name, const char* mode
 //   raw[k*2 + 0..1]  raw_input_contents[k] offset/length
 //   req[k*2 + 0..1]  requested output k name offset/length
 //   counts[0..8]     n_inputs, n_raw, n_requested, model_name off/len, model_version off/len, id off/len
+//   counts[9]        1 when an input or a requested output carries parameters (the shared-memory
+//                    extension's region references: the caller takes the protobuf path)
+//   meta[k*8 + 6]    1 when input k carries parameters
 // Returns 0, -1 malformed, -2 capacity exceeded.
 TCA_API int tca_kserve_parse_request(const uint8_t* buf, long len, int max_t, long* meta, int64_t* shapes,
                                      int max_dims, long* raw, long* req, long* counts) {
   if (!buf || len < 0 || max_t < 0 || max_dims < 0) return -1;
   Reader r{buf, buf + len};
   int n_in = 0, n_raw = 0, n_req = 0, nd_total = 0, err = 0;
-  for (int i = 0; i < 9; ++i) counts[i] = 0;
+  for (int i = 0; i < 10; ++i) counts[i] = 0;
   while (r.p < r.end && r.ok) {
     const uint64_t tag = r.varint();
     const int field = (int)(tag >> 3), wire = (int)(tag & 7);
@@ -263,6 +270,7 @@ TCA_API int tca_kserve_parse_request(const uint8_t* buf, long len, int max_t, lo
       if (!r.ok) return -1;
       if (n_in >= max_t) return -2;
       if (!parse_tensor(buf, s, l, meta + n_in * 8, shapes, max_dims, &nd_total, &err)) return err;
+      if (meta[n_in * 8 + 6]) counts[9] = 1;
       ++n_in;
     } else if (field == 6 && wire == 2) {
       uint64_t l;
@@ -280,6 +288,9 @@ TCA_API int tca_kserve_parse_request(const uint8_t* buf, long len, int max_t, lo
           if (!t.ok) break;
           req[n_req * 2] = q - buf;
           req[n_req * 2 + 1] = (long)sl;
+        } else if ((tt >> 3) == 2 && (tt & 7) == 2) {  // requested-output parameters
+          counts[9] = 1;
+          if (!t.skip(2)) return -1;
         } else if (!t.skip((int)(tt & 7))) {
           return -1;
         }

@@ -145,3 +145,48 @@ def test_served_dynamic_batch_matches_single_requests(cuda):
         assert na > 0 and abs(na - nb) <= max(2, na // 50), (na, nb)
         np.testing.assert_allclose(np.sort(a["pred_scores"])[-20:], np.sort(b["pred_scores"])[-20:], rtol=1e-4,
                                    atol=1e-5)
+
+
+def test_served_shared_memory_matches_raw_wire(cuda):
+    """KServe system shared memory (inputs and the 2D output in the client's
+    pinned region, messages carrying only references) returns the raw-wire
+    path's detections."""
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+    from triton_client_amd.clients import Yolov5client, client_for_model
+    from triton_client_amd.inference import RemoteDetector2D, RemoteDetector3D
+    from triton_client_amd.server import KServeServer, ModelRepository
+
+    repo = ModelRepository("cuda")
+    repo.load("YOLOv5nCOCO")
+    repo.load("pointpillar_kitti")
+    frames = [camera_frame(480, 640, s) for s in (1, 2, 3, 4, 5)]
+    clouds = [_cloud(s, 64, 1875) for s in (4, 5, 6)]
+    with KServeServer(repo, "127.0.0.1:0") as srv:
+        class F:
+            model_version, batch_size = "", 1
+
+        f2, f3 = F(), F()
+        f2.model_name, f3.model_name = "YOLOv5nCOCO", "pointpillar_kitti"
+        p = {"grpc_channel": srv.target}
+        ch2, ch3 = GRPCChannel(p, f2), GRPCChannel(p, f3)
+        cfg3 = ch3.get_metadata()["config_response"]
+        out = {}
+        for wire in ("raw", "shm"):
+            d2 = RemoteDetector2D(ch2, Yolov5client(), device=cuda, mode="async", wire=wire)
+            d3 = RemoteDetector3D(ch3, client_for_model("pointpillar_kitti", getattr(cfg3, "config", cfg3)),
+                                  device=cuda, mode="async", wire=wire)
+            d2.window = d3.window = 2  # slots are reused within the call
+            out[wire] = (d2.detect(frames), d3.detect(clouds))
+            if wire == "shm":
+                assert len(ch2.system_shared_memory_status().regions) == 2
+                d2.close_shm()
+                d3.close_shm()
+        assert len(ch2.system_shared_memory_status().regions) == 0
+        ch2.close()
+        ch3.close()
+    for a, b in zip(out["raw"][0], out["shm"][0]):
+        np.testing.assert_array_equal(a, b)
+    assert sum(len(a) for a in out["raw"][0]) > 10
+    for a, b in zip(out["raw"][1], out["shm"][1]):
+        assert len(a["pred_scores"]) > 0
+        np.testing.assert_array_equal(a["pred_boxes"], b["pred_boxes"])

@@ -184,3 +184,41 @@ def test_dynamic_batching_over_grpc():
             np.testing.assert_array_equal(o["OUTPUT0"], x)
         assert m._batcher is not None and m._batcher.batches <= 16
         ch.close()
+
+
+def test_system_shared_memory_extension_echo():
+    """Register / status / unregister, then an inference whose input and output
+    live in the client's region: the messages carry only region references."""
+    from triton_client_amd.channel.shm import ShmRegion, shm_params
+    from triton_client_amd.channel.wire import parse_request
+    from triton_client_amd.proto import service_pb2 as pbm
+
+    repo = ModelRepository("cpu")
+    repo.add(EchoModel("echo", n=1, dims=(-1, -1)))
+    with KServeServer(repo, "127.0.0.1:0") as srv, ShmRegion(1 << 16, pin=False) as reg:
+        ch = GRPCChannel({"grpc_channel": srv.target}, Flags("echo"))
+        assert "system_shared_memory" in list(ch.server_metadata().extensions)
+        ch.register_system_shared_memory("r0", reg.key, reg.byte_size)
+        st = ch.system_shared_memory_status()
+        assert st.regions["r0"].byte_size == reg.byte_size and st.regions["r0"].key == reg.key
+        x = reg.view(0, np.float32, (4, 5))
+        x[...] = np.arange(20, dtype=np.float32).reshape(4, 5)
+        req = pbm.ModelInferRequest(model_name="echo", id="7")
+        t = req.inputs.add(name="INPUT0", datatype="FP32", shape=[4, 5])
+        shm_params(t, "r0", 0, 80)
+        shm_params(req.outputs.add(name="OUTPUT0"), "r0", 4096, 80)
+        raw = req.SerializeToString()
+        assert len(raw) < 200 and parse_request(raw).has_params
+        resp = pbm.ModelInferResponse.FromString(ch._grpc_stub.ModelInferRaw(raw))
+        assert list(resp.outputs[0].shape) == [4, 5] and len(resp.raw_output_contents) == 0
+        np.testing.assert_array_equal(reg.view(4096, np.float32, (4, 5)), x)
+        # a slice past the region is a client error
+        bad = pbm.ModelInferRequest(model_name="echo")
+        shm_params(bad.inputs.add(name="INPUT0", datatype="FP32", shape=[1 << 15, 1]), "r0", 0, 4 << 15)
+        import grpc
+        with pytest.raises(grpc.RpcError) as ei:
+            ch._grpc_stub.ModelInfer(bad)
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        ch.unregister_system_shared_memory("r0")
+        assert len(ch.system_shared_memory_status().regions) == 0
+        ch.close()

@@ -46,6 +46,8 @@ def main(argv=None):
     ap.add_argument("--columns", type=int, default=1875)
     ap.add_argument("--workers", type=int, default=32, help="server threads")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--wire", default="raw", choices=("raw", "shm"),
+                    help="raw: tensors in the gRPC messages (C++ codec); shm: KServe system shared memory")
     ap.add_argument("--server-process", action="store_true",
                     help="run the server as its own process (the deployed topology: no GIL shared with the clients)")
     a = ap.parse_args(argv)
@@ -87,10 +89,10 @@ def main(argv=None):
 
     ch2, ch3 = channel("YOLOv5nCOCO"), channel("pointpillar_kitti")
     cr3 = ch3.get_metadata()["config_response"]
-    det2 = RemoteDetector2D(ch2, Yolov5client(), letterbox=False, conf_thres=0.3, mode="async", wire="raw",
+    det2 = RemoteDetector2D(ch2, Yolov5client(), letterbox=False, conf_thres=0.3, mode="async", wire=a.wire,
                             device=a.device)
     det3 = RemoteDetector3D(ch3, client_for_model("pointpillar_kitti", getattr(cr3, "config", cr3)), z_offset=1.5,
-                            mode="async", wire="raw", device=a.device)
+                            mode="async", wire=a.wire, device=a.device)
     det2.window = det3.window = a.window
     n = a.frames + a.warmup
     frames = [camera_frame(H0, W0, s) for s in range(8)]
@@ -124,6 +126,9 @@ def main(argv=None):
         ms_ = ch2.model_statistics(m).model_stats[0]
         stats[m] = SimpleNamespace(compute_ns=ms_.inference_stats.compute_infer.ns, inference_count=ms_.inference_count,
                                    execution_count=ms_.execution_count)
+    for d in (det2, det3):
+        if hasattr(d, "close_shm"):
+            d.close_shm()
     if srv is not None:
         srv.stop()
     if proc is not None:
@@ -143,10 +148,13 @@ def main(argv=None):
                                               for m, s in stats.items()},
             "server_requests_per_execution": {m: round(s.inference_count / max(1, s.execution_count), 2)
                                               for m, s in stats.items()},
-            "topology": "server process + client process" if proc else "one process",
+            "topology": "server process + client process" if proc else "one process", "wire": a.wire,
             "avg_dets_per_frame": {"2d": round(n2, 1), "3d": round(n3, 1)},
-            "path": "GPU preprocess/voxelise -> pinned staging -> C++ KServe encoder -> gRPC -> C++ parse -> pinned "
-                    "-> GPU model -> pinned -> C++ encoder -> gRPC -> zero-copy response views"}
+            "path": ("GPU preprocess/voxelise -> pinned shared-memory slot (KServe system shared memory) -> "
+                     "gRPC message with region references -> server view of the region -> pinned -> GPU model -> "
+                     "2D output written into the client's region / 3D outputs in the message") if a.wire == "shm" else
+                    ("GPU preprocess/voxelise -> pinned staging -> C++ KServe encoder -> gRPC -> C++ parse -> pinned "
+                     "-> GPU model -> pinned -> C++ encoder -> gRPC -> zero-copy response views")}
     print(json.dumps(line), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:

@@ -164,6 +164,18 @@ class GRPCChannel(BaseChannel):
     def server_metadata(self):
         return self._grpc_stub.ServerMetadata(pb.ServerMetadataRequest(), timeout=self.timeout_s)
 
+    # ------------------------------------------------- system shared memory
+    def register_system_shared_memory(self, name: str, key: str, byte_size: int, offset: int = 0):
+        return self._call(self._grpc_stub.SystemSharedMemoryRegister,
+                          pb.SystemSharedMemoryRegisterRequest(name=name, key=key, offset=offset, byte_size=byte_size))
+
+    def unregister_system_shared_memory(self, name: str = ""):
+        return self._call(self._grpc_stub.SystemSharedMemoryUnregister,
+                          pb.SystemSharedMemoryUnregisterRequest(name=name))
+
+    def system_shared_memory_status(self, name: str = ""):
+        return self._call(self._grpc_stub.SystemSharedMemoryStatus, pb.SystemSharedMemoryStatusRequest(name=name))
+
     def model_statistics(self, name: str = ""):
         return self._grpc_stub.ModelStatistics(pb.ModelStatisticsRequest(name=name), timeout=self.timeout_s)
 

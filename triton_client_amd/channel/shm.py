@@ -1,0 +1,67 @@
+"""Client side of the KServe-v2 system shared-memory extension (the role of
+``tritonclient.utils.shared_memory``): a POSIX shared-memory object under
+/dev/shm that the client writes request tensors into and the server writes
+responses into; requests carry only region references (server side:
+``server/shm.py``).  On a GPU client the mapping is page-locked so the
+preprocess kernel's D2H lands in it directly."""
+from __future__ import annotations
+
+import mmap
+import os
+import uuid
+from typing import Optional
+
+import numpy as np
+
+from ..server.shm import SHM_DIR, _host_register, _host_unregister
+
+
+class ShmRegion:
+    def __init__(self, byte_size: int, key: Optional[str] = None, pin: bool = True):
+        self.key = key or f"tca_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+        self.byte_size = int(byte_size)
+        self.path = os.path.join(SHM_DIR, self.key)
+        fd = os.open(self.path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+        try:
+            os.ftruncate(fd, self.byte_size)
+            self.mm = mmap.mmap(fd, self.byte_size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.pinned = _host_register(self.mm, self.byte_size) if pin else False
+
+    def view(self, offset: int, dtype, shape) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape))
+        if offset < 0 or offset + n * dt.itemsize > self.byte_size:
+            raise ValueError(f"[{offset}, {offset + n * dt.itemsize}) outside the {self.byte_size}-byte region")
+        return np.frombuffer(self.mm, dtype=dt, count=n, offset=offset).reshape(shape)
+
+    def close(self, unlink: bool = True) -> None:
+        if self.mm is None:
+            return
+        if self.pinned:
+            _host_unregister(self.mm)
+        try:
+            self.mm.close()
+        except BufferError:  # live views keep the mapping; the file is still unlinked below
+            pass
+        self.mm = None
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def shm_params(t, region: str, offset: int, nbytes: int) -> None:
+    """Set the extension's parameters on a request input / requested output."""
+    t.parameters["shared_memory_region"].string_param = region
+    t.parameters["shared_memory_byte_size"].int64_param = int(nbytes)
+    if offset:
+        t.parameters["shared_memory_offset"].int64_param = int(offset)

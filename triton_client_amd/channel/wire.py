@@ -170,6 +170,7 @@ class ParsedRequest:
         self.datatypes: Dict[str, str] = {}
         self.order: List[str] = []
         self.outputs: List[str] = []
+        self.has_params = False  # a tensor carries parameters (shared-memory references): protobuf path
 
 
 def parse_request(data: bytes, max_tensors: int = 64) -> ParsedRequest:
@@ -184,13 +185,14 @@ def parse_request(data: bytes, max_tensors: int = 64) -> ParsedRequest:
             out.datatypes[t.name] = t.datatype
             out.order.append(t.name)
         out.outputs = [o.name for o in req.outputs]
+        out.has_params = any(len(t.parameters) for t in req.inputs) or any(len(o.parameters) for o in req.outputs)
         return out
     mv = memoryview(data)
     meta = np.zeros((max_tensors, 8), np.int64)
     shapes = np.zeros((max_tensors * 8,), np.int64)
     raw = np.zeros((max_tensors, 2), np.int64)
     req = np.zeros((max_tensors, 2), np.int64)
-    counts = np.zeros((9,), np.int64)
+    counts = np.zeros((10,), np.int64)
     src = ctypes.c_char_p(data)
     rc = rt.tca_kserve_parse_request(ctypes.cast(src, ctypes.c_void_p), len(data), max_tensors, meta.ctypes.data,
                                      shapes.ctypes.data, shapes.size, raw.ctypes.data, req.ctypes.data,
@@ -198,6 +200,7 @@ def parse_request(data: bytes, max_tensors: int = 64) -> ParsedRequest:
     if rc != 0:
         raise ValueError(f"malformed ModelInferRequest ({rc})")
     n_in, n_raw, n_req = (int(v) for v in counts[:3])
+    out.has_params = bool(counts[9])
     txt = lambda o, ln: bytes(mv[o:o + ln]).decode()  # noqa: E731
     out.model_name, out.model_version, out.id = (txt(int(counts[3 + 2 * k]), int(counts[4 + 2 * k])) for k in range(3))
     for k in range(n_in):

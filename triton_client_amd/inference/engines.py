@@ -518,7 +518,7 @@ class _RemoteBase:
     def __init__(self, channel, client, mode: str = "sync", wire: str = "raw", window: int = 8):
         if mode not in ("sync", "async", "stream"):
             raise ValueError(f"mode {mode!r}")
-        if wire not in ("raw", "proto"):
+        if wire not in ("raw", "proto", "shm"):  # shm: KServe system shared memory (same-host server)
             raise ValueError(f"wire {wire!r}")
         self.channel, self.client, self.mode, self.wire, self.window = channel, client, mode, wire, window
         md = channel.get_metadata()
@@ -680,6 +680,110 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         a = np.ascontiguousarray(a.astype(_NP_OF.get(self.dtype, np.float32), copy=False))
         return a, xf
 
+    # ------------------------------------------------------------ shared memory
+    def _shm_setup(self):
+        """Client shm region of `window` slots (input tensor + requested outputs
+        each), registered with the server once."""
+        if getattr(self, "_shm", None) is not None:
+            return self._shm
+        from ..channel.shm import ShmRegion
+        from ..proto import KSERVE_TO_NP
+
+        def nbytes(shape, dt):
+            return int(np.prod(shape)) * np.dtype(dt).itemsize
+
+        def align(n):
+            return (n + 4095) // 4096 * 4096
+
+        in_shape = ((1,) if self.batch_dim else ()) + ((self.h, self.w, 3) if self.nhwc else (3, self.h, self.w))
+        in_dt = _NP_OF.get(self.dtype, np.float32)
+        layout, off = [], align(nbytes(in_shape, in_dt))
+        md = {o.name: o for o in self.model_metadata.outputs}
+        for n in self.requested:
+            shape = [int(d) for d in md[n].shape]
+            if any(d < 0 for d in shape):
+                raise ValueError(f"shared memory transport needs a static shape for output '{n}', got {shape}")
+            b = nbytes(shape, KSERVE_TO_NP[md[n].datatype])
+            layout.append((n, off, b))
+            off += align(b)
+        region = ShmRegion(off * self.window)
+        self.channel.register_system_shared_memory(region.key, region.key, region.byte_size)
+        self._shm = (region, off, in_shape, in_dt, layout)
+        return self._shm
+
+    def close_shm(self) -> None:
+        st = getattr(self, "_shm", None)
+        if st is not None:
+            try:
+                self.channel.unregister_system_shared_memory(st[0].key)
+            finally:
+                st[0].close()
+                self._shm = None
+
+    def _prep_into(self, frame: np.ndarray, dst: np.ndarray):
+        """Preprocess straight into a shm slot (GPU: one D2H into the pinned mapping)."""
+        if self.device.type == "cuda":
+            _, pin_in, dev_in, _, tdt = self._gpu_staging(tuple(frame.shape[:2]))
+            pin_in[0].numpy()[...] = frame[..., :3]
+            dev_in.copy_(pin_in, non_blocking=True)
+            x, xf = preprocess(dev_in, (self.h, self.w), self.mode2d, self.scaling, torch.float32,
+                               "NHWC" if self.nhwc else "NCHW")
+            if self.nhwc:
+                x = x.permute(0, 2, 3, 1)
+            if not self.batch_dim:
+                x = x[0]
+            torch.from_numpy(dst).copy_(x.to(tdt), non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return xf
+        a, xf = self._prep(frame)
+        np.copyto(dst, a.reshape(dst.shape), casting="same_kind")
+        return xf
+
+    def _detect_shm(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
+        from ..channel.shm import shm_params
+        from ..channel.wire import ParsedResponse
+        from ..proto import KSERVE_TO_NP, service_pb2 as pb
+
+        region, slot, in_shape, in_dt, layout = self._shm_setup()
+        ch, timer = self.channel, getattr(self, "timer", None)
+        res: List[Optional[np.ndarray]] = [None] * len(frames)
+        free, inflight = list(range(self.window)), []
+
+        def finish():
+            i, k, xf, fut = inflight.pop(0)
+            with _stage(timer, "rpc"):
+                resp = pb.ModelInferResponse.FromString(fut.result())
+            pr = ParsedResponse()
+            pr.model_name = resp.model_name
+            offs = {n: o for n, o, _ in layout}
+            for t in resp.outputs:
+                pr.outputs[t.name] = region.view(k * slot + offs[t.name], KSERVE_TO_NP[t.datatype], tuple(t.shape))
+                pr.datatypes[t.name] = t.datatype
+                pr.order.append(t.name)
+            d = self._extract(pr)  # consumed before slot k is reused
+            if len(d):
+                d[:, :4] = xf.unmap_boxes(d[:, :4])
+            res[i] = d
+            free.append(k)
+
+        for i, f in enumerate(frames):
+            if not free:
+                finish()
+            k = free.pop(0)
+            with _stage(timer, "preprocess"):
+                xf = self._prep_into(f, region.view(k * slot, in_dt, in_shape))
+            with _stage(timer, "encode"):
+                req = pb.ModelInferRequest(model_name=ch.model_name, model_version=ch.model_version, id=str(i))
+                t = req.inputs.add(name=self.input_name, datatype=self.dtype, shape=list(in_shape))
+                shm_params(t, region.key, k * slot, int(np.prod(in_shape)) * np.dtype(in_dt).itemsize)
+                for n, o, b in layout:
+                    shm_params(req.outputs.add(name=n), region.key, k * slot + o, b)
+                raw = req.SerializeToString()
+            inflight.append((i, k, xf, ch._grpc_stub.ModelInferRaw.future(raw, timeout=ch.timeout_s)))
+        while inflight:
+            finish()
+        return res
+
     def _extract(self, resp) -> np.ndarray:
         kw = {"conf_thres": self.conf_thres}
         if "iou_thres" in self.post.extract_boxes.__code__.co_varnames:
@@ -691,6 +795,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
         from ..utils.trace import trace_range
         timer = getattr(self, "timer", None)
+        if self.wire == "shm":
+            return self._detect_shm(frames)
         if self.wire == "raw" and self.mode != "stream":
             # prepare + encode frame by frame: the staging buffer is reused, each
             # request's bytes are complete before the next frame is prepared
@@ -778,11 +884,84 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
             resps = self._send(raws)
         return keep, resps
 
+    def _detect_gpu_shm(self, clouds) -> Tuple[List[int], list]:
+        """Voxelise on the GPU, copy the voxel tensors from pinned staging into a
+        slot of the client's shared-memory region and send only the region
+        references (KServe system shared memory); detections return as raw
+        outputs (variable-size)."""
+        from ..channel.shm import ShmRegion, shm_params
+        from ..channel.wire import parse_response
+        from ..proto import service_pb2 as pb
+
+        timer = getattr(self, "timer", None)
+        ch = self.channel
+        keys = [_voxel_key(spec["name"], k) for k, spec in enumerate(self.inputs)]
+        dts = {key: spec["dtype"] for key, spec in zip(keys, self.inputs)}
+        keep, resps, inflight = [], [], []
+        free = list(range(self.window))
+
+        def finish():
+            j, k, fut = inflight.pop(0)
+            with _stage(timer, "rpc"):
+                resps.append((j, parse_response(fut.result())))
+            free.append(k)
+
+        for i, c in enumerate(clouds):
+            with _stage(timer, "preprocess"):
+                d = self.pre.filter_cloud_gpu(c, self.normalize, self.z_offset, dts)
+            if d["voxels"].shape[0] == 0:
+                continue
+            if getattr(self, "_shm", None) is None:  # slot layout from the model's voxel budget
+                vm = int(self.pre.cfg.max_voxels)
+                lay, off = [], 0
+                for key in keys:
+                    b = vm * int(np.prod(d[key].shape[1:], dtype=np.int64)) * d[key].dtype.itemsize
+                    lay.append((key, off, b))
+                    off += (b + 4095) // 4096 * 4096
+                region = ShmRegion(off * self.window)
+                ch.register_system_shared_memory(region.key, region.key, region.byte_size)
+                self._shm = (region, off, lay)
+            region, slot, lay = self._shm
+            if not free:
+                finish()
+            k = free.pop(0)
+            with _stage(timer, "encode"):
+                req = pb.ModelInferRequest(model_name=ch.model_name, model_version=ch.model_version, id=str(i))
+                for (key, o, b), spec in zip(lay, self.inputs):
+                    a = np.asarray(d[key])
+                    if a.nbytes > b:
+                        raise ValueError(f"{key}: {a.nbytes} bytes exceed the {b}-byte shared memory slot")
+                    np.copyto(region.view(k * slot + o, a.dtype, a.shape), a)
+                    t = req.inputs.add(name=spec["name"], datatype=spec["dtype"], shape=list(a.shape))
+                    shm_params(t, region.key, k * slot + o, a.nbytes)
+                for n in self.out_names:
+                    req.outputs.add(name=n)
+                raw = req.SerializeToString()
+            inflight.append((i, k, ch._grpc_stub.ModelInferRaw.future(raw, timeout=ch.timeout_s)))
+            keep.append(i)
+        while inflight:
+            finish()
+        order = {j: r for j, r in resps}
+        return keep, [order[j] for j in keep]
+
+    def close_shm(self) -> None:
+        st = getattr(self, "_shm", None)
+        if st is not None:
+            try:
+                self.channel.unregister_system_shared_memory(st[0].key)
+            finally:
+                st[0].close()
+                self._shm = None
+
     def detect(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
         from ..ros.compat import cloud_to_numpy
 
-        if (self.wire == "raw" and self.mode != "stream" and getattr(self.pre, "device", None) is not None
-                and self.pre.device.type == "cuda" and hasattr(self.pre, "filter_cloud_gpu")):
+        gpu_pre = (getattr(self.pre, "device", None) is not None and self.pre.device.type == "cuda"
+                   and hasattr(self.pre, "filter_cloud_gpu"))
+        if self.wire == "shm" and gpu_pre:
+            keep, resps = self._detect_gpu_shm(clouds)
+            return self._outputs(clouds, keep, resps)
+        if self.wire == "raw" and self.mode != "stream" and gpu_pre:
             keep, resps = self._detect_gpu_raw(clouds)
             return self._outputs(clouds, keep, resps)
         batches, empty = [], []

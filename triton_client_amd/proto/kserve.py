@@ -302,6 +302,30 @@ def _service_file() -> descriptor_pb2.FileDescriptorProto:
     add(name="RepositoryModelLoadResponse")
     add(name="RepositoryModelUnloadResponse")
 
+    # system shared-memory extension (Triton grpc_service.proto SystemSharedMemory*)
+    m = add(name="SystemSharedMemoryStatusRequest")
+    _field(m, "name", 1, T_STRING)
+    m = add(name="SystemSharedMemoryStatusResponse")
+    rs = m.nested_type.add(name="RegionStatus")
+    _field(rs, "name", 1, T_STRING)
+    _field(rs, "key", 2, T_STRING)
+    _field(rs, "offset", 3, T_UINT64)
+    _field(rs, "byte_size", 4, T_UINT64)
+    e = m.nested_type.add(name="RegionsEntry")
+    e.options.map_entry = True
+    _field(e, "key", 1, T_STRING)
+    _field(e, "value", 2, T_MSG, type_name="SystemSharedMemoryStatusResponse.RegionStatus")
+    _field(m, "regions", 1, T_MSG, REP, type_name="SystemSharedMemoryStatusResponse.RegionsEntry")
+    m = add(name="SystemSharedMemoryRegisterRequest")
+    _field(m, "name", 1, T_STRING)
+    _field(m, "key", 2, T_STRING)
+    _field(m, "offset", 3, T_UINT64)
+    _field(m, "byte_size", 4, T_UINT64)
+    add(name="SystemSharedMemoryRegisterResponse")
+    m = add(name="SystemSharedMemoryUnregisterRequest")
+    _field(m, "name", 1, T_STRING)
+    add(name="SystemSharedMemoryUnregisterResponse")
+
     svc = fd.service.add(name="GRPCInferenceService")
     for rpc, req, resp, cs, ss in SERVICE_METHODS:
         mth = svc.method.add(name=rpc, input_type=f".{PKG}.{req}", output_type=f".{PKG}.{resp}")
@@ -324,6 +348,11 @@ SERVICE_METHODS = [
     ("RepositoryIndex", "RepositoryIndexRequest", "RepositoryIndexResponse", False, False),
     ("RepositoryModelLoad", "RepositoryModelLoadRequest", "RepositoryModelLoadResponse", False, False),
     ("RepositoryModelUnload", "RepositoryModelUnloadRequest", "RepositoryModelUnloadResponse", False, False),
+    ("SystemSharedMemoryStatus", "SystemSharedMemoryStatusRequest", "SystemSharedMemoryStatusResponse", False, False),
+    ("SystemSharedMemoryRegister", "SystemSharedMemoryRegisterRequest", "SystemSharedMemoryRegisterResponse", False,
+     False),
+    ("SystemSharedMemoryUnregister", "SystemSharedMemoryUnregisterRequest", "SystemSharedMemoryUnregisterResponse",
+     False, False),
 ]
 
 

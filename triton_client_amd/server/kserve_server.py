@@ -61,11 +61,28 @@ def _kserve_dtype(a: np.ndarray) -> str:
     return NP_TO_KSERVE[str(a.dtype)]
 
 
-def decode_inputs(req) -> Dict[str, np.ndarray]:
+def decode_inputs(req, shm=None) -> Dict[str, np.ndarray]:
+    """Inputs of a protobuf ModelInferRequest: shared-memory references become
+    views of the registered region, raw contents views of the message (raw
+    contents are indexed over the inputs that carry no region), else the
+    typed contents."""
+    from .shm import tensor_shm
     out = {}
     raw = list(req.raw_input_contents)
-    for i, t in enumerate(req.inputs):
+    k = 0
+    for t in req.inputs:
         shape = tuple(int(s) for s in t.shape)
+        ref = tensor_shm(t.parameters)
+        if ref is not None:
+            if shm is None:
+                raise InferError("shared memory inputs are not supported by this server")
+            region, off, nbytes = ref
+            dt = _np_dtype(t.datatype)
+            if nbytes != int(np.prod(shape)) * dt.itemsize:
+                raise InferError(f"input '{t.name}': {nbytes} shared memory bytes do not match shape {list(shape)}")
+            out[t.name] = shm.get(region).view(off, nbytes, dt, shape)
+            continue
+        i, k = k, k + 1
         if i < len(raw) and raw:
             a = np.frombuffer(raw[i], dtype=_np_dtype(t.datatype))
         else:  # typed contents
@@ -82,9 +99,14 @@ def decode_inputs(req) -> Dict[str, np.ndarray]:
     return out
 
 
-def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], corrupt: bool = False):
+def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], corrupt: bool = False, shm=None):
+    """Protobuf response; an output requested into a shared-memory region is
+    written there and answered with its shape / datatype (and the region
+    parameters) but no raw contents, as Triton does."""
+    from .shm import tensor_shm
     resp = pb.ModelInferResponse(model_name=model.name, model_version=model.version, id=req.id)
     names = [o.name for o in req.outputs] or list(outputs.keys())
+    params = {o.name: o.parameters for o in req.outputs}
     for n in names:
         if n not in outputs:
             raise InferError(f"unknown output '{n}' for model '{model.name}'")
@@ -92,6 +114,22 @@ def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], cor
         a = np.ascontiguousarray(a.numpy() if hasattr(a, "numpy") and not isinstance(a, np.ndarray) else a)
         t = resp.outputs.add(name=n, datatype=_kserve_dtype(a))
         t.shape.extend(a.shape)
+        ref = tensor_shm(params[n]) if n in params else None
+        if ref is not None:
+            if shm is None:
+                raise InferError("shared memory outputs are not supported by this server")
+            region, off, nbytes = ref
+            if a.nbytes > nbytes:
+                raise InferError(f"output '{n}': {a.nbytes} bytes exceed the {nbytes}-byte shared memory slice")
+            dst = shm.get(region).view(off, a.nbytes, a.dtype, a.shape)
+            if corrupt:
+                dst.fill(0)
+            else:
+                np.copyto(dst, a)
+            for key in ("shared_memory_region", "shared_memory_offset", "shared_memory_byte_size"):
+                if key in params[n]:
+                    t.parameters[key].CopyFrom(params[n][key])
+            continue
         b = a.tobytes()
         if corrupt and len(b):
             b = bytes(len(b))  # zeroed payload: detectable by clients, keeps the shape contract
@@ -106,6 +144,8 @@ class GRPCInferenceServicer:
         self.fault = fault or FaultInjector()
         self.metrics = metrics
         self.server_name, self.version = server_name, version
+        from .shm import SharedMemoryRegistry
+        self.shm = SharedMemoryRegistry()
 
     # -------------------------------------------------------------- health / metadata
     def ServerLive(self, req, ctx):
@@ -121,7 +161,7 @@ class GRPCInferenceServicer:
     def ServerMetadata(self, req, ctx):
         return pb.ServerMetadataResponse(name=self.server_name, version=self.version,
                                          extensions=["classification", "model_repository", "statistics",
-                                                     "binary_tensor_data", "schedule_policy"])
+                                                     "binary_tensor_data", "schedule_policy", "system_shared_memory"])
 
     def _model(self, name, version, ctx) -> ServedModel:
         m = self.repo.get(name, version)
@@ -178,10 +218,10 @@ class GRPCInferenceServicer:
         if self.fault.roll(self.fault.drop_rate):
             ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
         try:
-            inputs = decode_inputs(req)
+            inputs = decode_inputs(req, self.shm)
             corrupt = self.fault.roll(self.fault.corrupt_rate)
             resp = m(inputs, [o.name for o in req.outputs],
-                     encode=lambda outputs: encode_response(m, req, outputs, corrupt=corrupt))
+                     encode=lambda outputs: encode_response(m, req, outputs, corrupt=corrupt, shm=self.shm))
         except InferError as e:
             if self.metrics:
                 self.metrics.request(m.name, False, time.perf_counter() - t0)
@@ -192,6 +232,29 @@ class GRPCInferenceServicer:
 
     def ModelInfer(self, req, ctx):
         return self._infer(req, ctx)
+
+    # ------------------------------------------------- system shared memory
+    def SystemSharedMemoryStatus(self, req, ctx):
+        resp = pb.SystemSharedMemoryStatusResponse()
+        try:
+            regions = self.shm.status(req.name)
+        except InferError as e:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
+        for r in regions:
+            st = resp.regions[r.name]
+            st.name, st.key, st.offset, st.byte_size = r.name, r.key, r.offset, r.byte_size
+        return resp
+
+    def SystemSharedMemoryRegister(self, req, ctx):
+        try:
+            self.shm.register(req.name, req.key, int(req.offset), int(req.byte_size))
+        except InferError as e:
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        return pb.SystemSharedMemoryRegisterResponse()
+
+    def SystemSharedMemoryUnregister(self, req, ctx):
+        self.shm.unregister(req.name)
+        return pb.SystemSharedMemoryUnregisterResponse()
 
     def ModelInferBytes(self, data: bytes, ctx) -> bytes:
         """ModelInfer on the raw wire bytes through the C++ codec: inputs are
@@ -205,6 +268,8 @@ class GRPCInferenceServicer:
             req = parse_request(data)
         except ValueError as e:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        if req.has_params:  # shared-memory references: a small message, the protobuf path reads them
+            return self._infer(pb.ModelInferRequest.FromString(data), ctx).SerializeToString()
         m = self._model(req.model_name, req.model_version, ctx)
         if self.fault.delay_s:
             time.sleep(self.fault.delay_s)
