@@ -56,8 +56,9 @@ def add_framework_flags(p: argparse.ArgumentParser, params_default: str, three_d
                         "re-published in header.seq order); 1 = the reference's one frame per callback")
     g.add_argument("--live-workers", type=int, default=1,
                    help="live topic: micro-batches in flight (host work of one overlaps another's GPU work)")
-    g.add_argument("--wire", choices=["raw", "proto"], default="raw",
-                   help="raw: C++ zero-copy KServe codec; proto: reference-style protobuf request")
+    g.add_argument("--wire", choices=["raw", "proto", "shm"], default="raw",
+                   help="raw: C++ zero-copy KServe codec; proto: reference-style protobuf request; shm: KServe "
+                        "system shared memory (server on the same host; tensors stay in a /dev/shm region)")
     g.add_argument("--timeout", type=float, default=None, help="per-RPC deadline (s); default none")
     g.add_argument("--retries", type=int, default=2, help="retries on UNAVAILABLE/DEADLINE_EXCEEDED")
     g.add_argument("--weights", default=None, help="state_dict for the local engine: path, file://, http(s):// or s3:// URI (loaded with torch.load weights_only)")
