@@ -355,10 +355,21 @@ def main():
     if args.comm == "native" and info.world > 1 and not gloo_rehearsal:
         from triton_client_amd.parallel.rccl import NativeComm
 
-        native = NativeComm.from_info(info)
-        rccl_ranks = native.count()
-        comm_used = "native"
-    elif info.world > 1:
+        try:
+            native = NativeComm.from_info(info)
+            rccl_ranks = native.count()
+            comm_used = "native"
+        except Exception as e:  # noqa: BLE001 - the process group's own RCCL communicator still serves
+            print(f"[bench] rank {info.rank}: native RCCL communicator unavailable ({e}); "
+                  f"using torch.distributed p2p", file=sys.stderr, flush=True)
+            native = None
+        import torch.distributed as dist
+        ok = torch.tensor([1 if native is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same path
+        if int(ok.item()) == 0:
+            native = None
+            comm_used = "torch"
+    if native is None and info.world > 1:
         import torch.distributed as dist
         rccl_ranks = dist.get_world_size() if dist.get_backend() == "nccl" else 0
     if info.world > 1 and not gloo_rehearsal and rccl_ranks != args.gpus:
