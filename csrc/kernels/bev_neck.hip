@@ -504,8 +504,12 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
     issue(0);
     if (Y_STAGES == 3 && total > 1) nxt = issue(1);
   }
-  int c_k = 0, c_br = 0, c_kc = 0;
-  for (int g = 0; g < total; ++g) {
+  // compute side: nested loops (tile -> branch -> deconv K steps, head steps), each with
+  // one latch, so the accumulators stay in fixed registers (a flat step state machine
+  // made hipcc copy every accumulator back at each of its loop latches); the DMA side
+  // walks the same flat sequence one step ahead through begin_step()
+  int g = 0;
+  auto begin_step = [&]() -> const unsigned char* {
     const int cur = g % Y_STAGES;
     if constexpr (Y_STAGES == 3) wait_vm_rt<T>(nxt);
     else wait_vm<0>();
@@ -518,45 +522,69 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
     } else {
       nxt = 0;
     }
-
-    const unsigned char* sa = smem + cur * Y_STAGE;
-    const unsigned char* sb = sa + Y_A_BYTES;
-    const int nkc = a.cin[c_br] / 32;
-    if (c_kc < nkc) {
-      // ---- deconv K step: 2 x 8 fragment pairs, three MFMAs each
-      bf16x8 ah[Y_FM], al[Y_FM];
+    ++g;
+    return smem + cur * Y_STAGE;
+  };
+  auto head_chunk = [&](auto QC, const unsigned char* whb) {
+    constexpr int q = decltype(QC)::value;  // static register indices (a runtime index would spill acc1)
+    bf16x8 xh[Y_FM], xl[Y_FM];
 #pragma unroll
-      for (int i = 0; i < Y_FM; ++i) {
-        const int r = wid * 16 * Y_FM + i * 16 + fr;
-        if constexpr (PAIR) {
-          ah[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
-          al[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
-        } else {
-          const float4 x0 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
-          const float4 x1 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
-          split8(x0, x1, ah[i], al[i]);
+    for (int i = 0; i < Y_FM; ++i) {
+      const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];
+      split8(make_float4(p0[0], p0[1], p0[2], p0[3]), make_float4(p1[0], p1[1], p1[2], p1[3]), xh[i], xl[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < NH / 16; ++u) {
+      const int h = u * 16 + fr;
+      const bf16x8 wh_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq) ^ swz3(h)) << 4));
+      const bf16x8 wl_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq + 1) ^ swz3(h)) << 4));
+#pragma unroll
+      for (int i = 0; i < Y_FM; ++i) mfma3(acc2[i][u], wh_, wl_, xh[i], xl[i]);
+    }
+  };
+  for (int c_k = 0; c_k < my_tiles; ++c_k) {
+    for (int c_br = 0; c_br < a.nbr; ++c_br) {
+      const int nkc = a.cin[c_br] / 32;
+      const unsigned char* last = smem;
+      for (int c_kc = 0; c_kc < nkc; ++c_kc) {
+        // ---- deconv K step: 2 x 8 fragment pairs, three MFMAs each
+        const unsigned char* sa = begin_step();
+        const unsigned char* sb = sa + Y_A_BYTES;
+        last = sa;
+        bf16x8 ah[Y_FM], al[Y_FM];
+#pragma unroll
+        for (int i = 0; i < Y_FM; ++i) {
+          const int r = wid * 16 * Y_FM + i * 16 + fr;
+          if constexpr (PAIR) {
+            ah[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+            al[i] = *reinterpret_cast<const bf16x8*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+          } else {
+            const float4 x0 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+            const float4 x1 = *reinterpret_cast<const float4*>(sa + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+            split8(x0, x1, ah[i], al[i]);
+          }
         }
-      }
-      __builtin_amdgcn_s_setprio(1);
-      // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the VGPRs) to half the tile
+        __builtin_amdgcn_s_setprio(1);
+        // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the VGPRs) to half the tile
 #pragma unroll
-      for (int jh = 0; jh < 2; ++jh) {
-        bf16x8 wh_[4], wl_[4];
+        for (int jh = 0; jh < 2; ++jh) {
+          bf16x8 wh_[4], wl_[4];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int r = (jh * 4 + jj) * 16 + fr;
-          wh_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
-          wl_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+          for (int jj = 0; jj < 4; ++jj) {
+            const int r = (jh * 4 + jj) * 16 + fr;
+            wh_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
+            wl_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
+          }
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int i = 0; i < Y_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
+          __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-          for (int i = 0; i < Y_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
-        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
       }
-      __builtin_amdgcn_s_setprio(0);
-      if (c_kc == nkc - 1) {  // branch GEMM done: bias + ReLU (this stage carries the biases)
-        const float* bias = reinterpret_cast<const float*>(sb + Y_B_BYTES);
+      {  // branch GEMM done: bias + ReLU from the last deconv stage (not refilled before the next step)
+        const float* bias = reinterpret_cast<const float*>(last + Y_A_BYTES + Y_B_BYTES);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
@@ -569,46 +597,29 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
           }
         }
       }
-      ++c_kc;
-      continue;
-    }
-    // ---- head step t: branch channels 64t..64t+63 (acc1[.][4t .. 4t+3]) x 80 head rows
-    auto head_chunk = [&](auto QC, const unsigned char* whb) {
-      constexpr int q = decltype(QC)::value;  // static register indices (a runtime index would spill acc1)
-      bf16x8 xh[Y_FM], xl[Y_FM];
-#pragma unroll
-      for (int i = 0; i < Y_FM; ++i) {
-        const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];
-        split8(make_float4(p0[0], p0[1], p0[2], p0[3]), make_float4(p1[0], p1[1], p1[2], p1[3]), xh[i], xl[i]);
+      // ---- head steps: branch channels 64t..64t+63 (acc1[.][4t .. 4t+3]) x 80 head rows
+      static_assert(Y_HEAD_STEPS == 2, "head steps unrolled below");
+      {
+        const unsigned char* sa = begin_step();
+        __builtin_amdgcn_s_setprio(1);
+        head_chunk(IC<0>{}, sa);
+        __builtin_amdgcn_sched_barrier(0);
+        head_chunk(IC<1>{}, sa + NH * X_ROWB);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      {
+        const unsigned char* sa = begin_step();
+        __builtin_amdgcn_s_setprio(1);
+        head_chunk(IC<2>{}, sa);
+        __builtin_amdgcn_sched_barrier(0);
+        head_chunk(IC<3>{}, sa + NH * X_ROWB);
+        __builtin_amdgcn_s_setprio(0);
       }
 #pragma unroll
-      for (int u = 0; u < NH / 16; ++u) {
-        const int h = u * 16 + fr;
-        const bf16x8 wh_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq) ^ swz3(h)) << 4));
-        const bf16x8 wl_ = *reinterpret_cast<const bf16x8*>(whb + h * X_ROWB + (((2 * fq + 1) ^ swz3(h)) << 4));
+      for (int i = 0; i < Y_FM; ++i)
 #pragma unroll
-        for (int i = 0; i < Y_FM; ++i) mfma3(acc2[i][u], wh_, wl_, xh[i], xl[i]);
-      }
-    };
-    __builtin_amdgcn_s_setprio(1);
-    if (c_kc == nkc) {
-      head_chunk(IC<0>{}, sa);
-      __builtin_amdgcn_sched_barrier(0);
-      head_chunk(IC<1>{}, sa + NH * X_ROWB);
-    } else {
-      head_chunk(IC<2>{}, sa);
-      __builtin_amdgcn_sched_barrier(0);
-      head_chunk(IC<3>{}, sa + NH * X_ROWB);
+        for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    __builtin_amdgcn_s_setprio(0);
-    if (++c_kc != nkc + Y_HEAD_STEPS) continue;
-    c_kc = 0;
-#pragma unroll
-    for (int i = 0; i < Y_FM; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (++c_br != a.nbr) continue;
-    c_br = 0;
     {  // ---- tile done: head bias, fp32 store (lane: pixel fr, head rows 16u + 4fq .. +3)
       const int ct = t_lo + slot + c_k * nslot;
       const int cls = ct % ncls, pt = ct / ncls, cy = cls / S, cx = cls - cy * S;
@@ -637,7 +648,6 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
         for (int u = 0; u < NH / 16; ++u) acc2[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    ++c_k;
   }
   wait_vm<0>();  // no LDS DMA may outlive the workgroup (a tile-less workgroup still loaded the head bias)
 }
