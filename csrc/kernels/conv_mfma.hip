@@ -1630,7 +1630,7 @@ bool xb_ok(const ConvArgs& a) {
 
 template <bool PAIR_OUT>
 int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
-  if (tile >= 70 && !xb_ok(a)) return (int)hipErrorInvalidValue;
+  if (tile >= 68 && !xb_ok(a)) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 70: return launch_xb<128, 128, 2, 4, 2, PAIR_OUT>(a, stream);
     case 71: return launch_xb<256, 64, 4, 2, 2, PAIR_OUT>(a, stream);
@@ -1643,6 +1643,9 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     // 4 waves of 64x64: half the LDS fragment reads per MFMA of the 8-wave tiles
     case 78: return launch_xb<128, 128, 2, 2, 2, PAIR_OUT>(a, stream);
     case 79: return launch_xb<256, 64, 4, 1, 2, PAIR_OUT>(a, stream);
+    // one wave column: every wave reads the whole B tile, A fragments split over 8 waves
+    case 68: return launch_xb<256, 64, 8, 1, 2, PAIR_OUT>(a, stream);
+    case 69: return launch_xb<128, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 22: return launch_glds_x3<128, 64, 4, 2, 2, true, PAIR_OUT>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4, 2, true, PAIR_OUT>(a, stream);

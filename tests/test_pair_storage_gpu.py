@@ -47,7 +47,7 @@ def test_conv_pair_vs_fp64(cuda, tile, out_pair):
     assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
 
 
-XB_TWINS = [(70, 25), (71, 26), (72, 32), (73, 20), (74, 25), (75, 26), (76, 37), (77, 22), (78, 70), (79, 71)]
+XB_TWINS = [(70, 25), (71, 26), (72, 32), (73, 20), (74, 25), (75, 26), (76, 37), (77, 22), (78, 70), (79, 71), (68, 42), (69, 41)]
 
 
 @pytest.mark.parametrize("xb,glds", XB_TWINS)
