@@ -1789,6 +1789,8 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
     case 85: return launch_xb<64, 128, 2, 4, 2, false, false>(a, stream);   // 24
     case 86: return launch_xb<256, 64, 8, 1, 2, false, false>(a, stream);   // 42
     case 87: return launch_xb<64, 64, 4, 1, 2, false, false>(a, stream);    // 47
+    case 88: return launch_xb<128, 32, 4, 1, 2, false, false>(a, stream);   // N <= 32
+    case 89: return launch_xb<256, 32, 4, 1, 2, false, false>(a, stream);   // N <= 32
     case 20: return launch_glds_x3<128, 128, 4, 2>(a, stream);
     case 22: return launch_glds_x3<128, 64, 4, 2>(a, stream);
     case 24: return launch_glds_x3<64, 128, 2, 4>(a, stream);
