@@ -53,6 +53,9 @@ struct ConvArgs {
   const float* in_f;
   const float* res_f;
   float* out_f;
+  // xb kernels with OCC: uint8 [B, H, W] input-pixel occupancy; a pixel marked 0 is
+  // read as zeros through the descriptor range check (no memory traffic)
+  const uint8_t* occ;
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -1324,7 +1327,7 @@ __device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsr
 
 constexpr unsigned kOutOfRange = 0x80000000u;  // >= any num_records the launcher accepts (< 2^31)
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT, bool PAIR_IN = true>
+template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT, bool PAIR_IN = true, bool OCC = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
   static_assert(STAGES >= 2 && STAGES <= 4, "stages");
   constexpr int NW = WM * WN;
@@ -1355,15 +1358,28 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
 
   const int lrow = lane >> 3, lslot = lane & 7;
   int a_base[A_INS], a_iy0[A_INS], a_ix0[A_INS];  // element offset of the row's tap-(0,0) pixel + slot
+  unsigned a_occ[A_INS];                          // OCC: bit ky*KW+kx set when that tap's pixel is occupied
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = (wid * A_INS + j) * 8 + lrow;
     const int m = m0 + row;
+    a_occ[j] = ~0u;
     if (m < a.M) {
       const int ox = m % a.Wo, t = m / a.Wo, oy = t % a.Ho, b = t / a.Ho;
       a_iy0[j] = oy * a.S - a.P;
       a_ix0[j] = ox * a.S - a.P;
       a_base[j] = ((b * a.H + a_iy0[j]) * a.W + a_ix0[j]) * a.ldi + a.ci_off + (lslot ^ swzp(row)) * 4;
+      if constexpr (OCC) {  // once per tile, before any DMA is in flight
+        unsigned msk = 0;
+        for (int ky = 0; ky < a.KH; ++ky)
+          for (int kx = 0; kx < a.KW; ++kx) {
+            const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
+            if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W &&
+                a.occ[((long)b * a.H + iy) * a.W + ix])
+              msk |= 1u << (ky * a.KW + kx);
+          }
+        a_occ[j] = msk;
+      }
     } else {
       a_iy0[j] = -(1 << 28);
       a_ix0[j] = 0;
@@ -1382,7 +1398,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
       const int iy = a_iy0[j] + ky, ix = a_ix0[j] + kx;
-      const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+      if constexpr (OCC) ok = ok && ((a_occ[j] >> (ky * a.KW + kx)) & 1u);
       a_off[j] = ok ? (unsigned)(a_base[j] + (ky * a.W + kx) * a.ldi) * 4u : kOutOfRange;
     }
   };
@@ -1619,6 +1636,12 @@ int launch_glds_x3(const ConvArgs& a, hipStream_t stream) {
 template <int BM, int BN, int WM, int WN, int STAGES, bool PAIR_OUT, bool PAIR_IN = true>
 int launch_xb(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  if constexpr (PAIR_IN) {
+    if (a.occ) {
+      conv_xb_kernel<BM, BN, WM, WN, STAGES, PAIR_OUT, true, true><<<nwg, WM * WN * 64, 0, stream>>>(a);
+      return (int)hipGetLastError();
+    }
+  }
   conv_xb_kernel<BM, BN, WM, WN, STAGES, PAIR_OUT, PAIR_IN><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
@@ -1686,7 +1709,7 @@ TCA_API int tca_conv_nhwc(const void* in, int B, int H, int W, int Cin, int ldi,
   a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
   a.N = N; a.K = KH * KW * Cin; a.Kp = Kp; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off;
   a.act = act; a.shuffle = shuffle; a.M = B * Ho * Wo;
-  a.in_f = nullptr; a.res_f = nullptr; a.out_f = nullptr;
+  a.in_f = nullptr; a.res_f = nullptr; a.out_f = nullptr; a.occ = nullptr;
   if (a.K > Kp) return (int)hipErrorInvalidValue;
   // tile: 0 = auto
   // measured on MI355X (tools/bench_conv.py): 128x32 for N<=32, 128x64 for N<=64, 64x128 above
@@ -1760,7 +1783,7 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   ConvArgs a;
   a.in = nullptr; a.res = nullptr; a.out = nullptr;
-  a.in_f = in; a.res_f = res; a.out_f = out;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.occ = nullptr;
   a.w = (const __hip_bfloat16*)w; a.bias = bias;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off;
   a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
@@ -1829,17 +1852,18 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
 // `out` pairs when out_pair, else fp32.  Same slice / residual / pixel-shuffle
 // contract as tca_conv_nhwc_x3; the global_load_lds kernels only (Cin % 32 == 0,
 // Kp == K).  tile: 0 auto, else one of 20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42 (glds) or 70-77 (xb).
-TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
+namespace {
+int conv_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
                               const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
                               int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
-                              int tile, int out_pair, hipStream_t stream) {
+                              int tile, int out_pair, const uint8_t* occ, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((Cin & 7) || (ldi & 7) || (ci_off & 7) || (N & 7) || (ldo & 7) || (co_off & 7) || (Kp & 31)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7) || !out_pair)) return (int)hipErrorInvalidValue;
   if (shuffle > 0 && ((N / (shuffle * shuffle)) & 7)) return (int)hipErrorInvalidValue;
   ConvArgs a;
   a.in = nullptr; a.res = nullptr; a.out = nullptr;
-  a.in_f = in; a.res_f = res; a.out_f = out;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.occ = KH * KW <= 32 ? occ : nullptr;
   a.w = (const __hip_bfloat16*)w; a.bias = bias;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off;
   a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.S = S; a.P = P;
@@ -1855,4 +1879,27 @@ TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int
   if (tile == 0 && xb_ok(a)) tile = N <= 64 ? (S == 1 ? 71 : 77) : (S == 1 ? 70 : 73);
   if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
+}
+}  // namespace
+
+TCA_API int tca_conv_nhwc_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w,
+                              const float* bias, int N, int KH, int KW, int S, int P, int Kp, float* out, int Ho,
+                              int Wo, int ldo, int co_off, int act, const float* res, int ldr, int r_off, int shuffle,
+                              int tile, int out_pair, hipStream_t stream) {
+  return conv_x3p(in, B, H, W, Cin, ldi, ci_off, w, bias, N, KH, KW, S, P, Kp, out, Ho, Wo, ldo, co_off, act, res, ldr,
+                  r_off, shuffle, tile, out_pair, nullptr, stream);
+}
+
+// Same with an input-pixel occupancy map occ (uint8 [B, H, W]; the pillar scatter's,
+// tca_pillar_vfe_*_occ): the xb kernels read a pixel marked 0 as zeros without touching
+// memory (the descriptor range check), which for a sparse BEV canvas (a few % of cells
+// occupied) removes most of the first conv's input traffic.  Bit-identical to the plain
+// call whenever the unmarked pixels hold zeros; the glds tiles ignore occ.
+TCA_API int tca_conv_nhwc_x3p_occ(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off,
+                                  const void* w, const float* bias, int N, int KH, int KW, int S, int P, int Kp,
+                                  float* out, int Ho, int Wo, int ldo, int co_off, int act, const float* res, int ldr,
+                                  int r_off, int shuffle, int tile, int out_pair, const uint8_t* occ,
+                                  hipStream_t stream) {
+  return conv_x3p(in, B, H, W, Cin, ldi, ci_off, w, bias, N, KH, KW, S, P, Kp, out, Ho, Wo, ldo, co_off, act, res, ldr,
+                  r_off, shuffle, tile, out_pair, occ, stream);
 }

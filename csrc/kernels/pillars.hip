@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const float* __restrict__ voxels, const int* __restrict__ num_points,  // materialised source [V][P][4]
     const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P,
     const float* __restrict__ W /*[64][10]*/, const float* __restrict__ bias /*[64]*/, PillarGeom g,
-    CT* __restrict__ canvas, float* __restrict__ feat_out) {
+    CT* __restrict__ canvas, float* __restrict__ feat_out, uint8_t* __restrict__ occ) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -189,6 +189,8 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
       }
     }
     if (feat_out) feat_out[(long)v * 64 + ch] = val;
+    // occupancy byte per written cell: the first BEV conv gates its reads on it
+    if (occ && lane == 0) occ[((long)b * g.ny + co.z) * g.nx + co.w] = 1;
     v = vn;
     vn = vnn;
     idx_n = idx_nn;
@@ -201,7 +203,8 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
 // chunk of a pillar's C channels (C * esize % 16 == 0), frame per grid row.
 __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict__ coords,
                                                            const int* __restrict__ voxel_count, int max_voxels, int nx,
-                                                           int ny, int C, int esize, uint4* __restrict__ canvas) {
+                                                           int ny, int C, int esize, uint4* __restrict__ canvas,
+                                                           uint8_t* __restrict__ occ) {
   const int b = blockIdx.y;
   const int cpp = C * esize >> 4;
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -210,6 +213,7 @@ __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict
   const int* co = coords + ((long)b * max_voxels + vid) * 4;
   const long cell = ((long)b * ny + co[2]) * nx + co[3];
   canvas[cell * cpp + c] = make_uint4(0u, 0u, 0u, 0u);
+  if (occ && c == 0) occ[cell] = 0;
 }
 
 }  // namespace
@@ -219,21 +223,21 @@ template <bool FROM_SLOTS>
 int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
                const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
-               hipStream_t stream) {
+               uint8_t* occ, hipStream_t stream) {
   if (P > 32 || (dt != kBF16 && dt != kF32 && dt != kPair)) return (int)hipErrorInvalidValue;
   if (dt == kF32)
     pillar_vfe_kernel<FROM_SLOTS, float><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
                                                                    num_points, coords, voxel_count, batch, max_voxels,
-                                                                   P, W, bias, g, (float*)canvas, feat_out);
+                                                                   P, W, bias, g, (float*)canvas, feat_out, occ);
   else if (dt == kPair)
     pillar_vfe_kernel<FROM_SLOTS, PairTag><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
                                                                      num_points, coords, voxel_count, batch,
                                                                      max_voxels, P, W, bias, g, (PairTag*)canvas,
-                                                                     feat_out);
+                                                                     feat_out, occ);
   else
     pillar_vfe_kernel<FROM_SLOTS, __hip_bfloat16><<<2048, 256, 0, stream>>>(
         pts, pstride, max_pts, slots, vcount, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias,
-        g, (__hip_bfloat16*)canvas, feat_out);
+        g, (__hip_bfloat16*)canvas, feat_out, occ);
   TCA_LAUNCH_CHECK();
 }
 }  // namespace
@@ -247,7 +251,19 @@ TCA_API int tca_pillar_vfe_slots(const float* pts, int pstride, int max_pts, con
   if (batch <= 0) return 0;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
   return launch_vfe<true>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords, voxel_count, batch,
-                          max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, stream);
+                          max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, nullptr, stream);
+}
+
+// Same, also marking occ[b, y, x] = 1 (uint8 [B, ny, nx]) for every written cell.
+TCA_API int tca_pillar_vfe_slots_occ(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount,
+                                     const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
+                                     const float* W, const float* bias, const float* range, const float* vsize,
+                                     int nx, int ny, void* canvas, float* feat_out, int canvas_dtype, uint8_t* occ,
+                                     hipStream_t stream) {
+  if (batch <= 0) return 0;
+  PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
+  return launch_vfe<true>(pts, pstride, max_pts, slots, vcount, nullptr, nullptr, coords, voxel_count, batch,
+                          max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, occ, stream);
 }
 
 // Server path: source = materialised voxels [B*V][P][4] + num_points (KServe inputs).
@@ -258,16 +274,41 @@ TCA_API int tca_pillar_vfe_voxels(const float* voxels, const int* num_points, co
   if (batch <= 0) return 0;
   PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
   return launch_vfe<false>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords, voxel_count, batch,
-                           max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, stream);
+                           max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, nullptr, stream);
 }
 
-TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
-                                    int ny, int C, void* canvas, int canvas_dtype, hipStream_t stream) {
+TCA_API int tca_pillar_vfe_voxels_occ(const float* voxels, const int* num_points, const int* coords,
+                                      const int* voxel_count, int batch, int max_voxels, int P, const float* W,
+                                      const float* bias, const float* range, const float* vsize, int nx, int ny,
+                                      void* canvas, float* feat_out, int canvas_dtype, uint8_t* occ,
+                                      hipStream_t stream) {
+  if (batch <= 0) return 0;
+  PillarGeom g{range[0], range[1], range[2], vsize[0], vsize[1], vsize[2], nx, ny};
+  return launch_vfe<false>(nullptr, 4, 0, nullptr, nullptr, voxels, num_points, coords, voxel_count, batch,
+                           max_voxels, P, W, bias, g, canvas, feat_out, canvas_dtype, occ, stream);
+}
+
+namespace {
+int canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx, int ny, int C,
+                 void* canvas, int canvas_dtype, uint8_t* occ, hipStream_t stream) {
   if (batch <= 0) return 0;
   const int esize = (canvas_dtype == kF32 || canvas_dtype == kPair) ? 4 : 2;
   if ((C * esize) & 15 || (canvas_dtype != kBF16 && canvas_dtype != kF32 && canvas_dtype != kPair))
     return (int)hipErrorInvalidValue;
   canvas_clear_kernel<<<dim3((max_voxels * (C * esize / 16) + 255) / 256, batch), 256, 0, stream>>>(
-      coords, voxel_count, max_voxels, nx, ny, C, esize, (uint4*)canvas);
+      coords, voxel_count, max_voxels, nx, ny, C, esize, (uint4*)canvas, occ);
   TCA_LAUNCH_CHECK();
+}
+}  // namespace
+
+TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
+                                    int ny, int C, void* canvas, int canvas_dtype, hipStream_t stream) {
+  return canvas_clear(coords, voxel_count, batch, max_voxels, nx, ny, C, canvas, canvas_dtype, nullptr, stream);
+}
+
+// Same, also clearing those cells' occupancy bytes.
+TCA_API int tca_pillar_canvas_clear_occ(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
+                                        int ny, int C, void* canvas, int canvas_dtype, uint8_t* occ,
+                                        hipStream_t stream) {
+  return canvas_clear(coords, voxel_count, batch, max_voxels, nx, ny, C, canvas, canvas_dtype, occ, stream);
 }

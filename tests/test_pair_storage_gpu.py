@@ -170,3 +170,56 @@ def test_lidar_pipeline_uses_pair_canvas(cuda):
     r2 = lid.step()  # pair canvas from the scatter, cleared by cell list
     torch.cuda.synchronize()
     assert torch.equal(n1, r2.count) and int(n1.min()) > 0
+
+
+@pytest.mark.parametrize("tile", [0, 77, 71, 70])
+def test_conv_pair_occupancy_gated_reads(cuda, tile):
+    """tca_conv_nhwc_x3p_occ: pixels marked unoccupied read as zeros through the
+    descriptor range check, so (a) with zeros there the output is bit-identical to
+    the plain call, (b) garbage there is never read."""
+    torch.manual_seed(tile)
+    B, H, W, cin, cout = 2, 40, 36, 64, 128 if tile == 70 else 64
+    s = 2 if tile == 77 else 1
+    conv = nn.Conv2d(cin, cout, 3, s, 1, bias=True)
+    fc = FusedConv(conv, act=1, device=cuda, precision="fp32")
+    occ = (torch.rand(B, H, W) < 0.1).to(torch.uint8)
+    x = torch.randn(B, H, W, cin) * occ[..., None]
+    xz = NHWC(to_pairs(x).to(cuda), pair=True)
+    Ho, Wo = fc.out_hw(H, W)
+    plain = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    fc(xz, out=plain, tile=tile)
+    gated = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    fc(NHWC(xz.t, pair=True, occ=occ.to(cuda)), out=gated, tile=tile)
+    junk = x + torch.randn(B, H, W, cin) * (1 - occ[..., None])  # garbage in every unoccupied cell
+    gj = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    fc(NHWC(to_pairs(junk).to(cuda), pair=True, occ=occ.to(cuda)), out=gj, tile=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(plain.t, gated.t) and torch.equal(plain.t, gj.t)
+
+
+def test_lidar_pipeline_occupancy_matches_ungated(cuda):
+    import numpy as np
+
+    from triton_client_amd.pipelines import LidarPipeline
+    from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    lid = LidarPipeline(batch=2, max_points=32768, device=cuda, z_offset=1.5, precision="fp32")
+    for b in range(2):
+        c = lidar_sweep(spec, 10 + b)
+        raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+        lid.data[b * lid.frame_bytes: b * lid.frame_bytes + raw.numel()].copy_(raw)
+        lid.frame_n[b] = c.shape[0]
+    lid.calibrate_detection_density(500.0)
+    r1 = lid.step()
+    assert lid.enc.occ is not None
+    occ_cells = int(lid.enc.occ.sum())
+    n1, b1 = r1.count.clone(), r1.box.clone()
+    occ, lid.enc.occ = lid.enc.occ, None  # ungated: the first conv reads the whole canvas
+    r2 = lid.step()
+    torch.cuda.synchronize()
+    lid.enc.occ = occ
+    assert occ_cells > 0 and torch.equal(n1, r2.count)
+    for b in range(2):
+        k = int(n1[b])
+        assert torch.equal(b1[b, :k], r2.box[b, :k])

@@ -46,9 +46,13 @@ _KERNEL_SIGS = {
     "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, I, P],
+    "tca_pillar_vfe_slots_occ": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P, P],
+    "tca_pillar_vfe_voxels_occ": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P, P],
+    "tca_pillar_canvas_clear_occ": [P, P, I, I, I, I, I, P, I, P, P],
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3p": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P],
+    "tca_conv_nhwc_x3p_occ": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P],
     "tca_zero_i32": [P, I, P],
     "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],
     "tca_anchor_decode_filter_keyed": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, P, P, P, P, P, P, I,

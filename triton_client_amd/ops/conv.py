@@ -43,6 +43,9 @@ class NHWC:
     off: int = 0
     c: Optional[int] = None
     pair: bool = False
+    # optional uint8 [B, H, W] pixel occupancy (a sparse BEV canvas): pair convs read an
+    # unmarked pixel as zeros without fetching it (conv_mfma.hip tca_conv_nhwc_x3p_occ)
+    occ: Optional[torch.Tensor] = None
 
     def __post_init__(self):
         if self.c is None:
@@ -214,10 +217,15 @@ class FusedConv:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
-            _native.call("tca_conv_nhwc_x3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
-                         _native.ptr(self.w_gemm), _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p,
-                         self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, act, *rp, self.shuffle,
-                         tile if tile in PAIR_TILES else 0, int(out.pair), _native.stream_ptr(stream))
+            args = (_native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off, _native.ptr(self.w_gemm),
+                    _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p, self.Kp, _native.ptr(out.t), gh,
+                    gw, out.t.shape[-1], out.off, act, *rp, self.shuffle, tile if tile in PAIR_TILES else 0,
+                    int(out.pair))
+            if x.occ is not None and not self.transpose:
+                assert x.occ.dtype == torch.uint8 and tuple(x.occ.shape) == (B, H, W), (x.occ.shape, (B, H, W))
+                _native.call("tca_conv_nhwc_x3p_occ", *args, _native.ptr(x.occ), _native.stream_ptr(stream))
+            else:
+                _native.call("tca_conv_nhwc_x3p", *args, _native.stream_ptr(stream))
             return out
         fn = "tca_conv_nhwc_x3" if self.precision == "fp32" else "tca_conv_nhwc"
         _native.call(fn, _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,

@@ -237,6 +237,9 @@ class PillarEncoder:
             self.ws = Workspace(self.device)
             # NHWC canvas, zero-initialised once; cleared per frame by cell list
             self.canvas = self.ws.get("canvas", (batch, ny, nx, channels), dtype, init=0)
+            # pair mode: per-cell occupancy bytes written by the scatter, cleared with the cells;
+            # the first BEV conv skips the reads of unoccupied cells (most of the canvas)
+            self.occ = None
             self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
             self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
 
@@ -248,10 +251,14 @@ class PillarEncoder:
             raise ValueError("pair storage needs the fp32 canvas")
         self.pair = bool(pair)
         self._dt = 5 if pair else (0 if self.dtype == torch.float32 else 2)
+        if self.pair and self.occ is None and self.device.type == "cuda":
+            self.occ = self.ws.get("occ", (self.B, self.ny, self.nx), torch.uint8, init=0)
+            # the canvas was written without occupancy until now: mark nothing, the
+            # first frame after the switch rewrites its cells (and the canvas was cleared by cells)
 
     def canvas_nhwc(self):
         from .conv import NHWC
-        return NHWC(self.canvas, pair=self.pair)
+        return NHWC(self.canvas, pair=self.pair, occ=self.occ if self.pair else None)
 
     def canvas_nchw(self) -> torch.Tensor:
         if self.pair:
@@ -266,26 +273,35 @@ class PillarEncoder:
 
     def clear_coords(self, coords: torch.Tensor, voxel_count: torch.Tensor, stream=None) -> None:
         """coords [B, V, 4] (b, z, y, x), voxel_count [B]."""
-        _native.call("tca_pillar_canvas_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
-                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), self._dt,
-                     _native.stream_ptr(stream))
+        args = (_native.ptr(coords), _native.ptr(voxel_count), coords.shape[0], coords.shape[1], self.nx, self.ny,
+                self.C, _native.ptr(self.canvas), self._dt)
+        if self.occ is not None:
+            _native.call("tca_pillar_canvas_clear_occ", *args, _native.ptr(self.occ), _native.stream_ptr(stream))
+        else:
+            _native.call("tca_pillar_canvas_clear", *args, _native.stream_ptr(stream))
 
     def encode_from_slots(self, points: torch.Tensor, vox: Voxelizer, feat_out: Optional[torch.Tensor] = None,
                           stream=None) -> torch.Tensor:
-        _native.call("tca_pillar_vfe_slots", _native.ptr(points), points.shape[-1], vox.max_points,
-                     _native.ptr(vox.slots), _native.ptr(vox.vcount), _native.ptr(vox.coords),
-                     _native.ptr(vox.voxel_count), self.B, self.cfg.max_voxels, self.cfg.max_points_per_voxel,
-                     _native.ptr(self.W), _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny,
-                     _native.ptr(self.canvas), _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
+        args = (_native.ptr(points), points.shape[-1], vox.max_points, _native.ptr(vox.slots), _native.ptr(vox.vcount),
+                _native.ptr(vox.coords), _native.ptr(vox.voxel_count), self.B, self.cfg.max_voxels,
+                self.cfg.max_points_per_voxel, _native.ptr(self.W), _native.ptr(self.b), self._range, self._vsize,
+                self.nx, self.ny, _native.ptr(self.canvas), _native.ptr(feat_out), self._dt)
+        if self.occ is not None:
+            _native.call("tca_pillar_vfe_slots_occ", *args, _native.ptr(self.occ), _native.stream_ptr(stream))
+        else:
+            _native.call("tca_pillar_vfe_slots", *args, _native.stream_ptr(stream))
         # pair storage: the plan reads the raw buffer; decoding it here would cost a full pass
         return None if self.pair else self.canvas_nchw()
 
     def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
         """voxels [B, V, P, 4], num_points [B, V], coords [B, V, 4], voxel_count [B]."""
-        _native.call("tca_pillar_vfe_voxels", _native.ptr(voxels), _native.ptr(num_points), _native.ptr(coords),
-                     _native.ptr(voxel_count), voxels.shape[0], voxels.shape[1], voxels.shape[2], _native.ptr(self.W),
-                     _native.ptr(self.b), self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas),
-                     _native.ptr(feat_out), self._dt, _native.stream_ptr(stream))
+        args = (_native.ptr(voxels), _native.ptr(num_points), _native.ptr(coords), _native.ptr(voxel_count),
+                voxels.shape[0], voxels.shape[1], voxels.shape[2], _native.ptr(self.W), _native.ptr(self.b),
+                self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas), _native.ptr(feat_out), self._dt)
+        if self.occ is not None:
+            _native.call("tca_pillar_vfe_voxels_occ", *args, _native.ptr(self.occ), _native.stream_ptr(stream))
+        else:
+            _native.call("tca_pillar_vfe_voxels", *args, _native.stream_ptr(stream))
         # pair storage: the plan reads the raw buffer; decoding it here would cost a full pass
         return None if self.pair else self.canvas_nchw()
 
