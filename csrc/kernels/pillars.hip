@@ -44,14 +44,17 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
-template <bool FROM_SLOTS, typename CT>
+template <bool FROM_SLOTS, typename CT, int PFIX = 0>
 __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     const float* __restrict__ pts, int pstride, int max_pts,               // FROM_SLOTS source
     const int* __restrict__ slots, const int* __restrict__ vcount,        // FROM_SLOTS source
     const float* __restrict__ voxels, const int* __restrict__ num_points,  // materialised source [V][P][4]
-    const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P,
+    const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P_arg,
     const float* __restrict__ W /*[64][10]*/, const float* __restrict__ bias /*[64]*/, PillarGeom g,
     CT* __restrict__ canvas, float* __restrict__ feat_out, uint8_t* __restrict__ occ) {
+  // PFIX = 32 (every PointPillars config here): the slot bounds and the per-row
+  // masks of the point max are compile-time
+  const int P = PFIX ? PFIX : P_arg;
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -219,23 +222,41 @@ __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict
 }  // namespace
 
 namespace {
+template <bool FROM_SLOTS, int PFIX>
+int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
+                 const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
+                 const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
+                 uint8_t* occ, hipStream_t stream);
+
 template <bool FROM_SLOTS>
 int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
                const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
                uint8_t* occ, hipStream_t stream) {
   if (P > 32 || (dt != kBF16 && dt != kF32 && dt != kPair)) return (int)hipErrorInvalidValue;
+  if (P == 32) return launch_vfe_t<FROM_SLOTS, 32>(pts, pstride, max_pts, slots, vcount, voxels, num_points, coords,
+                                                    voxel_count, batch, max_voxels, P, W, bias, g, canvas, feat_out,
+                                                    dt, occ, stream);
+  return launch_vfe_t<FROM_SLOTS, 0>(pts, pstride, max_pts, slots, vcount, voxels, num_points, coords, voxel_count,
+                                     batch, max_voxels, P, W, bias, g, canvas, feat_out, dt, occ, stream);
+}
+
+template <bool FROM_SLOTS, int PFIX>
+int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
+                 const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
+                 const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
+                 uint8_t* occ, hipStream_t stream) {
   if (dt == kF32)
-    pillar_vfe_kernel<FROM_SLOTS, float><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
+    pillar_vfe_kernel<FROM_SLOTS, float, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
                                                                    num_points, coords, voxel_count, batch, max_voxels,
                                                                    P, W, bias, g, (float*)canvas, feat_out, occ);
   else if (dt == kPair)
-    pillar_vfe_kernel<FROM_SLOTS, PairTag><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
+    pillar_vfe_kernel<FROM_SLOTS, PairTag, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
                                                                      num_points, coords, voxel_count, batch,
                                                                      max_voxels, P, W, bias, g, (PairTag*)canvas,
                                                                      feat_out, occ);
   else
-    pillar_vfe_kernel<FROM_SLOTS, __hip_bfloat16><<<2048, 256, 0, stream>>>(
+    pillar_vfe_kernel<FROM_SLOTS, __hip_bfloat16, PFIX><<<2048, 256, 0, stream>>>(
         pts, pstride, max_pts, slots, vcount, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias,
         g, (__hip_bfloat16*)canvas, feat_out, occ);
   TCA_LAUNCH_CHECK();
