@@ -193,7 +193,7 @@ def main():
 
         def make_cam(b, m):
             return DetectronPipeline(model=m, batch=b, src_hw=(H0, W0), cfg=DetectronConfig(arch=args.camera_model),
-                                     device=dev)
+                                     device=dev, precision=args.precision)
     else:
         def make_cam(b, m):
             return CameraPipeline(model=m, batch=b, src_hw=(H0, W0), device=dev, precision=args.precision)
@@ -550,8 +550,9 @@ def main():
             "scaling": "weak",
             # BASELINE.json publishes no reference number: nothing to divide by
             "vs_baseline": None,
-            "dtype": args.precision if (args.camera_model == "yolov5n" and args.lidar_model == "pointpillars")
-            else "bf16",
+            # families with an fp32 mode report the mode; the others run bf16 only
+            "dtype": args.precision if (args.camera_model in ("yolov5n", "retinanet", "fcos") or not use_cam)
+            and (args.lidar_model == "pointpillars" or not use_lid) else "bf16",
             "data": (f"synthetic: {nd} distinct {W0}x{H0} "
                      + (f"JPEG (q{args.jpeg_quality}, decoded every step)" if jdec is not None else "uint8 RGB")
                      + f" camera frames + {nd} distinct "

@@ -188,27 +188,56 @@ __global__ void __launch_bounds__(256) segment_merge_kernel(
   if (threadIdx.x == 0) ocount[b] = min(off, cap_out);
 }
 
+// GroupNorm over NHWC slices of bf16 or fp32 activations (fp32 mode): 8 channels per
+// 16-B (bf16) or 2 x 16-B (fp32) vector; statistics and the affine in fp32.
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float (&f)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const __hip_bfloat16* e = reinterpret_cast<const __hip_bfloat16*>(&v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = __bfloat162float(e[k]);
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float (&f)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 v;
+    __hip_bfloat16* e = reinterpret_cast<__hip_bfloat16*>(&v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = __float2bfloat16(f[k]);
+    *reinterpret_cast<uint4*>(p) = v;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
 // GroupNorm stats: one block per (group, image).  C channels, G groups (C/G == 8).
-__global__ void __launch_bounds__(256) gn_stats_kernel(const __hip_bfloat16* __restrict__ x, int HW, int C, int ldc,
-                                                       int c_off, int G, float eps, float* __restrict__ stats) {
+template <typename T>
+__global__ void __launch_bounds__(256) gn_stats_kernel(const T* __restrict__ x, int HW, int C, int ldc, int c_off,
+                                                       int G, float eps, float* __restrict__ stats) {
   const int g = blockIdx.x, b = blockIdx.y;
   const int cg = C / G;
   float s = 0.f, ss = 0.f;
-  const __hip_bfloat16* base = x + (long)b * HW * ldc + c_off + g * cg;
+  const T* base = x + (long)b * HW * ldc + c_off + g * cg;
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
-    const __hip_bfloat16* q = base + (long)p * ldc;
+    const T* q = base + (long)p * ldc;
     if (cg == 8) {
-      const uint4 v = *reinterpret_cast<const uint4*>(q);
-      const __hip_bfloat16* e = reinterpret_cast<const __hip_bfloat16*>(&v);
+      float f[8];
+      load8(q, f);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float f = __bfloat162float(e[k]);
-        s += f;
-        ss += f * f;
+        s += f[k];
+        ss += f[k] * f[k];
       }
     } else {
       for (int k = 0; k < cg; ++k) {
-        const float f = __bfloat162float(q[k]);
+        const float f = to_f32(q[k]);
         s += f;
         ss += f * f;
       }
@@ -231,10 +260,11 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const __hip_bfloat16* __r
   }
 }
 
-__global__ void __launch_bounds__(256) gn_apply_kernel(const __hip_bfloat16* __restrict__ x, int B, int HW, int C,
-                                                       int ldc, int c_off, int G, const float* __restrict__ stats,
+template <typename T>
+__global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, int B, int HW, int C, int ldc,
+                                                       int c_off, int G, const float* __restrict__ stats,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       int relu, __hip_bfloat16* __restrict__ y, int ldy, int y_off) {
+                                                       int relu, T* __restrict__ y, int ldy, int y_off) {
   const unsigned c8 = C / 8;
   const unsigned total = (unsigned)B * HW * c8;  // < 2^31 (host-checked); 32-bit div/mod
   const int cg = C / G;
@@ -242,19 +272,28 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const __hip_bfloat16* __r
     const int cv = (int)(t % c8);
     const unsigned pix = t / c8;
     const int b = (int)(pix / (unsigned)HW);
-    uint4 v = *reinterpret_cast<const uint4*>(x + (long)pix * ldc + c_off + cv * 8);
-    __hip_bfloat16* e = reinterpret_cast<__hip_bfloat16*>(&v);
+    float f[8];
+    load8(x + (long)pix * ldc + c_off + cv * 8, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int ch = cv * 8 + k;
       const int g = ch / cg;
       const float mean = stats[(b * G + g) * 2], rstd = stats[(b * G + g) * 2 + 1];
-      float f = (__bfloat162float(e[k]) - mean) * rstd * gamma[ch] + beta[ch];
-      if (relu) f = fmaxf(f, 0.f);
-      e[k] = __float2bfloat16(f);
+      f[k] = (f[k] - mean) * rstd * gamma[ch] + beta[ch];
+      if (relu) f[k] = fmaxf(f[k], 0.f);
     }
-    *reinterpret_cast<uint4*>(y + (long)pix * ldy + y_off + cv * 8) = v;
+    store8(y + (long)pix * ldy + y_off + cv * 8, f);
   }
+}
+
+template <typename T>
+int group_norm(const void* x, int B, int HW, int C, int ldc, int c_off, int G, float eps, const float* gamma,
+               const float* beta, int relu, float* stats, void* y, int ldy, int y_off, hipStream_t stream) {
+  gn_stats_kernel<T><<<dim3(G, B), 256, 0, stream>>>((const T*)x, HW, C, ldc, c_off, G, eps, stats);
+  const long work = (long)B * HW * (C / 8);
+  gn_apply_kernel<T><<<(int)min((work + 255) / 256, (long)8192), 256, 0, stream>>>(
+      (const T*)x, B, HW, C, ldc, c_off, G, stats, gamma, beta, relu, (T*)y, ldy, y_off);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -323,16 +362,24 @@ TCA_API int tca_segment_merge(const float* box, const float* score, const int* c
   TCA_LAUNCH_CHECK();
 }
 
-// GroupNorm(G) + affine (+ ReLU) over NHWC bf16 [B, H*W, C] slices; y may alias x.
-TCA_API int tca_group_norm_nhwc(const void* x, int B, int HW, int C, int ldc, int c_off, int G, float eps,
-                                const float* gamma, const float* beta, int relu, float* stats, void* y, int ldy,
-                                int y_off, hipStream_t stream) {
+// GroupNorm(G) + affine (+ ReLU) over NHWC [B, H*W, C] slices (dtype kBF16 or kF32); y may alias x.
+TCA_API int tca_group_norm_nhwc_dt(const void* x, int B, int HW, int C, int ldc, int c_off, int G, float eps,
+                                   const float* gamma, const float* beta, int relu, float* stats, void* y, int ldy,
+                                   int y_off, int dtype, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((C % G) || (C & 7) || (ldc & 7) || (c_off & 7) || (ldy & 7) || (y_off & 7)) return (int)hipErrorInvalidValue;
   if ((long)B * HW * (C / 8) >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit index math
-  gn_stats_kernel<<<dim3(G, B), 256, 0, stream>>>((const __hip_bfloat16*)x, HW, C, ldc, c_off, G, eps, stats);
-  const long work = (long)B * HW * (C / 8);
-  gn_apply_kernel<<<(int)min((work + 255) / 256, (long)8192), 256, 0, stream>>>(
-      (const __hip_bfloat16*)x, B, HW, C, ldc, c_off, G, stats, gamma, beta, relu, (__hip_bfloat16*)y, ldy, y_off);
-  TCA_LAUNCH_CHECK();
+  if (dtype == kF32)
+    return group_norm<float>(x, B, HW, C, ldc, c_off, G, eps, gamma, beta, relu, stats, y, ldy, y_off, stream);
+  if (dtype == kBF16)
+    return group_norm<__hip_bfloat16>(x, B, HW, C, ldc, c_off, G, eps, gamma, beta, relu, stats, y, ldy, y_off,
+                                      stream);
+  return (int)hipErrorInvalidValue;
+}
+
+TCA_API int tca_group_norm_nhwc(const void* x, int B, int HW, int C, int ldc, int c_off, int G, float eps,
+                                const float* gamma, const float* beta, int relu, float* stats, void* y, int ldy,
+                                int y_off, hipStream_t stream) {
+  return tca_group_norm_nhwc_dt(x, B, HW, C, ldc, c_off, G, eps, gamma, beta, relu, stats, y, ldy, y_off, kBF16,
+                                stream);
 }

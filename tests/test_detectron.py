@@ -194,3 +194,59 @@ def test_reference_model_repository_families():
         assert type(by["pointpillar_kitti"]).__name__ == "PointPillarsModel"
     finally:
         shutil.rmtree(root)
+
+
+@pytest.mark.gpu
+def test_group_norm_kernel_fp32(cuda):
+    from triton_client_amd.ops.detectron import group_norm_nhwc
+    x = torch.randn(2, 13, 21, 256 + 16) * 3 + 1
+    g, b = torch.rand(256) + 0.5, torch.randn(256) * 0.1
+    xg = x.to(cuda)
+    out = torch.zeros_like(xg)
+    group_norm_nhwc(NHWC(xg, 16, 256), g.to(cuda), b.to(cuda), 32, 1e-5, True, out=NHWC(out, 16, 256))
+    torch.cuda.synchronize()
+    ref = torch.relu(torch.nn.functional.group_norm(x[..., 16:].double().permute(0, 3, 1, 2), 32, g.double(),
+                                                    b.double(), 1e-5))
+    got = out[..., 16:].double().cpu().permute(0, 3, 1, 2)
+    assert (got - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["retinanet", "fcos"])
+def test_fast_detectron_fp32_vs_fp64_module(cuda, arch):
+    """fp32 mode (the reference's libtorch fp32 serving precision): split-product
+    convs, fp32 activations, fp32 GroupNorm, against the fp64 module."""
+    import copy
+
+    from triton_client_amd.models.fast import FastDetectron
+    m = _model(arch)
+    x = torch.rand(2, 3, 128, 160) * 255
+    with torch.no_grad():
+        ref = copy.deepcopy(m).double()(x.double())
+    f = FastDetectron(m, 2, device=cuda, precision="fp32")
+    assert f.x.t.dtype == torch.float32
+    f.x.t.copy_(_fast_inputs(m, x).to(cuda))
+    outs = f.forward()
+    torch.cuda.synchronize()
+    for r, o in zip(ref, outs):
+        for rt, ot in zip(r, o):
+            got = ot.nchw().double().cpu()
+            rel = ((got - rt).norm() / rt.norm().clamp_min(1e-30)).item()
+            assert rel < 1e-4, rel
+
+
+@pytest.mark.gpu
+def test_detectron_pipeline_fp32(cuda):
+    from triton_client_amd.pipelines import DetectronPipeline, GraphRunner
+    from triton_client_amd.utils.synthetic import camera_frame
+    cfg = DetectronConfig(arch="retinanet", input_hw=(256, 384))
+    pipe = DetectronPipeline(batch=2, src_hw=(360, 640), cfg=cfg, device=cuda, precision="fp32")
+    for b in range(2):
+        pipe.frames[b].copy_(torch.from_numpy(camera_frame(360, 640, b)))
+    pipe.calibrate_detection_density(200.0)
+    e = pipe.step().per_image()
+    g = GraphRunner(pipe.step)().per_image()
+    torch.cuda.synchronize()
+    assert all(len(x["score"]) > 0 for x in e)
+    for a, b in zip(e, g):
+        np.testing.assert_array_equal(a["box"], b["box"])

@@ -66,6 +66,7 @@ _KERNEL_SIGS = {
     "tca_fcos_decode": [P, P, P, I, I, I, I, I, I, I, I, I, F, F, F, I, I, P, P, P, P, P, I, I, P],
     "tca_segment_merge": [P, P, P, P, I, I, P, P, I, I, I, P, P, P, P, P, I, P],
     "tca_group_norm_nhwc": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, P],
+    "tca_group_norm_nhwc_dt": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, I, P],
     "tca_yolov4_decode": [P, P, P, I, I, I, P, P, P, F, F, I, I, P, P, P, P, P, P, P, I, P],
     "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, I, P],
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, I, P],

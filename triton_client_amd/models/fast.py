@@ -406,17 +406,21 @@ class FastDetectron:
 
     IN_CHANNELS = 8
 
-    def __init__(self, model, batch: int, device="cuda"):
+    def __init__(self, model, batch: int, device="cuda", precision: str = "bf16"):
+        """precision: "bf16", or "fp32" (the reference serves these networks at fp32:
+        split-product convs, fp32 activations, fp32 GroupNorm / decode)."""
         from ..ops.conv import FusedConv
 
         self.device = torch.device(device)
+        self.precision = precision
         cfg = self.cfg = model.cfg
         B = self.B = batch
         H, W = cfg.input_hw
-        bufs = self.bufs = _Buffers(self.device)
+        bufs = self.bufs = _Buffers(self.device, precision)
         self.x = bufs.new(B, H, W, self.IN_CHANNELS)
         bb = model.backbone
-        self.stem = _fc(bb.stem, device, cin_pad=self.IN_CHANNELS)
+        P = precision
+        self.stem = _fc(bb.stem, device, P, cin_pad=self.IN_CHANNELS)
         h, w = _conv_out(H, 7, 2, 3), _conv_out(W, 7, 2, 3)
         self.stem_out = bufs.new(B, h, w, 64)
         h, w = _conv_out(h, 3, 2, 1), _conv_out(w, 3, 2, 1)
@@ -426,11 +430,11 @@ class FastDetectron:
         for st in bb.stages:
             blocks = []
             for blk in st:
-                c1, c2, c3 = _fc(blk.conv1, device), _fc(blk.conv2, device), blk.conv3
+                c1, c2, c3 = _fc(blk.conv1, device, P), _fc(blk.conv2, device, P), blk.conv3
                 s = blk.conv1.s if blk.conv1.s > 1 else blk.conv2.s
                 ho, wo = _conv_out(h, 1, s, 0), _conv_out(w, 1, s, 0)
-                f3 = FusedConv(c3.conv, act=ACT_RELU, device=device, post_res=True)
-                sc = _fc(blk.shortcut, device) if blk.shortcut is not None else None
+                f3 = FusedConv(c3.conv, act=ACT_RELU, device=device, post_res=True, precision=P)
+                sc = _fc(blk.shortcut, device, P) if blk.shortcut is not None else None
                 t1, t2 = bufs.new(B, ho, wo, c1.N), bufs.new(B, ho, wo, c2.N)
                 sbuf = bufs.new(B, ho, wo, sc.N) if sc is not None else None
                 out = bufs.new(B, ho, wo, f3.N)
@@ -440,16 +444,16 @@ class FastDetectron:
         fpn = model.fpn
         C = cfg.fpn_channels
         self.lv_hw = [blocks[-1][7].shape[1:3] for blocks in self.stages[1:]]  # res3..res5
-        self.lat = [_fc(m, device) for m in fpn.lateral]
-        self.outc = [_fc(m, device) for m in fpn.output]
+        self.lat = [_fc(m, device, P) for m in fpn.lateral]
+        self.outc = [_fc(m, device, P) for m in fpn.output]
         self.lat_buf = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw]
         self.up_buf = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw[:2]]
         self.p = [bufs.new(B, hh, ww, C) for hh, ww in self.lv_hw]
         self.p6p7_from_c5 = fpn.p6p7_from_c5
         p6 = fpn.p6.conv
-        self.p6 = FusedConv(p6, act=ACT_NONE, device=device)
-        self.p6r = FusedConv(p6, act=ACT_RELU, device=device)
-        self.p7 = _fc(fpn.p7, device)
+        self.p6 = FusedConv(p6, act=ACT_NONE, device=device, precision=P)
+        self.p6r = FusedConv(p6, act=ACT_RELU, device=device, precision=P)
+        self.p7 = _fc(fpn.p7, device, P)
         h5, w5 = self.lv_hw[2]
         h6, w6 = _conv_out(h5, 3, 2, 1), _conv_out(w5, 3, 2, 1)
         h7, w7 = _conv_out(h6, 3, 2, 1), _conv_out(w6, 3, 2, 1)
@@ -474,16 +478,16 @@ class FastDetectron:
         with torch.no_grad():
             first.weight.copy_(torch.cat([cls_convs[0].weight, box_convs[0].weight]).float())
             first.bias.copy_(torch.cat([cls_convs[0].bias, box_convs[0].bias]).float())
-        self.t_first = FusedConv(first, act=act, device=device)
-        self.t_cls = [FusedConv(m, act=act, device=device) for m in cls_convs[1:]]
-        self.t_box = [FusedConv(m, act=act, device=device) for m in box_convs[1:]]
-        self.cls_score = FusedConv(hd.cls_score, act=ACT_NONE, device=device)
+        self.t_first = FusedConv(first, act=act, device=device, precision=P)
+        self.t_cls = [FusedConv(m, act=act, device=device, precision=P) for m in cls_convs[1:]]
+        self.t_box = [FusedConv(m, act=act, device=device, precision=P) for m in box_convs[1:]]
+        self.cls_score = FusedConv(hd.cls_score, act=ACT_NONE, device=device, precision=P)
         if self.fcos:
             merged = nn.Conv2d(C, 5, 3, 1, 1)
             with torch.no_grad():
                 merged.weight.copy_(torch.cat([hd.bbox_pred.weight, hd.ctrness.weight]).float())
                 merged.bias.copy_(torch.cat([hd.bbox_pred.bias, hd.ctrness.bias]).float())
-            self.box_pred = FusedConv(merged, act=ACT_NONE, device=device)
+            self.box_pred = FusedConv(merged, act=ACT_NONE, device=device, precision=P)
             dev = self.device
             f32 = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
             self.gn_params = [(f32(torch.cat([gc.weight, gb.weight])), f32(torch.cat([gc.bias, gb.bias])))
@@ -493,7 +497,7 @@ class FastDetectron:
             self.gn_groups = self.gn_cls[0].num_groups
             self.gn_eps = self.gn_cls[0].eps
         else:
-            self.box_pred = FusedConv(hd.bbox_pred, act=ACT_NONE, device=device)
+            self.box_pred = FusedConv(hd.bbox_pred, act=ACT_NONE, device=device, precision=P)
         self.lvl = []
         for hh, ww in self.level_hw:
             self.lvl.append(dict(first=bufs.new(B, hh, ww, 2 * C), a=bufs.new(B, hh, ww, C), b=bufs.new(B, hh, ww, C),

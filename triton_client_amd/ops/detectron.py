@@ -42,9 +42,11 @@ def group_norm_nhwc(x: NHWC, gamma: torch.Tensor, beta: torch.Tensor, groups: in
         return out
     ws = ws or Workspace(x.t.device)
     stats = ws.get(f"gn_stats_{B}_{groups}", (B, groups, 2), torch.float32)
-    _native.call("tca_group_norm_nhwc", _native.ptr(x.t), B, H * W, C, x.t.shape[-1], x.off, groups, float(eps),
+    if x.t.dtype != out.t.dtype or x.t.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"group_norm_nhwc: bf16 or fp32 NHWC, got {x.t.dtype} -> {out.t.dtype}")
+    _native.call("tca_group_norm_nhwc_dt", _native.ptr(x.t), B, H * W, C, x.t.shape[-1], x.off, groups, float(eps),
                  _native.ptr(gamma), _native.ptr(beta), int(relu), _native.ptr(stats), _native.ptr(out.t),
-                 out.t.shape[-1], out.off, _native.stream_ptr(stream))
+                 out.t.shape[-1], out.off, dtype_code(x.t), _native.stream_ptr(stream))
     return out
 
 

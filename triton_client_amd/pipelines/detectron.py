@@ -27,15 +27,22 @@ from ..ops.image import frame_xform, preprocess
 class DetectronPipeline:
     def __init__(self, model: Optional[DetectronDetector] = None, batch: int = 16,
                  src_hw: Tuple[int, int] = (720, 1280), cfg: Optional[DetectronConfig] = None, device="cuda",
-                 seed: int = 0, mode: str = "letterbox"):
+                 seed: int = 0, mode: str = "letterbox", precision: str = "bf16"):
+        """precision "fp32": the reference's serving precision (libtorch fp32,
+        examples/RetinaNet_detectron/config.pbtxt) — fp32 activations and
+        split-product convs; "bf16" the faster secondary mode."""
         self.device = torch.device(device)
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {precision!r}")
+        self.precision = precision
+        self.dtype = torch.float32 if precision == "fp32" else torch.bfloat16
         if self.device.type != "cuda":
             raise ValueError("DetectronPipeline runs on the GPU; use models.detectron on the CPU")
         if model is None:
             model = build_detectron(cfg, seed)
         model = fuse_model(model.eval())
         self.cfg = model.cfg
-        self.model = model.to(device=self.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        self.model = model.to(device=self.device, dtype=self.dtype, memory_format=torch.channels_last)
         self.B, self.src_hw, self.mode = batch, tuple(src_hw), mode
         self.frames = torch.zeros((batch, *self.src_hw, 3), dtype=torch.uint8, device=self.device)
         self.xform, _ = frame_xform(self.src_hw, self.cfg.input_hw, mode)
@@ -48,12 +55,12 @@ class DetectronPipeline:
     def build_fast(self):
         from ..models.fast import FastDetectron
 
-        self.fast = FastDetectron(self.model, self.B, self.device)
+        self.fast = FastDetectron(self.model, self.B, self.device, precision=self.precision)
         return self.fast
 
     def _input_nchw(self):
-        """Un-normalised 0..255 NCHW bf16 input for the module path (calibration)."""
-        x, _ = preprocess(self.frames, self.cfg.input_hw, self.mode, ([1.0] * 3, [0.0] * 3), torch.bfloat16,
+        """Un-normalised 0..255 NCHW input (the mode's dtype) for the module path (calibration)."""
+        x, _ = preprocess(self.frames, self.cfg.input_hw, self.mode, ([1.0] * 3, [0.0] * 3), self.dtype,
                           "NHWC", 3)
         return x
 
@@ -105,6 +112,6 @@ class DetectronPipeline:
     @torch.no_grad()
     def step(self):
         f = self.fast or self.build_fast()
-        preprocess(self.frames, self.cfg.input_hw, self.mode, self.scaling, torch.bfloat16, "NHWC",
+        preprocess(self.frames, self.cfg.input_hw, self.mode, self.scaling, self.dtype, "NHWC",
                    f.IN_CHANNELS, out=f.input_view())
         return self.post(f.forward(), self.xform)
