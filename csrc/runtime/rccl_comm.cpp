@@ -25,6 +25,7 @@ extern "C" {
 int tca_rccl_unique_id_bytes() { return (int)sizeof(ncclUniqueId); }
 
 int tca_rccl_get_unique_id(void* out) {
+    if (!out) return (int)ncclInvalidArgument;
     ncclUniqueId id;
     ncclResult_t r = ncclGetUniqueId(&id);
     if (r != ncclSuccess) return (int)r;
@@ -35,6 +36,8 @@ int tca_rccl_get_unique_id(void* out) {
 // comm_out receives the ncclComm_t handle.  The caller has already selected
 // its HIP device (torch.cuda.set_device).
 int tca_rccl_comm_init(void** comm_out, int nranks, const void* id_bytes, int rank) {
+    if (!comm_out || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return (int)ncclInvalidArgument;
+    *comm_out = nullptr;
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
     ncclComm_t comm = nullptr;
@@ -49,6 +52,7 @@ int tca_rccl_comm_destroy(void* comm) { return comm ? (int)ncclCommDestroy((nccl
 int tca_rccl_comm_abort(void* comm) { return comm ? (int)ncclCommAbort((ncclComm_t)comm) : 0; }
 
 int tca_rccl_async_error(void* comm) {
+    if (!comm) return (int)ncclInvalidArgument;
     ncclResult_t e = ncclSuccess;
     ncclResult_t r = ncclCommGetAsyncError((ncclComm_t)comm, &e);
     return r != ncclSuccess ? (int)r : (int)e;
@@ -65,12 +69,23 @@ const char* tca_rccl_error_string(int code) { return ncclGetErrorString((ncclRes
 // One grouped p2p plan: n ops; op i moves bytes[i] bytes of buf[i] to
 // (kind[i] = 0, send) or from (kind[i] = 1, recv) rank peer[i].  Payloads go
 // as 4-byte words when size and alignment allow, bytes otherwise, so any
-// dtype travels unchanged.
+// dtype travels unchanged.  The whole plan is checked before the group opens
+// (kind 0/1, peer inside the communicator, a buffer for every non-empty op),
+// so a bad plan posts nothing and leaves no half-issued group behind.
 int tca_rccl_group_p2p(void* comm, int n, const int* kind, const int* peer, void* const* buf,
                        const int64_t* bytes, void* stream) {
     ncclComm_t c = (ncclComm_t)comm;
     hipStream_t s = (hipStream_t)stream;
-    ncclResult_t r = ncclGroupStart();
+    if (!c || n < 0) return (int)ncclInvalidArgument;
+    if (n > 0 && (!kind || !peer || !buf || !bytes)) return (int)ncclInvalidArgument;
+    int nranks = 0;
+    ncclResult_t r = ncclCommCount(c, &nranks);
+    if (r != ncclSuccess) return (int)r;
+    for (int i = 0; i < n; ++i) {
+        if (kind[i] != 0 && kind[i] != 1) return (int)ncclInvalidArgument;
+        if (bytes[i] > 0 && (peer[i] < 0 || peer[i] >= nranks || !buf[i])) return (int)ncclInvalidArgument;
+    }
+    r = ncclGroupStart();
     if (r != ncclSuccess) return (int)r;
     for (int i = 0; i < n && r == ncclSuccess; ++i) {
         const int64_t b = bytes[i];
@@ -86,11 +101,16 @@ int tca_rccl_group_p2p(void* comm, int n, const int* kind, const int* peer, void
 
 // in-place MAX all-reduce of n doubles (step-time aggregation in bench.py)
 int tca_rccl_allreduce_max_f64(void* comm, double* buf, int64_t n, void* stream) {
+    if (!comm || n < 0 || (n > 0 && !buf)) return (int)ncclInvalidArgument;
     return (int)ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclMax, (ncclComm_t)comm, (hipStream_t)stream);
 }
 
 // in-place broadcast of nbytes from root (parameter broadcast for DP replicas)
 int tca_rccl_broadcast(void* comm, void* buf, int64_t nbytes, int root, void* stream) {
+    int nranks = 0;
+    if (!comm || nbytes < 0 || (nbytes > 0 && !buf)) return (int)ncclInvalidArgument;
+    if (ncclCommCount((ncclComm_t)comm, &nranks) != ncclSuccess || root < 0 || root >= nranks)
+        return (int)ncclInvalidArgument;
     return (int)ncclBroadcast(buf, buf, (size_t)nbytes, ncclUint8, root, (ncclComm_t)comm, (hipStream_t)stream);
 }
 

@@ -50,7 +50,19 @@ def main(argv=None):
                     help="raw: tensors in the gRPC messages (C++ codec); shm: KServe system shared memory")
     ap.add_argument("--server-process", action="store_true",
                     help="run the server as its own process (the deployed topology: no GIL shared with the clients)")
+    ap.add_argument("--client-procs", type=int, default=0,
+                    help="P > 0: P camera + P LiDAR client processes (the reference runs each sensor client as its "
+                         "own ROS node), each streaming --frames frames; implies --server-process")
+    ap.add_argument("--burst", action="store_true",
+                    help="drain the window every --window frames (the previous protocol) instead of a sliding window")
+    ap.add_argument("--role", default=None, choices=("camera", "lidar"), help=argparse.SUPPRESS)
+    ap.add_argument("--target", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
+    if a.role is not None:
+        return client_proc(a)
+    if a.client_procs > 0:
+        return multi_proc(a)
 
     import torch
 
@@ -101,12 +113,7 @@ def main(argv=None):
               for s in range(8)]
 
     def run(det, items, count, out):
-        done = 0
-        while done < count:
-            k = min(a.window, count - done)
-            res = det.detect([items[(done + i) % len(items)] for i in range(k)])
-            done += k
-            out.append(res)
+        out.append(stream_frames(det, items, count, a.window, a.burst))
 
     # warm-up (graph capture, calibration, connection setup), then timed
     run(det2, frames, a.warmup, [])
@@ -149,12 +156,153 @@ def main(argv=None):
             "server_requests_per_execution": {m: round(s.inference_count / max(1, s.execution_count), 2)
                                               for m, s in stats.items()},
             "topology": "server process + client process" if proc else "one process", "wire": a.wire,
+            "window_mode": "burst" if a.burst else "sliding",
             "avg_dets_per_frame": {"2d": round(n2, 1), "3d": round(n3, 1)},
             "path": ("GPU preprocess/voxelise -> pinned shared-memory slot (KServe system shared memory) -> "
                      "gRPC message with region references -> server view of the region -> pinned -> GPU model -> "
                      "2D output written into the client's region / 3D outputs in the message") if a.wire == "shm" else
                     ("GPU preprocess/voxelise -> pinned staging -> C++ KServe encoder -> gRPC -> C++ parse -> pinned "
                      "-> GPU model -> pinned -> C++ encoder -> gRPC -> zero-copy response views")}
+    print(json.dumps(line), flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(json.dumps(line) + "\n")
+    return 0
+
+
+def stream_frames(det, items, count, window, burst=False):
+    """Send ``count`` frames (cycling over ``items``) through ``det``: one
+    detect() call, so its window of in-flight requests stays full (a sensor
+    stream), or with ``burst`` one call per ``window`` frames."""
+    if not burst:
+        return det.detect([items[i % len(items)] for i in range(count)])
+    res, done = [], 0
+    while done < count:
+        k = min(window, count - done)
+        res += det.detect([items[(done + i) % len(items)] for i in range(k)])
+        done += k
+    return res
+
+
+def _sensor_data(a, seed0=0):
+    from triton_client_amd.ros import compat
+    from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+
+    H0, W0 = (int(v) for v in a.cam.split("x"))
+    frames = [camera_frame(H0, W0, seed0 + s) for s in range(8)]
+    spec = LidarSpec(rings=a.rings, azimuth_steps=a.columns, sensor_height=3.23)
+    clouds = [compat.create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, seed0 + 500 + s).tobytes(), np.float32)
+                                       .reshape(-1, 4)) for s in range(8)]
+    return frames, clouds
+
+
+def _detector(a, target, role, wait_ready_s=300.0):
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+    from triton_client_amd.clients import Yolov5client, client_for_model
+    from triton_client_amd.inference.engines import RemoteDetector2D, RemoteDetector3D
+
+    model = "YOLOv5nCOCO" if role == "camera" else "pointpillar_kitti"
+    flags = SimpleNamespace(model_name=model, model_version="", batch_size=64, verbose=False)
+    ch = GRPCChannel({"grpc_channel": target}, flags, wait_ready_s=wait_ready_s)
+    if role == "camera":
+        det = RemoteDetector2D(ch, Yolov5client(), letterbox=False, conf_thres=0.3, mode="async", wire=a.wire,
+                               device=a.device)
+    else:
+        cr3 = ch.get_metadata()["config_response"]
+        det = RemoteDetector3D(ch, client_for_model(model, getattr(cr3, "config", cr3)), z_offset=1.5,
+                               mode="async", wire=a.wire, device=a.device)
+    det.window = a.window
+    return ch, det
+
+
+def client_proc(a) -> int:
+    """One sensor client process: warm up, report READY, wait for GO on stdin,
+    stream --frames frames, report its stage times and detection counts."""
+    frames, clouds = _sensor_data(a, 1000 * a.seed)
+    ch, det = _detector(a, a.target, a.role)
+    items = frames if a.role == "camera" else clouds
+    stream_frames(det, items, a.warmup, a.window, a.burst)
+    det.timer = {}
+    print("READY", flush=True)
+    sys.stdin.readline()
+    t0 = time.perf_counter()
+    res = stream_frames(det, items, a.frames, a.window, a.burst)
+    wall = time.perf_counter() - t0
+    if hasattr(det, "close_shm"):
+        det.close_shm()
+    n = float(np.mean([len(d) if a.role == "camera" else len(d["pred_scores"]) for d in res]))
+    print(json.dumps({"role": a.role, "wall_s": wall, "frames": len(res), "dets": n,
+                      "ms": {k: 1e3 * float(np.sum(v)) / a.frames for k, v in det.timer.items()}}), flush=True)
+    return 0
+
+
+def multi_proc(a) -> int:
+    """Server process + P camera and P LiDAR client processes; the clock runs
+    from GO to the last client's last response."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    target = f"127.0.0.1:{port}"
+    here = os.path.abspath(__file__)
+    server = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+                               str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
+                               "--models", "YOLOv5nCOCO,pointpillar_kitti"],
+                              cwd=os.path.dirname(os.path.dirname(here)))
+    common = ["--frames", str(a.frames), "--warmup", str(a.warmup), "--window", str(a.window), "--device", a.device,
+              "--cam", a.cam, "--rings", str(a.rings), "--columns", str(a.columns), "--wire", a.wire,
+              "--target", target] + (["--burst"] if a.burst else [])
+    clients = []
+    try:
+        for p in range(a.client_procs):
+            for role in ("camera", "lidar"):
+                clients.append(subprocess.Popen([sys.executable, here, "--role", role, "--seed", str(p)] + common,
+                                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True))
+        for c in clients:
+            line = c.stdout.readline()
+            if line.strip() != "READY":
+                raise RuntimeError(f"client failed before READY: {line!r}")
+        t0 = time.perf_counter()
+        for c in clients:
+            c.stdin.write("GO\n")
+            c.stdin.flush()
+        outs = [json.loads(c.stdout.readline()) for c in clients]
+        wall = time.perf_counter() - t0
+        for c in clients:
+            if c.wait(60) != 0:
+                raise RuntimeError("a client process failed")
+        from triton_client_amd.channel.grpc_channel import GRPCChannel
+
+        ch = GRPCChannel({"grpc_channel": target}, SimpleNamespace(model_name="YOLOv5nCOCO", model_version="",
+                                                                   batch_size=64, verbose=False))
+        rpe = {}
+        for m in ("YOLOv5nCOCO", "pointpillar_kitti"):
+            st = ch.model_statistics(m).model_stats[0]
+            rpe[m] = round(st.inference_count / max(1, st.execution_count), 2)
+    finally:
+        for c in clients:
+            if c.poll() is None:
+                c.kill()
+        server.terminate()
+        server.wait(30)
+
+    def mean_ms(role):
+        rs = [o for o in outs if o["role"] == role]
+        return {k: round(float(np.mean([o["ms"][k] for o in rs])), 3) for k in rs[0]["ms"]}
+
+    pairs = a.client_procs * a.frames
+    line = {"metric": "served-path frame pairs/s (camera + LiDAR over KServe gRPC, localhost)",
+            "value": round(pairs / wall, 2), "unit": "frame pairs/s", "frames": pairs, "window": a.window,
+            "wall_s": round(wall, 3), "device": a.device,
+            "client_ms_per_frame": {"camera": mean_ms("camera"), "lidar": mean_ms("lidar")},
+            "client_wall_s": {o["role"] + str(i // 2): round(o["wall_s"], 3) for i, o in enumerate(outs)},
+            "server_requests_per_execution": rpe,
+            "topology": f"server process + {a.client_procs} camera and {a.client_procs} LiDAR client processes",
+            "wire": a.wire, "window_mode": "burst" if a.burst else "sliding",
+            "avg_dets_per_frame": {"2d": round(float(np.mean([o["dets"] for o in outs if o["role"] == "camera"])), 1),
+                                   "3d": round(float(np.mean([o["dets"] for o in outs if o["role"] == "lidar"])), 1)}}
     print(json.dumps(line), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:

@@ -99,13 +99,17 @@ class PointpillarPreprocess:
     _TORCH = {"FP32": torch.float32, "INT32": torch.int32, "INT64": torch.int64, "FP16": torch.float16}
 
     def filter_cloud_gpu(self, cloud, normalize_intensity: bool = True, z_offset: float = 0.0,
-                         dtypes: Optional[Dict[str, str]] = None) -> Dict[str, torch.Tensor]:
+                         dtypes: Optional[Dict[str, str]] = None,
+                         out: Optional[Dict[str, np.ndarray]] = None) -> Dict[str, torch.Tensor]:
         """PointCloud2 → {voxels, voxel_coords, voxel_num_points} as PINNED host
         tensors the wire encoder reads directly.  The payload bytes are uploaded
         once (pinned → device); unpack (K6: skip NaN, i /= max, z += offset —
         reference ros_inference3d.py:125-128), the spconv-order voxeliser (K7)
         and the dtype casts run on the GPU; only the V valid rows come back, by
-        one DMA per tensor into reusable pinned staging."""
+        one DMA per tensor into reusable pinned staging — or, for a name in
+        ``out`` (page-locked host arrays of max_voxels rows, e.g. a slot of a
+        registered shared-memory region), straight into that array; the
+        returned tensor is then a view of its first V rows."""
         from ..ops._ws import Workspace
         from ..ops.lidar import pc2_unpack
         from ..ros.compat import cloud_layout
@@ -144,9 +148,15 @@ class PointpillarPreprocess:
             if name == "voxel_coords":
                 t = t.clone()
                 t[:, 0] = 0
-            pin = self._pin_out[name]
-            if pin.dtype != tdt:
-                pin = self._pin_out[name] = torch.empty(pin.shape, dtype=tdt).pin_memory()
+            if out is not None and name in out:
+                pin = torch.from_numpy(out[name])
+                if pin.dtype != tdt or pin.shape[0] < k or tuple(pin.shape[1:]) != tuple(t.shape[1:]):
+                    raise ValueError(f"{name}: destination {tuple(pin.shape)} {pin.dtype} cannot take "
+                                     f"{k} rows of {tuple(t.shape[1:])} {tdt}")
+            else:
+                pin = self._pin_out[name]
+                if pin.dtype != tdt:
+                    pin = self._pin_out[name] = torch.empty(pin.shape, dtype=tdt).pin_memory()
             pin[:k].copy_(t.to(tdt), non_blocking=True)
             out[name] = pin[:k]
         torch.cuda.current_stream(self.device).synchronize()
