@@ -15,7 +15,7 @@ through rank 0, then a grouped RCCL scatter over xGMI), the captured
 camera + LiDAR hipGraph runs, and the detections of all ranks are gathered to
 rank 0 over RCCL and copied to its host.  Weak scaling: B frames per GPU per
 step.  Data: synthetic sensors, random-init weights (no datasets/checkpoints
-reachable); compute dtype bf16 with fp32 accumulation.
+reachable); compute precision per ``--precision`` below (fp32 by default).
 
 Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (the script
 starts N rank processes itself, before any GPU call) or ``torchrun

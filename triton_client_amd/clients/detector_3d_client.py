@@ -142,14 +142,14 @@ class PointpillarPreprocess:
         v, c, num, vc = self._vox(pts, cnt)
         k = int(vc[0])  # the one small sync: how many rows to bring back
         dts = dtypes or {}
-        out = {}
+        dst, out = out or {}, {}
         for name, t in (("voxels", v[0, :k]), ("voxel_coords", c[0, :k]), ("voxel_num_points", num[0, :k])):
             tdt = self._TORCH.get(dts.get(name, ""), t.dtype if name == "voxels" else torch.int32)
             if name == "voxel_coords":
                 t = t.clone()
                 t[:, 0] = 0
-            if out is not None and name in out:
-                pin = torch.from_numpy(out[name])
+            if name in dst:
+                pin = torch.from_numpy(dst[name])
                 if pin.dtype != tdt or pin.shape[0] < k or tuple(pin.shape[1:]) != tuple(t.shape[1:]):
                     raise ValueError(f"{name}: destination {tuple(pin.shape)} {pin.dtype} cannot take "
                                      f"{k} rows of {tuple(t.shape[1:])} {tdt}")
