@@ -65,3 +65,51 @@ def test_device_tensor_refused():
         t = torch.zeros(2, device="cuda")
     with pytest.raises(ValueError):
         wire.encode_request("m", [("x", t)])
+
+
+def test_runtime_published_only_after_signatures(monkeypatch):
+    """A thread on runtime()'s lock-free fast path must never get the library
+    before its argtypes are declared (pointers would be truncated to C ints:
+    the served-path segfault under concurrent first requests)."""
+    from triton_client_amd import _runtime_sigs
+
+    seen = []
+    real = _runtime_sigs.declare
+
+    def spy(lib):
+        seen.append(_native._RUNTIME)
+        real(lib)
+
+    monkeypatch.setattr(_native, "_RUNTIME", None)
+    monkeypatch.setattr(_runtime_sigs, "declare", spy)
+    lib = _native.runtime()
+    assert seen == [None] and _native._RUNTIME is lib
+
+
+def test_concurrent_first_parse_requests():
+    """Many threads parse requests while the runtime loads for the first time."""
+    import threading
+
+    from triton_client_amd.proto import service_pb2 as pb
+
+    req = pb.ModelInferRequest(model_name="m", id="7")
+    t = req.inputs.add(name="x", datatype="FP32", shape=[4, 8])
+    req.raw_input_contents.append(np.arange(32, dtype=np.float32).tobytes())
+    data = req.SerializeToString()
+    _native._RUNTIME = None
+    errs = []
+
+    def work():
+        try:
+            for _ in range(50):
+                p = wire.parse_request(data)
+                assert p.inputs["x"].shape == (4, 8) and float(p.inputs["x"][3, 7]) == 31.0
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work) for _ in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:3]

@@ -247,7 +247,7 @@ def multi_proc(a) -> int:
         port = sk.getsockname()[1]
     target = f"127.0.0.1:{port}"
     here = os.path.abspath(__file__)
-    server = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+    server = subprocess.Popen([sys.executable, "-X", "faulthandler", "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
                                str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
                                "--models", "YOLOv5nCOCO,pointpillar_kitti"],
                               cwd=os.path.dirname(os.path.dirname(here)))
@@ -263,7 +263,7 @@ def multi_proc(a) -> int:
         for c in clients:
             line = c.stdout.readline()
             if line.strip() != "READY":
-                raise RuntimeError(f"client failed before READY: {line!r}")
+                raise RuntimeError(f"client failed before READY: {line!r} (server exit code {server.poll()})")
         t0 = time.perf_counter()
         for c in clients:
             c.stdin.write("GO\n")

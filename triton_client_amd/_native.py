@@ -96,17 +96,22 @@ class NativeError(RuntimeError):
 def _load_hip() -> ctypes.CDLL:
     global _HIP
     if _HIP is None:
-        for cand in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
-            try:
-                _HIP = ctypes.CDLL(cand)
-                break
-            except OSError:
-                continue
-        if _HIP is not None:
-            _HIP.hipGetErrorString.restype = ctypes.c_char_p
-            _HIP.hipGetErrorString.argtypes = [I]
-            _HIP.hipGetLastError.restype = I
-            _HIP.hipGetLastError.argtypes = []
+        with _LOCK:
+            if _HIP is not None:
+                return _HIP
+            lib = None
+            for cand in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+                try:
+                    lib = ctypes.CDLL(cand)
+                    break
+                except OSError:
+                    continue
+            if lib is not None:
+                lib.hipGetErrorString.restype = ctypes.c_char_p
+                lib.hipGetErrorString.argtypes = [I]
+                lib.hipGetLastError.restype = I
+                lib.hipGetLastError.argtypes = []
+            _HIP = lib  # published only once its signatures are declared
     return _HIP
 
 
@@ -148,10 +153,14 @@ def runtime(auto_build: bool = True) -> ctypes.CDLL:
             _build.build(verbose=False)
         if not os.path.exists(path):
             raise NativeError(f"{path} is missing: run `python -m triton_client_amd._build`")
-        _RUNTIME = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         from . import _runtime_sigs  # noqa: F401  (declares argtypes)
-        _runtime_sigs.declare(_RUNTIME)
-        return _RUNTIME
+        _runtime_sigs.declare(lib)
+        # published only after argtypes are declared: another thread takes the
+        # lock-free fast path above, and an undeclared pointer argument would be
+        # truncated to a C int (a served-path segfault under concurrent requests)
+        _RUNTIME = lib
+        return lib
 
 
 def check(rc: int, what: str) -> None:
