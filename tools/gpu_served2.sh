@@ -5,7 +5,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 400 python -u -m pytest tests/test_drivers_gpu.py -x -v -m gpu -k "served" --timeout 300 --timeout-method thread > gpurun_out/served_tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAILED|Error" gpurun_out/served_tests.log | tail -20; tail -40 gpurun_out/served_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_drivers_gpu.py tests/test_detectron.py tests/test_yolov4.py tests/test_kserve.py -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/served_tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAILED|Error" gpurun_out/served_tests.log | tail -20; tail -40 gpurun_out/served_tests.log; exit 1; }
 tail -1 gpurun_out/served_tests.log
 timeout -k 10 300 python tools/served_bench.py --frames 512 --window 8 --server-process --wire shm --json-out gpurun_out/served2_thr_shm.json > gpurun_out/served2_thr_shm.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/served2_thr_shm.log; exit 1; }
 tail -1 gpurun_out/served2_thr_shm.log | cut -c1-900

@@ -27,6 +27,25 @@ from .model import InferError
 
 SHM_DIR = "/dev/shm"
 
+# page-locked registered mappings, base address -> bytes: a request view inside one
+# is DMA'd to the GPU straight from the client's memory (no staging copy)
+_PINNED: Dict[int, int] = {}
+_PINNED_LOCK = threading.Lock()
+
+
+def _base(mm: mmap.mmap) -> int:
+    import ctypes
+    return ctypes.addressof(ctypes.c_char.from_buffer(mm))
+
+
+def pinned_host(a: np.ndarray) -> bool:
+    """True when ``a`` lies entirely inside a page-locked registered region."""
+    if not isinstance(a, np.ndarray) or not a.flags.c_contiguous:
+        return False
+    p, n = a.ctypes.data, a.nbytes
+    with _PINNED_LOCK:
+        return any(b <= p and p + n <= b + sz for b, sz in _PINNED.items())
+
 
 @dataclass
 class Region:
@@ -106,6 +125,9 @@ class SharedMemoryRegistry:
         r = Region(name, key, int(offset), int(byte_size), mm)
         if self.pin:
             r.pinned = _host_register(mm, offset + byte_size)
+            if r.pinned:
+                with _PINNED_LOCK:
+                    _PINNED[_base(mm)] = offset + byte_size
         with self._lock:
             self._regions[name] = r
         return r
@@ -116,6 +138,8 @@ class SharedMemoryRegistry:
             regs = [self._regions.pop(n) for n in names if n in self._regions]
         for r in regs:
             if r.pinned:
+                with _PINNED_LOCK:
+                    _PINNED.pop(_base(r.mm), None)
                 _host_unregister(r.mm)
             try:
                 r.mm.close()
