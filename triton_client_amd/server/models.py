@@ -82,14 +82,21 @@ class _YoloPlan:
     def __init__(self, pipe, B: int, img: int, device):
         from ..models.fast import FastYOLOv5
         from ..pipelines.graph import GraphRunner
+        import copy
+
+        from ..ops._ws import Workspace
         self.B, self.img = B, img
         self.fast = FastYOLOv5(pipe.model, B, (img, img), device, precision=pipe.precision)
+        # a postprocess of its own: the workspace re-allocates its buffers when the batch
+        # changes, which would free memory that another plan's captured graph writes
+        post = copy.copy(pipe.post)
+        post.ws = Workspace(device)
         self.x_dev = torch.zeros((B, 3, img, img), dtype=torch.float32, device=device)
         self.pin_in = torch.empty((B, 3, img, img), dtype=torch.float32).pin_memory()
 
         def step():
             self.fast.set_input(self.x_dev)
-            return pipe.post.decode(self.fast.forward())
+            return post.decode(self.fast.forward())
         self.runner = GraphRunner(step)
         self.runner.capture()  # under the repository's exclusive GPU phase, never lazily while serving
         self.pin_out = torch.empty(self.runner.out.shape, dtype=torch.float32).pin_memory()
