@@ -202,7 +202,7 @@ def main():
         from triton_client_amd.pipelines import CenterPointPipeline
 
         def make_lid(b, m):
-            return CenterPointPipeline(model=m, batch=b, max_points=max_points, device=dev)
+            return CenterPointPipeline(model=m, batch=b, max_points=max_points, device=dev, precision=args.precision)
     elif use_lid and sec:
         from triton_client_amd.pipelines import SecondPipeline
 
@@ -552,7 +552,7 @@ def main():
             "vs_baseline": None,
             # families with an fp32 mode report the mode; the others run bf16 only
             "dtype": args.precision if (args.camera_model in ("yolov5n", "retinanet", "fcos") or not use_cam)
-            and (args.lidar_model == "pointpillars" or not use_lid) else "bf16",
+            and (args.lidar_model in ("pointpillars", "centerpoint") or not use_lid) else "bf16",
             "data": (f"synthetic: {nd} distinct {W0}x{H0} "
                      + (f"JPEG (q{args.jpeg_quality}, decoded every step)" if jdec is not None else "uint8 RGB")
                      + f" camera frames + {nd} distinct "

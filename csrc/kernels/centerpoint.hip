@@ -15,6 +15,9 @@
 //   layer 2: [y1 | max1] (64) -> Linear(64->64) on MFMA (y1 re-laid out through
 //   a 2 KiB per-wave LDS tile so lanes own rows), + bias, ReLU, max over slots;
 //   scatter: one 128-B NHWC canvas line per pillar.
+//   F32 (the fp32 precision mode): layer 2 also runs as split products (y1 / max1
+//   and W2 as hi + lo bf16 halves, 3 MFMAs per step, fp32 accumulation) and the
+//   canvas is fp32 (256-B lines).
 //
 // centerhead_decode — one thread per (frame, task, pixel); the merged head
 // output is NHWC with each task's channels [reg 2 | height 1 | dim 3 | rot 2 |
@@ -41,7 +44,7 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
-template <bool FROM_SLOTS>
+template <bool FROM_SLOTS, bool F32>
 __global__ void __launch_bounds__(256) pfn2_kernel(
     const float* __restrict__ pts, int pstride, int max_pts,                // FROM_SLOTS source
     const int* __restrict__ slots, const int* __restrict__ vcount,
@@ -49,8 +52,9 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
     const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P,
     const float* __restrict__ W1 /*[32][10]*/, const float* __restrict__ b1 /*[32]*/,
     const float* __restrict__ W2 /*[64][64]*/, const float* __restrict__ b2 /*[64]*/, PfnGeom g,
-    __hip_bfloat16* __restrict__ canvas, float* __restrict__ feat_out) {
-  __shared__ __attribute__((aligned(16))) __hip_bfloat16 s_y1[4][32 * 32 + 32];  // per wave: y1 rows + max1
+    void* __restrict__ canvas, float* __restrict__ feat_out) {
+  constexpr int Y1 = 32 * 32 + 32;  // per wave: y1 rows + max1 (F32: hi tile, then lo tile)
+  __shared__ __attribute__((aligned(16))) __hip_bfloat16 s_y1[4][F32 ? 2 * Y1 : Y1];
   const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -69,13 +73,18 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
     w1l[j] = lo;
   }
   // layer-2 weights: tile t (cols 32t..32t+31), k-step s: W2[32t + r][16s + 8h + j]
-  bf16x8 w2[2][4];
+  bf16x8 w2[2][4], w2l[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w2[t][s][j] = (__bf16)W2[(32 * t + r) * 64 + 16 * s + 8 * h + j];
+      for (int j = 0; j < 8; ++j) {
+        __bf16 hi, lo;
+        split_bf16(W2[(32 * t + r) * 64 + 16 * s + 8 * h + j], hi, lo);
+        w2[t][s][j] = hi;
+        w2l[t][s][j] = F32 ? lo : (__bf16)0.f;
+      }
   const float bias1 = b1[r];
   const float bias2_0 = b2[r], bias2_1 = b2[32 + r];
 
@@ -139,11 +148,27 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
     for (int j = 0; j < 16; ++j) {
       const int row = (j & 3) + 8 * (j >> 2) + 4 * h;
       const float y = fmaxf(acc[j] + bias1, 0.f);
-      y1s[row * 32 + r] = __float2bfloat16(y);
+      if constexpr (F32) {
+        __bf16 hi, lo;
+        split_bf16(y, hi, lo);
+        reinterpret_cast<__bf16*>(y1s)[row * 32 + r] = hi;
+        reinterpret_cast<__bf16*>(y1s)[Y1 + row * 32 + r] = lo;
+      } else {
+        y1s[row * 32 + r] = __float2bfloat16(y);
+      }
       if (row < P) m1 = fmaxf(m1, y);
     }
     m1 = fmaxf(m1, __shfl_xor(m1, 32, 64));
-    if (h == 0) y1s[32 * 32 + r] = __float2bfloat16(m1);
+    if (h == 0) {
+      if constexpr (F32) {
+        __bf16 hi, lo;
+        split_bf16(m1, hi, lo);
+        reinterpret_cast<__bf16*>(y1s)[32 * 32 + r] = hi;
+        reinterpret_cast<__bf16*>(y1s)[Y1 + 32 * 32 + r] = lo;
+      } else {
+        y1s[32 * 32 + r] = __float2bfloat16(m1);
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
     __builtin_amdgcn_wave_barrier();
     // ---- layer 2: A rows = slots, k = [y1 (32) | max1 (32)]
@@ -152,8 +177,18 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
     for (int s = 0; s < 4; ++s) {
       const __hip_bfloat16* src = s < 2 ? y1s + r * 32 + 16 * s + 8 * h : y1s + 32 * 32 + 16 * (s - 2) + 8 * h;
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(src);
+      if constexpr (F32) {
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(src + Y1);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) a2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2[t][s], a2[t], 0, 0, 0);
+        for (int t = 0; t < 2; ++t) {
+          a2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2l[t][s], a2[t], 0, 0, 0);
+          a2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, w2[t][s], a2[t], 0, 0, 0);
+          a2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2[t][s], a2[t], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w2[t][s], a2[t], 0, 0, 0);
+      }
     }
     float m2[2];
 #pragma unroll
@@ -171,7 +206,10 @@ __global__ void __launch_bounds__(256) pfn2_kernel(
     const int ch = 32 * h + r;
     if (canvas) {
       const long cell = ((long)b * g.ny + co[2]) * g.nx + co[3];
-      canvas[cell * 64 + ch] = __float2bfloat16(val);
+      if constexpr (F32)
+        reinterpret_cast<float*>(canvas)[cell * 64 + ch] = val;
+      else
+        reinterpret_cast<__hip_bfloat16*>(canvas)[cell * 64 + ch] = __float2bfloat16(val);
     }
     if (feat_out) feat_out[v * 64 + ch] = val;
   }
@@ -255,26 +293,37 @@ __global__ void __launch_bounds__(256) centerhead_decode_kernel(
 TCA_API int tca_pfn2_slots(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount,
                            const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                            const float* W1, const float* b1, const float* W2, const float* b2, const float* range,
-                           const float* vsize, int nx, int ny, void* canvas, float* feat_out, hipStream_t stream) {
+                           const float* vsize, int nx, int ny, void* canvas, float* feat_out, int f32,
+                           hipStream_t stream) {
   if (batch <= 0) return 0;
   if (P > 32) return (int)hipErrorInvalidValue;
   PfnGeom g{range[0], range[1], vsize[0], vsize[1], nx, ny};
-  pfn2_kernel<true><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, 5, nullptr, coords,
-                                              voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g,
-                                              (__hip_bfloat16*)canvas, feat_out);
+  if (f32)
+    pfn2_kernel<true, true><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, 5, nullptr, coords,
+                                                      voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g, canvas,
+                                                      feat_out);
+  else
+    pfn2_kernel<true, false><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, nullptr, 5, nullptr,
+                                                       coords, voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g,
+                                                       canvas, feat_out);
   TCA_LAUNCH_CHECK();
 }
 
 TCA_API int tca_pfn2_voxels(const float* voxels, int vfeat, const int* num_points, const int* coords,
                             const int* voxel_count, int batch, int max_voxels, int P, const float* W1,
                             const float* b1, const float* W2, const float* b2, const float* range, const float* vsize,
-                            int nx, int ny, void* canvas, float* feat_out, hipStream_t stream) {
+                            int nx, int ny, void* canvas, float* feat_out, int f32, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (P > 32 || vfeat < 4) return (int)hipErrorInvalidValue;
   PfnGeom g{range[0], range[1], vsize[0], vsize[1], nx, ny};
-  pfn2_kernel<false><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, vfeat, num_points, coords,
-                                               voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g,
-                                               (__hip_bfloat16*)canvas, feat_out);
+  if (f32)
+    pfn2_kernel<false, true><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, vfeat, num_points,
+                                                       coords, voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g,
+                                                       canvas, feat_out);
+  else
+    pfn2_kernel<false, false><<<2048, 256, 0, stream>>>(nullptr, 4, 0, nullptr, nullptr, voxels, vfeat, num_points,
+                                                        coords, voxel_count, batch, max_voxels, P, W1, b1, W2, b2, g,
+                                                        canvas, feat_out);
   TCA_LAUNCH_CHECK();
 }
 

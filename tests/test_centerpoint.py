@@ -170,3 +170,98 @@ def test_centerpoint_pipeline_graph(cuda):
     for a, b, c in zip(e, g, g2):
         np.testing.assert_array_equal(b["pred_boxes"], c["pred_boxes"])
         assert a["pred_boxes"].shape[1] == 9 and len(a["pred_scores"]) <= 6 * 83
+
+
+def _rel_l2(got: torch.Tensor, ref: torch.Tensor) -> float:
+    got, ref = got.double().cpu(), ref.double().cpu()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.gpu
+def test_pfn2_fp32_mode_vs_fp64(cuda):
+    """fp32 mode PFN (both layers split-product, fp32 canvas) against an fp64
+    evaluation of the module: relative L2 at the fp32 plans' bound (2e-4; the
+    bf16 PFN's second layer alone sits near 2e-3)."""
+    from triton_client_amd.ops.centerpoint import PFNEncoder
+    cfg = _small_cfg()
+    m = _model(cfg)
+    p5 = _cloud(cfg, 1)
+    v, zyx, num, _ = voxelize_np(p5, cfg.voxel, 5)
+    V = len(v)
+    coords = np.pad(zyx, ((0, 0), (1, 0))).astype(np.int32)
+    Vm = cfg.voxel.max_voxels
+    vox = torch.zeros((1, Vm, 20, 5), device=cuda)
+    vox[0, :V] = torch.from_numpy(v).to(cuda)
+    nump = torch.zeros((1, Vm), dtype=torch.int32, device=cuda)
+    nump[0, :V] = torch.from_numpy(num).to(cuda)
+    co = torch.zeros((1, Vm, 4), dtype=torch.int32, device=cuda)
+    co[0, :V] = torch.from_numpy(coords).to(cuda)
+    vc = torch.tensor([V], dtype=torch.int32, device=cuda)
+    with torch.no_grad():
+        f = pfn_point_features(torch.from_numpy(v).double(), torch.from_numpy(num.astype(np.int64)),
+                               torch.from_numpy(coords), cfg.voxel)
+        ref = m.pfn.double()(f)
+    m.pfn.float()
+    errs = {}
+    for precision in ("fp32", "bf16"):
+        enc = PFNEncoder(cfg.voxel, m.pfn, 1, device=cuda, precision=precision)
+        feat = torch.zeros((1, Vm, 64), dtype=torch.float32, device=cuda)
+        enc.encode_from_voxels(vox, nump, co, vc, feat_out=feat)
+        torch.cuda.synchronize()
+        errs[precision] = _rel_l2(feat[0, :V], ref)
+        cv = enc.canvas[0].float().cpu()
+        assert enc.canvas.dtype == (torch.float32 if precision == "fp32" else torch.bfloat16)
+        if precision == "fp32":  # the canvas holds exactly the features
+            torch.testing.assert_close(cv[coords[:, 2], coords[:, 3]], feat[0, :V].cpu(), rtol=0, atol=0)
+    print("pfn rel L2", errs)
+    assert errs["fp32"] < 2e-4 and errs["fp32"] < errs["bf16"], errs
+
+
+@pytest.mark.gpu
+def test_fast_centerpoint_fp32_vs_fp64_module(cuda):
+    """fp32 mode RPN + CenterHead plan against an fp64 evaluation of the fused
+    module, per task: relative L2 below the fp32 plans' bound (2e-4)."""
+    from triton_client_amd.models.fast import FastCenterPoint
+    cfg = _small_cfg()
+    m = _model(cfg)
+    nx, ny, _ = cfg.voxel.grid_size
+    canvas = torch.zeros(2, ny, nx, 64)
+    canvas[:, ::3, ::2] = torch.rand(2, (ny + 2) // 3, (nx + 1) // 2, 64)
+    with torch.no_grad():
+        ref = merged_task_outputs(m.double().bev_forward(canvas.double().permute(0, 3, 1, 2)))
+    f = FastCenterPoint(m.float(), 2, device=cuda, precision="fp32")
+    out = f.forward(NHWC(canvas.to(cuda))).t
+    torch.cuda.synchronize()
+    assert out.dtype == torch.float32
+    errs = [_rel_l2(out[..., f.task_offsets[t]:f.task_offsets[t] + r.shape[1]].permute(0, 3, 1, 2), r)
+            for t, r in enumerate(ref)]
+    print("centerpoint fp32 rel L2", errs)
+    assert max(errs) < 2e-4, errs
+
+
+@pytest.mark.gpu
+def test_centerpoint_pipeline_fp32_matches_bf16_kept_set(cuda):
+    """Same weights, same sweeps: the fp32 pipeline's detections and the bf16
+    pipeline's agree on the strong boxes (bf16 is the secondary mode)."""
+    from triton_client_amd.pipelines import CenterPointPipeline
+    res = {}
+    base = None
+    for precision in ("fp32", "bf16"):
+        import copy
+        pipe = CenterPointPipeline(model=None if base is None else copy.deepcopy(base), batch=2, max_points=32768,
+                                   device=cuda, precision=precision)
+        for b in range(2):
+            c = lidar_sweep(LidarSpec(rings=32, azimuth_steps=1024, sensor_height=1.8), b)
+            raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+            pipe.data[b * pipe.frame_bytes: b * pipe.frame_bytes + raw.numel()].copy_(raw)
+            pipe.frame_n[b] = c.shape[0]
+        if base is None:
+            pipe.calibrate_detection_density(300.0)
+            base = pipe.model
+        res[precision] = pipe.step().per_image()
+        torch.cuda.synchronize()
+    for a, b in zip(res["fp32"], res["bf16"]):
+        assert len(a["pred_scores"]) > 0
+        k = min(10, len(a["pred_scores"]), len(b["pred_scores"]))
+        np.testing.assert_allclose(np.sort(a["pred_scores"])[::-1][:k], np.sort(b["pred_scores"])[::-1][:k],
+                                   rtol=0.05, atol=0.02)

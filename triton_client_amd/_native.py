@@ -58,8 +58,8 @@ _KERNEL_SIGS = {
     "tca_anchor_decode_filter_keyed": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, P, P, P, P, P, P, I,
                                        P],
     "tca_anchor_topk_threshold": [P, I, I, I, I, I, I, I, I, I, P, P, P],
-    "tca_pfn2_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
-    "tca_pfn2_voxels": [P, I, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, P],
+    "tca_pfn2_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, I, P],
+    "tca_pfn2_voxels": [P, I, P, P, P, I, I, I, P, P, P, P, P, P, I, I, P, P, I, P],
     "tca_centerhead_decode": [P, I, I, I, I, I, I, P, P, I, F, P, P, I, P, P, P, P, P, P, I, P],
     "tca_maxpool2d_nhwc": [P, I, I, I, I, I, I, I, I, I, P, I, I, I, I, I, P],
     "tca_retina_decode": [P, P, I, I, I, I, I, I, I, I, I, P, F, F, F, F, I, I, P, P, P, P, P, I, I, P],

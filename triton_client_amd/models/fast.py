@@ -323,7 +323,8 @@ class FastBEV:
 
 
 class FastCenterPoint:
-    """CenterPoint-PP RPN + CenterHead on fused convs.
+    """CenterPoint-PP RPN + CenterHead on fused convs (bf16 or fp32 split-product
+    activations, like the other plans).
 
     * shared conv 3x3 384→64 (+BN+ReLU);
     * all tasks' first-level head convs (6 tasks × 6 heads × conv3x3 64→64
@@ -336,18 +337,19 @@ class FastCenterPoint:
 
     TASK_STRIDE = 16
 
-    def __init__(self, model, batch: int, device="cuda"):
+    def __init__(self, model, batch: int, device="cuda", precision: str = "bf16"):
         from .centerpoint import HEAD_ORDER
 
         self.device = torch.device(device)
+        self.precision = precision
         cfg = self.cfg = model.cfg
         nx, ny, _ = cfg.voxel.grid_size
         B = batch
-        bufs = self.bufs = _Buffers(self.device)
+        bufs = self.bufs = _Buffers(self.device, precision)
         self.bb = _BEVBackbonePlan(model.backbone, B, ny, nx, bufs, device)
         H0, W0 = self.bb.out_hw
         hd = model.head
-        self.shared = _fc(hd.shared, device)
+        self.shared = _fc(hd.shared, device, precision)
         self.sh = bufs.new(B, H0, W0, self.shared.N)
         names = list(HEAD_ORDER) + ["hm"]
         pre = [t.pre[n] for t in hd.tasks for n in names]
@@ -356,7 +358,7 @@ class FastCenterPoint:
         with torch.no_grad():
             big.weight.copy_(torch.cat([m.conv.weight for m in pre]).float())
             big.bias.copy_(torch.cat([m.conv.bias for m in pre]).float())
-        self.pre = FusedConv(big, act=ACT_RELU, device=device)
+        self.pre = FusedConv(big, act=ACT_RELU, device=device, precision=precision)
         self.mid = bufs.new(B, H0, W0, self.pre.N)
         self.c_task_in = c_mid * len(names)
         self.finals = []
@@ -373,7 +375,7 @@ class FastCenterPoint:
                     conv.weight[o0:o0 + o.out_channels, h * c_mid:(h + 1) * c_mid] = o.weight.float()
                     conv.bias[o0:o0 + o.out_channels] = o.bias.float()
                     o0 += o.out_channels
-            self.finals.append(FusedConv(conv, act=ACT_NONE, device=device))
+            self.finals.append(FusedConv(conv, act=ACT_NONE, device=device, precision=precision))
         self.task_offsets = [t * self.TASK_STRIDE for t in range(len(hd.tasks))]
         self.hout = bufs.new(B, H0, W0, self.TASK_STRIDE * len(hd.tasks))
 

@@ -30,9 +30,10 @@ def _carr(ctype, vals):
 
 
 class PFNEncoder:
-    """Fused 2-layer PillarFeatureNet (BN folded) + scatter into an NHWC bf16 canvas."""
+    """Fused 2-layer PillarFeatureNet (BN folded) + scatter into an NHWC canvas:
+    bf16, or fp32 with both layers as split products (``precision="fp32"``)."""
 
-    def __init__(self, cfg: VoxelConfig, pfn, batch: int, device="cuda"):
+    def __init__(self, cfg: VoxelConfig, pfn, batch: int, device="cuda", precision: str = "bf16"):
         l1, l2 = pfn.layers
         assert l1.fused_weight is not None, "fuse_bn() the PillarFeatureNet first"
         self.cfg, self.B = cfg, batch
@@ -44,13 +45,16 @@ class PFNEncoder:
         nx, ny, _ = cfg.grid_size
         self.nx, self.ny = nx, ny
         self.ws = Workspace(self.device)
-        self.canvas = self.ws.get("canvas", (batch, ny, nx, self.C), torch.bfloat16, init=0)
+        self.f32 = precision == "fp32"
+        self.canvas = self.ws.get("canvas", (batch, ny, nx, self.C), torch.float32 if self.f32 else torch.bfloat16,
+                                  init=0)
         self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
         self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
 
     def clear_coords(self, coords: torch.Tensor, voxel_count: torch.Tensor, stream=None) -> None:
         _native.call("tca_pillar_canvas_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
-                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), 2, _native.stream_ptr(stream))
+                     coords.shape[1], self.nx, self.ny, self.C, _native.ptr(self.canvas), dtype_code(self.canvas),
+                     _native.stream_ptr(stream))
 
     def clear(self, vox: Voxelizer, stream=None) -> None:
         self.clear_coords(vox.coords, vox.voxel_count, stream)
@@ -60,7 +64,7 @@ class PFNEncoder:
                      _native.ptr(vox.vcount), _native.ptr(vox.coords), _native.ptr(vox.voxel_count), self.B,
                      self.cfg.max_voxels, self.cfg.max_points_per_voxel, _native.ptr(self.W1), _native.ptr(self.b1),
                      _native.ptr(self.W2), _native.ptr(self.b2), self._range, self._vsize, self.nx, self.ny,
-                     _native.ptr(self.canvas), _native.ptr(feat_out), _native.stream_ptr(stream))
+                     _native.ptr(self.canvas), _native.ptr(feat_out), int(self.f32), _native.stream_ptr(stream))
         return self.canvas
 
     def encode_from_voxels(self, voxels, num_points, coords, voxel_count, feat_out=None, stream=None):
@@ -69,7 +73,7 @@ class PFNEncoder:
                      _native.ptr(coords), _native.ptr(voxel_count), voxels.shape[0], voxels.shape[1], voxels.shape[2],
                      _native.ptr(self.W1), _native.ptr(self.b1), _native.ptr(self.W2), _native.ptr(self.b2),
                      self._range, self._vsize, self.nx, self.ny, _native.ptr(self.canvas), _native.ptr(feat_out),
-                     _native.stream_ptr(stream))
+                     int(self.f32), _native.stream_ptr(stream))
         return self.canvas
 
 

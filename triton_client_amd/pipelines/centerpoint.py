@@ -3,14 +3,16 @@ raw PointCloud2 payloads → 9-d boxes.
 
     PointCloud2 bytes ─K6 unpack→ points ─K7 voxelise (0.2 m pillars, 20 pts,
     20000 voxels, det3d order)→ slot lists ─K8b/K9 MFMA 2-layer PFN + scatter→
-    NHWC bf16 canvas [B,512,512,64] ─RPN + CenterHead (fused MFMA convs)→
+    NHWC canvas [B,512,512,64] ─RPN + CenterHead (fused MFMA convs)→
     merged task maps ─K12 decode/filter (+K13 per-class thresholds)→ candidates
     per (frame, task) ─K10 top-1000 + rotated NMS 0.2 → ≤83 per task
 
 Reference: ``data/nusc_centerpoint_pp_02voxel_two_pfn_10sweep.py``; the
 client's det3d voxeliser ``clients/preprocess/voxelize.py:11-49`` (zero time
 lag as the 5th feature — synthesised inside the PFN kernel, not stored).
-Captured as one hipGraph like the PointPillars pipeline.
+Captured as one hipGraph like the PointPillars pipeline.  ``precision="fp32"``
+(default; the reference's serving precision) keeps fp32 activations with
+split-product MFMA convs and an fp32 PFN/canvas; ``"bf16"`` is the secondary mode.
 """
 from __future__ import annotations
 
@@ -30,8 +32,12 @@ from ..ops.lidar import PointLayout, Voxelizer, pc2_unpack
 class CenterPointPipeline:
     def __init__(self, model: Optional[CenterPoint] = None, batch: int = 16, max_points: int = 131072,
                  layout: Optional[PointLayout] = None, z_offset: float = 0.0, normalize_intensity: bool = True,
-                 device="cuda", cfg: Optional[CenterPointConfig] = None, seed: int = 0, class_thresh=None):
+                 device="cuda", cfg: Optional[CenterPointConfig] = None, seed: int = 0, class_thresh=None,
+                 precision: str = "fp32"):
         self.device = torch.device(device)
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {precision!r}")
+        self.precision = precision
         if self.device.type != "cuda":
             raise ValueError("CenterPointPipeline runs on the GPU; use models.centerpoint on the CPU")
         self.B, self.max_points = batch, max_points
@@ -41,7 +47,8 @@ class CenterPointPipeline:
             model = build_centerpoint(cfg, seed)
         model = fuse_model(model.eval())
         self.cfg = model.cfg
-        self.model = model.to(device=self.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        self.model = model.to(device=self.device, dtype=torch.float32 if precision == "fp32" else torch.bfloat16,
+                              memory_format=torch.channels_last)
         self.frame_bytes = max_points * self.layout.point_step
         self.data = torch.zeros(batch * self.frame_bytes, dtype=torch.uint8, device=self.device)
         self.frame_off = torch.arange(batch, dtype=torch.int64, device=self.device) * self.frame_bytes
@@ -49,7 +56,7 @@ class CenterPointPipeline:
         self.ws = Workspace(self.device)
         v = self.cfg.voxel
         self.vox = Voxelizer(v, batch, max_points, device=self.device, materialize=False)
-        self.enc = PFNEncoder(v, self.model.pfn, batch, device=self.device)
+        self.enc = PFNEncoder(v, self.model.pfn, batch, device=self.device, precision=precision)
         self.class_thresh = class_thresh
         self.fast = None
         self.post = None
@@ -66,7 +73,7 @@ class CenterPointPipeline:
     def build_fast(self):
         from ..models.fast import FastCenterPoint
 
-        self.fast = FastCenterPoint(self.model, self.B, self.device)
+        self.fast = FastCenterPoint(self.model, self.B, self.device, precision=self.precision)
         self.post = CenterPointPostprocess(self.cfg, self.B, self.fast.task_offsets, self.device, self.class_thresh)
         return self.fast
 
