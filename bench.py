@@ -186,7 +186,7 @@ def main():
         from triton_client_amd.pipelines import Yolov4Pipeline
 
         def make_cam(b, m):
-            return Yolov4Pipeline(model=m, batch=b, src_hw=(H0, W0), img=512, device=dev)
+            return Yolov4Pipeline(model=m, batch=b, src_hw=(H0, W0), img=512, device=dev, precision=args.precision)
     elif use_cam and det2:
         from triton_client_amd.config.detectron import DetectronConfig
         from triton_client_amd.pipelines import DetectronPipeline
@@ -551,7 +551,7 @@ def main():
             # BASELINE.json publishes no reference number: nothing to divide by
             "vs_baseline": None,
             # families with an fp32 mode report the mode; the others run bf16 only
-            "dtype": args.precision if (args.camera_model in ("yolov5n", "retinanet", "fcos") or not use_cam)
+            "dtype": args.precision if (args.camera_model in ("yolov5n", "yolov4", "retinanet", "fcos") or not use_cam)
             and (args.lidar_model in ("pointpillars", "centerpoint") or not use_lid) else "bf16",
             "data": (f"synthetic: {nd} distinct {W0}x{H0} "
                      + (f"JPEG (q{args.jpeg_quality}, decoded every step)" if jdec is not None else "uint8 RGB")

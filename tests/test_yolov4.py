@@ -95,3 +95,28 @@ def test_yolov4_pipeline_and_served_model(cuda):
         assert d.shape[1] == 6 and len(d) > 0
         assert d[:, [0, 2]].max() <= 640 + 1e-3
         ch.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fast_graph_gpu_vs_fp64_module(cuda, precision):
+    """The YOLOv4 plan against an fp64 evaluation of the fused module: relative
+    L2 per head below the precision's bound (fp32 split-product 2e-4, bf16 2e-2;
+    tests/test_fast_plans.py PLAN_REL_L2)."""
+    from triton_client_amd.models.fast import FastGraph
+    m = _model()
+    x = torch.rand(2, 3, 128, 128)
+    with torch.no_grad():
+        ref = m.double()(x.double())
+    dt = torch.float32 if precision == "fp32" else torch.bfloat16
+    f = FastGraph(m.float().to(cuda, dt), 2, (128, 128), device=cuda, outputs=YOLOV4_OUTPUTS, precision=precision)
+    f.input_view()[:, :3].copy_(x.to(cuda, dt))
+    outs = f.forward()
+    torch.cuda.synchronize()
+    assert outs[0].t.dtype == dt
+    errs = []
+    for r, o in zip(ref, outs):
+        g = o.nchw()[:, :255].double().cpu()
+        errs.append(((g - r).norm() / r.norm()).item())
+    print(precision, "yolov4 rel L2", errs)
+    assert max(errs) < {"fp32": 2e-4, "bf16": 2e-2}[precision], errs

@@ -583,14 +583,16 @@ class FastGraph:
 
     IN_CHANNELS = 8
 
-    def __init__(self, model, batch: int, img_hw, device="cuda", outputs: Sequence[str] = ()):
+    def __init__(self, model, batch: int, img_hw, device="cuda", outputs: Sequence[str] = (),
+                 precision: str = "bf16"):
         from ..ops.conv import FusedConv
 
         self.device = torch.device(device)
+        self.precision = precision
         B = self.B = batch
         H, W = img_hw
         spec, layers = model.spec, model.layers
-        bufs = self.bufs = _Buffers(self.device)
+        bufs = self.bufs = _Buffers(self.device, precision)
         shape = {"input": (H, W)}
         chan = {"input": self.IN_CHANNELS}
         consumers: dict = {}
@@ -656,7 +658,7 @@ class FastGraph:
             if op == "conv":
                 m = layers[name]
                 assert m.fused, "call fuse_model() first"
-                fc = FusedConv(m.conv, act=m.act, device=device,
+                fc = FusedConv(m.conv, act=m.act, device=device, precision=precision,
                                cin_pad=self.IN_CHANNELS if a["src"] == "input" else None)
                 res = fused_add[name][1] if name in fused_add else None
                 self.ops.append(("conv", fc, a["src"], target, res))

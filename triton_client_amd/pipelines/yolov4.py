@@ -1,7 +1,9 @@
 """2D YOLOv4 pipeline on one GPU (reference ``examples/YOLOv4/config.pbtxt`` model):
 raw uint8 frames → K1 (resize, /255) → CSPDarknet53-SPP-PANet (fused MFMA
 convs, Mish / Leaky epilogues, in-place routes) → K5 decode + filter → K4
-per-class NMS (0.6) with the box rescale → detections.  One hipGraph."""
+per-class NMS (0.6) with the box rescale → detections.  One hipGraph.
+``precision="fp32"`` (default; the served model is FP32, ``examples/YOLOv4/config.pbtxt``):
+fp32 activations with split-product MFMA convs; ``"bf16"`` is the secondary mode."""
 from __future__ import annotations
 
 from typing import Optional, Tuple
@@ -17,14 +19,18 @@ from ..ops.yolov4 import Yolov4Postprocess
 class Yolov4Pipeline:
     def __init__(self, model: Optional[YOLOv4] = None, batch: int = 16, src_hw: Tuple[int, int] = (720, 1280),
                  img: int = 512, nc: int = 80, mode: str = "stretch", conf_thres: float = 0.4,
-                 nms_thres: float = 0.6, device="cuda", seed: int = 0):
+                 nms_thres: float = 0.6, device="cuda", seed: int = 0, precision: str = "fp32"):
         self.device = torch.device(device)
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {precision!r}")
+        self.precision = precision
+        self.dtype = torch.float32 if precision == "fp32" else torch.bfloat16
         if self.device.type != "cuda":
             raise ValueError("Yolov4Pipeline runs on the GPU; use models.yolov4 on the CPU")
         if model is None:
             model = build_yolov4(nc, img, seed)
         model = fuse_model(model.eval())
-        self.model = model.to(device=self.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        self.model = model.to(device=self.device, dtype=self.dtype, memory_format=torch.channels_last)
         self.cfg = model.cfg
         self.B, self.src_hw, self.mode = batch, tuple(src_hw), mode
         self.img_hw = self.cfg.img
@@ -36,14 +42,15 @@ class Yolov4Pipeline:
     def build_fast(self):
         from ..models.fast import FastGraph
 
-        self.fast = FastGraph(self.model, self.B, self.img_hw, self.device, outputs=YOLOV4_OUTPUTS)
+        self.fast = FastGraph(self.model, self.B, self.img_hw, self.device, outputs=YOLOV4_OUTPUTS,
+                              precision=self.precision)
         return self.fast
 
     @torch.no_grad()
     def calibrate_detection_density(self, target_per_frame: float = 100.0, lsuv: bool = True) -> float:
         """LSUV on the current frames, then one logit shift on objectness and
         class biases so ~target rows per frame pass conf > conf_thres."""
-        x, _ = preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", 3)
+        x, _ = preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", 3)
         heads = [self.model.layers[n] for n in YOLOV4_OUTPUTS]
         if lsuv:
             lsuv_rescale(self.model, lambda: self.model(x), head_modules=heads, head_std=1.5)
@@ -77,6 +84,6 @@ class Yolov4Pipeline:
     @torch.no_grad()
     def step(self):
         f = self.fast or self.build_fast()
-        preprocess(self.frames, self.img_hw, self.mode, "COCO", torch.bfloat16, "NHWC", f.IN_CHANNELS,
+        preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", f.IN_CHANNELS,
                    out=f.input_view())
         return self.post(f.forward(), self.xform)
