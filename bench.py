@@ -207,7 +207,8 @@ def main():
         from triton_client_amd.pipelines import SecondPipeline
 
         def make_lid(b, m):
-            return SecondPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5)
+            return SecondPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5,
+                                  precision=args.precision)
     else:
         def make_lid(b, m):
             return LidarPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5,
@@ -552,7 +553,7 @@ def main():
             "vs_baseline": None,
             # families with an fp32 mode report the mode; the others run bf16 only
             "dtype": args.precision if (args.camera_model in ("yolov5n", "yolov4", "retinanet", "fcos") or not use_cam)
-            and (args.lidar_model in ("pointpillars", "centerpoint") or not use_lid) else "bf16",
+            and (args.lidar_model in ("pointpillars", "centerpoint", "second_iou") or not use_lid) else "bf16",
             "data": (f"synthetic: {nd} distinct {W0}x{H0} "
                      + (f"JPEG (q{args.jpeg_quality}, decoded every step)" if jdec is not None else "uint8 RGB")
                      + f" camera frames + {nd} distinct "

@@ -42,6 +42,29 @@ __device__ __forceinline__ long site(const int4& c, const Dims& d) {
   return (((long)c.x * d.z + c.y) * d.y + c.z) * d.x + c.w;
 }
 
+// 8 consecutive channels from fp32 values: one 16-B bf16 store, or two fp32 float4
+// stores (the fp32 precision mode keeps sparse features in fp32)
+__device__ __forceinline__ void store8(__hip_bfloat16* dst, const float* v) {
+  __hip_bfloat16 o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = __float2bfloat16(v[k]);
+  *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
+}
+__device__ __forceinline__ void store8(float* dst, const float* v) {
+  *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void load8(const __hip_bfloat16* src, float* v) {
+  const uint4 q = *reinterpret_cast<const uint4*>(src);
+  const __hip_bfloat16* e = reinterpret_cast<const __hip_bfloat16*>(&q);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = __bfloat162float(e[k]);
+}
+__device__ __forceinline__ void load8(const float* src, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // ---- level 0: MeanVFE + coords + grid ------------------------------------------
 __global__ void sp_offsets_kernel(const int* __restrict__ voxel_count, int batch, int* __restrict__ off,
                                   int* __restrict__ total) {
@@ -57,10 +80,11 @@ __global__ void sp_offsets_kernel(const int* __restrict__ voxel_count, int batch
 
 // From the voxeliser's sorted slot lists (pipeline path: the [V, P, F] voxel
 // tensor is never materialised).  One thread per (frame, voxel).
+template <typename T>
 __global__ void __launch_bounds__(256) sp_vfe_slots_kernel(
     const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ slots,
     const int* __restrict__ vcount, int P, const int* __restrict__ vox_coords, const int* __restrict__ voxel_count,
-    int max_voxels, const int* __restrict__ off, Dims g0, __hip_bfloat16* __restrict__ feats,
+    int max_voxels, const int* __restrict__ off, Dims g0, T* __restrict__ feats,
     int4* __restrict__ coords0, int* __restrict__ grid0) {
   const int b = blockIdx.y, vid = blockIdx.x * 256 + threadIdx.x;
   if (vid >= voxel_count[b]) return;
@@ -73,12 +97,8 @@ __global__ void __launch_bounds__(256) sp_vfe_slots_kernel(
   }
   const float inv = 1.f / (float)max(m, 1);
   const int row = off[b] + vid;
-  __hip_bfloat16 f[8];
-  f[0] = __float2bfloat16(s0 * inv); f[1] = __float2bfloat16(s1 * inv);
-  f[2] = __float2bfloat16(s2 * inv); f[3] = __float2bfloat16(s3 * inv);
-#pragma unroll
-  for (int k = 4; k < 8; ++k) f[k] = __float2bfloat16(0.f);
-  *reinterpret_cast<uint4*>(feats + (long)row * 8) = *reinterpret_cast<const uint4*>(f);
+  const float f[8] = {s0 * inv, s1 * inv, s2 * inv, s3 * inv, 0.f, 0.f, 0.f, 0.f};
+  store8(feats + (long)row * 8, f);
   const int4 c = *reinterpret_cast<const int4*>(vox_coords + g * 4);
   coords0[row] = c;
   grid0[site(c, g0)] = row;
@@ -86,10 +106,11 @@ __global__ void __launch_bounds__(256) sp_vfe_slots_kernel(
 
 // From materialised voxels [V, P, F] (served-model path; OpenPCDet MeanVFE sums
 // all P slots, the padding is zero).  Batch index taken from the coords.
+template <typename T>
 __global__ void __launch_bounds__(256) sp_vfe_voxels_kernel(const float* __restrict__ voxels, int P, int F,
                                                             const int* __restrict__ num_points,
                                                             const int* __restrict__ coords, const int* __restrict__ n_p,
-                                                            Dims g0, __hip_bfloat16* __restrict__ feats,
+                                                            Dims g0, T* __restrict__ feats,
                                                             int4* __restrict__ coords0, int* __restrict__ grid0) {
   const int v = blockIdx.x * 256 + threadIdx.x;
   if (v >= *n_p) return;
@@ -98,12 +119,8 @@ __global__ void __launch_bounds__(256) sp_vfe_voxels_kernel(const float* __restr
 #pragma unroll
     for (int f = 0; f < 4; ++f) s[f] += voxels[((long)v * P + k) * F + f];
   const float inv = 1.f / fmaxf((float)num_points[v], 1.f);
-  __hip_bfloat16 o[8];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) o[f] = __float2bfloat16(s[f] * inv);
-#pragma unroll
-  for (int f = 4; f < 8; ++f) o[f] = __float2bfloat16(0.f);
-  *reinterpret_cast<uint4*>(feats + (long)v * 8) = *reinterpret_cast<const uint4*>(o);
+  const float o[8] = {s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv, 0.f, 0.f, 0.f, 0.f};
+  store8(feats + (long)v * 8, o);
   const int4 c = *reinterpret_cast<const int4*>(coords + (long)v * 4);
   coords0[v] = c;
   grid0[site(c, g0)] = v;
@@ -223,16 +240,16 @@ __global__ void __launch_bounds__(256) sp_grid_reset_kernel(const int4* __restri
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) grid[site(coords[i], d)] = -1;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) sp_bev_clear_kernel(const int4* __restrict__ coords, const int* __restrict__ n_p,
-                                                           int cap, int nch, __hip_bfloat16* __restrict__ bev, int H,
-                                                           int W, int C) {
+                                                           int cap, int nch, T* __restrict__ bev, int H, int W, int C) {
   const int n = min(*n_p, cap);
   const int q = nch >> 3;
+  const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (long i = blockIdx.x * 256 + threadIdx.x; i < (long)n * q; i += gridDim.x * 256) {
     const int row = (int)(i / q), j = (int)(i - (long)row * q);
     const int4 c = coords[row];
-    *reinterpret_cast<uint4*>(bev + (((long)c.x * H + c.z) * W + c.w) * C + c.y * nch + j * 8) =
-        make_uint4(0, 0, 0, 0);
+    store8(bev + (((long)c.x * H + c.z) * W + c.w) * C + c.y * nch + j * 8, z);
   }
 }
 
@@ -418,21 +435,227 @@ __global__ void __launch_bounds__(256) sp_gemm_kernel(SpGemmArgs a) {
   }
 }
 
+// ---- fp32 mode: split-product gather GEMM ----------------------------------------
+// Same rulebook, tap-skipping step list and persistent tile loop as sp_gemm_kernel;
+// rows are fp32 ([*, Cin] float) and the weights are stored pre-split as 8-channel
+// {hi | lo} bf16 pairs ([N, 2 * Kp]).  A K step stages 32 fp32 channels per row
+// (128 B) and 32 channel pairs per weight row (128 B); a fragment read splits the
+// A values into hi / lo bf16 and every fragment pair costs three MFMAs
+// (hi*hi + hi*lo + lo*hi, fp32 accumulation), the conv kernels' x3 scheme.
+struct SpGemmX3Args {
+  const float* in;
+  int cin_log2;
+  const int* nbr;
+  int kt;
+  const unsigned* tapmask;
+  const __hip_bfloat16* w;  // [N, 2 * Kp] pairs
+  const float* bias;
+  int n, kp;
+  const int* m_count;
+  int cap;
+  float* out;
+  const int4* coords;
+  float* bev;
+  int bev_h, bev_w, bev_c;
+  int act;
+};
+
+// 16-B chunk c (0..7) of row r in a [rows][128 B] tile (conflict-free b128 reads)
+__device__ __forceinline__ int swz8(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+__device__ __forceinline__ void split8f(const float4& x0, const float4& x1, bf16x8& h, bf16x8& l) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 hi = (__bf16)v[k];
+    h[k] = hi;
+    l[k] = (__bf16)(v[k] - (float)hi);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256) sp_gemm_x3_kernel(SpGemmX3Args a) {
+  static_assert(WM * WN == 4 && BM == 64, "4 waves, one tap-mask word per tile");
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_CHUNKS = BM * 8, B_CHUNKS = BN * 8;
+  constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  __shared__ int s_nbr[BM * kMaxTaps];
+  __shared__ int s_steps[kMaxSteps];
+  __shared__ int s_nsteps;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = min(*a.m_count, a.cap);
+  const int nk = a.kp / SBK;
+  const int KT = a.kt;
+  const int cmask = (1 << a.cin_log2) - 1;
+
+  for (int tile = blockIdx.x; tile * BM < M; tile += gridDim.x) {
+    const int m0 = tile * BM;
+    const int rows = min(BM, M - m0);
+    for (int i = tid; i < BM * KT; i += 256) s_nbr[i] = (i & 63) < rows ? a.nbr[(long)tile * KT * 64 + i] : -1;
+    if (tid == 0) {
+      const unsigned msk = a.tapmask[tile];
+      int ns = 0;
+      for (int s = 0; s < nk; ++s) {
+        const int t0 = (s * SBK) >> a.cin_log2;
+        if (t0 >= KT) break;
+        const int t1 = min((s * SBK + SBK - 1) >> a.cin_log2, KT - 1);
+        const int w = t1 - t0 + 1;
+        const unsigned sm = (w >= 32 ? 0xffffffffu : ((1u << w) - 1u)) << t0;
+        if (msk & sm) s_steps[ns++] = s;
+      }
+      s_nsteps = ns;
+    }
+    __syncthreads();
+    const int ns = s_nsteps;
+
+    uint4 ra[A_PER_T], rb[B_PER_T];
+    auto load_tiles = [&](int s) {
+#pragma unroll
+      for (int t = 0; t < A_PER_T; ++t) {
+        const int id = tid + t * 256;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < A_CHUNKS) {
+          const int row = id >> 3, k0 = s * SBK + (id & 7) * 4;
+          const int tap = k0 >> a.cin_log2;
+          if (tap < KT) {
+            const int r = s_nbr[tap * 64 + row];
+            if (r >= 0) v = *reinterpret_cast<const uint4*>(a.in + ((long)r << a.cin_log2) + (k0 & cmask));
+          }
+        }
+        ra[t] = v;
+      }
+#pragma unroll
+      for (int t = 0; t < B_PER_T; ++t) {
+        const int id = tid + t * 256;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (id < B_CHUNKS) {
+          const int nn = id >> 3;
+          if (nn < a.n) v = *reinterpret_cast<const uint4*>(a.w + (long)nn * 2 * a.kp + s * 2 * SBK + (id & 7) * 8);
+        }
+        rb[t] = v;
+      }
+    };
+    auto store_tiles = [&](int buf) {
+      unsigned char* sa = smem + buf * STAGE;
+      unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+      for (int t = 0; t < A_PER_T; ++t) {
+        const int id = tid + t * 256;
+        if (id < A_CHUNKS) *reinterpret_cast<uint4*>(sa + swz8(id >> 3, id & 7)) = ra[t];
+      }
+#pragma unroll
+      for (int t = 0; t < B_PER_T; ++t) {
+        const int id = tid + t * 256;
+        if (id < B_CHUNKS) *reinterpret_cast<uint4*>(sb + swz8(id >> 3, id & 7)) = rb[t];
+      }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (ns > 0) {
+      load_tiles(s_steps[0]);
+      store_tiles(0);
+    }
+    __syncthreads();
+    for (int i = 0; i < ns; ++i) {
+      const int cur = i & 1;
+      if (i + 1 < ns) load_tiles(s_steps[i + 1]);
+      const unsigned char* sa = smem + cur * STAGE;
+      const unsigned char* sb = sa + A_BYTES;
+      bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+      for (int x = 0; x < FM; ++x) {
+        const int r = wm * TM + x * 16 + fr;
+        const float4 x0 = *reinterpret_cast<const float4*>(sa + swz8(r, 2 * fq));
+        const float4 x1 = *reinterpret_cast<const float4*>(sa + swz8(r, 2 * fq + 1));
+        split8f(x0, x1, ah[x], al[x]);
+      }
+#pragma unroll
+      for (int y = 0; y < FN; ++y) {
+        const int r = wn * TN + y * 16 + fr;
+        bh[y] = *reinterpret_cast<const bf16x8*>(sb + swz8(r, 2 * fq));
+        bl[y] = *reinterpret_cast<const bf16x8*>(sb + swz8(r, 2 * fq + 1));
+      }
+#pragma unroll
+      for (int x = 0; x < FM; ++x)
+#pragma unroll
+        for (int y = 0; y < FN; ++y) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[y], ah[x], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[y], al[x], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[y], ah[x], acc[x][y], 0, 0, 0);
+        }
+      if (i + 1 < ns) store_tiles(cur ^ 1);
+      __syncthreads();
+    }
+
+    constexpr int LD = BN + 4;
+    float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int x = 0; x < FM; ++x) {
+      const int ml = wm * TM + x * 16 + fr;
+#pragma unroll
+      for (int y = 0; y < FN; ++y) {
+        const int nl = wn * TN + y * 16 + fq * 4;
+        float q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nn = nl + r;
+          float v = acc[x][y][r];
+          if (nn < a.n) v += a.bias[nn];
+          if (a.act == 1) v = fmaxf(v, 0.f);
+          q[r] = v;
+        }
+        *reinterpret_cast<float4*>(st + ml * LD + nl) = make_float4(q[0], q[1], q[2], q[3]);
+      }
+    }
+    __syncthreads();
+    constexpr int VPR = BN / 4;
+    for (int id = tid; id < BM * VPR; id += 256) {
+      const int ml = id / VPR, c4 = (id % VPR) * 4;
+      if (ml >= rows || c4 >= a.n) continue;
+      const int m = m0 + ml;
+      const float4 v = *reinterpret_cast<const float4*>(st + ml * LD + c4);
+      long o;
+      if (a.bev) {
+        const int4 c = a.coords[m];
+        o = (((long)c.x * a.bev_h + c.z) * a.bev_w + c.w) * a.bev_c + (long)c.y * a.n + c4;
+      } else {
+        o = (long)m * a.n + c4;
+      }
+      *reinterpret_cast<float4*>((a.bev ? a.bev : a.out) + o) = v;
+    }
+    __syncthreads();
+  }
+}
+
 // ---- SECONDHead RoI grid pool ------------------------------------------------------
 // One block per RoI; affine_grid + grid_sample(bilinear, zeros,
 // align_corners=False) exactly as PyTorch evaluates them; a lane handles 8
 // channels of one grid point (16-B corner loads, a wave reads 1 KiB of
 // contiguous NHWC channels per corner).  Output row = (gy, gx, c).
-__global__ void __launch_bounds__(256) roi_grid_pool_kernel(const __hip_bfloat16* __restrict__ feat, int H, int W,
+template <typename T>
+__global__ void __launch_bounds__(256) roi_grid_pool_kernel(const T* __restrict__ feat, int H, int W,
                                                             int C, int ldc, int coff, const float* __restrict__ rois,
                                                             int rdim, const int* __restrict__ roi_count, int R,
                                                             float min_x, float min_y, float cell_x, float cell_y, int G,
-                                                            __hip_bfloat16* __restrict__ out) {
+                                                            T* __restrict__ out) {
   const int b = blockIdx.y, r = blockIdx.x;
   const int q = C >> 3;
-  __hip_bfloat16* dst = out + ((long)b * R + r) * G * G * C;
+  T* dst = out + ((long)b * R + r) * G * G * C;
   if (r >= roi_count[b]) {
-    for (int i = threadIdx.x; i < G * G * q; i += 256) reinterpret_cast<uint4*>(dst)[i] = make_uint4(0, 0, 0, 0);
+    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < G * G * q; i += 256) store8(dst + i * 8, z);
     return;
   }
   const float* ro = rois + ((long)b * R + r) * rdim;
@@ -443,7 +666,7 @@ __global__ void __launch_bounds__(256) roi_grid_pool_kernel(const __hip_bfloat16
   const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
   const float t00 = (x2 - x1) / wm1 * ca, t01 = (x2 - x1) / wm1 * (-sa), t02 = (x1 + x2 - wm1) / wm1;
   const float t10 = (y2 - y1) / hm1 * sa, t11 = (y2 - y1) / hm1 * ca, t12 = (y1 + y2 - hm1) / hm1;
-  const __hip_bfloat16* fb = feat + (long)b * H * W * ldc + coff;
+  const T* fb = feat + (long)b * H * W * ldc + coff;
   for (int i = threadIdx.x; i < G * G * q; i += 256) {
     const int p = i / q, c8 = (i - p * q) * 8;
     const int gy = p / G, gx = p - gy * G;
@@ -461,15 +684,12 @@ __global__ void __launch_bounds__(256) roi_grid_pool_kernel(const __hip_bfloat16
         const int xx = x0 + cx, yy = y0 + cy;
         if ((unsigned)xx >= (unsigned)W || (unsigned)yy >= (unsigned)H) continue;
         const float wgt = (cx ? wx1 : wx0) * (cy ? wy1 : wy0);
-        const uint4 v = *reinterpret_cast<const uint4*>(fb + ((long)yy * W + xx) * ldc + c8);
-        const __hip_bfloat16* e = reinterpret_cast<const __hip_bfloat16*>(&v);
+        float e[8];
+        load8(fb + ((long)yy * W + xx) * ldc + c8, e);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += wgt * __bfloat162float(e[k]);
+        for (int k = 0; k < 8; ++k) acc[k] += wgt * e[k];
       }
-    __hip_bfloat16 o[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = __float2bfloat16(acc[k]);
-    *reinterpret_cast<uint4*>(dst + (long)p * C + c8) = *reinterpret_cast<const uint4*>(o);
+    store8(dst + (long)p * C + c8, acc);
   }
 }
 
@@ -537,12 +757,34 @@ TCA_API int tca_sp_vfe_slots(const float* pts, int pstride, int max_points, cons
   TCA_LAUNCH_CHECK();
 }
 
+// fp32 mode twin: feats [cap0, 8] fp32.
+TCA_API int tca_sp_vfe_slots_f32(const float* pts, int pstride, int max_points, const int* slots, const int* vcount,
+                                 int P, const int* vox_coords, const int* voxel_count, int batch, int max_voxels,
+                                 const int* off, const int* dims0, void* feats, int* coords0, int* grid0,
+                                 hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (pstride < 4 || (pstride & 3)) return (int)hipErrorInvalidValue;
+  sp_vfe_slots_kernel<<<dim3((max_voxels + 255) / 256, batch), 256, 0, stream>>>(
+      pts, pstride, max_points, slots, vcount, P, vox_coords, voxel_count, max_voxels, off, make_dims(dims0),
+      (float*)feats, (int4*)coords0, grid0);
+  TCA_LAUNCH_CHECK();
+}
+
 TCA_API int tca_sp_vfe_voxels(const float* voxels, int cap, int P, int F, const int* num_points, const int* coords,
                               const int* n, const int* dims0, void* feats, int* coords0, int* grid0,
                               hipStream_t stream) {
   if (F < 4) return (int)hipErrorInvalidValue;
   sp_vfe_voxels_kernel<<<grid_for(cap, 256, 1 << 20), 256, 0, stream>>>(
       voxels, P, F, num_points, coords, n, make_dims(dims0), (__hip_bfloat16*)feats, (int4*)coords0, grid0);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_sp_vfe_voxels_f32(const float* voxels, int cap, int P, int F, const int* num_points, const int* coords,
+                                  const int* n, const int* dims0, void* feats, int* coords0, int* grid0,
+                                  hipStream_t stream) {
+  if (F < 4) return (int)hipErrorInvalidValue;
+  sp_vfe_voxels_kernel<<<grid_for(cap, 256, 1 << 20), 256, 0, stream>>>(
+      voxels, P, F, num_points, coords, n, make_dims(dims0), (float*)feats, (int4*)coords0, grid0);
   TCA_LAUNCH_CHECK();
 }
 
@@ -580,6 +822,14 @@ TCA_API int tca_sp_bev_clear(const int* coords, const int* n, int cap, int nch, 
   TCA_LAUNCH_CHECK();
 }
 
+TCA_API int tca_sp_bev_clear_f32(const int* coords, const int* n, int cap, int nch, void* bev, int H, int W, int C,
+                                 hipStream_t stream) {
+  if (nch & 7) return (int)hipErrorInvalidValue;
+  sp_bev_clear_kernel<<<grid_for((long)cap * (nch / 8), 256, 4096), 256, 0, stream>>>(
+      (const int4*)coords, n, cap, nch, (float*)bev, H, W, C);
+  TCA_LAUNCH_CHECK();
+}
+
 // out = relu?(gather(in, nbr) @ W^T + bias) over the device row count.
 // Contract: Cin a power of two >= 8, KT <= 27, Kp % 32 == 0, Kp / 32 <= 64,
 // N % 8 == 0 and N <= 128; bev != null -> scatter rows into the NHWC map.
@@ -601,6 +851,25 @@ TCA_API int tca_sp_gemm(const void* in, int cin, const int* nbr, int kt, const u
   TCA_LAUNCH_CHECK();
 }
 
+// fp32 mode twin of tca_sp_gemm: in / out / bev fp32, w [N, 2 * Kp] {hi | lo} pairs per 8 channels.
+TCA_API int tca_sp_gemm_x3(const void* in, int cin, const int* nbr, int kt, const unsigned* tapmask, const void* w,
+                           const float* bias, int n, int kp, const int* m_count, int cap, void* out, const int* coords,
+                           void* bev, int bev_h, int bev_w, int bev_c, int act, hipStream_t stream) {
+  int lg = 0;
+  while ((1 << lg) < cin) ++lg;
+  if ((1 << lg) != cin || cin < 8 || kt > kMaxTaps || (kp % SBK) || kp / SBK > kMaxSteps || (n & 7) || n > 128 ||
+      kp < kt * cin)
+    return (int)hipErrorInvalidValue;
+  SpGemmX3Args a{(const float*)in, lg, nbr, kt, tapmask, (const __hip_bfloat16*)w, bias, n, kp, m_count, cap,
+                 (float*)out, (const int4*)coords, (float*)bev, bev_h, bev_w, bev_c, act};
+  const int grid = grid_for(cap, 64, 1024);
+  if (n <= 16) sp_gemm_x3_kernel<64, 16, 4, 1><<<grid, 256, 0, stream>>>(a);
+  else if (n <= 32) sp_gemm_x3_kernel<64, 32, 4, 1><<<grid, 256, 0, stream>>>(a);
+  else if (n <= 64) sp_gemm_x3_kernel<64, 64, 2, 2><<<grid, 256, 0, stream>>>(a);
+  else sp_gemm_x3_kernel<64, 128, 2, 2><<<grid, 256, 0, stream>>>(a);
+  TCA_LAUNCH_CHECK();
+}
+
 // feat: NHWC [B, H, W, ldc], channels [coff, coff + C); rois [B, R, rdim]
 // (x, y, z, dx, dy, dz, yaw, ...); out [B * R, G * G * C] bf16 in (gy, gx, c) order.
 TCA_API int tca_roi_grid_pool(const void* feat, int batch, int H, int W, int C, int ldc, int coff, const float* rois,
@@ -611,6 +880,17 @@ TCA_API int tca_roi_grid_pool(const void* feat, int batch, int H, int W, int C, 
   roi_grid_pool_kernel<<<dim3(R, batch), 256, 0, stream>>>((const __hip_bfloat16*)feat, H, W, C, ldc, coff, rois, rdim,
                                                            roi_count, R, min_x, min_y, cell_x, cell_y, G,
                                                            (__hip_bfloat16*)out);
+  TCA_LAUNCH_CHECK();
+}
+
+TCA_API int tca_roi_grid_pool_f32(const void* feat, int batch, int H, int W, int C, int ldc, int coff,
+                                  const float* rois, int rdim, const int* roi_count, int R, float min_x, float min_y,
+                                  float cell_x, float cell_y, int G, void* out, hipStream_t stream) {
+  if (batch <= 0 || R <= 0) return 0;
+  if ((C & 7) || (ldc & 7) || (coff & 7) || rdim < 7) return (int)hipErrorInvalidValue;
+  roi_grid_pool_kernel<<<dim3(R, batch), 256, 0, stream>>>((const float*)feat, H, W, C, ldc, coff, rois, rdim,
+                                                           roi_count, R, min_x, min_y, cell_x, cell_y, G,
+                                                           (float*)out);
   TCA_LAUNCH_CHECK();
 }
 

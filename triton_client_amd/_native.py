@@ -84,6 +84,11 @@ _KERNEL_SIGS = {
     "tca_sp_grid_reset": [P, P, I, P, P, P],
     "tca_sp_bev_clear": [P, P, I, I, P, I, I, I, P],
     "tca_sp_gemm": [P, I, P, I, P, P, P, I, I, P, I, P, P, P, I, I, I, I, P],
+    "tca_sp_vfe_slots_f32": [P, I, I, P, P, I, P, P, I, I, P, P, P, P, P, P],
+    "tca_sp_vfe_voxels_f32": [P, I, I, I, P, P, P, P, P, P, P, P],
+    "tca_sp_bev_clear_f32": [P, P, I, I, P, I, I, I, P],
+    "tca_roi_grid_pool_f32": [P, I, I, I, I, I, I, P, I, P, I, F, F, F, F, I, P, P],
+    "tca_sp_gemm_x3": [P, I, P, I, P, P, P, I, I, P, I, P, P, P, I, I, I, I, P],
     "tca_roi_grid_pool": [P, I, I, I, I, I, I, P, I, P, I, F, F, F, F, I, P, P],
     "tca_roi_rescore": [P, P, I, P, P, I, I, F, P, P, P, P, P, P],
 }

@@ -33,6 +33,7 @@ import torch
 from .. import _native
 from ..config.lidar import SecondIoUConfig, SparseConvSpec
 from ._ws import Workspace
+from .conv import split_pairs
 from .nms import Candidates, NmsResult, sort_and_nms
 
 
@@ -82,9 +83,17 @@ def _pow2_at_least(c: int, lo: int = 8) -> int:
 class SparseBackbone:
     """GPU executor of MeanVFE + VoxelBackBone8x + HeightCompression."""
 
-    def __init__(self, cfg: SecondIoUConfig, layers, batch: int, device="cuda", max_rows0: Optional[int] = None):
-        """layers: the BN-folded :class:`~..models.second.SparseConv3d` modules."""
+    def __init__(self, cfg: SecondIoUConfig, layers, batch: int, device="cuda", max_rows0: Optional[int] = None,
+                 precision: str = "bf16"):
+        """layers: the BN-folded :class:`~..models.second.SparseConv3d` modules.
+        precision "fp32": fp32 rows / BEV map, weights as {hi | lo} bf16 pairs,
+        split-product gather GEMMs (tca_sp_gemm_x3)."""
         self.cfg, self.B = cfg, batch
+        self.f32 = precision == "fp32"
+        fdt = torch.float32 if self.f32 else torch.bfloat16
+        sfx = "_f32" if self.f32 else ""
+        self._k_vfe_slots, self._k_vfe_voxels = "tca_sp_vfe_slots" + sfx, "tca_sp_vfe_voxels" + sfx
+        self._k_bev_clear, self._k_gemm = "tca_sp_bev_clear" + sfx, "tca_sp_gemm_x3" if self.f32 else "tca_sp_gemm"
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("SparseBackbone runs on the GPU; models.second is the CPU path")
@@ -97,11 +106,11 @@ class SparseBackbone:
         cap0 = max_rows0 or batch * cfg.voxel.max_voxels
         self.levels: List[_Level] = []
         self.levels.append(self._new_level(0, shapes[0], cap0))
-        self.feats0 = ws.get("sp_feats0", (cap0, 8), torch.bfloat16, init=0)
+        self.feats0 = ws.get("sp_feats0", (cap0, 8), fdt, init=0)
         C, D = specs[-1].cout, shapes[-1][0]
         _, Hb, Wb = cfg.bev_shape
         self.bev_c = C * D
-        self.bev = ws.get("sp_bev", (batch, Hb, Wb, self.bev_c), torch.bfloat16, init=0)
+        self.bev = ws.get("sp_bev", (batch, Hb, Wb, self.bev_c), fdt, init=0)
         self.layers: List[_Layer] = []
         cur = 0
         x = self.feats0
@@ -127,7 +136,8 @@ class SparseBackbone:
             W[:, :K] = wk.reshape(spec.cout, K)
             bias = mod.bias.detach().float() if mod.bias is not None else torch.zeros(spec.cout)
             ksp = _iarr(list(spec.kernel) + list(spec.stride) + list(spec.padding))
-            L = _Layer(spec, cur, cin_p, W.to(self.device, torch.bfloat16).contiguous(),
+            Wd = split_pairs(W).to(self.device) if self.f32 else W.to(self.device, torch.bfloat16).contiguous()
+            L = _Layer(spec, cur, cin_p, Wd,
                        bias.to(self.device).contiguous(), kp, ksp)
             if spec.subm:
                 if lev.subm_nbr is None:
@@ -143,7 +153,7 @@ class SparseBackbone:
                 L.out = None
             else:
                 if lev.bufs is None or lev.bufs[0].shape[1] != spec.cout:
-                    lev.bufs = [ws.get(f"sp_f{cur}_{spec.cout}_{k}", (lev.cap, spec.cout), torch.bfloat16)
+                    lev.bufs = [ws.get(f"sp_f{cur}_{spec.cout}_{k}", (lev.cap, spec.cout), fdt)
                                 for k in range(2)]
                 L.out = lev.bufs[0] if L.inp is not lev.bufs[0] else lev.bufs[1]
                 x = L.out
@@ -175,7 +185,7 @@ class SparseBackbone:
         P = _native.ptr
         last = self.levels[-1]
         Hb, Wb = self._bev_hw
-        _native.call("tca_sp_bev_clear", P(last.coords), self._cnt(last), last.cap, self.layers[-1].spec.cout,
+        _native.call(self._k_bev_clear, P(last.coords), self._cnt(last), last.cap, self.layers[-1].spec.cout,
                      P(self.bev), Hb, Wb, self.bev_c, s)
         for lev in self.levels:
             _native.call("tca_sp_grid_reset", P(lev.coords), self._cnt(lev), lev.cap, lev.dims, P(lev.grid), s)
@@ -188,7 +198,7 @@ class SparseBackbone:
         l0 = self.levels[0]
         v = self.cfg.voxel
         _native.call("tca_sp_offsets", P(vox.voxel_count), self.B, P(self.off), self._cnt(l0), s)
-        _native.call("tca_sp_vfe_slots", P(points), points.shape[-1], vox.max_points, P(vox.slots), P(vox.vcount),
+        _native.call(self._k_vfe_slots, P(points), points.shape[-1], vox.max_points, P(vox.slots), P(vox.vcount),
                      v.max_points_per_voxel, P(vox.coords), P(vox.voxel_count), self.B, v.max_voxels, P(self.off),
                      l0.dims, P(self.feats0), P(l0.coords), P(l0.grid), s)
 
@@ -200,7 +210,7 @@ class SparseBackbone:
         P = _native.ptr
         l0 = self.levels[0]
         self.counts[0:1].copy_(n)
-        _native.call("tca_sp_vfe_voxels", P(voxels), voxels.shape[0], voxels.shape[1], voxels.shape[2],
+        _native.call(self._k_vfe_voxels, P(voxels), voxels.shape[0], voxels.shape[1], voxels.shape[2],
                      P(num_points), P(coords), P(n), l0.dims, P(self.feats0), P(l0.coords), P(l0.grid), s)
 
     def forward(self, stream=None) -> torch.Tensor:
@@ -222,7 +232,7 @@ class SparseBackbone:
                              P(lev.grid), P(L.nbr), P(L.mask), s)
                 built.add(L.level)
             last = L.out is None
-            _native.call("tca_sp_gemm", P(L.inp), L.cin_p, P(L.nbr), L.spec.taps, P(L.mask), P(L.w), P(L.b),
+            _native.call(self._k_gemm, P(L.inp), L.cin_p, P(L.nbr), L.spec.taps, P(L.mask), P(L.w), P(L.b),
                          L.spec.cout, L.kp, self._cnt(lev), lev.cap, P(L.out), P(lev.coords),
                          P(self.bev) if last else 0, Hb, Wb, self.bev_c, 1, s)
         return self.bev
@@ -236,8 +246,11 @@ class RoIHead:
     """SECONDHead on the GPU: RoI grid pool (HIP) → BN-folded FC stack
     (hipBLASLt) → sigmoid(IoU) rescoring (HIP) → rotated NMS (K10)."""
 
-    def __init__(self, cfg: SecondIoUConfig, head, batch: int, feat_channels: int, device="cuda"):
+    def __init__(self, cfg: SecondIoUConfig, head, batch: int, feat_channels: int, device="cuda",
+                 precision: str = "bf16"):
         self.cfg, self.B = cfg, batch
+        self.f32 = precision == "fp32"
+        adt = torch.float32 if self.f32 else torch.bfloat16
         self.device = torch.device(device)
         self.R, self.G, self.C = cfg.proposal_post_max, cfg.roi_grid, feat_channels
         lin = head.folded_linears()
@@ -246,15 +259,15 @@ class RoIHead:
         # OpenPCDet flattens pooled [N, C, G, G] as (c, gy, gx); the kernel writes (gy, gx, c)
         w0 = w0.view(w0.shape[0], C, G, G).permute(0, 2, 3, 1).reshape(w0.shape[0], -1)
         lin = [(w0, b0, r0)] + lin[1:]
-        self.mid = [(w.t().contiguous().to(self.device, torch.bfloat16), b.to(self.device, torch.bfloat16), r)
+        self.mid = [(w.t().contiguous().to(self.device, adt), b.to(self.device, adt), r)
                     for w, b, r in lin[:-1]]
         wl, bl, _ = lin[-1]
         self.w_last = wl.t().contiguous().to(self.device, torch.float32)  # [256, 1]
         self.b_last = bl.to(self.device, torch.float32)
         self.ws = Workspace(self.device)
         N = batch * self.R
-        self.pooled = self.ws.get("roi_pooled", (N, G * G * C), torch.bfloat16, init=0)
-        self.acts = [self.ws.get(f"roi_act{i}", (N, w.shape[1]), torch.bfloat16) for i, (w, _, _) in
+        self.pooled = self.ws.get("roi_pooled", (N, G * G * C), adt, init=0)
+        self.acts = [self.ws.get(f"roi_act{i}", (N, w.shape[1]), adt) for i, (w, _, _) in
                      enumerate(self.mid)]
         self.logit = self.ws.get("roi_logit", (N, 1), torch.float32)
         v = cfg.voxel
@@ -268,7 +281,7 @@ class RoIHead:
         the proposal NMS result (box [B, R, 7], cls, count).  → [B*R, 1] fp32."""
         B, H, W, ldc = feat.shape
         assert props.box.shape[1] == self.R and B == self.B
-        _native.call("tca_roi_grid_pool", _native.ptr(feat), B, H, W, self.C, ldc, coff, _native.ptr(props.box),
+        _native.call("tca_roi_grid_pool_f32" if self.f32 else "tca_roi_grid_pool", _native.ptr(feat), B, H, W, self.C, ldc, coff, _native.ptr(props.box),
                      props.box.shape[2], _native.ptr(props.count), self.R, *self.geom, self.G,
                      _native.ptr(self.pooled), _native.stream_ptr(stream))
         x = self.pooled

@@ -34,10 +34,17 @@ from ..ops.spconv import RoIHead, SparseBackbone
 class SecondPipeline:
     def __init__(self, model: Optional[SECONDNetIoU] = None, batch: int = 16, max_points: int = 131072,
                  layout: Optional[PointLayout] = None, z_offset: float = 1.5, normalize_intensity: bool = True,
-                 device="cuda", cfg: Optional[SecondIoUConfig] = None, seed: int = 0, from_voxels: bool = False):
+                 device="cuda", cfg: Optional[SecondIoUConfig] = None, seed: int = 0, from_voxels: bool = False,
+                 precision: str = "fp32"):
         """from_voxels: the served-model variant (level 0 comes from received
-        voxels via :meth:`run_voxels`; no point-cloud buffers)."""
+        voxels via :meth:`run_voxels`; no point-cloud buffers).  precision
+        "fp32" (default; the reference serves SECOND-IoU in fp32): fp32 sparse
+        rows, BEV maps and RoI features with split-product MFMA GEMMs / convs;
+        "bf16": the secondary mode."""
         self.device = torch.device(device)
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision {precision!r}")
+        self.precision = precision
         if self.device.type != "cuda":
             raise ValueError("SecondPipeline runs on the GPU; use models.second on the CPU")
         self.B, self.max_points = batch, max_points
@@ -66,7 +73,7 @@ class SecondPipeline:
         """(Re)build the GPU plans from the current weights."""
         cfg = self.cfg
         self.sparse = SparseBackbone(cfg, self.model.backbone3d.layers, self.B, self.device,
-                                     max_rows0=self.B * cfg.voxel.max_voxels)
+                                     max_rows0=self.B * cfg.voxel.max_voxels, precision=self.precision)
         # the GPU BEV map is z-level-major (channel z*128 + c): permute the first
         # 2D conv's input channels to match (models.second.bev_channel_permutation)
         bb = copy.deepcopy(self.model.backbone)
@@ -76,8 +83,8 @@ class SecondPipeline:
             first.weight.copy_(first.weight[:, perm])
         shim = types.SimpleNamespace(cfg=cfg, backbone=bb, head=self.model.head)
         _, Hb, Wb = cfg.bev_shape
-        self.fast = FastBEVPlan(shim, self.B, self.device, (Hb, Wb))
-        self.roi = RoIHead(cfg, self.model.roi_head, self.B, self.fast.cat_channels, self.device)
+        self.fast = FastBEVPlan(shim, self.B, self.device, (Hb, Wb), self.precision)
+        self.roi = RoIHead(cfg, self.model.roi_head, self.B, self.fast.cat_channels, self.device, self.precision)
         return self
 
     # ------------------------------------------------------------------ calibration
@@ -193,9 +200,10 @@ class FastBEVPlan:
     """BaseBEVBackbone + merged anchor head on the fused convs, keeping the
     512-channel concat (SECONDHead pools its RoI grids from it)."""
 
-    def __init__(self, shim, batch: int, device, bev_hw):
+    def __init__(self, shim, batch: int, device, bev_hw, precision: str = "bf16"):
         from ..models.fast import FastBEV
-        self.plan = FastBEV(shim, batch, device, fused_neck=False, bev_hw=bev_hw)
+        # fp32: plain fp32 activations (the sparse BEV map is fp32 rows; SECONDHead pools the concat)
+        self.plan = FastBEV(shim, batch, device, fused_neck=False, bev_hw=bev_hw, precision=precision, pair=False)
         self.cat = self.plan.cat
         self.cat_channels = self.cat.t.shape[-1]
 
