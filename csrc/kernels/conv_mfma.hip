@@ -1486,6 +1486,200 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
   epilogue_f32<BM, BN, WM, WN, PAIR_OUT>(a, acc, smem, m0, n0);
 }
 
+// ---- x3 pair, halo-tiled 3x3 stride 1 ("hx"): the xb kernel re-reads every
+// input pixel once per tap (9x the activation bytes through L2 -> LDS, a fresh
+// A tile per K step).  Here a workgroup owns a 2D output tile of TH rows x 16
+// columns; per 32-channel chunk it stages the (TH + 2) x 18 halo ONCE (buffer-
+// descriptor LDS DMA, zero padding by the range check) and runs the chunk's 9
+// tap steps from it, only the weight tile (BN x 32 channel pairs) streaming per
+// step through a 2-deep ring.  A fragment is one output row of 16 pixels, i.e. 16
+// consecutive halo rows at any base (ky * 18 + kx + row offset), so the 16-row
+// periodic slot swizzle keeps the b128 fragment reads conflict-free.  K order is
+// (chunk, tap) instead of xb's (tap, chunk): same products, different fp32
+// summation order (not bit-identical to xb; same accuracy vs fp64).
+template <int TH, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
+  constexpr int TW = 16, BM = TH * TW, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  static_assert(TM % 16 == 0 && TN % 16 == 0, "fragments");
+  constexpr int HWD = TW + 2, HROWS = (TH + 2) * HWD;
+  constexpr int HINS = (HROWS + 7) / 8;  // 8-row (1 KiB) DMA instructions per chunk
+  constexpr int HPW = (HINS + NW - 1) / NW;
+  constexpr int HBYTES = HINS * 1024, BBYTES = BN * 128;
+  static_assert(BN % (8 * NW) == 0, "weight rows split over the waves' 8-row DMAs");
+  constexpr int B_INS = BN / (8 * NW);
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int RING = 2 * HBYTES + 2 * BBYTES;
+  constexpr int LDS = RING > EPI ? RING : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+  unsigned char* const halo = smem;
+  unsigned char* const bring = smem + 2 * HBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int tx_n = (a.Wo + TW - 1) / TW, ty_n = (a.Ho + TH - 1) / TH;
+  const int nmt = a.B * ty_n * tx_n, nnt = (a.N + BN - 1) / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
+  const int oy0 = (rem / tx_n) * TH, ox0 = (rem - (rem / tx_n) * tx_n) * TW;
+  const int n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.N * a.Kp * 4, 0x00020000);
+
+  const int lrow = lane >> 3, lslot = lane & 7;
+  unsigned h_off[HPW];  // byte offset of this lane's 16-B piece of halo row p (chunk 0)
+#pragma unroll
+  for (int j = 0; j < HPW; ++j) {
+    const int p = (wid + j * NW) * 8 + lrow;
+    const int hy = p / HWD, hx = p - (p / HWD) * HWD;
+    const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+    const bool ok = p < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    h_off[j] = ok ? (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + (lslot ^ swzp(p)) * 4) * 4)
+                  : kOutOfRange;
+  }
+  unsigned b_off[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wid * B_INS + j) * 8 + lrow;
+    const int n = n0 + row;
+    b_off[j] = n < a.N ? (unsigned)(n * 2 * a.Kp + (lslot ^ swzp(row)) * 8) * 2u : kOutOfRange;
+  }
+  auto issue_halo = [&](int buf, int c) {
+    unsigned char* dst = halo + buf * HBYTES;
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) {
+      const int ins = wid + j * NW;  // wave-uniform
+      if (ins < HINS) bdma16(h_off[j], rin, dst + ins * 1024, (unsigned)c * 128u);
+    }
+  };
+  auto issue_b = [&](int buf, int kt) {
+    unsigned char* dst = bring + buf * BBYTES + __builtin_amdgcn_readfirstlane(wid) * (B_INS * 1024);
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) bdma16(b_off[j], rw, dst + j * 1024, (unsigned)kt * 128u);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nc = a.Cin / 32, S = 9 * nc;
+  issue_halo(0, 0);
+  issue_b(0, 0);  // step 0 = (chunk 0, tap 0): weight K step tap * nc + chunk = 0
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sb_ = swzp(fr);
+  const int b_hi = (wn * TN + fr) * 128 + (((2 * fq) ^ sb_) << 4);
+  const int b_lo = (wn * TN + fr) * 128 + (((2 * fq + 1) ^ sb_) << 4);
+  int c = 0, t = 0;
+  for (int s = 0; s < S; ++s) {
+    // everything in flight is this step's weights (and at t == 0 the chunk's halo)
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int c1 = t == 8 ? c + 1 : c, t1 = t == 8 ? 0 : t + 1;
+    if (s + 1 < S) {
+      // the next halo buffer was last read in chunk c - 1: every wave is past it (barrier)
+      if (t1 == 0) issue_halo(c1 & 1, c1);
+      issue_b((s + 1) & 1, t1 * nc + c1);
+    }
+    const unsigned char* hb = halo + (c & 1) * HBYTES;
+    const unsigned char* bb = bring + (s & 1) * BBYTES;
+    const int ky = t / 3, kx = t - (t / 3) * 3;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(bb + b_hi + j * 16 * 128);
+      bl[j] = *reinterpret_cast<const bf16x8*>(bb + b_lo + j * 16 * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int hp = (wm * FM + i + ky) * HWD + kx + fr;
+      const int sw = swzp(hp);
+      ah[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
+      al[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+    __builtin_amdgcn_s_setprio(0);
+    c = c1;
+    t = t1;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the ring LDS
+  asm volatile("" ::: "memory");
+
+  // epilogue: tile row ml = (output row within the tile) * 16 + column
+  constexpr int LD = BN + 4;
+  float* st = reinterpret_cast<float*>(smem);
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = wm * TM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int nl = wn * TN + j * 16 + fq * 4;
+      float4 q;
+      float* qv = reinterpret_cast<float*>(&q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + nl + r;
+        float v = acc[i][j][r];
+        if (a.bias && n < a.N) v += a.bias[n];
+        qv[r] = post_res ? v : act_fn(v, act);
+      }
+      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+    }
+  }
+  __syncthreads();
+  constexpr int V8 = BN / 8;
+  for (int id = tid; id < BM * V8; id += NW * 64) {
+    const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
+    const int oy = oy0 + ml / TW, ox = ox0 + (ml & (TW - 1)), n = n0 + c8;
+    if (oy >= a.Ho || ox >= a.Wo || n >= a.N) continue;
+    float v[8];
+    const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
+    const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
+    if (a.res_f) {
+      float r[8];
+      pair_join8(a.res_f + pix * a.ldr + a.r_off + n, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
+    }
+    uint4 hi, lo;
+    pair_split8(v, hi, lo);
+    const long o = pix * a.ldo + a.co_off + n;
+    *reinterpret_cast<uint4*>(a.out_f + o) = hi;
+    *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+  }
+}
+
+// hx contract: pair in and out, 3x3, stride 1, pad 1, no pixel shuffle, Cin % 32 == 0, Kp == 9 * Cin
+bool hx_ok(const ConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.S == 1 && a.P == 1 && a.shuffle == 0 && a.Cin % 32 == 0 &&
+         a.Kp == 9 * a.Cin && a.Ho == a.H && a.Wo == a.W;
+}
+
+template <int TH, int BN, int WM, int WN>
+int launch_hx(const ConvArgs& a, hipStream_t stream) {
+  const int nwg = a.B * ((a.Ho + TH - 1) / TH) * ((a.Wo + 15) / 16) * ((a.N + BN - 1) / BN);
+  conv_hx_kernel<TH, BN, WM, WN><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
 // ---- x3 small halo: 3x3, pad 1, stride 1/2, Cin and N in {16, 32}.  The fp32
 // halo is split once while staging (register path: every halo pixel is read by
 // 9 taps, so splitting at the fragment read would cost 9x the VALU); hi and lo
@@ -1667,6 +1861,11 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     case 78: return launch_xb<128, 128, 2, 2, 2, PAIR_OUT>(a, stream);
     case 79: return launch_xb<256, 64, 4, 1, 2, PAIR_OUT>(a, stream);
     // one wave column: every wave reads the whole B tile, A fragments split over 8 waves
+    // halo-tiled 3x3 stride-1 (pair in and out only): TH x 16 output tiles
+    case 90: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 128, 2, 4>(a, stream) : (int)hipErrorInvalidValue;
+    case 91: return PAIR_OUT && hx_ok(a) ? launch_hx<16, 64, 4, 2>(a, stream) : (int)hipErrorInvalidValue;
+    case 92: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 64, 2, 4>(a, stream) : (int)hipErrorInvalidValue;
+    case 93: return PAIR_OUT && hx_ok(a) ? launch_hx<16, 128, 4, 2>(a, stream) : (int)hipErrorInvalidValue;
     case 68: return launch_xb<256, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 69: return launch_xb<128, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);

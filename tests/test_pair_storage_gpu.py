@@ -223,3 +223,33 @@ def test_lidar_pipeline_occupancy_matches_ungated(cuda):
     for b in range(2):
         k = int(n1[b])
         assert torch.equal(b1[b, :k], r2.box[b, :k])
+
+
+@pytest.mark.parametrize("tile", [90, 91, 92, 93])
+@pytest.mark.parametrize("shape", [(2, 23, 31, 64, 128), (1, 21, 37, 256, 256), (2, 19, 50, 64, 64), (3, 9, 16, 96, 72)])
+def test_conv_pair_halo_tiles_vs_fp64(cuda, tile, shape):
+    """Halo-tiled 3x3 stride-1 pair kernels (tiles 90-93): channel-offset input
+    and output slices, partial row / column tiles, N not a multiple of the tile,
+    a residual, against an fp64 reference; and close to the xb kernel (same
+    products, (chunk, tap) instead of (tap, chunk) summation order)."""
+    torch.manual_seed(tile + shape[3])
+    B, H, W, cin, cout = shape
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    res = torch.randn(B, H, W, cout, dtype=torch.float64)
+    xin = buf[..., 8:8 + cin]
+    x = NHWC(to_pairs(buf.float()).to(cuda), 8, cin, pair=True)
+    r = NHWC(to_pairs(res.float()).to(cuda), pair=True)
+    outs = {}
+    for t in (tile, 0):
+        out = torch.zeros(B, H, W, cout + 16, dtype=torch.float32, device=cuda)
+        fc(x, out=NHWC(out, 8, cout, pair=True), res=r, tile=t)
+        torch.cuda.synchronize()
+        outs[t] = out
+        assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
+    ref = torch.relu(conv(xin.permute(0, 3, 1, 2))) + from_pairs(r.t).double().cpu().permute(0, 3, 1, 2)
+    got = NHWC(outs[tile], 8, cout, pair=True).nchw()
+    assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
+    xb = NHWC(outs[0], 8, cout, pair=True).nchw()
+    assert rel_l2(got, xb) < 2e-6, rel_l2(got, xb)

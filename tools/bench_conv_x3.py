@@ -41,6 +41,10 @@ SHAPES = [
     ("y.c3c.1x1", B, 40, 40, 128, 64, 1, 1, 2),
     ("y.c3c.3x3", B, 40, 40, 64, 64, 3, 1, 2),
     ("y.b7", B, 40, 40, 128, 256, 3, 2, 2),
+    # Detect heads (1x1, 255 -> 256 outputs, no activation): short K, output-write bound
+    ("y.det80", B, 80, 80, 64, 256, 1, 1, 0),
+    ("y.det40", B, 40, 40, 128, 256, 1, 1, 0),
+    ("y.det20", B, 20, 20, 256, 256, 1, 1, 0),
 ]
 
 

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--marker", default="pc2_count")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--sequence", action="store_true",
+                    help="also list the last step's dispatches in launch order (duration, grid, kernel)")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -45,6 +47,13 @@ def main():
     print(f"{'us/step':>9} {'share':>6} {'calls':>6}  kernel")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[: a.top]:
         print(f"{v / n:9.1f} {100 * v / n / ksum:5.1f}% {cnt[k] / n:6.1f}  {k}")
+    if a.sequence:
+        s, e = starts[-2], starts[-1]
+        print(f"\n# last step in launch order\n{'#':>4} {'us':>8} {'grid':>10}  kernel")
+        for i, r in enumerate(rows[s:e]):
+            us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            grid = r.get("Grid_Size_X") or r.get("Grid_Size") or ""
+            print(f"{i:4d} {us:8.1f} {grid:>10}  {short(r['Kernel_Name'])}")
 
 
 if __name__ == "__main__":
