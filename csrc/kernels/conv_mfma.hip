@@ -1493,10 +1493,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
 // descriptor LDS DMA, zero padding by the range check) and runs the chunk's 9
 // tap steps from it, only the weight tile (BN x 32 channel pairs) streaming per
 // step through a 2-deep ring.  A fragment is one output row of 16 pixels, i.e. 16
-// consecutive halo rows at any base (ky * 18 + kx + row offset), so the 16-row
-// periodic slot swizzle keeps the b128 fragment reads conflict-free.  K order is
+// consecutive halo rows at base ky * 18 + kx + row offset
+// (the xb 16-row periodic swizzle is conflict-free only at 16-aligned bases; a
+// fragment here starts at column kx = 0..2, so the slot swizzle is a function of
+// the halo column found by exhaustive search to be conflict-free for every ds_read_b128
+// lane group at all three shifts: hswz below).  K order is
 // (chunk, tap) instead of xb's (tap, chunk): same products, different fp32
 // summation order (not bit-identical to xb; same accuracy vs fp64).
+// slot swizzle of halo column hx (0..17): 3 bits per column pair
+__device__ __forceinline__ int hswz(int hx) { return (0xb29108 >> (3 * (hx >> 1))) & 7; }
+
 template <int TH, int BN, int WM, int WN>
 __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN;
@@ -1541,7 +1547,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
     const int hy = p / HWD, hx = p - (p / HWD) * HWD;
     const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
     const bool ok = p < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-    h_off[j] = ok ? (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + (lslot ^ swzp(p)) * 4) * 4)
+    h_off[j] = ok ? (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + (lslot ^ hswz(hx)) * 4) * 4)
                   : kOutOfRange;
   }
   unsigned b_off[B_INS];
@@ -1602,7 +1608,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int hp = (wm * FM + i + ky) * HWD + kx + fr;
-      const int sw = swzp(hp);
+      const int sw = hswz(kx + fr);
       ah[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
       al[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
     }
