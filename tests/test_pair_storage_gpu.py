@@ -121,7 +121,10 @@ def test_conv_pair_residual_and_deconv_shuffle(cuda):
 
 def test_bev_plan_pair_equals_fp32_plan(cuda):
     """Pair storage feeds the MFMAs the same hi / lo halves the fp32 plan splits
-    at its fragment reads: the head outputs match bit for bit."""
+    at its fragment reads.  The pair plan's wide 3x3 stride-1 layers take the
+    halo-tiled kernel (same products, (chunk, tap) summation order), so the two
+    plans agree to fp32 rounding; a plain canvas converted on entry matches the
+    pair canvas bit for bit."""
     from triton_client_amd.config.lidar import KITTI_PILLARS, PointPillarsConfig
     from triton_client_amd.models.common import fuse_model, randomize_bn
     from triton_client_amd.models.fast import FastBEV
@@ -142,7 +145,7 @@ def test_bev_plan_pair_equals_fp32_plan(cuda):
     c = [o.values().clone() for o in fp.forward(NHWC(canvas.to(cuda)))]  # plain canvas: converted on entry
     torch.cuda.synchronize()
     for x, y, z in zip(a, b, c):
-        assert torch.equal(x, y) and torch.equal(x, z)
+        assert torch.equal(x, z) and rel_l2(x, y) < 2e-6, rel_l2(x, y)
     with torch.no_grad():
         ref = m.double().bev_forward(canvas.double().permute(0, 3, 1, 2))
     m.float()
