@@ -1503,7 +1503,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
 // slot swizzle of halo column hx (0..17): 3 bits per column pair
 __device__ __forceinline__ int hswz(int hx) { return (0xb29108 >> (3 * (hx >> 1))) & 7; }
 
-template <int TH, int BN, int WM, int WN>
+// CM (column-major): the fragment axis is y instead of x: tiles of 16 rows x TH
+// columns, halo stored column by column (18 rows per column), so narrow images
+// (pp.b3: 54 wide) tile without the 16-column waste.
+template <int TH, int BN, int WM, int WN, bool CM = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -1523,7 +1526,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int tx_n = (a.Wo + TW - 1) / TW, ty_n = (a.Ho + TH - 1) / TH;
+  // tile extent along x / y (the fragment axis spans 16)
+  constexpr int EX = CM ? TH : TW, EY = CM ? TW : TH;
+  const int tx_n = (a.Wo + EX - 1) / EX, ty_n = (a.Ho + EY - 1) / EY;
   const int nmt = a.B * ty_n * tx_n, nnt = (a.N + BN - 1) / BN, nwg = nmt * nnt;
   int bid = blockIdx.x;
   {
@@ -1532,7 +1537,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
   }
   const int mt = bid / nnt, nt = bid - mt * nnt;
   const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
-  const int oy0 = (rem / tx_n) * TH, ox0 = (rem - (rem / tx_n) * tx_n) * TW;
+  const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
   const int n0 = nt * BN;
 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
@@ -1544,10 +1549,11 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < HPW; ++j) {
     const int p = (wid + j * NW) * 8 + lrow;
-    const int hy = p / HWD, hx = p - (p / HWD) * HWD;
+    const int u = p / HWD, v = p - (p / HWD) * HWD;  // (line, position along the fragment axis)
+    const int hy = CM ? v : u, hx = CM ? u : v;
     const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
     const bool ok = p < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-    h_off[j] = ok ? (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + (lslot ^ hswz(hx)) * 4) * 4)
+    h_off[j] = ok ? (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off + (lslot ^ hswz(v)) * 4) * 4)
                   : kOutOfRange;
   }
   unsigned b_off[B_INS];
@@ -1599,6 +1605,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
     const unsigned char* hb = halo + (c & 1) * HBYTES;
     const unsigned char* bb = bring + (s & 1) * BBYTES;
     const int ky = t / 3, kx = t - (t / 3) * 3;
+    const int kl = CM ? kx : ky, kf = CM ? ky : kx;  // tap offset across lines / along the fragment axis
     bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -1607,8 +1614,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int hp = (wm * FM + i + ky) * HWD + kx + fr;
-      const int sw = hswz(kx + fr);
+      const int hp = (wm * FM + i + kl) * HWD + kf + fr;
+      const int sw = hswz(kf + fr);
       ah[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
       al[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
     }
@@ -1652,7 +1659,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
   constexpr int V8 = BN / 8;
   for (int id = tid; id < BM * V8; id += NW * 64) {
     const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
-    const int oy = oy0 + ml / TW, ox = ox0 + (ml & (TW - 1)), n = n0 + c8;
+    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15)), n = n0 + c8;
     if (oy >= a.Ho || ox >= a.Wo || n >= a.N) continue;
     float v[8];
     const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
@@ -1679,10 +1686,11 @@ bool hx_ok(const ConvArgs& a) {
          a.Kp == 9 * a.Cin && a.Ho == a.H && a.Wo == a.W;
 }
 
-template <int TH, int BN, int WM, int WN>
+template <int TH, int BN, int WM, int WN, bool CM = false>
 int launch_hx(const ConvArgs& a, hipStream_t stream) {
-  const int nwg = a.B * ((a.Ho + TH - 1) / TH) * ((a.Wo + 15) / 16) * ((a.N + BN - 1) / BN);
-  conv_hx_kernel<TH, BN, WM, WN><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
+  const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * ((a.N + BN - 1) / BN);
+  conv_hx_kernel<TH, BN, WM, WN, CM><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -1872,6 +1880,9 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     case 91: return PAIR_OUT && hx_ok(a) ? launch_hx<16, 64, 4, 2>(a, stream) : (int)hipErrorInvalidValue;
     case 92: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 64, 2, 4>(a, stream) : (int)hipErrorInvalidValue;
     case 93: return PAIR_OUT && hx_ok(a) ? launch_hx<16, 128, 4, 2>(a, stream) : (int)hipErrorInvalidValue;
+    // column-major twins: 16 rows x TH columns
+    case 94: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 128, 2, 4, true>(a, stream) : (int)hipErrorInvalidValue;
+    case 95: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 64, 2, 4, true>(a, stream) : (int)hipErrorInvalidValue;
     case 68: return launch_xb<256, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 69: return launch_xb<128, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);
