@@ -2092,10 +2092,15 @@ int conv_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off,
   // (4-wave 64x64-per-wave tiles measured slower on every layer)
   // xb (buffer-descriptor DMA) twins, same bits, 8-10% faster on every PointPillars layer
   // (profiles/r2/xb_tiles.jsonl): 256x64 / 128x64 for N <= 64 (stride 1 / 2), 128x128 2x4 / 4x2
-  // halo-tiled hx 8x16 for 3x3 stride-1 layers with N >= 128 whose width wastes <= 5% in 16-column
-  // tiles (pp.b2.conv 325 vs 338 us; the 54-wide pp.b3 would waste 18%: profiles/r2/hx_tiles_v2.jsonl)
-  if (tile == 0 && out_pair && !a.occ && N >= 128 && xb_ok(a) && hx_ok(a) && ((Wo + 15) / 16 * 16 - Wo) * 20 <= Wo)
-    tile = 90;
+  // halo-tiled hx for 3x3 stride-1 layers with N >= 128: row-major 8x16 tiles (90) or column-major
+  // 16x8 (94), whichever pads the image less, when that padding is <= 10% of the pixels
+  // (pp.b2.conv 335 vs 353 us, pp.b3.conv 297 vs 312: profiles/r2/hx_tiles_v3.jsonl)
+  if (tile == 0 && out_pair && !a.occ && N >= 128 && xb_ok(a) && hx_ok(a)) {
+    const long px = (long)Ho * Wo;
+    const long rm = (long)((Wo + 15) / 16 * 16) * ((Ho + 7) / 8 * 8), cm = (long)((Ho + 15) / 16 * 16) * ((Wo + 7) / 8 * 8);
+    const long best = cm <= rm ? cm : rm;
+    if (best * 10 <= px * 11) tile = cm <= rm ? 94 : 90;
+  }
   if (tile == 0 && xb_ok(a)) tile = N <= 64 ? (S == 1 ? 71 : 77) : (S == 1 ? 70 : 73);
   if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);
