@@ -2,4 +2,4 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-bash tools/gpu_round_check2.sh && TAG=r2_hx bash tools/gpu_step_profile.sh
+bash tools/gpu_round_check2.sh && TAG=${TAG:-r2_hx} bash tools/gpu_step_profile.sh
