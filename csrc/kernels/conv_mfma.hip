@@ -1420,144 +1420,65 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_xb_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (OCC) {
-    // Occupancy-gated step list: a K step whose tap reads no occupied pixel for ANY
-    // row of the tile contributes exact zeros, so it is skipped (no DMA, no MFMA).
-    __shared__ unsigned s_tmask;
-    __shared__ int s_steps[64];
-    __shared__ int s_ns;
-    unsigned lm = 0;
-#pragma unroll
-    for (int j = 0; j < A_INS; ++j) lm |= a_iy0[j] > -(1 << 27) ? a_occ[j] : 0u;
-    if (tid == 0) s_tmask = 0u;
-    __syncthreads();
-    if (lm) atomicOr(&s_tmask, lm);
-    __syncthreads();
-    const int nk = a.Kp / BKC, cpt = a.Cin / BKC;
-    if (tid == 0) {
-      const unsigned tm = s_tmask;
-      int ns = 0;
-      for (int k = 0; k < nk; ++k)
-        if (nk > 64 || ((tm >> (k / cpt)) & 1u)) {
-          if (ns < 64) s_steps[ns] = k;
-          ++ns;
-        }
-      s_ns = nk > 64 ? -1 : ns;
+  const int nk = a.Kp / BKC;
+  int ky = 0, kx = 0, ci0 = 0;
+  tap_offsets(0, 0);
+  auto advance = [&]() {
+    ci0 += BKC;
+    if (ci0 == a.Cin) {
+      ci0 = 0;
+      if (++kx == a.KW) { kx = 0; ++ky; }
+      if (ky < a.KH) tap_offsets(ky, kx);
     }
-    __syncthreads();
-    const int ns = s_ns < 0 ? nk : s_ns;
-    const bool listed = s_ns >= 0;
-    auto step_of = [&](int i) { return listed ? s_steps[i] : i; };
-    auto issue_step = [&](int i, int buf) {
-      const int k = step_of(i), tap = k / cpt;
-      tap_offsets(tap / a.KW, tap - (tap / a.KW) * a.KW);
-      issue(k, buf, (k - tap * cpt) * BKC);
-    };
+  };
 #pragma unroll
-    for (int st0 = 0; st0 < STAGES - 1; ++st0)
-      if (st0 < ns) issue_step(st0, st0);
-    const int fr = lane & 15, fq = lane >> 4;
-    // per-lane fragment bases (fragment i / j: + i * 16 rows, a constant)
-    const int sw = swzp(fr);
-    const int a_hi = (wm * TM + fr) * ROWB + (((2 * fq) ^ sw) << 4), a_lo = (wm * TM + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
-    const int b_hi = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq) ^ sw) << 4);
-    const int b_lo = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
-    for (int si = 0; si < ns; ++si) {
-      const int cur = si % STAGES;
-      const int after = (ns - 1 - si) < (STAGES - 2) ? (ns - 1 - si) : (STAGES - 2);
-      wait_vmcnt_upto<NL>(after);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const int nx = si + STAGES - 1;
-      if (nx < ns) issue_step(nx, nx % STAGES);
-      const unsigned char* st = smem + cur * STAGE;
-      bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(st + b_hi + j * 16 * ROWB);
-        bl[j] = *reinterpret_cast<const bf16x8*>(st + b_lo + j * 16 * ROWB);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        if constexpr (PAIR_IN) {  // slots hold hi / lo of 8 channels as stored
-          ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
-          al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
-        } else {  // slots hold fp32 channels 8fq..8fq+3 / +4..+7: split here
-          const float4 x0 = *reinterpret_cast<const float4*>(st + a_hi + i * 16 * ROWB);
-          const float4 x1 = *reinterpret_cast<const float4*>(st + a_lo + i * 16 * ROWB);
-          split8(x0, x1, ah[i], al[i]);
-        }
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
-      __builtin_amdgcn_s_setprio(0);
+  for (int st = 0; st < STAGES - 1; ++st)
+    if (st < nk) {
+      issue(st, st, ci0);
+      advance();
     }
-  } else {
-    const int nk = a.Kp / BKC;
-    int ky = 0, kx = 0, ci0 = 0;
-    tap_offsets(0, 0);
-    auto advance = [&]() {
-      ci0 += BKC;
-      if (ci0 == a.Cin) {
-        ci0 = 0;
-        if (++kx == a.KW) { kx = 0; ++ky; }
-        if (ky < a.KH) tap_offsets(ky, kx);
-      }
-    };
-  #pragma unroll
-    for (int st = 0; st < STAGES - 1; ++st)
-      if (st < nk) {
-        issue(st, st, ci0);
-        advance();
-      }
-    const int fr = lane & 15, fq = lane >> 4;
-    // per-lane fragment bases (fragment i / j: + i * 16 rows, a constant)
-    const int sw = swzp(fr);
-    const int a_hi = (wm * TM + fr) * ROWB + (((2 * fq) ^ sw) << 4), a_lo = (wm * TM + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
-    const int b_hi = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq) ^ sw) << 4);
-    const int b_lo = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt % STAGES;
-      const int after = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
-      wait_vmcnt_upto<NL>(after);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const int nx = kt + STAGES - 1;
-      if (nx < nk) {
-        issue(nx, nx % STAGES, ci0);
-        advance();
-      }
-      const unsigned char* st = smem + cur * STAGE;
-      bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(st + b_hi + j * 16 * ROWB);
-        bl[j] = *reinterpret_cast<const bf16x8*>(st + b_lo + j * 16 * ROWB);
-      }
-  #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        if constexpr (PAIR_IN) {  // slots hold hi / lo of 8 channels as stored
-          ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
-          al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
-        } else {  // slots hold fp32 channels 8fq..8fq+3 / +4..+7: split here
-          const float4 x0 = *reinterpret_cast<const float4*>(st + a_hi + i * 16 * ROWB);
-          const float4 x1 = *reinterpret_cast<const float4*>(st + a_lo + i * 16 * ROWB);
-          split8(x0, x1, ah[i], al[i]);
-        }
-      }
-      __builtin_amdgcn_s_setprio(1);
-  #pragma unroll
-      for (int i = 0; i < FM; ++i)
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
-      __builtin_amdgcn_s_setprio(0);
+  const int fr = lane & 15, fq = lane >> 4;
+  // per-lane fragment bases (fragment i / j: + i * 16 rows, a constant)
+  const int sw = swzp(fr);
+  const int a_hi = (wm * TM + fr) * ROWB + (((2 * fq) ^ sw) << 4), a_lo = (wm * TM + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
+  const int b_hi = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq) ^ sw) << 4);
+  const int b_lo = A_BYTES + (wn * TN + fr) * ROWB + (((2 * fq + 1) ^ sw) << 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % STAGES;
+    const int after = (nk - 1 - kt) < (STAGES - 2) ? (nk - 1 - kt) : (STAGES - 2);
+    wait_vmcnt_upto<NL>(after);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int nx = kt + STAGES - 1;
+    if (nx < nk) {
+      issue(nx, nx % STAGES, ci0);
+      advance();
     }
-
+    const unsigned char* st = smem + cur * STAGE;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(st + b_hi + j * 16 * ROWB);
+      bl[j] = *reinterpret_cast<const bf16x8*>(st + b_lo + j * 16 * ROWB);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if constexpr (PAIR_IN) {  // slots hold hi / lo of 8 channels as stored
+        ah[i] = *reinterpret_cast<const bf16x8*>(st + a_hi + i * 16 * ROWB);
+        al[i] = *reinterpret_cast<const bf16x8*>(st + a_lo + i * 16 * ROWB);
+      } else {  // slots hold fp32 channels 8fq..8fq+3 / +4..+7: split here
+        const float4 x0 = *reinterpret_cast<const float4*>(st + a_hi + i * 16 * ROWB);
+        const float4 x1 = *reinterpret_cast<const float4*>(st + a_lo + i * 16 * ROWB);
+        split8(x0, x1, ah[i], al[i]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], bh[j], bl[j], ah[i], al[i]);
+    __builtin_amdgcn_s_setprio(0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // the epilogue reuses the staging LDS
