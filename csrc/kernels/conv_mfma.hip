@@ -2098,11 +2098,14 @@ int conv_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off,
   // halo-tiled hx for 3x3 stride-1 layers with N >= 128: row-major 8x16 tiles (90) or column-major
   // 16x8 (94), whichever pads the image less, when that padding is <= 10% of the pixels
   // (pp.b2.conv 335 vs 353 us, pp.b3.conv 297 vs 312: profiles/r2/hx_tiles_v3.jsonl)
-  if (tile == 0 && out_pair && !a.occ && N >= 128 && xb_ok(a) && hx_ok(a)) {
+  // N = 64: 16 x 12 tiles (96 column-major / 97 row-major; pp.b1.conv 439 / 436 vs 455 us)
+  if (tile == 0 && out_pair && !a.occ && (N >= 128 || N == 64) && xb_ok(a) && hx_ok(a)) {
+    const int th = N == 64 ? 12 : 8;
     const long px = (long)Ho * Wo;
-    const long rm = (long)((Wo + 15) / 16 * 16) * ((Ho + 7) / 8 * 8), cm = (long)((Ho + 15) / 16 * 16) * ((Wo + 7) / 8 * 8);
+    const long rm = (long)((Wo + 15) / 16 * 16) * ((Ho + th - 1) / th * th);
+    const long cm = (long)((Ho + 15) / 16 * 16) * ((Wo + th - 1) / th * th);
     const long best = cm <= rm ? cm : rm;
-    if (best * 10 <= px * 11) tile = cm <= rm ? 94 : 90;
+    if (best * 10 <= px * 11) tile = N == 64 ? (cm <= rm ? 96 : 97) : (cm <= rm ? 94 : 90);
   }
   if (tile == 0 && xb_ok(a)) tile = N <= 64 ? (S == 1 ? 71 : 77) : (S == 1 ? 70 : 73);
   if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
