@@ -1506,7 +1506,9 @@ __device__ __forceinline__ int hswz(int hx) { return (0xb29108 >> (3 * (hx >> 1)
 // CM (column-major): the fragment axis is y instead of x: tiles of 16 rows x TH
 // columns, halo stored column by column (18 rows per column), so narrow images
 // (pp.b3: 54 wide) tile without the 16-column waste.
-template <int TH, int BN, int WM, int WN, bool CM = false>
+// PAIR = false: plain fp32 activations (split at the fragment read, xb's fp32-input
+// form) and plain fp32 output.
+template <int TH, int BN, int WM, int WN, bool CM = false, bool PAIR = true>
 __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -1616,8 +1618,14 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
     for (int i = 0; i < FM; ++i) {
       const int hp = (wm * FM + i + kl) * HWD + kf + fr;
       const int sw = hswz(kf + fr);
-      ah[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
-      al[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
+      if constexpr (PAIR) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
+        al[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
+      } else {
+        const float4 x0 = *reinterpret_cast<const float4*>(hb + hp * 128 + (((2 * fq) ^ sw) << 4));
+        const float4 x1 = *reinterpret_cast<const float4*>(hb + hp * 128 + (((2 * fq + 1) ^ sw) << 4));
+        split8(x0, x1, ah[i], al[i]);
+      }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1668,15 +1676,26 @@ __global__ void __launch_bounds__(WM * WN * 64) conv_hx_kernel(ConvArgs a) {
     const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
     if (a.res_f) {
       float r[8];
-      pair_join8(a.res_f + pix * a.ldr + a.r_off + n, r);
+      const float* rp = a.res_f + pix * a.ldr + a.r_off + n;
+      if constexpr (PAIR) {
+        pair_join8(rp, r);
+      } else {
+        const float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+        r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
     }
-    uint4 hi, lo;
-    pair_split8(v, hi, lo);
     const long o = pix * a.ldo + a.co_off + n;
-    *reinterpret_cast<uint4*>(a.out_f + o) = hi;
-    *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+    if constexpr (PAIR) {
+      uint4 hi, lo;
+      pair_split8(v, hi, lo);
+      *reinterpret_cast<uint4*>(a.out_f + o) = hi;
+      *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+    } else {
+      *reinterpret_cast<float4*>(a.out_f + o) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(a.out_f + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
   }
 }
 
@@ -1686,12 +1705,25 @@ bool hx_ok(const ConvArgs& a) {
          a.Kp == 9 * a.Cin && a.Ho == a.H && a.Wo == a.W;
 }
 
-template <int TH, int BN, int WM, int WN, bool CM = false>
+template <int TH, int BN, int WM, int WN, bool CM = false, bool PAIR = true>
 int launch_hx(const ConvArgs& a, hipStream_t stream) {
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * ((a.N + BN - 1) / BN);
-  conv_hx_kernel<TH, BN, WM, WN, CM><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_hx_kernel<TH, BN, WM, WN, CM, PAIR><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
+}
+
+// auto hx choice for a 3x3 stride-1 layer: 8 x 16 (N >= 128) or 12 x 16 (N = 64) tiles, row- or
+// column-major by the smaller padding, when that padding is <= 10% of the pixels.  Returns the
+// tile pair {column-major tile, row-major tile} entry to use, or 0.
+int hx_pick(const ConvArgs& a, int cm_tile_wide, int rm_tile_wide, int cm_tile_64, int rm_tile_64) {
+  if (!hx_ok(a) || !(a.N >= 128 || a.N == 64)) return 0;
+  const int th = a.N == 64 ? 12 : 8;
+  const long px = (long)a.Ho * a.Wo;
+  const long rm = (long)((a.Wo + 15) / 16 * 16) * ((a.Ho + th - 1) / th * th);
+  const long cm = (long)((a.Ho + 15) / 16 * 16) * ((a.Wo + th - 1) / th * th);
+  if ((cm <= rm ? cm : rm) * 10 > px * 11) return 0;
+  return a.N == 64 ? (cm <= rm ? cm_tile_64 : rm_tile_64) : (cm <= rm ? cm_tile_wide : rm_tile_wide);
 }
 
 // ---- x3 small halo: 3x3, pad 1, stride 1/2, Cin and N in {16, 32}.  The fp32
@@ -2016,12 +2048,18 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
   if (tile == 0 && small_halo_x3_ok(a) && a.S == 1) tile = 60;
   // glds-class layers go to the xb twins (same bits; profiles/r2/xbf_tiles.jsonl at batch 32: 128x64 8x1 for
   // N <= 64 and for small M (YOLOv5n b7 39 vs 54 us on the old glds 128x128), 128x128 4x2 above)
+  // halo-tiled hx (plain fp32 twins of the pair tiles) for large 3x3 stride-1 layers
+  if (tile == 0 && v2ok && xb_ok(a) && a.M >= 40000) tile = hx_pick(a, 98, 99, 100, 101);
   if (tile == 0 && N > 32 && v2ok && xb_ok(a)) tile = (N <= 64 || a.M < 40000) ? 81 : 80;
   if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 41 : 20) : (N <= 64 ? 2 : 5);
   if (((tile >= 10 && tile < 60) || tile >= 70) && !v2ok) return (int)hipErrorInvalidValue;
   if (tile >= 80 && !xb_ok(a)) return (int)hipErrorInvalidValue;
   switch (tile) {
     case 60: return launch_small_halo_x3(a, stream);
+    case 98: return hx_ok(a) ? launch_hx<8, 128, 2, 4, true, false>(a, stream) : (int)hipErrorInvalidValue;
+    case 99: return hx_ok(a) ? launch_hx<8, 128, 2, 4, false, false>(a, stream) : (int)hipErrorInvalidValue;
+    case 100: return hx_ok(a) ? launch_hx<12, 64, 4, 2, true, false>(a, stream) : (int)hipErrorInvalidValue;
+    case 101: return hx_ok(a) ? launch_hx<12, 64, 4, 2, false, false>(a, stream) : (int)hipErrorInvalidValue;
     // xb twins (buffer-descriptor DMA, split at the fragment read; same bits as the glds tile named)
     case 80: return launch_xb<128, 128, 4, 2, 2, false, false>(a, stream);  // 20
     case 81: return launch_xb<128, 64, 8, 1, 2, false, false>(a, stream);   // 41
@@ -2099,14 +2137,7 @@ int conv_x3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off,
   // 16x8 (94), whichever pads the image less, when that padding is <= 10% of the pixels
   // (pp.b2.conv 335 vs 353 us, pp.b3.conv 297 vs 312: profiles/r2/hx_tiles_v3.jsonl)
   // N = 64: 16 x 12 tiles (96 column-major / 97 row-major; pp.b1.conv 439 / 436 vs 455 us)
-  if (tile == 0 && out_pair && !a.occ && (N >= 128 || N == 64) && xb_ok(a) && hx_ok(a)) {
-    const int th = N == 64 ? 12 : 8;
-    const long px = (long)Ho * Wo;
-    const long rm = (long)((Wo + 15) / 16 * 16) * ((Ho + th - 1) / th * th);
-    const long cm = (long)((Ho + 15) / 16 * 16) * ((Wo + th - 1) / th * th);
-    const long best = cm <= rm ? cm : rm;
-    if (best * 10 <= px * 11) tile = N == 64 ? (cm <= rm ? 96 : 97) : (cm <= rm ? 94 : 90);
-  }
+  if (tile == 0 && out_pair && !a.occ && xb_ok(a)) tile = hx_pick(a, 94, 90, 96, 97);
   if (tile == 0 && xb_ok(a)) tile = N <= 64 ? (S == 1 ? 71 : 77) : (S == 1 ? 70 : 73);
   if (tile == 0) tile = N <= 64 ? (S == 1 ? 26 : 32) : 25;
   return out_pair ? launch_glds_x3p<true>(a, tile, stream) : launch_glds_x3p<false>(a, tile, stream);

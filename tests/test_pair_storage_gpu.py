@@ -256,3 +256,30 @@ def test_conv_pair_halo_tiles_vs_fp64(cuda, tile, shape):
     assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
     xb = NHWC(outs[0], 8, cout, pair=True).nchw()
     assert rel_l2(got, xb) < 2e-6, rel_l2(got, xb)
+
+
+@pytest.mark.parametrize("tile", [98, 99, 100, 101])
+@pytest.mark.parametrize("shape", [(2, 23, 31, 64, 128), (1, 21, 37, 256, 256), (2, 19, 50, 64, 64)])
+def test_conv_fp32_halo_tiles_vs_fp64(cuda, tile, shape):
+    """Plain-fp32 twins of the halo tiles (split at the fragment read, fp32
+    output): channel-offset slices, partial tiles, a residual, vs fp64 and
+    close to the xb kernel."""
+    torch.manual_seed(tile + shape[3])
+    B, H, W, cin, cout = shape
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    res = torch.randn(B, H, W, cout, dtype=torch.float64)
+    x = NHWC(buf.float().to(cuda), 8, cin)
+    r = NHWC(res.float().to(cuda))
+    outs = {}
+    for t in (tile, 81 if cout <= 64 else 80):
+        out = torch.zeros(B, H, W, cout + 16, dtype=torch.float32, device=cuda)
+        fc(x, out=NHWC(out, 8, cout), res=r, tile=t)
+        torch.cuda.synchronize()
+        outs[t] = out
+        assert out[..., :8].abs().sum().item() == 0 and out[..., 8 + cout:].abs().sum().item() == 0
+    ref = torch.relu(conv(buf[..., 8:8 + cin].permute(0, 3, 1, 2))) + res.permute(0, 3, 1, 2)
+    got = NHWC(outs[tile], 8, cout).nchw()
+    assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
+    assert rel_l2(got, NHWC(outs[81 if cout <= 64 else 80], 8, cout).nchw()) < 2e-6
