@@ -2048,8 +2048,8 @@ TCA_API int tca_conv_nhwc_x3(const float* in, int B, int H, int W, int Cin, int 
   if (tile == 0 && small_halo_x3_ok(a) && a.S == 1) tile = 60;
   // glds-class layers go to the xb twins (same bits; profiles/r2/xbf_tiles.jsonl at batch 32: 128x64 8x1 for
   // N <= 64 and for small M (YOLOv5n b7 39 vs 54 us on the old glds 128x128), 128x128 4x2 above)
-  // halo-tiled hx (plain fp32 twins of the pair tiles) for large 3x3 stride-1 layers
-  if (tile == 0 && v2ok && xb_ok(a) && a.M >= 40000) tile = hx_pick(a, 98, 99, 100, 101);
+  // plain-fp32 hx twins (tiles 98-101) stay opt-in: auto-selected they measured +1.7% on CenterPoint,
+  // +0% on SECOND-IoU and -2.5% on RetinaNet / FCOS (profiles/r2/fam_hx_fp32/)
   if (tile == 0 && N > 32 && v2ok && xb_ok(a)) tile = (N <= 64 || a.M < 40000) ? 81 : 80;
   if (tile == 0) tile = N <= 16 ? 6 : N <= 32 ? 1 : v2ok ? (N <= 64 ? 41 : 20) : (N <= 64 ? 2 : 5);
   if (((tile >= 10 && tile < 60) || tile >= 70) && !v2ok) return (int)hipErrorInvalidValue;
