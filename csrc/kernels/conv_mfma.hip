@@ -1918,6 +1918,8 @@ int launch_glds_x3p(const ConvArgs& a, int tile, hipStream_t stream) {
     // N = 64 layers: 16 x 12 tiles (192 rows, 3 fragments per wave row), 80 KiB LDS -> 2 workgroups per CU
     case 96: return PAIR_OUT && hx_ok(a) ? launch_hx<12, 64, 4, 2, true>(a, stream) : (int)hipErrorInvalidValue;
     case 97: return PAIR_OUT && hx_ok(a) ? launch_hx<12, 64, 4, 2, false>(a, stream) : (int)hipErrorInvalidValue;
+    // 4x2 waves (2 A / 4 B fragments per wave) instead of 2x4
+    case 102: return PAIR_OUT && hx_ok(a) ? launch_hx<8, 128, 4, 2, true>(a, stream) : (int)hipErrorInvalidValue;
     case 68: return launch_xb<256, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 69: return launch_xb<128, 64, 8, 1, 2, PAIR_OUT>(a, stream);
     case 20: return launch_glds_x3<128, 128, 4, 2, 2, true, PAIR_OUT>(a, stream);

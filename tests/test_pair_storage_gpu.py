@@ -228,7 +228,7 @@ def test_lidar_pipeline_occupancy_matches_ungated(cuda):
         assert torch.equal(b1[b, :k], r2.box[b, :k])
 
 
-@pytest.mark.parametrize("tile", [90, 91, 92, 93, 94, 95, 96, 97])
+@pytest.mark.parametrize("tile", [90, 91, 92, 93, 94, 95, 96, 97, 102])
 @pytest.mark.parametrize("shape", [(2, 23, 31, 64, 128), (1, 21, 37, 256, 256), (2, 19, 50, 64, 64), (3, 9, 16, 96, 72)])
 def test_conv_pair_halo_tiles_vs_fp64(cuda, tile, shape):
     """Halo-tiled 3x3 stride-1 pair kernels (tiles 90-93): channel-offset input
