@@ -64,6 +64,9 @@ struct Huffman {
     int code = 0, k = 0;
     for (int len = 1; len <= 16; ++len) {
       const int n = counts[len - 1];
+      // over-subscribed table (a crafted DHT): reject before any fast-table write, whose
+      // index (code << shift) | j must stay below 1 << kFastBits
+      if (code + n > (1 << len) || k + n > nsym) return false;
       valptr[len] = k;
       mincode[len] = code;
       for (int i = 0; i < n; ++i, ++k, ++code) {
@@ -76,7 +79,6 @@ struct Huffman {
         }
       }
       maxcode[len] = n ? code - 1 : -1;
-      if (code > (1 << len)) return false;  // over-subscribed table
       code <<= 1;
     }
     maxcode[17] = 0x7fffffff;

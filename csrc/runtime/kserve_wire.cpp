@@ -192,7 +192,10 @@ bool parse_tensor(const uint8_t* buf, const uint8_t* s, uint64_t l, long* m, int
       if (*nd_total >= max_dims) { *err = -2; return false; }
       shapes[(*nd_total)++] = (int64_t)d;
       ++m[4];
-    } else if (f == 4 && w == 2) {  // parameters (e.g. shared_memory_region): flagged for the caller
+    } else if ((f == 4 || f == 5) && w == 2) {
+      // parameters (e.g. shared_memory_region) or typed contents (InferTensorContents,
+      // fp32_contents etc. instead of raw_input_contents): flagged so the caller serves
+      // the request through the protobuf path, which decodes both
       m[6] = 1;
       if (!t.skip(w)) { *err = -1; return false; }
     } else if (!t.skip(w)) {
@@ -245,8 +248,9 @@ TCA_API long tca_kserve_encode_response(const char* model_name, const char* mode
 //   req[k*2 + 0..1]  requested output k name offset/length
 //   counts[0..8]     n_inputs, n_raw, n_requested, model_name off/len, model_version off/len, id off/len
 //   counts[9]        1 when an input or a requested output carries parameters (the shared-memory
-//                    extension's region references: the caller takes the protobuf path)
-//   meta[k*8 + 6]    1 when input k carries parameters
+//                    extension's region references) or an input carries typed contents: the caller
+//                    takes the protobuf path
+//   meta[k*8 + 6]    1 when input k carries parameters or typed contents
 // Returns 0, -1 malformed, -2 capacity exceeded.
 TCA_API int tca_kserve_parse_request(const uint8_t* buf, long len, int max_t, long* meta, int64_t* shapes,
                                      int max_dims, long* raw, long* req, long* counts) {

@@ -43,6 +43,43 @@ int main(int argc, char** argv) {
     if (tca_jpeg_decode_coefs(f.data(), (int64_t)f.size(), coef.data(), cap, q.data(), geom.data()) != 0) return 4;
     ++ok;
   }
+  // crafted over-subscribed DHT tables: every table of every file gets all its
+  // symbols moved to code length 1 (counts[0] = nsym, the rest 0; the segment
+  // length stays consistent) or 3 of them (counts[0] = 3).  Both must be rejected
+  // before the fast lookup table is written.
+  int crafted = 0;
+  for (auto& f : files) {
+    for (size_t p = 2; p + 4 < f.size(); ++p) {
+      if (f[p] != 0xFF || f[p + 1] != 0xC4) continue;
+      const size_t seg_end = p + 2 + ((size_t)f[p + 2] << 8 | f[p + 3]);
+      for (size_t t = p + 4; t + 17 <= seg_end && t + 17 <= f.size();) {
+        int nsym = 0;
+        for (int l = 0; l < 16; ++l) nsym += f[t + 1 + l];
+        for (int variant = 0; variant < 2; ++variant) {
+          if (variant == 1 && nsym < 4) continue;
+          std::vector<uint8_t> v = f;
+          if (variant == 0) {
+            for (int l = 0; l < 16; ++l) v[t + 1 + l] = 0;
+            v[t + 1] = (uint8_t)nsym;
+          } else {
+            // 3 codes of length 1, the remaining symbols at the longest used length
+            int last = 15;
+            while (last > 0 && f[t + 1 + last] == 0) --last;
+            for (int l = 0; l < 16; ++l) v[t + 1 + l] = 0;
+            v[t + 1] = 3;
+            v[t + 1 + last] = (uint8_t)(nsym - 3);
+          }
+          int32_t g[16];
+          if (tca_jpeg_probe(v.data(), (int64_t)v.size(), g) == 0) return 5;
+          if (tca_jpeg_decode_coefs(v.data(), (int64_t)v.size(), coef.data(), cap, q.data(), geom.data()) == 0)
+            return 6;
+          ++crafted;
+        }
+        t += 17 + nsym;
+      }
+    }
+  }
+  if (crafted == 0) return 7;
   std::mt19937 rng(1234);
   int rejected = 0;
   for (int it = 0; it < iters; ++it) {
@@ -75,6 +112,7 @@ int main(int argc, char** argv) {
     tca_cpu_preprocess(img.data(), h0, w0, c0, rng() & 1, out.data(), rng() & 1, H, W, top, left, nh, nw, 114.f,
                        rng() & 1, sc, bi, 1 + rng() % 3);
   }
-  std::printf("jpeg fuzz ok: %d files, %d iterations, %d corrupt frames rejected\n", ok, iters, rejected);
+  std::printf("jpeg fuzz ok: %d files, %d crafted DHT tables rejected, %d iterations, %d corrupt frames rejected\n",
+              ok, crafted, iters, rejected);
   return 0;
 }

@@ -89,6 +89,52 @@ def test_unsupported_and_corrupt_inputs_fail_cleanly():
         assert rc in (0, -1, -2, -3, -4, -5)
 
 
+def _dht_tables(data):
+    """(offset of the 16 counts, nsym) of every Huffman table in every DHT segment."""
+    out = []
+    p = 2
+    while p + 4 < len(data):
+        if data[p] == 0xFF and data[p + 1] == 0xC4:
+            end = p + 2 + (data[p + 2] << 8 | data[p + 3])
+            t = p + 4
+            while t + 17 <= end:
+                nsym = sum(data[t + 1:t + 17])
+                out.append((t + 1, nsym))
+                t += 17 + nsym
+            p = end
+        else:
+            p += 1
+    return out
+
+
+@pytest.mark.parametrize("variant", ["all_len1", "three_len1"])
+def test_oversubscribed_huffman_table_is_rejected(variant):
+    """A DHT whose code counts over-subscribe a length (counts[0] >= 3) must be
+    rejected before the fast lookup table is filled (its index would run past
+    the table).  The segment length stays consistent, so only the code-space
+    check can catch it."""
+    good = _jpeg(camera_frame(48, 64, seed=3))
+    tables = _dht_tables(good)
+    assert tables
+    coef = np.empty((4096, 64), np.int16)
+    q = np.empty(192, np.float32)
+    g = np.zeros(16, np.int32)
+    rt = J._rt()
+    for off, nsym in tables:
+        b = bytearray(good)
+        counts = [0] * 16
+        if variant == "all_len1":
+            counts[0] = nsym
+        else:
+            last = max(i for i in range(16) if good[off + i])
+            counts[0], counts[last] = 3, nsym - 3
+        b[off:off + 16] = bytes(counts)
+        with pytest.raises(ValueError):
+            J.probe(bytes(b))
+        rc = rt.tca_jpeg_decode_coefs(bytes(b), len(b), coef.ctypes.data, 4096, q.ctypes.data, g.ctypes.data)
+        assert rc < 0
+
+
 def test_batch_decode_threads_and_status():
     """tca_jpeg_decode_batch on 4 threads == one-by-one decode; a progressive
     frame in the batch reports its error without disturbing the others."""

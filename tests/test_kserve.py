@@ -92,6 +92,35 @@ def test_channel_round_trip_echo(echo_server):
     ch.close()
 
 
+def test_typed_contents_through_the_default_raw_server(echo_server):
+    """A valid KServe request may carry its tensors as typed contents
+    (InferInputTensor.contents.fp32_contents) instead of raw_input_contents.  The
+    default server parses ModelInfer with the C++ codec, which must flag such an
+    input so the request is served by the protobuf path, not rejected as 'missing
+    input'."""
+    from triton_client_amd.channel.wire import parse_request
+
+    x0 = np.arange(6, dtype=np.float32) * 0.5
+    x1 = -np.arange(6, dtype=np.float32)
+    req = pb.ModelInferRequest(model_name="echo")
+    for n, x in (("INPUT0", x0), ("INPUT1", x1)):
+        t = req.inputs.add(name=n, datatype="FP32")
+        t.shape.extend(x.shape)
+        t.contents.fp32_contents.extend(x.tolist())
+    req.outputs.add(name="OUTPUT0")
+    req.outputs.add(name="OUTPUT1")
+    data = req.SerializeToString()
+    pr = parse_request(data)
+    assert pr.has_params  # served by the protobuf path
+    ch = GRPCChannel({"grpc_channel": echo_server.target}, Flags("echo"))
+    ch.request.CopyFrom(req)
+    resp = ch.do_inference()
+    got = {o.name: np.frombuffer(r, np.float32) for o, r in zip(resp.outputs, resp.raw_output_contents)}
+    np.testing.assert_array_equal(got["OUTPUT0"], x0)
+    np.testing.assert_array_equal(got["OUTPUT1"], x1)
+    ch.close()
+
+
 def test_server_errors_and_faults():
     repo = ModelRepository("cpu")
     repo.add(EchoModel("echo"))
@@ -222,3 +251,57 @@ def test_system_shared_memory_extension_echo():
         ch.unregister_system_shared_memory("r0")
         assert len(ch.system_shared_memory_status().regions) == 0
         ch.close()
+
+
+def test_gpu_phase_lock_prefers_a_waiting_writer():
+    """Under continuous overlapping executions (shared holders) a model load
+    (exclusive) must still get in: once a writer waits, new readers queue."""
+    import threading
+    import time
+
+    from triton_client_amd.server.model import _RWLock
+
+    lk = _RWLock()
+    lk.acquire_shared()  # an execution in flight
+    order = []
+    w = threading.Thread(target=lambda: (lk.acquire_exclusive(), order.append("w"), lk.release_exclusive()))
+    w.start()
+    time.sleep(0.05)  # the writer is waiting now
+    r = threading.Thread(target=lambda: (lk.acquire_shared(), order.append("r"), lk.release_shared()))
+    r.start()
+    time.sleep(0.05)
+    assert order == []  # the new reader yields to the pending writer
+    lk.release_shared()
+    w.join(2)
+    r.join(2)
+    assert order == ["w", "r"]
+
+
+def test_shm_unregister_waits_for_in_flight_executions(tmp_path):
+    """Unpinning a registered region must not race an execution that may be
+    DMA'ing from it: unregister waits until no execution holds GPU_PHASE."""
+    import os
+    import threading
+    import time
+
+    from triton_client_amd.server.model import GPU_PHASE
+    from triton_client_amd.server.shm import SharedMemoryRegistry
+
+    key = f"tca_test_{os.getpid()}"
+    path = os.path.join("/dev/shm", key)
+    with open(path, "wb") as f:
+        f.write(bytes(4096))
+    try:
+        reg = SharedMemoryRegistry(pin=False)
+        reg.register("r0", key, 0, 4096)
+        GPU_PHASE.acquire_shared()  # an execution in flight
+        done = threading.Event()
+        t = threading.Thread(target=lambda: (reg.unregister("r0"), done.set()))
+        t.start()
+        time.sleep(0.05)
+        assert not done.is_set()
+        GPU_PHASE.release_shared()
+        t.join(2)
+        assert done.is_set() and reg.status() == []
+    finally:
+        os.unlink(path)

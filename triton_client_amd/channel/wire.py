@@ -185,7 +185,8 @@ def parse_request(data: bytes, max_tensors: int = 64) -> ParsedRequest:
             out.datatypes[t.name] = t.datatype
             out.order.append(t.name)
         out.outputs = [o.name for o in req.outputs]
-        out.has_params = any(len(t.parameters) for t in req.inputs) or any(len(o.parameters) for o in req.outputs)
+        out.has_params = (any(len(t.parameters) for t in req.inputs) or any(len(o.parameters) for o in req.outputs)
+                          or len(req.raw_input_contents) < len(req.inputs))  # typed contents: protobuf path
         return out
     mv = memoryview(data)
     meta = np.zeros((max_tensors, 8), np.int64)

@@ -62,10 +62,11 @@ class _RWLock:
         self._cv = threading.Condition()
         self._readers = 0
         self._writer = False
+        self._writers_waiting = 0  # new readers yield to a pending writer (no load starvation)
 
     def acquire_shared(self):
         with self._cv:
-            while self._writer:
+            while self._writer or self._writers_waiting:
                 self._cv.wait()
             self._readers += 1
 
@@ -77,8 +78,12 @@ class _RWLock:
 
     def acquire_exclusive(self):
         with self._cv:
-            while self._writer or self._readers:
-                self._cv.wait()
+            self._writers_waiting += 1
+            try:
+                while self._writer or self._readers:
+                    self._cv.wait()
+            finally:
+                self._writers_waiting -= 1
             self._writer = True
 
     def release_exclusive(self):
@@ -132,10 +137,12 @@ class DynamicBatcher:
         return item.result
 
     def stop(self) -> None:
+        """Stop taking requests and wait for the batch in flight (if any) to
+        finish: the model frees its plans only after no batch runs on them."""
         with self.cv:
             self.stopped = True
             self.cv.notify_all()
-        self.thread.join(timeout=5)
+        self.thread.join()
 
     def _take(self):
         with self.cv:
@@ -235,7 +242,13 @@ class ServedModel(ABC):
         if self._batcher is not None:
             self._batcher.stop()
             self._batcher = None
-        self.ready = False
+        # no execution of this model (batched or direct) is mid-run past this point
+        GPU_PHASE.acquire_exclusive()
+        try:
+            with self._lock:
+                self.ready = False
+        finally:
+            GPU_PHASE.release_exclusive()
 
     def instance_kind(self) -> int:
         return mc.ModelInstanceGroup.KIND_GPU

@@ -120,6 +120,35 @@ class _YoloPlan:
         return [{"output": self.pin_out[i:i + 1]} for i in range(n)]
 
 
+def check_voxel_inputs(inputs: Dict[str, np.ndarray], P: int, max_voxels: int, grid_size) -> int:
+    """Validate one request's (voxels, voxel_coords, voxel_num_points) against the
+    model's voxel grid before any byte reaches the device.  The GPU consumers index
+    ``(b * ny + y) * nx + x`` (pillar scatter, canvas clear, sparse-conv rulebook)
+    without a range check, so an out-of-range cell of one request would write into
+    another request's canvas slot of a dynamic batch, or outside the allocation.
+    Returns V.  Reference contract: ``examples/pointpillar_kitti/config.pbtxt:27-52``
+    (voxels [-1, P, 4], voxel_coords [-1, 4] = (b, z, y, x), voxel_num_points [-1])."""
+    vox, co, n = inputs["voxels"], inputs["voxel_coords"], inputs["voxel_num_points"]
+    if vox.ndim != 3 or vox.shape[1] != P or vox.shape[2] < 4:
+        raise InferError(f"voxels must be [-1, {P}, 4], got {list(vox.shape)}")
+    V = vox.shape[0]
+    if V > max_voxels:
+        raise InferError(f"{V} voxels > max_voxels {max_voxels}")
+    if co.ndim != 2 or co.shape[0] != V or co.shape[1] != 4:
+        raise InferError(f"voxel_coords must be [{V}, 4], got {list(co.shape)}")
+    if n.ndim != 1 or n.shape[0] != V:
+        raise InferError(f"voxel_num_points must be [{V}], got {list(n.shape)}")
+    if V:
+        nx, ny, nz = (int(g) for g in grid_size)
+        z, y, x = co[:, 1], co[:, 2], co[:, 3]
+        if (int(z.min()) < 0 or int(z.max()) >= nz or int(y.min()) < 0 or int(y.max()) >= ny
+                or int(x.min()) < 0 or int(x.max()) >= nx):
+            raise InferError(f"voxel_coords outside the {nz}x{ny}x{nx} (z, y, x) grid")
+        if int(n.min()) < 1 or int(n.max()) > P:
+            raise InferError(f"voxel_num_points must be in [1, {P}]")
+    return V
+
+
 class _PointPillarsPlan:
     """A captured batch-B PointPillars pass from received voxels: per-frame batch
     index -> pillar VFE + canvas scatter -> BEV plan -> anchor decode + rotated
@@ -323,18 +352,15 @@ class PointPillarsModel(ServedModel):
             self.model = fuse_model(model.eval())
         self.ready = True
 
-    def _check(self, vox):
-        if vox.ndim != 3 or vox.shape[1] != self.P or vox.shape[2] < 4:
-            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
-        if vox.shape[0] > self.cfg.voxel.max_voxels:
-            raise InferError(f"{vox.shape[0]} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+    def _check(self, inputs):
+        return check_voxel_inputs(inputs, self.P, self.cfg.voxel.max_voxels, self.cfg.voxel.grid_size)
 
     @torch.no_grad()
     def execute_batch(self, batch, requested):
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
         for inp in batch:
-            self._check(inp["voxels"])
+            self._check(inp)
         return _pick(self.plans, len(batch)).run(batch)
 
     @torch.no_grad()
@@ -342,7 +368,7 @@ class PointPillarsModel(ServedModel):
         vox = inputs["voxels"]
         co = inputs["voxel_coords"]
         n = inputs["voxel_num_points"]
-        self._check(vox)
+        self._check(inputs)
         if self.device.type == "cuda":
             return self.plans[1].run([inputs])[0]
         else:
@@ -437,11 +463,7 @@ class SecondIoUModel(ServedModel):
     @torch.no_grad()
     def execute(self, inputs, requested):
         vox, co, n = inputs["voxels"], inputs["voxel_coords"], inputs["voxel_num_points"]
-        V = vox.shape[0]
-        if vox.shape[1] != self.P or vox.shape[2] < 4:
-            raise InferError(f"voxels must be [-1, {self.P}, 4], got {list(vox.shape)}")
-        if V > self.cfg.voxel.max_voxels:
-            raise InferError(f"{V} voxels > max_voxels {self.cfg.voxel.max_voxels}")
+        V = check_voxel_inputs(inputs, self.P, self.cfg.voxel.max_voxels, self.cfg.voxel.grid_size)
         v = torch.from_numpy(np.require(vox[..., :4], np.float32, ['C', 'W']))
         c = torch.from_numpy(np.require(co, np.int32, ['C', 'W'])).clone()
         c[:, 0] = 0

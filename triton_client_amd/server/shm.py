@@ -136,11 +136,25 @@ class SharedMemoryRegistry:
         with self._lock:
             names = [name] if name else list(self._regions)
             regs = [self._regions.pop(n) for n in names if n in self._regions]
+        if not regs:
+            return
+        from .model import GPU_PHASE
+
+        # An execution that chose the direct (pinned) path for a view of this region
+        # may still be DMA'ing from it: unpin only when no execution is in flight.
+        # Executions hold GPU_PHASE shared; one that starts after this block finds
+        # the region gone from _PINNED and stages its copy instead.
+        GPU_PHASE.acquire_exclusive()
+        try:
+            for r in regs:
+                if r.pinned:
+                    with _PINNED_LOCK:
+                        _PINNED.pop(_base(r.mm), None)
+                    _host_unregister(r.mm)
+                    r.pinned = False
+        finally:
+            GPU_PHASE.release_exclusive()
         for r in regs:
-            if r.pinned:
-                with _PINNED_LOCK:
-                    _PINNED.pop(_base(r.mm), None)
-                _host_unregister(r.mm)
             try:
                 r.mm.close()
             except BufferError:  # a response still references it: the mapping goes with the last view
