@@ -376,6 +376,21 @@ def main():
     if info.world > 1 and not gloo_rehearsal and rccl_ranks != args.gpus:
         raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
     ex = FrameExchange(info, native=native)
+    # with the native RCCL communicator the detection gather (grouped send / recv of fixed-shape
+    # result buffers) is stream work: capture it inside the step graph, so a step is one replay
+    gather_in_graph = (native is not None and isinstance(runner, GraphRunner) and runner.enabled
+                       and args.ingest == "local")
+    gbuf = {}
+    if gather_in_graph:
+        def step_and_gather():
+            r2, r3 = pipeline_step()
+            src = outputs(r2, r3)
+            if "dst" not in gbuf:  # allocated in the eager warm-up, before capture
+                gbuf["dst"] = ([list(src)] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)]
+                               if info.is_main else None)
+            ex.gather(src, gbuf["dst"])
+            return r2, r3
+        runner = GraphRunner(step_and_gather)
 
     jdec = None
     if use_cam and args.camera_input == "jpeg":
@@ -435,18 +450,22 @@ def main():
                 lid.data.copy_(pc_host[0], non_blocking=True)
                 lid.frame_n.copy_(n_host[0], non_blocking=True)
             return
-        src = None
         if info.is_main:
             if use_cam:
                 node["cam"].copy_(cam_host, non_blocking=True)
             if use_lid:
                 node["pc"].copy_(pc_host, non_blocking=True)
                 node["n"].copy_(n_host, non_blocking=True)
-            src = [[t for t in ((node["cam"][r],) if use_cam else ()) + ((node["pc"][r], node["n"][r]) if use_lid else ())]
-                   for r in range(info.world)]
-        ex.scatter(src, dsts)
+        ex.scatter(scatter_src(), dsts)
+
+    def scatter_src():
+        if not info.is_main:
+            return None
+        return [[t for t in ((node["cam"][r],) if use_cam else ()) + ((node["pc"][r], node["n"][r]) if use_lid else ())]
+                for r in range(info.world)]
 
     gather_dst = None
+    last_src = [None]
     host_out = None  # [2][world][k]: double-buffered so step t's D2H overlaps step t+1
     out_ready = [torch.cuda.Event(), torch.cuda.Event()]
     it = [0]
@@ -471,13 +490,16 @@ def main():
         if jdec is not None:
             stage_next_jpegs()  # host decode overlaps this step's GPU work
         src = outputs(r2, r3)
+        last_src[0] = src
         if gather_dst is None and info.is_main:
             # rank 0's own detections are D2H-copied straight from the graph's result
             # buffers (stream order keeps the next replay behind that copy)
-            gather_dst = [list(src)] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)]
+            gather_dst = (gbuf["dst"] if gather_in_graph else
+                          [list(src)] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)])
             host_out = [[[torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in src] for _ in range(info.world)]
                         for _ in range(2)]
-        ex.gather(src, gather_dst if info.is_main else None)
+        if not gather_in_graph:
+            ex.gather(src, gather_dst if info.is_main else None)
         k = it[0] % 2
         if info.is_main:
             for r in range(info.world):
@@ -504,6 +526,27 @@ def main():
     barrier(info)
     elapsed = time.perf_counter() - t0
     elapsed = allreduce_max(info, elapsed)
+    # DP communication alone, after the timed run (every rank takes part): the
+    # detection gather (captured in the step graph when gather_in_graph) and the
+    # --ingest rccl frame scatter, µs per step, max over ranks
+    comm_us = None
+    if info.world > 1:
+        def _time_us(fn, reps=10):
+            barrier(info)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            return allreduce_max(info, 1e3 * e0.elapsed_time(e1) / reps)
+        comm_us = {"gather": round(_time_us(lambda: ex.gather(last_src[0], gather_dst if info.is_main else None)), 1),
+                   "gather_bytes_per_rank": int(sum(t.numel() * t.element_size() for t in last_src[0])),
+                   "gather_in_graph": gather_in_graph}
+        if args.ingest == "rccl":
+            comm_us["scatter"] = round(_time_us(lambda: ex.scatter(scatter_src(), dsts)), 1)
+            comm_us["scatter_bytes_per_rank"] = int(sum(t.numel() * t.element_size() for t in dsts))
     jpeg_info = None
     if jdec is not None:
         host_us = jdec.host_us_per_frame()
@@ -584,6 +627,7 @@ def main():
                                (args.graph_mode if side is not None else "single")),
                 "sub_batches": S,
                 "host_bytes_per_gpu_per_step": step_bytes,
+                "dp_comm_us_per_step": comm_us,
                 "avg_2d_dets_per_frame": det2,
                 "avg_3d_dets_per_frame": det3,
                 "setup_plus_warmup_s": round(t0 - t_setup, 1),

@@ -1,0 +1,335 @@
+// fp32-mode halo-tiled 3x3 stride-1 convolution with register-streamed weights
+// ("hx3") for the PointPillars / CenterPoint BEV backbones
+// (data/pointpillar.yaml:64-70 BaseBEVBackbone, run by
+// examples/pointpillar_kitti/1/model.py:163): pair activations in and out,
+// split-product MFMA (bf16 x3, fp32 accumulation; see conv_mfma.hip "fp32 mode").
+#include "tca_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Hx3Args {
+  const float* in_f;   // pair storage [B, H, W, ldi], channels [ci_off, ci_off + Cin)
+  const float* res_f;  // pair residual [B, H, W, ldr] (channels [r_off, r_off + N)) or null
+  float* out_f;        // pair output [B, H, W, ldo], channels [co_off, co_off + N)
+  const void* w;       // fragment-order split weights (tca_conv_hx3p)
+  const float* bias;   // [N] or null
+  int B, H, W, Cin, ldi, ci_off, Ho, Wo;
+  int N, ldo, co_off, ldr, r_off;
+  int act;  // 0 none, 1 relu, 2 silu, 3 leaky(0.1); | 16: act after the residual add
+};
+
+constexpr unsigned kOutOfRange = 0x80000000u;  // buffer offset past any num_records (< 2^31): reads zeros
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  switch (act) {
+    case 1: return fmaxf(v, 0.f);
+    case 2: return v / (1.f + __expf(-v));
+    case 3: return v > 0.f ? v : 0.1f * v;
+    default: return v;
+  }
+}
+
+// slot swizzle of halo position hx (0..17), as conv_mfma.hip hx: conflict-free b128
+// fragment reads at the three tap shifts
+__device__ __forceinline__ int hswz(int hx) { return (0xb29108 >> (3 * (hx >> 1))) & 7; }
+
+// x * w ~= xh*wh + xh*wl + xl*wh on the bf16 MFMA (fp32 accumulate), same order as conv_mfma.hip
+__device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
+                                      const bf16x8& al) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ void pair_split8(const float* v, uint4& hi, uint4& lo) {
+  __bf16 h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  hi = *reinterpret_cast<const uint4*>(h);
+  lo = *reinterpret_cast<const uint4*>(l);
+}
+
+__device__ __forceinline__ void pair_join8(const float* p, float* v) {
+  const uint4 hq = *reinterpret_cast<const uint4*>(p);
+  const uint4 lq = *reinterpret_cast<const uint4*>(p + 4);
+  const __bf16* h = reinterpret_cast<const __bf16*>(&hq);
+  const __bf16* l = reinterpret_cast<const __bf16*>(&lq);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
+}
+
+// ---- x3 pair, halo-tiled 3x3 stride 1, v3 ("hx3"): weights streamed to registers.
+//
+// PMC of hx (profiles/r2/pmc_lidar_end/summary.md): waves 34% parked at the per-step
+// `vmcnt(0)` + barrier that the shared LDS weight ring needs (a 2-deep ring: the
+// weights of step s+1 must land inside step s), 24 MFMAs per wave between barriers.
+// Here the LDS holds only the input halo; each wave owns its own output channels
+// (WM = 1: no two waves of a workgroup need the same weight fragment) and loads
+// its B fragments straight from HBM/L2 into a 3-deep register ring, two steps
+// ahead, from a host-permuted weight image in MFMA fragment order
+// ([K step][16-channel group][hi | lo][lane][8 bf16]: every fragment load is one
+// contiguous 1 KiB).  No barrier inside a 32-channel chunk: the 9 tap steps of a
+// chunk run barrier-free (one or two barriers per chunk, at the halo swap).  The
+// next chunk's halo is fetched into registers at the start of a chunk by
+// buffer loads (zero padding by the descriptor range check; every load counted
+// by the compiler, no mixed DMA / register-load queues) and written to LDS at
+// its end.  Per wave 128 pixels x 32 channels: 16 ds_read_b128 per 48 MFMAs.
+// Same products and fp32 summation order per output as hx (chunk-major, tap
+// inner), so the results are bit-identical to hx.
+template <int TH, int BN, int WM, int WN, bool CM, int HB>
+__global__ void __launch_bounds__(WM * WN * 64, 2) conv_hx3_kernel(Hx3Args a) {
+  constexpr int TW = 16, BM = TH * TW, NW = WM * WN, NT = NW * 64;
+  constexpr int FM = TH / WM, FN = BN / WN / 16;
+  static_assert(TH % WM == 0 && BN % (WN * 16) == 0 && FN >= 1, "tiles");
+  static_assert(HB == 1 || HB == 2, "halo buffers");
+  constexpr int HWD = TW + 2, HP = (TH + 2) * HWD;  // halo pixels (lines x positions)
+  constexpr int HPIECES = HP * 8;                    // 16-B pieces of one 32-channel pair chunk
+  constexpr int HPL = (HPIECES + NT - 1) / NT;       // halo loads per lane per chunk
+  constexpr int HBYTES = HP * 128;
+  constexpr int EPI = BM * (BN + 4) * 4;
+  constexpr int LDS = (HB * HBYTES > EPI) ? HB * HBYTES : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  constexpr int EX = CM ? TH : TW, EY = CM ? TW : TH;
+  const int tx_n = (a.Wo + EX - 1) / EX, ty_n = (a.Ho + EY - 1) / EY;
+  const int nmt = a.B * ty_n * tx_n, nnt = a.N / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
+  const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
+  const int n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
+  // halo pieces of this lane: global byte offset (chunk 0) and LDS byte offset (-1: none)
+  unsigned h_off[HPL];
+  int h_lds[HPL];
+#pragma unroll
+  for (int k = 0; k < HPL; ++k) {
+    const int q = tid + k * NT, p = q >> 3, piece = q & 7;
+    h_off[k] = kOutOfRange;
+    h_lds[k] = -1;
+    if (q < HPIECES) {
+      const int u = p / HWD, v = p - (p / HWD) * HWD;
+      const int hy = CM ? v : u, hx = CM ? u : v;
+      const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+      if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+        h_off[k] = (unsigned)((((b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off) * 4 + piece * 16);
+      h_lds[k] = p * 128 + ((piece ^ hswz(v)) << 4);
+    }
+  }
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 hreg[HPL];
+  auto halo_load = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < HPL; ++k) hreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, h_off[k], c * 128, 0);
+  };
+  auto halo_write = [&](int buf) {
+    unsigned char* dst = smem + buf * HBYTES;
+#pragma unroll
+    for (int k = 0; k < HPL; ++k)
+      if (k + 1 < HPL || h_lds[k] >= 0) *reinterpret_cast<u32x4*>(dst + h_lds[k]) = hreg[k];
+  };
+
+  // weights, fragment image: block (ks, g, h) = 64 lanes x 8 bf16
+  const int NG = a.N / 16, g0 = (n0 + wn * FN * 16) / 16;
+  const __bf16* wf = reinterpret_cast<const __bf16*>(a.w) + (long)g0 * 1024 + lane * 8;
+  const int nc = a.Cin / 32;
+  auto wload = [&](int ks, bf16x8 (&dst)[FN][2]) {  // ks: K step in the [tap][ci] weight K order
+    const __bf16* p = wf + (long)ks * NG * 1024;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      dst[j][0] = *reinterpret_cast<const bf16x8*>(p + j * 1024);
+      dst[j][1] = *reinterpret_cast<const bf16x8*>(p + j * 1024 + 512);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A tap group = the 3 taps that share one shift kf along the fragment axis: their
+  // A fragments are the same halo lines offset by kl = 0..2, so the group reads
+  // FM + 2 line fragments (not 3 * FM) and feeds each to up to 3 taps at once.
+  // Its 3 taps' weights are live for the whole group; the next group's are
+  // prefetched into the second register set when the group starts.
+  const int G = 3 * nc;
+  auto gload = [&](int gs, bf16x8 (&dst)[3][FN][2]) {  // group gs = chunk gs / 3, shift gs % 3
+    const int c = gs / 3, kf = gs - (gs / 3) * 3;
+#pragma unroll
+    for (int kl = 0; kl < 3; ++kl) {
+      const int t = CM ? 3 * kf + kl : 3 * kl + kf;  // tap index ky * 3 + kx
+      wload(t * nc + c, dst[kl]);
+    }
+  };
+  bf16x8 wc[3][FN][2], wx[3][FN][2];
+  halo_load(0);
+  gload(0, wc);
+  halo_write(0);
+  halo_load(nc > 1 ? 1 : 0);  // next chunk's halo rides in registers through chunk 0
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int c = 0; c < nc; ++c) {
+    const unsigned char* hb = smem + (HB == 2 ? (c & 1) * HBYTES : 0);
+#pragma unroll
+    for (int kf = 0; kf < 3; ++kf) {
+      {
+        const int gs = c * 3 + kf + 1;
+        gload(gs < G ? gs : G - 1, wx);  // unconditional (clamped): no branch around the loads
+      }
+      // keep the prefetch at the top of the group: hipcc's scheduler otherwise sinks the
+      // loads next to the register copy at the group's end and waits for them there
+      __builtin_amdgcn_sched_barrier(0);
+      const int sw = hswz(kf + fr);
+      const unsigned char* colp = hb + (wm * FM) * HWD * 128 + (kf + fr) * 128;
+      const int o_hi = ((2 * fq) ^ sw) << 4, o_lo = ((2 * fq + 1) ^ sw) << 4;
+#pragma unroll
+      for (int L = 0; L < FM + 2; ++L) {
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
+#pragma unroll
+        for (int kl = 0; kl < 3; ++kl) {
+          const int i = L - kl;
+          if (i < 0 || i >= FM) continue;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wc[kl][j][0], wc[kl][j][1], ah, al);
+        }
+      }
+#pragma unroll
+      for (int kl = 0; kl < 3; ++kl)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          wc[kl][j][0] = wx[kl][j][0];
+          wc[kl][j][1] = wx[kl][j][1];
+        }
+    }
+    if (c + 1 < nc) {
+      if constexpr (HB == 1) {  // every wave done with this chunk's halo before it is overwritten
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      halo_write(HB == 2 ? (c + 1) & 1 : 0);
+      halo_load(c + 2 < nc ? c + 2 : nc - 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
+  asm volatile("" ::: "memory");
+
+  // epilogue (as hx): tile row ml = (line) * 16 + position along the fragment axis
+  constexpr int LD = BN + 4;
+  float* st = reinterpret_cast<float*>(smem);
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
+  const int eact = post_res ? 0 : act;  // wave-uniform: one branch per fragment, not per element
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = (wn * FN + j) * 16 + fq * 4;
+    const float4 bv = a.bias ? *reinterpret_cast<const float4*>(a.bias + n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = (wm * FM + i) * 16 + fr;
+      float4 q = make_float4(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w);
+      if (eact == 1) {
+        q.x = fmaxf(q.x, 0.f); q.y = fmaxf(q.y, 0.f); q.z = fmaxf(q.z, 0.f); q.w = fmaxf(q.w, 0.f);
+      } else if (eact != 0) {
+        q.x = act_fn(q.x, eact); q.y = act_fn(q.y, eact); q.z = act_fn(q.z, eact); q.w = act_fn(q.w, eact);
+      }
+      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+    }
+  }
+  __syncthreads();
+  constexpr int V8 = BN / 8;
+  for (int id = tid; id < BM * V8; id += NT) {
+    const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
+    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15)), n = n0 + c8;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    float v[8];
+    const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
+    const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
+    if (a.res_f) {
+      float r[8];
+      pair_join8(a.res_f + pix * a.ldr + a.r_off + n, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
+    }
+    const long o = pix * a.ldo + a.co_off + n;
+    uint4 hi, lo;
+    pair_split8(v, hi, lo);
+    *reinterpret_cast<uint4*>(a.out_f + o) = hi;
+    *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+  }
+}
+
+template <int TH, int BN, int WM, int WN, bool CM, int HB>
+int launch_hx3(const Hx3Args& a, hipStream_t stream) {
+  if (a.N % BN) return (int)hipErrorInvalidValue;
+  const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
+  const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
+  conv_hx3_kernel<TH, BN, WM, WN, CM, HB><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// hx3 tiles.  0 = auto: N % 128 == 0 -> 8 x 16 tiles, 4 waves of 128 pixels x 32 channels
+// (row- or column-major by the smaller padding); N == 64 -> 8 x 16 tiles, 2 x 2 waves of
+// 64 pixels x 32 channels.  Every variant: 2 waves per SIMD (<= 256 VGPRs, no spill), two
+// workgroups per CU (<= 80 KiB LDS).
+int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
+  if (tile == 0) {
+    const long rm8 = (long)((a.Wo + 15) / 16 * 16) * ((a.Ho + 7) / 8 * 8);
+    const long cm8 = (long)((a.Ho + 15) / 16 * 16) * ((a.Wo + 7) / 8 * 8);
+    if (a.N % 128 == 0) tile = cm8 < rm8 ? 2 : 1;
+    else if (a.N % 64 == 0) tile = cm8 < rm8 ? 4 : 3;
+    else return (int)hipErrorInvalidValue;
+  }
+  switch (tile) {
+    case 1: return launch_hx3<8, 128, 1, 4, false, 2>(a, stream);
+    case 2: return launch_hx3<8, 128, 1, 4, true, 2>(a, stream);
+    case 3: return launch_hx3<8, 64, 2, 2, false, 2>(a, stream);
+    case 4: return launch_hx3<8, 64, 2, 2, true, 2>(a, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// fp32 mode, pair activations in and out, 3x3 stride 1 pad 1 (conv_hx3_kernel).
+// wfrag: the split weights permuted to MFMA fragment order (ops/conv.py frag_weights):
+// [9 * Cin / 32][N / 16][hi | lo][64 lanes][8 bf16]; N % 64 == 0, Cin % 32 == 0.
+// Residual (pairs) and act as tca_conv_nhwc_x3p.  tile: 0 auto, 1-4 (hx3_launch).
+TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
+                          const float* bias, int N, float* out, int ldo, int co_off, int act, const float* res,
+                          int ldr, int r_off, int tile, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
+  if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
+  Hx3Args a;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
+  a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
+  if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
+  return hx3_launch(a, tile, stream);
+}

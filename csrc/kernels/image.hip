@@ -213,7 +213,79 @@ __global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict
   for (int v = 0; v < NV; ++v) o[v] = reinterpret_cast<uint4*>(px)[v];
 }
 
+// Served-model input path: a request tensor that is already model-sized fp32 NCHW
+// RGB (the reference's contracts: examples/YOLOv5/config.pbtxt "images" [3, H, W],
+// examples/RetinaNet_detectron/config.pbtxt "input__00" [3, 640, 480], 0..255 un-
+// normalised) -> per-channel affine (x * scale + bias, e.g. Detectron2's (x - mean) / std
+// folded in) -> the plans' input layouts: NHWC x 8 (3 channels + 5 zeros, 16-B stores) or
+// space-to-depth 2x2 x 16 (YOLOv5 S2D stem).  One thread per pixel / 2x2 block.
+template <typename T, int LAYOUT>
+__global__ void __launch_bounds__(256) planar_affine_kernel(const float* __restrict__ src, T* __restrict__ dst,
+                                                            int B, int H, int W, float sc0, float sc1, float sc2,
+                                                            float b0, float b1, float b2) {
+  const float sc[3] = {sc0, sc1, sc2}, bi[3] = {b0, b1, b2};
+  const long plane = (long)H * W;
+  const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (LAYOUT == 1) {
+    if (gid >= (unsigned)(B * plane)) return;
+    const long b = gid / plane, pix = gid - b * plane;
+    const float* s = src + b * 3 * plane + pix;
+    T px[8];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) px[c] = from_f32<T>(s[c * plane] * sc[c] + bi[c]);
+#pragma unroll
+    for (int c = 3; c < 8; ++c) px[c] = from_f32<T>(0.f);
+    uint4* o = reinterpret_cast<uint4*>(dst + (long)gid * 8);
+#pragma unroll
+    for (int v = 0; v < (int)(8 * sizeof(T) / 16); ++v) o[v] = reinterpret_cast<uint4*>(px)[v];
+  } else {
+    const int h2 = H >> 1, w2 = W >> 1;
+    if (gid >= (unsigned)(B * h2 * w2)) return;
+    const int X = gid % w2, Y = (gid / w2) % h2, b = gid / (w2 * h2);
+    const float* s = src + (long)b * 3 * plane;
+    T px[16];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const long pix = (long)(2 * Y + (d >> 1)) * W + 2 * X + (d & 1);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) px[d * 3 + c] = from_f32<T>(s[c * plane + pix] * sc[c] + bi[c]);
+    }
+#pragma unroll
+    for (int c = 12; c < 16; ++c) px[c] = from_f32<T>(0.f);
+    uint4* o = reinterpret_cast<uint4*>(dst + (long)gid * 16);
+#pragma unroll
+    for (int v = 0; v < (int)(16 * sizeof(T) / 16); ++v) o[v] = reinterpret_cast<uint4*>(px)[v];
+  }
+}
+
 }  // namespace
+
+// fp32 NCHW [B, 3, H, W] -> dst NHWC x 8 (layout 1) or space-to-depth [B, H/2, W/2, 16]
+// (layout 2), fp32 or bf16, x * scale[c] + bias[c].
+TCA_API int tca_planar_affine(const float* src, int B, int H, int W, void* dst, int dst_dtype, int dst_layout,
+                              float sc0, float sc1, float sc2, float b0, float b1, float b2, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((dst_layout != 1 && dst_layout != 2) || (dst_layout == 2 && ((H & 1) || (W & 1))) ||
+      (dst_dtype != kF32 && dst_dtype != kBF16))
+    return (int)hipErrorInvalidValue;
+  const long n = dst_layout == 1 ? (long)B * H * W : (long)B * (H / 2) * (W / 2);
+  if (n >= (1L << 31)) return (int)hipErrorInvalidValue;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (dst_layout == 1) {
+    if (dst_dtype == kF32)
+      planar_affine_kernel<float, 1><<<g, 256, 0, stream>>>(src, (float*)dst, B, H, W, sc0, sc1, sc2, b0, b1, b2);
+    else
+      planar_affine_kernel<__hip_bfloat16, 1><<<g, 256, 0, stream>>>(src, (__hip_bfloat16*)dst, B, H, W, sc0, sc1,
+                                                                      sc2, b0, b1, b2);
+  } else {
+    if (dst_dtype == kF32)
+      planar_affine_kernel<float, 2><<<g, 256, 0, stream>>>(src, (float*)dst, B, H, W, sc0, sc1, sc2, b0, b1, b2);
+    else
+      planar_affine_kernel<__hip_bfloat16, 2><<<g, 256, 0, stream>>>(src, (__hip_bfloat16*)dst, B, H, W, sc0, sc1,
+                                                                      sc2, b0, b1, b2);
+  }
+  TCA_LAUNCH_CHECK();
+}
 
 // Preprocess `batch` frames of identical geometry.
 TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src_h, int src_w, int src_row_stride,

@@ -166,6 +166,37 @@ def test_detectron_served_contract(cuda):
         ch.close()
 
 
+@pytest.mark.gpu
+def test_served_test_model_fp32_matches_local_engine(cuda):
+    """The served ``test_model`` (RetinaNet, examples/RetinaNet_detectron/config.pbtxt:
+    FP32 input__00 [3, 640, 480]) runs the fp32 plan, normalisation folded into the
+    input-layout kernel, as a captured batch plan; its kept set equals the local fp32
+    engine's on the same frame (stretch at the model size: the same input values),
+    singly and inside a dynamic batch."""
+    from triton_client_amd.inference.engines import LocalDetector2D
+    from triton_client_amd.server.models import DetectronModel
+    from triton_client_amd.utils.synthetic import camera_frame
+
+    served = DetectronModel("test_model", device=cuda)
+    served.load()
+    assert served.pipe.precision == "fp32"
+    assert next(served.model.parameters()).dtype == torch.float32
+    local = LocalDetector2D(family="retinanet", img=(640, 480), batch=2, letterbox=False, device=cuda)
+    local.calibrate_synthetic(0)
+    frame = camera_frame(640, 480, 11)
+    want = local.detect([frame])[0]
+    x = np.ascontiguousarray(frame.transpose(2, 0, 1)).astype(np.float32)
+    one = served.execute({"input__00": x}, None)
+    many = served.execute_batch([{"input__00": x}, {"input__00": x[:, ::-1].copy()}, {"input__00": x}], None)
+    assert len(want) > 0
+    for got in (one, many[0], many[2]):
+        assert len(got["scores__2"]) == len(want)
+        np.testing.assert_allclose(got["bboxex__0"], want[:, :4], rtol=1e-4, atol=1e-3)
+        np.testing.assert_allclose(got["scores__2"], want[:, 4], rtol=1e-4, atol=1e-5)
+        np.testing.assert_array_equal(got["classes__1"], want[:, 5].astype(np.int64))
+        assert got["dims__3"].tolist() == [[640, 480]]
+
+
 def test_reference_model_repository_families():
     """Every config.pbtxt of the reference maps to a served model family with the
     same tensor contract (no model is loaded)."""

@@ -94,3 +94,81 @@ def test_dp_device_resident_two_ranks(cuda):
         if p.is_alive():
             p.kill()
     assert res == {0: "ok", 1: "served 1 1"}, res
+
+
+def _family_worker(rank, world, port, q, family):
+    """Every reference family on the device-resident DP path: rank 0's gathered
+    detections vs a single-rank run of the same engine on the same inputs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import faulthandler
+    faulthandler.dump_traceback_later(280, exit=True)
+    try:
+        import torch
+
+        from triton_client_amd.inference.engines import LocalDetector2D, LocalDetector3D
+        from triton_client_amd.parallel.dp import DataParallelDetector2D, DataParallelDetector3D, init_distributed
+        from triton_client_amd.ros.compat import create_cloud_xyzi
+        from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+
+        info = init_distributed("gloo")
+        three_d = family in ("centerpoint", "second_iou")
+        if three_d:
+            det = LocalDetector3D(batch=2, device=info.device, max_points=65536, family=family)
+            dp = DataParallelDetector3D(det, info, max_out=500, box_dim=det.box_dim)
+        else:
+            det = LocalDetector2D(batch=2, device=info.device, family=family, img=(640, 480) if family != "yolov4"
+                                  else 512, nc=80)
+            dp = DataParallelDetector2D(det, info, max_det=300)
+        det.calibrate_synthetic(0)
+        if rank != 0:
+            def no_host(*a, **k):
+                raise AssertionError("worker rank used the host detect() path")
+            det.detect = no_host
+        if info.is_main:
+            if three_d:
+                spec = LidarSpec(rings=32, azimuth_steps=1800, sensor_height=1.8)
+                items = [create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, 300 + i).tobytes(), np.float32)
+                                           .reshape(-1, 4)) for i in range(3)]
+            else:
+                items = [camera_frame(360, 640, 400 + i) for i in range(3)]
+            got = dp.detect(items)
+            dp.close()
+            want = det.detect(items)
+            for g, w in zip(got, want):
+                if three_d:
+                    gs, ws = g["pred_scores"], w["pred_scores"]
+                    assert g["pred_boxes"].shape[1] == w["pred_boxes"].shape[1] == det.box_dim
+                else:
+                    gs, ws = g[:, 4], w[:, 4]
+                assert len(ws) > 0 and abs(len(gs) - len(ws)) <= max(1, len(ws) // 50), (len(gs), len(ws))
+                np.testing.assert_allclose(np.sort(gs)[-10:], np.sort(ws)[-10:], rtol=1e-4, atol=1e-5)
+            q.put((0, "ok"))
+        else:
+            q.put((rank, f"served {dp.serve()}"))
+        torch.cuda.synchronize()
+        q.close()
+        q.join_thread()
+        os._exit(0)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        q.close()
+        q.join_thread()
+        os._exit(1)
+
+
+@pytest.mark.parametrize("family", ["centerpoint", "retinanet", "fcos", "yolov4"])
+def test_dp_families_two_ranks(cuda, family):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_family_worker, args=(r, 2, port, q, family)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert res == {0: "ok", 1: "served 1"}, res

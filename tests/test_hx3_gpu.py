@@ -1,0 +1,97 @@
+"""conv_hx3.hip: halo-tiled 3x3 stride-1 pair convolution with register-streamed
+fragment-order weights (the fp32-mode BEV backbone layers), against fp64
+references, and close to the conv_mfma.hip halo kernel (same products)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+from triton_client_amd.ops.conv import NHWC, FusedConv, frag_weights, from_pairs, split_bf16, to_pairs
+
+
+def rel_l2(got, ref):
+    got, ref = got.double().cpu(), ref.double().cpu()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+def test_frag_weights_layout_cpu():
+    """Block (ks, g, h), lane fq * 16 + fr, element e holds W[16 g + fr, 32 ks + 8 fq + e] (hi / lo)."""
+    torch.manual_seed(0)
+    N, Kp = 48, 96
+    W = torch.randn(N, Kp)
+    wf = frag_weights(W)
+    assert wf.shape == (Kp // 32, N // 16, 2, 4, 16, 8) and wf.dtype == torch.bfloat16
+    hi, lo = split_bf16(W)
+    for ks, g, fq, fr, e in [(0, 0, 0, 0, 0), (2, 1, 3, 15, 7), (1, 2, 1, 7, 3)]:
+        n, k = 16 * g + fr, 32 * ks + 8 * fq + e
+        assert wf[ks, g, 0, fq, fr, e] == hi[n, k] and wf[ks, g, 1, fq, fr, e] == lo[n, k]
+
+
+SHAPES = [(2, 23, 31, 64, 128), (1, 21, 37, 256, 256), (2, 19, 50, 64, 64), (3, 9, 16, 96, 128),
+          (2, 8, 16, 32, 64), (1, 62, 54, 128, 256)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [110, 111, 112, 113, 114])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_hx3_tiles_vs_fp64(cuda, tile, shape):
+    """Channel-offset input / output slices, partial row and column tiles, odd
+    chunk counts (Cin 96), a pair residual and ReLU, against fp64; the channels
+    outside the output slice stay untouched; and agreement with the halo kernel
+    of conv_mfma.hip (tile 90: the same products in another summation order)."""
+    B, H, W, cin, cout = shape
+    if tile in (111, 112) and cout % 128:
+        pytest.skip("128-channel tiles need N % 128 == 0")
+    torch.manual_seed(tile + cin + cout)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    assert fc.hx3_ok()
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    res = torch.randn(B, H, W, cout, dtype=torch.float64)
+    x = NHWC(to_pairs(buf.float()).to(cuda), 8, cin, pair=True)
+    r = NHWC(to_pairs(res.float()).to(cuda), pair=True)
+    outs = {}
+    for t in (tile, 90):
+        out = torch.full((B, H, W, cout + 16), 7.0, dtype=torch.float32, device=cuda)
+        fc(x, out=NHWC(out, 8, cout, pair=True), res=r, tile=t)
+        torch.cuda.synchronize()
+        outs[t] = out
+        assert (out[..., :8] == 7.0).all() and (out[..., 8 + cout:] == 7.0).all()
+    ref = torch.relu(conv(buf[..., 8:8 + cin].permute(0, 3, 1, 2))) + from_pairs(r.t).double().cpu().permute(0, 3, 1, 2)
+    got = NHWC(outs[tile], 8, cout, pair=True).nchw()
+    assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
+    hx = NHWC(outs[90], 8, cout, pair=True).nchw()
+    assert rel_l2(got, hx) < 2e-5, rel_l2(got, hx)
+
+
+@pytest.mark.gpu
+def test_hx3_post_residual_act_and_no_bias(cuda):
+    """act(conv + residual) (the ResNet form, act flag | 16) and a bias-free conv."""
+    torch.manual_seed(3)
+    B, H, W, cin, cout = 2, 17, 29, 64, 128
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32", post_res=True)
+    xin = torch.randn(B, H, W, cin, dtype=torch.float64)
+    res = torch.randn(B, H, W, cout, dtype=torch.float64)
+    out = NHWC(torch.empty(B, H, W, cout, device=cuda), pair=True)
+    fc(NHWC(to_pairs(xin.float()).to(cuda), pair=True), out=out, res=NHWC(to_pairs(res.float()).to(cuda), pair=True),
+       tile=110)
+    torch.cuda.synchronize()
+    ref = torch.relu(conv(xin.permute(0, 3, 1, 2)) + from_pairs(to_pairs(res.float())).double().permute(0, 3, 1, 2))
+    assert rel_l2(out.nchw(), ref) < 5e-5
+
+
+@pytest.mark.gpu
+def test_hx3_is_the_default_for_pair_backbone_layers(cuda):
+    """tile 0 routes an eligible pair conv to hx3 (the same bits as tile 110)."""
+    torch.manual_seed(5)
+    B, H, W, cin, cout = 2, 20, 24, 128, 128
+    fc = FusedConv(nn.Conv2d(cin, cout, 3, 1, 1), act=1, device=cuda, precision="fp32")
+    x = NHWC(to_pairs(torch.randn(B, H, W, cin)).to(cuda), pair=True)
+    a = NHWC(torch.empty(B, H, W, cout, device=cuda), pair=True)
+    b = NHWC(torch.empty(B, H, W, cout, device=cuda), pair=True)
+    fc(x, out=a, tile=0)
+    fc(x, out=b, tile=110)
+    torch.cuda.synchronize()
+    assert torch.equal(a.t, b.t)

@@ -81,6 +81,36 @@ def test_preprocess_s2d_gpu(cuda, mode):
     assert torch.equal(got.cpu(), exp.cpu())
 
 
+def _greedy_replay(gbox, box, score, cls, tie, thr, pre_max, max_out, agnostic, eps=1e-5):
+    """Replay greedy rotated NMS over the candidates in the GPU's sort order (score
+    desc, tie asc), taking the GPU's keep / drop decision for each and checking it
+    against the fp64 IoU with the boxes the GPU kept before it.  Returns (decisions
+    that differ from fp64, decisions whose fp64 max-IoU lies within eps of the
+    threshold); asserts every difference is one of the latter and that the replay
+    reproduces the GPU's whole kept list in order."""
+    from triton_client_amd.ops import golden
+
+    row = {box[i].tobytes(): i for i in range(len(box))}
+    gidx = [row[r.astype(np.float32).tobytes()] for r in gbox]
+    gset = set(gidx)
+    order = np.lexsort((tie, -score.astype(np.float64)))[:pre_max]
+    kept, flips, near = [], 0, 0
+    for i in order:
+        if len(kept) >= max_out:
+            break
+        prior = [k for k in kept if agnostic or cls[k] == cls[i]]
+        mx = float(golden.rotated_iou_bev(box[i].astype(np.float64), box[prior].astype(np.float64)).max()) if prior else 0.0
+        borderline = abs(mx - thr) < eps
+        near += borderline
+        if (i in gset) != (mx <= thr):
+            assert borderline, (i, mx, thr)
+            flips += 1
+        if i in gset:
+            kept.append(int(i))
+    assert kept == gidx, "the GPU kept list is not a greedy outcome in score order"
+    return flips, near
+
+
 @pytest.mark.parametrize("rotated,agnostic", [(False, False), (True, True), (True, False)])
 @pytest.mark.parametrize("pre_max", [64, 1000, 4096])
 def test_sort_nms_gpu_vs_golden(cuda, rotated, agnostic, pre_max):
@@ -103,10 +133,16 @@ def test_sort_nms_gpu_vs_golden(cuda, rotated, agnostic, pre_max):
                                 agnostic)
         ref_box = box[b, keep]
         g = got[b]
-        if rotated:  # rotated IoU: allow a borderline flip or two from fp32 clipping order
-            assert abs(len(keep) - len(g["box"])) <= 2
-            k = min(len(keep), len(g["box"]), 20)
-            np.testing.assert_allclose(g["box"][:k], ref_box[:k], rtol=1e-6)
+        if rotated:
+            # the GPU's full kept list must be the greedy outcome under the fp64 rotated IoU
+            # (ops/golden.py): a decision may differ from fp64 only where the fp64 IoU is
+            # within 1e-5 of the threshold (fp32 polygon clipping), and those are counted
+            flips, near = _greedy_replay(g["box"], box[b, :m], score[b, :m], cls[b, :m], tie, thr, pre_max,
+                                         max_out, agnostic)
+            assert flips <= near, (flips, near)
+            if near == 0:
+                np.testing.assert_array_equal(g["box"], ref_box)  # no borderline pair: the exact fp64 kept set
+            np.testing.assert_array_equal(g["cls"], cls[b, keep] if flips == 0 else g["cls"])
         else:
             assert len(keep) == len(g["box"])
             np.testing.assert_allclose(g["box"], ref_box, rtol=1e-6)

@@ -1,0 +1,153 @@
+"""Live-driver GPU bench: the reference's actual loop, message in -> message published.
+
+The reference's product is the subscriber callback: CompressedImage -> decode ->
+preprocess -> ModelInfer -> NMS -> draw -> publish ``Image``
+(``communicator/ros_inference.py:117-175``), and PointCloud2 -> ``read_points`` ->
+voxelise -> ModelInfer -> filter -> jsk ``BoundingBoxArray`` -> publish
+(``communicator/ros_inference3d.py:120-213``).  ``bench.py`` times the device step
+from raw pinned bytes to device detections; this tool times the drivers
+(:class:`RosInference` / :class:`RosInference3D`) with the local GPU engines over
+the in-process topic bus, including JPEG decode, micro-batching, the ordered
+re-publisher, GPU annotation and building the published messages.
+
+    python tools/driver_bench.py [--camera N] [--lidar N] [--batch B] [--workers W]
+
+Messages are published paced so the latest-wins windows never drop (every
+message is detected and published); throughput = messages / wall time from the
+first publish to the last published result.  Prints one JSON line.
+"""
+import argparse
+import io
+import json
+import sys
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, ".")
+
+
+class _Stages:
+    """ClientMetrics stand-in: per-stage sums (StageTimer calls .stage / .frame)."""
+
+    def __init__(self):
+        self.sum, self.n, self.lock = {}, {}, threading.Lock()
+
+    def stage(self, name, seconds):
+        with self.lock:
+            self.sum[name] = self.sum.get(name, 0.0) + seconds
+            self.n[name] = self.n.get(name, 0) + 1
+
+    def frame(self, n=1):
+        pass
+
+    def bytes(self, n):
+        pass
+
+    def summary(self):
+        return {k: {"calls": self.n[k], "ms_per_call": round(1e3 * v / self.n[k], 3)} for k, v in self.sum.items()}
+
+
+def _run(bus, pub_topic, out_topic, out_type, messages, window, timeout):
+    from triton_client_amd.ros import compat
+
+    got = []
+    done = threading.Event()
+
+    def on_out(m):
+        got.append(time.perf_counter())
+        if len(got) >= len(messages):
+            done.set()
+    sub = compat.Subscriber(out_topic, out_type, on_out, bus=bus)
+    pub = compat.Publisher(pub_topic, type(messages[0]), bus=bus)
+    t0 = time.perf_counter()
+    for i, m in enumerate(messages):
+        while i - len(got) >= window:  # pace: never more than `window` messages in flight
+            time.sleep(0.0002)
+        pub.publish(m)
+    ok = done.wait(timeout)
+    t1 = time.perf_counter()
+    sub.unregister()
+    return len(got), (t1 - t0), ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--camera", type=int, default=512, help="CompressedImage messages (0: skip)")
+    ap.add_argument("--lidar", type=int, default=512, help="PointCloud2 messages (0: skip)")
+    ap.add_argument("--batch", type=int, default=32, help="micro-batch per engine call")
+    ap.add_argument("--workers", type=int, default=2, help="driver worker threads (host || device overlap)")
+    ap.add_argument("--hw", default="720,1280")
+    ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args()
+
+    import torch
+    from PIL import Image
+
+    from triton_client_amd.inference.engines import LocalDetector2D, LocalDetector3D
+    from triton_client_amd.inference.ros_inference import RosInference
+    from triton_client_amd.inference.ros_inference3d import RosInference3D
+    from triton_client_amd.ros import compat, msgs
+    from triton_client_amd.ros.bus import TopicBus
+    from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+
+    H, W = (int(v) for v in a.hw.split(","))
+    out = {"tool": "driver_bench", "batch": a.batch, "workers": a.workers,
+           "device": torch.cuda.get_device_name(0) if a.device == "cuda" else a.device}
+    bus = TopicBus()
+    window = 2 * a.batch * a.workers
+    if a.camera:
+        jpegs = []
+        for s in range(8):
+            buf = io.BytesIO()
+            Image.fromarray(camera_frame(H, W, s)).save(buf, format="JPEG", quality=90)
+            jpegs.append(buf.getvalue())
+        # header.seq strictly increasing over warm-up + run: the re-publisher drops a seq that is
+        # not newer than the last one it published
+        warm = 2 * a.batch
+        msgs_in = [msgs.CompressedImage(header=msgs.Header(seq=i + 1, frame_id="cam"), format="jpeg",
+                                        data=jpegs[i % 8]) for i in range(warm + a.camera)]
+        eng = LocalDetector2D(batch=a.batch, device=a.device, letterbox=True)
+        st = _Stages()
+        drv = RosInference(engine=eng, params={"sub_topic": "/cam", "pub_topic": "/cam_out"}, bus=bus,
+                           batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
+        drv.start_inference(spin=False)
+        _run(bus, "/cam", "/cam_out", msgs.Image, msgs_in[:warm], window, a.timeout)  # warm-up + graphs
+        st.sum.clear(), st.n.clear()
+        n, dt, ok = _run(bus, "/cam", "/cam_out", msgs.Image, msgs_in[warm:], window, a.timeout)
+        drv.stop()
+        out["camera"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
+                         "input": f"CompressedImage JPEG {W}x{H} q90", "output": "annotated Image + Detection2DArray",
+                         "stages": st.summary()}
+    if a.lidar:
+        spec = LidarSpec(sensor_height=3.23)
+        clouds = [compat.create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, s).tobytes(), np.float32).reshape(-1, 4))
+                  for s in range(8)]
+        warm = 2 * a.batch
+        msgs_in = []
+        for i in range(warm + a.lidar):
+            c = clouds[i % 8]
+            msgs_in.append(msgs.PointCloud2(header=msgs.Header(seq=i + 1, frame_id="os"), height=c.height,
+                                            width=c.width, fields=c.fields, is_bigendian=False,
+                                            point_step=c.point_step, row_step=c.row_step, data=c.data,
+                                            is_dense=True))
+        eng = LocalDetector3D(batch=a.batch, device=a.device)
+        st = _Stages()
+        drv = RosInference3D(engine=eng, params={"sub_topic": "/pc", "pub_topic": "/pc_out"}, bus=bus,
+                             batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
+        drv.start_inference(spin=False)
+        _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, msgs_in[:warm], window, a.timeout)
+        st.sum.clear(), st.n.clear()
+        n, dt, ok = _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, msgs_in[warm:], window, a.timeout)
+        drv.stop()
+        out["lidar"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
+                        "input": f"PointCloud2 {clouds[0].width} points x {clouds[0].point_step} B",
+                        "output": "jsk BoundingBoxArray (label 2, score > 0.5)", "stages": st.summary()}
+    bus.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,10 @@ _KERNEL_SIGS = {
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3p": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P],
+    # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, res, ldr, r_off, tile, stream
+    "tca_conv_hx3p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, I, P],
+    # src, B, H, W, dst, dst_dtype, dst_layout, sc0, sc1, sc2, b0, b1, b2, stream
+    "tca_planar_affine": [P, I, I, I, P, I, I, F, F, F, F, F, F, P],
     "tca_conv_nhwc_x3p_occ": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P],
     "tca_zero_i32": [P, I, P],
     "tca_anchor_decode_filter": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, F, F, F, F, F, F, F, P, P, P, P, P, I, P],

@@ -18,6 +18,32 @@ def yolo_spec(model_name: str, classes: int):
     return variant, classes, 640, os.path.join(DATA, "coco.names")
 
 
+def camera_spec(model_name: str, classes: int):
+    """Local camera engine for a served 2D model name (the reference's ``-m``):
+    (family, YOLOv5 variant, nc, model input (H, W), names file).  The names follow
+    the reference's model repository: YOLOv5* / weed_detector / *CROP
+    (``examples/YOLOv5/config.pbtxt``), YOLOv4 (``examples/YOLOv4/config.pbtxt``),
+    ``test_model`` = RetinaNet (``examples/RetinaNet_detectron/config.pbtxt``,
+    input [3, 640, 480]), *retina* / *fcos* / *detectron* (Detectron2, the 1333x800
+    class).  An unknown name raises instead of running another network."""
+    n = model_name.lower()
+    coco = os.path.join(DATA, "coco.names")
+    if "yolov4" in n:
+        return "yolov4", "n", classes, (512, 512), coco
+    if n.startswith("yolov5") or "weed_detector" == n or "crop" in n or n.startswith("yolo"):
+        variant, nc, img, names = yolo_spec(model_name, classes)
+        return "yolov5", variant, nc, (img, img), names
+    if n == "test_model":
+        return "retinanet", "n", classes, (640, 480), coco
+    if "fcos" in n or "retina" in n or "detectron" in n:
+        fam = "fcos" if "fcos" in n else "retinanet"
+        if "weed" in n:  # main.py:75 -m fcos_weed_detector: weeds, maize
+            return fam, "n", 2, (800, 1344), os.path.join(DATA, "crop.names")
+        return fam, "n", classes, (800, 1344), coco
+    raise ValueError(f"-m {model_name!r}: no local camera engine for this model name (YOLOv5*, weed_detector, "
+                     "YOLOv4, test_model, *retina*, *fcos*); use --engine remote to serve it elsewhere")
+
+
 def engine_2d(flags, params, letterbox=None, conf_thres=None):
     """→ (engine, channel, client)."""
     lb = flags.letterbox if letterbox is None else letterbox
@@ -26,9 +52,12 @@ def engine_2d(flags, params, letterbox=None, conf_thres=None):
         from ..inference import LocalDetector2D
         from ..clients.postprocess.base_postprocess import Postprocess
 
-        variant, nc, img, names = yolo_spec(flags.model_name, flags.classes)
+        family, variant, nc, img, names = camera_spec(flags.model_name, flags.classes)
+        if family == "yolov4" and conf_thres is None and flags.conf_thres == 0.3:
+            conf = 0.4  # tools/utils.py:166-233 post-processing (conf 0.4, NMS 0.6)
         eng = LocalDetector2D(variant, nc, img, batch=max(1, flags.frames_per_step), letterbox=lb, conf_thres=conf,
-                              device=flags.device, weights=flags.weights,
+                              iou_thres=0.6 if family == "yolov4" else 0.45, device=flags.device,
+                              weights=flags.weights, family=family,
                               names=Postprocess.load_class_names(names) if os.path.exists(names) else None)
         return eng, None, None
     from ..inference import RemoteDetector2D

@@ -74,39 +74,108 @@ class Detector3D(ABC):
         """PointCloud2 messages → per-cloud {pred_boxes, pred_scores, pred_labels}."""
 
 
+def pack_task_segments(res, k: int, max_out: int):
+    """CenterPointResult (NMS segments [B * T, mo, 9] internal box order, counts [B * T])
+    -> the first ``k`` frames as fixed-size device rows: box [k, max_out, 9] in det3d
+    order, score [k, max_out], label [k, max_out] int64, count [k] int32.  Segment t of
+    frame b lands at rows sum(count[b, :t]) ..; rows past max_out are dropped.  Pure
+    device ops (an exclusive prefix sum and one scatter): no host sync, graph-safe."""
+    from ..ops.centerpoint import DET3D_ORDER
+
+    T, nms = res.ntask, res.nms
+    mo, D = nms.box.shape[1], nms.box.shape[2]
+    dev = nms.box.device
+    seg_box = nms.box[:k * T].view(k, T, mo, D)[..., list(DET3D_ORDER)].float().reshape(k, T * mo, D)
+    seg_sc = nms.score[:k * T].reshape(k, T * mo).float()
+    seg_lb = nms.cls[:k * T].reshape(k, T * mo).long()
+    c = nms.count[:k * T].view(k, T).long().clamp(max=mo)
+    ar = torch.arange(mo, device=dev)
+    dest = (torch.cumsum(c, 1) - c)[..., None] + ar  # [k, T, mo]
+    dest = torch.where((ar < c[..., None]) & (dest < max_out), dest, max_out).reshape(k, T * mo)  # max_out: trash row
+    box = torch.zeros((k, max_out + 1, D), dtype=torch.float32, device=dev)
+    score = torch.zeros((k, max_out + 1), dtype=torch.float32, device=dev)
+    lab = torch.zeros((k, max_out + 1), dtype=torch.int64, device=dev)
+    box.scatter_(1, dest[..., None].expand(-1, -1, D), seg_box)
+    score.scatter_(1, dest, seg_sc)
+    lab.scatter_(1, dest, seg_lb)
+    return box[:, :max_out], score[:, :max_out], lab[:, :max_out], c.sum(1).clamp(max=max_out).to(torch.int32)
+
+
 # =============================================================================== local
+CAMERA_FAMILIES = ("yolov5", "yolov4", "retinanet", "fcos")
+
+
 class LocalDetector2D(Detector2D):
-    """YOLOv5 on this GPU through :class:`~triton_client_amd.pipelines.CameraPipeline`."""
+    """A camera detector on this GPU, one captured graph per source geometry:
 
-    def __init__(self, variant: str = "n", nc: int = 80, img: int = 640, batch: int = 1, letterbox: bool = True,
+    * ``family="yolov5"`` — :class:`~triton_client_amd.pipelines.CameraPipeline`
+      (the reference's ``Yolov5client`` models: YOLOv5nCOCO, YOLOv5nCROP / weed_detector);
+    * ``"yolov4"`` — :class:`~triton_client_amd.pipelines.yolov4.Yolov4Pipeline`
+      (``examples/YOLOv4/config.pbtxt``: 512 x 512, decode + per-class NMS);
+    * ``"retinanet"`` / ``"fcos"`` — :class:`~triton_client_amd.pipelines.detectron.DetectronPipeline`
+      (the reference's ``FCOS_client`` models, ``test_model`` =
+      ``examples/RetinaNet_detectron/config.pbtxt``), fp32 like the served libtorch model.
+
+    ``img`` is the model input (int: square); ``variant`` applies to YOLOv5 only."""
+
+    def __init__(self, variant: str = "n", nc: int = 80, img=640, batch: int = 1, letterbox: bool = True,
                  conf_thres: float = 0.3, iou_thres: float = 0.45, max_det: int = 300, device="auto",
-                 graph: bool = True, weights: Optional[str] = None, calibrate_target: Optional[float] = 100.0,
-                 seed: int = 0, names: Optional[Sequence[str]] = None, precision: str = "fp32"):
-        from ..models.yolov5 import build_yolov5
-
+                 graph: bool = True, weights: Optional[str] = None, calibrate_target: Optional[float] = "auto",
+                 seed: int = 0, names: Optional[Sequence[str]] = None, precision: str = "fp32",
+                 family: str = "yolov5"):
+        if family not in CAMERA_FAMILIES:
+            raise ValueError(f"family {family!r}: one of {CAMERA_FAMILIES}")
+        self.family = family
         self.device = _device(device)
+        if family != "yolov5" and self.device.type != "cuda":
+            raise ValueError(f"the local {family} engine runs on the GPU (device {self.device}); "
+                             "on a GPU-less host serve the model and use --engine remote")
         self.precision = precision
         self.B, self.img = batch, (img, img) if isinstance(img, int) else tuple(img)
         self.mode = "letterbox" if letterbox else "stretch"
         self.conf_thres, self.iou_thres, self.max_det = conf_thres, iou_thres, max_det
         self.graph = graph and self.device.type == "cuda"
-        self.model = build_yolov5(variant, nc, self.img, seed)
+        if family == "yolov5":
+            from ..models.yolov5 import build_yolov5
+            self.model = build_yolov5(variant, nc, self.img, seed)
+        elif family == "yolov4":
+            from ..models.yolov4 import build_yolov4
+            self.model = build_yolov4(nc, self.img, seed)
+        else:
+            from ..config.detectron import DetectronConfig
+            from ..models.detectron import build_detectron
+            self.det_cfg = DetectronConfig(arch=family, input_hw=self.img, num_classes=nc)
+            self.model = build_detectron(self.det_cfg, seed)
+            self.max_det = min(max_det, self.det_cfg.max_detections)
         if weights:
             self.model.load_state_dict(load_state_dict(weights))
             calibrate_target = None
+        if calibrate_target == "auto":
+            calibrate_target = 300.0 if family in ("retinanet", "fcos") else 100.0
         self.calibrate_target = calibrate_target
         self.names = list(names) if names is not None else [str(i) for i in range(nc)]
         self._pipes: Dict[Tuple[int, int], tuple] = {}
         self._lock = threading.Lock()
 
+    def _new_pipeline(self, hw: Tuple[int, int]):
+        kw = dict(batch=self.B, src_hw=hw, mode=self.mode, device=self.device, precision=self.precision)
+        if self.family == "yolov5":
+            from ..pipelines import CameraPipeline
+            return CameraPipeline(self.model, img_hw=self.img, conf_thres=self.conf_thres, iou_thres=self.iou_thres,
+                                  max_det=self.max_det, **kw)
+        if self.family == "yolov4":
+            from ..pipelines.yolov4 import Yolov4Pipeline
+            return Yolov4Pipeline(self.model, img=self.img[0], nc=self.model.cfg.nc, conf_thres=self.conf_thres,
+                                  nms_thres=self.iou_thres, **kw)
+        from ..pipelines.detectron import DetectronPipeline
+        return DetectronPipeline(self.model, **kw)
+
     def _pipe(self, hw: Tuple[int, int], sample: np.ndarray):
         if hw in self._pipes:
             return self._pipes[hw]
-        from ..pipelines import CameraPipeline, GraphRunner
+        from ..pipelines import GraphRunner
 
-        p = CameraPipeline(self.model, batch=self.B, src_hw=hw, img_hw=self.img, mode=self.mode,
-                           conf_thres=self.conf_thres, iou_thres=self.iou_thres, max_det=self.max_det,
-                           device=self.device, precision=self.precision)
+        p = self._new_pipeline(hw)
         if self.calibrate_target is not None:  # random-init weights: set the head prior once
             p.frames.copy_(torch.from_numpy(np.array(sample, np.uint8)).to(p.frames.device).expand_as(p.frames))
             p.calibrate_detection_density(self.calibrate_target)
@@ -368,13 +437,14 @@ class LocalDetector3D(Detector3D):
         [n, maxb] uint8 PointCloud2 payloads and ``npts`` [n] already in this
         GPU's memory; → ``(box [n, M, D], score [n, M], label [n, M] int64,
         count [n] int32)`` on the device, boxes in the sensor frame (z offset
-        removed).  PointPillars / SECOND-IoU (NmsResult pipelines)."""
+        removed).  PointPillars / SECOND-IoU return their NmsResult rows; CenterPoint's
+        per-(frame, task) NMS segments (6 tasks x <= 83, ``nms_post_max``) are packed on
+        the device into each frame's first ``count`` rows, in task order, with the 9-d
+        det3d box order (the layout of ``CenterPointResult.per_image``)."""
         from ..ops.lidar import PointLayout
 
         if self.device.type != "cuda" or not data.is_cuda:
             raise ValueError("detect_device needs a GPU engine and GPU payloads")
-        if self.family == "centerpoint":
-            raise NotImplementedError("centerpoint results are per-task segments: use detect()")
         by = {f.name: f for f in fields}
         names = ("x", "y", "z", "intensity")
         layout = PointLayout(int(point_step), tuple(by[k].offset for k in names), tuple(by[k].datatype for k in names))
@@ -397,6 +467,12 @@ class LocalDetector3D(Detector3D):
                 slots[:k, :maxb].copy_(data[s:s + k])
                 p.frame_n[:k].copy_(npts[s:s + k].to(torch.int32))
                 res = run()
+                if self.family == "centerpoint":
+                    b, sc, lb, c = pack_task_segments(res, k, max_out)
+                    box[s:s + k] = b
+                    box[s:s + k, :, 2] -= self.z_offset
+                    score[s:s + k], lab[s:s + k], cnt[s:s + k] = sc, lb, c
+                    continue
                 m = min(max_out, res.box.shape[1])
                 b = res.box[:k, :m, :D].float()
                 box[s:s + k, :m] = b

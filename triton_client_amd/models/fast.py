@@ -165,6 +165,12 @@ class FastYOLOv5:
 
     def set_input(self, x: torch.Tensor) -> None:
         """x: [B, 3, H, W] normalised image -> the plan's input buffer."""
+        if (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and self.x.t.is_contiguous()
+                and self.x.t.shape[-1] in (8, 16)):
+            from ..ops.image import planar_affine
+
+            planar_affine(x, self.x.t)  # one kernel: layout change + channel pad (+ S2D)
+            return
         if self.s2d:
             from ..ops.image import space_to_depth2
 

@@ -19,6 +19,7 @@ on the GPU-less host).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -98,6 +99,25 @@ PRECISIONS = ("fp32", "bf16")
 # split-product tiles with pair-storage instantiations (conv_mfma.hip launch_glds_x3p: global_load_lds
 # kernels 20-42, buffer-descriptor DMA kernels 68-79)
 PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 90, 91, 92, 93, 94, 95, 96, 97, 102)
+
+
+# conv_hx3.hip (3x3 stride-1 pair convs with register-streamed fragment-order weights): on
+# by default for every eligible layer; TCA_HX3=0 falls back to the conv_mfma.hip tiles.
+# Tiles 110 (auto) and 111-114 select it explicitly.
+HX3 = os.environ.get("TCA_HX3", "0") != "0"
+HX3_TILES = (110, 111, 112, 113, 114)
+
+
+def frag_weights(W: torch.Tensor) -> torch.Tensor:
+    """[N, Kp] fp32 GEMM weights (N % 16 == 0, Kp % 32 == 0) -> the split weights in MFMA
+    fragment order, [Kp/32][N/16][hi, lo][64 lanes][8] bf16: lane = fq * 16 + fr holds
+    output channel 16 g + fr, K indices 32 ks + 8 fq .. + 8 (the B operand of
+    mfma_f32_16x16x32_bf16), so one fragment load is one contiguous 1 KiB."""
+    N, Kp = W.shape
+    assert N % 16 == 0 and Kp % 32 == 0, (N, Kp)
+    hi, lo = split_bf16(W)
+    t = torch.stack([hi, lo], 0).reshape(2, N // 16, 16, Kp // 32, 4, 8)  # h, g, fr, ks, fq, e
+    return t.permute(3, 1, 0, 4, 2, 5).contiguous()  # ks, g, h, fq, fr, e
 
 
 def act_dtype(precision: str) -> torch.dtype:
@@ -186,6 +206,8 @@ class FusedConv:
         else:
             self.w_gemm = W.to(self.device, torch.bfloat16).contiguous()
         self.b_gemm = self.bias.to(self.device).contiguous()
+        # fragment-order weights of the hx3 kernel (built here, never inside a graph capture)
+        self._w_frag = frag_weights(W).to(self.device) if self.hx3_ok() and self.device.type == "cuda" else None
         # fp32 copies for the CPU path
         self.w_f32, self.b_f32 = w, b
 
@@ -217,6 +239,13 @@ class FusedConv:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
+            if (out.pair and x.occ is None and self.hx3_ok() and
+                    (tile in HX3_TILES or (tile == 0 and HX3))):
+                _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                             _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
+                             _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp,
+                             tile - 110 if tile in HX3_TILES else 0, _native.stream_ptr(stream))
+                return out
             args = (_native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off, _native.ptr(self.w_gemm),
                     _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p, self.Kp, _native.ptr(out.t), gh,
                     gw, out.t.shape[-1], out.off, act, *rp, self.shuffle, tile if tile in PAIR_TILES else 0,
@@ -233,6 +262,16 @@ class FusedConv:
                      self.Kp, _native.ptr(out.t), gh, gw, out.t.shape[-1], out.off, act, *rp, self.shuffle, tile,
                      _native.stream_ptr(stream))
         return out
+
+    def hx3_ok(self) -> bool:
+        """conv_hx3.hip takes this conv: fp32, 3x3 stride 1 pad 1, Cin % 32, N % 64."""
+        return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s == 1 and self.p == 1
+                and self.cin_p % 32 == 0 and self.K == self.Kp and self.N % 64 == 0)
+
+    def hx3_weights(self) -> torch.Tensor:
+        if self._w_frag is None:
+            self._w_frag = frag_weights(self.w_f32_gemm).to(self.device)
+        return self._w_frag
 
     def pair_ok(self) -> bool:
         """The pair-storage kernels take this conv (Cin % 32, K == Kp)."""

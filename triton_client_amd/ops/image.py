@@ -145,6 +145,36 @@ def _preprocess_cpu_native(rt, frames, dst_hw, layout, swap_rb, pad_value, quant
     return t, xf
 
 
+def planar_affine(x: torch.Tensor, out: torch.Tensor, scale=(1.0, 1.0, 1.0), bias=(0.0, 0.0, 0.0),
+                  stream=None) -> torch.Tensor:
+    """A model-sized fp32 NCHW request tensor ``x`` [B, 3, H, W] (the served contracts'
+    input) -> ``out``: NHWC [B, H, W, 8] (3 channels + zero pad) or space-to-depth
+    [B, H/2, W/2, 16], fp32 or bf16, with ``x * scale[c] + bias[c]`` — one kernel
+    (image.hip tca_planar_affine), capturable, instead of a normalise + permute +
+    pad chain of PyTorch element-wise ops."""
+    B, C, H, W = x.shape
+    assert C == 3 and x.dtype == torch.float32 and x.is_contiguous(), (x.shape, x.dtype)
+    if tuple(out.shape) == (B, H, W, 8):
+        layout = 1
+    elif tuple(out.shape) == (B, H // 2, W // 2, 16):
+        layout = 2
+    else:
+        raise ValueError(f"planar_affine: output {tuple(out.shape)} is neither NHWC x 8 nor S2D x 16 of {tuple(x.shape)}")
+    if not x.is_cuda:
+        y = x * torch.tensor(scale).view(1, 3, 1, 1) + torch.tensor(bias).view(1, 3, 1, 1)
+        y = y.permute(0, 2, 3, 1)
+        if layout == 2:
+            y = space_to_depth2(y)
+        else:
+            y = torch.cat([y, torch.zeros(B, H, W, 5)], -1)
+        out.copy_(y.to(out.dtype))
+        return out
+    assert out.is_contiguous() and out.dtype in (torch.float32, torch.bfloat16)
+    _native.call("tca_planar_affine", _native.ptr(x), B, H, W, _native.ptr(out), 0 if out.dtype == torch.float32 else 2,
+                 layout, *[float(v) for v in scale], *[float(v) for v in bias], _native.stream_ptr(stream))
+    return out
+
+
 def space_to_depth2(x: torch.Tensor) -> torch.Tensor:
     """[B, H, W, 3] -> [B, H/2, W/2, 16]: channel (dy*2 + dx)*3 + c = x[2Y+dy, 2X+dx, c];
     channels 12..15 are zero.  A k=6, s=2, p=2 conv over x equals a 3x3, s=1,

@@ -27,7 +27,7 @@ from ..ops.image import frame_xform, preprocess
 class DetectronPipeline:
     def __init__(self, model: Optional[DetectronDetector] = None, batch: int = 16,
                  src_hw: Tuple[int, int] = (720, 1280), cfg: Optional[DetectronConfig] = None, device="cuda",
-                 seed: int = 0, mode: str = "letterbox", precision: str = "bf16"):
+                 seed: int = 0, mode: str = "letterbox", precision: str = "fp32"):
         """precision "fp32": the reference's serving precision (libtorch fp32,
         examples/RetinaNet_detectron/config.pbtxt) — fp32 activations and
         split-product convs; "bf16" the faster secondary mode."""

@@ -200,7 +200,7 @@ class FastBEVPlan:
     """BaseBEVBackbone + merged anchor head on the fused convs, keeping the
     512-channel concat (SECONDHead pools its RoI grids from it)."""
 
-    def __init__(self, shim, batch: int, device, bev_hw, precision: str = "bf16"):
+    def __init__(self, shim, batch: int, device, bev_hw, precision: str = "fp32"):
         from ..models.fast import FastBEV
         # fp32: plain fp32 activations (the sparse BEV map is fp32 rows; SECONDHead pools the concat)
         self.plan = FastBEV(shim, batch, device, fused_neck=False, bev_hw=bev_hw, precision=precision, pair=False)

@@ -4,15 +4,17 @@
   ``examples/YOLOv5/config.pbtxt``) and ``YOLOv5nCOCO`` (640, 80 classes,
   ``.vscode/launch.json:12``): input ``images`` FP32 NCHW [3,H,W] (reshape
   [1,3,H,W]), output ``output`` FP32 [1, N, 5+nc] decoded rows — what the
-  reference's ONNX export returns.  On MI355X: bf16 channels_last network +
-  the HIP decode kernel writing the decoded tensor.
+  reference's ONNX export returns.  On MI355X: fp32 (split-product MFMA) captured
+  batch plans + the HIP decode kernel writing the decoded tensor.
 * :class:`SecondIoUModel` — ``second_iou`` (sparse 3D conv backbone + RoI IoU head).
+* :class:`DetectronModel` — ``test_model`` (RetinaNet, ``examples/RetinaNet_detectron/config.pbtxt``)
+  and the FCOS / RetinaNet Detectron2 names, fp32 like the reference's libtorch model.
 * :class:`PointPillarsModel` — ``pointpillar_kitti``
   (``examples/pointpillar_kitti/config.pbtxt``): inputs ``voxels`` [-1,P,4],
   ``voxel_coords`` INT32 [-1,4] (b,z,y,x), ``voxel_num_points`` INT32 [-1];
   outputs ``pred_boxes`` [-1,7], ``pred_scores`` [-1], ``pred_labels`` INT64
   [-1] (1-based).  On MI355X: MFMA PillarVFE+scatter from the received
-  voxels, bf16 backbone, anchor decode + rotated NMS kernels.  The voxel
+  voxels, fp32 pair-storage backbone, anchor decode + rotated NMS kernels.  The voxel
   geometry is published in ``ModelConfig.parameters`` so clients voxelise
   with the model's own parameters (fixes SURVEY Appendix A9).
 
@@ -606,24 +608,83 @@ class CenterPointModel(ServedModel):
         return out
 
 
+class _DetectronPlan:
+    """A captured batch-B RetinaNet / FCOS pass from the served input tensor: request
+    images (straight from a pinned shm region, else one host copy into pinned staging)
+    -> DMA -> one kernel for (x - mean) / std + NCHW -> NHWC x 8 (image.hip
+    tca_planar_affine) -> fused-MFMA ResNet-50-FPN + head -> decode / top-k / NMS
+    -> one D2H per output into pinned staging."""
+
+    def __init__(self, pipe, B: int, device):
+        from ..models.fast import FastDetectron
+        from ..ops.detectron import DetectronPostprocess
+        from ..ops.image import planar_affine
+        from ..pipelines.graph import GraphRunner
+
+        H, W = pipe.cfg.input_hw
+        self.B, self.H, self.W = B, H, W
+        self.fast = FastDetectron(pipe.model, B, device, precision=pipe.precision)
+        post = DetectronPostprocess(pipe.cfg, B, device)
+        self.x_dev = torch.zeros((B, 3, H, W), dtype=torch.float32, device=device)
+        self.pin_in = torch.empty((B, 3, H, W), dtype=torch.float32).pin_memory()
+        sc, bi = pipe.scaling
+        x_nhwc = self.fast.x.t
+
+        def step():
+            planar_affine(self.x_dev, x_nhwc, sc, bi)
+            return post(self.fast.forward())
+        self.runner = GraphRunner(step)
+        self.runner.capture()  # under the repository's exclusive GPU phase
+        r = self.runner.out
+        self.outs = (r.count, r.box, r.score, r.cls)
+        self.pin_out = [torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in self.outs]
+
+    def run(self, images: Sequence[np.ndarray]) -> List[Dict[str, np.ndarray]]:
+        n, H, W = len(images), self.H, self.W
+        srcs = [None] * n
+
+        def stage(i):
+            a = images[i].reshape(3, H, W)
+            srcs[i] = _direct(a, np.float32)
+            if srcs[i] is None:
+                np.copyto(self.pin_in[i].numpy(), a, casting="same_kind")
+                srcs[i] = self.pin_in[i]
+        _stage_parallel(stage, n)
+        for i in range(n):  # slots >= n: stale, outputs unused
+            self.x_dev[i].copy_(srcs[i], non_blocking=True)
+        self.runner()
+        for p, t in zip(self.pin_out, self.outs):
+            p[:n].copy_(t[:n], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        cnt, box, score, cls = self.pin_out
+        dims = np.array([[H, W]], np.int64)
+        return [{"bboxex__0": box[i, :k].numpy(), "classes__1": cls[i, :k].numpy().astype(np.int64),
+                 "scores__2": score[i, :k].numpy(), "dims__3": dims} for i, k in enumerate(cnt[:n].tolist())]
+
+
 class DetectronModel(ServedModel):
     """Detectron2 RetinaNet / FCOS with the reference's served contract
     (``examples/RetinaNet_detectron/config.pbtxt``): input ``input__00`` FP32 NCHW
     [3, 640, 480] RGB 0..255 (the model normalises), outputs ``bboxex__0`` FP32
     [-1, 4] (xyxy, input pixels), ``classes__1`` INT64 [-1], ``scores__2`` FP32
-    [-1], ``dims__3`` INT64 [1, 2] (input H, W).  GPU: ResNet-50-FPN + head on
-    the fused MFMA convs, decode / per-level top-k / merge / NMS kernels."""
+    [-1], ``dims__3`` INT64 [1, 2] (input H, W).  GPU: fp32 like the reference's
+    libtorch model (``config.pbtxt:7,16`` TYPE_FP32; split-product MFMA convs, fp32
+    activations, GroupNorm and decode), as captured batch plans (1 / 4) with the
+    normalisation folded into the input-layout kernel; ``precision="bf16"`` is the
+    faster secondary mode."""
 
     platform = "pytorch_libtorch"
 
     def __init__(self, name: str = "test_model", arch: str = "retinanet", hw=(640, 480), nc: int = 80,
-                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 300.0):
+                 device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 300.0,
+                 precision: str = "fp32", batch: int = 4):
         from ..config.detectron import DetectronConfig
 
         super().__init__(name)
         self.cfg = DetectronConfig(arch=arch, input_hw=tuple(hw), num_classes=nc)
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
+        self.precision, self.batch = precision, batch
 
     def inputs(self):
         H, W = self.cfg.input_hw
@@ -650,11 +711,15 @@ class DetectronModel(ServedModel):
             from ..utils.synthetic import camera_frame
 
             H, W = self.cfg.input_hw
-            self.pipe = DetectronPipeline(model, batch=1, src_hw=(H, W), device=self.device, mode="stretch")
+            self.pipe = DetectronPipeline(model, batch=1, src_hw=(H, W), device=self.device, mode="stretch",
+                                          precision=self.precision)
             if not self.weights:
                 self.pipe.frames[0].copy_(torch.from_numpy(camera_frame(H, W, self.seed)))
                 self.pipe.calibrate_detection_density(self.calibrate_target)
             self.model = self.pipe.model
+            sizes = sorted({b for b in (1, 4) if b <= max(1, self.batch)} | {max(1, self.batch)})
+            self.plans = {b: _DetectronPlan(self.pipe, b, self.device) for b in sizes}
+            self.dynamic_batch = max(sizes)
         else:
             self.model = fuse_model(model.eval())
         self.ready = True
@@ -662,25 +727,22 @@ class DetectronModel(ServedModel):
     @torch.no_grad()
     def execute(self, inputs, requested):
         H, W = self.cfg.input_hw
-        x = np.require(inputs["input__00"], np.float32, ["C", "W"]).reshape(1, 3, H, W)
         if self.device.type == "cuda":
-            p = self.pipe
-            f = p.fast or p.build_fast()
-            xt = torch.from_numpy(x).to(self.device, non_blocking=True)
-            mean = torch.tensor(self.cfg.pixel_mean, device=self.device).view(1, 3, 1, 1)
-            std = torch.tensor(self.cfg.pixel_std, device=self.device).view(1, 3, 1, 1)
-            f.x.t.zero_()
-            f.x.t[..., :3].copy_(((xt - mean) / std).permute(0, 2, 3, 1))
-            res = p.post(f.forward()).per_image()[0]
-        else:
-            from ..models.detectron import decode_reference
+            return self.plans[1].run([inputs["input__00"]])[0]
+        from ..models.detectron import decode_reference
 
-            bx, sc, cl = decode_reference(self.model(torch.from_numpy(x)), self.cfg)[0]
-            res = {"box": bx, "score": sc, "cls": cl}
-        return {"bboxex__0": np.asarray(res["box"], np.float32).reshape(-1, 4),
-                "classes__1": np.asarray(res["cls"]).astype(np.int64),
-                "scores__2": np.asarray(res["score"], np.float32),
+        x = np.require(inputs["input__00"], np.float32, ["C", "W"]).reshape(1, 3, H, W)
+        bx, sc, cl = decode_reference(self.model(torch.from_numpy(x)), self.cfg)[0]
+        return {"bboxex__0": np.asarray(bx, np.float32).reshape(-1, 4),
+                "classes__1": np.asarray(cl).astype(np.int64),
+                "scores__2": np.asarray(sc, np.float32),
                 "dims__3": np.array([[H, W]], np.int64)}
+
+    @torch.no_grad()
+    def execute_batch(self, batch, requested):
+        if self.device.type != "cuda":
+            return [self.execute(x, requested) for x in batch]
+        return _pick(self.plans, len(batch)).run([x["input__00"] for x in batch])
 
 
 class YoloV4Model(ServedModel):
