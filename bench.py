@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--lidar-model", choices=["pointpillars", "centerpoint", "second_iou"], default="pointpillars",
                     help="3D detector: PointPillars KITTI (headline), CenterPoint-PP nuScenes or SECOND-IoU KITTI "
                          "(sparse 3D conv backbone + RoI head)")
+    ap.add_argument("--sweeps", type=int, default=1,
+                    help="CenterPoint: LiDAR sweeps merged per frame (det3d nuScenes '10sweep': 10; device ring, "
+                         "time lag as the 5th point feature)")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32 (default): the reference's serving precision — fp32 activations, split-product "
                          "MFMA convs; bf16: bf16 activations (secondary, labelled)")
@@ -198,11 +201,14 @@ def main():
         def make_cam(b, m):
             return CameraPipeline(model=m, batch=b, src_hw=(H0, W0), device=dev, precision=args.precision)
     sec = args.lidar_model == "second_iou"
+    if args.sweeps > 1 and not (use_lid and cp):
+        raise SystemExit("--sweeps needs --lidar-model centerpoint")
     if use_lid and cp:
         from triton_client_amd.pipelines import CenterPointPipeline
 
         def make_lid(b, m):
-            return CenterPointPipeline(model=m, batch=b, max_points=max_points, device=dev, precision=args.precision)
+            return CenterPointPipeline(model=m, batch=b, max_points=max_points, device=dev, precision=args.precision,
+                                       nsweeps=args.sweeps)
     elif use_lid and sec:
         from triton_client_amd.pipelines import SecondPipeline
 
@@ -606,13 +612,14 @@ def main():
             "config": {
                 "model": ({"both": cam_name + " + ", "camera": cam_name, "lidar": ""}[args.only]
                           + ("" if args.only == "camera" else
-                             ("CenterPoint-PP (nuScenes, 10 cls)" if cp else
+                             (f"CenterPoint-PP (nuScenes, 10 cls, {args.sweeps} sweep{'s' if args.sweeps > 1 else ''}/frame)" if cp else
                               ("SECOND-IoU (KITTI, 3 cls)" if sec else "PointPillars (KITTI, 3 cls)")))),
                 "global_batch": info.world * B,
                 "seq_len": None,
                 "parallelism": f"dp{info.world}",
                 "frames_per_gpu_per_step": B,
                 "precision": args.precision,
+                "lidar_sweeps_per_frame": args.sweeps if (use_lid and cp) else None,
                 "distinct_frames_per_rank": nd,
                 "rccl_ranks": rccl_ranks,
                 "vs_reference_equivalent_emulation": round(fps / REFERENCE_EQUIVALENT_FPS, 2),

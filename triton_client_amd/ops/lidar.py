@@ -216,6 +216,69 @@ class Voxelizer:
         return torch.from_numpy(vox), torch.from_numpy(co), torch.from_numpy(nump), torch.from_numpy(vc)
 
 
+# ----------------------------------------------------------------------------- K7s
+IDENTITY_POSE = (1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+
+
+def merge_sweeps_np(cur: np.ndarray, history: Sequence[Tuple[np.ndarray, float, np.ndarray]], t_cur: float,
+                    pose_cur: np.ndarray) -> np.ndarray:
+    """Reference of the multi-sweep merge for one frame: ``cur`` [n, >=4] points of the
+    current sweep; ``history`` newest first, (points [m, 4], timestamp, 3x4 pose) of
+    earlier sweeps.  Returns [N, 5]: current sweep (lag 0), then each earlier sweep in
+    the current sensor frame, inv(T_cur) * T_k, with lag t_cur - t_k (det3d order)."""
+    Tc = np.asarray(pose_cur, np.float64).reshape(3, 4)
+    out = [np.concatenate([cur[:, :4], np.zeros((len(cur), 1))], 1)]
+    for pts, t, pose in history:
+        Tk = np.asarray(pose, np.float64).reshape(3, 4)
+        q = pts[:, :3].astype(np.float64) @ Tk[:, :3].T + Tk[:, 3] - Tc[:, 3]
+        p = q @ Tc[:, :3]
+        out.append(np.concatenate([p, pts[:, 3:4], np.full((len(pts), 1), t_cur - t)], 1))
+    return np.concatenate(out).astype(np.float32)
+
+
+class SweepAccumulator:
+    """Device ring of the last ``nsweeps - 1`` sweeps per frame slot + the merge into
+    one (x, y, z, intensity, time lag) point list per frame (sweeps.hip
+    tca_sweep_step): det3d's multi-sweep input for CenterPoint
+    (``data/nusc_centerpoint_pp_02voxel_two_pfn_10sweep.py`` ``nsweeps``).  ``clock``
+    [B] (seconds) and ``pose`` [B, 12] (3x4 sensor-to-world) are the current sweep's,
+    set by the caller before a step or auto-advanced by ``dt`` per step; the whole
+    step is capture-safe (the ring position lives on the device)."""
+
+    def __init__(self, nsweeps: int, batch: int, max_points: int, device="cuda", dt: float = 0.05):
+        if not 2 <= nsweeps <= 32:
+            raise ValueError(f"nsweeps {nsweeps}: 2..32")
+        self.S, self.R, self.B, self.maxp, self.dt = nsweeps, nsweeps - 1, batch, max_points, float(dt)
+        dev = torch.device(device)
+        f = dict(dtype=torch.float32, device=dev)
+        self.ring = torch.zeros((self.R, batch, max_points, 4), **f)
+        self.ring_n = torch.zeros((self.R, batch), dtype=torch.int32, device=dev)
+        self.ring_t = torch.zeros((self.R, batch), **f)
+        self.ring_pose = torch.zeros((self.R, batch, 12), **f)
+        self.head = torch.zeros((1,), dtype=torch.int32, device=dev)
+        self.clock = torch.zeros((batch,), **f)
+        self.pose = torch.tensor(IDENTITY_POSE, **f).repeat(batch, 1).contiguous()
+        self.out = torch.zeros((batch, nsweeps * max_points, 5), **f)
+        self.out_n = torch.zeros((batch,), dtype=torch.int32, device=dev)
+
+    @property
+    def out_points(self) -> int:
+        return self.S * self.maxp
+
+    def reset(self) -> None:
+        self.ring_n.zero_()
+        self.head.zero_()
+
+    def __call__(self, points: torch.Tensor, npts: torch.Tensor, stream=None):
+        """points [B, maxp, >=4], npts [B] -> (merged [B, S * maxp, 5], count [B])."""
+        assert points.shape[:2] == (self.B, self.maxp) and points.is_contiguous(), points.shape
+        P = _native.ptr
+        _native.call("tca_sweep_step", P(points), points.shape[-1], P(npts), self.B, self.maxp, self.R, P(self.ring),
+                     P(self.ring_n), P(self.ring_t), P(self.ring_pose), P(self.head), P(self.clock), P(self.pose),
+                     self.dt, P(self.out), P(self.out_n), _native.stream_ptr(stream))
+        return self.out, self.out_n
+
+
 # ----------------------------------------------------------------------------- K8/K9
 class PillarEncoder:
     """Fused PillarVFE (BN folded) + scatter into an NHWC BEV canvas (bf16, or

@@ -26,14 +26,19 @@ from ..models.common import fuse_model, lsuv_rescale
 from ..ops._ws import Workspace
 from ..ops.centerpoint import CenterPointPostprocess, PFNEncoder
 from ..ops.conv import NHWC
-from ..ops.lidar import PointLayout, Voxelizer, pc2_unpack
+from ..ops.lidar import PointLayout, SweepAccumulator, Voxelizer, pc2_unpack
 
 
 class CenterPointPipeline:
     def __init__(self, model: Optional[CenterPoint] = None, batch: int = 16, max_points: int = 131072,
                  layout: Optional[PointLayout] = None, z_offset: float = 0.0, normalize_intensity: bool = True,
                  device="cuda", cfg: Optional[CenterPointConfig] = None, seed: int = 0, class_thresh=None,
-                 precision: str = "fp32"):
+                 precision: str = "fp32", nsweeps: int = 1, sweep_dt: float = 0.05):
+        """nsweeps > 1: det3d multi-sweep input (the config's "10sweep"): every frame slot
+        is one sensor stream whose last nsweeps - 1 sweeps ride in a device ring and are
+        merged, moved into the current sensor frame, with the time lag as the PFN's 5th
+        point feature (ops.lidar.SweepAccumulator; ``self.sweeps.clock`` / ``.pose`` hold
+        the current stamps and poses, auto-advanced by ``sweep_dt`` per step)."""
         self.device = torch.device(device)
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision {precision!r}")
@@ -55,7 +60,10 @@ class CenterPointPipeline:
         self.frame_n = torch.zeros(batch, dtype=torch.int32, device=self.device)
         self.ws = Workspace(self.device)
         v = self.cfg.voxel
-        self.vox = Voxelizer(v, batch, max_points, device=self.device, materialize=False)
+        self.nsweeps = max(1, int(nsweeps))
+        self.sweeps = (SweepAccumulator(self.nsweeps, batch, max_points, self.device, sweep_dt)
+                       if self.nsweeps > 1 else None)
+        self.vox = Voxelizer(v, batch, max_points * self.nsweeps, device=self.device, materialize=False)
         self.enc = PFNEncoder(v, self.model.pfn, batch, device=self.device, precision=precision)
         self.class_thresh = class_thresh
         self.fast = None
@@ -64,6 +72,8 @@ class CenterPointPipeline:
     def _encode(self):
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
+        if self.sweeps is not None:
+            pts, cnt = self.sweeps(pts, cnt)  # [B, nsweeps * max_points, 5] with the time lag
         self.enc.clear(self.vox)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
