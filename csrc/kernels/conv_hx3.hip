@@ -82,8 +82,8 @@ __device__ __forceinline__ void pair_join8(const float* p, float* v) {
 // its end.  Per wave 128 pixels x 32 channels: 16 ds_read_b128 per 48 MFMAs.
 // Same products and fp32 summation order per output as hx (chunk-major, tap
 // inner), so the results are bit-identical to hx.
-template <int TH, int BN, int WM, int WN, bool CM, int HB>
-__global__ void __launch_bounds__(WM * WN * 64, 2) conv_hx3_kernel(Hx3Args a) {
+template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
+__global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN, NT = NW * 64;
   constexpr int FM = TH / WM, FN = BN / WN / 16;
   static_assert(TH % WM == 0 && BN % (WN * 16) == 0 && FN >= 1, "tiles");
@@ -284,12 +284,12 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_hx3_kernel(Hx3Args a) {
   }
 }
 
-template <int TH, int BN, int WM, int WN, bool CM, int HB>
+template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
 int launch_hx3(const Hx3Args& a, hipStream_t stream) {
   if (a.N % BN) return (int)hipErrorInvalidValue;
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
-  conv_hx3_kernel<TH, BN, WM, WN, CM, HB><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -310,6 +310,10 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     case 2: return launch_hx3<8, 128, 1, 4, true, 2>(a, stream);
     case 3: return launch_hx3<8, 64, 2, 2, false, 2>(a, stream);
     case 4: return launch_hx3<8, 64, 2, 2, true, 2>(a, stream);
+    // one wave row, 16 channels per wave: no weight fragment loaded twice per workgroup,
+    // <= 168 VGPRs -> 3 workgroups (12 waves) per CU
+    case 5: return launch_hx3<8, 64, 1, 4, false, 2, 3>(a, stream);
+    case 6: return launch_hx3<8, 64, 1, 4, true, 2, 3>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

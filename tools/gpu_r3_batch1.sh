@@ -6,7 +6,7 @@ mkdir -p $R/gpurun_out
 cd $R
 timeout -k 10 240 python tools/hx3_debug.py > gpurun_out/hx3_debug.log 2>&1 || { echo PROBE_FAILED; tail -20 gpurun_out/hx3_debug.log; }
 tail -4 gpurun_out/hx3_debug.log
-timeout -k 10 500 python -u -m pytest tests/test_hx3_gpu.py tests/test_centerpoint.py tests/test_ops_gpu.py tests/test_detectron.py -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/r3b1_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_hx3_gpu.py tests/test_centerpoint.py tests/test_ops_gpu.py tests/test_detectron.py "tests/test_fp32_mode_gpu.py::test_pipeline_fp32_detection_parity_headline_shape" -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/r3b1_tests.log 2>&1
 echo "tests rc=$?"
 grep -E "passed|failed" gpurun_out/r3b1_tests.log | tail -3
 grep -E "^FAILED" gpurun_out/r3b1_tests.log | head -20

@@ -103,9 +103,9 @@ PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73
 
 # conv_hx3.hip (3x3 stride-1 pair convs with register-streamed fragment-order weights): on
 # by default for every eligible layer; TCA_HX3=0 falls back to the conv_mfma.hip tiles.
-# Tiles 110 (auto) and 111-114 select it explicitly.
-HX3 = os.environ.get("TCA_HX3", "0") != "0"
-HX3_TILES = (110, 111, 112, 113, 114)
+# Tiles 110 (auto) and 111-116 (conv_hx3.hip hx3_launch tiles 1-6) select it explicitly.
+HX3 = os.environ.get("TCA_HX3", "1") != "0"
+HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 
 
 def frag_weights(W: torch.Tensor) -> torch.Tensor:

@@ -172,7 +172,15 @@ def rotated_overlap(a, b) -> float:
 
 def rotated_iou_bev(a, bs) -> np.ndarray:
     out = np.zeros(len(bs), np.float64)
-    for k, b in enumerate(bs):
+    if len(bs) == 0:
+        return out
+    bs_ = np.asarray(bs, np.float64)
+    # exact prefilter: boxes whose bounding circles do not meet have no overlap (IoU 0)
+    ra = 0.5 * math.hypot(a[3], a[4])
+    rb = 0.5 * np.hypot(bs_[:, 3], bs_[:, 4])
+    near = np.hypot(bs_[:, 0] - a[0], bs_[:, 1] - a[1]) <= ra + rb
+    for k in np.nonzero(near)[0]:
+        b = bs_[k]
         ov = rotated_overlap(a, b)
         out[k] = ov / max(a[3] * a[4] + b[3] * b[4] - ov, 1e-8)
     return out
