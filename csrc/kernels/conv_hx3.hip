@@ -294,15 +294,17 @@ int launch_hx3(const Hx3Args& a, hipStream_t stream) {
 }
 
 // hx3 tiles.  0 = auto: N % 128 == 0 -> 8 x 16 tiles, 4 waves of 128 pixels x 32 channels
-// (row- or column-major by the smaller padding); N == 64 -> 8 x 16 tiles, 2 x 2 waves of
-// 64 pixels x 32 channels.  Every variant: 2 waves per SIMD (<= 256 VGPRs, no spill), two
+// (row- or column-major by the smaller padding); N == 64 -> 8 x 16 tiles, 4 waves of 128
+// pixels x 16 channels (3 workgroups per CU).  Every variant: 2 waves per SIMD (<= 256 VGPRs, no spill), two
 // workgroups per CU (<= 80 KiB LDS).
 int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
   if (tile == 0) {
     const long rm8 = (long)((a.Wo + 15) / 16 * 16) * ((a.Ho + 7) / 8 * 8);
     const long cm8 = (long)((a.Ho + 15) / 16 * 16) * ((a.Wo + 7) / 8 * 8);
+    // measured at batch 32 (profiles/r3/hx3_tiles2.jsonl): pp.b1.conv (N 64) 362 us on tile 6 vs 427 on
+    // tile 4 (2 x 2 waves load every weight fragment twice per workgroup); pp.b2 / b3 283 / 257 us on tile 1 / 2
     if (a.N % 128 == 0) tile = cm8 < rm8 ? 2 : 1;
-    else if (a.N % 64 == 0) tile = cm8 < rm8 ? 4 : 3;
+    else if (a.N % 64 == 0) tile = cm8 < rm8 ? 6 : 5;
     else return (int)hipErrorInvalidValue;
   }
   switch (tile) {

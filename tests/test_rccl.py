@@ -103,3 +103,40 @@ def test_native_p2p_plan_graph_capture():
         assert ok
     finally:
         comm.abort()  # never block on teardown of a communicator a graph has used
+
+
+@pytest.mark.gpu
+def test_native_gather_plan_in_step_graph():
+    """The bench's in-graph detection gather: a step producing the detection buffers
+    (mixed dtypes: boxes / scores fp32, classes / counts int32, as the 2D and 3D
+    results) followed by the grouped gather plan, captured as ONE graph with
+    GraphRunner and replayed.  At world 1 the peer is this rank itself: rank 0's
+    receives and a worker's sends of the same plan, in one RCCL group."""
+    from triton_client_amd.parallel.rccl import RECV, SEND, NativeComm
+    from triton_client_amd.pipelines.graph import GraphRunner
+
+    torch.cuda.set_device(0)
+    comm = NativeComm(0, 1)
+    try:
+        seed = torch.zeros(1, device="cuda")
+        src = [torch.zeros((32, 300, 4), device="cuda"), torch.zeros((32, 300), device="cuda"),
+               torch.zeros((32, 300), dtype=torch.int32, device="cuda"),
+               torch.zeros((32,), dtype=torch.int32, device="cuda"), torch.zeros((32, 500, 7), device="cuda")]
+        dst = [torch.empty_like(t) for t in src]
+
+        def step():
+            for k, t in enumerate(src):  # the "pipeline": every result buffer rewritten from the input
+                t.copy_((seed + k).expand_as(t).to(t.dtype) if t.dtype != torch.int32 else (seed + k).to(torch.int32).expand_as(t))
+            comm.group_p2p([(RECV, d, 0) for d in dst] + [(SEND, s, 0) for s in src])
+            return src
+        run = GraphRunner(step)
+        for v in (3.0, 7.0, 11.0):
+            seed.fill_(v)
+            run()
+            torch.cuda.synchronize()
+            for k, (d, s) in enumerate(zip(dst, src)):
+                assert torch.equal(d, s) and float(d.reshape(-1)[0]) == v + k
+        del run  # the graph holds RCCL work: release it before the communicator goes
+        torch.cuda.synchronize()
+    finally:
+        comm.abort()
