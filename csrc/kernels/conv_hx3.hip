@@ -5,6 +5,8 @@
 // split-product MFMA (bf16 x3, fp32 accumulation; see conv_mfma.hip "fp32 mode").
 #include "tca_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -82,7 +84,11 @@ __device__ __forceinline__ void pair_join8(const float* p, float* v) {
 // its end.  Per wave 128 pixels x 32 channels: 16 ds_read_b128 per 48 MFMAs.
 // Same products and fp32 summation order per output as hx (chunk-major, tap
 // inner), so the results are bit-identical to hx.
-template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
+template <int V> struct IC { static constexpr int value = V; };
+
+// PAIRS: two chunks per loop iteration (even chunk counts), the tap groups alternating
+// between two static weight register sets: no register copy between groups
+template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2, bool PAIRS = false>
 __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN, NT = NW * 64;
   constexpr int FM = TH / WM, FN = BN / WN / 16;
@@ -186,40 +192,31 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   asm volatile("" ::: "memory");
 
   const int fr = lane & 15, fq = lane >> 4;
-  for (int c = 0; c < nc; ++c) {
-    const unsigned char* hb = smem + (HB == 2 ? (c & 1) * HBYTES : 0);
+  // one tap group: prefetch the weights of group gs_next into wl, then 3 * FM * FN fragment
+  // pairs from the FM + 2 halo lines at shift kf with the weights in wu
+  auto group = [&](auto KF, const unsigned char* hb, bf16x8 (&wu)[3][FN][2], bf16x8 (&wl)[3][FN][2], int gs_next) {
+    constexpr int kf = decltype(KF)::value;
+    gload(gs_next < G ? gs_next : G - 1, wl);  // unconditional (clamped): no branch around the loads
+    // keep the prefetch at the top of the group: hipcc's scheduler otherwise sinks the
+    // loads to their first use and waits for them there
+    __builtin_amdgcn_sched_barrier(0);
+    const int sw = hswz(kf + fr);
+    const unsigned char* colp = hb + (wm * FM) * HWD * 128 + (kf + fr) * 128;
+    const int o_hi = ((2 * fq) ^ sw) << 4, o_lo = ((2 * fq + 1) ^ sw) << 4;
 #pragma unroll
-    for (int kf = 0; kf < 3; ++kf) {
-      {
-        const int gs = c * 3 + kf + 1;
-        gload(gs < G ? gs : G - 1, wx);  // unconditional (clamped): no branch around the loads
+    for (int L = 0; L < FM + 2; ++L) {
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
+#pragma unroll
+      for (int kl = 0; kl < 3; ++kl) {
+        const int i = L - kl;
+        if (i < 0 || i >= FM) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wu[kl][j][0], wu[kl][j][1], ah, al);
       }
-      // keep the prefetch at the top of the group: hipcc's scheduler otherwise sinks the
-      // loads next to the register copy at the group's end and waits for them there
-      __builtin_amdgcn_sched_barrier(0);
-      const int sw = hswz(kf + fr);
-      const unsigned char* colp = hb + (wm * FM) * HWD * 128 + (kf + fr) * 128;
-      const int o_hi = ((2 * fq) ^ sw) << 4, o_lo = ((2 * fq + 1) ^ sw) << 4;
-#pragma unroll
-      for (int L = 0; L < FM + 2; ++L) {
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
-#pragma unroll
-        for (int kl = 0; kl < 3; ++kl) {
-          const int i = L - kl;
-          if (i < 0 || i >= FM) continue;
-#pragma unroll
-          for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wc[kl][j][0], wc[kl][j][1], ah, al);
-        }
-      }
-#pragma unroll
-      for (int kl = 0; kl < 3; ++kl)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          wc[kl][j][0] = wx[kl][j][0];
-          wc[kl][j][1] = wx[kl][j][1];
-        }
     }
+  };
+  auto chunk_end = [&](int c) {
     if (c + 1 < nc) {
       if constexpr (HB == 1) {  // every wave done with this chunk's halo before it is overwritten
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -231,6 +228,39 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+    }
+  };
+  if constexpr (PAIRS) {
+    const unsigned char* hb1 = smem + (HB == 2 ? HBYTES : 0);
+    for (int c = 0; c < nc; c += 2) {
+      group(IC<0>{}, smem, wc, wx, 3 * c + 1);
+      group(IC<1>{}, smem, wx, wc, 3 * c + 2);
+      group(IC<2>{}, smem, wc, wx, 3 * c + 3);
+      chunk_end(c);
+      group(IC<0>{}, hb1, wx, wc, 3 * c + 4);
+      group(IC<1>{}, hb1, wc, wx, 3 * c + 5);
+      group(IC<2>{}, hb1, wx, wc, 3 * c + 6);
+      chunk_end(c + 1);
+    }
+  } else {
+    for (int c = 0; c < nc; ++c) {
+      const unsigned char* hb = smem + (HB == 2 ? (c & 1) * HBYTES : 0);
+      auto copyw = [&]() {  // the prefetched set becomes the current one
+#pragma unroll
+        for (int kl = 0; kl < 3; ++kl)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            wc[kl][j][0] = wx[kl][j][0];
+            wc[kl][j][1] = wx[kl][j][1];
+          }
+      };
+      group(IC<0>{}, hb, wc, wx, 3 * c + 1);
+      copyw();
+      group(IC<1>{}, hb, wc, wx, 3 * c + 2);
+      copyw();
+      group(IC<2>{}, hb, wc, wx, 3 * c + 3);
+      copyw();
+      chunk_end(c);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -284,12 +314,24 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   }
 }
 
+// TCA_HX3_PAIRS=0: the single-chunk loop with register copies (A/B measurement)
+bool hx3_no_pairs() {
+  static const bool off = [] {
+    const char* e = getenv("TCA_HX3_PAIRS");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
 int launch_hx3(const Hx3Args& a, hipStream_t stream) {
   if (a.N % BN) return (int)hipErrorInvalidValue;
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
-  conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  if ((a.Cin / 32) % 2 == 0 && !hx3_no_pairs())
+    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, true><<<nwg, WM * WN * 64, 0, stream>>>(a);
+  else
+    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, false><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 

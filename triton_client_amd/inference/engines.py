@@ -166,7 +166,7 @@ class LocalDetector2D(Detector2D):
         if self.family == "yolov4":
             from ..pipelines.yolov4 import Yolov4Pipeline
             return Yolov4Pipeline(self.model, img=self.img[0], nc=self.model.cfg.nc, conf_thres=self.conf_thres,
-                                  nms_thres=self.iou_thres, **kw)
+                                  nms_thres=self.iou_thres, max_out=self.max_det, **kw)
         from ..pipelines.detectron import DetectronPipeline
         return DetectronPipeline(self.model, **kw)
 

@@ -19,7 +19,8 @@ from ..ops.yolov4 import Yolov4Postprocess
 class Yolov4Pipeline:
     def __init__(self, model: Optional[YOLOv4] = None, batch: int = 16, src_hw: Tuple[int, int] = (720, 1280),
                  img: int = 512, nc: int = 80, mode: str = "stretch", conf_thres: float = 0.4,
-                 nms_thres: float = 0.6, device="cuda", seed: int = 0, precision: str = "fp32"):
+                 nms_thres: float = 0.6, device="cuda", seed: int = 0, precision: str = "fp32",
+                 max_out: int = 1000):
         self.device = torch.device(device)
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision {precision!r}")
@@ -36,7 +37,8 @@ class Yolov4Pipeline:
         self.img_hw = self.cfg.img
         self.frames = torch.zeros((batch, *self.src_hw, 3), dtype=torch.uint8, device=self.device)
         self.xform, _ = frame_xform(self.src_hw, self.img_hw, mode)
-        self.post = Yolov4Postprocess(self.cfg.nc, self.img_hw, conf_thres, nms_thres, device=self.device)
+        self.post = Yolov4Postprocess(self.cfg.nc, self.img_hw, conf_thres, nms_thres,
+                                      max_out=max_out, device=self.device)
         self.fast = None
 
     def build_fast(self):
