@@ -310,11 +310,11 @@ constexpr int X_ROWB = 128;                       // 32 fp32 channels / 4 x {hi 
 // <8, 3>: one 512-thread workgroup per CU; <4, 2>: two independent 256-thread
 // workgroups per CU (66.5 KiB each), whose barriers do not line up, so one
 // workgroup's MFMAs fill the other's barrier / LDS-latency bubbles.
-template <int NWV, int STAGES>
+template <int NWV, int STAGES, int FM_ = 2>
 struct NeckX3 {
   static constexpr int NWAVES = NWV, NTH = NWV * 64;
-  static constexpr int BM = 32 * NWV;                      // pixels per tile
-  static constexpr int FM = 2;                             // 16-pixel fragments per wave
+  static constexpr int FM = FM_;                           // 16-pixel fragments per wave
+  static constexpr int BM = 16 * FM * NWV;                 // pixels per tile
   static constexpr int A_BYTES = BM * X_ROWB;              // head steps: 2 x [80 rows][128 B]
   static constexpr int B_BYTES = CB * X_ROWB;              // 16 KiB
   static constexpr int STAGE = A_BYTES + B_BYTES + BIAS_BYTES;
@@ -385,9 +385,9 @@ struct NeckArgsX3 {
 
 // PAIR: branch inputs in pair storage ({hi 8 | lo 8} per 8 channels, see
 // conv_mfma.hip pair_split8): the A fragments are read as stored, no split.
-template <bool PAIR, int NWV, int STAGES>
+template <bool PAIR, int NWV, int STAGES, int FM_ = 2>
 __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a) {
-  using T = NeckX3<NWV, STAGES>;
+  using T = NeckX3<NWV, STAGES, FM_>;
   constexpr int Y_BM = T::BM, Y_FM = T::FM, Y_STAGES = STAGES, Y_STAGE = T::STAGE, Y_A_BYTES = T::A_BYTES;
   constexpr int Y_B_BYTES = T::B_BYTES, Y_BH_OFF = T::BH_OFF, Y_A_INS = T::A_INS, Y_B_INS = T::B_INS;
   constexpr int Y_DC_LOADS = T::DC_LOADS, Y_HEAD_PIECES = T::HEAD_PIECES, NW = NWV;
@@ -565,20 +565,21 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
           }
         }
         __builtin_amdgcn_s_setprio(1);
-        // two halves of 4 B fragments each: keeps the hoisted LDS reads (and so the VGPRs) to half the tile
+        // B fragments in groups of JB: keeps the hoisted LDS reads (and so the VGPRs) to part of the tile
+        constexpr int JB = Y_FM >= 4 ? 2 : 4;
 #pragma unroll
-        for (int jh = 0; jh < 2; ++jh) {
-          bf16x8 wh_[4], wl_[4];
+        for (int jh = 0; jh < 8 / JB; ++jh) {
+          bf16x8 wh_[JB], wl_[JB];
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int r = (jh * 4 + jj) * 16 + fr;
+          for (int jj = 0; jj < JB; ++jj) {
+            const int r = (jh * JB + jj) * 16 + fr;
             wh_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq) ^ swz3(r)) << 4));
             wl_[jj] = *reinterpret_cast<const bf16x8*>(sb + r * X_ROWB + (((2 * fq + 1) ^ swz3(r)) << 4));
           }
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
+          for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
-            for (int i = 0; i < Y_FM; ++i) mfma3(acc1[i][jh * 4 + jj], wh_[jj], wl_[jj], ah[i], al[i]);
+            for (int i = 0; i < Y_FM; ++i) mfma3(acc1[i][jh * JB + jj], wh_[jj], wl_[jj], ah[i], al[i]);
           __builtin_amdgcn_sched_barrier(0);
         }
         __builtin_amdgcn_s_setprio(0);
@@ -698,12 +699,12 @@ namespace {
 // profiles/r2/neck_variants.json)
 constexpr int kNeckX3Auto = 3;
 
-template <int NWV, int STAGES>
+template <int NWV, int STAGES, int FM = 2>
 void launch_neck_x3(NeckArgsX3& a, long np, int grid, bool pair, hipStream_t stream) {
-  using T = NeckX3<NWV, STAGES>;
+  using T = NeckX3<NWV, STAGES, FM>;
   a.ntiles = (int)((np + T::BM - 1) / T::BM) * a.S * a.S;
-  if (pair) bev_neck_head_x3_kernel<true, NWV, STAGES><<<grid, T::NTH, 0, stream>>>(a);
-  else bev_neck_head_x3_kernel<false, NWV, STAGES><<<grid, T::NTH, 0, stream>>>(a);
+  if (pair) bev_neck_head_x3_kernel<true, NWV, STAGES, FM><<<grid, T::NTH, 0, stream>>>(a);
+  else bev_neck_head_x3_kernel<false, NWV, STAGES, FM><<<grid, T::NTH, 0, stream>>>(a);
 }
 
 int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin, const int* s,
@@ -713,7 +714,7 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
   if (variant == 0) variant = kNeckX3Auto;
-  if (variant < 1 || variant > 3) return (int)hipErrorInvalidValue;
+  if (variant < 1 || variant > 5) return (int)hipErrorInvalidValue;
   NeckArgsX3 a;
   int S = 1, nsteps = 0;
   for (int i = 0; i < nbr; ++i) {
@@ -744,6 +745,10 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   switch (variant) {
     case 1: launch_neck_x3<8, 3>(a, B * nq, grid, pair, stream); break;
     case 2: launch_neck_x3<4, 2>(a, B * nq, 2 * grid, pair, stream); break;
+    // 4 waves of 64 pixels (FM 4) at one wave per SIMD: each B fragment read from LDS feeds
+    // four fragment pairs (half the LDS read bytes per MFMA of the 32-pixel waves)
+    case 4: launch_neck_x3<4, 3, 4>(a, B * nq, grid, pair, stream); break;
+    case 5: launch_neck_x3<4, 2, 4>(a, B * nq, grid, pair, stream); break;
     default: launch_neck_x3<8, 2>(a, B * nq, grid, pair, stream); break;
   }
   TCA_LAUNCH_CHECK();

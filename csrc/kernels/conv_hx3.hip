@@ -21,6 +21,7 @@ struct Hx3Args {
   int B, H, W, Cin, ldi, ci_off, Ho, Wo;
   int N, ldo, co_off, ldr, r_off;
   int act;  // 0 none, 1 relu, 2 silu, 3 leaky(0.1); | 16: act after the residual add
+  const unsigned char* occ;  // stride 2 only: uint8 [B, H, W] input occupancy (0: read as zeros) or null
 };
 
 constexpr unsigned kOutOfRange = 0x80000000u;  // buffer offset past any num_records (< 2^31): reads zeros
@@ -64,6 +65,60 @@ __device__ __forceinline__ void pair_join8(const float* p, float* v) {
   const __bf16* l = reinterpret_cast<const __bf16*>(&lq);
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
+}
+
+// epilogue (as hx): bias + act from the accumulators into an fp32 LDS tile (tile row
+// ml = line * 16 + position along the fragment axis), then 16-B pair stores (+ residual)
+template <int TH, int BN, int WM, int WN, bool CM>
+__device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* smem,
+                                             const f32x4 (&acc)[TH / WM][BN / WN / 16], int b, int oy0, int ox0,
+                                             int n0) {
+  constexpr int BM = TH * 16, NT = WM * WN * 64, FM = TH / WM, FN = BN / WN / 16, LD = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
+  float* st = reinterpret_cast<float*>(smem);
+  const int act = a.act & 15;
+  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
+  const int eact = post_res ? 0 : act;  // wave-uniform: one branch per fragment, not per element
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = (wn * FN + j) * 16 + fq * 4;
+    const float4 bv = a.bias ? *reinterpret_cast<const float4*>(a.bias + n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = (wm * FM + i) * 16 + fr;
+      float4 q = make_float4(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w);
+      if (eact == 1) {
+        q.x = fmaxf(q.x, 0.f); q.y = fmaxf(q.y, 0.f); q.z = fmaxf(q.z, 0.f); q.w = fmaxf(q.w, 0.f);
+      } else if (eact != 0) {
+        q.x = act_fn(q.x, eact); q.y = act_fn(q.y, eact); q.z = act_fn(q.z, eact); q.w = act_fn(q.w, eact);
+      }
+      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+    }
+  }
+  __syncthreads();
+  constexpr int V8 = BN / 8;
+  for (int id = tid; id < BM * V8; id += NT) {
+    const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
+    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15)), n = n0 + c8;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    float v[8];
+    const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
+    const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
+    if (a.res_f) {
+      float r[8];
+      pair_join8(a.res_f + pix * a.ldr + a.r_off + n, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
+    }
+    const long o = pix * a.ldo + a.co_off + n;
+    uint4 hi, lo;
+    pair_split8(v, hi, lo);
+    *reinterpret_cast<uint4*>(a.out_f + o) = hi;
+    *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+  }
 }
 
 // ---- x3 pair, halo-tiled 3x3 stride 1, v3 ("hx3"): weights streamed to registers.
@@ -267,51 +322,197 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
   asm volatile("" ::: "memory");
 
-  // epilogue (as hx): tile row ml = (line) * 16 + position along the fragment axis
-  constexpr int LD = BN + 4;
-  float* st = reinterpret_cast<float*>(smem);
-  const int act = a.act & 15;
-  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
-  const int eact = post_res ? 0 : act;  // wave-uniform: one branch per fragment, not per element
+  hx3_epilogue<TH, BN, WM, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
+}
+
+// ---- stride 2 ("hx3s2"): the 3x3 stride-2 pad-1 conv as four phase sub-convolutions.
+//
+// Output pixel o reads input 2o - 1 + k along each axis: k = 0 -> 2(o - 1) + 1, k = 1 -> 2o,
+// k = 2 -> 2o + 1.  On the space-to-depth view of the input (S2D pixel P, phase p: input
+// 2P + p), phase 0 carries tap 1 at P = o and phase 1 carries taps 0 (P = o - 1) and 2
+// (P = o).  So each of the four (line, fragment-axis) phases is a stride-1 conv with one or
+// two taps per axis over a (TH + 1) x 17 halo of S2D pixels, staged exactly like hx3's
+// (stride-2 gathers from global, stride-1 fragment reads from LDS, the same hswz swizzle):
+// 9 taps per 32-channel chunk in 6 groups (taps sharing the fragment-axis shift), 4 halo
+// swaps per chunk.  Per chunk a wave reads 6 FM + 3 line fragments for 9 FM x FN fragment
+// pairs (hx3: 3 FM + 6); the weight stream per MFMA is hx3's.  OCC: the halo loader reads an
+// input pixel whose occupancy byte is 0 as zeros without fetching it (the sparse pillar canvas).
+// Group g of a chunk: line parity PL = g >= 3, fragment parity PF and fragment tap FI.
+template <int G> struct S2Group {
+  static constexpr int PL = G >= 3 ? 1 : 0;
+  static constexpr int PF = (G == 0 || G == 3) ? 0 : 1;
+  static constexpr int FI = (G == 2 || G == 5) ? 1 : 0;
+  static constexpr int KF = PF == 0 ? 1 : 2 * FI;     // fragment-axis tap (original index)
+  static constexpr int FOFF = PF == 0 ? 1 : FI;        // its halo shift
+  static constexpr int NL = PL == 0 ? 1 : 2;           // line taps
+  static constexpr int PH = PL * 2 + PF;               // phase (halo buffer) of the group
+  static constexpr bool LAST_OF_PHASE = G == 0 || G == 2 || G == 3 || G == 5;
+  __device__ static constexpr int kl(int li) { return PL == 0 ? 1 : 2 * li; }   // line tap (original index)
+  __device__ static constexpr int loff(int li) { return PL == 0 ? 1 : li; }     // its halo line shift
+};
+
+template <int TH, int BN, int WN, bool CM, int MINW, bool OCC>
+__global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
+  constexpr int TW = 16, NT = WN * 64;
+  constexpr int FM = TH, FN = BN / WN / 16;
+  static_assert(BN % (WN * 16) == 0 && FN >= 1, "tiles");
+  constexpr int HWD = TW + 1, HP = (TH + 1) * HWD;  // S2D halo pixels of one phase
+  constexpr int HPIECES = HP * 8;
+  constexpr int HPL = (HPIECES + NT - 1) / NT;
+  constexpr int HBYTES = HP * 128;
+  constexpr int EPI = TH * TW * (BN + 4) * 4;
+  constexpr int LDS = (2 * HBYTES > EPI) ? 2 * HBYTES : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  constexpr int EX = CM ? TH : TW, EY = CM ? TW : TH;
+  const int tx_n = (a.Wo + EX - 1) / EX, ty_n = (a.Ho + EY - 1) / EY;
+  const int nmt = a.B * ty_n * tx_n, nnt = a.N / BN, nwg = nmt * nnt;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
+  const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
+  const int n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
+  // phase byte offsets: line parity, fragment-axis parity
+  const int pix_b = a.ldi * 4, row_b = a.W * a.ldi * 4;
+  const int dl = CM ? pix_b : row_b, df = CM ? row_b : pix_b;
+  // halo pieces of this lane: byte offset of the phase-(0, 0) input pixel, LDS offset, and the
+  // phases (bit PL * 2 + PF) whose pixel is inside the image (and occupied)
+  unsigned h_off[HPL];
+  int h_lds[HPL];
+  unsigned h_ph[HPL];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int nl = (wn * FN + j) * 16 + fq * 4;
-    const float4 bv = a.bias ? *reinterpret_cast<const float4*>(a.bias + n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < HPL; ++k) {
+    const int q = tid + k * NT, p = q >> 3, piece = q & 7;
+    h_off[k] = kOutOfRange;
+    h_lds[k] = -1;
+    h_ph[k] = 0;
+    if (q < HPIECES) {
+      const int u = p / HWD, v = p - (p / HWD) * HWD;
+      const int hy = CM ? v : u, hx = CM ? u : v;
+      const int Y = oy0 - 1 + hy, X = ox0 - 1 + hx;
+      if (Y >= 0 && X >= 0 && 2 * Y < a.H && 2 * X < a.W) {
+        h_off[k] = (unsigned)((((b * a.H + 2 * Y) * a.W + 2 * X) * a.ldi + a.ci_off) * 4 + piece * 16);
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int ml = (wm * FM + i) * 16 + fr;
-      float4 q = make_float4(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w);
-      if (eact == 1) {
-        q.x = fmaxf(q.x, 0.f); q.y = fmaxf(q.y, 0.f); q.z = fmaxf(q.z, 0.f); q.w = fmaxf(q.w, 0.f);
-      } else if (eact != 0) {
-        q.x = act_fn(q.x, eact); q.y = act_fn(q.y, eact); q.z = act_fn(q.z, eact); q.w = act_fn(q.w, eact);
+        for (int ph = 0; ph < 4; ++ph) {
+          const int pl = ph >> 1, pf = ph & 1;
+          const int iy = 2 * Y + (CM ? pf : pl), ix = 2 * X + (CM ? pl : pf);
+          bool ok = iy < a.H && ix < a.W;
+          if constexpr (OCC) ok = ok && a.occ[((long)b * a.H + iy) * a.W + ix] != 0;
+          h_ph[k] |= ok ? (1u << ph) : 0u;
+        }
       }
-      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+      h_lds[k] = p * 128 + ((piece ^ hswz(v)) << 4);
     }
   }
-  __syncthreads();
-  constexpr int V8 = BN / 8;
-  for (int id = tid; id < BM * V8; id += NT) {
-    const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
-    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15)), n = n0 + c8;
-    if (oy >= a.Ho || ox >= a.Wo) continue;
-    float v[8];
-    const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
-    const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
-    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
-    const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
-    if (a.res_f) {
-      float r[8];
-      pair_join8(a.res_f + pix * a.ldr + a.r_off + n, r);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 hreg[HPL];
+  auto halo_load = [&](int ph, int c) {  // ph: runtime-uniform phase
+    const int so = c * 128 + (ph >> 1) * dl + (ph & 1) * df;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
+    for (int k = 0; k < HPL; ++k)
+      hreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, ((h_ph[k] >> ph) & 1u) ? h_off[k] : kOutOfRange, so, 0);
+  };
+  auto halo_write = [&](int buf) {
+    unsigned char* dst = smem + buf * HBYTES;
+#pragma unroll
+    for (int k = 0; k < HPL; ++k)
+      if (k + 1 < HPL || h_lds[k] >= 0) *reinterpret_cast<u32x4*>(dst + h_lds[k]) = hreg[k];
+  };
+
+  const int NG = a.N / 16, g0 = (n0 + wn * FN * 16) / 16;
+  const __bf16* wf = reinterpret_cast<const __bf16*>(a.w) + (long)g0 * 1024 + lane * 8;
+  const int nc = a.Cin / 32;
+  auto wload = [&](int ks, bf16x8 (&dst)[FN][2]) {
+    const __bf16* p = wf + (long)ks * NG * 1024;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      dst[j][0] = *reinterpret_cast<const bf16x8*>(p + j * 1024);
+      dst[j][1] = *reinterpret_cast<const bf16x8*>(p + j * 1024 + 512);
     }
-    const long o = pix * a.ldo + a.co_off + n;
-    uint4 hi, lo;
-    pair_split8(v, hi, lo);
-    *reinterpret_cast<uint4*>(a.out_f + o) = hi;
-    *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
+  };
+  // weights of group G of chunk c (c clamped by the caller)
+  auto gload = [&](auto GC, int c, bf16x8 (&dst)[2][FN][2]) {
+    using S = S2Group<decltype(GC)::value>;
+#pragma unroll
+    for (int li = 0; li < S::NL; ++li) {
+      const int t = CM ? 3 * S::KF + S::kl(li) : 3 * S::kl(li) + S::KF;
+      wload(t * nc + c, dst[li]);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 w0[2][FN][2], w1[2][FN][2];
+  halo_load(0, 0);
+  gload(IC<0>{}, 0, w0);
+  halo_write(0);
+  halo_load(1, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // phase-chunk q = 4 c + ph lives in halo buffer q & 1 = ph & 1
+  auto phase_end = [&](int ph, int c) {
+    const int q = 4 * c + ph;
+    if (q + 1 < 4 * nc) {
+      halo_write((ph + 1) & 1);
+      const int q2 = q + 2 < 4 * nc ? q + 2 : 4 * nc - 1;
+      halo_load(q2 & 3, q2 >> 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
+  auto group = [&](auto GC, int c, bf16x8 (&wu)[2][FN][2], bf16x8 (&wl)[2][FN][2]) {
+    constexpr int G = decltype(GC)::value;
+    using S = S2Group<G>;
+    // prefetch the next group's weights (group 0 of chunk c + 1 after group 5, clamped)
+    if constexpr (G < 5) gload(IC<G + 1>{}, c, wl);
+    else gload(IC<0>{}, c + 1 < nc ? c + 1 : nc - 1, wl);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* hb = smem + (S::PH & 1) * HBYTES;
+    const int sw = hswz(S::FOFF + fr);
+    const unsigned char* colp = hb + (S::FOFF + fr) * 128;
+    const int o_hi = ((2 * fq) ^ sw) << 4, o_lo = ((2 * fq + 1) ^ sw) << 4;
+#pragma unroll
+    for (int L = (S::NL == 1 ? 1 : 0); L < FM + 1; ++L) {
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
+#pragma unroll
+      for (int li = 0; li < S::NL; ++li) {
+        const int i = L - S::loff(li);
+        if (i < 0 || i >= FM) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wu[li][j][0], wu[li][j][1], ah, al);
+      }
+    }
+    if constexpr (S::LAST_OF_PHASE) phase_end(S::PH, c);
+  };
+  for (int c = 0; c < nc; ++c) {
+    group(IC<0>{}, c, w0, w1);
+    group(IC<1>{}, c, w1, w0);
+    group(IC<2>{}, c, w0, w1);
+    group(IC<3>{}, c, w1, w0);
+    group(IC<4>{}, c, w0, w1);
+    group(IC<5>{}, c, w1, w0);
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
+  asm volatile("" ::: "memory");
+  hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
 }
 
 // TCA_HX3_PAIRS=0: the single-chunk loop with register copies (A/B measurement)
@@ -362,6 +563,36 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
   }
 }
 
+
+template <int TH, int BN, int WN, bool CM, int MINW>
+int launch_hx3s2(const Hx3Args& a, hipStream_t stream) {
+  if (a.N % BN) return (int)hipErrorInvalidValue;
+  const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
+  const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
+  if (a.occ) conv_hx3s2_kernel<TH, BN, WN, CM, MINW, true><<<nwg, WN * 64, 0, stream>>>(a);
+  else conv_hx3s2_kernel<TH, BN, WN, CM, MINW, false><<<nwg, WN * 64, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// stride-2 tiles.  0 = auto: 8 x 16 output tiles (row- or column-major by the smaller padding),
+// 4 waves of 128 pixels x 32 (N % 128 == 0) or 16 (N == 64) channels
+int hx3s2_launch(const Hx3Args& a, int tile, hipStream_t stream) {
+  if (tile == 0) {
+    const long rm8 = (long)((a.Wo + 15) / 16 * 16) * ((a.Ho + 7) / 8 * 8);
+    const long cm8 = (long)((a.Ho + 15) / 16 * 16) * ((a.Wo + 7) / 8 * 8);
+    if (a.N % 128 == 0) tile = cm8 < rm8 ? 2 : 1;
+    else if (a.N % 64 == 0) tile = cm8 < rm8 ? 4 : 3;
+    else return (int)hipErrorInvalidValue;
+  }
+  switch (tile) {
+    case 1: return launch_hx3s2<8, 128, 4, false, 2>(a, stream);
+    case 2: return launch_hx3s2<8, 128, 4, true, 2>(a, stream);
+    case 3: return launch_hx3s2<8, 64, 4, false, 3>(a, stream);
+    case 4: return launch_hx3s2<8, 64, 4, true, 3>(a, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
 }  // namespace
 
 // fp32 mode, pair activations in and out, 3x3 stride 1 pad 1 (conv_hx3_kernel).
@@ -375,9 +606,27 @@ TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi
   if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
-  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = nullptr;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   return hx3_launch(a, tile, stream);
+}
+
+// fp32 mode, pair activations in and out, 3x3 stride 2 pad 1 (conv_hx3s2_kernel), same weight
+// image as tca_conv_hx3p.  Output [B, Ho, Wo, ldo] with Ho = (H + 1) / 2, Wo = (W + 1) / 2.
+// occ: optional uint8 [B, H, W] input occupancy (a pixel marked 0 is read as zeros).
+// tile: 0 auto, 1-4 (hx3s2_launch).
+TCA_API int tca_conv_hx3s2p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
+                            const float* bias, int N, float* out, int ldo, int co_off, int act, const float* res,
+                            int ldr, int r_off, const unsigned char* occ, int tile, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
+  if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
+  Hx3Args a;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = occ;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
+  a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
+  if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
+  return hx3s2_launch(a, tile, stream);
 }

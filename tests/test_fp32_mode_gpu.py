@@ -135,7 +135,7 @@ def test_preprocess_s2d_fp32(cuda):
     assert (out.cpu() - ref).abs().mean().item() < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_fused_neck_x3_vs_unfused(cuda, variant):
     """fp32 fused deconv + head (streamed split head weights) == the fp32 module,
     for every tiling variant (per-pixel math is the same, so the bits are too)."""

@@ -95,3 +95,66 @@ def test_hx3_is_the_default_for_pair_backbone_layers(cuda):
     fc(x, out=b, tile=110)
     torch.cuda.synchronize()
     assert torch.equal(a.t, b.t)
+
+
+# stride 2: odd and even extents (partial tiles, the bottom / right halo past the image)
+S2_SHAPES = [(2, 23, 31, 64, 128), (1, 48, 34, 64, 64), (2, 19, 50, 128, 256), (3, 16, 32, 96, 64),
+             (1, 124, 108, 128, 256)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [120, 121, 122, 123, 124])
+@pytest.mark.parametrize("shape", S2_SHAPES)
+def test_hx3s2_tiles_vs_fp64(cuda, tile, shape):
+    """3x3 stride-2 phase kernel: channel-offset slices, a pair residual and ReLU against
+    fp64, untouched channels outside the output slice, and agreement with the xb
+    implicit-GEMM kernel (tile 73) on the same split products."""
+    B, H, W, cin, cout = shape
+    if tile in (121, 122) and cout % 128:
+        pytest.skip("128-channel tiles need N % 128 == 0")
+    torch.manual_seed(tile + cin + cout + H)
+    conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    assert fc.hx3_ok()
+    Ho, Wo = fc.out_hw(H, W)
+    buf = torch.randn(B, H, W, cin + 16, dtype=torch.float64)
+    res = torch.randn(B, Ho, Wo, cout, dtype=torch.float64)
+    x = NHWC(to_pairs(buf.float()).to(cuda), 8, cin, pair=True)
+    r = NHWC(to_pairs(res.float()).to(cuda), pair=True)
+    outs = {}
+    for t in (tile, 73):
+        out = torch.full((B, Ho, Wo, cout + 16), 7.0, dtype=torch.float32, device=cuda)
+        fc(x, out=NHWC(out, 8, cout, pair=True), res=r, tile=t)
+        torch.cuda.synchronize()
+        outs[t] = out
+        assert (out[..., :8] == 7.0).all() and (out[..., 8 + cout:] == 7.0).all()
+    ref = torch.relu(conv(buf[..., 8:8 + cin].permute(0, 3, 1, 2))) + from_pairs(r.t).double().cpu().permute(0, 3, 1, 2)
+    got = NHWC(outs[tile], 8, cout, pair=True).nchw()
+    assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
+    xb = NHWC(outs[73], 8, cout, pair=True).nchw()
+    assert rel_l2(got, xb) < 2e-5, rel_l2(got, xb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [120, 123, 124])
+def test_hx3s2_occupancy_reads_unmarked_pixels_as_zero(cuda, tile):
+    """The sparse-canvas form: garbage in the unmarked pixels, occupancy 0 there; the
+    result equals the conv of the masked input (and the default route takes it)."""
+    torch.manual_seed(11)
+    B, H, W, cin, cout = 2, 50, 38, 64, 64
+    conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    occ = (torch.rand(B, H, W) < 0.1).to(torch.uint8)
+    xin = torch.randn(B, H, W, cin, dtype=torch.float64)
+    garbage = torch.full_like(xin, 1e6)
+    stored = torch.where(occ.bool()[..., None], xin, garbage)
+    x = NHWC(to_pairs(stored.float()).to(cuda), pair=True, occ=occ.to(cuda))
+    Ho, Wo = fc.out_hw(H, W)
+    out = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    fc(x, out=out, tile=tile)
+    dflt = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    fc(x, out=dflt)
+    torch.cuda.synchronize()
+    ref = torch.relu(conv((xin * occ[..., None].double()).permute(0, 3, 1, 2)))
+    assert rel_l2(out.nchw(), ref) < 5e-5, rel_l2(out.nchw(), ref)
+    assert rel_l2(dflt.nchw(), ref) < 5e-5

@@ -101,11 +101,15 @@ PRECISIONS = ("fp32", "bf16")
 PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 90, 91, 92, 93, 94, 95, 96, 97, 102)
 
 
-# conv_hx3.hip (3x3 stride-1 pair convs with register-streamed fragment-order weights): on
-# by default for every eligible layer; TCA_HX3=0 falls back to the conv_mfma.hip tiles.
-# Tiles 110 (auto) and 111-116 (conv_hx3.hip hx3_launch tiles 1-6) select it explicitly.
+# conv_hx3.hip (3x3 stride-1 / stride-2 pair convs with register-streamed fragment-order
+# weights): on by default for every eligible layer; TCA_HX3=0 falls back to the conv_mfma.hip
+# tiles (TCA_HX3S2=0: only the stride-2 layers do).  Tiles 110 (auto) and 111-116
+# (hx3_launch tiles 1-6) select the stride-1 kernel explicitly, 120 and 121-124
+# (hx3s2_launch tiles 1-4) the stride-2 one.
 HX3 = os.environ.get("TCA_HX3", "1") != "0"
+HX3S2 = HX3 and os.environ.get("TCA_HX3S2", "1") != "0"
 HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
+HX3S2_TILES = (120, 121, 122, 123, 124)
 
 
 def frag_weights(W: torch.Tensor) -> torch.Tensor:
@@ -239,7 +243,16 @@ class FusedConv:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
-            if (out.pair and x.occ is None and self.hx3_ok() and
+            if out.pair and self.hx3_ok() and self.s == 2 and (tile in HX3S2_TILES or (tile == 0 and HX3S2)):
+                occ = x.occ
+                if occ is not None:
+                    assert occ.dtype == torch.uint8 and tuple(occ.shape) == (B, H, W), (occ.shape, (B, H, W))
+                _native.call("tca_conv_hx3s2p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                             _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
+                             _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp, _native.ptr(occ),
+                             tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
+                return out
+            if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
                 _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
@@ -264,8 +277,8 @@ class FusedConv:
         return out
 
     def hx3_ok(self) -> bool:
-        """conv_hx3.hip takes this conv: fp32, 3x3 stride 1 pad 1, Cin % 32, N % 64."""
-        return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s == 1 and self.p == 1
+        """conv_hx3.hip takes this conv: fp32, 3x3 stride 1 or 2, pad 1, Cin % 32, N % 64."""
+        return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s in (1, 2) and self.p == 1
                 and self.cin_p % 32 == 0 and self.K == self.Kp and self.N % 64 == 0)
 
     def hx3_weights(self) -> torch.Tensor:
