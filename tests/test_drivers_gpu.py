@@ -190,3 +190,61 @@ def test_served_shared_memory_matches_raw_wire(cuda):
     for a, b in zip(out["raw"][1], out["shm"][1]):
         assert len(a["pred_scores"]) > 0
         np.testing.assert_array_equal(a["pred_boxes"], b["pred_boxes"])
+
+
+def test_served_device_shared_memory_matches_raw_wire(cuda):
+    """Device shared memory (HIP IPC handles registered with a server in another process:
+    the camera input and 2D output, and the voxel tensors, stay in GPU buffers; only
+    region references cross gRPC) returns the raw-wire path's detections."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+    from triton_client_amd.clients import Yolov5client, client_for_model
+    from triton_client_amd.inference import RemoteDetector2D, RemoteDetector3D
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    srv = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+                            str(port), "--models", "YOLOv5nCOCO,pointpillar_kitti", "--device", "cuda",
+                            "--metrics-port", "0"], cwd=root)
+    try:
+        frames = [camera_frame(480, 640, s) for s in (1, 2, 3, 4, 5)]
+        clouds = [_cloud(s, 64, 1875) for s in (4, 5, 6)]
+
+        class F:
+            model_version, batch_size = "", 1
+
+        f2, f3 = F(), F()
+        f2.model_name, f3.model_name = "YOLOv5nCOCO", "pointpillar_kitti"
+        p = {"grpc_channel": f"127.0.0.1:{port}"}
+        ch2, ch3 = GRPCChannel(p, f2, wait_ready_s=240.0), GRPCChannel(p, f3, wait_ready_s=240.0)
+        cfg3 = ch3.get_metadata()["config_response"]
+        out = {}
+        for wire in ("raw", "devshm"):
+            d2 = RemoteDetector2D(ch2, Yolov5client(), device=cuda, mode="async", wire=wire)
+            d3 = RemoteDetector3D(ch3, client_for_model("pointpillar_kitti", getattr(cfg3, "config", cfg3)),
+                                  device=cuda, mode="async", wire=wire)
+            d2.window = d3.window = 2  # slots are reused within the call
+            out[wire] = (d2.detect(frames), d3.detect(clouds))
+            if wire == "devshm":
+                assert len(ch2.cuda_shared_memory_status().regions) == 2
+                assert len(ch2.system_shared_memory_status().regions) == 0
+                d2.close_shm()
+                d3.close_shm()
+        assert len(ch2.cuda_shared_memory_status().regions) == 0
+        ch2.close()
+        ch3.close()
+    finally:
+        srv.terminate()
+        srv.wait(60)
+    for a, b in zip(out["raw"][0], out["devshm"][0]):
+        np.testing.assert_array_equal(a, b)
+    assert sum(len(a) for a in out["raw"][0]) > 10
+    for a, b in zip(out["raw"][1], out["devshm"][1]):
+        assert len(a["pred_scores"]) > 0
+        np.testing.assert_array_equal(a["pred_boxes"], b["pred_boxes"])

@@ -1,5 +1,6 @@
 """KServe-v2 protocol: runtime protos vs wire codec, server + channel round
 trips over real gRPC on 127.0.0.1 (CPU models)."""
+import os
 import numpy as np
 import pytest
 
@@ -305,3 +306,48 @@ def test_shm_unregister_waits_for_in_flight_executions(tmp_path):
         assert done.is_set() and reg.status() == []
     finally:
         os.unlink(path)
+
+
+def test_multi_process_server_shares_the_port_and_stops_cleanly():
+    """--procs 3: three server processes on one port (SO_REUSEPORT); every connection is
+    served, and SIGTERM to the parent ends the children too (the port is free again)."""
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    import grpc
+
+    from triton_client_amd.channel.wire import encode_request, parse_response
+    from triton_client_amd.proto import SERVICE
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port", str(port),
+                          "--models", "echo", "--device", "cpu", "--metrics-port", "0", "--procs", "3"], cwd=root)
+    try:
+        deadline = time.time() + 120
+        served = 0
+        for i in range(6):
+            while True:
+                ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+                f = ch.unary_unary(f"/{SERVICE}/ModelInfer", request_serializer=None, response_deserializer=None)
+                try:
+                    x = np.arange(4 + i, dtype=np.float32)
+                    r = parse_response(f(encode_request("echo", [("INPUT0", x)]), timeout=20))
+                    assert np.array_equal(r["OUTPUT0"], x)
+                    served += 1
+                    break
+                except grpc.RpcError:
+                    assert time.time() < deadline, "server did not come up"
+                    time.sleep(0.5)
+                finally:
+                    ch.close()
+        assert served == 6
+    finally:
+        p.terminate()
+        assert p.wait(60) == 0
+    with socket.socket() as sk:  # no child process still holds the port
+        sk.bind(("127.0.0.1", port))

@@ -46,8 +46,9 @@ def main(argv=None):
     ap.add_argument("--columns", type=int, default=1875)
     ap.add_argument("--workers", type=int, default=32, help="server threads")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--wire", default="raw", choices=("raw", "shm"),
-                    help="raw: tensors in the gRPC messages (C++ codec); shm: KServe system shared memory")
+    ap.add_argument("--wire", default="raw", choices=("raw", "shm", "devshm"),
+                    help="raw: tensors in the gRPC messages (C++ codec); shm: KServe system shared memory; "
+                         "devshm: device shared memory (GPU buffers shared by HIP IPC handle, Triton's CUDA shm)")
     ap.add_argument("--server-process", action="store_true",
                     help="run the server as its own process (the deployed topology: no GIL shared with the clients)")
     ap.add_argument("--client-procs", type=int, default=0,
@@ -58,6 +59,9 @@ def main(argv=None):
     ap.add_argument("--role", default=None, choices=("camera", "lidar"), help=argparse.SUPPRESS)
     ap.add_argument("--target", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--server-procs", type=int, default=1, help="server processes sharing the port (--procs)")
+    ap.add_argument("--server-profile", default=None, metavar="JSON",
+                    help="multi-process runs: the server's stage clock (TCA_SERVER_PROFILE) written here")
     a = ap.parse_args(argv)
     if a.role is not None:
         return client_proc(a)
@@ -249,8 +253,10 @@ def multi_proc(a) -> int:
     here = os.path.abspath(__file__)
     server = subprocess.Popen([sys.executable, "-X", "faulthandler", "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
                                str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
-                               "--models", "YOLOv5nCOCO,pointpillar_kitti"],
-                              cwd=os.path.dirname(os.path.dirname(here)))
+                               "--models", "YOLOv5nCOCO,pointpillar_kitti", "--procs", str(a.server_procs)],
+                              cwd=os.path.dirname(os.path.dirname(here)),
+                              env=dict(os.environ, **({"TCA_SERVER_PROFILE": os.path.abspath(a.server_profile)}
+                                                      if a.server_profile else {})))
     common = ["--frames", str(a.frames), "--warmup", str(a.warmup), "--window", str(a.window), "--device", a.device,
               "--cam", a.cam, "--rings", str(a.rings), "--columns", str(a.columns), "--wire", a.wire,
               "--target", target] + (["--burst"] if a.burst else [])
@@ -299,8 +305,16 @@ def multi_proc(a) -> int:
             "client_ms_per_frame": {"camera": mean_ms("camera"), "lidar": mean_ms("lidar")},
             "client_wall_s": {o["role"] + str(i // 2): round(o["wall_s"], 3) for i, o in enumerate(outs)},
             "server_requests_per_execution": rpe,
-            "topology": f"server process + {a.client_procs} camera and {a.client_procs} LiDAR client processes",
+            "topology": (f"{a.server_procs} server process{'es' if a.server_procs > 1 else ''} + {a.client_procs} camera "
+                         f"and {a.client_procs} LiDAR client processes"),
             "wire": a.wire, "window_mode": "burst" if a.burst else "sliding",
+            "path": {"raw": "tensors inside the gRPC messages (C++ codec both ends)",
+                     "shm": "GPU preprocess -> page-locked /dev/shm slot -> region references in the message -> "
+                            "server DMA from / into the client's slot",
+                     "devshm": "GPU preprocess into the client's device buffer (HIP IPC handle registered with the "
+                               "server) -> region references in the message -> server copies device to device, "
+                               "writes the 2D output into the client's device buffer; only detections cross PCIe"
+                     }[a.wire],
             "avg_dets_per_frame": {"2d": round(float(np.mean([o["dets"] for o in outs if o["role"] == "camera"])), 1),
                                    "3d": round(float(np.mean([o["dets"] for o in outs if o["role"] == "lidar"])), 1)}}
     print(json.dumps(line), flush=True)

@@ -176,6 +176,19 @@ class GRPCChannel(BaseChannel):
     def system_shared_memory_status(self, name: str = ""):
         return self._call(self._grpc_stub.SystemSharedMemoryStatus, pb.SystemSharedMemoryStatusRequest(name=name))
 
+    def register_cuda_shared_memory(self, name: str, raw_handle: bytes, device_id: int, byte_size: int):
+        """Device shared memory (Triton's CudaSharedMemoryRegister; here a HIP IPC handle,
+        ``utils.hip_ipc.DeviceAllocation``)."""
+        return self._call(self._grpc_stub.CudaSharedMemoryRegister,
+                          pb.CudaSharedMemoryRegisterRequest(name=name, raw_handle=raw_handle, device_id=device_id,
+                                                             byte_size=byte_size))
+
+    def unregister_cuda_shared_memory(self, name: str = ""):
+        return self._call(self._grpc_stub.CudaSharedMemoryUnregister, pb.CudaSharedMemoryUnregisterRequest(name=name))
+
+    def cuda_shared_memory_status(self, name: str = ""):
+        return self._call(self._grpc_stub.CudaSharedMemoryStatus, pb.CudaSharedMemoryStatusRequest(name=name))
+
     def model_statistics(self, name: str = ""):
         return self._grpc_stub.ModelStatistics(pb.ModelStatisticsRequest(name=name), timeout=self.timeout_s)
 

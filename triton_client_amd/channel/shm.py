@@ -16,7 +16,46 @@ import numpy as np
 from ..server.shm import SHM_DIR, _host_register, _host_unregister
 
 
+class DeviceShmRegion:
+    """Client side of the device shared-memory transport: a dedicated GPU allocation
+    whose HIP IPC handle the server maps (``register`` → Triton's
+    CudaSharedMemoryRegister).  ``view`` returns torch tensors on the GPU; the
+    preprocess writes the request inputs there and the server writes the outputs
+    back there, device to device."""
+
+    def __init__(self, byte_size: int, device="cuda", key: Optional[str] = None):
+        from ..utils.hip_ipc import DeviceAllocation
+        self.key = key or f"tca_dev_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+        self.byte_size = int(byte_size)
+        self.alloc = DeviceAllocation(self.byte_size, device)
+        self.device = self.alloc.device
+
+    def register(self, channel) -> None:
+        channel.register_cuda_shared_memory(self.key, self.alloc.handle, self.alloc.device_id, self.byte_size)
+
+    def unregister(self, channel) -> None:
+        channel.unregister_cuda_shared_memory(self.key)
+
+    def view(self, offset: int, dtype, shape):
+        import torch
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape))
+        if offset < 0 or offset + n * dt.itemsize > self.byte_size:
+            raise ValueError(f"[{offset}, {offset + n * dt.itemsize}) outside the {self.byte_size}-byte region")
+        tdt = torch.from_numpy(np.empty(0, dt)).dtype
+        return self.alloc.tensor[offset:offset + n * dt.itemsize].view(tdt).reshape(shape)
+
+    def close(self, unlink: bool = True) -> None:
+        self.alloc.close()
+
+
 class ShmRegion:
+    def register(self, channel) -> None:
+        channel.register_system_shared_memory(self.key, self.key, self.byte_size)
+
+    def unregister(self, channel) -> None:
+        channel.unregister_system_shared_memory(self.key)
+
     def __init__(self, byte_size: int, key: Optional[str] = None, pin: bool = True):
         self.key = key or f"tca_{os.getpid()}_{uuid.uuid4().hex[:12]}"
         self.byte_size = int(byte_size)

@@ -148,8 +148,8 @@ class PointpillarPreprocess:
             if name == "voxel_coords":
                 t = t.clone()
                 t[:, 0] = 0
-            if name in dst:
-                pin = torch.from_numpy(dst[name])
+            if name in dst:  # a host (page-locked) array, or a device tensor (device shared memory)
+                pin = dst[name] if isinstance(dst[name], torch.Tensor) else torch.from_numpy(dst[name])
                 if pin.dtype != tdt or pin.shape[0] < k or tuple(pin.shape[1:]) != tuple(t.shape[1:]):
                     raise ValueError(f"{name}: destination {tuple(pin.shape)} {pin.dtype} cannot take "
                                      f"{k} rows of {tuple(t.shape[1:])} {tdt}")

@@ -590,11 +590,35 @@ def _set_outputs(channel, names: Sequence[str]):
     channel.output = pb.ModelInferRequest.InferRequestedOutputTensor(name=names[0]) if names else None
 
 
+def _new_region(wire: str, nbytes: int, device):
+    """The client's shared-memory region for a wire: system (page-locked /dev/shm
+    mapping) or device (a GPU allocation shared by HIP IPC handle)."""
+    from ..channel.shm import DeviceShmRegion, ShmRegion
+    if wire == "devshm":
+        if torch.device(device).type != "cuda":
+            raise ValueError("wire='devshm' needs a GPU client (device='cuda')")
+        return DeviceShmRegion(nbytes, device)
+    return ShmRegion(nbytes)
+
+
+def _device_output_to_host(a: torch.Tensor, conf_thres: float) -> np.ndarray:
+    """A model output in device shared memory → the host array the postprocess reads.
+    A decoded YOLO prediction [1, N, 5 + nc] comes back as only its rows with
+    objectness > conf_thres (the postprocess's first filter, so its results are
+    unchanged: the surviving rows keep their order); anything else whole."""
+    if a.dim() == 3 and a.shape[0] == 1 and a.shape[2] > 5 and a.dtype == torch.float32:
+        rows = a[0][a[0, :, 4] > conf_thres]
+        return rows.cpu().numpy()[None]
+    return a.cpu().numpy()
+
+
 class _RemoteBase:
     def __init__(self, channel, client, mode: str = "sync", wire: str = "raw", window: int = 8):
         if mode not in ("sync", "async", "stream"):
             raise ValueError(f"mode {mode!r}")
-        if wire not in ("raw", "proto", "shm"):  # shm: KServe system shared memory (same-host server)
+        # shm: KServe system shared memory (same-host server); devshm: device shared memory
+        # (a GPU allocation shared by HIP IPC handle: tensors stay on the GPU end to end)
+        if wire not in ("raw", "proto", "shm", "devshm"):
             raise ValueError(f"wire {wire!r}")
         self.channel, self.client, self.mode, self.wire, self.window = channel, client, mode, wire, window
         md = channel.get_metadata()
@@ -782,8 +806,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
             b = nbytes(shape, KSERVE_TO_NP[md[n].datatype])
             layout.append((n, off, b))
             off += align(b)
-        region = ShmRegion(off * self.window)
-        self.channel.register_system_shared_memory(region.key, region.key, region.byte_size)
+        region = _new_region(self.wire, off * self.window, self.device)
+        region.register(self.channel)
         self._shm = (region, off, in_shape, in_dt, layout)
         return self._shm
 
@@ -791,12 +815,12 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         st = getattr(self, "_shm", None)
         if st is not None:
             try:
-                self.channel.unregister_system_shared_memory(st[0].key)
+                st[0].unregister(self.channel)
             finally:
                 st[0].close()
                 self._shm = None
 
-    def _prep_into(self, frame: np.ndarray, dst: np.ndarray):
+    def _prep_into(self, frame: np.ndarray, dst):
         """Preprocess straight into a shm slot (GPU: one D2H into the pinned mapping)."""
         if self.device.type == "cuda":
             _, pin_in, dev_in, _, tdt = self._gpu_staging(tuple(frame.shape[:2]))
@@ -808,8 +832,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
                 x = x.permute(0, 2, 3, 1)
             if not self.batch_dim:
                 x = x[0]
-            torch.from_numpy(dst).copy_(x.to(tdt), non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
+            (dst if isinstance(dst, torch.Tensor) else torch.from_numpy(dst)).copy_(x.to(tdt), non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()  # complete before the server reads it
             return xf
         a, xf = self._prep(frame)
         np.copyto(dst, a.reshape(dst.shape), casting="same_kind")
@@ -833,7 +857,10 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
             pr.model_name = resp.model_name
             offs = {n: o for n, o, _ in layout}
             for t in resp.outputs:
-                pr.outputs[t.name] = region.view(k * slot + offs[t.name], KSERVE_TO_NP[t.datatype], tuple(t.shape))
+                a = region.view(k * slot + offs[t.name], KSERVE_TO_NP[t.datatype], tuple(t.shape))
+                if isinstance(a, torch.Tensor):  # device shared memory: only what the host needs comes back
+                    a = _device_output_to_host(a, self.conf_thres)
+                pr.outputs[t.name] = a
                 pr.datatypes[t.name] = t.datatype
                 pr.order.append(t.name)
             d = self._extract(pr)  # consumed before slot k is reused
@@ -871,7 +898,7 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
     def detect(self, frames: Sequence[np.ndarray]) -> List[np.ndarray]:
         from ..utils.trace import trace_range
         timer = getattr(self, "timer", None)
-        if self.wire == "shm":
+        if self.wire in ("shm", "devshm"):
             return self._detect_shm(frames)
         if self.wire == "raw" and self.mode != "stream":
             # prepare + encode frame by frame: the staging buffer is reused, each
@@ -993,8 +1020,9 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
                 b = int(np.prod(shapes[key], dtype=np.int64)) * dt.itemsize
                 lay.append((key, off, b, dt, shapes[key]))
                 off += (b + 4095) // 4096 * 4096
-            region = ShmRegion(off * self.window)  # page-locked: the voxeliser's D2H lands in it
-            ch.register_system_shared_memory(region.key, region.key, region.byte_size)
+            # system: page-locked, the voxeliser's D2H lands in it; device: written on the GPU
+            region = _new_region(self.wire, off * self.window, getattr(self.pre, "device", "cpu"))
+            region.register(ch)
             self._shm = (region, off, lay)
         region, slot, lay = self._shm
 
@@ -1028,7 +1056,7 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
         st = getattr(self, "_shm", None)
         if st is not None:
             try:
-                self.channel.unregister_system_shared_memory(st[0].key)
+                st[0].unregister(self.channel)
             finally:
                 st[0].close()
                 self._shm = None
@@ -1038,7 +1066,9 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
 
         gpu_pre = (getattr(self.pre, "device", None) is not None and self.pre.device.type == "cuda"
                    and hasattr(self.pre, "filter_cloud_gpu"))
-        if self.wire == "shm" and gpu_pre:
+        if self.wire == "devshm" and not gpu_pre:
+            raise ValueError("wire='devshm' needs the GPU preprocess (device='cuda')")
+        if self.wire in ("shm", "devshm") and gpu_pre:
             keep, resps = self._detect_gpu_shm(clouds)
             return self._outputs(clouds, keep, resps)
         if self.wire == "raw" and self.mode != "stream" and gpu_pre:

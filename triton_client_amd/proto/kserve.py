@@ -326,6 +326,30 @@ def _service_file() -> descriptor_pb2.FileDescriptorProto:
     _field(m, "name", 1, T_STRING)
     add(name="SystemSharedMemoryUnregisterResponse")
 
+    # device shared-memory extension (Triton grpc_service.proto CudaSharedMemory*; on this
+    # framework the handle is a HIP IPC memory handle of a device allocation, server/shm.py)
+    m = add(name="CudaSharedMemoryStatusRequest")
+    _field(m, "name", 1, T_STRING)
+    m = add(name="CudaSharedMemoryStatusResponse")
+    rs = m.nested_type.add(name="RegionStatus")
+    _field(rs, "name", 1, T_STRING)
+    _field(rs, "device_id", 2, T_UINT64)
+    _field(rs, "byte_size", 3, T_UINT64)
+    e = m.nested_type.add(name="RegionsEntry")
+    e.options.map_entry = True
+    _field(e, "key", 1, T_STRING)
+    _field(e, "value", 2, T_MSG, type_name="CudaSharedMemoryStatusResponse.RegionStatus")
+    _field(m, "regions", 1, T_MSG, REP, type_name="CudaSharedMemoryStatusResponse.RegionsEntry")
+    m = add(name="CudaSharedMemoryRegisterRequest")
+    _field(m, "name", 1, T_STRING)
+    _field(m, "raw_handle", 2, T_BYTES)
+    _field(m, "device_id", 3, T_INT64)
+    _field(m, "byte_size", 4, T_UINT64)
+    add(name="CudaSharedMemoryRegisterResponse")
+    m = add(name="CudaSharedMemoryUnregisterRequest")
+    _field(m, "name", 1, T_STRING)
+    add(name="CudaSharedMemoryUnregisterResponse")
+
     svc = fd.service.add(name="GRPCInferenceService")
     for rpc, req, resp, cs, ss in SERVICE_METHODS:
         mth = svc.method.add(name=rpc, input_type=f".{PKG}.{req}", output_type=f".{PKG}.{resp}")
@@ -353,6 +377,10 @@ SERVICE_METHODS = [
      False),
     ("SystemSharedMemoryUnregister", "SystemSharedMemoryUnregisterRequest", "SystemSharedMemoryUnregisterResponse",
      False, False),
+    ("CudaSharedMemoryStatus", "CudaSharedMemoryStatusRequest", "CudaSharedMemoryStatusResponse", False, False),
+    ("CudaSharedMemoryRegister", "CudaSharedMemoryRegisterRequest", "CudaSharedMemoryRegisterResponse", False, False),
+    ("CudaSharedMemoryUnregister", "CudaSharedMemoryUnregisterRequest", "CudaSharedMemoryUnregisterResponse", False,
+     False),
 ]
 
 

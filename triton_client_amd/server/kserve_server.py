@@ -26,7 +26,7 @@ import grpc
 import numpy as np
 
 from ..proto import KSERVE_TO_NP, SERVICE, service_pb2 as pb
-from .model import InferError, ServedModel
+from .model import PROFILE, InferError, ServedModel
 from .repository import ModelRepository
 
 _BF16 = "BF16"
@@ -99,6 +99,21 @@ def decode_inputs(req, shm=None) -> Dict[str, np.ndarray]:
     return out
 
 
+def output_slices(req, shm) -> Optional[Dict[str, np.ndarray]]:
+    """{output name: uint8 view of its shared-memory slice} for the outputs a request
+    asks to receive in shared memory (None: none does)."""
+    from .shm import tensor_shm
+    if shm is None:
+        return None
+    out = {}
+    for o in req.outputs:
+        ref = tensor_shm(o.parameters)
+        if ref is not None:
+            region, off, nbytes = ref
+            out[o.name] = shm.get(region).view(off, nbytes, np.uint8, (nbytes,))
+    return out or None
+
+
 def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], corrupt: bool = False, shm=None):
     """Protobuf response; an output requested into a shared-memory region is
     written there and answered with its shape / datatype (and the region
@@ -111,10 +126,33 @@ def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], cor
         if n not in outputs:
             raise InferError(f"unknown output '{n}' for model '{model.name}'")
         a = outputs[n]
+        ref = tensor_shm(params[n]) if n in params else None
+        reg = shm.get(ref[0]) if (ref is not None and shm is not None) else None
+        if reg is not None and reg.device and getattr(a, "is_cuda", False):
+            # device output for a device region: written there by the model (or copied on the device)
+            import torch
+            dt = np.dtype(str(a.dtype).replace("torch.", ""))
+            t = resp.outputs.add(name=n, datatype=_kserve_dtype(np.empty(0, dt)))
+            t.shape.extend(a.shape)
+            region, off, nbytes = ref
+            size = a.numel() * a.element_size()
+            if size > nbytes:
+                raise InferError(f"output '{n}': {size} bytes exceed the {nbytes}-byte shared memory slice")
+            dst = reg.view(off, size, dt, tuple(a.shape))
+            if corrupt:
+                dst.zero_()
+            elif dst.data_ptr() != a.data_ptr():
+                dst.copy_(a)
+                torch.cuda.current_stream(dst.device).synchronize()
+            for key in ("shared_memory_region", "shared_memory_offset", "shared_memory_byte_size"):
+                if key in params[n]:
+                    t.parameters[key].CopyFrom(params[n][key])
+            continue
+        if getattr(a, "is_cuda", False):
+            a = a.cpu()
         a = np.ascontiguousarray(a.numpy() if hasattr(a, "numpy") and not isinstance(a, np.ndarray) else a)
         t = resp.outputs.add(name=n, datatype=_kserve_dtype(a))
         t.shape.extend(a.shape)
-        ref = tensor_shm(params[n]) if n in params else None
         if ref is not None:
             if shm is None:
                 raise InferError("shared memory outputs are not supported by this server")
@@ -123,8 +161,12 @@ def encode_response(model: ServedModel, req, outputs: Dict[str, np.ndarray], cor
                 raise InferError(f"output '{n}': {a.nbytes} bytes exceed the {nbytes}-byte shared memory slice")
             dst = shm.get(region).view(off, a.nbytes, a.dtype, a.shape)
             if corrupt:
-                dst.fill(0)
-            else:
+                dst[...] = 0
+            elif reg is not None and reg.device:
+                import torch
+                dst.copy_(torch.from_numpy(a))
+                torch.cuda.current_stream(dst.device).synchronize()
+            elif dst.ctypes.data != a.ctypes.data:  # not already written there by the device
                 np.copyto(dst, a)
             for key in ("shared_memory_region", "shared_memory_offset", "shared_memory_byte_size"):
                 if key in params[n]:
@@ -219,9 +261,12 @@ class GRPCInferenceServicer:
             ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
         try:
             inputs = decode_inputs(req, self.shm)
+            if PROFILE.on:
+                PROFILE.add("pb.decode_inputs", time.perf_counter() - t0)
             corrupt = self.fault.roll(self.fault.corrupt_rate)
             resp = m(inputs, [o.name for o in req.outputs],
-                     encode=lambda outputs: encode_response(m, req, outputs, corrupt=corrupt, shm=self.shm))
+                     encode=lambda outputs: encode_response(m, req, outputs, corrupt=corrupt, shm=self.shm),
+                     out_dst=None if corrupt else output_slices(req, self.shm))
         except InferError as e:
             if self.metrics:
                 self.metrics.request(m.name, False, time.perf_counter() - t0)
@@ -253,8 +298,31 @@ class GRPCInferenceServicer:
         return pb.SystemSharedMemoryRegisterResponse()
 
     def SystemSharedMemoryUnregister(self, req, ctx):
-        self.shm.unregister(req.name)
+        self.shm.unregister(req.name, device=False)
         return pb.SystemSharedMemoryUnregisterResponse()
+
+    # ------------------------------------------------- device shared memory (HIP IPC)
+    def CudaSharedMemoryStatus(self, req, ctx):
+        resp = pb.CudaSharedMemoryStatusResponse()
+        try:
+            regions = self.shm.status(req.name, device=True)
+        except InferError as e:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, str(e))
+        for r in regions:
+            st = resp.regions[r.name]
+            st.name, st.device_id, st.byte_size = r.name, r.device_id, r.byte_size
+        return resp
+
+    def CudaSharedMemoryRegister(self, req, ctx):
+        try:
+            self.shm.register_device(req.name, bytes(req.raw_handle), int(req.device_id), int(req.byte_size))
+        except InferError as e:
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        return pb.CudaSharedMemoryRegisterResponse()
+
+    def CudaSharedMemoryUnregister(self, req, ctx):
+        self.shm.unregister(req.name, device=True)
+        return pb.CudaSharedMemoryUnregisterResponse()
 
     def ModelInferBytes(self, data: bytes, ctx) -> bytes:
         """ModelInfer on the raw wire bytes through the C++ codec: inputs are
@@ -268,8 +336,21 @@ class GRPCInferenceServicer:
             req = parse_request(data)
         except ValueError as e:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        if PROFILE.on:
+            PROFILE.add("wire.parse", time.perf_counter() - t0)
         if req.has_params:  # shared-memory references: a small message, the protobuf path reads them
-            return self._infer(pb.ModelInferRequest.FromString(data), ctx).SerializeToString()
+            t1 = time.perf_counter()
+            pr = pb.ModelInferRequest.FromString(data)
+            t2 = time.perf_counter()
+            out = self._infer(pr, ctx)
+            t3 = time.perf_counter()
+            out = out.SerializeToString()
+            if PROFILE.on:
+                PROFILE.add("pb.from_string", t2 - t1)
+                PROFILE.add("pb.infer", t3 - t2)
+                PROFILE.add("pb.serialize", time.perf_counter() - t3)
+                PROFILE.add("request_total", time.perf_counter() - t0)
+            return out
         m = self._model(req.model_name, req.model_version, ctx)
         if self.fault.delay_s:
             time.sleep(self.fault.delay_s)
@@ -296,6 +377,8 @@ class GRPCInferenceServicer:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         if self.metrics:
             self.metrics.request(m.name, True, time.perf_counter() - t0)
+        if PROFILE.on:
+            PROFILE.add("request_total", time.perf_counter() - t0)
         return resp
 
     def ModelStreamInfer(self, req_iter, ctx):
@@ -342,18 +425,20 @@ def _handlers(servicer: GRPCInferenceServicer, raw_infer: bool = True):
 class KServeServer:
     def __init__(self, repo: ModelRepository, address: str = "127.0.0.1:8001", max_workers: int = 8,
                  max_message_bytes: int = 512 << 20, fault: Optional[FaultInjector] = None,
-                 metrics_port: Optional[int] = None, raw_infer: bool = True):
+                 metrics_port: Optional[int] = None, raw_infer: bool = True, switch_interval_s: float = 2e-4):
         """raw_infer: serve ModelInfer through the C++ codec on the wire bytes
         (False: the protobuf runtime, as a Triton-like reference path)."""
         self.repo = repo
         self.address = address
+        self.switch_interval_s = switch_interval_s
         metrics = None
         if metrics_port is not None:
             from ..utils.metrics import ServerMetrics
             metrics = ServerMetrics(port=metrics_port)
         self.servicer = GRPCInferenceServicer(repo, fault, metrics)
         opts = [("grpc.max_send_message_length", max_message_bytes),
-                ("grpc.max_receive_message_length", max_message_bytes)]
+                ("grpc.max_receive_message_length", max_message_bytes),
+                ("grpc.so_reuseport", 1)]  # `python -m triton_client_amd.server --procs N` shares the port
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers), options=opts)
         self.server.add_generic_rpc_handlers((_handlers(self.servicer, raw_infer),))
         self.port = self.server.add_insecure_port(address)
@@ -366,6 +451,13 @@ class KServeServer:
         return f"{host}:{self.port}"
 
     def start(self) -> "KServeServer":
+        # GIL hand-off: a batcher thread returning from a device wait (or a request thread
+        # from a socket read) otherwise waits up to the 5 ms default switch interval for a
+        # thread running Python to yield — several times per batch (measured on the served
+        # bench: ~6 ms of every 15 ms PointPillars execution, TCA_SERVER_PROFILE)
+        import sys
+        if sys.getswitchinterval() > self.switch_interval_s:
+            sys.setswitchinterval(self.switch_interval_s)
         self.server.start()
         return self
 

@@ -95,11 +95,51 @@ class _RWLock:
 GPU_PHASE = _RWLock()
 
 
-class _Pending:
-    __slots__ = ("inputs", "requested", "encode", "done", "result", "exc")
+class StageProfile:
+    """Server-side stage clock for the served-path bench (``TCA_SERVER_PROFILE=<json path>``):
+    per stage the summed seconds and count, over every request / execution thread;
+    written by :meth:`dump` (the standalone server does at SIGTERM).  Disabled: one
+    attribute test per stage."""
 
-    def __init__(self, inputs, requested, encode):
-        self.inputs, self.requested, self.encode = inputs, requested, encode
+    def __init__(self, path: Optional[str]):
+        self.path, self.on = path, bool(path)
+        self.t: Dict[str, float] = collections.defaultdict(float)
+        self.n: Dict[str, int] = collections.defaultdict(int)
+        self.lock = threading.Lock()
+        self.t0 = time.perf_counter()
+
+    def add(self, stage: str, seconds: float, n: int = 1) -> None:
+        with self.lock:
+            self.t[stage] += seconds
+            self.n[stage] += n
+
+    def summary(self) -> dict:
+        wall = time.perf_counter() - self.t0
+        with self.lock:
+            return {"wall_s": round(wall, 3),
+                    "stages": {k: {"count": self.n[k], "total_s": round(v, 4),
+                                   "ms_each": round(1e3 * v / max(1, self.n[k]), 4)} for k, v in sorted(self.t.items())}}
+
+    def dump(self) -> None:
+        if self.on:
+            import json
+            with open(self.path, "w") as f:
+                json.dump(self.summary(), f)
+
+
+def _profile_from_env() -> StageProfile:
+    import os
+    return StageProfile(os.environ.get("TCA_SERVER_PROFILE") or None)
+
+
+PROFILE = _profile_from_env()
+
+
+class _Pending:
+    __slots__ = ("inputs", "requested", "encode", "out_dst", "done", "result", "exc")
+
+    def __init__(self, inputs, requested, encode, out_dst=None):
+        self.inputs, self.requested, self.encode, self.out_dst = inputs, requested, encode, out_dst
         self.done = threading.Event()
         self.result = None
         self.exc: Optional[BaseException] = None
@@ -124,8 +164,8 @@ class DynamicBatcher:
         self.thread = threading.Thread(target=self._run, name=f"batcher-{model.name}", daemon=True)
         self.thread.start()
 
-    def submit(self, inputs, requested, encode):
-        item = _Pending(inputs, requested, encode)
+    def submit(self, inputs, requested, encode, out_dst=None):
+        item = _Pending(inputs, requested, encode, out_dst)
         with self.cv:
             if self.stopped:
                 raise InferError(f"model '{self.model.name}' is unloading")
@@ -167,16 +207,27 @@ class DynamicBatcher:
             m = self.model
             GPU_PHASE.acquire_shared()
             try:
-                self._execute(m, items)
+                with m.stream_context():
+                    self._execute(m, items)
             finally:
                 GPU_PHASE.release_shared()
 
     def _execute(self, m: "ServedModel", items) -> None:
         with m._lock:
             try:
-                outs = m.execute_batch([it.inputs for it in items], items[0].requested)
+                t0 = time.perf_counter()
+                dsts = [it.out_dst for it in items]
+                if m.accepts_out_dst and any(d for d in dsts):
+                    outs = m.execute_batch([it.inputs for it in items], items[0].requested, dsts=dsts)
+                else:
+                    outs = m.execute_batch([it.inputs for it in items], items[0].requested)
+                t1 = time.perf_counter()
                 for it, o in zip(items, outs):
                     self._finish(it, o)
+                if PROFILE.on:
+                    PROFILE.add(f"{m.name}.execute_batch", t1 - t0)
+                    PROFILE.add(f"{m.name}.batch_items", float(len(items)))
+                    PROFILE.add(f"{m.name}.encode_in_batcher", time.perf_counter() - t1, len(items))
             except Exception:
                 for it in items:  # isolate the failing request(s)
                     if it.done.is_set():
@@ -204,6 +255,12 @@ class ServedModel(ABC):
     # a model sets dynamic_batch > 1 in load() once it has an execute_batch
     dynamic_batch = 1
     batch_delay_s = 0.0005
+    # execute_batch(..., dsts=[per request {output: uint8 view of its shared-memory output
+    # slice} or None]) writes outputs there directly (see models._direct_out)
+    accepts_out_dst = False
+    # inputs from a device shared-memory region arrive as torch tensors on the GPU when
+    # the model reads them there (device_inputs), else as host copies
+    device_inputs = False
 
     def __init__(self, name: str, version: str = "1"):
         self.name = name
@@ -213,6 +270,20 @@ class ServedModel(ABC):
         self._config: Optional[mc.ModelConfig] = None
         self._lock = threading.Lock()  # one execution at a time per instance (GPU graph buffers)
         self._batcher: Optional[DynamicBatcher] = None
+        self._stream = None  # a HIP stream of this model's own: two served models overlap on the GPU
+
+    def stream_context(self):
+        """Context running this model's executions on a stream of its own (GPU
+        models; a no-op on the CPU): the batcher threads of two models would
+        otherwise serialise on the default stream."""
+        import contextlib
+        dev = getattr(self, "device", None)
+        if dev is None or getattr(dev, "type", None) != "cuda":
+            return contextlib.nullcontext()
+        import torch
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=dev)
+        return torch.cuda.stream(self._stream)
 
     # ---------------------------------------------------------------- contract
     @abstractmethod
@@ -287,23 +358,29 @@ class ServedModel(ABC):
                 if d != -1 and d != s:
                     raise InferError(f"input '{spec.name}': shape {list(a.shape)} does not match {ref}")
 
-    def __call__(self, inputs: Dict[str, np.ndarray], requested: Sequence[str], encode=None):
+    def __call__(self, inputs: Dict[str, np.ndarray], requested: Sequence[str], encode=None, out_dst=None):
         """Run the model; ``encode(outputs)`` (the response serialiser) runs
         under the model lock too, because GPU models return their reusable
         pinned output staging, which the next request overwrites."""
         t0 = time.perf_counter_ns()
         try:
+            if not self.device_inputs and any(getattr(a, "is_cuda", False) for a in inputs.values()):
+                inputs = {k: (a.cpu().numpy() if getattr(a, "is_cuda", False) else a) for k, a in inputs.items()}
             self.validate(inputs)
             if self.dynamic_batch > 1:
                 if self._batcher is None:
                     with self._lock:
                         if self._batcher is None:
                             self._batcher = DynamicBatcher(self, self.dynamic_batch, self.batch_delay_s)
-                out = self._batcher.submit(inputs, requested, encode)
+                t1 = time.perf_counter_ns()
+                out = self._batcher.submit(inputs, requested, encode, out_dst)
+                if PROFILE.on:
+                    PROFILE.add(f"{self.name}.validate", (t1 - t0) * 1e-9)
+                    PROFILE.add(f"{self.name}.submit_to_done", (time.perf_counter_ns() - t1) * 1e-9)
             else:
                 GPU_PHASE.acquire_shared()
                 try:
-                    with self._lock:
+                    with self._lock, self.stream_context():
                         out = self.execute(inputs, requested)
                         if encode is not None:
                             out = encode(out)

@@ -25,6 +25,7 @@ state_dict is supported for real checkpoints.
 from __future__ import annotations
 
 import json
+import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -32,7 +33,7 @@ import torch
 
 from ..config.lidar import PointPillarsConfig, VoxelConfig
 from ..proto import model_config_pb2 as mc
-from .model import InferError, ServedModel, tensor_spec
+from .model import PROFILE, InferError, ServedModel, tensor_spec
 from ..utils.model_store import load_state_dict
 
 
@@ -60,16 +61,68 @@ def _device(device) -> torch.device:
     return torch.device(device)
 
 
-PLAN_SIZES = (1, 4, 16)  # captured batch sizes per served model; a dynamic batch runs on the smallest >= n
+PLAN_SIZES = (1, 4, 8, 16)  # captured batch sizes per served model; a dynamic batch runs on the smallest >= n
 
 
-def _direct(a: np.ndarray, dtype) -> Optional[torch.Tensor]:
-    """The request tensor itself as a DMA source when it is a contiguous view of
-    a page-locked shared-memory region with the model's dtype (no staging copy)."""
+def _direct(a, dtype) -> Optional[torch.Tensor]:
+    """The request tensor itself as a copy source: a view of a device shared-memory
+    region (a device-to-device copy, any dtype: the copy converts), or a contiguous
+    view of a page-locked system region with the model's dtype (a DMA, no staging copy)."""
+    if isinstance(a, torch.Tensor):
+        return a if a.is_cuda else None
     from .shm import pinned_host
     if a.dtype == np.dtype(dtype) and pinned_host(a):
         return torch.from_numpy(a)
     return None
+
+
+def _direct_out(dst: Optional[Dict[str, np.ndarray]], name: str, staging: torch.Tensor) -> torch.Tensor:
+    """Where one request's output goes from the device: its shared-memory output slice
+    (``dst[name]``, raw bytes) viewed with the staging tensor's dtype and shape when that
+    slice is large enough and page-locked, else the pinned staging."""
+    from .shm import pinned_host
+    d = dst.get(name) if dst else None
+    nb = staging.numel() * staging.element_size()
+    if isinstance(d, torch.Tensor):  # a device region: the output is copied on the device
+        if d.is_cuda and d.numel() >= nb:
+            return d[:nb].view(staging.dtype).view(tuple(staging.shape))
+        return staging
+    if d is not None and d.nbytes >= nb:
+        v = d[:nb]
+        if pinned_host(v):
+            return torch.from_numpy(v.view(staging.numpy().dtype).reshape(tuple(staging.shape)))
+    return staging
+
+
+class _PlanClock:
+    """Served-plan phase clock for the server stage profile (TCA_SERVER_PROFILE):
+    host time of each phase's issue and the device time between HIP events on the
+    plan's stream (H2D, graph replay, D2H).  Inert when profiling is off."""
+
+    def __init__(self, tag: str):
+        from .model import PROFILE
+        self.on, self.tag = PROFILE.on, tag
+        if self.on:
+            self.ev = [(None, torch.cuda.Event(enable_timing=True))]
+            self.ev[0][1].record()
+            self.t = time.perf_counter()
+
+    def mark(self, name: str) -> None:
+        if self.on:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.ev.append((name, e))
+            from .model import PROFILE
+            t = time.perf_counter()
+            PROFILE.add(f"{self.tag}.host.{name}", t - self.t)
+            self.t = t
+
+    def done(self) -> None:
+        if self.on:
+            from .model import PROFILE
+            self.ev[-1][1].synchronize()
+            for (_, a), (name, b) in zip(self.ev[:-1], self.ev[1:]):
+                PROFILE.add(f"{self.tag}.gpu.{name}", a.elapsed_time(b) * 1e-3)
 
 
 def _pick(plans: Dict[int, object], n: int):
@@ -103,7 +156,10 @@ class _YoloPlan:
         self.runner.capture()  # under the repository's exclusive GPU phase, never lazily while serving
         self.pin_out = torch.empty(self.runner.out.shape, dtype=torch.float32).pin_memory()
 
-    def run(self, images: Sequence[np.ndarray]) -> List[Dict[str, torch.Tensor]]:
+    def run(self, images: Sequence[np.ndarray], dsts=None) -> List[Dict[str, torch.Tensor]]:
+        """dsts: per request None or {output name: uint8 view of the request's output
+        shared-memory slice}; a slice inside a page-locked region receives its output
+        by DMA straight from the device (the response encoder then has nothing to copy)."""
         n, img = len(images), self.img
         srcs = [None] * n
 
@@ -113,13 +169,22 @@ class _YoloPlan:
             if srcs[i] is None:
                 np.copyto(self.pin_in[i].numpy(), a, casting="same_kind")
                 srcs[i] = self.pin_in[i]
+        clk = _PlanClock("YOLOv5")
         _stage_parallel(stage, n)
-        for i in range(n):  # slots >= n: stale, outputs unused
-            self.x_dev[i].copy_(srcs[i], non_blocking=True)
+        clk.mark("host_stage")
+        torch._foreach_copy_([self.x_dev[i] for i in range(n)], srcs, non_blocking=True)  # slots >= n: stale
+        clk.mark("h2d")
         dec = self.runner()
-        self.pin_out[:n].copy_(dec[:n].float(), non_blocking=True)
+        clk.mark("graph")
+        outs = [None] * n
+        for i in range(n):
+            outs[i] = _direct_out(dsts[i] if dsts else None, "output", self.pin_out[i:i + 1])
+            outs[i].copy_(dec[i:i + 1], non_blocking=True)
+        clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
-        return [{"output": self.pin_out[i:i + 1]} for i in range(n)]
+        clk.mark("sync")
+        clk.done()
+        return [{"output": o} for o in outs]
 
 
 def check_voxel_inputs(inputs: Dict[str, np.ndarray], P: int, max_voxels: int, grid_size) -> int:
@@ -131,6 +196,7 @@ def check_voxel_inputs(inputs: Dict[str, np.ndarray], P: int, max_voxels: int, g
     Returns V.  Reference contract: ``examples/pointpillar_kitti/config.pbtxt:27-52``
     (voxels [-1, P, 4], voxel_coords [-1, 4] = (b, z, y, x), voxel_num_points [-1])."""
     vox, co, n = inputs["voxels"], inputs["voxel_coords"], inputs["voxel_num_points"]
+    dev = isinstance(co, torch.Tensor)
     if vox.ndim != 3 or vox.shape[1] != P or vox.shape[2] < 4:
         raise InferError(f"voxels must be [-1, {P}, 4], got {list(vox.shape)}")
     V = vox.shape[0]
@@ -142,11 +208,18 @@ def check_voxel_inputs(inputs: Dict[str, np.ndarray], P: int, max_voxels: int, g
         raise InferError(f"voxel_num_points must be [{V}], got {list(n.shape)}")
     if V:
         nx, ny, nz = (int(g) for g in grid_size)
-        z, y, x = co[:, 1], co[:, 2], co[:, 3]
-        if (int(z.min()) < 0 or int(z.max()) >= nz or int(y.min()) < 0 or int(y.max()) >= ny
-                or int(x.min()) < 0 or int(x.max()) >= nx):
+        if dev:  # device shared memory: the reductions on the GPU, one small copy back
+            lo, hi = torch.aminmax(co.to(torch.int64), dim=0)
+            nlo, nhi = torch.aminmax(n.to(torch.int64))
+            v = torch.cat([lo, hi, nlo.view(1), nhi.view(1)]).cpu().tolist()
+            lo, hi, nmin, nmax = v[0:4], v[4:8], v[8], v[9]
+        else:
+            lo, hi = co.min(axis=0), co.max(axis=0)  # (b, z, y, x): two passes, not six
+            nmin, nmax = n.min(), n.max()
+        if (int(lo[1]) < 0 or int(hi[1]) >= nz or int(lo[2]) < 0 or int(hi[2]) >= ny
+                or int(lo[3]) < 0 or int(hi[3]) >= nx):
             raise InferError(f"voxel_coords outside the {nz}x{ny}x{nx} (z, y, x) grid")
-        if int(n.min()) < 1 or int(n.max()) > P:
+        if int(nmin) < 1 or int(nmax) > P:
             raise InferError(f"voxel_num_points must be in [1, {P}]")
     return V
 
@@ -196,8 +269,11 @@ class _PointPillarsPlan:
         def stage(i):
             vox, co, nn_ = batch[i]["voxels"], batch[i]["voxel_coords"], batch[i]["voxel_num_points"]
             V = vox.shape[0]
-            sv = _direct(vox, np.float32) if vox.shape[-1] == 4 else None
-            sc, sn = _direct(co, np.int32), _direct(nn_, np.int32)
+            if isinstance(vox, torch.Tensor) and vox.is_cuda:  # device shared memory: device-to-device
+                sv, sc, sn = vox[..., :4], co, nn_
+            else:
+                sv = _direct(vox, np.float32) if vox.shape[-1] == 4 else None
+                sc, sn = _direct(co, np.int32), _direct(nn_, np.int32)
             if sv is None:
                 np.copyto(self.pin_vox[i, :V].numpy(), vox[..., :4], casting="same_kind")
                 sv = self.pin_vox[i, :V]
@@ -209,21 +285,32 @@ class _PointPillarsPlan:
                 sn = self.pin_n[i, :V]
             srcs[i] = (V, sv, sc, sn)
             self.pin_vcount[i] = V
+            if PROFILE.on:
+                PROFILE.add("PointPillars.staged_inputs", float(sv.data_ptr() == self.pin_vox[i].data_ptr()))
+        clk = _PlanClock("PointPillars")
         _stage_parallel(stage, n)
+        clk.mark("host_stage")
+        dst, src = [self.vcount], [self.pin_vcount]  # slots >= n: no voxels
         for i, (V, sv, sc, sn) in enumerate(srcs):
             if V:
-                self.voxels[i, :V].copy_(sv, non_blocking=True)
-                self.coords[i, :V].copy_(sc, non_blocking=True)
-                self.nump[i, :V].copy_(sn, non_blocking=True)
-        self.vcount.copy_(self.pin_vcount, non_blocking=True)  # slots >= n: no voxels
+                dst += [self.voxels[i, :V], self.coords[i, :V], self.nump[i, :V]]
+                src += [sv, sc, sn]
+        torch._foreach_copy_(dst, src, non_blocking=True)  # one call: no per-copy Python dispatch
+        clk.mark("h2d")
         self.runner()
+        clk.mark("graph")
         for p, t in zip(self.pin_out, self.outs):
             p[:n].copy_(t[:n], non_blocking=True)
+        clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
+        clk.mark("sync")
         cnt, box, score, cls = self.pin_out
-        return [{"pred_boxes": box[i, :k].numpy(), "pred_scores": score[i, :k].numpy(),
-                 "pred_labels": cls[i, :k].numpy().astype(np.int64, copy=False)}
-                for i, k in enumerate(cnt[:n].tolist())]
+        res = [{"pred_boxes": box[i, :k].numpy(), "pred_scores": score[i, :k].numpy(),
+                "pred_labels": cls[i, :k].numpy().astype(np.int64, copy=False)}
+               for i, k in enumerate(cnt[:n].tolist())]
+        clk.mark("result")
+        clk.done()
+        return res
 
 
 class YoloV5Model(ServedModel):
@@ -288,11 +375,14 @@ class YoloV5Model(ServedModel):
         out = yolo_decode_reference(heads, self.model.anchors).numpy()
         return {"output": out.astype(np.float32, copy=False)}
 
+    accepts_out_dst = True
+    device_inputs = True
+
     @torch.no_grad()
-    def execute_batch(self, batch, requested):
+    def execute_batch(self, batch, requested, dsts=None):
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
-        return _pick(self.plans, len(batch)).run([x["images"] for x in batch])
+        return _pick(self.plans, len(batch)).run([x["images"] for x in batch], dsts)
 
 
 class PointPillarsModel(ServedModel):
@@ -357,12 +447,17 @@ class PointPillarsModel(ServedModel):
     def _check(self, inputs):
         return check_voxel_inputs(inputs, self.P, self.cfg.voxel.max_voxels, self.cfg.voxel.grid_size)
 
+    device_inputs = True
+
+    def validate(self, inputs):
+        super().validate(inputs)
+        self._check(inputs)  # in the request thread, off the batcher's critical path
+
     @torch.no_grad()
     def execute_batch(self, batch, requested):
+        """Inputs validated by :meth:`validate` (every request reaches the batcher through it)."""
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
-        for inp in batch:
-            self._check(inp)
         return _pick(self.plans, len(batch)).run(batch)
 
     @torch.no_grad()
@@ -650,8 +745,7 @@ class _DetectronPlan:
                 np.copyto(self.pin_in[i].numpy(), a, casting="same_kind")
                 srcs[i] = self.pin_in[i]
         _stage_parallel(stage, n)
-        for i in range(n):  # slots >= n: stale, outputs unused
-            self.x_dev[i].copy_(srcs[i], non_blocking=True)
+        torch._foreach_copy_([self.x_dev[i] for i in range(n)], srcs, non_blocking=True)  # slots >= n: stale
         self.runner()
         for p, t in zip(self.pin_out, self.outs):
             p[:n].copy_(t[:n], non_blocking=True)

@@ -1,6 +1,9 @@
 """KServe-v2 system shared-memory extension (Triton's ``SystemSharedMemory*``
 RPCs and the ``shared_memory_region`` / ``shared_memory_offset`` /
-``shared_memory_byte_size`` tensor parameters).
+``shared_memory_byte_size`` tensor parameters), and its device twin (Triton's
+``CudaSharedMemory*`` RPCs): a client's GPU allocation, shared by a HIP IPC
+memory handle, that the request's inputs are read from and its outputs
+written into on the device (``utils/hip_ipc.py``).
 
 A client on the same host registers a POSIX shared-memory object
 (``/dev/shm/<key>``) as a named region; an inference request then names a
@@ -53,15 +56,26 @@ class Region:
     key: str
     offset: int
     byte_size: int
-    mm: mmap.mmap
+    mm: Optional[mmap.mmap]
     pinned: bool = False
+    dev: Optional[object] = None  # device region: utils.hip_ipc.OpenedHandle
+    device_id: int = 0
 
-    def view(self, offset: int, nbytes: int, dtype, shape) -> np.ndarray:
+    @property
+    def device(self) -> bool:
+        return self.dev is not None
+
+    def view(self, offset: int, nbytes: int, dtype, shape):
+        """ndarray view of a system region; for a device region a torch tensor on its GPU."""
         if offset < 0 or nbytes < 0 or offset + nbytes > self.byte_size:
             raise InferError(f"shared memory region '{self.name}': [{offset}, {offset + nbytes}) outside "
                              f"its {self.byte_size} bytes")
         dt = np.dtype(dtype)
         count = nbytes // dt.itemsize
+        if self.dev is not None:
+            import torch
+            tdt = torch.from_numpy(np.empty(0, dt)).dtype
+            return self.dev.tensor[offset:offset + count * dt.itemsize].view(tdt).reshape(shape)
         a = np.frombuffer(self.mm, dtype=dt, count=count, offset=self.offset + offset)
         return a.reshape(shape)
 
@@ -132,9 +146,32 @@ class SharedMemoryRegistry:
             self._regions[name] = r
         return r
 
-    def unregister(self, name: str = "") -> None:
+    def register_device(self, name: str, raw_handle: bytes, device_id: int, byte_size: int) -> Region:
+        """Map a client's device allocation (HIP IPC handle, Triton's CudaSharedMemoryRegister)."""
+        if not name:
+            raise InferError("shared memory region needs a name")
         with self._lock:
-            names = [name] if name else list(self._regions)
+            if name in self._regions:
+                raise InferError(f"shared memory region '{name}' already registered")
+        if byte_size <= 0:
+            raise InferError(f"device shared memory region '{name}': byte_size {byte_size}")
+        try:
+            from ..utils.hip_ipc import OpenedHandle
+            h = OpenedHandle(raw_handle, byte_size, device_id)
+        except Exception as e:  # noqa: BLE001 - a bad handle / no GPU is the client's error
+            raise InferError(f"unable to open device shared memory handle for '{name}': {e}") from e
+        r = Region(name, "", 0, int(byte_size), None, dev=h, device_id=int(device_id))
+        with self._lock:
+            if name in self._regions:
+                h.close()
+                raise InferError(f"shared memory region '{name}' already registered")
+            self._regions[name] = r
+        return r
+
+    def unregister(self, name: str = "", device: Optional[bool] = None) -> None:
+        """Unregister ``name`` (or every region of the kind: device True / system False / both None)."""
+        with self._lock:
+            names = [name] if name else [n for n, r in self._regions.items() if device is None or r.device == device]
             regs = [self._regions.pop(n) for n in names if n in self._regions]
         if not regs:
             return
@@ -147,6 +184,10 @@ class SharedMemoryRegistry:
         GPU_PHASE.acquire_exclusive()
         try:
             for r in regs:
+                if r.dev is not None:
+                    import torch
+                    torch.cuda.synchronize(r.dev.device)  # no copy from / into it still queued
+                    r.dev.close()
                 if r.pinned:
                     with _PINNED_LOCK:
                         _PINNED.pop(_base(r.mm), None)
@@ -155,6 +196,8 @@ class SharedMemoryRegistry:
         finally:
             GPU_PHASE.release_exclusive()
         for r in regs:
+            if r.mm is None:
+                continue
             try:
                 r.mm.close()
             except BufferError:  # a response still references it: the mapping goes with the last view
@@ -167,11 +210,11 @@ class SharedMemoryRegistry:
             raise InferError(f"unable to find shared memory region '{name}'")
         return r
 
-    def status(self, name: str = ""):
+    def status(self, name: str = "", device: bool = False):
         with self._lock:
-            if name and name not in self._regions:
+            if name and (name not in self._regions or self._regions[name].device != device):
                 raise InferError(f"unable to find shared memory region '{name}'")
-            return [r for n, r in self._regions.items() if not name or n == name]
+            return [r for n, r in self._regions.items() if (not name or n == name) and r.device == device]
 
 
 def tensor_shm(params) -> Optional[tuple]:
