@@ -320,3 +320,22 @@ def test_second_iou_served_over_kserve():
     from triton_client_amd.cli.engines import lidar_family
     assert [lidar_family(n) for n in ("second_iou", "pointpillar_kitti", "centerpoint_pp")] == [
         "second_iou", "pointpillars", "centerpoint"]
+
+
+def test_check_voxel_inputs_rejects_out_of_range_cells():
+    """Host-side validation of served voxel inputs (the GPU consumers index the canvas
+    with these coordinates): cells outside the grid and counts outside [1, P] are refused."""
+    from triton_client_amd.server.model import InferError
+    from triton_client_amd.server.models import check_voxel_inputs
+
+    V, P = 5, 32
+    grid = (432, 496, 1)
+    ok = {"voxels": np.zeros((V, P, 4), np.float32), "voxel_coords": np.zeros((V, 4), np.int32),
+          "voxel_num_points": np.ones((V,), np.int32)}
+    assert check_voxel_inputs(ok, P, 100, grid) == V
+    for key, idx, val in (("voxel_coords", (2, 3), 432), ("voxel_coords", (1, 2), -1), ("voxel_coords", (0, 1), 1),
+                          ("voxel_num_points", (3,), 0), ("voxel_num_points", (4,), P + 1)):
+        bad = {k: v.copy() for k, v in ok.items()}
+        bad[key][idx] = val
+        with pytest.raises(InferError):
+            check_voxel_inputs(bad, P, 100, grid)

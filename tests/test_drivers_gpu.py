@@ -145,6 +145,17 @@ def test_served_dynamic_batch_matches_single_requests(cuda):
         assert na > 0 and abs(na - nb) <= max(2, na // 50), (na, nb)
         np.testing.assert_allclose(np.sort(a["pred_scores"])[-20:], np.sort(b["pred_scores"])[-20:], rtol=1e-4,
                                    atol=1e-5)
+    # the device range check inside the plan (tca_voxel_check): a request with a cell outside
+    # the grid (reaching execute_batch unvalidated) gets its error, its neighbours their boxes
+    bad = {k: v.copy() for k, v in reqs[1].items()}
+    bad["voxel_coords"][7, 3] = int(s3.cfg.voxel.grid_size[0]) + 5
+    mixed = s3.execute_batch([reqs[0], bad, reqs[2]], [])
+    from triton_client_amd.server.model import InferError
+    assert isinstance(mixed[1], InferError) and not isinstance(mixed[0], Exception)
+    for a, b in ((single3[0], mixed[0]), (single3[2], mixed[2])):
+        assert abs(len(a["pred_scores"]) - len(b["pred_scores"])) <= max(2, len(a["pred_scores"]) // 50)
+    with pytest.raises(InferError):
+        s3.execute(bad, [])
 
 
 def test_served_shared_memory_matches_raw_wire(cuda):

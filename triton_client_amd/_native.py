@@ -56,6 +56,10 @@ _KERNEL_SIGS = {
     "tca_conv_hx3p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, I, P],
     # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, res, ldr, r_off, occ, tile, stream
     "tca_conv_hx3s2p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, P, I, P],
+    # n, dst[], src[], nbytes[], stream (csrc/kernels/copy.hip)
+    "tca_copy_segments": [I, P, P, P, P],
+    # coords, nump, vcount, B, V, P, nz, ny, nx, flags, stream
+    "tca_voxel_check": [P, P, P, I, I, I, I, I, I, P, P],
     # cur, cs, cur_n, B, maxp, R, ring, ring_n, ring_t, ring_pose, head, clock, pose, dt, out, out_n, stream
     "tca_sweep_step": [P, I, P, I, I, I, P, P, P, P, P, P, P, F, P, P, P],
     # src, B, H, W, dst, dst_dtype, dst_layout, sc0, sc1, sc2, b0, b1, b2, stream

@@ -223,7 +223,11 @@ class DynamicBatcher:
                     outs = m.execute_batch([it.inputs for it in items], items[0].requested)
                 t1 = time.perf_counter()
                 for it, o in zip(items, outs):
-                    self._finish(it, o)
+                    if isinstance(o, BaseException):  # this request failed inside the batch (e.g. bad values)
+                        it.exc = o
+                        it.done.set()
+                    else:
+                        self._finish(it, o)
                 if PROFILE.on:
                     PROFILE.add(f"{m.name}.execute_batch", t1 - t0)
                     PROFILE.add(f"{m.name}.batch_items", float(len(items)))

@@ -94,6 +94,31 @@ def _direct_out(dst: Optional[Dict[str, np.ndarray]], name: str, staging: torch.
     return staging
 
 
+def _copy_all(dsts: Sequence[torch.Tensor], srcs: Sequence[torch.Tensor]) -> None:
+    """dst[i] <- src[i] on the current stream: device-to-device pairs of one dtype and
+    contiguous layout as ONE launch of the segment-copy kernel (csrc/kernels/copy.hip;
+    an IPC-mapped slot would otherwise take the runtime's peer-copy path), the rest
+    (host sources, dtype conversions, strided views) by one torch foreach call."""
+    seg_d, seg_s, seg_n, rest_d, rest_s = [], [], [], [], []
+    for d, s_ in zip(dsts, srcs):
+        if (d.is_cuda and s_.is_cuda and d.dtype == s_.dtype and d.numel() == s_.numel()
+                and d.is_contiguous() and s_.is_contiguous()):
+            if d.numel():
+                seg_d.append(d.data_ptr())
+                seg_s.append(s_.data_ptr())
+                seg_n.append(d.numel() * d.element_size())
+        else:
+            rest_d.append(d)
+            rest_s.append(s_.view(d.shape) if s_.numel() == d.numel() and s_.shape != d.shape else s_)
+    if seg_d:
+        from .. import _native
+        dp, sp, nb = (np.asarray(v, np.int64) for v in (seg_d, seg_s, seg_n))
+        _native.call("tca_copy_segments", len(seg_d), dp.ctypes.data, sp.ctypes.data, nb.ctypes.data,
+                     _native.stream_ptr(torch.cuda.current_stream()))
+    if rest_d:
+        torch._foreach_copy_(rest_d, rest_s, non_blocking=True)
+
+
 class _PlanClock:
     """Served-plan phase clock for the server stage profile (TCA_SERVER_PROFILE):
     host time of each phase's issue and the device time between HIP events on the
@@ -172,19 +197,32 @@ class _YoloPlan:
         clk = _PlanClock("YOLOv5")
         _stage_parallel(stage, n)
         clk.mark("host_stage")
-        torch._foreach_copy_([self.x_dev[i] for i in range(n)], srcs, non_blocking=True)  # slots >= n: stale
+        _copy_all([self.x_dev[i] for i in range(n)], srcs)  # slots >= n: stale
         clk.mark("h2d")
         dec = self.runner()
         clk.mark("graph")
-        outs = [None] * n
-        for i in range(n):
-            outs[i] = _direct_out(dsts[i] if dsts else None, "output", self.pin_out[i:i + 1])
-            outs[i].copy_(dec[i:i + 1], non_blocking=True)
+        outs = [_direct_out(dsts[i] if dsts else None, "output", self.pin_out[i:i + 1]) for i in range(n)]
+        _copy_all(outs, [dec[i:i + 1] for i in range(n)])
         clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
         clk.mark("sync")
         clk.done()
         return [{"output": o} for o in outs]
+
+
+def check_voxel_shapes(inputs, P: int, max_voxels: int) -> int:
+    """The shape part of :func:`check_voxel_inputs` (no value reads) → V."""
+    vox, co, n = inputs["voxels"], inputs["voxel_coords"], inputs["voxel_num_points"]
+    if vox.ndim != 3 or vox.shape[1] != P or vox.shape[2] < 4:
+        raise InferError(f"voxels must be [-1, {P}, 4], got {list(vox.shape)}")
+    V = vox.shape[0]
+    if V > max_voxels:
+        raise InferError(f"{V} voxels > max_voxels {max_voxels}")
+    if co.ndim != 2 or co.shape[0] != V or co.shape[1] != 4:
+        raise InferError(f"voxel_coords must be [{V}, 4], got {list(co.shape)}")
+    if n.ndim != 1 or n.shape[0] != V:
+        raise InferError(f"voxel_num_points must be [{V}], got {list(n.shape)}")
+    return V
 
 
 def check_voxel_inputs(inputs: Dict[str, np.ndarray], P: int, max_voxels: int, grid_size) -> int:
@@ -246,6 +284,9 @@ class _PointPillarsPlan:
         self.pin_vox = torch.empty((B, V, P, 4), dtype=torch.float32).pin_memory()
         self.pin_co = torch.empty((B, V, 4), dtype=torch.int32).pin_memory()
         self.pin_n = torch.empty((B, V), dtype=torch.int32).pin_memory()
+        self.flags = torch.zeros((B,), dtype=torch.int32, device=device)  # per slot: coordinates out of range
+        self.pin_flags = torch.zeros((B,), dtype=torch.int32).pin_memory()
+        self.grid = tuple(int(g) for g in cfg.voxel.grid_size)  # nx, ny, nz
         self.enc.clear(self.pipe.vox)
         fast = self.pipe.fast or self.pipe.build_fast()  # sets the canvas storage first
 
@@ -295,17 +336,28 @@ class _PointPillarsPlan:
             if V:
                 dst += [self.voxels[i, :V], self.coords[i, :V], self.nump[i, :V]]
                 src += [sv, sc, sn]
-        torch._foreach_copy_(dst, src, non_blocking=True)  # one call: no per-copy Python dispatch
+        _copy_all(dst, src)  # one launch for the device-resident ones, no per-copy Python dispatch
+        # range check on the device (whatever the transport): a bad slot's voxel count is zeroed
+        # before the graph reads it, and the request is answered with an error below
+        from .. import _native
+        nx, ny, nz = self.grid
+        _native.call("tca_voxel_check", _native.ptr(self.coords), _native.ptr(self.nump), _native.ptr(self.vcount),
+                     n, self.V, self.P, nz, ny, nx, _native.ptr(self.flags),
+                     _native.stream_ptr(torch.cuda.current_stream()))
         clk.mark("h2d")
         self.runner()
         clk.mark("graph")
         for p, t in zip(self.pin_out, self.outs):
             p[:n].copy_(t[:n], non_blocking=True)
+        self.pin_flags[:n].copy_(self.flags[:n], non_blocking=True)
         clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
         clk.mark("sync")
         cnt, box, score, cls = self.pin_out
-        res = [{"pred_boxes": box[i, :k].numpy(), "pred_scores": score[i, :k].numpy(),
+        bad = self.pin_flags[:n].tolist()
+        res = [InferError(f"voxel_coords outside the {self.grid[2]}x{self.grid[1]}x{self.grid[0]} (z, y, x) grid "
+                          f"or voxel_num_points outside [1, {self.P}]") if bad[i] else
+               {"pred_boxes": box[i, :k].numpy(), "pred_scores": score[i, :k].numpy(),
                 "pred_labels": cls[i, :k].numpy().astype(np.int64, copy=False)}
                for i, k in enumerate(cnt[:n].tolist())]
         clk.mark("result")
@@ -451,14 +503,20 @@ class PointPillarsModel(ServedModel):
 
     def validate(self, inputs):
         super().validate(inputs)
-        self._check(inputs)  # in the request thread, off the batcher's critical path
+        if isinstance(inputs.get("voxel_coords"), torch.Tensor):
+            check_voxel_shapes(inputs, self.P, self.cfg.voxel.max_voxels)  # values: once per batch, on the GPU
+        else:
+            self._check(inputs)  # in the request thread, off the batcher's critical path
 
     @torch.no_grad()
     def execute_batch(self, batch, requested):
-        """Inputs validated by :meth:`validate` (every request reaches the batcher through it)."""
+        """Host inputs validated by :meth:`validate` (every request reaches the batcher
+        through it); every slot's coordinate / count ranges are checked again on the device
+        inside the plan (csrc/kernels/copy.hip tca_voxel_check), which is the check for
+        device shared-memory inputs."""
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
-        return _pick(self.plans, len(batch)).run(batch)
+        return _pick(self.plans, len(batch)).run(batch)  # an out-of-range request's entry is its InferError
 
     @torch.no_grad()
     def execute(self, inputs, requested):
@@ -467,7 +525,10 @@ class PointPillarsModel(ServedModel):
         n = inputs["voxel_num_points"]
         self._check(inputs)
         if self.device.type == "cuda":
-            return self.plans[1].run([inputs])[0]
+            r = self.plans[1].run([inputs])[0]
+            if isinstance(r, BaseException):
+                raise r
+            return r
         else:
             from ..models.pointpillars import pillar_point_features, scatter_to_bev
             from ..ops.lidar import AnchorPostprocess
@@ -745,7 +806,7 @@ class _DetectronPlan:
                 np.copyto(self.pin_in[i].numpy(), a, casting="same_kind")
                 srcs[i] = self.pin_in[i]
         _stage_parallel(stage, n)
-        torch._foreach_copy_([self.x_dev[i] for i in range(n)], srcs, non_blocking=True)  # slots >= n: stale
+        _copy_all([self.x_dev[i] for i in range(n)], srcs)  # slots >= n: stale
         self.runner()
         for p, t in zip(self.pin_out, self.outs):
             p[:n].copy_(t[:n], non_blocking=True)

@@ -60,6 +60,7 @@ class Region:
     pinned: bool = False
     dev: Optional[object] = None  # device region: utils.hip_ipc.OpenedHandle
     device_id: int = 0
+    _views: Optional[dict] = None
 
     @property
     def device(self) -> bool:
@@ -72,10 +73,18 @@ class Region:
                              f"its {self.byte_size} bytes")
         dt = np.dtype(dtype)
         count = nbytes // dt.itemsize
-        if self.dev is not None:
-            import torch
-            tdt = torch.from_numpy(np.empty(0, dt)).dtype
-            return self.dev.tensor[offset:offset + count * dt.itemsize].view(tdt).reshape(shape)
+        if self.dev is not None:  # cached: clients reuse a few slots, and torch views cost a dispatch each
+            key = (offset, nbytes, dt.str, tuple(shape))
+            v = self._views.get(key) if self._views is not None else None
+            if v is None:
+                import torch
+                tdt = torch.from_numpy(np.empty(0, dt)).dtype
+                v = self.dev.tensor[offset:offset + count * dt.itemsize].view(tdt).reshape(shape)
+                if self._views is None:
+                    self._views = {}
+                if len(self._views) < 4096:
+                    self._views[key] = v
+            return v
         a = np.frombuffer(self.mm, dtype=dt, count=count, offset=self.offset + offset)
         return a.reshape(shape)
 
@@ -187,6 +196,7 @@ class SharedMemoryRegistry:
                 if r.dev is not None:
                     import torch
                     torch.cuda.synchronize(r.dev.device)  # no copy from / into it still queued
+                    r._views = None
                     r.dev.close()
                 if r.pinned:
                     with _PINNED_LOCK:

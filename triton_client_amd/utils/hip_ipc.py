@@ -98,7 +98,7 @@ class DeviceAllocation:
         except Exception:
             hip.hipFree(ctypes.c_void_p(self.ptr))
             raise
-        self.handle = bytes(h.reserved)
+        self.handle = bytes(h)  # all 64 bytes (h.reserved would stop at the first NUL)
         self.tensor = device_tensor(self.ptr, self.nbytes, self.device)
 
     def close(self) -> None:
@@ -120,7 +120,7 @@ class OpenedHandle:
         hip = _hip()
         _check(hip.hipSetDevice(self.device_id), "hipSetDevice")
         h = _Handle()
-        ctypes.memmove(h.reserved, raw_handle, HANDLE_BYTES)
+        ctypes.memmove(ctypes.addressof(h), raw_handle, HANDLE_BYTES)
         p = ctypes.c_void_p()
         _check(hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _LAZY_PEER_ACCESS), "hipIpcOpenMemHandle")
         self.ptr = int(p.value)
