@@ -270,12 +270,32 @@ def multi_proc(a) -> int:
             line = c.stdout.readline()
             if line.strip() != "READY":
                 raise RuntimeError(f"client failed before READY: {line!r} (server exit code {server.poll()})")
+        import psutil
+
+        procs = [psutil.Process(server.pid)] + [psutil.Process(c.pid) for c in clients]
+
+        def cpu_s():  # user + system seconds of the server (and its children) and the clients
+            tot = 0.0
+            for p in procs:
+                try:
+                    for q in [p] + p.children(recursive=True):
+                        t = q.cpu_times()
+                        tot += t.user + t.system
+                except psutil.NoSuchProcess:
+                    pass
+            return tot
+        c0 = cpu_s()
         t0 = time.perf_counter()
         for c in clients:
             c.stdin.write("GO\n")
             c.stdin.flush()
         outs = [json.loads(c.stdout.readline()) for c in clients]
         wall = time.perf_counter() - t0
+        cpu_cores = (cpu_s() - c0) / wall
+        try:
+            cpu_avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            cpu_avail = os.cpu_count()
         for c in clients:
             if c.wait(60) != 0:
                 raise RuntimeError("a client process failed")
@@ -305,6 +325,7 @@ def multi_proc(a) -> int:
             "client_ms_per_frame": {"camera": mean_ms("camera"), "lidar": mean_ms("lidar")},
             "client_wall_s": {o["role"] + str(i // 2): round(o["wall_s"], 3) for i, o in enumerate(outs)},
             "server_requests_per_execution": rpe,
+            "host_cpu_cores_busy": round(cpu_cores, 2), "host_cpus_in_affinity": cpu_avail,
             "topology": (f"{a.server_procs} server process{'es' if a.server_procs > 1 else ''} + {a.client_procs} camera "
                          f"and {a.client_procs} LiDAR client processes"),
             "wire": a.wire, "window_mode": "burst" if a.burst else "sliding",

@@ -425,11 +425,14 @@ def _handlers(servicer: GRPCInferenceServicer, raw_infer: bool = True):
 class KServeServer:
     def __init__(self, repo: ModelRepository, address: str = "127.0.0.1:8001", max_workers: int = 8,
                  max_message_bytes: int = 512 << 20, fault: Optional[FaultInjector] = None,
-                 metrics_port: Optional[int] = None, raw_infer: bool = True, switch_interval_s: float = 2e-4):
+                 metrics_port: Optional[int] = None, raw_infer: bool = True, switch_interval_s: Optional[float] = None):
         """raw_infer: serve ModelInfer through the C++ codec on the wire bytes
         (False: the protobuf runtime, as a Triton-like reference path)."""
         self.repo = repo
         self.address = address
+        if switch_interval_s is None:
+            import os
+            switch_interval_s = float(os.environ.get("TCA_GIL_SWITCH_S", "2e-4"))
         self.switch_interval_s = switch_interval_s
         metrics = None
         if metrics_port is not None:

@@ -40,12 +40,13 @@ from ..utils.model_store import load_state_dict
 _STAGE_POOL = None
 
 
-def _stage_parallel(fn, n: int) -> None:
+def _stage_parallel(fn, n: int, inline: bool = False) -> None:
     """Run fn(0..n-1) on a small shared thread pool: the per-request copies of a
     dynamic batch into pinned staging (numpy releases the GIL inside copyto, so
-    the host memcpys of several multi-MB requests overlap)."""
+    the host memcpys of several multi-MB requests overlap).  inline: no host
+    copies to overlap (device or page-locked sources), run in this thread."""
     global _STAGE_POOL
-    if n <= 1:
+    if n <= 1 or inline:
         for i in range(n):
             fn(i)
         return
@@ -119,6 +120,55 @@ def _copy_all(dsts: Sequence[torch.Tensor], srcs: Sequence[torch.Tensor]) -> Non
         torch._foreach_copy_(rest_d, rest_s, non_blocking=True)
 
 
+class _Segs:
+    """Device-to-device copy segments gathered from raw pointers and issued as ONE
+    launch (csrc/kernels/copy.hip): the served plans' per-request copies cost no
+    torch op each (every torch op drops and re-takes the GIL, which the server's
+    request threads contend for)."""
+    __slots__ = ("d", "s", "n")
+
+    def __init__(self):
+        self.d, self.s, self.n = [], [], []
+
+    def add(self, dst: int, src: int, nbytes: int) -> None:
+        if nbytes > 0:
+            self.d.append(dst)
+            self.s.append(src)
+            self.n.append(nbytes)
+
+    def launch(self) -> None:
+        if self.d:
+            from .. import _native
+            dp, sp, nb = (np.asarray(v, np.int64) for v in (self.d, self.s, self.n))
+            _native.call("tca_copy_segments", len(self.d), dp.ctypes.data, sp.ctypes.data, nb.ctypes.data,
+                         _native.stream_ptr(torch.cuda.current_stream()))
+
+
+def _dev_src(a, dtype: torch.dtype, nbytes: int) -> Optional[int]:
+    """Pointer of a device-resident request tensor usable as a raw copy source
+    (dtype, contiguity and size as the plan's slot), else None."""
+    if (isinstance(a, torch.Tensor) and a.is_cuda and a.dtype == dtype and a.is_contiguous()
+            and a.numel() * a.element_size() == nbytes):
+        return a.data_ptr()
+    return None
+
+
+_OUT_VIEWS: Dict[tuple, torch.Tensor] = {}
+
+
+def _typed_out(d: torch.Tensor, staging: torch.Tensor) -> torch.Tensor:
+    """A device output slot (uint8 view of a device region) as staging's dtype / shape, cached."""
+    key = (d.data_ptr(), d.numel(), staging.dtype, tuple(staging.shape))
+    v = _OUT_VIEWS.get(key)
+    if v is None:
+        nb = staging.numel() * staging.element_size()
+        v = d[:nb].view(staging.dtype).view(tuple(staging.shape))
+        if len(_OUT_VIEWS) > 4096:
+            _OUT_VIEWS.clear()
+        _OUT_VIEWS[key] = v
+    return v
+
+
 class _PlanClock:
     """Served-plan phase clock for the server stage profile (TCA_SERVER_PROFILE):
     host time of each phase's issue and the device time between HIP events on the
@@ -180,29 +230,59 @@ class _YoloPlan:
         self.runner = GraphRunner(step)
         self.runner.capture()  # under the repository's exclusive GPU phase, never lazily while serving
         self.pin_out = torch.empty(self.runner.out.shape, dtype=torch.float32).pin_memory()
+        # static per-slot views and pointers: the run loop issues no torch op per request
+        self.x_slots = [self.x_dev[i] for i in range(B)]
+        self.pin_slots = [self.pin_out[i:i + 1] for i in range(B)]
+        self.dec_slots = [self.runner.out[i:i + 1] for i in range(B)]
+        self.x_bytes = 3 * img * img * 4
+        self.o_bytes = self.pin_slots[0].numel() * 4
+        self.dec_f32 = self.runner.out.dtype == torch.float32
 
     def run(self, images: Sequence[np.ndarray], dsts=None) -> List[Dict[str, torch.Tensor]]:
         """dsts: per request None or {output name: uint8 view of the request's output
         shared-memory slice}; a slice inside a page-locked region receives its output
-        by DMA straight from the device (the response encoder then has nothing to copy)."""
+        by DMA straight from the device, a device region (device shared memory) by the
+        segment-copy kernel (the response encoder then has nothing to copy)."""
         n, img = len(images), self.img
-        srcs = [None] * n
+        clk = _PlanClock("YOLOv5")
+        segs, host = _Segs(), []
+        xb = self.x_dev.data_ptr()
+        for i, a in enumerate(images):
+            p = _dev_src(a, torch.float32, self.x_bytes)
+            if p is None:
+                host.append(i)
+            else:
+                segs.add(xb + i * self.x_bytes, p, self.x_bytes)
+        srcs = {}
 
         def stage(i):
             a = images[i].reshape(3, img, img)
-            srcs[i] = _direct(a, np.float32)
-            if srcs[i] is None:
+            src = _direct(a, np.float32)
+            if src is None:
                 np.copyto(self.pin_in[i].numpy(), a, casting="same_kind")
-                srcs[i] = self.pin_in[i]
-        clk = _PlanClock("YOLOv5")
-        _stage_parallel(stage, n)
+                src = self.pin_in[i]
+            srcs[i] = src
+        _stage_parallel(lambda k: stage(host[k]), len(host))
         clk.mark("host_stage")
-        _copy_all([self.x_dev[i] for i in range(n)], srcs)  # slots >= n: stale
+        segs.launch()  # slots >= n: stale, outputs unused
+        if host:
+            _copy_all([self.x_slots[i] for i in host], [srcs[i] for i in host])
         clk.mark("h2d")
-        dec = self.runner()
+        self.runner()
         clk.mark("graph")
-        outs = [_direct_out(dsts[i] if dsts else None, "output", self.pin_out[i:i + 1]) for i in range(n)]
-        _copy_all(outs, [dec[i:i + 1] for i in range(n)])
+        outs, segs, rest = [None] * n, _Segs(), []
+        ob = self.runner.out.data_ptr()
+        for i in range(n):
+            d = dsts[i].get("output") if dsts and dsts[i] else None
+            if isinstance(d, torch.Tensor) and d.is_cuda and self.dec_f32 and d.numel() >= self.o_bytes:
+                outs[i] = _typed_out(d, self.pin_slots[i])
+                segs.add(outs[i].data_ptr(), ob + i * self.o_bytes, self.o_bytes)
+            else:
+                outs[i] = _direct_out(dsts[i] if dsts else None, "output", self.pin_slots[i])
+                rest.append(i)
+        segs.launch()
+        if rest:
+            _copy_all([outs[i] for i in rest], [self.dec_slots[i] for i in rest])
         clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
         clk.mark("sync")
@@ -301,10 +381,35 @@ class _PointPillarsPlan:
         r = self.runner.out
         self.outs = (r.count, r.box, r.score, r.cls)
         self.pin_out = [torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in self.outs]
+        # numpy views / raw slot strides: the run loop issues no torch op per request
+        self.pin_np = [t.numpy() for t in self.pin_out]
+        self.pin_vcount_np, self.pin_flags_np = self.pin_vcount.numpy(), self.pin_flags.numpy()
+        self.d2h_src, self.d2h_dst = list(self.outs) + [self.flags], list(self.pin_out) + [self.pin_flags]
+        self.vox_stride, self.co_stride, self.n_stride = V * P * 16, V * 16, V * 4
+
+    def _device_slot(self, i: int, x, segs: "_Segs") -> bool:
+        """Slot i's D2D copies when the request's tensors are device-resident (device shared
+        memory) in the plan's dtypes and layouts."""
+        vox, co, nn_ = x["voxels"], x["voxel_coords"], x["voxel_num_points"]
+        if not (isinstance(vox, torch.Tensor) and vox.is_cuda and vox.dim() == 3 and vox.shape[2] == 4):
+            return False
+        V = vox.shape[0]
+        pv = _dev_src(vox, torch.float32, V * self.P * 16)
+        pc = _dev_src(co, torch.int32, V * 16)
+        pn = _dev_src(nn_, torch.int32, V * 4)
+        if pv is None or pc is None or pn is None:
+            return False
+        segs.add(self.voxels.data_ptr() + i * self.vox_stride, pv, V * self.P * 16)
+        segs.add(self.coords.data_ptr() + i * self.co_stride, pc, V * 16)
+        segs.add(self.nump.data_ptr() + i * self.n_stride, pn, V * 4)
+        self.pin_vcount_np[i] = V
+        return True
 
     def run(self, batch: Sequence[Dict[str, np.ndarray]]) -> List[Dict[str, np.ndarray]]:
         n = len(batch)
-        self.pin_vcount.zero_()
+        self.pin_vcount_np[:] = 0
+        segs = _Segs()
+        host = [i for i in range(n) if not self._device_slot(i, batch[i], segs)]
         srcs = [None] * n
 
         def stage(i):
@@ -325,18 +430,18 @@ class _PointPillarsPlan:
                 np.copyto(self.pin_n[i, :V].numpy(), nn_, casting="unsafe")
                 sn = self.pin_n[i, :V]
             srcs[i] = (V, sv, sc, sn)
-            self.pin_vcount[i] = V
-            if PROFILE.on:
-                PROFILE.add("PointPillars.staged_inputs", float(sv.data_ptr() == self.pin_vox[i].data_ptr()))
+            self.pin_vcount_np[i] = V
         clk = _PlanClock("PointPillars")
-        _stage_parallel(stage, n)
+        _stage_parallel(lambda k: stage(host[k]), len(host))
         clk.mark("host_stage")
+        segs.launch()
         dst, src = [self.vcount], [self.pin_vcount]  # slots >= n: no voxels
-        for i, (V, sv, sc, sn) in enumerate(srcs):
+        for i in host:
+            V, sv, sc, sn = srcs[i]
             if V:
                 dst += [self.voxels[i, :V], self.coords[i, :V], self.nump[i, :V]]
                 src += [sv, sc, sn]
-        _copy_all(dst, src)  # one launch for the device-resident ones, no per-copy Python dispatch
+        _copy_all(dst, src)
         # range check on the device (whatever the transport): a bad slot's voxel count is zeroed
         # before the graph reads it, and the request is answered with an error below
         from .. import _native
@@ -347,18 +452,16 @@ class _PointPillarsPlan:
         clk.mark("h2d")
         self.runner()
         clk.mark("graph")
-        for p, t in zip(self.pin_out, self.outs):
-            p[:n].copy_(t[:n], non_blocking=True)
-        self.pin_flags[:n].copy_(self.flags[:n], non_blocking=True)
+        torch._foreach_copy_(self.d2h_dst, self.d2h_src, non_blocking=True)  # all B slots: one call
         clk.mark("d2h")
         torch.cuda.current_stream().synchronize()
         clk.mark("sync")
-        cnt, box, score, cls = self.pin_out
-        bad = self.pin_flags[:n].tolist()
+        cnt, box, score, cls = self.pin_np
+        bad = self.pin_flags_np
         res = [InferError(f"voxel_coords outside the {self.grid[2]}x{self.grid[1]}x{self.grid[0]} (z, y, x) grid "
                           f"or voxel_num_points outside [1, {self.P}]") if bad[i] else
-               {"pred_boxes": box[i, :k].numpy(), "pred_scores": score[i, :k].numpy(),
-                "pred_labels": cls[i, :k].numpy().astype(np.int64, copy=False)}
+               {"pred_boxes": box[i, :k], "pred_scores": score[i, :k],
+                "pred_labels": cls[i, :k].astype(np.int64, copy=False)}
                for i, k in enumerate(cnt[:n].tolist())]
         clk.mark("result")
         clk.done()
