@@ -50,8 +50,27 @@ class _Buffers:
         return sum(t.numel() * t.element_size() for t in self.bufs)
 
 
+def _merged_1x1(a: ConvBNAct, b: ConvBNAct) -> Optional[nn.Conv2d]:
+    """One 1x1 conv computing [a(x) | b(x)] (output channels concatenated) when a and b are
+    fused 1x1 stride-1 convs of the same input with the same activation, else None."""
+    ca, cb = a.conv, b.conv
+    if not (a.fused and b.fused and a.act == b.act and ca.kernel_size == cb.kernel_size == (1, 1)
+            and ca.stride == cb.stride == (1, 1) and ca.in_channels == cb.in_channels and ca.groups == cb.groups == 1):
+        return None
+    m = nn.Conv2d(ca.in_channels, ca.out_channels + cb.out_channels, 1, 1, 0, bias=True)
+    with torch.no_grad():
+        m.weight.copy_(torch.cat([ca.weight.detach().float(), cb.weight.detach().float()], 0))
+        zb = lambda c: c.bias.detach().float() if c.bias is not None else torch.zeros(c.out_channels)  # noqa: E731
+        m.bias.copy_(torch.cat([zb(ca), zb(cb)], 0))
+    return m
+
+
 class _C3Plan:
-    """C3: cv3(cat(m(cv1(x)), cv2(x))) with the cat buffer written in place."""
+    """C3: cv3(cat(m(cv1(x)), cv2(x))) with the cat buffer written in place.  cv1 and cv2
+    (two 1x1 convs of the same input) run as ONE conv writing [cv1 | cv2] straight into
+    the cat buffer (x read once, one launch); the bottlenecks then start from its cv1 half
+    and the last one writes its output back over that half (per-element residual in
+    place: each output element's residual is read by the thread that writes it)."""
 
     def __init__(self, c3, B, H, W, bufs: _Buffers, device):
         pr = bufs.precision
@@ -59,6 +78,8 @@ class _C3Plan:
         self.m = [(_fc(b.cv1, device, pr), _fc(b.cv2, device, pr), b.add) for b in c3.m]
         c_ = self.cv1.N
         self.c_ = c_
+        mc = _merged_1x1(c3.cv1, c3.cv2) if self.cv1.N == self.cv1.cout_real == self.cv2.N else None
+        self.cv12 = FusedConv(mc, act=c3.cv1.act, device=device, precision=pr) if mc is not None else None
         self.cat = bufs.new(B, H, W, 2 * c_)
         self.a = [bufs.new(B, H, W, c_), bufs.new(B, H, W, c_)]
         self.tmp = bufs.new(B, H, W, c_)
@@ -66,14 +87,19 @@ class _C3Plan:
 
     def __call__(self, x: NHWC, out: NHWC) -> NHWC:
         c_ = self.c_
-        cur = self.cv1(x, out=self.a[0])
+        if self.cv12 is not None:
+            self.cv12(x, out=NHWC(self.cat.t, 0, 2 * c_))
+            cur = NHWC(self.cat.t, 0, c_)
+        else:
+            cur = self.cv1(x, out=self.a[0])
         for i, (b1, b2, add) in enumerate(self.m):
             last = i == len(self.m) - 1
             dst = NHWC(self.cat.t, 0, c_) if last else self.a[(i + 1) % 2]
             u = b1(cur, out=self.tmp)
             b2(u, out=dst, res=cur if add else None)
             cur = dst
-        self.cv2(x, out=NHWC(self.cat.t, c_, c_))
+        if self.cv12 is None:
+            self.cv2(x, out=NHWC(self.cat.t, c_, c_))
         return self.cv3(self.cat, out=out)
 
 
