@@ -190,7 +190,10 @@ def test_conv_pair_occupancy_gated_reads(cuda, tile):
     xz = NHWC(to_pairs(x).to(cuda), pair=True)
     Ho, Wo = fc.out_hw(H, W)
     plain = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
-    fc(xz, out=plain, tile=tile)
+    # auto (tile 0) at stride 1 routes an ungated call to conv_hx3 (a different summation
+    # order): the ungated reference is then the gated kernel with every cell occupied
+    ones = torch.ones(B, H, W, dtype=torch.uint8, device=cuda)
+    fc(NHWC(xz.t, pair=True, occ=ones) if (tile == 0 and s == 1) else xz, out=plain, tile=tile)
     gated = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
     fc(NHWC(xz.t, pair=True, occ=occ.to(cuda)), out=gated, tile=tile)
     junk = x + torch.randn(B, H, W, cin) * (1 - occ[..., None])  # garbage in every unoccupied cell
