@@ -258,6 +258,252 @@ __global__ void __launch_bounds__(256) planar_affine_kernel(const float* __restr
   }
 }
 
+
+// ---- K1 fused into the YOLOv5 stem and its first stride-2 conv (fp32 mode).
+//
+// Unfused, the camera branch writes the space-to-depth input [B, 320, 320, 16] fp32
+// (210 MB at batch 32), the s2d stem reads it and writes [B, 320, 320, 16] (210 MB), and
+// the 3x3 stride-2 conv b1 reads that back: ~840 MB of HBM traffic for ~0.6 GFLOP per frame.
+// Here one workgroup owns an 8 x 16 tile of b1's output (160 x 160 grid) and builds
+// everything it needs in LDS: the 19 x 35 s2d input pixels are sampled straight from the
+// uint8 frame (sample_px: the same resize / letterbox / affine arithmetic as
+// prep_s2d_kernel, so the same fp32 values) and split to bf16 hi / lo; the stem (3x3 over
+// 16 s2d channels, 16 outputs) runs on the 17 x 33 pixels b1 reads, its bias + activation
+// outputs (zero outside the 320 x 320 image: b1's padding) are split into a second LDS image
+// that overlays the first, and b1 (16 -> 32, stride 2) reads it.  Products and K-step order
+// are those of conv_small_halo_x3 / conv_nhwc_x3 (bf16 x3, fp32 accumulation), so the
+// output matches the unfused chain.  Only the frames are read and only b1's output written.
+// LDS 44 KiB (3 workgroups per CU).  Weights: split_pairs images [N, 2 * 160] of the
+// FusedConvs (K = 9 taps x 16 channels, padded to 160), read as MFMA fragments from L2.
+struct StemArgs {
+  const uint8_t* src;
+  PrepParams p;
+  const __hip_bfloat16* w0;  // stem [16, 2 * 160]
+  const float* b0;
+  const __hip_bfloat16* w1;  // b1 [32, 2 * 160]
+  const float* b1;
+  int act0, act1;
+  float* out;  // [B, H1, W1, ldo], channels [co_off, co_off + 32)
+  int ldo, co_off;
+  int B, H0, W0, H1, W1;  // stem grid (s2d, dst / 2) and b1 grid
+};
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float stem_act(float v, int act) {  // conv_mfma.hip act_fn (same expressions)
+  switch (act) {
+    case 1: return fmaxf(v, 0.f);
+    case 2: return v / (1.f + __expf(-v));
+    case 3: return v > 0.f ? v : 0.1f * v;
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ void stem_mfma3(f32x4_t& acc, const bf16x8_t& bh, const bf16x8_t& bl, const bf16x8_t& ah,
+                                           const bf16x8_t& al) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
+  constexpr int TY = 8, TX = 16;                     // b1 output tile
+  constexpr int SH = 2 * TY + 1, SW = 2 * TX + 1;    // stem pixels b1 reads (17 x 33)
+  constexpr int IH = SH + 2, IW = SW + 2;            // s2d input pixels the stem reads (19 x 35)
+  constexpr int NS = SH * SW, NMS = (NS + 15) / 16;  // stem pixels, 16-pixel M tiles (36)
+  constexpr int IMG = IH * IW * 32;                  // one input image (hi or lo): 32 B per pixel
+  constexpr int SPB = 80;                            // stem pixel: hi 32 B | lo 32 B | 16 B pad (conflict-free stride-2 reads)
+  constexpr int LDS = (2 * IMG > NS * SPB) ? 2 * IMG : NS * SPB;
+  constexpr int KP = 160;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  unsigned char* const himg = smem;
+  unsigned char* const limg = smem + IMG;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int ntx = (a.W1 + TX - 1) / TX, nty = (a.H1 + TY - 1) / TY;
+  const int tile = blockIdx.x;
+  const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
+  const int oy0 = (rem / ntx) * TY, ox0 = (rem - (rem / ntx) * ntx) * TX;
+  const int sy0 = 2 * oy0 - 1, sx0 = 2 * ox0 - 1;  // stem region origin
+  const int iy0 = sy0 - 1, ix0 = sx0 - 1;          // input region origin
+
+  // phase A: s2d input pixels from the frame, split into the hi / lo images
+  const uint8_t* s = a.src + (long)b * a.p.src_batch_stride;
+  const float sc[3] = {a.p.sc0, a.p.sc1, a.p.sc2}, bi[3] = {a.p.b0, a.p.b1, a.p.b2};
+  // exact 2:1 downscale of a 3-channel frame into an even-aligned region (1280 x 720 -> 640 x 360
+  // letterboxed): coord() gives s = 2 dst, a = 0.5 everywhere, so an s2d pixel's 2 x 2 block reads
+  // one 4 x 4 source block -- 4 rows of 12 aligned bytes (3 dword loads each) instead of 48 byte loads
+  const bool half = a.p.src_c == 3 && a.p.reg_h * 2 == a.p.src_h && a.p.reg_w * 2 == a.p.src_w &&
+                    !(a.p.reg_top & 1) && !(a.p.reg_left & 1) && !(a.p.reg_h & 1) && !(a.p.reg_w & 1) &&
+                    !(a.p.src_row_stride & 3) && !(a.p.src_batch_stride & 3);
+  for (int g = tid; g < IH * IW; g += 256) {
+    const int hy = g / IW, hx = g - (g / IW) * IW;
+    const int Y = iy0 + hy, X = ix0 + hx;
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = 0.f;
+    if ((unsigned)Y < (unsigned)a.H0 && (unsigned)X < (unsigned)a.W0) {
+      const int ly = 2 * Y - a.p.reg_top, lx = 2 * X - a.p.reg_left;
+      if (half) {
+        float o[4][3];
+        if (ly >= 0 && ly < a.p.reg_h && lx >= 0 && lx < a.p.reg_w) {  // the whole block (even alignment)
+          const uint8_t* r = s + (long)(2 * ly) * a.p.src_row_stride + 6 * lx;
+          unsigned w[4][3];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) w[k][j] = reinterpret_cast<const unsigned*>(r + (long)k * a.p.src_row_stride)[j];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const int dy = d >> 1, dx = d & 1;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const int b0 = (2 * dx) * 3 + c, b1 = b0 + 3;  // bytes of source columns 2 dx, 2 dx + 1
+              const float v00 = (float)((w[2 * dy][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
+              const float v01 = (float)((w[2 * dy][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
+              const float v10 = (float)((w[2 * dy + 1][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
+              const float v11 = (float)((w[2 * dy + 1][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
+              const float top = v00 + 0.5f * (v01 - v00);
+              const float bot = v10 + 0.5f * (v11 - v10);
+              float q = top + 0.5f * (bot - top);
+              if (a.p.quantize_u8) q = fminf(fmaxf(rintf(q), 0.f), 255.f);
+              o[d][c] = q;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) o[d][0] = o[d][1] = o[d][2] = a.p.pad_value;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[d][a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float o[3];
+          sample_px(a.p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
+        }
+      }
+    }
+    __bf16 h[16], l[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      h[c] = (__bf16)v[c];
+      l[c] = (__bf16)(v[c] - (float)h[c]);
+    }
+    *reinterpret_cast<uint4*>(himg + g * 32) = reinterpret_cast<const uint4*>(h)[0];
+    *reinterpret_cast<uint4*>(himg + g * 32 + 16) = reinterpret_cast<const uint4*>(h)[1];
+    *reinterpret_cast<uint4*>(limg + g * 32) = reinterpret_cast<const uint4*>(l)[0];
+    *reinterpret_cast<uint4*>(limg + g * 32 + 16) = reinterpret_cast<const uint4*>(l)[1];
+  }
+  __syncthreads();
+
+  // phase B: stem, M tiles wid, wid + 4, ... of the 17 x 33 stem pixels (row-major), 16 outputs
+  constexpr int MW = (NMS + 3) / 4;  // M tiles per wave (9)
+  f32x4_t acc0[MW];
+  int hbase[MW];
+#pragma unroll
+  for (int i = 0; i < MW; ++i) {
+    acc0[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int p = (wid + 4 * i) * 16 + fr;
+    const int py = p / SW, px = p - (p / SW) * SW;
+    hbase[i] = p < NS ? py * IW + px : -1;
+  }
+#pragma unroll
+  for (int st = 0; st < KP / 32; ++st) {
+    const int k0 = st * 32 + fq * 8, tap = k0 >> 4, ci0 = k0 & 15;
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    const __hip_bfloat16* wp = a.w0 + fr * 2 * KP + (k0 >> 3) * 16;
+    const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(wp);
+    const bf16x8_t bl = *reinterpret_cast<const bf16x8_t*>(wp + 8);
+#pragma unroll
+    for (int i = 0; i < MW; ++i) {
+      if (wid + 4 * i >= NMS) continue;
+      bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
+      if (tap < 9 && hbase[i] >= 0) {
+        const int hp = hbase[i] + ky * IW + kx;
+        ah = *reinterpret_cast<const bf16x8_t*>(himg + hp * 32 + ci0 * 2);
+        al = *reinterpret_cast<const bf16x8_t*>(limg + hp * 32 + ci0 * 2);
+      }
+      stem_mfma3(acc0[i], bh, bl, ah, al);
+    }
+  }
+  __syncthreads();  // every wave done reading the input images: the stem image overlays them
+  {
+    float bb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bb[r] = a.b0 ? a.b0[fq * 4 + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < MW; ++i) {
+      if (wid + 4 * i >= NMS) continue;
+      const int p = (wid + 4 * i) * 16 + fr;
+      if (p >= NS) continue;
+      const int py = p / SW, px = p - (p / SW) * SW;
+      const bool in = (unsigned)(sy0 + py) < (unsigned)a.H0 && (unsigned)(sx0 + px) < (unsigned)a.W0;
+      __bf16 h[4], l[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = in ? stem_act(acc0[i][r] + bb[r], a.act0) : 0.f;
+        h[r] = (__bf16)v;
+        l[r] = (__bf16)(v - (float)h[r]);
+      }
+      *reinterpret_cast<uint2*>(smem + p * SPB + fq * 8) = *reinterpret_cast<const uint2*>(h);
+      *reinterpret_cast<uint2*>(smem + p * SPB + 32 + fq * 8) = *reinterpret_cast<const uint2*>(l);
+    }
+  }
+  __syncthreads();
+
+  // phase C: b1 (3x3 stride 2, 16 -> 32): wave wid owns output rows 2 wid, 2 wid + 1 of the tile
+  f32x4_t acc1[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < KP / 32; ++st) {
+    const int k0 = st * 32 + fq * 8, tap = k0 >> 4, ci0 = k0 & 15;
+    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    bf16x8_t bh[2], bl[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const __hip_bfloat16* wp = a.w1 + (j * 16 + fr) * 2 * KP + (k0 >> 3) * 16;
+      bh[j] = *reinterpret_cast<const bf16x8_t*>(wp);
+      bl[j] = *reinterpret_cast<const bf16x8_t*>(wp + 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
+      if (tap < 9) {
+        const int sp = (2 * (2 * wid + i) + ky) * SW + 2 * fr + kx;
+        ah = *reinterpret_cast<const bf16x8_t*>(smem + sp * SPB + ci0 * 2);
+        al = *reinterpret_cast<const bf16x8_t*>(smem + sp * SPB + 32 + ci0 * 2);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) stem_mfma3(acc1[i][j], bh[j], bl[j], ah, al);
+    }
+  }
+  const int ox = ox0 + fr;
+  if (ox >= a.W1) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oy = oy0 + 2 * wid + i;
+    if (oy >= a.H1) break;
+    float* o = a.out + (((long)b * a.H1 + oy) * a.W1 + ox) * a.ldo + a.co_off;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = j * 16 + fq * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = stem_act(acc1[i][j][r] + (a.b1 ? a.b1[n + r] : 0.f), a.act1);
+      *reinterpret_cast<float4*>(o + n) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
 }  // namespace
 
 // fp32 NCHW [B, 3, H, W] -> dst NHWC x 8 (layout 1) or space-to-depth [B, H/2, W/2, 16]
@@ -324,4 +570,31 @@ TCA_API int tca_image_preprocess(const void* src, long src_batch_stride, int src
     default: return (int)hipErrorInvalidValue;
   }
   TCA_LAUNCH_CHECK();
+}
+
+// K1 + YOLOv5 s2d stem + b1 in one kernel (yolo_stem_fused_kernel): uint8 frames [B, src_h,
+// src_w, src_c] -> b1's output fp32 [B, dst_h / 4, dst_w / 4, ldo] channels [co_off, co_off + 32).
+// Geometry / affine arguments as tca_image_preprocess (letterbox region, pad value, quantize);
+// w0 / w1: split_pairs weight images (stem 16 x 2*160 over the s2d channels, b1 32 x 2*160).
+TCA_API int tca_yolo_stem_fused(const void* src, long src_batch_stride, int src_h, int src_w, int src_row_stride,
+                                int src_c, int swap_rb, int dst_h, int dst_w, int batch, int reg_top, int reg_left,
+                                int reg_h, int reg_w, float pad_value, int quantize_u8, float sc0, float sc1,
+                                float sc2, float b0, float b1, float b2, const void* w0, const float* bias0, int act0,
+                                const void* w1, const float* bias1, int act1, float* out, int ldo, int co_off,
+                                hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (src_c < 3 || (dst_h & 3) || (dst_w & 3) || reg_h <= 0 || reg_w <= 0 || (ldo & 3) || (co_off & 3) ||
+      ldo < co_off + 32 || !w0 || !w1 || !out)
+    return (int)hipErrorInvalidValue;
+  StemArgs a;
+  a.src = (const uint8_t*)src;
+  a.p = PrepParams{src_h, src_w, src_row_stride, src_c, src_batch_stride, swap_rb, dst_h, dst_w, 16, 2,
+                   reg_top, reg_left, reg_h, reg_w, pad_value, quantize_u8, sc0, sc1, sc2, b0, b1, b2};
+  a.w0 = (const __hip_bfloat16*)w0; a.b0 = bias0; a.w1 = (const __hip_bfloat16*)w1; a.b1 = bias1;
+  a.act0 = act0; a.act1 = act1; a.out = out; a.ldo = ldo; a.co_off = co_off;
+  a.B = batch; a.H0 = dst_h / 2; a.W0 = dst_w / 2; a.H1 = dst_h / 4; a.W1 = dst_w / 4;
+  const long tiles = (long)batch * ((a.H1 + 7) / 8) * ((a.W1 + 15) / 16);
+  if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
+  yolo_stem_fused_kernel<<<(unsigned)tiles, 256, 0, stream>>>(a);
+  return (int)hipGetLastError();
 }

@@ -32,6 +32,10 @@ _KERNEL_SIGS = {
     "tca_jpeg_idct": [P, P, P, P, L, L, I, P],
     "tca_jpeg_color": [P, P, P, L, L, I, P],
     "tca_image_preprocess": [P, L, I, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P],
+    # src, batch stride, src_h, src_w, row stride, src_c, swap_rb, dst_h, dst_w, B, top, left, reg_h, reg_w, pad,
+    # quantize, sc0-2, b0-2, w0, bias0, act0, w1, bias1, act1, out, ldo, co_off, stream
+    "tca_yolo_stem_fused": [P, L, I, I, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P, P, I, P, P, I, P, I,
+                            I, P],
     "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
     "tca_topk_sort": [P, P, I, I, I, P, P, P],
     "tca_nms_mask": [I, P, I, P, P, P, I, I, I, F, I, P, I, P],

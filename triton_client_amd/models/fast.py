@@ -19,6 +19,7 @@ neck's three up-sampled scales), so no concat kernel ever runs.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -26,6 +27,9 @@ import torch.nn as nn
 
 from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, to_pairs, upsample2x_nhwc
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
+
+# fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
+STEM_FUSED = os.environ.get("TCA_STEM_FUSED", "1") != "0"
 
 
 def _fc(m: ConvBNAct, device, precision: str = "bf16", **kw) -> FusedConv:
@@ -116,6 +120,7 @@ class FastYOLOv5:
         self.device = torch.device(device)
         self.precision = pr = precision
         H, W = img_hw
+        self.H, self.W = H, W
         B = batch
         bufs = self.bufs = _Buffers(self.device, precision)
         m = model
@@ -181,6 +186,16 @@ class FastYOLOv5:
         self.dout = [bufs.new(B, *s, d.N) for s, d in zip((s8, s16, s32), self.det)]
         self.no_real = m.detect[0].out_channels
 
+    def stem_fused_ok(self) -> bool:
+        """The fused K1 + stem + b1 kernel (ops/image.py yolo_stem_fused) takes this plan:
+        fp32, s2d stem 16 -> 16, b1 3x3 stride 2 16 -> 32, image sides divisible by 4.
+        TCA_STEM_FUSED=0 keeps the three-kernel chain."""
+        b0, b1 = self.b0, self.b1
+        return (STEM_FUSED and self.s2d and self.precision == "fp32" and b0.N == 16 and b0.cin_p == 16
+                and b0.Kp == 160 and b0.k == 3 and b0.s == 1 and b1.cin_p == 16 and b1.N == 32 and b1.Kp == 160
+                and b1.k == 3 and b1.s == 2 and b1.p == 1 and not self.t1.pair
+                and self.H % 4 == 0 and self.W % 4 == 0 and b0.act in (0, 1, 2, 3) and b1.act in (0, 1, 2, 3))
+
     def input_view(self) -> torch.Tensor:
         """[B, 3, H, W] channels_last view of the RGB part of the input buffer
         (what the preprocess kernel writes; channels 3..7 stay zero).  Not
@@ -205,9 +220,13 @@ class FastYOLOv5:
             self.x.t.zero_()
             self.x.t[..., :3].copy_(x.permute(0, 2, 3, 1))
 
-    def forward(self) -> List[NHWC]:
-        t = self.b0(self.x, out=self.t0)
-        t = self.b1(t, out=self.t1)
+    def forward(self, from_t1: bool = False) -> List[NHWC]:
+        """from_t1: b1's output is already in ``t1`` (the fused K1 + stem + b1 kernel ran)."""
+        if from_t1:
+            t = self.t1
+        else:
+            t = self.b0(self.x, out=self.t0)
+            t = self.b1(t, out=self.t1)
         t = self.c3_2(t, out=self.t2)
         t = self.b3(t, out=self.t3)
         p3 = self.c3_4(t, out=self.p3)

@@ -216,6 +216,26 @@ def _preprocess_s2d(frames, dst_hw, mode, scale, bias, swap_rb, pad_value, quant
     return out, xf
 
 
+def yolo_stem_fused(frames: torch.Tensor, dst_hw: Tuple[int, int], mode: str, stem, b1, out,
+                    scaling: str = "COCO", swap_rb: bool = False, pad_value: float = 114.0, quantize_u8: bool = True,
+                    stream=None):
+    """K1 + the YOLOv5 s2d stem + its first 3x3 stride-2 conv in one kernel
+    (``tca_yolo_stem_fused``, ``csrc/kernels/image.hip``): uint8 frames [B, h0, w0, 3] ->
+    ``out`` (an fp32 NHWC view, 32 channels) at dst_hw / 4.  ``stem`` / ``b1`` are the plan's
+    fp32 FusedConvs (split weights).  Same values as preprocess(S2D) -> stem -> b1."""
+    B, h0, w0, c0 = frames.shape
+    H, W = dst_hw
+    scale, bias = SCALING_PRESETS[scaling.upper()] if isinstance(scaling, str) else scaling
+    xf, (top, left, nh, nw) = frame_xform((h0, w0), (H, W), mode)
+    frames = frames.contiguous()
+    _native.call("tca_yolo_stem_fused", _native.ptr(frames), h0 * w0 * c0, h0, w0, w0 * c0, c0, int(swap_rb), H, W, B,
+                 top, left, nh, nw, float(pad_value), int(quantize_u8), float(scale[0]), float(scale[1]),
+                 float(scale[2]), float(bias[0]), float(bias[1]), float(bias[2]), _native.ptr(stem.w_gemm),
+                 _native.ptr(stem.b_gemm), stem.act, _native.ptr(b1.w_gemm), _native.ptr(b1.b_gemm), b1.act,
+                 _native.ptr(out.t), out.t.shape[-1], out.off, _native.stream_ptr(stream))
+    return out, xf
+
+
 def draw_boxes_(frames: torch.Tensor, box: torch.Tensor, cls: torch.Tensor, count: torch.Tensor,
                 thickness: int = 2, stream=None) -> torch.Tensor:
     """K15: draw result boxes onto uint8 frames in place (``csrc/kernels/draw.hip``).

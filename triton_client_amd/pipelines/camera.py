@@ -22,7 +22,7 @@ import torch
 from ..models.common import fuse_model, lsuv_rescale
 from ..models.yolov5 import YOLOv5, build_yolov5
 from ..ops.conv import act_dtype
-from ..ops.image import frame_xform, preprocess
+from ..ops.image import frame_xform, preprocess, yolo_stem_fused
 from ..ops.yolo import YoloPostprocess
 
 
@@ -102,6 +102,9 @@ class CameraPipeline:
         """Capture-safe: reads ``self.frames``, returns the NmsResult buffers."""
         if self.use_fast:
             f = self.fast or self.build_fast()
+            if f.stem_fused_ok():  # one kernel: frames -> b1's output
+                yolo_stem_fused(self.frames, self.img_hw, self.mode, f.b0, f.b1, f.t1, "COCO", swap_rb=self.swap_rb)
+                return self.post(f.forward(from_t1=True), self.xform)
             if f.s2d:
                 preprocess(self.frames, self.img_hw, self.mode, "COCO", f.x.t.dtype, "S2D",
                            swap_rb=self.swap_rb, out=f.x.t)
