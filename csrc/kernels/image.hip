@@ -338,58 +338,7 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
   const bool half = a.p.src_c == 3 && a.p.reg_h * 2 == a.p.src_h && a.p.reg_w * 2 == a.p.src_w &&
                     !(a.p.reg_top & 1) && !(a.p.reg_left & 1) && !(a.p.reg_h & 1) && !(a.p.reg_w & 1) &&
                     !(a.p.src_row_stride & 3) && !(a.p.src_batch_stride & 3);
-  for (int g = tid; g < IH * IW; g += 256) {
-    const int hy = g / IW, hx = g - (g / IW) * IW;
-    const int Y = iy0 + hy, X = ix0 + hx;
-    float v[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] = 0.f;
-    if ((unsigned)Y < (unsigned)a.H0 && (unsigned)X < (unsigned)a.W0) {
-      const int ly = 2 * Y - a.p.reg_top, lx = 2 * X - a.p.reg_left;
-      if (half) {
-        float o[4][3];
-        if (ly >= 0 && ly < a.p.reg_h && lx >= 0 && lx < a.p.reg_w) {  // the whole block (even alignment)
-          const uint8_t* r = s + (long)(2 * ly) * a.p.src_row_stride + 6 * lx;
-          unsigned w[4][3];
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) w[k][j] = reinterpret_cast<const unsigned*>(r + (long)k * a.p.src_row_stride)[j];
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int dy = d >> 1, dx = d & 1;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const int b0 = (2 * dx) * 3 + c, b1 = b0 + 3;  // bytes of source columns 2 dx, 2 dx + 1
-              const float v00 = (float)((w[2 * dy][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
-              const float v01 = (float)((w[2 * dy][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
-              const float v10 = (float)((w[2 * dy + 1][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
-              const float v11 = (float)((w[2 * dy + 1][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
-              const float top = v00 + 0.5f * (v01 - v00);
-              const float bot = v10 + 0.5f * (v11 - v10);
-              float q = top + 0.5f * (bot - top);
-              if (a.p.quantize_u8) q = fminf(fmaxf(rintf(q), 0.f), 255.f);
-              o[d][c] = q;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) o[d][0] = o[d][1] = o[d][2] = a.p.pad_value;
-        }
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[d][a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
-      } else {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          float o[3];
-          sample_px(a.p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
-#pragma unroll
-          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
-        }
-      }
-    }
+  auto put = [&](int g, const float (&v)[16]) {
     __bf16 h[16], l[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -400,6 +349,78 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
     *reinterpret_cast<uint4*>(himg + g * 32 + 16) = reinterpret_cast<const uint4*>(h)[1];
     *reinterpret_cast<uint4*>(limg + g * 32) = reinterpret_cast<const uint4*>(l)[0];
     *reinterpret_cast<uint4*>(limg + g * 32 + 16) = reinterpret_cast<const uint4*>(l)[1];
+  };
+  if (half) {
+    // all of this thread's source blocks are requested before any is used (one memory latency
+    // per workgroup, not one per pixel)
+    constexpr int NPT = (IH * IW + 255) / 256;
+    unsigned w[NPT][4][3];
+    int state[NPT];  // 0 outside the s2d image (zeros), 1 letterbox pad, 2 frame block
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int g = tid + u * 256;
+      const int hy = g / IW, hx = g - (g / IW) * IW;
+      const int Y = iy0 + hy, X = ix0 + hx;
+      const int ly = 2 * Y - a.p.reg_top, lx = 2 * X - a.p.reg_left;
+      state[u] = 0;
+      if (g < IH * IW && (unsigned)Y < (unsigned)a.H0 && (unsigned)X < (unsigned)a.W0)
+        state[u] = (ly >= 0 && ly < a.p.reg_h && lx >= 0 && lx < a.p.reg_w) ? 2 : 1;
+      const uint8_t* r = s + (state[u] == 2 ? (long)(2 * ly) * a.p.src_row_stride + 6 * lx : 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          w[u][k][j] = state[u] == 2 ? reinterpret_cast<const unsigned*>(r + (long)k * a.p.src_row_stride)[j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int g = tid + u * 256;
+      if (g >= IH * IW) break;
+      float o[4][3], v[16];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int dy = d >> 1, dx = d & 1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int b0 = (2 * dx) * 3 + c, b1 = b0 + 3;  // bytes of source columns 2 dx, 2 dx + 1
+          const float v00 = (float)((w[u][2 * dy][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
+          const float v01 = (float)((w[u][2 * dy][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
+          const float v10 = (float)((w[u][2 * dy + 1][b0 >> 2] >> (8 * (b0 & 3))) & 255u);
+          const float v11 = (float)((w[u][2 * dy + 1][b1 >> 2] >> (8 * (b1 & 3))) & 255u);
+          const float top = v00 + 0.5f * (v01 - v00);
+          const float bot = v10 + 0.5f * (v11 - v10);
+          float q = top + 0.5f * (bot - top);
+          if (a.p.quantize_u8) q = fminf(fmaxf(rintf(q), 0.f), 255.f);
+          o[d][c] = state[u] == 2 ? q : a.p.pad_value;
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          v[d * 3 + c] = state[u] ? o[d][a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c] : 0.f;
+#pragma unroll
+      for (int c = 12; c < 16; ++c) v[c] = 0.f;
+      put(g, v);
+    }
+  } else {
+    for (int g = tid; g < IH * IW; g += 256) {
+      const int hy = g / IW, hx = g - (g / IW) * IW;
+      const int Y = iy0 + hy, X = ix0 + hx;
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 0.f;
+      if ((unsigned)Y < (unsigned)a.H0 && (unsigned)X < (unsigned)a.W0) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float o[3];
+          sample_px(a.p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
+        }
+      }
+      put(g, v);
+    }
   }
   __syncthreads();
 
