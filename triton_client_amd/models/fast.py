@@ -25,11 +25,14 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
+from .. import _native
 from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, to_pairs, upsample2x_nhwc
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 # fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
 STEM_FUSED = os.environ.get("TCA_STEM_FUSED", "1") != "0"
+# fused YOLOv5n first C3 block (_C3Plan.fused_ok)
+C3_FUSED = os.environ.get("TCA_C3_FUSED", "1") != "0"
 
 
 def _fc(m: ConvBNAct, device, precision: str = "bf16", **kw) -> FusedConv:
@@ -89,8 +92,33 @@ class _C3Plan:
         self.tmp = bufs.new(B, H, W, c_)
         self.out_c = self.cv3.N
 
+    def fused_ok(self, x: NHWC, out: NHWC) -> bool:
+        """yolo_c3s_fused (csrc/kernels/image.hip) takes this block: fp32, 32 -> 32 channels,
+        c_ = 16, one bottleneck (1x1 then 3x3), plain fp32 activations.  TCA_C3_FUSED=0: unfused."""
+        if not (C3_FUSED and self.cv12 is not None and len(self.m) == 1 and self.c_ == 16):
+            return False
+        b1, b2, _ = self.m[0]
+        convs = (self.cv12, b1, b2, self.cv3)
+        return (all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) for c in convs)
+                and self.cv12.cin_p == 32 and self.cv12.N == 32 and self.cv12.k == 1 and self.cv12.Kp == 32
+                and b1.cin_p == 16 and b1.N == 16 and b1.k == 1 and b1.Kp == 32
+                and b2.cin_p == 16 and b2.N == 16 and b2.k == 3 and b2.s == 1 and b2.p == 1 and b2.Kp == 160
+                and self.cv3.cin_p == 32 and self.cv3.N == 32 and self.cv3.k == 1 and self.cv3.Kp == 32
+                and not x.pair and not out.pair and x.c == 32 and out.c == 32 and x.t.dtype == torch.float32
+                and x.t.is_cuda)
+
     def __call__(self, x: NHWC, out: NHWC) -> NHWC:
         c_ = self.c_
+        if self.fused_ok(x, out):
+            b1, b2, add = self.m[0]
+            B, H, W, _ = x.shape
+            _native.call("tca_yolo_c3s_fused", _native.ptr(x.t), B, H, W, x.t.shape[-1], x.off,
+                         _native.ptr(self.cv12.w_gemm), _native.ptr(self.cv12.b_gemm), self.cv12.act,
+                         _native.ptr(b1.w_gemm), _native.ptr(b1.b_gemm), b1.act, _native.ptr(b2.w_gemm),
+                         _native.ptr(b2.b_gemm), b2.act, _native.ptr(self.cv3.w_gemm), _native.ptr(self.cv3.b_gemm),
+                         self.cv3.act, int(bool(add)), _native.ptr(out.t), out.t.shape[-1], out.off,
+                         _native.stream_ptr(None))
+            return out
         if self.cv12 is not None:
             self.cv12(x, out=NHWC(self.cat.t, 0, 2 * c_))
             cur = NHWC(self.cat.t, 0, c_)
