@@ -161,8 +161,13 @@ class DynamicBatcher:
         self.cv = threading.Condition()
         self.stopped = False
         self.batches = 0
-        self.thread = threading.Thread(target=self._run, name=f"batcher-{model.name}", daemon=True)
-        self.thread.start()
+        # one batcher thread per model instance (Triton instance_group count): instance k runs
+        # its batches on its own plans, stream and lock, so one instance stages / encodes while
+        # another's graph runs on the GPU
+        self.threads = [threading.Thread(target=self._run, args=(k,), name=f"batcher-{model.name}-{k}", daemon=True)
+                        for k in range(max(1, model.instances))]
+        for t in self.threads:
+            t.start()
 
     def submit(self, inputs, requested, encode, out_dst=None):
         item = _Pending(inputs, requested, encode, out_dst)
@@ -182,7 +187,8 @@ class DynamicBatcher:
         with self.cv:
             self.stopped = True
             self.cv.notify_all()
-        self.thread.join()
+        for t in self.threads:
+            t.join()
 
     def _take(self):
         with self.cv:
@@ -198,29 +204,31 @@ class DynamicBatcher:
                 self.cv.wait(left)
             return [self.q.popleft() for _ in range(min(self.max_batch, len(self.q)))]
 
-    def _run(self) -> None:
+    def _run(self, k: int = 0) -> None:
         while True:
             items = self._take()
             if items is None:
                 return
-            self.batches += 1
+            with self.cv:
+                self.batches += 1
             m = self.model
             GPU_PHASE.acquire_shared()
             try:
-                with m.stream_context():
-                    self._execute(m, items)
+                with m.stream_context(k):
+                    self._execute(m, items, k)
             finally:
                 GPU_PHASE.release_shared()
 
-    def _execute(self, m: "ServedModel", items) -> None:
-        with m._lock:
+    def _execute(self, m: "ServedModel", items, k: int = 0) -> None:
+        with m.instance_lock(k):
             try:
                 t0 = time.perf_counter()
                 dsts = [it.out_dst for it in items]
+                kw = {"inst": k} if m.instances > 1 else {}
                 if m.accepts_out_dst and any(d for d in dsts):
-                    outs = m.execute_batch([it.inputs for it in items], items[0].requested, dsts=dsts)
+                    outs = m.execute_batch([it.inputs for it in items], items[0].requested, dsts=dsts, **kw)
                 else:
-                    outs = m.execute_batch([it.inputs for it in items], items[0].requested)
+                    outs = m.execute_batch([it.inputs for it in items], items[0].requested, **kw)
                 t1 = time.perf_counter()
                 for it, o in zip(items, outs):
                     if isinstance(o, BaseException):  # this request failed inside the batch (e.g. bad values)
@@ -265,6 +273,9 @@ class ServedModel(ABC):
     # inputs from a device shared-memory region arrive as torch tensors on the GPU when
     # the model reads them there (device_inputs), else as host copies
     device_inputs = False
+    # Triton instance_group count: dynamic-batching executions in flight at once (a model with
+    # instances > 1 takes execute_batch(..., inst=k) and keeps per-instance plans)
+    instances = 1
 
     def __init__(self, name: str, version: str = "1"):
         self.name = name
@@ -274,20 +285,28 @@ class ServedModel(ABC):
         self._config: Optional[mc.ModelConfig] = None
         self._lock = threading.Lock()  # one execution at a time per instance (GPU graph buffers)
         self._batcher: Optional[DynamicBatcher] = None
-        self._stream = None  # a HIP stream of this model's own: two served models overlap on the GPU
+        self._streams: Dict[int, object] = {}  # HIP streams of this model's own (per instance)
+        self._inst_locks: Dict[int, threading.Lock] = {0: self._lock}
 
-    def stream_context(self):
-        """Context running this model's executions on a stream of its own (GPU
-        models; a no-op on the CPU): the batcher threads of two models would
-        otherwise serialise on the default stream."""
+    def instance_lock(self, k: int = 0) -> threading.Lock:
+        """Lock of instance k (instance 0: the model lock of direct executions)."""
+        if k not in self._inst_locks:
+            with self._lock:
+                self._inst_locks.setdefault(k, threading.Lock())
+        return self._inst_locks[k]
+
+    def stream_context(self, k: int = 0):
+        """Context running this model's executions (of instance k) on a stream of its own
+        (GPU models; a no-op on the CPU): the batcher threads of two models, or two instances
+        of one, would otherwise serialise on the default stream."""
         import contextlib
         dev = getattr(self, "device", None)
         if dev is None or getattr(dev, "type", None) != "cuda":
             return contextlib.nullcontext()
         import torch
-        if self._stream is None:
-            self._stream = torch.cuda.Stream(device=dev)
-        return torch.cuda.stream(self._stream)
+        if k not in self._streams:
+            self._streams[k] = torch.cuda.Stream(device=dev)
+        return torch.cuda.stream(self._streams[k])
 
     # ---------------------------------------------------------------- contract
     @abstractmethod
@@ -320,8 +339,14 @@ class ServedModel(ABC):
         # no execution of this model (batched or direct) is mid-run past this point
         GPU_PHASE.acquire_exclusive()
         try:
-            with self._lock:
+            locks = [self.instance_lock(k) for k in range(max(1, self.instances))]
+            for lk in locks:
+                lk.acquire()
+            try:
                 self.ready = False
+            finally:
+                for lk in reversed(locks):
+                    lk.release()
         finally:
             GPU_PHASE.release_exclusive()
 
@@ -335,7 +360,7 @@ class ServedModel(ABC):
                                max_batch_size=self.max_batch_size)
             c.input.extend(self.inputs())
             c.output.extend(self.outputs())
-            c.instance_group.add(kind=self.instance_kind(), count=1)
+            c.instance_group.add(kind=self.instance_kind(), count=max(1, self.instances))
             self._config = c
         return self._config
 

@@ -25,6 +25,7 @@ state_dict is supported for real checkpoints.
 from __future__ import annotations
 
 import json
+import os
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -198,6 +199,15 @@ class _PlanClock:
             self.ev[-1][1].synchronize()
             for (_, a), (name, b) in zip(self.ev[:-1], self.ev[1:]):
                 PROFILE.add(f"{self.tag}.gpu.{name}", a.elapsed_time(b) * 1e-3)
+
+
+def _instances(n: Optional[int]) -> int:
+    """Model instances of the GPU models with captured batch plans (Triton instance_group count):
+    the explicit value, else TCA_SERVE_INSTANCES, else 2 (one instance stages and encodes while
+    the other's graph runs)."""
+    if n is None:
+        n = int(os.environ.get("TCA_SERVE_INSTANCES", "2"))
+    return max(1, int(n))
 
 
 def _pick(plans: Dict[int, object], n: int):
@@ -471,9 +481,10 @@ class _PointPillarsPlan:
 class YoloV5Model(ServedModel):
     def __init__(self, name: str = "YOLOv5nCOCO", variant: str = "n", nc: int = 80, img: int = 640,
                  device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0,
-                 batch: int = 16):
+                 batch: int = 16, instances: Optional[int] = None):
         super().__init__(name)
         self.batch = batch  # dynamic batching: concurrent requests run as one captured batch-`batch` graph
+        self.instances = _instances(instances)
         self.variant, self.nc, self.img = variant, nc, img
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -507,7 +518,9 @@ class YoloV5Model(ServedModel):
             # captured plans at PLAN_SIZES up to the dynamic batch (the same kernels as the local camera
             # pipeline), all over the calibrated module
             sizes = sorted({b for b in PLAN_SIZES if b <= max(1, self.batch)} | {max(1, self.batch)})
-            self.plans = {b: _YoloPlan(self.pipe, b, self.img, self.device) for b in sizes}
+            self.plan_sets = [{b: _YoloPlan(self.pipe, b, self.img, self.device) for b in sizes}
+                              for _ in range(self.instances)]
+            self.plans = self.plan_sets[0]
             self.dynamic_batch = max(sizes)
         else:
             from ..models.common import fuse_model
@@ -534,18 +547,19 @@ class YoloV5Model(ServedModel):
     device_inputs = True
 
     @torch.no_grad()
-    def execute_batch(self, batch, requested, dsts=None):
+    def execute_batch(self, batch, requested, dsts=None, inst: int = 0):
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
-        return _pick(self.plans, len(batch)).run([x["images"] for x in batch], dsts)
+        return _pick(self.plan_sets[inst], len(batch)).run([x["images"] for x in batch], dsts)
 
 
 class PointPillarsModel(ServedModel):
     def __init__(self, name: str = "pointpillar_kitti", cfg: Optional[PointPillarsConfig] = None, device="auto",
                  weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 2000.0,
-                 batch: int = 16):
+                 batch: int = 16, instances: Optional[int] = None):
         super().__init__(name)
         self.batch = batch  # dynamic batching: concurrent requests share one batch-`batch` pass
+        self.instances = _instances(instances)
         self.cfg = cfg or PointPillarsConfig()
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -592,7 +606,9 @@ class PointPillarsModel(ServedModel):
                 self.pipe.calibrate_detection_density(self.calibrate_target)
             self.model = self.pipe.model
             sizes = sorted({b for b in PLAN_SIZES if b <= max(1, self.batch)} | {max(1, self.batch)})
-            self.plans = {b: _PointPillarsPlan(self.model, self.cfg, b, self.device) for b in sizes}
+            self.plan_sets = [{b: _PointPillarsPlan(self.model, self.cfg, b, self.device) for b in sizes}
+                              for _ in range(self.instances)]
+            self.plans = self.plan_sets[0]
             self.dynamic_batch = max(sizes)
         else:
             from ..models.common import fuse_model
@@ -612,14 +628,14 @@ class PointPillarsModel(ServedModel):
             self._check(inputs)  # in the request thread, off the batcher's critical path
 
     @torch.no_grad()
-    def execute_batch(self, batch, requested):
+    def execute_batch(self, batch, requested, inst: int = 0):
         """Host inputs validated by :meth:`validate` (every request reaches the batcher
         through it); every slot's coordinate / count ranges are checked again on the device
         inside the plan (csrc/kernels/copy.hip tca_voxel_check), which is the check for
         device shared-memory inputs."""
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
-        return _pick(self.plans, len(batch)).run(batch)  # an out-of-range request's entry is its InferError
+        return _pick(self.plan_sets[inst], len(batch)).run(batch)  # an out-of-range request's entry is its InferError
 
     @torch.no_grad()
     def execute(self, inputs, requested):
