@@ -161,6 +161,7 @@ class DynamicBatcher:
         self.cv = threading.Condition()
         self.stopped = False
         self.batches = 0
+        self.forming = threading.Lock()
         # one batcher thread per model instance (Triton instance_group count): instance k runs
         # its batches on its own plans, stream and lock, so one instance stages / encodes while
         # another's graph runs on the GPU
@@ -206,7 +207,10 @@ class DynamicBatcher:
 
     def _run(self, k: int = 0) -> None:
         while True:
-            items = self._take()
+            # one instance forms a batch at a time: the next one gathers the requests that arrive
+            # while this batch runs (two instances forming at once would split every batch in two)
+            with self.forming:
+                items = self._take()
             if items is None:
                 return
             with self.cv:

@@ -203,10 +203,11 @@ class _PlanClock:
 
 def _instances(n: Optional[int]) -> int:
     """Model instances of the GPU models with captured batch plans (Triton instance_group count):
-    the explicit value, else TCA_SERVE_INSTANCES, else 2 (one instance stages and encodes while
-    the other's graph runs)."""
+    the explicit value, else TCA_SERVE_INSTANCES, else 1.  Measured with 4 + 4 client processes
+    (profiles/r3/served_instances.json): 2 instances split the arriving requests into batches of
+    2-3 (vs 3-8 at one instance) and run slower on every wire, so one stays the default."""
     if n is None:
-        n = int(os.environ.get("TCA_SERVE_INSTANCES", "2"))
+        n = int(os.environ.get("TCA_SERVE_INSTANCES", "1"))
     return max(1, int(n))
 
 
