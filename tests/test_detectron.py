@@ -190,15 +190,25 @@ def test_served_test_model_fp32_matches_local_engine(cuda):
     many = served.execute_batch([{"input__00": x}, {"input__00": x[:, ::-1].copy()}, {"input__00": x}], None)
     assert len(want) > 0
 
-    def canon(box, score, cls):  # kept set in a canonical order (NMS output order breaks exact-score ties freely)
-        rows = np.concatenate([np.round(score[:, None], 5), cls[:, None].astype(np.float64), box], 1)
-        return rows[np.lexsort(rows.T[::-1])]
-    w = canon(want[:, :4], want[:, 4], want[:, 5])
+    def unmatched(box, score, cls):
+        """Kept-set comparison independent of output order (NMS breaks near-ties freely, and the
+        two paths' scores differ in the last bits): each expected detection must pair with an
+        unused served one of the same class, box within 2e-3 px + 1e-4 relative, score within 1e-4."""
+        used = np.zeros(len(score), bool)
+        miss = 0
+        for row in want:
+            ok = (~used & (cls == row[5]) & (np.abs(score - row[4]) <= 1e-4)
+                  & np.all(np.abs(box - row[None, :4]) <= 2e-3 + 1e-4 * np.abs(row[None, :4]), 1))
+            idx = np.flatnonzero(ok)
+            if len(idx) == 0:
+                miss += 1
+            else:
+                used[idx[np.argmin(np.abs(score[idx] - row[4]))]] = True
+        return miss
     for got in (one, many[0], many[2]):
         assert got["dims__3"].tolist() == [[640, 480]]
         assert len(got["scores__2"]) == len(want)
-        g = canon(got["bboxex__0"], got["scores__2"], got["classes__1"])
-        np.testing.assert_allclose(g, w, rtol=1e-4, atol=2e-3)
+        assert unmatched(got["bboxex__0"], got["scores__2"], got["classes__1"]) == 0
 
 
 def test_reference_model_repository_families():
