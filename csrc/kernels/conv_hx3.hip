@@ -871,10 +871,6 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     // <= 168 VGPRs -> 3 workgroups (12 waves) per CU
     case 5: return launch_hx3<8, 64, 1, 4, false, 2, 3>(a, stream);
     case 6: return launch_hx3<8, 64, 1, 4, true, 2, 3>(a, stream);
-    // 16 lines x 16 channels per wave (N = 64): twice the MFMAs per staged halo line
-    case 7: return launch_hx3<16, 64, 1, 4, false, 2, 2>(a, stream);
-    case 8: return launch_hx3<16, 64, 1, 4, true, 2, 2>(a, stream);
-    case 9: return launch_hx3<16, 64, 1, 4, true, 1, 2>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -108,7 +108,7 @@ PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73
 # (hx3s2_launch tiles 1-4) the stride-2 one.
 HX3 = os.environ.get("TCA_HX3", "1") != "0"
 HX3S2 = HX3 and os.environ.get("TCA_HX3S2", "1") != "0"
-HX3_TILES = (110, 111, 112, 113, 114, 115, 116, 117, 118, 119)
+HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
 # conv_wx3 (conv_hx3.hip: Winograd F(2,3) along one axis, 6 split products per pixel instead of 9)
 # for the 3x3 stride-1 pair layers (N % 64 == 0); TCA_WX3=1 makes it the default for them.
