@@ -41,8 +41,25 @@ struct VoxGeom {
   float r0, r1, r2;      // range min
   float vs0, vs1, vs2;   // voxel size
   int nx, ny, nz;
-  long cells;            // nx*ny*nz
+  long cells;            // per-frame rows of cell_first / cell_vid: nx*ny*nz (dense) or the hash table size
+  int* keys;             // hash mode: per-frame open-addressing table [B][cells] of cell ids (-1 empty), else null
+  int hbits;             // log2 of the hash table size
 };
+
+// Hash mode (grids far larger than a frame's points, e.g. SECOND's 1408 x 1600 x 40): a cell's
+// row is its slot in a per-frame linear-probing table of >= 2x max_points entries (load <= 1/2),
+// claimed by atomicCAS on the key; point_cell then holds the slot, every later stage indexes
+// by it unchanged, and the cell id (for coords) is read back from the key.  Voxel ids depend
+// only on each cell's first point index, so the results equal the dense grid's bit for bit.
+__device__ __forceinline__ int hash_slot(int* keys, int hbits, int cell) {
+  const unsigned mask = (1u << hbits) - 1u;
+  unsigned h = ((unsigned)cell * 0x9E3779B1u) >> (32 - hbits);
+  while (true) {
+    const int k = atomicCAS(&keys[h], -1, cell);
+    if (k == -1 || k == cell) return (int)h;
+    h = (h + 1u) & mask;
+  }
+}
 
 __device__ __forceinline__ int cell_of(const float* p, const VoxGeom& g, int& cx, int& cy, int& cz) {
   cx = (int)floorf((p[0] - g.r0) / g.vs0);
@@ -63,6 +80,7 @@ __global__ void __launch_bounds__(kBlock) vox_cell_kernel(const float* __restric
     const float* p = pts + ((long)b * max_pts + i) * pstride;
     int cx, cy, cz;
     cell = cell_of(p, g, cx, cy, cz);
+    if (cell >= 0 && g.keys) cell = hash_slot(g.keys + (long)b * g.cells, g.hbits, cell);
     if (cell >= 0) atomicMin(&cell_first[(long)b * g.cells + cell], i);
   }
   point_cell[(long)b * max_pts + i] = cell;
@@ -134,7 +152,8 @@ __global__ void __launch_bounds__(kBlock) vox_assign_kernel(const int* __restric
     if (vid < max_voxels) {
       const int c = pc[first + k];
       cell_vid[cbase + c] = vid;
-      const int cx = c % g.nx, cy = (c / g.nx) % g.ny, cz = c / (g.nx * g.ny);
+      const int cell = g.keys ? g.keys[cbase + c] : c;
+      const int cx = cell % g.nx, cy = (cell / g.nx) % g.ny, cz = cell / (g.nx * g.ny);
       int* co = coords + ((long)b * max_voxels + vid) * 4;
       co[0] = b; co[1] = cz; co[2] = cy; co[3] = cx;
     }
@@ -184,7 +203,7 @@ __global__ void __launch_bounds__(256) vox_gather_reset_kernel(
     const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ npts, int nfeat, int batch,
     int max_voxels, int P, const int* __restrict__ voxel_count, int* __restrict__ vcount, int* __restrict__ slots,
     float* __restrict__ voxels, int* __restrict__ num_points, const int* __restrict__ point_cell, long cells,
-    int* __restrict__ cell_first, int* __restrict__ cell_vid, int gather) {
+    int* __restrict__ cell_first, int* __restrict__ cell_vid, int* __restrict__ keys, int gather) {
   const int lane = threadIdx.x & 63;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
@@ -220,6 +239,7 @@ __global__ void __launch_bounds__(256) vox_gather_reset_kernel(
     if (c < 0) continue;
     cell_first[(long)b * cells + c] = kEmpty;
     cell_vid[(long)b * cells + c] = -1;
+    if (keys) keys[(long)b * cells + c] = -1;
   }
 }
 
@@ -393,21 +413,25 @@ __global__ void __launch_bounds__(256) vox_slot_reset_kernel(int max_voxels, int
 
 __global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const int* __restrict__ npts,
                                                              const int* __restrict__ point_cell, long cells,
-                                                             int* __restrict__ cell_first, int* __restrict__ cell_vid) {
+                                                             int* __restrict__ cell_first, int* __restrict__ cell_vid,
+                                                             int* __restrict__ keys) {
   const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
   if (i >= npts[b]) return;
   const int c = point_cell[(long)b * max_pts + i];
   if (c < 0) return;
   cell_first[(long)b * cells + c] = kEmpty;
   cell_vid[(long)b * cells + c] = -1;
+  if (keys) keys[(long)b * cells + c] = -1;
 }
 
-VoxGeom make_geom(const float* range, const float* vsize, const int* grid) {
+VoxGeom make_geom(const float* range, const float* vsize, const int* grid, int* keys, int hbits) {
   VoxGeom g;
   g.r0 = range[0]; g.r1 = range[1]; g.r2 = range[2];
   g.vs0 = vsize[0]; g.vs1 = vsize[1]; g.vs2 = vsize[2];
   g.nx = grid[0]; g.ny = grid[1]; g.nz = grid[2];
-  g.cells = (long)g.nx * g.ny * g.nz;
+  g.keys = hbits > 0 ? keys : nullptr;
+  g.hbits = hbits;
+  g.cells = g.keys ? (1L << hbits) : (long)g.nx * g.ny * g.nz;
   return g;
 }
 
@@ -419,6 +443,8 @@ TCA_API int tca_vox_blocks_per_frame(int max_points) { return (max_points + kPts
 //   cell_first int[B*cells] = INT_MAX, cell_vid int[B*cells] = -1,
 //   slots int[B*V*P] = INT_MAX, vcount int[B*V] = 0,
 //   point_cell int[B*max_points], block_count int[B*blocks_per_frame].
+// Hash mode (hash_bits > 0): cell_first / cell_vid / keys are int[B << hash_bits] (keys = -1) with
+// 1 << hash_bits >= 2 * max_points; dense (hash_bits = 0, keys unused): int[B*cells].
 // Stages: mode bit 1 = run assignment (a,b1,b2,c); bit 2 = run gather/reset (d).
 // The fused PointPillars path runs mode 1, then its VFE kernel consumes the
 // slots, then mode 2 with gather = 0 to reset.
@@ -426,9 +452,11 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
                          const float* range, const float* vsize, const int* grid, int P, int max_voxels, int nfeat,
                          int* cell_first, int* cell_vid, int* point_cell, int* block_count, int* slots, int* vcount,
                          float* voxels, int* coords, int* num_points, int* voxel_count, int mode, int gather,
-                         hipStream_t stream) {
+                         int* keys, int hash_bits, hipStream_t stream) {
   if (batch <= 0) return 0;
-  VoxGeom g = make_geom(range, vsize, grid);
+  if (hash_bits < 0 || hash_bits > 30 || (hash_bits > 0 && (!keys || (1L << hash_bits) < 2L * max_points)))
+    return (int)hipErrorInvalidValue;  // the probe loop needs free slots: load <= 1/2
+  VoxGeom g = make_geom(range, vsize, grid, keys, hash_bits);
   const int bpf = (max_points + kPtsPerBlock - 1) / kPtsPerBlock;
   dim3 pgrid((max_points + kBlock - 1) / kBlock, batch);
   dim3 sgrid(bpf, batch);
@@ -445,12 +473,13 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
   if ((mode & 2) && !gather && (P & 3) == 0) {
     vox_slot_reset_kernel<<<dim3((max_voxels * (P / 4) + 255) / 256, batch), 256, 0, stream>>>(
         max_voxels, P, voxel_count, vcount, slots, num_points);
-    vox_cell_reset_kernel<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid);
+    vox_cell_reset_kernel<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid,
+                                                        g.keys);
   } else if (mode & 2) {
     vox_gather_reset_kernel<<<1024, 256, 0, stream>>>(pts, pstride, max_points, npts, nfeat, batch,
                                                                max_voxels, P, voxel_count, vcount, slots, voxels,
                                                                num_points, point_cell, g.cells, cell_first, cell_vid,
-                                                               gather);
+                                                               g.keys, gather);
   }
   TCA_LAUNCH_CHECK();
 }
@@ -461,10 +490,10 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
 TCA_API int tca_vox_slots_csr(const int* point_cell, int max_points, const int* npts, int batch, const int* grid,
                               const int* cell_vid, int max_voxels, int P, const int* voxel_count, int* vcount,
                               int* offs, int* cursor, int* csr, int* dense, int* dense_count, int* slots,
-                              hipStream_t stream) {
+                              int hash_bits, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (P > 64 || P < 1) return (int)hipErrorInvalidValue;
-  const long cells = (long)grid[0] * grid[1] * grid[2];
+  const long cells = hash_bits > 0 ? (1L << hash_bits) : (long)grid[0] * grid[1] * grid[2];
   dim3 pgrid((max_points + kBlock - 1) / kBlock, batch);
   vox_count_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, cells, cell_vid, max_voxels, vcount);
   vox_scan_kernel<<<batch, kScanT, 0, stream>>>(voxel_count, max_voxels, vcount, offs, cursor, dense_count);

@@ -192,7 +192,12 @@ def test_pc2_unpack_gpu(cuda):
 
 
 @pytest.mark.parametrize("vcfg", [KITTI_PILLARS, KITTI_SECOND_VOXELS, NUSC_PILLARS])
-def test_voxelize_gpu_exact(cuda, vcfg):
+@pytest.mark.parametrize("hash_mode", ["auto", "1", "0"])
+def test_voxelize_gpu_exact(cuda, vcfg, hash_mode, monkeypatch):
+    """Order-exact vs the NumPy spconv golden, with the cell rows as the dense grid and as the
+    per-frame hash table (voxelize.hip hash_slot; auto: hash for SECOND's 90 M-cell grid)."""
+    if hash_mode != "auto":
+        monkeypatch.setenv("TCA_VOX_HASH", hash_mode)
     cfg = dataclasses.replace(vcfg, max_voxels=2000)
     B, N = 2, 20000
     nf = cfg.num_point_features
@@ -216,10 +221,13 @@ def test_voxelize_gpu_exact(cuda, vcfg):
 
 
 @pytest.mark.parametrize("vcfg", [KITTI_PILLARS, KITTI_SECOND_VOXELS])
-def test_voxelize_gpu_dense_voxels(cuda, vcfg):
+@pytest.mark.parametrize("hash_mode", ["auto", "1"])
+def test_voxelize_gpu_dense_voxels(cuda, vcfg, hash_mode, monkeypatch):
     """Clustered clouds: voxels with 9..300 points exercise the dense-voxel
     (wave bitonic top-P) path of the CSR slot sort; slot order must still be
     the first P points in point order (spconv)."""
+    if hash_mode != "auto":
+        monkeypatch.setenv("TCA_VOX_HASH", hash_mode)
     cfg = dataclasses.replace(vcfg, max_voxels=3000)
     rng = np.random.default_rng(7)
     r = np.asarray(cfg.point_cloud_range, np.float32)

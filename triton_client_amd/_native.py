@@ -48,7 +48,7 @@ _KERNEL_SIGS = {
     "tca_pc2_unpack": [P, P, P, I, I, I, P, P, I, F, P, I, P, P, P, P],
     "tca_pc2_blocks_per_frame": [I],
     "tca_vox_blocks_per_frame": [I],
-    "tca_voxelize": [P, I, I, P, I, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P],
+    "tca_voxelize": [P, I, I, P, I, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P, I, P],
     "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, I, P],
@@ -90,7 +90,7 @@ _KERNEL_SIGS = {
     "tca_yolov4_decode": [P, P, P, I, I, I, P, P, P, F, F, I, I, P, P, P, P, P, P, P, I, P],
     "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, I, P],
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, I, P],
-    "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, P],
+    "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, I, P],
     "tca_bev_neck_head": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     "tca_bev_neck_head_x3": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],
     "tca_bev_neck_head_x3p": [I, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P],

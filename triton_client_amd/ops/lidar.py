@@ -8,6 +8,7 @@ semantics (tested against ``golden``).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -124,6 +125,18 @@ def voxelize_np(points: np.ndarray, cfg: VoxelConfig, nfeat: Optional[int] = Non
     return voxels, coords, num, slots
 
 
+def voxel_hash_bits(cells: int, max_points: int) -> int:
+    """log2 of the voxeliser's per-frame hash table (0: dense cell grid).  Hash when the grid has
+    more than 16x as many cells as the table would (2 x max_points, rounded up to a power of 2)."""
+    bits = max(10, int(2 * max(1, max_points) - 1).bit_length())
+    force = os.environ.get("TCA_VOX_HASH")
+    if force == "0":
+        return 0
+    if force == "1" or cells > 16 * (1 << bits):
+        return bits
+    return 0
+
+
 class Voxelizer:
     """Batched voxeliser with persistent, self-resetting GPU scratch."""
 
@@ -138,8 +151,14 @@ class Voxelizer:
             cells = cfg.num_cells
             V, P = cfg.max_voxels, cfg.max_points_per_voxel
             g = self.ws.get
-            self.cell_first = g("cell_first", (batch, cells), torch.int32, init=INT_MAX)
-            self.cell_vid = g("cell_vid", (batch, cells), torch.int32, init=-1)
+            # cell rows: the dense grid, or (grids much larger than a frame's points: SECOND's 90 M
+            # cells, 720 MB per frame dense) a per-frame hash table of >= 2 x max_points slots
+            # (voxelize.hip hash_slot; TCA_VOX_HASH=1 / 0 forces it on / off)
+            self.hash_bits = voxel_hash_bits(cells, max_points)
+            rows = (1 << self.hash_bits) if self.hash_bits else cells
+            self.cell_first = g("cell_first", (batch, rows), torch.int32, init=INT_MAX)
+            self.cell_vid = g("cell_vid", (batch, rows), torch.int32, init=-1)
+            self.keys = g("cell_keys", (batch, rows), torch.int32, init=-1) if self.hash_bits else None
             self.point_cell = g("point_cell", (batch, max_points), torch.int32)
             bpf = _native.kernels().tca_vox_blocks_per_frame(max_points)
             self.block_count = g("block_count", (batch, bpf), torch.int32)
@@ -168,7 +187,7 @@ class Voxelizer:
             _native.call("tca_vox_slots_csr", P(self.point_cell), self.max_points, P(npts), points.shape[0],
                          self._grid, P(self.cell_vid), self.cfg.max_voxels, self.cfg.max_points_per_voxel,
                          P(self.voxel_count), P(self.vcount), P(self.offs), P(self.cursor), P(self.csr),
-                         P(self.dense), P(self.dense_count), P(self.slots), _native.stream_ptr(stream))
+                         P(self.dense), P(self.dense_count), P(self.slots), self.hash_bits, _native.stream_ptr(stream))
             mode &= ~1
             if not mode:
                 return
@@ -182,7 +201,7 @@ class Voxelizer:
                      _native.ptr(self.point_cell), _native.ptr(self.block_count), _native.ptr(self.slots),
                      _native.ptr(self.vcount), _native.ptr(self.voxels), _native.ptr(self.coords),
                      _native.ptr(self.num_points), _native.ptr(self.voxel_count), mode, int(gather),
-                     _native.stream_ptr(stream))
+                     _native.ptr(self.keys), self.hash_bits, _native.stream_ptr(stream))
 
     def assign(self, points: torch.Tensor, npts: torch.Tensor, stream=None) -> None:
         """Stage a-c: voxel ids, coords, sorted slot lists (GPU only)."""
