@@ -70,13 +70,13 @@ def parse():
                     help="DP scatter/gather: the C++ RCCL communicator (default) or torch batch_isend_irecv")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
+    ap.add_argument("--single-input-set", action="store_true",
+                    help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
+                         "of two captured graphs alternating over two input sets")
     ap.add_argument("--serial", action="store_true", help="camera and LiDAR branches on one stream")
     ap.add_argument("--graph-mode", choices=["split", "fork"], default="fork",
                     help="split: one hipGraph per branch, replayed on two streams; fork: one graph with two "
                          "forked branches")
-    ap.add_argument("--sub-batches", type=int, default=1,
-                    help="split each branch's B frames into S sub-pipelines, one hipGraph + stream each "
-                         "(low-occupancy phases of one overlap another's convolutions)")
     ap.add_argument("--lidar-priority", type=int, default=0, help="1: LiDAR branch on a high-priority stream")
     ap.add_argument("--only", choices=["both", "camera", "lidar"], default="both")
     ap.add_argument("--camera-model", choices=["yolov5n", "yolov4", "retinanet", "fcos"], default="yolov5n",
@@ -184,7 +184,7 @@ def main():
 
     torch.manual_seed(0)
     det2 = args.camera_model in ("retinanet", "fcos")
-    S = max(1, args.sub_batches)
+    S = 1  # frames per branch run as one pipeline (sub-batched multistream variants measured slower, removed)
     if use_cam and args.camera_model == "yolov4":
         from triton_client_amd.pipelines import Yolov4Pipeline
 
@@ -219,13 +219,8 @@ def main():
         def make_lid(b, m):
             return LidarPipeline(model=m, batch=b, max_points=max_points, device=dev, z_offset=1.5,
                                  precision=args.precision)
-    if S > 1:
-        from triton_client_amd.pipelines.multistream import SubBatched
-        cam = SubBatched(make_cam, B, S) if use_cam else None
-        lid = SubBatched(make_lid, B, S) if use_lid else None
-    else:
-        cam = make_cam(B, None) if use_cam else None
-        lid = make_lid(B, None) if use_lid else None
+    cam = make_cam(B, None) if use_cam else None
+    lid = make_lid(B, None) if use_lid else None
 
     # ---------------- synthetic sensor data in pinned host memory
     shards = info.world if (args.ingest == "rccl" and info.is_main) else 1
@@ -319,21 +314,7 @@ def main():
         main.wait_stream(side)
         return r2, r3
 
-    if S > 1:
-        # every sub-pipeline is its own graph on its own stream; LiDAR (the critical
-        # path) is launched first
-        from triton_client_amd.pipelines.multistream import MultiStreamRunner
-        subs = ([p.step for p in lid.pipes] if use_lid else []) + ([p.step for p in cam.pipes] if use_cam else [])
-        ms = MultiStreamRunner(subs, enabled=not args.no_graph)
-        nl = S if use_lid else 0
-
-        class _Multi:
-            def __call__(self):
-                outs = ms()
-                return outs[nl:], outs[:nl]  # ([camera results], [lidar results])
-
-        runner = _Multi()
-    elif side is not None and args.graph_mode == "split" and not args.no_graph:
+    if side is not None and args.graph_mode == "split" and not args.no_graph:
         # one graph per branch, each replayed on its own stream (its own HW queue):
         # the overlap no longer depends on how the runtime maps a forked graph's
         # branches onto queues
@@ -400,8 +381,8 @@ def main():
 
     jdec = None
     if use_cam and args.camera_input == "jpeg":
-        if args.ingest != "local" or S > 1:
-            raise SystemExit("--camera-input jpeg needs --ingest local and --sub-batches 1")
+        if args.ingest != "local":
+            raise SystemExit("--camera-input jpeg needs --ingest local")
         from triton_client_amd.ops.jpeg import JpegBatchDecoder
         jdec = JpegBatchDecoder(B, dev, threads=args.decode_threads)
         jpeg_copy = torch.cuda.Stream()
@@ -438,9 +419,68 @@ def main():
         consumed.record()
         issue_h2d()
 
+    # two captured graphs over two input sets: the prefetch writes straight into the set the next
+    # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
+    db = (prefetch and isinstance(runner, GraphRunner) and runner.enabled and jdec is None
+          and not args.single_input_set)
+    if db:
+        owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
+        in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
+        base_fn = runner.fn
+
+        def bound(k):
+            def fn():
+                for (o, attr), t in zip(owners, in_sets[k]):
+                    setattr(o, attr, t)
+                try:
+                    return base_fn()
+                finally:
+                    for (o, attr), t in zip(owners, in_sets[0]):
+                        setattr(o, attr, t)
+            return fn
+        db_runners = [GraphRunner(bound(0)), GraphRunner(bound(1))]
+        db_done = [torch.cuda.Event(), torch.cuda.Event()]
+        db_free = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def db_h2d(k):
+            copy_stream.wait_event(db_free[k])
+            with torch.cuda.stream(copy_stream):
+                for d, h in zip(in_sets[k], host_src):
+                    d.copy_(h, non_blocking=True)
+                db_done[k].record(copy_stream)
+
+        torch.cuda.synchronize()  # the landing-buffer prefetch issued above is not used
+        for k in (0, 1):
+            db_free[k].record()
+            db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
+        torch.cuda.synchronize()
+
+        class _DoubleBuffered:
+            t = 0
+
+            def __call__(self):
+                if self.t == 0:  # capture both (the first warm-up step); both input sets hold frames
+                    for r_ in db_runners:
+                        r_.capture()
+                    o0, o1 = (outputs(*r_.out) for r_ in db_runners)
+                    if [t.data_ptr() for t in o0] != [t.data_ptr() for t in o1]:
+                        raise SystemExit("double-buffered graphs: the two captures return different result buffers")
+                k = self.t % 2
+                cur = torch.cuda.current_stream()
+                cur.wait_event(db_done[k])
+                out = db_runners[k]()
+                db_free[k].record(cur)
+                db_h2d(1 - k)  # the other set (read by the previous step) streams in the next frames
+                self.t += 1
+                return out
+
+        runner = _DoubleBuffered()
+
     def ingest():
         if jdec is not None:
             jdec.reconstruct(cam.frames)  # this step's JPEGs, staged during the previous step
+        if db:
+            return  # the double-buffered runner orders its own H2D
         if prefetch:
             cur = torch.cuda.current_stream()
             cur.wait_event(h2d_done)
@@ -630,9 +670,8 @@ def main():
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,
                 "branch_streams": 2 if side is not None else 1,
-                "graph_mode": (f"multistream x{S}" if S > 1 else
-                               (args.graph_mode if side is not None else "single")),
-                "sub_batches": S,
+                "graph_mode": args.graph_mode if side is not None else "single",
+                "graph_input_sets": 2 if db else 1,
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
                 "avg_2d_dets_per_frame": det2,
