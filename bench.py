@@ -421,6 +421,7 @@ def main():
 
     # two captured graphs over two input sets: the prefetch writes straight into the set the next
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
+    d2h_stage = None
     db = (prefetch and isinstance(runner, GraphRunner) and runner.enabled and jdec is None
           and not args.single_input_set)
     if db:
@@ -433,11 +434,21 @@ def main():
                 for (o, attr), t in zip(owners, in_sets[k]):
                     setattr(o, attr, t)
                 try:
-                    return base_fn()
+                    res = base_fn()
                 finally:
                     for (o, attr), t in zip(owners, in_sets[0]):
                         setattr(o, attr, t)
+                if info.world == 1:  # results -> this graph's D2H stage (device copies inside the graph)
+                    src_ = outputs(*res)
+                    if d2h_stage[k] is None:  # allocated in the eager warm-up, before capture
+                        d2h_stage[k] = [torch.empty_like(t) for t in src_]
+                    for d, t in zip(d2h_stage[k], src_):
+                        d.copy_(t, non_blocking=True)
+                return res
             return fn
+        d2h_stage = [None, None]
+        d2h_stream = torch.cuda.Stream()
+        d2h_free = [torch.cuda.Event(), torch.cuda.Event()]
         db_runners = [GraphRunner(bound(0)), GraphRunner(bound(1))]
         db_done = [torch.cuda.Event(), torch.cuda.Event()]
         db_free = [torch.cuda.Event(), torch.cuda.Event()]
@@ -468,6 +479,8 @@ def main():
                 k = self.t % 2
                 cur = torch.cuda.current_stream()
                 cur.wait_event(db_done[k])
+                if self.t >= 2:
+                    cur.wait_event(d2h_free[k])  # stage[k]'s D2H (two steps ago) is done
                 out = db_runners[k]()
                 db_free[k].record(cur)
                 db_h2d(1 - k)  # the other set (read by the previous step) streams in the next frames
@@ -548,10 +561,23 @@ def main():
             ex.gather(src, gather_dst if info.is_main else None)
         k = it[0] % 2
         if info.is_main:
-            for r in range(info.world):
-                for h, d in zip(host_out[k][r], gather_dst[r]):
-                    h.copy_(d, non_blocking=True)
-        out_ready[k].record()
+            if db and d2h_stage is not None and info.world == 1:
+                # the replay already copied its results into stage[j] (graph-side D2D): the D2H runs on
+                # the copy stream beside the next replay, which writes the other stage
+                j = (runner.t - 1) % 2
+                d2h_stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(d2h_stream):
+                    for h, d in zip(host_out[k][0], d2h_stage[j]):
+                        h.copy_(d, non_blocking=True)
+                    out_ready[k].record(d2h_stream)
+                    d2h_free[j].record(d2h_stream)
+            else:
+                for r in range(info.world):
+                    for h, d in zip(host_out[k][r], gather_dst[r]):
+                        h.copy_(d, non_blocking=True)
+                out_ready[k].record()
+        else:
+            out_ready[k].record()
         # detections of the previous step are on rank 0's host now; this step's
         # D2H completes while the next step is issued
         if it[0] > 0:
