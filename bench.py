@@ -422,8 +422,10 @@ def main():
     # two captured graphs over two input sets: the prefetch writes straight into the set the next
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
     d2h_stage = None
+    # (not with the RCCL gather captured in the step graph: two graphs replaying the same
+    # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     db = (prefetch and isinstance(runner, GraphRunner) and runner.enabled and jdec is None
-          and not args.single_input_set)
+          and not args.single_input_set and not gather_in_graph)
     if db:
         owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
         in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
