@@ -455,6 +455,18 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (OCC) {
+    // a tile whose whole input halo is unoccupied (the sparse pillar canvas far from the sensor)
+    // reads only zeros: its accumulators are exactly 0, so skip the K loop (bias / act / residual
+    // epilogue only) -- bit-identical to running it
+    unsigned mine = 0;
+#pragma unroll
+    for (int k = 0; k < HPL; ++k) mine |= h_ph[k];
+    if (!__syncthreads_or(mine != 0u)) {
+      hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
+      return;
+    }
+  }
   bf16x8 w0[2][FN][2], w1[2][FN][2];
   halo_load(0, 0);
   gload(IC<0>{}, 0, w0);
