@@ -13,6 +13,8 @@
 // by ~1-4 output pixels); the kernel is store-bound.
 #include "tca_common.h"
 
+#include <cstdlib>
+
 using namespace tca;
 
 namespace {
@@ -307,8 +309,10 @@ __device__ __forceinline__ void stem_mfma3(f32x4_t& acc, const bf16x8_t& bh, con
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
 }
 
+template <int TY>
 __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
-  constexpr int TY = 8, TX = 16;                     // b1 output tile
+  constexpr int TX = 16, RW = TY / 4;                // b1 output tile TY x 16; RW rows per wave
+  static_assert(TY % 4 == 0, "tile rows");
   constexpr int SH = 2 * TY + 1, SW = 2 * TX + 1;    // stem pixels b1 reads (17 x 33)
   constexpr int IH = SH + 2, IW = SW + 2;            // s2d input pixels the stem reads (19 x 35)
   constexpr int NS = SH * SW, NMS = (NS + 15) / 16;  // stem pixels, 16-pixel M tiles (36)
@@ -480,9 +484,9 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
   __syncthreads();
 
   // phase C: b1 (3x3 stride 2, 16 -> 32): wave wid owns output rows 2 wid, 2 wid + 1 of the tile
-  f32x4_t acc1[2][2];
+  f32x4_t acc1[RW][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RW; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -497,10 +501,10 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
       bl[j] = *reinterpret_cast<const bf16x8_t*>(wp + 8);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RW; ++i) {
       bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
       if (tap < 9) {
-        const int sp = (2 * (2 * wid + i) + ky) * SW + 2 * fr + kx;
+        const int sp = (2 * (RW * wid + i) + ky) * SW + 2 * fr + kx;
         ah = *reinterpret_cast<const bf16x8_t*>(smem + sp * SPB + ci0 * 2);
         al = *reinterpret_cast<const bf16x8_t*>(smem + sp * SPB + 32 + ci0 * 2);
       }
@@ -511,8 +515,8 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
   const int ox = ox0 + fr;
   if (ox >= a.W1) return;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int oy = oy0 + 2 * wid + i;
+  for (int i = 0; i < RW; ++i) {
+    const int oy = oy0 + RW * wid + i;
     if (oy >= a.H1) break;
     float* o = a.out + (((long)b * a.H1 + oy) * a.W1 + ox) * a.ldo + a.co_off;
 #pragma unroll
@@ -854,9 +858,16 @@ TCA_API int tca_yolo_stem_fused(const void* src, long src_batch_stride, int src_
   a.w0 = (const __hip_bfloat16*)w0; a.b0 = bias0; a.w1 = (const __hip_bfloat16*)w1; a.b1 = bias1;
   a.act0 = act0; a.act1 = act1; a.out = out; a.ldo = ldo; a.co_off = co_off;
   a.B = batch; a.H0 = dst_h / 2; a.W0 = dst_w / 2; a.H1 = dst_h / 4; a.W1 = dst_w / 4;
-  const long tiles = (long)batch * ((a.H1 + 7) / 8) * ((a.W1 + 15) / 16);
+  // 8-row tiles (44 KiB LDS, three workgroups per CU); TCA_STEM_TY=4 takes 4-row tiles (23 KiB, more
+  // workgroups per CU but 11 / 4 instead of 19 / 8 sampled rows per output row): measured 244 vs 204 us
+  static const int ty = [] {
+    const char* e = getenv("TCA_STEM_TY");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  const long tiles = (long)batch * ((a.H1 + ty - 1) / ty) * ((a.W1 + 15) / 16);
   if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
-  yolo_stem_fused_kernel<<<(unsigned)tiles, 256, 0, stream>>>(a);
+  if (ty == 8) yolo_stem_fused_kernel<8><<<(unsigned)tiles, 256, 0, stream>>>(a);
+  else yolo_stem_fused_kernel<4><<<(unsigned)tiles, 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
