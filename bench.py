@@ -138,6 +138,16 @@ def self_launch(n: int) -> int:
     return rc
 
 
+class _Split:
+    """--graph-mode split: one step graph per branch, replayed on two streams."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self):
+        return self.fn()
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -330,11 +340,7 @@ def main():
             main.wait_stream(side)
             return r2, r3
 
-        class _Split:
-            def __call__(self):
-                return split_step()
-
-        runner = _Split()
+        runner = _Split(split_step)
     else:
         runner = GraphRunner(pipeline_step, enabled=not args.no_graph)
     native = None
@@ -424,14 +430,23 @@ def main():
     d2h_stage = None
     # (not with the RCCL gather captured in the step graph: two graphs replaying the same
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
-    db = (prefetch and isinstance(runner, GraphRunner) and runner.enabled and jdec is None
-          and not args.single_input_set and not gather_in_graph)
+    # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
+    # 8.92-8.98 vs 8.45 ms, profiles/r3/sched_ab.txt)
+    split_mode = False
+    db = (prefetch and jdec is None and not args.single_input_set and not gather_in_graph
+          and isinstance(runner, GraphRunner) and runner.enabled)
     if db:
         owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
         in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
-        base_fn = runner.fn
+        # graph units: the whole forked step, or (split mode) one graph per branch; each is captured
+        # twice, once per input set, with its results copied into a per-capture D2H stage
+        if split_mode:
+            units = [("cam", cam.step, lambda r: outputs(r, None)), ("lid", lid.step, lambda r: outputs(None, r))]
+        else:
+            units = [("all", runner.fn, lambda r: outputs(*r))]
+        stages = {name: [None, None] for name, _, _ in units}
 
-        def bound(k):
+        def bound(name, base_fn, outs_of, k):
             def fn():
                 for (o, attr), t in zip(owners, in_sets[k]):
                     setattr(o, attr, t)
@@ -440,20 +455,30 @@ def main():
                 finally:
                     for (o, attr), t in zip(owners, in_sets[0]):
                         setattr(o, attr, t)
-                if info.world == 1:  # results -> this graph's D2H stage (device copies inside the graph)
-                    src_ = outputs(*res)
-                    if d2h_stage[k] is None:  # allocated in the eager warm-up, before capture
-                        d2h_stage[k] = [torch.empty_like(t) for t in src_]
-                    for d, t in zip(d2h_stage[k], src_):
+                if info.world == 1:  # results -> this capture's D2H stage (device copies inside the graph)
+                    src_ = outs_of(res)
+                    if stages[name][k] is None:  # allocated in the eager warm-up, before capture
+                        stages[name][k] = [torch.empty_like(t) for t in src_]
+                    for d, t in zip(stages[name][k], src_):
                         d.copy_(t, non_blocking=True)
                 return res
             return fn
-        d2h_stage = [None, None]
+        unit_runners = {name: [GraphRunner(bound(name, fn, of, k)) for k in (0, 1)] for name, fn, of in units}
         d2h_stream = torch.cuda.Stream()
         d2h_free = [torch.cuda.Event(), torch.cuda.Event()]
-        db_runners = [GraphRunner(bound(0)), GraphRunner(bound(1))]
         db_done = [torch.cuda.Event(), torch.cuda.Event()]
         db_free = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def db_replay(k):
+            if not split_mode:
+                return unit_runners["all"][k]()
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                r3 = unit_runners["lid"][k]()
+            r2 = unit_runners["cam"][k]()
+            main.wait_stream(side)
+            return r2, r3
 
         def db_h2d(k):
             copy_stream.wait_event(db_free[k])
@@ -472,18 +497,26 @@ def main():
             t = 0
 
             def __call__(self):
-                if self.t == 0:  # capture both (the first warm-up step); both input sets hold frames
-                    for r_ in db_runners:
-                        r_.capture()
-                    o0, o1 = (outputs(*r_.out) for r_ in db_runners)
-                    if [t.data_ptr() for t in o0] != [t.data_ptr() for t in o1]:
+                nonlocal d2h_stage
+                if self.t == 0:  # capture every graph (the first warm-up step); both input sets hold frames
+                    for rs in unit_runners.values():
+                        for r_ in rs:
+                            r_.capture()
+                    if split_mode:
+                        o = [outputs(unit_runners["cam"][k].out, unit_runners["lid"][k].out) for k in (0, 1)]
+                    else:
+                        o = [outputs(*unit_runners["all"][k].out) for k in (0, 1)]
+                    if [t.data_ptr() for t in o[0]] != [t.data_ptr() for t in o[1]]:
                         raise SystemExit("double-buffered graphs: the two captures return different result buffers")
+                    if info.world == 1:
+                        d2h_stage = [sum((stages[name][k] for name, _, _ in sorted(units, key=lambda u: u[0])), [])
+                                     for k in (0, 1)]
                 k = self.t % 2
                 cur = torch.cuda.current_stream()
                 cur.wait_event(db_done[k])
                 if self.t >= 2:
                     cur.wait_event(d2h_free[k])  # stage[k]'s D2H (two steps ago) is done
-                out = db_runners[k]()
+                out = db_replay(k)
                 db_free[k].record(cur)
                 db_h2d(1 - k)  # the other set (read by the previous step) streams in the next frames
                 self.t += 1
