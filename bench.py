@@ -432,18 +432,14 @@ def main():
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
     # 8.92-8.98 vs 8.45 ms, profiles/r3/sched_ab.txt)
-    split_mode = False
     db = (prefetch and jdec is None and not args.single_input_set and not gather_in_graph
           and isinstance(runner, GraphRunner) and runner.enabled)
     if db:
         owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
         in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
-        # graph units: the whole forked step, or (split mode) one graph per branch; each is captured
-        # twice, once per input set, with its results copied into a per-capture D2H stage
-        if split_mode:
-            units = [("cam", cam.step, lambda r: outputs(r, None)), ("lid", lid.step, lambda r: outputs(None, r))]
-        else:
-            units = [("all", runner.fn, lambda r: outputs(*r))]
+        # the step graph is captured twice, once per input set, with its results copied into a
+        # per-capture D2H stage
+        units = [("all", runner.fn, lambda r: outputs(*r))]
         stages = {name: [None, None] for name, _, _ in units}
 
         def bound(name, base_fn, outs_of, k):
@@ -470,15 +466,7 @@ def main():
         db_free = [torch.cuda.Event(), torch.cuda.Event()]
 
         def db_replay(k):
-            if not split_mode:
-                return unit_runners["all"][k]()
-            main = torch.cuda.current_stream()
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                r3 = unit_runners["lid"][k]()
-            r2 = unit_runners["cam"][k]()
-            main.wait_stream(side)
-            return r2, r3
+            return unit_runners["all"][k]()
 
         def db_h2d(k):
             copy_stream.wait_event(db_free[k])
@@ -502,15 +490,11 @@ def main():
                     for rs in unit_runners.values():
                         for r_ in rs:
                             r_.capture()
-                    if split_mode:
-                        o = [outputs(unit_runners["cam"][k].out, unit_runners["lid"][k].out) for k in (0, 1)]
-                    else:
-                        o = [outputs(*unit_runners["all"][k].out) for k in (0, 1)]
+                    o = [outputs(*unit_runners["all"][k].out) for k in (0, 1)]
                     if [t.data_ptr() for t in o[0]] != [t.data_ptr() for t in o[1]]:
                         raise SystemExit("double-buffered graphs: the two captures return different result buffers")
                     if info.world == 1:
-                        d2h_stage = [sum((stages[name][k] for name, _, _ in sorted(units, key=lambda u: u[0])), [])
-                                     for k in (0, 1)]
+                        d2h_stage = [stages["all"][k] for k in (0, 1)]
                 k = self.t % 2
                 cur = torch.cuda.current_stream()
                 cur.wait_event(db_done[k])
