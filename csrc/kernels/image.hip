@@ -879,7 +879,8 @@ TCA_API int tca_yolo_c3s_fused(const float* x, int B, int H, int W, int ldx, int
                                const void* wm2, const float* bm2, int actm2, const void* w3, const float* b3, int act3,
                                int add, float* y, int ldy, int y_off, hipStream_t stream) {
   if (B <= 0) return 0;
-  if ((ldx & 3) || (x_off & 3) || (ldy & 3) || (y_off & 3) || !w12 || !wm1 || !wm2 || !w3 || !x || !y)
+  if ((ldx & 3) || (x_off & 3) || (ldy & 3) || (y_off & 3) || ldx < x_off + 32 || ldy < y_off + 32 || !w12 || !wm1 ||
+      !wm2 || !w3 || !x || !y)
     return (int)hipErrorInvalidValue;
   C3sArgs a;
   a.x = x; a.y = y;
