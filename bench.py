@@ -371,8 +371,13 @@ def main():
     ex = FrameExchange(info, native=native)
     # with the native RCCL communicator the detection gather (grouped send / recv of fixed-shape
     # result buffers) is stream work: capture it inside the step graph, so a step is one replay
+    # ... unless the step runs as two double-buffered graphs (the default with local ingest): two graphs
+    # replaying one communicator's captured p2p have not run on a multi-GPU node yet, so then the
+    # gather is issued after the replay (same RCCL group, host-launched)
+    will_db = (args.ingest == "local" and not args.no_prefetch and not (use_cam and args.camera_input == "jpeg")
+               and not args.single_input_set and isinstance(runner, GraphRunner) and runner.enabled)
     gather_in_graph = (native is not None and isinstance(runner, GraphRunner) and runner.enabled
-                       and args.ingest == "local")
+                       and args.ingest == "local" and not will_db)
     gbuf = {}
     if gather_in_graph:
         def step_and_gather():
@@ -432,8 +437,8 @@ def main():
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
     # 8.92-8.98 vs 8.45 ms, profiles/r3/sched_ab.txt)
-    db = (prefetch and jdec is None and not args.single_input_set and not gather_in_graph
-          and isinstance(runner, GraphRunner) and runner.enabled)
+    db = will_db and prefetch and jdec is None and not gather_in_graph
+    assert db == will_db, (db, will_db)
     if db:
         owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
         in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
