@@ -70,6 +70,10 @@ def parse():
                     help="DP scatter/gather: the C++ RCCL communicator (default) or torch batch_isend_irecv")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
+    ap.add_argument("--lidar-pipeline", type=int, default=0,
+                    help="1: LiDAR software pipeline over two pipelines: step t runs the BEV network / NMS of "
+                         "batch t beside the unpack / voxelise / VFE of batch t+1 (double-buffered graphs only; "
+                         "LiDAR-only 6.81 vs 7.1 ms, headline unchanged: profiles/r3/lpipe/)")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
@@ -433,6 +437,7 @@ def main():
     # two captured graphs over two input sets: the prefetch writes straight into the set the next
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
     d2h_stage = None
+    piped = False
     # (not with the RCCL gather captured in the step graph: two graphs replaying the same
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
@@ -444,10 +449,47 @@ def main():
         in_sets = [list(dsts), [torch.empty_like(t) for t in dsts]]
         # the step graph is captured twice, once per input set, with its results copied into a
         # per-capture D2H stage
-        units = [("all", runner.fn, lambda r: outputs(*r))]
+        piped = bool(args.lidar_pipeline) and use_lid and not cp and not sec
+        if piped:
+            # two LiDAR pipelines over one model: graph k finishes pipeline k's batch (network + NMS)
+            # and preprocesses the next batch into pipeline 1-k, whose own data buffer is its input set
+            lids = [lid, make_lid(B, lid.model)]
+            for lp in lids:
+                lp.build_fast()
+            side2 = torch.cuda.Stream()
+            lside = side if side is not None else torch.cuda.Stream()
+
+            def piped_fn(k):
+                def fn():
+                    main = torch.cuda.current_stream()
+                    lside.wait_stream(main)
+                    side2.wait_stream(main)
+                    with torch.cuda.stream(lside):
+                        r3 = lids[k].step_post()
+                    with torch.cuda.stream(side2):
+                        lids[1 - k].step_pre()
+                    r2 = cam.step() if use_cam else None
+                    main.wait_stream(lside)
+                    main.wait_stream(side2)
+                    return r2, r3
+                return fn
+            owners = [(cam, "frames")] if use_cam else []
+            in_sets = [in_sets[0][:len(owners)], in_sets[1][:len(owners)]]
+            base_fns = [piped_fn(0), piped_fn(1)]
+        else:
+            base_fns = [runner.fn, runner.fn]
+        units = [("all", None, lambda r: outputs(*r))]
         stages = {name: [None, None] for name, _, _ in units}
 
-        def bound(name, base_fn, outs_of, k):
+        def h2d_pairs(k):  # (device, host) pairs of the inputs graph k reads
+            if not piped:
+                return list(zip(in_sets[k], host_src))
+            pairs = [(in_sets[k][0], host_src[0])] if use_cam else []
+            return pairs + [(lids[1 - k].data, pc_host[0]), (lids[1 - k].frame_n, n_host[0])]
+
+        def bound(name, _unused, outs_of, k):
+            base_fn = base_fns[k]
+
             def fn():
                 for (o, attr), t in zip(owners, in_sets[k]):
                     setattr(o, attr, t)
@@ -476,7 +518,7 @@ def main():
         def db_h2d(k):
             copy_stream.wait_event(db_free[k])
             with torch.cuda.stream(copy_stream):
-                for d, h in zip(in_sets[k], host_src):
+                for d, h in h2d_pairs(k):
                     d.copy_(h, non_blocking=True)
                 db_done[k].record(copy_stream)
 
@@ -485,6 +527,9 @@ def main():
             db_free[k].record()
             db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
         torch.cuda.synchronize()
+        if piped:
+            lids[0].step_pre()  # prologue: graph 0's first replay finishes pipeline 0's batch
+            torch.cuda.synchronize()
 
         class _DoubleBuffered:
             t = 0
@@ -496,7 +541,7 @@ def main():
                         for r_ in rs:
                             r_.capture()
                     o = [outputs(*unit_runners["all"][k].out) for k in (0, 1)]
-                    if [t.data_ptr() for t in o[0]] != [t.data_ptr() for t in o[1]]:
+                    if not piped and [t.data_ptr() for t in o[0]] != [t.data_ptr() for t in o[1]]:
                         raise SystemExit("double-buffered graphs: the two captures return different result buffers")
                     if info.world == 1:
                         d2h_stage = [stages["all"][k] for k in (0, 1)]
@@ -577,8 +622,9 @@ def main():
         if gather_dst is None and info.is_main:
             # rank 0's own detections are D2H-copied straight from the graph's result
             # buffers (stream order keeps the next replay behind that copy)
+            own = [torch.empty_like(t) for t in src] if piped else list(src)  # piped: results alternate buffers
             gather_dst = (gbuf["dst"] if gather_in_graph else
-                          [list(src)] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)])
+                          [own] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)])
             host_out = [[[torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in src] for _ in range(info.world)]
                         for _ in range(2)]
         if not gather_in_graph:
@@ -722,6 +768,7 @@ def main():
                 "branch_streams": 2 if side is not None else 1,
                 "graph_mode": args.graph_mode if side is not None else "single",
                 "graph_input_sets": 2 if db else 1,
+                "lidar_pipelined": piped,
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
                 "avg_2d_dets_per_frame": det2,

@@ -111,14 +111,29 @@ class LidarPipeline:
 
     @torch.no_grad()
     def step(self):
-        f = (self.fast or self.build_fast()) if self.use_fast else None  # sets the canvas storage first
+        canvas = self.step_pre()
+        return self.step_post(canvas)
+
+    @torch.no_grad()
+    def step_pre(self):
+        """Unpack + voxelise + PillarVFE scatter into this pipeline's canvas (capture-safe).
+        The two halves let a caller run the next batch's preprocessing beside this one's
+        network (bench.py --lidar-pipeline: two pipelines alternating)."""
+        if self.use_fast and self.fast is None:
+            self.build_fast()  # sets the canvas storage first
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
         self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
-        if f is not None:
+        return canvas
+
+    @torch.no_grad()
+    def step_post(self, canvas=None):
+        """BEV network + decode + rotated NMS over the canvas step_pre filled."""
+        if self.use_fast:
+            f = self.fast or self.build_fast()
             return self.post(*f.forward(self.enc.canvas_nhwc()))
-        cls, box, dir_ = self.model.bev_forward(canvas)
+        cls, box, dir_ = self.model.bev_forward(canvas if canvas is not None else self.enc.canvas_nchw())
         return self.post(cls, box, dir_)
