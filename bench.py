@@ -70,10 +70,13 @@ def parse():
                     help="DP scatter/gather: the C++ RCCL communicator (default) or torch batch_isend_irecv")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
-    ap.add_argument("--lidar-pipeline", type=int, default=0,
-                    help="1: LiDAR software pipeline over two pipelines: step t runs the BEV network / NMS of "
-                         "batch t beside the unpack / voxelise / VFE of batch t+1 (double-buffered graphs only; "
-                         "LiDAR-only 6.81 vs 7.1 ms, headline unchanged: profiles/r3/lpipe/)")
+    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3],
+                    help="LiDAR software pipeline over two LidarPipelines sharing one model (double-buffered "
+                         "graphs only; every step still runs one full batch through every stage, results come "
+                         "out one step later). 0: off. 1: network + NMS of batch t beside preprocessing of "
+                         "batch t+1. 2: preprocessing + network of batch t beside decode + NMS of batch t-1. "
+                         "3 (default): preprocessing + down blocks of batch t beside the fused neck + head + "
+                         "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/)")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
@@ -437,7 +440,7 @@ def main():
     # two captured graphs over two input sets: the prefetch writes straight into the set the next
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
     d2h_stage = None
-    piped = False
+    piped = post_split = False
     # (not with the RCCL gather captured in the step graph: two graphs replaying the same
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
@@ -450,6 +453,7 @@ def main():
         # the step graph is captured twice, once per input set, with its results copied into a
         # per-capture D2H stage
         piped = bool(args.lidar_pipeline) and use_lid and not cp and not sec
+        post_split = piped and args.lidar_pipeline >= 2
         if piped:
             # two LiDAR pipelines over one model: graph k finishes pipeline k's batch (network + NMS)
             # and preprocesses the next batch into pipeline 1-k, whose own data buffer is its input set
@@ -464,10 +468,16 @@ def main():
                     main = torch.cuda.current_stream()
                     lside.wait_stream(main)
                     side2.wait_stream(main)
-                    with torch.cuda.stream(lside):
-                        r3 = lids[k].step_post()
-                    with torch.cuda.stream(side2):
-                        lids[1 - k].step_pre()
+                    if post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
+                        with torch.cuda.stream(lside):
+                            lids[k].step_front(neck_back=args.lidar_pipeline == 3)
+                        with torch.cuda.stream(side2):
+                            r3 = lids[1 - k].step_back()
+                    else:  # graph k: pipeline k's network / NMS beside pipeline 1-k's preprocessing
+                        with torch.cuda.stream(lside):
+                            r3 = lids[k].step_post()
+                        with torch.cuda.stream(side2):
+                            lids[1 - k].step_pre()
                     r2 = cam.step() if use_cam else None
                     main.wait_stream(lside)
                     main.wait_stream(side2)
@@ -485,7 +495,24 @@ def main():
             if not piped:
                 return list(zip(in_sets[k], host_src))
             pairs = [(in_sets[k][0], host_src[0])] if use_cam else []
-            return pairs + [(lids[1 - k].data, pc_host[0]), (lids[1 - k].frame_n, n_host[0])]
+            p = k if post_split else 1 - k  # the pipeline whose preprocessing graph k runs
+            return pairs + [(lids[p].data, pc_host[0]), (lids[p].frame_n, n_host[0])]
+
+        def stage_copy(dst_, src_):
+            # every result tensor into the stage with ONE batched copy kernel (a graph node per
+            # tensor cost ~11 us each at the end of the step: 9 copyBuffer nodes, ~100 us)
+            from triton_client_amd import _native
+            pairs = [(d, t) for d, t in zip(dst_, src_) if t.numel()]
+            if (os.environ.get("TCA_STAGE_COPY", "1") == "0"
+                    or not all(d.is_contiguous() and t.is_contiguous() for d, t in pairs)):
+                for d, t in pairs:
+                    d.copy_(t, non_blocking=True)
+                return
+            dp, sp, nb = (np.asarray(v, np.int64) for v in (
+                [d.data_ptr() for d, _ in pairs], [t.data_ptr() for _, t in pairs],
+                [t.numel() * t.element_size() for _, t in pairs]))
+            _native.call("tca_copy_segments", len(pairs), dp.ctypes.data, sp.ctypes.data, nb.ctypes.data,
+                         _native.stream_ptr(torch.cuda.current_stream()))
 
         def bound(name, _unused, outs_of, k):
             base_fn = base_fns[k]
@@ -502,8 +529,7 @@ def main():
                     src_ = outs_of(res)
                     if stages[name][k] is None:  # allocated in the eager warm-up, before capture
                         stages[name][k] = [torch.empty_like(t) for t in src_]
-                    for d, t in zip(stages[name][k], src_):
-                        d.copy_(t, non_blocking=True)
+                    stage_copy(stages[name][k], src_)
                 return res
             return fn
         unit_runners = {name: [GraphRunner(bound(name, fn, of, k)) for k in (0, 1)] for name, fn, of in units}
@@ -527,8 +553,8 @@ def main():
             db_free[k].record()
             db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
         torch.cuda.synchronize()
-        if piped:
-            lids[0].step_pre()  # prologue: graph 0's first replay finishes pipeline 0's batch
+        if piped:  # prologue: graph 0's first replay finishes a batch of pipeline 0 (mode 1) / 1 (mode 2)
+            lids[1].step_front(neck_back=args.lidar_pipeline == 3) if post_split else lids[0].step_pre()
             torch.cuda.synchronize()
 
         class _DoubleBuffered:
@@ -768,7 +794,7 @@ def main():
                 "branch_streams": 2 if side is not None else 1,
                 "graph_mode": args.graph_mode if side is not None else "single",
                 "graph_input_sets": 2 if db else 1,
-                "lidar_pipelined": piped,
+                "lidar_pipelined": (["off", "pre", "post", "neck"][args.lidar_pipeline] if piped else "off"),
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
                 "avg_2d_dets_per_frame": det2,

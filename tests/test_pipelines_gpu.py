@@ -90,3 +90,43 @@ def test_lidar_graph_replay_twice_is_stable(cuda):
         assert n == int(r2.count[b])
         assert torch.equal(a[0][b, :n], r2.box[b, :n])
         assert torch.equal(a[1][b, :n], r2.score[b, :n])
+
+
+@pytest.mark.parametrize("neck_back", [False, True])
+def test_lidar_post_split_pipelining_matches_step(cuda, neck_back):
+    """bench.py --lidar-pipeline 2: pipeline B's front (preprocessing + network) on one
+    stream beside pipeline A's back (decode + rotated NMS of A's previous front) on
+    another gives A exactly the detections of a plain step()."""
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    la = LidarPipeline(batch=2, max_points=32768, device=cuda)
+    _load_lidar(la, spec, [5, 6])
+    la.calibrate_detection_density(500.0)
+    lb = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
+    _load_lidar(lb, spec, [7, 8])
+
+    def snap(r):
+        return [t.clone() for t in (r.box, r.score, r.count)]
+
+    ref_a = snap(la.step())
+    ref_b = snap(lb.step())
+    torch.cuda.synchronize()
+    la.step_front(neck_back)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    s1.wait_stream(main)
+    s2.wait_stream(main)
+    with torch.cuda.stream(s1):
+        lb.step_front(neck_back)
+    with torch.cuda.stream(s2):
+        got_a = snap(la.step_back())
+    main.wait_stream(s1)
+    main.wait_stream(s2)
+    got_b = snap(lb.step_back())
+    torch.cuda.synchronize()
+    assert int(ref_a[2].sum()) > 0 and int(ref_b[2].sum()) > 0
+    for ref, got in ((ref_a, got_a), (ref_b, got_b)):
+        for b in range(2):
+            n = int(ref[2][b])
+            assert n == int(got[2][b])
+            assert torch.equal(ref[0][b, :n], got[0][b, :n])
+            assert torch.equal(ref[1][b, :n], got[1][b, :n])

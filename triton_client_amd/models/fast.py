@@ -396,6 +396,19 @@ class FastBEV:
             self.neck(self.bb.forward_blocks(canvas), self.hout)
         else:
             self.head(self.bb.forward(canvas), out=self.hout)
+        return self.head_maps()
+
+    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
+        """The down blocks only (pair canvas); forward_neck finishes the batch from their outputs,
+        which stay in this plan's buffers until its next forward_blocks."""
+        assert self.neck is not None and canvas.pair == self.pair
+        return self.bb.forward_blocks(canvas)
+
+    def forward_neck(self, blocks: List[NHWC]):
+        self.neck(blocks, self.hout)
+        return self.head_maps()
+
+    def head_maps(self):
         t = self.hout.t
         return (NHWC(t, 0, self.n_cls), NHWC(t, self.n_cls, self.n_box),
                 NHWC(t, self.n_cls + self.n_box, self.n_dir))

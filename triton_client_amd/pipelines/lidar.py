@@ -130,6 +130,28 @@ class LidarPipeline:
         return canvas
 
     @torch.no_grad()
+    def step_front(self, neck_back: bool = False):
+        """Preprocessing + BEV network; the head maps stay in this pipeline's plan buffers
+        for step_back (bench.py --lidar-pipeline 2: the decode / rotated NMS of one batch,
+        a few low-occupancy kernels, runs beside the next batch's network).  neck_back
+        (--lidar-pipeline 3): stop after the down blocks; step_back runs the fused neck +
+        head as well."""
+        canvas = self.step_pre()
+        self._blocks = self._head = None
+        if self.use_fast and neck_back and self.fast.neck is not None:
+            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc())
+        elif self.use_fast:
+            self._head = self.fast.forward(self.enc.canvas_nhwc())
+        else:
+            self._head = self.model.bev_forward(canvas)
+
+    @torch.no_grad()
+    def step_back(self):
+        """(Neck + head, then) decode + rotated NMS of what the last step_front left."""
+        head = self._head if self._blocks is None else self.fast.forward_neck(self._blocks)
+        return self.post(*head)
+
+    @torch.no_grad()
     def step_post(self, canvas=None):
         """BEV network + decode + rotated NMS over the canvas step_pre filled."""
         if self.use_fast:
