@@ -656,11 +656,12 @@ def main():
                           [own] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)])
             host_out = [[[torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in src] for _ in range(info.world)]
                         for _ in range(2)]
-        if not gather_in_graph:
+        staged = db and d2h_stage is not None and info.world == 1
+        if not gather_in_graph and not staged:  # (one rank with a staged D2H: nothing to gather)
             ex.gather(src, gather_dst if info.is_main else None)
         k = it[0] % 2
         if info.is_main:
-            if db and d2h_stage is not None and info.world == 1:
+            if staged:
                 # the replay already copied its results into stage[j] (graph-side D2D): the D2H runs on
                 # the copy stream beside the next replay, which writes the other stage
                 j = (runner.t - 1) % 2

@@ -49,11 +49,15 @@ def main():
         print(f"{v / n:9.1f} {100 * v / n / ksum:5.1f}% {cnt[k] / n:6.1f}  {k}")
     if a.sequence:
         s, e = starts[-2], starts[-1]
-        print(f"\n# last step in launch order\n{'#':>4} {'us':>8} {'grid':>10}  kernel")
+        t0 = int(rows[s]["Start_Timestamp"])
+        print(f"\n# last step in launch order (start / end: us from the marker's start; q: queue)\n"
+              f"{'#':>4} {'us':>8} {'start':>8} {'end':>8} {'q':>3} {'grid':>10}  kernel")
         for i, r in enumerate(rows[s:e]):
-            us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            b_, e_ = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
             grid = r.get("Grid_Size_X") or r.get("Grid_Size") or ""
-            print(f"{i:4d} {us:8.1f} {grid:>10}  {short(r['Kernel_Name'])}")
+            q = r.get("Queue_Id", "")
+            print(f"{i:4d} {(e_ - b_) / 1e3:8.1f} {b_ / 1e3:8.1f} {e_ / 1e3:8.1f} {q:>3} {grid:>10}  "
+                  f"{short(r['Kernel_Name'])}")
 
 
 if __name__ == "__main__":
