@@ -92,11 +92,13 @@ def test_lidar_graph_replay_twice_is_stable(cuda):
         assert torch.equal(a[1][b, :n], r2.score[b, :n])
 
 
-@pytest.mark.parametrize("neck_back", [False, True])
-def test_lidar_post_split_pipelining_matches_step(cuda, neck_back):
-    """bench.py --lidar-pipeline 2: pipeline B's front (preprocessing + network) on one
-    stream beside pipeline A's back (decode + rotated NMS of A's previous front) on
-    another gives A exactly the detections of a plain step()."""
+@pytest.mark.parametrize("neck_back,side_clean", [(False, False), (True, False), (True, True)])
+def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, side_clean):
+    """bench.py --lidar-pipeline 2 / 3: pipeline B's front (preprocessing + network) on one
+    stream beside pipeline A's back (neck + head / decode + rotated NMS of A's previous
+    front) on another gives A exactly the detections of a plain step().  side_clean: the
+    canvas clear + voxeliser reset of each front on a third stream after the first conv;
+    two rounds over swapped frames catch a canvas cell left uncleared."""
     spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
     la = LidarPipeline(batch=2, max_points=32768, device=cuda)
     _load_lidar(la, spec, [5, 6])
@@ -107,26 +109,35 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back):
     def snap(r):
         return [t.clone() for t in (r.box, r.score, r.count)]
 
-    ref_a = snap(la.step())
-    ref_b = snap(lb.step())
+    ref = {}
+    for name, lp, seeds in (("a1", la, [5, 6]), ("b1", lb, [7, 8]), ("a2", la, [7, 8]), ("b2", lb, [5, 6])):
+        _load_lidar(lp, spec, seeds)
+        ref[name] = snap(lp.step())
     torch.cuda.synchronize()
-    la.step_front(neck_back)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    side = s3 if side_clean else None
     main = torch.cuda.current_stream()
-    s1.wait_stream(main)
-    s2.wait_stream(main)
-    with torch.cuda.stream(s1):
-        lb.step_front(neck_back)
-    with torch.cuda.stream(s2):
-        got_a = snap(la.step_back())
-    main.wait_stream(s1)
-    main.wait_stream(s2)
-    got_b = snap(lb.step_back())
-    torch.cuda.synchronize()
-    assert int(ref_a[2].sum()) > 0 and int(ref_b[2].sum()) > 0
-    for ref, got in ((ref_a, got_a), (ref_b, got_b)):
+    got = {}
+    for rnd, (sa, sb) in enumerate((([5, 6], [7, 8]), ([7, 8], [5, 6])), 1):
+        _load_lidar(la, spec, sa)
+        _load_lidar(lb, spec, sb)
+        torch.cuda.synchronize()
+        la.step_front(neck_back, side)
+        s1.wait_stream(main)
+        s2.wait_stream(main)
+        with torch.cuda.stream(s1):
+            lb.step_front(neck_back, side)
+        with torch.cuda.stream(s2):
+            got[f"a{rnd}"] = snap(la.step_back())
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+        got[f"b{rnd}"] = snap(lb.step_back())
+        torch.cuda.synchronize()
+    for name in ref:
+        r, g = ref[name], got[name]
+        assert int(r[2].sum()) > 0, name
         for b in range(2):
-            n = int(ref[2][b])
-            assert n == int(got[2][b])
-            assert torch.equal(ref[0][b, :n], got[0][b, :n])
-            assert torch.equal(ref[1][b, :n], got[1][b, :n])
+            n = int(r[2][b])
+            assert n == int(g[2][b]), (name, b)
+            assert torch.equal(r[0][b, :n], g[0][b, :n]), (name, b)
+            assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)

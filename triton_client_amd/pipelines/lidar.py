@@ -115,7 +115,7 @@ class LidarPipeline:
         return self.step_post(canvas)
 
     @torch.no_grad()
-    def step_pre(self):
+    def step_pre(self, cleanup: bool = True):
         """Unpack + voxelise + PillarVFE scatter into this pipeline's canvas (capture-safe).
         The two halves let a caller run the next batch's preprocessing beside this one's
         network (bench.py --lidar-pipeline: two pipelines alternating)."""
@@ -123,23 +123,48 @@ class LidarPipeline:
             self.build_fast()  # sets the canvas storage first
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
-        self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
+        self._pc = (pts, cnt)
+        if cleanup or getattr(self, "_dirty", False):
+            self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
-        self.vox.finish(pts, cnt, gather=False)
+        if cleanup:
+            self.vox.finish(pts, cnt, gather=False)
+        # the canvas holds this frame's cells until the next step_pre clears them (cleanup) or
+        # the caller's _cleanup runs
+        self._dirty = cleanup
         return canvas
 
+    def _cleanup(self):
+        """This frame's canvas cells + occupancy bytes back to zero, voxeliser scratch reset
+        (what the next step_pre would otherwise do first / last)."""
+        pts, cnt = self._pc
+        self.enc.clear(self.vox)
+        self.vox.finish(pts, cnt, gather=False)
+
     @torch.no_grad()
-    def step_front(self, neck_back: bool = False):
+    def step_front(self, neck_back: bool = False, side=None):
         """Preprocessing + BEV network; the head maps stay in this pipeline's plan buffers
         for step_back (bench.py --lidar-pipeline 2: the decode / rotated NMS of one batch,
         a few low-occupancy kernels, runs beside the next batch's network).  neck_back
         (--lidar-pipeline 3): stop after the down blocks; step_back runs the fused neck +
-        head as well."""
-        canvas = self.step_pre()
+        head as well.  side (a stream, with neck_back): the canvas clear and voxeliser reset
+        run there once the first conv has read the canvas, off this stream's critical path
+        (joined before return, so the step stays self-contained)."""
+        fast_neck = self.use_fast and neck_back and self.fast is not None and self.fast.neck is not None
+        deferred = side is not None and fast_neck
+        canvas = self.step_pre(cleanup=not deferred)
         self._blocks = self._head = None
-        if self.use_fast and neck_back and self.fast.neck is not None:
-            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc())
+        if fast_neck:
+            main = torch.cuda.current_stream()
+
+            def after_first():
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._cleanup()
+            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc(), after_first if deferred else None)
+            if deferred:
+                main.wait_stream(side)
         elif self.use_fast:
             self._head = self.fast.forward(self.enc.canvas_nhwc())
         else:
