@@ -60,6 +60,7 @@ class LidarPipeline:
         self.post = AnchorPostprocess(self.cfg, batch, device=self.device)
         self.use_fast = fast and self.device.type == "cuda"
         self.fast = None
+        self._dirty = False  # the canvas holds the last frame's cells (the next step_pre clears them)
 
     def build_fast(self):
         from ..models.fast import FastBEV
@@ -84,6 +85,7 @@ class LidarPipeline:
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
         self.enc.set_pair(pair)  # (the next frame's scatter; its clear zeroes these cells)
+        self._dirty = True
         if lsuv:
             h = self.model.head
             lsuv_rescale(self.model, lambda: self.model.bev_forward(canvas), head_modules=[h.conv_cls, h.conv_dir])
@@ -124,7 +126,7 @@ class LidarPipeline:
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
         self._pc = (pts, cnt)
-        if cleanup or getattr(self, "_dirty", False):
+        if cleanup or self._dirty:
             self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
