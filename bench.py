@@ -462,8 +462,8 @@ def main():
                 lp.build_fast()
             side2 = torch.cuda.Stream()
             lside = side if side is not None else torch.cuda.Stream()
-            lclean = torch.cuda.Stream() if os.environ.get("TCA_LIDAR_SIDE_CLEAN", "1") != "0" else None
-            # (the back half starts with the step: held until the front's VFE is done, so that the neck
+            # (the canvas clear moved from the front into the back half: 7.60 vs 7.60 ms, not kept;
+            # the back half starts with the step: held until the front's VFE is done, so that the neck
             # runs beside the backbone convs instead, 9.55 vs 7.43-7.54 ms; a 128 / 64-workgroup neck
             # grid 7.44-7.72 / 8.01-8.06 vs 7.38-7.60; the front on a high-priority stream 9.7 ms)
 
@@ -474,7 +474,7 @@ def main():
                     side2.wait_stream(main)
                     if post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
                         with torch.cuda.stream(lside):
-                            lids[k].step_front(neck_back=args.lidar_pipeline == 3, side=lclean)
+                            lids[k].step_front(neck_back=args.lidar_pipeline == 3)
                         with torch.cuda.stream(side2):
                             r3 = lids[1 - k].step_back()
                     else:  # graph k: pipeline k's network / NMS beside pipeline 1-k's preprocessing
@@ -558,7 +558,7 @@ def main():
             db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
         torch.cuda.synchronize()
         if piped:  # prologue: graph 0's first replay finishes a batch of pipeline 0 (mode 1) / 1 (mode 2)
-            lids[1].step_front(neck_back=args.lidar_pipeline == 3, side=lclean) if post_split else lids[0].step_pre()
+            lids[1].step_front(neck_back=args.lidar_pipeline == 3) if post_split else lids[0].step_pre()
             torch.cuda.synchronize()
 
         class _DoubleBuffered:

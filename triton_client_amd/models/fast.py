@@ -319,16 +319,12 @@ class _BEVBackbonePlan:
             self.ups.append((fc, off, c))
             off += c
 
-    def forward_blocks(self, canvas: NHWC, after_first=None) -> List[NHWC]:
-        """The down blocks only: each block's output (the deblocks' inputs).  after_first:
-        called once the first conv (the only reader of the canvas) has been issued."""
+    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
+        """The down blocks only: each block's output (the deblocks' inputs)."""
         x, outs = canvas, []
         for convs, pp, H, W in self.blocks:
             for i, cv in enumerate(convs):
                 x = cv(x, out=pp[i % 2])
-                if after_first is not None:
-                    after_first()
-                    after_first = None
             outs.append(x)
         return outs
 
@@ -402,11 +398,11 @@ class FastBEV:
             self.head(self.bb.forward(canvas), out=self.hout)
         return self.head_maps()
 
-    def forward_blocks(self, canvas: NHWC, after_first=None) -> List[NHWC]:
+    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
         """The down blocks only (pair canvas); forward_neck finishes the batch from their outputs,
         which stay in this plan's buffers until its next forward_blocks."""
         assert self.neck is not None and canvas.pair == self.pair
-        return self.bb.forward_blocks(canvas, after_first)
+        return self.bb.forward_blocks(canvas)
 
     def forward_neck(self, blocks: List[NHWC]):
         self.neck(blocks, self.hout)

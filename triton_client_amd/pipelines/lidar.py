@@ -60,7 +60,6 @@ class LidarPipeline:
         self.post = AnchorPostprocess(self.cfg, batch, device=self.device)
         self.use_fast = fast and self.device.type == "cuda"
         self.fast = None
-        self._dirty = False  # the canvas holds the last frame's cells (the next step_pre clears them)
 
     def build_fast(self):
         from ..models.fast import FastBEV
@@ -85,7 +84,6 @@ class LidarPipeline:
         canvas = self.enc.encode_from_slots(pts, self.vox)
         self.vox.finish(pts, cnt, gather=False)
         self.enc.set_pair(pair)  # (the next frame's scatter; its clear zeroes these cells)
-        self._dirty = True
         if lsuv:
             h = self.model.head
             lsuv_rescale(self.model, lambda: self.model.bev_forward(canvas), head_modules=[h.conv_cls, h.conv_dir])
@@ -117,7 +115,7 @@ class LidarPipeline:
         return self.step_post(canvas)
 
     @torch.no_grad()
-    def step_pre(self, cleanup: bool = True):
+    def step_pre(self):
         """Unpack + voxelise + PillarVFE scatter into this pipeline's canvas (capture-safe).
         The two halves let a caller run the next batch's preprocessing beside this one's
         network (bench.py --lidar-pipeline: two pipelines alternating)."""
@@ -125,48 +123,23 @@ class LidarPipeline:
             self.build_fast()  # sets the canvas storage first
         pts, cnt = pc2_unpack(self.ws, self.data, self.frame_off, self.frame_n, self.layout, self.max_points,
                               self.normalize, self.z_offset)
-        self._pc = (pts, cnt)
-        if cleanup or self._dirty:
-            self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
+        self.enc.clear(self.vox)  # previous frame's pillars (coords still hold them)
         self.vox.assign(pts, cnt)
         canvas = self.enc.encode_from_slots(pts, self.vox)
-        if cleanup:
-            self.vox.finish(pts, cnt, gather=False)
-        # the canvas holds this frame's cells until the next step_pre clears them (cleanup) or
-        # the caller's _cleanup runs
-        self._dirty = cleanup
+        self.vox.finish(pts, cnt, gather=False)
         return canvas
 
-    def _cleanup(self):
-        """This frame's canvas cells + occupancy bytes back to zero, voxeliser scratch reset
-        (what the next step_pre would otherwise do first / last)."""
-        pts, cnt = self._pc
-        self.enc.clear(self.vox)
-        self.vox.finish(pts, cnt, gather=False)
-
     @torch.no_grad()
-    def step_front(self, neck_back: bool = False, side=None):
+    def step_front(self, neck_back: bool = False):
         """Preprocessing + BEV network; the head maps stay in this pipeline's plan buffers
         for step_back (bench.py --lidar-pipeline 2: the decode / rotated NMS of one batch,
         a few low-occupancy kernels, runs beside the next batch's network).  neck_back
         (--lidar-pipeline 3): stop after the down blocks; step_back runs the fused neck +
-        head as well.  side (a stream, with neck_back): the canvas clear and voxeliser reset
-        run there once the first conv has read the canvas, off this stream's critical path
-        (joined before return, so the step stays self-contained)."""
-        fast_neck = self.use_fast and neck_back and self.fast is not None and self.fast.neck is not None
-        deferred = side is not None and fast_neck
-        canvas = self.step_pre(cleanup=not deferred)
+        head as well."""
+        canvas = self.step_pre()
         self._blocks = self._head = None
-        if fast_neck:
-            main = torch.cuda.current_stream()
-
-            def after_first():
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._cleanup()
-            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc(), after_first if deferred else None)
-            if deferred:
-                main.wait_stream(side)
+        if self.use_fast and neck_back and self.fast.neck is not None:
+            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc())
         elif self.use_fast:
             self._head = self.fast.forward(self.enc.canvas_nhwc())
         else:
