@@ -796,10 +796,14 @@ def main():
                 "comm": comm_used,
                 "hipgraph": not args.no_graph,
                 "ingest_prefetch": prefetch,
-                "branch_streams": 2 if side is not None else 1,
+                "branch_streams": (3 if piped else 2) if side is not None else 1,
                 "graph_mode": args.graph_mode if side is not None else "single",
                 "graph_input_sets": 2 if db else 1,
                 "lidar_pipelined": (["off", "pre", "post", "neck"][args.lidar_pipeline] if piped else "off"),
+                "lidar_pipeline_note": ("two LiDAR pipelines alternate: each timed step runs one full batch through "
+                                        "every stage (batch t's preprocessing + down blocks beside batch t-1's "
+                                        "neck + head + decode + NMS); detections leave one step later"
+                                        if piped else None),
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
                 "avg_2d_dets_per_frame": det2,
