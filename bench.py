@@ -801,8 +801,8 @@ def main():
                 "graph_input_sets": 2 if db else 1,
                 "lidar_pipelined": (["off", "pre", "post", "neck"][args.lidar_pipeline] if piped else "off"),
                 "lidar_pipeline_note": ("two LiDAR pipelines alternate: each timed step runs one full batch through "
-                                        "every stage (batch t's preprocessing + down blocks beside batch t-1's "
-                                        "neck + head + decode + NMS); detections leave one step later"
+                                        "every stage, one batch's first half beside the previous batch's second "
+                                        "half (split point: lidar_pipelined); detections leave one step later"
                                         if piped else None),
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
