@@ -28,6 +28,7 @@ F = ctypes.c_float
 # name -> argtypes (restype is always int = hipError_t)
 _KERNEL_SIGS = {
     "tca_draw_boxes": [P, L, I, I, I, I, P, I, I, P, P, I, P],
+    "tca_draw_annotations": [P, L, I, I, I, I, P, I, I, P, P, P, I, P, I, P],
     # JPEG pixel reconstruction (csrc/kernels/jpeg.hip)
     "tca_jpeg_idct": [P, P, P, P, L, L, I, P],
     "tca_jpeg_color": [P, P, P, L, L, I, P],

@@ -18,6 +18,8 @@ SIGS = {
     "tca_jpeg_probe": (I, [P, ctypes.c_int64, P]),
     "tca_jpeg_decode_coefs": (I, [P, ctypes.c_int64, P, ctypes.c_int64, P, P]),
     "tca_jpeg_decode_batch": (I, [P, P, I, P, ctypes.c_int64, P, P, P, I]),
+    # batched host payload copies into pinned staging (csrc/runtime/host_copy.cpp)
+    "tca_host_gather_copy": (I, [I, P, P, P, I]),
     # host preprocess for GPU-less hosts (csrc/runtime/cpu_image.cpp)
     "tca_cpu_preprocess": (I, [P, I, I, I, I, P, I, I, I, I, I, I, I, ctypes.c_float, I, P, P, I]),
     # native RCCL communicator (csrc/runtime/rccl_comm.cpp)

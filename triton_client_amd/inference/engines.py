@@ -170,17 +170,39 @@ class LocalDetector2D(Detector2D):
         from ..pipelines.detectron import DetectronPipeline
         return DetectronPipeline(self.model, **kw)
 
+    def _calibrated_pipeline(self, hw: Tuple[int, int], sample: Optional[np.ndarray]):
+        """A new pipeline for frames of ``hw``; the first one built sets the
+        random-init head prior from ``sample`` (HxWx3 uint8) once."""
+        p = self._new_pipeline(hw)
+        if self.calibrate_target is not None:  # random-init weights: set the head prior once
+            if sample is None:
+                from ..utils.synthetic import camera_frame
+                sample = camera_frame(hw[0], hw[1], 0)
+            p.frames.copy_(torch.from_numpy(np.array(sample, np.uint8)).to(p.frames.device).expand_as(p.frames))
+            p.calibrate_detection_density(self.calibrate_target)
+            self.calibrate_target = None
+        self.model = p.model
+        return p
+
+    def live(self):
+        """The streaming executor over this engine's model (``inference/live.py``):
+        the live drivers' device path (GPU JPEG ingest, double-buffered graphs,
+        GPU annotation, zero-copy publish); None on a GPU-less host."""
+        if self.device.type != "cuda":
+            return None
+        if getattr(self, "_live", None) is None:
+            from .live import LiveCamera
+            with self._lock:
+                if getattr(self, "_live", None) is None:
+                    self._live = LiveCamera(self)
+        return self._live
+
     def _pipe(self, hw: Tuple[int, int], sample: np.ndarray):
         if hw in self._pipes:
             return self._pipes[hw]
         from ..pipelines import GraphRunner
 
-        p = self._new_pipeline(hw)
-        if self.calibrate_target is not None:  # random-init weights: set the head prior once
-            p.frames.copy_(torch.from_numpy(np.array(sample, np.uint8)).to(p.frames.device).expand_as(p.frames))
-            p.calibrate_detection_density(self.calibrate_target)
-            self.calibrate_target = None
-        self.model = p.model
+        p = self._calibrated_pipeline(hw, sample)
         pinned = torch.empty((self.B, *hw, 3), dtype=torch.uint8, pin_memory=self.device.type == "cuda")
         entry = (p, GraphRunner(p.step, enabled=self.graph), pinned)
         self._pipes[hw] = entry
@@ -332,6 +354,37 @@ class LocalDetector3D(Detector3D):
         from ..pipelines import LidarPipeline
         return LidarPipeline
 
+    def _calibrated_pipeline(self, layout, max_points: int, sample: Optional[msgs.PointCloud2]):
+        """A new pipeline for clouds of ``layout`` (<= max_points points); the
+        first one built sets the random-init head prior from ``sample`` once."""
+        p = self._pipeline_cls()(self.model, batch=self.B, max_points=max_points, layout=layout,
+                                 z_offset=self.z_offset, normalize_intensity=self.normalize, device=self.device)
+        if self.calibrate_target is not None:
+            if sample is None:
+                sample = self._sample_cloud(0)
+            raw = torch.frombuffer(bytearray(sample.data), dtype=torch.uint8)
+            raw = raw[:min(raw.numel(), p.frame_bytes)]
+            for b in range(self.B):
+                p.data[b * p.frame_bytes: b * p.frame_bytes + raw.numel()].copy_(raw)
+            p.frame_n.fill_(min(sample.width * sample.height, p.max_points))
+            p.calibrate_detection_density(self.calibrate_target)
+            self.calibrate_target = None
+        self.model = p.model
+        return p
+
+    def live(self):
+        """The streaming executor over this engine's model (``inference/live.py``):
+        the live driver's device path (pinned payload ring, double-buffered
+        graphs, one D2H of the results per batch)."""
+        if self.device.type != "cuda":
+            return None
+        if getattr(self, "_live", None) is None:
+            from .live import LiveLidar
+            with self._lock:
+                if getattr(self, "_live", None) is None:
+                    self._live = LiveLidar(self)
+        return self._live
+
     def _pipe(self, layout, npts: int, sample: msgs.PointCloud2):
         from ..pipelines import GraphRunner
 
@@ -342,16 +395,7 @@ class LocalDetector3D(Detector3D):
         ent = self._pipes.get(key)
         if ent is not None and ent[0].max_points >= npts:
             return ent
-        p = self._pipeline_cls()(self.model, batch=self.B, max_points=maxp, layout=layout, z_offset=self.z_offset,
-                                 normalize_intensity=self.normalize, device=self.device)
-        if self.calibrate_target is not None:
-            raw = torch.frombuffer(bytearray(sample.data), dtype=torch.uint8)
-            for b in range(self.B):
-                p.data[b * p.frame_bytes: b * p.frame_bytes + raw.numel()].copy_(raw)
-            p.frame_n.fill_(sample.width * sample.height)
-            p.calibrate_detection_density(self.calibrate_target)
-            self.calibrate_target = None
-        self.model = p.model
+        p = self._calibrated_pipeline(layout, maxp, sample)
         pinned = torch.empty((self.B * p.frame_bytes,), dtype=torch.uint8, pin_memory=True)
         ent = (p, GraphRunner(p.step, enabled=self.graph), pinned, torch.zeros(self.B, dtype=torch.int32))
         self._pipes[key] = ent

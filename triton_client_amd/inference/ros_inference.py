@@ -35,16 +35,22 @@ def decode_image_msg(msg) -> np.ndarray:
 
 
 def detections_to_msg(dets: np.ndarray, header: msgs.Header, source: Optional[msgs.Image] = None) -> msgs.Detection2DArray:
-    out = msgs.Detection2DArray(header=header)
-    src = msgs.Image(header=header) if source is None else source
-    for d in np.asarray(dets).reshape(-1, 6):
-        x1, y1, x2, y2, conf, c = (float(v) for v in d)
-        out.detections.append(msgs.Detection2D(
-            header=header, results=[msgs.ObjectHypothesisWithPose(id=int(c), score=conf)],
-            bbox=msgs.BoundingBox2D(center=msgs.Pose2D((x1 + x2) / 2, (y1 + y2) / 2, 0.0), size_x=x2 - x1,
-                                    size_y=y2 - y1),
-            source_img=src))
-    return out
+    """Detection2DArray over dets [n, 6]; the Detection2D objects are built only
+    if a subscriber reads ``detections`` (:class:`~triton_client_amd.ros.msgs.ArrayList`,
+    columns ``{"dets": dets}``)."""
+    dets = np.asarray(dets, np.float32).reshape(-1, 6)
+
+    def build():
+        src = msgs.Image(header=header) if source is None else source
+        out = []
+        for x1, y1, x2, y2, conf, c in dets.tolist():
+            out.append(msgs.Detection2D(
+                header=header, results=[msgs.ObjectHypothesisWithPose(id=int(c), score=conf)],
+                bbox=msgs.BoundingBox2D(center=msgs.Pose2D((x1 + x2) / 2, (y1 + y2) / 2, 0.0), size_x=x2 - x1,
+                                        size_y=y2 - y1),
+                source_img=src))
+        return out
+    return msgs.Detection2DArray(header=header, detections=msgs.ArrayList(len(dets), build, {"dets": dets}))
 
 
 class RosInference(BaseInference):
@@ -97,10 +103,28 @@ class RosInference(BaseInference):
             self.det_pub.publish(det)
 
     # ------------------------------------------------------------------ work
+    def _live(self):
+        """The engine's streaming device path (LocalDetector2D on a GPU), else None."""
+        if not hasattr(self, "_live_exec"):
+            fn = getattr(self.engine, "live", None)
+            self._live_exec = fn() if callable(fn) else None
+        return self._live_exec
+
     def process(self, images: Sequence) -> List[tuple]:
         """Messages → [(annotated Image msg, Detection2DArray, dets [n,6])]."""
         t0 = time.perf_counter()
         timer = StageTimer(self.metrics)
+        live = self._live()
+        if live is not None:  # device path: GPU decode, graph step, GPU annotation, zero-copy Image
+            with timer("device"):
+                res = live.process(images, draw=self.draw, names=self.class_names)
+            with timer("messages"):
+                out = [(im, detections_to_msg(d, m.header), d) for m, (im, d) in zip(images, res)]
+            self.frames += len(images)
+            if self.metrics is not None:
+                self.metrics.stage("frame", (time.perf_counter() - t0) / max(len(images), 1))
+                self.metrics.frame(len(images))
+            return out
         with timer("decode"):
             rgb = [decode_image_msg(m) for m in images]
         gpu_draw = self.draw and hasattr(self.engine, "detect_annotated") and \

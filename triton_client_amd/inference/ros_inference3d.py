@@ -30,18 +30,35 @@ def select_boxes(pred: dict, labels: Optional[Sequence[int]] = (2,), score_thres
     return np.nonzero(keep)[0]
 
 
+def jsk_columns(pred: dict, idx) -> dict:
+    """The published fields of the selected boxes as columns (float64 like the
+    message): position [n, 3], orientation [n, 4] (yaw about +z, reference
+    ``yaw2quaternion`` :117-118), dimensions [n, 3] with the reference's x/y
+    swap (:169-171), value [n] fp32, label [n] uint32."""
+    idx = np.asarray(idx, np.int64)
+    b = np.asarray(pred["pred_boxes"])[idx].astype(np.float64)
+    yaw = b[:, 8 if b.shape[-1] >= 9 else 6] if len(b) else np.zeros((0,))
+    quat = np.zeros((len(b), 4))
+    quat[:, 2], quat[:, 3] = np.sin(yaw / 2), np.cos(yaw / 2)
+    return {"position": b[:, :3], "orientation": quat, "dimensions": b[:, [4, 3, 5]] if len(b) else np.zeros((0, 3)),
+            "value": np.asarray(pred["pred_scores"])[idx].astype(np.float32),
+            "label": np.asarray(pred["pred_labels"])[idx].astype(np.uint32)}
+
+
 def boxes_to_jsk(pred: dict, idx, header: msgs.Header) -> msgs.BoundingBoxArray:
-    arr = msgs.BoundingBoxArray(header=header)
-    b = pred["pred_boxes"]
-    yaw_i = 8 if b.shape[-1] >= 9 else 6
-    for i in idx:
-        x = b[i]
-        arr.boxes.append(msgs.BoundingBox(
-            header=header,
-            pose=msgs.Pose(msgs.Point(float(x[0]), float(x[1]), float(x[2])), compat.yaw2quaternion(float(x[yaw_i]))),
-            dimensions=msgs.Vector3(float(x[4]), float(x[3]), float(x[5])),
-            value=float(pred["pred_scores"][i]), label=int(pred["pred_labels"][i])))
-    return arr
+    """jsk BoundingBoxArray of the selected boxes, built from columns: the
+    BoundingBox objects are made only if a subscriber reads ``boxes``
+    (:class:`~triton_client_amd.ros.msgs.ArrayList`); serialisation packs the
+    columns directly (``ros.rosmsg``)."""
+    cols = jsk_columns(pred, idx)
+
+    def build():
+        P, Q, D = cols["position"].tolist(), cols["orientation"].tolist(), cols["dimensions"].tolist()
+        V, L = cols["value"].tolist(), cols["label"].tolist()
+        return [msgs.BoundingBox(header=header, pose=msgs.Pose(msgs.Point(*p), msgs.Quaternion(*q)),
+                                 dimensions=msgs.Vector3(*d), value=v, label=lb)
+                for p, q, d, v, lb in zip(P, Q, D, V, L)]
+    return msgs.BoundingBoxArray(header=header, boxes=msgs.ArrayList(len(cols["value"]), build, cols))
 
 
 def boxes_to_detection3d(pred: dict, idx, header: msgs.Header) -> msgs.Detection3DArray:
@@ -106,11 +123,19 @@ class RosInference3D(BaseInference):
         hdr = msgs.Header(seq=header.seq, stamp=header.stamp, frame_id=header.frame_id)
         return boxes_to_jsk(pred, idx, hdr) if self.jsk else boxes_to_detection3d(pred, idx, hdr)
 
+    def _live(self):
+        """The engine's streaming device path (LocalDetector3D on a GPU), else None."""
+        if not hasattr(self, "_live_exec"):
+            fn = getattr(self.engine, "live", None)
+            self._live_exec = fn() if callable(fn) else None
+        return self._live_exec
+
     def process(self, clouds: Sequence[msgs.PointCloud2]) -> List[tuple]:
         t0 = time.perf_counter()
         timer = StageTimer(self.metrics)
+        live = self._live()
         with timer("detect3d"):
-            preds = self.engine.detect(clouds)
+            preds = live.process(clouds) if live is not None else self.engine.detect(clouds)
         with timer("boxes_publish"):
             out = [(self.to_msg(p, c.header), p) for c, p in zip(clouds, preds)]
         self.frames += len(clouds)

@@ -266,3 +266,41 @@ def draw_boxes_(frames: torch.Tensor, box: torch.Tensor, cls: torch.Tensor, coun
             x = box[b, k].tolist()
             draw_rect(img, x[0], x[1], x[2], x[3], class_color(int(cls[b, k])), thickness)
     return frames
+
+
+def draw_annotations_(frames: torch.Tensor, box: torch.Tensor, score: torch.Tensor, cls: torch.Tensor,
+                      count: torch.Tensor, names_dev: torch.Tensor | None = None, names=None, thickness: int = 2,
+                      stream=None) -> torch.Tensor:
+    """K15 with labels: every result box's rectangle, then its ``"<name> <conf>"``
+    label, drawn in place on uint8 frames [B, H, W, 3] (``tca_draw_annotations``;
+    capture-safe).  ``names_dev``: the [n, 32] uint8 device table of
+    :func:`triton_client_amd.utils.draw.names_table` (None: numeric class ids).
+    Pixel-identical to :func:`triton_client_amd.utils.draw.draw_detections`
+    (``names``: the same class names, used by the CPU path)."""
+    B, H, W, C = frames.shape
+    if C != 3 or frames.dtype != torch.uint8 or frames.stride(2) != 3 or frames.stride(1) != 3 * W:
+        raise ValueError("frames must be [B, H, W, 3] uint8 with contiguous rows")
+    if box.dim() != 3 or box.shape[0] != B or box.shape[2] < 4 or not box.is_contiguous():
+        raise ValueError("box must be contiguous [B, K, >=4]")
+    if (tuple(cls.shape) != tuple(box.shape[:2]) or cls.dtype != torch.int32 or count.dtype != torch.int32
+            or tuple(score.shape) != tuple(box.shape[:2]) or score.dtype != torch.float32):
+        raise ValueError("score [B, K] fp32, cls [B, K] int32 and count [B] int32")
+    if frames.is_cuda:
+        if names_dev is not None and (names_dev.dtype != torch.uint8 or names_dev.dim() != 2
+                                      or names_dev.shape[1] != 32 or not names_dev.is_cuda):
+            raise ValueError("names_dev must be a [n, 32] uint8 device table")
+        nn = 0 if names_dev is None else names_dev.shape[0]
+        _native.call("tca_draw_annotations", _native.ptr(frames), frames.stride(0), B, H, W, frames.stride(1),
+                     _native.ptr(box), box.shape[1], box.shape[2], _native.ptr(score.contiguous()),
+                     _native.ptr(cls.contiguous()), _native.ptr(count), thickness,
+                     _native.ptr(names_dev) if nn else 0, nn, _native.stream_ptr(stream))
+        return frames
+    from ..utils.draw import draw_detections
+
+    cnt = count.numpy()
+    for b in range(B):
+        k = min(int(cnt[b]), box.shape[1])
+        d = np.concatenate([box[b, :k, :4].numpy(), score[b, :k, None].numpy(),
+                            cls[b, :k, None].numpy().astype(np.float32)], 1)
+        draw_detections(frames[b].numpy(), d, names, thickness)
+    return frames

@@ -17,13 +17,16 @@ import torch
 
 class GraphRunner:
     def __init__(self, fn: Callable[[], object], warmup: int = 3, enabled: bool = True,
-                 pool=None):
+                 pool=None, capture_error_mode: str = "global"):
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.out = None
         self.warmup = warmup
         self.pool = pool
+        # "thread_local": other host threads may keep issuing HIP calls (event
+        # waits, pinned allocations) while this thread captures (live drivers)
+        self.capture_error_mode = capture_error_mode
 
     def capture(self) -> None:
         if not self.enabled:
@@ -36,7 +39,7 @@ class GraphRunner:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        with torch.cuda.graph(g, pool=self.pool, capture_error_mode=self.capture_error_mode):
             self.out = self.fn()
         self.graph = g
 

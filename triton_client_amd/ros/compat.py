@@ -91,6 +91,8 @@ class Publisher:
         if self._bus is not None:
             self._bus.publish(self.topic, msg)
         else:
+            if isinstance(getattr(msg, "data", None), memoryview):  # genpy packs uint8[] from bytes
+                msg.data = msg.data.tobytes()
             self._impl.publish(msg)
 
     def get_num_connections(self) -> int:

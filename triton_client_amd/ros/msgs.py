@@ -10,6 +10,62 @@ from dataclasses import dataclass, field, fields, is_dataclass
 from typing import Any, Dict, List
 
 
+class ArrayList(list):
+    """A message's list field (``BoundingBoxArray.boxes``, ``Detection2DArray.detections``)
+    kept as the detector's columns until something reads it.
+
+    The live drivers publish one message per frame at thousands of frames/s;
+    building every ``BoundingBox`` / ``Detection2D`` object up front costs more
+    host time than the GPU step.  This list is built by ``build()`` on first
+    access (iteration, indexing, ``len`` is known without building), so a
+    subscriber that reads the field sees ordinary message objects, while one
+    that only forwards or serialises the message never pays for them
+    (``ros.rosmsg`` serialises an unbuilt BoundingBoxArray straight from the
+    columns).  ``columns`` holds the arrays it was made from."""
+
+    def __init__(self, n: int, build, columns=None):
+        super().__init__()
+        self._n, self._build, self.columns = int(n), build, columns
+
+    @property
+    def built(self) -> bool:
+        return self._build is None
+
+    def _fill(self) -> None:
+        b = self._build
+        if b is not None:
+            self._build = None
+            list.extend(self, b())
+
+    def __len__(self):
+        return self._n if self._build is not None else list.__len__(self)
+
+    def __bool__(self):
+        return len(self) > 0
+
+    def __reduce__(self):  # pickles / deep-copies as a plain list of messages
+        self._fill()
+        return (list, (list(list.__iter__(self)),))
+
+
+def _filled(name):
+    base = getattr(list, name)
+
+    def method(self, *a, **kw):
+        self._fill()
+        return base(self, *a, **kw)
+    method.__name__ = name
+    return method
+
+
+for _m in ("__iter__", "__getitem__", "__contains__", "__eq__", "__ne__", "__repr__", "__reversed__", "__add__",
+           "__mul__", "__rmul__", "__iadd__", "__imul__", "__setitem__", "__delitem__", "__lt__", "__le__",
+           "__gt__", "__ge__", "index", "count", "copy", "append", "extend", "insert", "pop", "remove", "sort",
+           "reverse", "clear"):
+    setattr(ArrayList, _m, _filled(_m))
+ArrayList.__hash__ = None
+
+
 @dataclass
 class Time:
     secs: int = 0

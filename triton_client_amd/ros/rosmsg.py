@@ -198,7 +198,32 @@ def _write_scalar(buf: bytearray, value: Any, base: str) -> None:
         _write_msg(buf, value, base)
 
 
+def _write_jsk_columns(buf: bytearray, msg: Any) -> None:
+    """BoundingBoxArray whose boxes are still columns (``msgs.ArrayList`` from the
+    live driver): every box record is fixed-size (its header is the array's), so
+    the whole array is one packed structured-array write."""
+    import numpy as np
+
+    cols = msg.boxes.columns
+    hdr = bytearray()
+    _write_msg(hdr, msg.header, "std_msgs/Header")
+    n = len(cols["value"])
+    rec = np.zeros(n, np.dtype([("h", f"V{len(hdr)}"), ("p", "<f8", 3), ("q", "<f8", 4), ("d", "<f8", 3),
+                                ("v", "<f4"), ("l", "<u4")]))
+    if n:
+        rec["h"] = np.frombuffer(bytes(hdr), f"V{len(hdr)}")[0]
+        rec["p"], rec["q"], rec["d"] = cols["position"], cols["orientation"], cols["dimensions"]
+        rec["v"], rec["l"] = cols["value"], cols["label"]
+    buf += hdr
+    buf += struct.pack("<I", n)
+    buf += rec.tobytes()
+
+
 def _write_msg(buf: bytearray, msg: Any, msg_type: str) -> None:
+    if (msg_type == "jsk_recognition_msgs/BoundingBoxArray" and isinstance(getattr(msg, "boxes", None), msgs.ArrayList)
+            and not msg.boxes.built and msg.boxes.columns is not None and "position" in msg.boxes.columns):
+        _write_jsk_columns(buf, msg)
+        return
     for f in spec(msg_type)[1]:
         _write(buf, _get(msg, f.name, msg_type, f) if msg is not None else None, f, msg_type)
 
