@@ -23,10 +23,10 @@ namespace {
 struct SweepRing {
   float* ring;        // [R][B][maxp][4]
   int* ring_n;        // [R][B]
-  float* ring_t;      // [R][B]
+  double* ring_t;     // [R][B] timestamps (fp64: epoch-second stamps / hours of auto-clock keep ms lags)
   float* ring_pose;   // [R][B][12]
   int* head;          // [1]
-  float* clock;       // [B] current timestamps
+  double* clock;      // [B] current timestamps (fp64)
   float* pose;        // [B][12] current poses
   int R, B, maxp;
 };
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(256) sweep_merge_kernel(const float* __restric
 #pragma unroll
   for (int a = 0; a < 3; ++a) o[a] = Tc[a] * q[0] + Tc[4 + a] * q[1] + Tc[8 + a] * q[2];
   o[3] = p[3];
-  o[4] = r.clock[b] - r.ring_t[slot * r.B + b];
+  o[4] = (float)(r.clock[b] - r.ring_t[slot * r.B + b]);
 }
 
 __global__ void __launch_bounds__(256) sweep_push_kernel(const float* __restrict__ cur, int cs,
@@ -85,10 +85,10 @@ __global__ void __launch_bounds__(256) sweep_push_kernel(const float* __restrict
   *reinterpret_cast<float4*>(r.ring + (((long)slot * r.B + b) * r.maxp + i) * 4) = make_float4(p[0], p[1], p[2], p[3]);
 }
 
-__global__ void sweep_advance_kernel(SweepRing r, float dt) {
+__global__ void sweep_advance_kernel(SweepRing r, double dt) {
   const int t = threadIdx.x;
   if (t == 0) *r.head = (*r.head + 1) % r.R;
-  if (dt != 0.f)
+  if (dt != 0.0)
     for (int b = t; b < r.B; b += blockDim.x) r.clock[b] += dt;
 }
 
@@ -97,9 +97,10 @@ __global__ void sweep_advance_kernel(SweepRing r, float dt) {
 // cur [B, maxp, cs] (cs >= 4) unpacked points with counts cur_n [B]; ring state as in
 // SweepRing; out [B, (R + 1) * maxp, 5], out_n [B].  dt: seconds added to every
 // clock after the step (0: the caller sets the clock from message stamps).
+// ring_t [R, B] and clock [B] are fp64 seconds.
 TCA_API int tca_sweep_step(const float* cur, int cs, const int* cur_n, int B, int maxp, int R, float* ring, int* ring_n,
-                           float* ring_t, float* ring_pose, int* head, float* clock, float* pose, float dt, float* out,
-                           int* out_n, hipStream_t stream) {
+                           double* ring_t, float* ring_pose, int* head, double* clock, float* pose, double dt,
+                           float* out, int* out_n, hipStream_t stream) {
   if (B <= 0) return 0;
   if (R < 1 || R > 31 || cs < 4 || maxp <= 0) return (int)hipErrorInvalidValue;
   SweepRing r{ring, ring_n, ring_t, ring_pose, head, clock, pose, R, B, maxp};

@@ -320,6 +320,33 @@ def test_sweep_ring_gpu_matches_reference(cuda):
 
 
 @pytest.mark.gpu
+def test_sweep_ring_epoch_clock_keeps_ms_lags(cuda):
+    """Message stamps in epoch seconds (~1.7e9 s) and an auto-advanced clock after
+    hours of streaming: the time-lag feature stays exact to well under a ms (the
+    ring's stamps are fp64; fp32 stamps would quantise them to 128 s)."""
+    from triton_client_amd.ops.lidar import SweepAccumulator
+
+    B, maxp, S = 2, 64, 3
+    pts = torch.ones((B, maxp, 4), device=cuda)
+    n = torch.full((B,), maxp, dtype=torch.int32, device=cuda)
+    acc = SweepAccumulator(S, B, maxp, cuda, dt=0.0)
+    t0 = 1.7e9 + 0.123
+    for step in range(3):
+        acc.clock.fill_(t0 + 0.05 * step)
+        out, cnt = acc(pts, n)
+    torch.cuda.synchronize()
+    lags = out[0, :S * maxp, 4].cpu().numpy().reshape(S, maxp)[:, 0]
+    np.testing.assert_allclose(lags, [0.0, 0.05, 0.1], atol=1e-6)
+    auto = SweepAccumulator(S, B, maxp, cuda, dt=0.05)
+    auto.clock.fill_(3600.0 * 5)  # five hours in
+    for _ in range(3):
+        out, cnt = auto(pts, n)
+    torch.cuda.synchronize()
+    lags = out[1, :S * maxp, 4].cpu().numpy().reshape(S, maxp)[:, 0]
+    np.testing.assert_allclose(lags, [0.0, 0.05, 0.1], atol=1e-6)
+
+
+@pytest.mark.gpu
 def test_centerpoint_pipeline_multisweep_graph(cuda):
     """nsweeps = 3: the merged point list feeds the voxeliser and the PFN (time lag
     as the 5th feature); the ring advances inside the captured graph, so the first

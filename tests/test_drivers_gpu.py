@@ -248,8 +248,19 @@ def test_served_device_shared_memory_matches_raw_wire(cuda):
                 d2.close_shm()
                 d3.close_shm()
         assert len(ch2.cuda_shared_memory_status().regions) == 0
+        # a registration claiming more bytes than the handle maps, or another GPU, is refused
+        import grpc
+        from triton_client_amd.utils.hip_ipc import DeviceAllocation
+        alloc = DeviceAllocation(1 << 20, cuda)
+        for nbytes, dev in ((4 << 20, alloc.device_id), (1 << 20, alloc.device_id + 1)):
+            with pytest.raises(grpc.RpcError):
+                ch2.register_cuda_shared_memory("bad", alloc.handle, dev, nbytes)
+        ch2.register_cuda_shared_memory("ok", alloc.handle, alloc.device_id, 1 << 20)
+        assert len(ch2.cuda_shared_memory_status().regions) == 1
+        ch2.unregister_cuda_shared_memory("ok")
         ch2.close()
         ch3.close()
+        alloc.close()
     finally:
         srv.terminate()
         srv.wait(60)

@@ -308,6 +308,42 @@ def test_shm_unregister_waits_for_in_flight_executions(tmp_path):
         os.unlink(path)
 
 
+def test_device_region_lease_defers_close(monkeypatch):
+    """A device region a queued request still holds stays mapped through an
+    unregister (its name is gone at once); the last release closes it.  A region
+    on another device than the server's models is refused."""
+    import torch
+
+    from triton_client_amd.server.model import InferError
+    from triton_client_amd.server.shm import Region, SharedMemoryRegistry
+
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    closed = []
+
+    class Dev:
+        device = "cpu"
+
+        def close(self):
+            closed.append(1)
+
+    reg = SharedMemoryRegistry(pin=False, device_id=0)
+    reg._regions["a"] = Region("a", "", 0, 64, None, dev=Dev())
+    held = reg.lease(["a", "a"])
+    assert len(held) == 1 and held[0].inflight == 1
+    reg.unregister("", device=True)  # "unregister all", e.g. from another client
+    assert closed == [] and reg.status(device=True) == []
+    with pytest.raises(InferError):
+        reg.lease(["a"])
+    reg.release(held)
+    assert closed == [1]
+    reg._regions["b"] = Region("b", "", 0, 64, None, dev=Dev())
+    reg.release(reg.lease(["b"]))  # not unregistered: stays open
+    reg.unregister("b", device=True)
+    assert closed == [1, 1]
+    with pytest.raises(InferError, match="device 1"):
+        reg.register_device("c", bytes(64), 1, 64)
+
+
 def test_multi_process_server_shares_the_port_and_stops_cleanly():
     """--procs 3: three server processes on one port (SO_REUSEPORT); every connection is
     served, and SIGTERM to the parent ends the children too (the port is free again)."""

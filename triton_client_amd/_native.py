@@ -70,7 +70,7 @@ _KERNEL_SIGS = {
     # coords, nump, vcount, B, V, P, nz, ny, nx, flags, stream
     "tca_voxel_check": [P, P, P, I, I, I, I, I, I, P, P],
     # cur, cs, cur_n, B, maxp, R, ring, ring_n, ring_t, ring_pose, head, clock, pose, dt, out, out_n, stream
-    "tca_sweep_step": [P, I, P, I, I, I, P, P, P, P, P, P, P, F, P, P, P],
+    "tca_sweep_step": [P, I, P, I, I, I, P, P, P, P, P, P, P, ctypes.c_double, P, P, P],
     # src, B, H, W, dst, dst_dtype, dst_layout, sc0, sc1, sc2, b0, b1, b2, stream
     "tca_planar_affine": [P, I, I, I, P, I, I, F, F, F, F, F, F, P],
     "tca_conv_nhwc_x3p_occ": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P, P],

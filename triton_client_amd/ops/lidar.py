@@ -272,10 +272,11 @@ class SweepAccumulator:
         f = dict(dtype=torch.float32, device=dev)
         self.ring = torch.zeros((self.R, batch, max_points, 4), **f)
         self.ring_n = torch.zeros((self.R, batch), dtype=torch.int32, device=dev)
-        self.ring_t = torch.zeros((self.R, batch), **f)
+        # fp64 stamps: message times in epoch seconds (or hours of auto-clock) keep ms-exact lags
+        self.ring_t = torch.zeros((self.R, batch), dtype=torch.float64, device=dev)
         self.ring_pose = torch.zeros((self.R, batch, 12), **f)
         self.head = torch.zeros((1,), dtype=torch.int32, device=dev)
-        self.clock = torch.zeros((batch,), **f)
+        self.clock = torch.zeros((batch,), dtype=torch.float64, device=dev)
         self.pose = torch.tensor(IDENTITY_POSE, **f).repeat(batch, 1).contiguous()
         self.out = torch.zeros((batch, nsweeps * max_points, 5), **f)
         self.out_n = torch.zeros((batch,), dtype=torch.int32, device=dev)

@@ -17,7 +17,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--procs", type=int, default=1,
                     help="server processes sharing the port (SO_REUSEPORT), each with its own copy of the models on "
                          "the GPU and its own Python interpreter: the kernel spreads client connections over them. "
-                         "Repository-control RPCs (load / unload) act on the process that receives them.")
+                         "Repository-control RPCs (load / unload) act on the process that receives them, and so do "
+                         "shared-memory registrations (system and device): a client must register its regions and "
+                         "infer over the same gRPC channel (connection), which one process serves; after a reconnect "
+                         "it registers again.")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--export-repository", default=None, metavar="DIR",
                     help="write a Triton-layout repository for --models into DIR and exit")

@@ -99,6 +99,17 @@ def decode_inputs(req, shm=None) -> Dict[str, np.ndarray]:
     return out
 
 
+def request_regions(req) -> List[str]:
+    """Names of the shared-memory regions a request's inputs and outputs reference."""
+    from .shm import tensor_shm
+    names = []
+    for t in list(req.inputs) + list(req.outputs):
+        ref = tensor_shm(t.parameters)
+        if ref is not None:
+            names.append(ref[0])
+    return names
+
+
 def output_slices(req, shm) -> Optional[Dict[str, np.ndarray]]:
     """{output name: uint8 view of its shared-memory slice} for the outputs a request
     asks to receive in shared memory (None: none does)."""
@@ -187,7 +198,15 @@ class GRPCInferenceServicer:
         self.metrics = metrics
         self.server_name, self.version = server_name, version
         from .shm import SharedMemoryRegistry
-        self.shm = SharedMemoryRegistry()
+        dev_id = None
+        try:
+            import torch
+            d = torch.device(getattr(repo, "device", "cpu") or "cpu")
+            if d.type == "cuda" and torch.cuda.is_available():
+                dev_id = d.index if d.index is not None else torch.cuda.current_device()
+        except Exception:  # noqa: BLE001 - a CPU-only server has no device regions to check
+            dev_id = None
+        self.shm = SharedMemoryRegistry(device_id=dev_id)
 
     # -------------------------------------------------------------- health / metadata
     def ServerLive(self, req, ctx):
@@ -248,7 +267,10 @@ class GRPCInferenceServicer:
         return pb.RepositoryModelLoadResponse()
 
     def RepositoryModelUnload(self, req, ctx):
-        self.repo.unload(req.model_name)
+        try:
+            self.repo.unload(req.model_name)
+        except InferError as e:  # a batch stuck on the device: the model stays loaded, not ready
+            ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, str(e))
         return pb.RepositoryModelUnloadResponse()
 
     # -------------------------------------------------------------- inference
@@ -259,7 +281,11 @@ class GRPCInferenceServicer:
             time.sleep(self.fault.delay_s)
         if self.fault.roll(self.fault.drop_rate):
             ctx.abort(grpc.StatusCode.UNAVAILABLE, "fault injection: dropped request")
+        leased = []
         try:
+            # device regions stay mapped until this request's batch has run and its response is
+            # encoded, even if the client (or another one) unregisters them meanwhile
+            leased = self.shm.lease(request_regions(req))
             inputs = decode_inputs(req, self.shm)
             if PROFILE.on:
                 PROFILE.add("pb.decode_inputs", time.perf_counter() - t0)
@@ -271,6 +297,8 @@ class GRPCInferenceServicer:
             if self.metrics:
                 self.metrics.request(m.name, False, time.perf_counter() - t0)
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        finally:
+            self.shm.release(leased)
         if self.metrics:
             self.metrics.request(m.name, True, time.perf_counter() - t0)
         return resp

@@ -182,14 +182,23 @@ class DynamicBatcher:
             raise item.exc
         return item.result
 
-    def stop(self) -> None:
+    def stop(self, timeout_s: float = 60.0) -> None:
         """Stop taking requests and wait for the batch in flight (if any) to
-        finish: the model frees its plans only after no batch runs on them."""
+        finish: the model frees its plans only after no batch runs on them.
+        Raises :class:`InferError` if a batch is still running after
+        ``timeout_s`` (e.g. stuck on a hung device wait): the caller must then
+        leave the model loaded-but-not-ready rather than free live plans, and
+        a control RPC never blocks forever."""
         with self.cv:
             self.stopped = True
             self.cv.notify_all()
+        deadline = time.perf_counter() + timeout_s
         for t in self.threads:
-            t.join()
+            t.join(max(0.0, deadline - time.perf_counter()))
+        stuck = [t.name for t in self.threads if t.is_alive()]
+        if stuck:
+            raise InferError(f"model '{self.model.name}': batcher threads {stuck} still running after "
+                             f"{timeout_s:g} s; not unloaded")
 
     def _take(self):
         with self.cv:
@@ -338,7 +347,11 @@ class ServedModel(ABC):
 
     def unload(self) -> None:
         if self._batcher is not None:
-            self._batcher.stop()
+            try:
+                self._batcher.stop()
+            except InferError:
+                self.ready = False  # no new requests; the plans stay allocated under the stuck batch
+                raise
             self._batcher = None
         # no execution of this model (batched or direct) is mid-run past this point
         GPU_PHASE.acquire_exclusive()

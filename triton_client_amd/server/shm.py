@@ -61,6 +61,10 @@ class Region:
     dev: Optional[object] = None  # device region: utils.hip_ipc.OpenedHandle
     device_id: int = 0
     _views: Optional[dict] = None
+    # device regions: requests holding a lease (their batch may still read / write the
+    # mapping); an unregister while any is held defers the close to the last release
+    inflight: int = 0
+    closing: bool = False
 
     @property
     def device(self) -> bool:
@@ -121,10 +125,14 @@ def _host_unregister(mm: mmap.mmap) -> None:
 
 
 class SharedMemoryRegistry:
-    def __init__(self, pin: bool = True):
+    """``device_id``: the GPU the served models run on (device regions on another
+    GPU are refused: the server's copy kernels read them as same-device memory)."""
+
+    def __init__(self, pin: bool = True, device_id: Optional[int] = None):
         self._regions: Dict[str, Region] = {}
         self._lock = threading.Lock()
         self.pin = pin
+        self.device_id = device_id
 
     def register(self, name: str, key: str, offset: int, byte_size: int) -> Region:
         if not name:
@@ -164,6 +172,9 @@ class SharedMemoryRegistry:
                 raise InferError(f"shared memory region '{name}' already registered")
         if byte_size <= 0:
             raise InferError(f"device shared memory region '{name}': byte_size {byte_size}")
+        if self.device_id is not None and int(device_id) != self.device_id:
+            raise InferError(f"device shared memory region '{name}' is on device {device_id}; this server's models "
+                             f"run on device {self.device_id}")
         try:
             from ..utils.hip_ipc import OpenedHandle
             h = OpenedHandle(raw_handle, byte_size, device_id)
@@ -177,13 +188,47 @@ class SharedMemoryRegistry:
             self._regions[name] = r
         return r
 
+    def lease(self, names) -> list:
+        """Hold the device regions a request references until :meth:`release`:
+        an unregister meanwhile removes the name but leaves the mapping open
+        for this request's batch (closed by the last release)."""
+        regs = []
+        with self._lock:
+            for n in set(names):
+                r = self._regions.get(n)
+                if r is None:
+                    raise InferError(f"unable to find shared memory region '{n}'")
+                if r.dev is not None:
+                    regs.append(r)
+            for r in regs:
+                r.inflight += 1
+        return regs
+
+    def release(self, regs) -> None:
+        done = []
+        with self._lock:
+            for r in regs:
+                r.inflight -= 1
+                if r.inflight == 0 and r.closing:
+                    done.append(r)
+        if done:
+            self._close(done)
+
     def unregister(self, name: str = "", device: Optional[bool] = None) -> None:
-        """Unregister ``name`` (or every region of the kind: device True / system False / both None)."""
+        """Unregister ``name`` (or every region of the kind: device True / system False / both None).
+        A device region a queued or running request still holds (:meth:`lease`) is
+        closed when that request releases it."""
         with self._lock:
             names = [name] if name else [n for n, r in self._regions.items() if device is None or r.device == device]
             regs = [self._regions.pop(n) for n in names if n in self._regions]
-        if not regs:
-            return
+            for r in regs:
+                if r.dev is not None and r.inflight > 0:
+                    r.closing = True
+            regs = [r for r in regs if not r.closing]
+        if regs:
+            self._close(regs)
+
+    def _close(self, regs) -> None:
         from .model import GPU_PHASE
 
         # An execution that chose the direct (pinned) path for a view of this region

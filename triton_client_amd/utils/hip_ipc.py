@@ -50,6 +50,8 @@ def _hip() -> ctypes.CDLL:
                                    ("hipIpcGetMemHandle", [ctypes.POINTER(_Handle), vp]),
                                    ("hipIpcOpenMemHandle", [pp, _Handle, ctypes.c_uint]),
                                    ("hipIpcCloseMemHandle", [vp]), ("hipSetDevice", [ctypes.c_int]),
+                                   ("hipGetDevice", [ctypes.POINTER(ctypes.c_int)]),
+                                   ("hipMemGetAddressRange", [pp, ctypes.POINTER(ctypes.c_size_t), vp]),
                                    ("hipGetErrorString", [ctypes.c_int])):
                     f = getattr(lib, name)
                     f.argtypes = args
@@ -110,20 +112,45 @@ class DeviceAllocation:
 
 
 class OpenedHandle:
-    """The server side: another process's allocation mapped into this one."""
+    """The server side: another process's allocation mapped into this one.
+
+    The client's declared ``nbytes`` is checked against the size of the
+    allocation actually mapped (``hipMemGetAddressRange``), so a region view can
+    never reach past it, and the calling thread's current device is restored
+    afterwards (a gRPC worker thread must not be left on another GPU)."""
 
     def __init__(self, raw_handle: bytes, nbytes: int, device_id: int):
         if len(raw_handle) != HANDLE_BYTES:
             raise ValueError(f"raw_handle must be {HANDLE_BYTES} bytes, got {len(raw_handle)}")
         self.nbytes, self.device_id = int(nbytes), int(device_id)
+        if self.nbytes <= 0:
+            raise ValueError(f"byte_size {self.nbytes}")
         self.device = torch.device("cuda", self.device_id)
+        self.ptr = 0
         hip = _hip()
-        _check(hip.hipSetDevice(self.device_id), "hipSetDevice")
-        h = _Handle()
-        ctypes.memmove(ctypes.addressof(h), raw_handle, HANDLE_BYTES)
-        p = ctypes.c_void_p()
-        _check(hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _LAZY_PEER_ACCESS), "hipIpcOpenMemHandle")
-        self.ptr = int(p.value)
+        prev = ctypes.c_int(-1)
+        _check(hip.hipGetDevice(ctypes.byref(prev)), "hipGetDevice")
+        try:
+            _check(hip.hipSetDevice(self.device_id), "hipSetDevice")
+            h = _Handle()
+            ctypes.memmove(ctypes.addressof(h), raw_handle, HANDLE_BYTES)
+            p = ctypes.c_void_p()
+            _check(hip.hipIpcOpenMemHandle(ctypes.byref(p), h, _LAZY_PEER_ACCESS), "hipIpcOpenMemHandle")
+            self.ptr = int(p.value)
+            base, size = ctypes.c_void_p(), ctypes.c_size_t()
+            _check(hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(self.ptr)),
+                   "hipMemGetAddressRange")
+            mapped = int(base.value or 0) + int(size.value) - self.ptr
+            if self.nbytes > mapped:
+                raise ValueError(f"byte_size {self.nbytes} exceeds the {mapped} bytes the handle maps")
+        except Exception:
+            if self.ptr:
+                hip.hipIpcCloseMemHandle(ctypes.c_void_p(self.ptr))
+                self.ptr = 0
+            raise
+        finally:
+            if prev.value >= 0:
+                hip.hipSetDevice(prev.value)
         self.tensor = device_tensor(self.ptr, self.nbytes, self.device)
 
     def close(self) -> None:
