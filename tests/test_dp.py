@@ -100,7 +100,8 @@ def _worker(rank, world, port, q):
                     np.testing.assert_allclose(a[k], b[k], rtol=1e-6)
             dp3.close()
         else:
-            assert dp.serve() == 3  # one 7-frame batch + the 2 single-frame calls of the mixed batch
+            # the 7-frame batch; the mixed batch's single-frame steps run on rank 0 alone
+            assert dp.serve() == 1
             assert dp3.serve() == 1
         barrier(info)
         shutdown(info)
@@ -157,8 +158,7 @@ def _fault_worker(rank, world, port, q):
             assert dp.serve() == 3
             q.put((1, "ok"))
         else:
-            hdr = dp._recv_header()
-            dp._step(hdr, None)
+            assert dp.serve(max_steps=1) == 1
             mon.stop()
             os._exit(0)  # simulated crash: no close, no heartbeat, sockets drop
         mon.stop()

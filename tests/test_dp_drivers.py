@@ -1,0 +1,251 @@
+"""The data-parallel live drivers over the node's shared host ring
+(parallel/host_ring.py, parallel/ring_dp.py, csrc/runtime/host_ring.cpp):
+cross-process signalling, NUMA binding, and 2-rank replays of the fixture bag
+whose outputs must be bit-identical to a single rank's (CPU here; on the GPU
+box the same replays run two ranks on the one card over gloo)."""
+import multiprocessing as mp
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = os.path.join(ROOT, "tests", "fixtures", "ros1_sensors.bag")
+
+
+def _runtime_or_skip():
+    from triton_client_amd import _native
+    try:
+        return _native.runtime()
+    except _native.NativeError:
+        pytest.skip("runtime library not built")
+
+
+# ------------------------------------------------------------------ host ring signalling
+def _peer(name, q):
+    from triton_client_amd.parallel.host_ring import HostRing
+
+    ring = HostRing(name)
+    for seq in range(1, 7):
+        s = seq % ring.nslots
+        assert ring.wait_ready(s, seq, 10000)
+        hdr = ring.header(s)
+        data = ring.use_generation(int(hdr[1]), int(hdr[2]))
+        v = data.slot(s)[:8].copy()
+        data.slot(s)[8:16] = v[::-1]  # an "output"
+        ring.ack(s, 1, seq)
+    q.put("ok")
+
+
+def test_host_ring_cross_process():
+    _runtime_or_skip()
+    from triton_client_amd.parallel.host_ring import HostRing
+
+    name = f"tca_test_ring_{os.getpid()}"
+    ring = HostRing(name, nslots=3, world=2, create=True, pin=False)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_peer, args=(name, q))
+    p.start()
+    try:
+        for seq in range(1, 7):
+            s = seq % 3
+            if seq > 3:
+                assert ring.wait_acks(s, [1], seq - 3, 10000) == []
+            if seq in (1, 4):  # a new data generation mid-stream
+                ring.new_generation(4096 * seq)
+            data = ring.data
+            data.slot(s)[:8] = np.arange(seq, seq + 8, dtype=np.uint8)
+            hdr = ring.header(s)
+            hdr[1], hdr[2] = ring.gen, data.slot_bytes
+            ring.publish(s, seq)
+        for seq in range(4, 7):
+            s = seq % 3
+            assert ring.wait_acks(s, [1], seq, 10000) == []
+            np.testing.assert_array_equal(ring.data.slot(s)[8:16], np.arange(seq, seq + 8, dtype=np.uint8)[::-1])
+        assert q.get(timeout=30) == "ok"
+        # a rank that never acks: the wait times out and names it
+        assert ring.wait_acks(0, [1, 2], 100, 50) == [1, 2]
+        assert not ring.wait_ready(0, 99, 20)
+    finally:
+        p.join(10)
+        ring.close()
+    assert not os.path.exists(ring.ctl_path) and not os.path.exists(ring.data_path(1))
+
+
+def test_numa_binding_from_sysfs(tmp_path, monkeypatch):
+    from triton_client_amd.parallel import numa
+
+    assert numa.parse_cpulist("0-3,8,10-11") == {0, 1, 2, 3, 8, 10, 11}
+    for bdf, vendor, cls, cpus in (("0000:05:00.0", "0x1002", "0x038000", "0-1"),
+                                   ("0000:15:00.0", "0x1002", "0x038000", "2-3"),
+                                   ("0000:16:00.0", "0x8086", "0x038000", "4-5"),   # not AMD
+                                   ("0000:17:00.0", "0x1002", "0x020000", "6-7")):  # not a GPU
+        d = tmp_path / bdf
+        d.mkdir()
+        (d / "vendor").write_text(vendor + "\n")
+        (d / "class").write_text(cls + "\n")
+        (d / "local_cpulist").write_text(cpus + "\n")
+    root = str(tmp_path)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert [os.path.basename(d) for d in numa.amd_gpus(root)] == ["0000:05:00.0", "0000:15:00.0"]
+    assert numa.gpu_cpus(1, root) == {2, 3}
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert numa.gpu_cpus(0, root) == {2, 3}
+    before = os.sched_getaffinity(0)
+    try:
+        got = numa.bind_to_gpu(0, root)
+        want = {2, 3} & before
+        assert got == (want if want and want != before else None)
+        if got:
+            assert os.sched_getaffinity(0) == want
+    finally:
+        os.sched_setaffinity(0, before)
+    monkeypatch.setenv("TCA_NUMA_BIND", "0")
+    assert numa.bind_to_gpu(0, root) is None
+
+
+# ------------------------------------------------------------------ bag replays, 1 rank vs 2 ranks
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, ranks, device, extra_env=None):
+    env = dict(os.environ, OMP_NUM_THREADS="2", TCA_DP_HEARTBEAT="0")
+    if extra_env:
+        env.update(extra_env)
+    if ranks == 1:
+        cmd = [sys.executable, "-m"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m"] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+def _bag_messages(path, topic):
+    from triton_client_amd.ros.bag import Bag
+    with Bag(path) as b:
+        return [m for _, m, _ in b.read_messages(topics=[topic])]
+
+
+def _replay_pair(tmp_path, device, env=None):
+    out = {}
+    for ranks in (1, 2):
+        ob2, ob3 = str(tmp_path / f"cam{ranks}.bag"), str(tmp_path / f"pc{ranks}.bag")
+        _run(["triton_client_amd.cli.bag2d", "--bag", FIX, "--engine", "local", "--device", device, "--out", "",
+              "--out-bag", ob2, "--frames-per-step", "2"], ranks, device, env)
+        _run(["triton_client_amd.cli.bag3d", "--bag", FIX, "--engine", "local", "--device", device, "--out-bag", ob3,
+              "--labels", "all", "--score-thresh", "0", "--frames-per-step", "1"], ranks, device, env)
+        out[ranks] = (_bag_messages(ob2, "/aver_01/camera_color/detection/detections"),
+                      _bag_messages(ob2, "/aver_01/camera_color/detection"),
+                      _bag_messages(ob3, "/detections_3d"))
+    return out
+
+
+def _assert_identical(out):
+    from triton_client_amd.ros import rosmsg
+
+    d1, im1, b1 = out[1]
+    d2, im2, b2 = out[2]
+    assert len(d1) == len(d2) == 3 and len(b1) == len(b2) == 2
+    assert [m.header.seq for m in d2] == [m.header.seq for m in d1]
+    for a, b in zip(d1 + im1 + b1, d2 + im2 + b2):  # byte-identical messages
+        assert rosmsg.serialize(a) == rosmsg.serialize(b)
+    assert sum(len(m.boxes) for m in b1) > 0
+
+
+def test_bag_replays_two_ranks_identical_cpu(tmp_path):
+    _runtime_or_skip()
+    _assert_identical(_replay_pair(tmp_path, "cpu"))
+
+
+@pytest.mark.gpu
+def test_bag_replays_two_ranks_identical_gpu(cuda, tmp_path):
+    """The verdict's rehearsal: bag2d / bag3d --engine local on the GPU, two ranks on the
+    one card (gloo), the node batch through the host ring; outputs == one rank's."""
+    _assert_identical(_replay_pair(tmp_path, "cuda", {"TCA_DIST_BACKEND": "gloo"}))
+
+
+def _dp_camera_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import faulthandler
+    faulthandler.dump_traceback_later(280, exit=True)
+    try:
+        import io
+
+        import torch
+        from PIL import Image
+
+        from triton_client_amd.inference.engines import LocalDetector2D
+        from triton_client_amd.parallel.dp import DataParallelDetector2D, init_distributed
+        from triton_client_amd.ros import msgs
+        from triton_client_amd.utils.synthetic import camera_frame
+
+        info = init_distributed("gloo")
+        det = LocalDetector2D(batch=3, device=info.device, letterbox=True, names=[f"c{i}" for i in range(80)])
+        det.calibrate_synthetic(0)
+        dp = DataParallelDetector2D(det, info)
+        if info.is_main:
+            jp = []
+            for i in range(7):
+                buf = io.BytesIO()
+                Image.fromarray(camera_frame(240, 320, 30 + i)).save(buf, format="JPEG", quality=85)
+                jp.append(buf.getvalue())
+            ms = [msgs.CompressedImage(header=msgs.Header(seq=i + 1), format="jpeg", data=d) for i, d in enumerate(jp)]
+            got = dp.live().process(ms, draw=True, names=det.names)
+            held = [im for im, _ in got]  # published messages still viewing the ring
+            again = dp.live().process(ms, draw=True, names=det.names)  # slots in use: a new data generation
+            dp.close()
+            want = det.live().process(ms, draw=True, names=det.names)
+            assert sum(len(d) for _, d in want) > 0
+            for res in (got, again):
+                for (im, d), (wim, wd), m in zip(res, want, ms):
+                    np.testing.assert_array_equal(d, wd)
+                    assert im.header is m.header and bytes(im.data) == bytes(wim.data)
+            assert held[0].data.obj is not None
+            q.put((0, "ok"))
+        else:
+            q.put((rank, f"served {dp.serve()}"))
+        torch.cuda.synchronize()
+        q.close()
+        q.join_thread()
+        os._exit(0)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        q.close()
+        q.join_thread()
+        os._exit(1)
+
+
+@pytest.mark.gpu
+def test_dp_camera_jpeg_annotated_two_ranks(cuda):
+    """JPEG messages through the ring on two ranks (each decodes its own shard on the
+    device, annotated frames DMA'd into the ring): detections and published images
+    equal one rank's live path bit for bit."""
+    import torch.multiprocessing as tmp
+
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_camera_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    # 7 frames, batch 3 per rank: steps of 6 (3 + 3) and 1 (rank 0 alone), twice
+    assert res == {0: "ok", 1: "served 2"}, res

@@ -20,6 +20,12 @@ SIGS = {
     "tca_jpeg_decode_batch": (I, [P, P, I, P, ctypes.c_int64, P, P, P, I]),
     # batched host payload copies into pinned staging (csrc/runtime/host_copy.cpp)
     "tca_host_gather_copy": (I, [I, P, P, P, I]),
+    # node host ring signalling (csrc/runtime/host_ring.cpp)
+    "tca_ring_publish": (I, [P, ctypes.c_uint32]),
+    "tca_ring_load": (ctypes.c_uint32, [P]),
+    "tca_ring_wait": (I, [P, ctypes.c_uint32, ctypes.c_int64]),
+    "tca_ring_wait_all": (I, [P, I, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64,
+                              ctypes.POINTER(ctypes.c_uint64)]),
     # host preprocess for GPU-less hosts (csrc/runtime/cpu_image.cpp)
     "tca_cpu_preprocess": (I, [P, I, I, I, I, P, I, I, I, I, I, I, I, ctypes.c_float, I, P, P, I]),
     # native RCCL communicator (csrc/runtime/rccl_comm.cpp)

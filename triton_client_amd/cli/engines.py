@@ -107,12 +107,8 @@ def maybe_data_parallel(engine, three_d: bool = False):
     from ..parallel.dp import DataParallelDetector2D, DataParallelDetector3D, init_distributed
 
     info = init_distributed()
-    if hasattr(engine, "calibrate_synthetic"):
-        engine.calibrate_synthetic()
-    if hasattr(engine, "model"):
-        from ..models.common import broadcast_parameters
-
-        broadcast_parameters(engine.model)  # every replica runs rank 0's weights
+    # random-init weights: every rank calibrates the head prior from the same frame, the node
+    # batch's first (what one GPU does); the DP gather checks that the replicas' weights agree
     # rank-failure detection: heartbeats over the c10d store; a dead rank's
     # shards are re-split over the survivors (TCA_DP_HEARTBEAT=0 disables)
     monitor = None
@@ -121,6 +117,32 @@ def maybe_data_parallel(engine, three_d: bool = False):
 
         monitor = HealthMonitor(info, timeout=float(os.environ.get("TCA_DP_HEARTBEAT_TIMEOUT", "5")))
     box_dim = 9 if getattr(engine, "family", "") == "centerpoint" else 7
-    wrap = (DataParallelDetector3D(engine, info, box_dim=box_dim, monitor=monitor) if three_d
-            else DataParallelDetector2D(engine, info, monitor=monitor))
+    comm = native_comm(info)
+    wrap = (DataParallelDetector3D(engine, info, box_dim=box_dim, monitor=monitor, comm=comm) if three_d
+            else DataParallelDetector2D(engine, info, monitor=monitor, comm=comm))
     return wrap, info
+
+
+_COMM = {}
+
+
+def native_comm(info):
+    """The C++ RCCL communicator for the DP detection gather (one per process, shared
+    by the 2D and 3D detectors), or None under the gloo rehearsal / on CPU.  Every
+    rank takes the same decision (an all-reduce of the outcome)."""
+    import torch.distributed as dist
+
+    if info.world <= 1 or info.device.type != "cuda" or dist.get_backend() != "nccl":
+        return None
+    if "comm" not in _COMM:
+        import torch
+
+        from ..parallel.rccl import NativeComm
+        try:
+            comm = NativeComm.from_info(info)
+        except Exception:  # noqa: BLE001 - the process group's own RCCL path still serves
+            comm = None
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=info.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        _COMM["comm"] = comm if int(ok.item()) else None
+    return _COMM["comm"]

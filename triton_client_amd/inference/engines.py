@@ -208,6 +208,7 @@ class LocalDetector2D(Detector2D):
         self._pipes[hw] = entry
         return entry
 
+    @torch.no_grad()
     def calibrate_synthetic(self, seed: int = 0) -> None:
         """Set the random-init head prior from a synthetic frame (same on every
         rank, so data-parallel replicas agree before the parameter broadcast)."""
@@ -410,6 +411,7 @@ class LocalDetector3D(Detector3D):
         pts = lidar_sweep(spec, seed)
         return create_cloud_xyzi(np.frombuffer(pts.tobytes(), np.float32).reshape(-1, 4))
 
+    @torch.no_grad()
     def calibrate_synthetic(self, seed: int = 0) -> None:
         """Set the random-init head prior from a synthetic sweep (rank-independent)."""
         if self.calibrate_target is None:

@@ -151,8 +151,14 @@ class _CameraEngine:
                     self.live.threads)
 
     # ------------------------------------------------------------------ one batch
-    def run(self, batch: Sequence) -> List[tuple]:
+    def submit(self, batch: Sequence, out_frames: Optional[Sequence[torch.Tensor]] = None):
+        """Stage ``batch`` (<= B messages of this engine's kind and geometry) and
+        enqueue its device work; returns the pending batch for :meth:`finish`.
+        ``out_frames``: page-locked [H, W, 3] host tensors (one per message) the
+        annotated frames are copied into instead of a fresh pinned buffer."""
         n = len(batch)
+        if not 0 < n <= self.B:
+            raise ValueError(f"{n} frames for a batch of {self.B}")
         s = self.slots.acquire()
         ticket = None
         try:
@@ -178,15 +184,25 @@ class _CameraEngine:
                 def copies(k):
                     return [(self.ex.inputs[k][0], s.frames[:n])]
                 pre = None
-            ticket = self.ex.submit(copies, pre, lambda k: [self.ex.inputs[k][0][:n]])
-            ticket.wait()
+            if out_frames is not None:
+                ticket = self.ex.submit(copies, pre, lambda k: [self.ex.inputs[k][0][i] for i in range(n)],
+                                        extras_dst=list(out_frames))
+            else:
+                ticket = self.ex.submit(copies, pre, lambda k: [self.ex.inputs[k][0][:n]])
         finally:
+            # the slot is read by the H2D (and the host-decoded frames by pre() on the compute
+            # stream): free once the batch's last device work is done
             self.slots.release(s, ticket.done if ticket is not None else None)
+        return SimpleNamespace(batch=batch, ticket=ticket, out_frames=out_frames)
+
+    def finish(self, pend) -> List[tuple]:
+        """-> [(Image, dets [n, 6])] of a submitted batch (waits for its D2H)."""
+        ticket, batch = pend.ticket.wait(), pend.batch
         res = ticket.result()
         cnt = res.count.numpy()
         box, score, cls = res.box.numpy(), res.score.numpy(), res.cls.numpy()
-        frames = ticket.extras[0].numpy()
         H, W = self.hw
+        frames = [f.numpy() for f in ticket.extras] if pend.out_frames is not None else ticket.extras[0].numpy()
         out = []
         for j, m in enumerate(batch):
             c = int(min(cnt[j], box.shape[1]))
@@ -198,6 +214,15 @@ class _CameraEngine:
                             data=memoryview(frames[j].reshape(-1)))  # zero-copy view of the pinned D2H buffer
             out.append((im, d))
         return out
+
+    def run(self, batch: Sequence) -> List[tuple]:
+        return self.finish(self.submit(batch))
+
+    def zero_stage(self) -> List[torch.Tensor]:
+        """Result-shaped device zeros (an empty shard's part of a gather)."""
+        if getattr(self, "_zero", None) is None:
+            self._zero = [torch.zeros_like(t) for t in self.ex.stage[0]]
+        return self._zero
 
 
 class LiveCamera:
@@ -287,8 +312,10 @@ class _LidarEngine:
             return s
         self.slots = PinnedSlots(live.slots, make_slot)
 
-    def run(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
+    def submit(self, clouds: Sequence[msgs.PointCloud2]):
         n, fb, step = len(clouds), self.fb, self.layout.point_step
+        if not 0 < n <= self.B:
+            raise ValueError(f"{n} clouds for a batch of {self.B}")
         counts = [int(c.width * c.height) for c in clouds]
         sizes = [k * step for k in counts]
         for c, sz in zip(clouds, sizes):
@@ -308,10 +335,20 @@ class _LidarEngine:
                 return [(d[j * fb:j * fb + sz], s.data[j * fb:j * fb + sz]) for j, sz in enumerate(sizes) if sz] + \
                     [(nd, s.n)]
             ticket = self.ex.submit(copies)
-            ticket.wait()
         finally:
             self.slots.release(s, ticket.uploaded if ticket is not None else None)
-        return self.live.det._frames_out(ticket.result())[:n]
+        return SimpleNamespace(n=n, ticket=ticket)
+
+    def finish(self, pend) -> List[dict]:
+        return self.live.det._frames_out(pend.ticket.wait().result())[:pend.n]
+
+    def run(self, clouds: Sequence[msgs.PointCloud2]) -> List[dict]:
+        return self.finish(self.submit(clouds))
+
+    def zero_stage(self) -> List[torch.Tensor]:
+        if getattr(self, "_zero", None) is None:
+            self._zero = [torch.zeros_like(t) for t in self.ex.stage[0]]
+        return self._zero
 
 
 class LiveLidar:

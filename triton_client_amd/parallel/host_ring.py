@@ -1,0 +1,226 @@
+"""The node's shared host ring: how a batch of sensor messages reaches every GPU.
+
+Data-parallel drivers run one process per GPU (``torchrun`` / self-launch).
+The ROS subscriber lives in rank 0; instead of copying the node batch to rank
+0's GPU and scattering it over xGMI (what the bench's ``--ingest rccl``
+measures), rank 0 writes the batch's raw message payloads — JPEG bytes, rgb8
+rows, PointCloud2 records — into one slot of a POSIX shared-memory ring, and
+every rank pulls *its own shard* straight out of that mapping over its own
+PCIe link (the mapping is page-locked in every process, so the H2D is a DMA
+from the shared pages).  Each rank decodes its own JPEGs on its own (NUMA-
+local) cores.  Annotated frames come back the same way: each rank DMAs them
+into the slot's output area.  Only the detections travel over RCCL.
+
+Two shared-memory files per ring:
+
+* control ``/dev/shm/<name>_ctl``: a header page, then per slot a 64 KiB
+  control block — the slot's ``ready`` sequence word, one ``ack`` word per
+  rank (each on its own cache line), a 64-int header and the item table;
+* data ``/dev/shm/<name>_d<gen>``: per slot ``slot_bytes`` of payload + output
+  area.  When a batch needs more room rank 0 starts a new generation (after
+  every slot has drained); the header names the generation and peers attach
+  to it on sight.
+
+Signalling is by 32-bit sequence words with release/acquire ordering and
+futex sleep/wake (``csrc/runtime/host_ring.cpp``): rank 0 writes a slot, then
+``publish(ready, seq)``; a rank waits for ``ready >= seq``, reads its shard,
+writes its outputs and ``publish(ack[rank], seq)``; rank 0 reuses a slot only
+after every participant's ack of its previous sequence number.
+
+Reference: none — the reference has no parallelism; this is the
+"host ring shared by the sensor process" of SURVEY §5.8 / ``parallel/dp.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import mmap
+import os
+from typing import Iterable, List, Optional
+
+import numpy as np
+
+from .. import _native
+
+MAGIC = 0x54434152494E4731  # "TCARING1"
+CTL_SLOT = 1 << 16
+HDR_INTS = 64
+ITEM_INTS = 8
+ITEMS_OFF = 8192
+MAX_ITEMS = (CTL_SLOT - ITEMS_OFF) // (ITEM_INTS * 8)
+ACK_OFF, ACK_STRIDE = 64, 64  # bytes: ack word of rank r at ACK_OFF + r * ACK_STRIDE
+HDR_OFF = ACK_OFF + 64 * ACK_STRIDE
+
+
+def _rt():
+    return _native.runtime()
+
+
+def _open(path: str, size: int, create: bool) -> mmap.mmap:
+    flags = os.O_RDWR | (os.O_CREAT | os.O_TRUNC if create else 0)
+    fd = os.open(path, flags, 0o600)
+    try:
+        if create:
+            os.ftruncate(fd, size)
+        elif os.fstat(fd).st_size < size:
+            raise RuntimeError(f"{path}: {os.fstat(fd).st_size} bytes, expected {size}")
+        return mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+    finally:
+        os.close(fd)
+
+
+def _host_register(mm: mmap.mmap, size: int) -> bool:
+    """Page-lock a mapping for DMA in this process (hipHostRegister)."""
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return False
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+        return int(torch.cuda.cudart().cudaHostRegister(addr, size, 0)) == 0
+    except Exception:  # noqa: BLE001 - an unpinned ring still works (the copies are staged)
+        return False
+
+
+def _host_unregister(mm: mmap.mmap) -> None:
+    try:
+        import torch
+        torch.cuda.cudart().cudaHostUnregister(ctypes.addressof(ctypes.c_char.from_buffer(mm)))
+    except Exception:  # noqa: BLE001
+        pass
+
+
+class DataRing:
+    """One generation's payload / output area: ``nslots`` slots of ``slot_bytes``."""
+
+    def __init__(self, path: str, nslots: int, slot_bytes: int, create: bool, pin: bool):
+        self.path, self.nslots, self.slot_bytes = path, nslots, slot_bytes
+        self.mm = _open(path, nslots * slot_bytes, create)
+        self.buf = np.frombuffer(self.mm, np.uint8)
+        self.base = self.buf.ctypes.data
+        self.pinned = _host_register(self.mm, nslots * slot_bytes) if pin else False
+
+    def slot(self, s: int) -> np.ndarray:
+        return self.buf[s * self.slot_bytes:(s + 1) * self.slot_bytes]
+
+    def close(self, unlink: bool = False) -> None:
+        if self.pinned:
+            _host_unregister(self.mm)
+            self.pinned = False
+        self.buf = None
+        try:
+            self.mm.close()
+        except BufferError:  # views still published (zero-copy messages): the mapping goes with them
+            pass
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+class HostRing:
+    """Control ring + the current data generation.  Rank 0 ``create``s, the
+    other ranks ``attach`` (after a barrier)."""
+
+    def __init__(self, name: str, nslots: int = 4, world: int = 1, create: bool = False, pin: bool = True):
+        if not name or "/" in name:
+            raise ValueError(f"ring name {name!r}")
+        if world > 64:
+            raise ValueError("at most 64 ranks share one host ring")
+        self.name, self.pin = name, pin
+        self.ctl_path = os.path.join("/dev/shm", name + "_ctl")
+        size = 4096 + nslots * CTL_SLOT
+        if create:
+            self.mm = _open(self.ctl_path, size, True)
+            hdr = np.frombuffer(self.mm, np.int64, 4, 0)
+            hdr[:] = (MAGIC, nslots, world, 0)
+        else:
+            mm = _open(self.ctl_path, 4096, False)
+            magic, nslots, world, _ = np.frombuffer(mm, np.int64, 4, 0).tolist()
+            mm.close()
+            if magic != MAGIC:
+                raise RuntimeError(f"{self.ctl_path} is not a host ring")
+            self.mm = _open(self.ctl_path, 4096 + nslots * CTL_SLOT, False)
+        self.nslots, self.world = int(nslots), int(world)
+        self.ctl = np.frombuffer(self.mm, np.uint8)
+        self.ctl_base = self.ctl.ctypes.data
+        self.data: Optional[DataRing] = None
+        self.gen = -1
+        self.owner = create
+
+    # ------------------------------------------------------------------ layout
+    def _blk(self, s: int) -> int:
+        return 4096 + s * CTL_SLOT
+
+    def ready_addr(self, s: int) -> int:
+        return self.ctl_base + self._blk(s)
+
+    def ack_addr(self, s: int, rank: int) -> int:
+        return self.ctl_base + self._blk(s) + ACK_OFF + rank * ACK_STRIDE
+
+    def header(self, s: int) -> np.ndarray:
+        return np.frombuffer(self.mm, np.int64, HDR_INTS, self._blk(s) + HDR_OFF)
+
+    def items(self, s: int) -> np.ndarray:
+        return np.frombuffer(self.mm, np.int64, MAX_ITEMS * ITEM_INTS, self._blk(s) + ITEMS_OFF).reshape(
+            MAX_ITEMS, ITEM_INTS)
+
+    # ------------------------------------------------------------------ data generations
+    def data_path(self, gen: int) -> str:
+        return os.path.join("/dev/shm", f"{self.name}_d{gen}")
+
+    def new_generation(self, slot_bytes: int) -> DataRing:
+        """Rank 0: a (larger) data area; the caller has drained every slot."""
+        old = self.data
+        self.gen += 1
+        slot_bytes = (int(slot_bytes) + 4095) // 4096 * 4096
+        self.data = DataRing(self.data_path(self.gen), self.nslots, slot_bytes, True, self.pin)
+        if old is not None:
+            old.close(unlink=True)
+        return self.data
+
+    def use_generation(self, gen: int, slot_bytes: int) -> DataRing:
+        """Peers: attach the generation a header names."""
+        if gen != self.gen:
+            if self.data is not None:
+                self.data.close()
+            self.data = DataRing(self.data_path(gen), self.nslots, slot_bytes, False, self.pin)
+            self.gen = gen
+        return self.data
+
+    # ------------------------------------------------------------------ signalling
+    def publish(self, s: int, seq: int) -> None:
+        _rt().tca_ring_publish(self.ready_addr(s), seq & 0xFFFFFFFF)
+
+    def wait_ready(self, s: int, seq: int, timeout_ms: int = -1) -> bool:
+        return _rt().tca_ring_wait(self.ready_addr(s), seq & 0xFFFFFFFF, timeout_ms) == 0
+
+    def ack(self, s: int, rank: int, seq: int) -> None:
+        _rt().tca_ring_publish(self.ack_addr(s, rank), seq & 0xFFFFFFFF)
+
+    def wait_acks(self, s: int, ranks: Iterable[int], seq: int, timeout_ms: int = -1) -> List[int]:
+        """Ranks (of ``ranks``) that had not acked ``seq`` when the wait ended."""
+        mask = 0
+        for r in ranks:
+            mask |= 1 << r
+        if not mask:
+            return []
+        missing = ctypes.c_uint64(0)
+        rc = _rt().tca_ring_wait_all(self.ack_addr(s, 0), ACK_STRIDE // 4, mask, seq & 0xFFFFFFFF, timeout_ms,
+                                     ctypes.byref(missing))
+        if rc < 0:
+            raise RuntimeError("tca_ring_wait_all: bad arguments")
+        return [r for r in range(64) if (missing.value >> r) & 1]
+
+    def close(self) -> None:
+        if self.data is not None:
+            self.data.close(unlink=self.owner)
+            self.data = None
+        try:
+            self.mm.close()
+        except BufferError:
+            pass
+        if self.owner:
+            try:
+                os.unlink(self.ctl_path)
+            except FileNotFoundError:
+                pass

@@ -86,12 +86,15 @@ def copy_segments(dst: Sequence[torch.Tensor], src: Sequence[torch.Tensor], stre
 
 class Ticket:
     """One submitted batch: ``wait()`` blocks (GIL released) until its results
-    and extras are in the pinned host tensors."""
+    and extras are in the pinned host tensors.  ``stage`` / ``ran``: the
+    device copies of the results and the event after which they are complete
+    (for device consumers such as the data-parallel gather, which then
+    :meth:`StreamExecutor.hold` the set until they are done reading)."""
 
     def __init__(self, k: int, done: torch.cuda.Event, host: List[torch.Tensor], extras: List[torch.Tensor],
-                 uploaded: torch.cuda.Event, template):
+                 uploaded: torch.cuda.Event, template, ran: torch.cuda.Event, stage: List[torch.Tensor]):
         self.k, self.done, self.host, self.extras, self.uploaded = k, done, host, extras, uploaded
-        self.template = template
+        self.template, self.ran, self.stage = template, ran, stage
 
     def wait(self):
         self.done.synchronize()
@@ -127,7 +130,7 @@ class StreamExecutor:
         self.compute = torch.cuda.Stream(self.device)
         self.h2d = torch.cuda.Stream(self.device)
         self.d2h = torch.cuda.Stream(self.device)
-        self.set_free: List[Optional[torch.cuda.Event]] = [None] * sets
+        self.set_free: List[List[torch.cuda.Event]] = [[] for _ in range(sets)]
         self.next = 0
         self.lock = threading.Lock()
         self.batches = 0
@@ -163,20 +166,30 @@ class StreamExecutor:
             return res
         return fn
 
+    def hold(self, k: int, event: torch.cuda.Event) -> None:
+        """Set k is not rewritten (inputs or stage) before ``event`` — e.g. a
+        device-side gather still reading its stage."""
+        with self.lock:
+            self.set_free[k].append(event)
+
     def submit(self, copies: Callable[[int], Sequence[Tuple[torch.Tensor, torch.Tensor]]],
                pre: Optional[Callable[[int], None]] = None,
-               extras: Optional[Callable[[int], Sequence[torch.Tensor]]] = None) -> Ticket:
+               extras: Optional[Callable[[int], Sequence[torch.Tensor]]] = None,
+               extras_dst: Optional[Sequence[Optional[torch.Tensor]]] = None) -> Ticket:
         """Enqueue one batch.  ``copies(k)``: (device, pinned host) pairs to
         upload into set k (a host tensor may be shorter than its device
         buffer: its leading elements are written); ``pre(k)``: extra work on
         the compute stream before the replay (e.g. JPEG reconstruction into
         set k); ``extras(k)``: device tensors copied back after the replay
-        (e.g. the annotated frames of set k) into fresh pinned tensors."""
+        (e.g. the annotated frames of set k) into fresh pinned tensors, or
+        into ``extras_dst[i]`` (page-locked host tensors, e.g. slots of the
+        data-parallel host ring) where given."""
         with self.lock:
             k = self.next
             self.next = (k + 1) % self.sets
-            if self.set_free[k] is not None:  # set k's inputs / stage are still being read back
-                self.h2d.wait_event(self.set_free[k])
+            for ev in self.set_free[k]:  # set k's inputs / stage are still being read back
+                self.h2d.wait_event(ev)
+            self.set_free[k] = []
             with torch.cuda.stream(self.h2d):
                 for d, h in copies(k):
                     d.view(-1)[:h.numel()].copy_(h.view(-1), non_blocking=True)
@@ -195,15 +208,17 @@ class StreamExecutor:
                 for h, d in zip(host, self.stage[k]):
                     h.copy_(d, non_blocking=True)
                 ex = []
-                for d in (extras(k) if extras is not None else ()):
-                    h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
+                for i, d in enumerate(extras(k) if extras is not None else ()):
+                    h = extras_dst[i] if extras_dst is not None and i < len(extras_dst) else None
+                    if h is None:
+                        h = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
                     h.copy_(d, non_blocking=True)
                     ex.append(h)
                 done = torch.cuda.Event()
                 done.record(self.d2h)
-            self.set_free[k] = done
+            self.set_free[k].append(done)
             self.batches += 1
-            return Ticket(k, done, host, ex, up, self.template)
+            return Ticket(k, done, host, ex, up, self.template, ran, self.stage[k])
 
     def synchronize(self) -> None:
         for s in (self.h2d, self.compute, self.d2h):
