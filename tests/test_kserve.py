@@ -385,5 +385,7 @@ def test_multi_process_server_shares_the_port_and_stops_cleanly():
     finally:
         p.terminate()
         assert p.wait(60) == 0
-    with socket.socket() as sk:  # no child process still holds the port
+    with socket.socket() as sk:  # no child process still listens on the port
+        # (SO_REUSEADDR: closed connections in TIME_WAIT must not count, a listener still does)
+        sk.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         sk.bind(("127.0.0.1", port))
