@@ -206,7 +206,25 @@ def call(name: str, *args) -> None:
     hip = _HIP if _HIP is not None else _load_hip()
     if hip is not None:
         hip.hipGetLastError()
+    if args and _KERNEL_SIGS.get(name, [None])[-1] is P and _capturing():
+        _check_capture_stream(name, args[-1])
     check(fn(*args), name)
+
+
+def _capturing() -> bool:
+    from .pipelines.graph import capturing_thread
+    return capturing_thread()
+
+
+def _check_capture_stream(name: str, stream) -> None:
+    """While this thread captures a graph, a launch must target a capturing
+    stream: one outside the capture would run once now, not on every replay."""
+    from .pipelines.graph import GraphCaptureError, stream_is_capturing
+
+    h = int(stream or 0)
+    if not stream_is_capturing(h):
+        raise GraphCaptureError(f"{name}: launched onto stream {hex(h)}, which is not part of the graph being "
+                                "captured (its work would not replay)")
 
 
 def ptr(t) -> int:

@@ -7,12 +7,147 @@ captured once and replayed: static input buffers are written (H2D copy or
 RCCL receive) before ``replay()``, outputs are read from static buffers
 after it.  Every op in this package is capture-safe by construction (no
 allocation, no host sync, device-side counts).
+
+Capture hygiene is checked, not assumed.  A step that forks work onto a side
+stream and does not join it back before the capture ends leaves HIP with an
+unjoined capture; on this ROCm ``hipStreamEndCapture`` then crashed the
+process inside ``torch.cuda.graphs.capture_end`` (round 3, a three-stream
+variant of the pipelined LiDAR step).  :meth:`GraphRunner.capture` therefore
+records every stream the step enters (``torch.cuda.stream`` contexts) and,
+before the capture ends, asks HIP for each stream's capture tips
+(``hipStreamGetCaptureInfo_v2``): a side stream whose last captured work is
+not an ancestor of the capturing stream's tips (``hipGraphNodeGetDependencies``)
+was never joined.  Such streams are joined back (so the capture ends
+cleanly), the graph is discarded and :class:`GraphCaptureError` names them.  A native launch (``_native.call``)
+onto a stream that is *not* part of the capture while one is active on the
+thread — work that would silently run once, eagerly, instead of on every
+replay — raises the same error.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+import ctypes
+import threading
+from typing import Callable, Dict, Optional, Set
 
 import torch
+
+
+class GraphCaptureError(RuntimeError):
+    pass
+
+
+_TL = threading.local()
+_SPY_LOCK = threading.Lock()
+_SPY = {"installed": False}
+
+
+def _install_stream_spy() -> None:
+    """Wrap ``torch.cuda.set_stream`` once: while this thread captures, the
+    streams it makes current are recorded (``torch.cuda.stream(s)`` goes
+    through ``set_stream``)."""
+    with _SPY_LOCK:
+        if _SPY["installed"]:
+            return
+        real = torch.cuda.set_stream
+
+        def set_stream(stream):
+            rec = getattr(_TL, "streams", None)
+            if rec is not None and stream is not None:
+                rec[int(stream.cuda_stream)] = stream
+            return real(stream)
+        torch.cuda.set_stream = set_stream
+        _SPY["installed"] = True
+
+
+def capturing_thread() -> bool:
+    """True while this thread is inside :meth:`GraphRunner.capture`."""
+    return getattr(_TL, "streams", None) is not None
+
+
+_HIPF: Dict[str, object] = {}
+
+
+def _hip_fn(name: str, argtypes):
+    """A HIP runtime entry point with its argtypes (None if unavailable)."""
+    if name not in _HIPF:
+        from .. import _native
+
+        hip = _native._load_hip()
+        fn = getattr(hip, name, None) if hip is not None else None
+        if fn is not None:
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _HIPF[name] = fn
+    return _HIPF[name]
+
+
+def stream_is_capturing(handle: int) -> bool:
+    """hipStreamIsCapturing on a raw stream handle (0: the null stream)."""
+    fn = _hip_fn("hipStreamIsCapturing", [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)])
+    if fn is None:
+        return False
+    st = ctypes.c_int(0)
+    rc = fn(ctypes.c_void_p(int(handle)), ctypes.byref(st))
+    return rc == 0 and st.value == 1  # hipStreamCaptureStatusActive
+
+
+def _capture_tips(handle: int) -> Optional[Set[int]]:
+    """Graph nodes the next captured op on this stream would depend on (its capture
+    "tips"); None if the stream is not capturing or the query is unavailable."""
+    fn = _hip_fn("hipStreamGetCaptureInfo_v2",
+                 [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong),
+                  ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.POINTER(ctypes.c_void_p)),
+                  ctypes.POINTER(ctypes.c_size_t)])
+    if fn is None:
+        return None
+    st, cid, graph = ctypes.c_int(0), ctypes.c_ulonglong(0), ctypes.c_void_p()
+    deps, n = ctypes.POINTER(ctypes.c_void_p)(), ctypes.c_size_t(0)
+    if fn(ctypes.c_void_p(int(handle)), ctypes.byref(st), ctypes.byref(cid), ctypes.byref(graph), ctypes.byref(deps),
+          ctypes.byref(n)) != 0 or st.value != 1:
+        return None
+    return {int(deps[i] or 0) for i in range(n.value)}
+
+
+def _ancestors(nodes: Set[int]) -> Set[int]:
+    """``nodes`` and every node they (transitively) depend on."""
+    fn = _hip_fn("hipGraphNodeGetDependencies",
+                 [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)])
+    seen, todo = set(nodes), list(nodes)
+    while todo and fn is not None:
+        node = ctypes.c_void_p(todo.pop())
+        n = ctypes.c_size_t(0)
+        if fn(node, None, ctypes.byref(n)) != 0 or n.value == 0:
+            continue
+        arr = (ctypes.c_void_p * n.value)()
+        if fn(node, arr, ctypes.byref(n)) != 0:
+            continue
+        for d in arr[:n.value]:
+            d = int(d or 0)
+            if d not in seen:
+                seen.add(d)
+                todo.append(d)
+    return seen
+
+
+def unjoined_streams(origin, streams: Dict[int, object]) -> Dict[int, object]:
+    """Streams forked into the capture on ``origin`` whose last captured work is
+    not (yet) a dependency of the origin stream's tips."""
+    otips = _capture_tips(int(origin.cuda_stream))
+    if otips is None:
+        return {}
+    anc = None
+    out = {}
+    for h, st in streams.items():
+        if h == int(origin.cuda_stream):
+            continue
+        tips = _capture_tips(h)
+        if not tips:
+            continue  # not part of this capture, or nothing captured on it
+        if anc is None:
+            anc = _ancestors(otips)
+        if not tips <= anc:
+            out[h] = st
+    return out
 
 
 class GraphRunner:
@@ -38,9 +173,27 @@ class GraphRunner:
                 self.out = self.fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        _install_stream_spy()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool, capture_error_mode=self.capture_error_mode):
-            self.out = self.fn()
+        unjoined: Dict[int, object] = {}
+        _TL.streams = {}
+        try:
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode=self.capture_error_mode):
+                origin = torch.cuda.current_stream()
+                try:
+                    self.out = self.fn()
+                finally:
+                    # before capture_end: every forked stream must be joined back
+                    unjoined.update(unjoined_streams(origin, _TL.streams))
+                    for st in unjoined.values():
+                        origin.wait_stream(st)  # join it, so the capture ends cleanly
+        finally:
+            _TL.streams = None
+        if unjoined:
+            self.graph = None
+            raise GraphCaptureError(f"the captured step left {len(unjoined)} forked stream(s) unjoined "
+                                    f"(handles {[hex(h) for h in unjoined]}): join every side stream back into "
+                                    "the capturing stream (current_stream().wait_stream(side)) before it returns")
         self.graph = g
 
     def __call__(self):
