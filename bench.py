@@ -377,16 +377,16 @@ def main():
         raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
     ex = FrameExchange(info, native=native)
     # with the native RCCL communicator the detection gather (grouped send / recv of fixed-shape
-    # result buffers) is stream work: capture it inside the step graph, so a step is one replay
-    # ... unless the step runs as two double-buffered graphs (the default with local ingest): two graphs
-    # replaying one communicator's captured p2p have not run on a multi-GPU node yet, so then the
-    # gather is issued after the replay (same RCCL group, host-launched)
+    # result buffers) is stream work: it is captured inside the step graph(s), so a step is one
+    # replay.  With the double-buffered graphs (the default) each of the two captures holds its own
+    # copy of the grouped plan over the one communicator, gathering into that set's receive buffers
+    # (tests/test_rccl.py: two graphs replaying one communicator's plan, alternately)
     will_db = (args.ingest == "local" and not args.no_prefetch and not (use_cam and args.camera_input == "jpeg")
                and not args.single_input_set and isinstance(runner, GraphRunner) and runner.enabled)
     gather_in_graph = (native is not None and isinstance(runner, GraphRunner) and runner.enabled
-                       and args.ingest == "local" and not will_db)
+                       and args.ingest == "local")
     gbuf = {}
-    if gather_in_graph:
+    if gather_in_graph and not will_db:
         def step_and_gather():
             r2, r3 = pipeline_step()
             src = outputs(r2, r3)
@@ -445,7 +445,7 @@ def main():
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
     # 8.92-8.98 vs 8.45 ms, profiles/r3/sched_ab.txt)
-    db = will_db and prefetch and jdec is None and not gather_in_graph
+    db = will_db and prefetch and jdec is None
     assert db == will_db, (db, will_db)
     if db:
         owners = ([(cam, "frames")] if use_cam else []) + ([(lid, "data"), (lid, "frame_n")] if use_lid else [])
@@ -534,6 +534,12 @@ def main():
                     if stages[name][k] is None:  # allocated in the eager warm-up, before capture
                         stages[name][k] = [torch.empty_like(t) for t in src_]
                     stage_copy(stages[name][k], src_)
+                elif gather_in_graph:  # the grouped RCCL gather into this set's receive buffers
+                    src_ = outs_of(res)
+                    if stages[name][k] is None:
+                        stages[name][k] = ([[torch.empty_like(t) for t in src_] for _ in range(info.world)]
+                                           if info.is_main else [])
+                    ex.gather(src_, stages[name][k] if info.is_main else None)
                 return res
             return fn
         unit_runners = {name: [GraphRunner(bound(name, fn, of, k)) for k in (0, 1)] for name, fn, of in units}
@@ -573,7 +579,7 @@ def main():
                     o = [outputs(*unit_runners["all"][k].out) for k in (0, 1)]
                     if not piped and [t.data_ptr() for t in o[0]] != [t.data_ptr() for t in o[1]]:
                         raise SystemExit("double-buffered graphs: the two captures return different result buffers")
-                    if info.world == 1:
+                    if info.world == 1 or gather_in_graph:
                         d2h_stage = [stages["all"][k] for k in (0, 1)]
                 k = self.t % 2
                 cur = torch.cuda.current_stream()
@@ -653,23 +659,25 @@ def main():
             # rank 0's own detections are D2H-copied straight from the graph's result
             # buffers (stream order keeps the next replay behind that copy)
             own = [torch.empty_like(t) for t in src] if piped else list(src)  # piped: results alternate buffers
-            gather_dst = (gbuf["dst"] if gather_in_graph else
+            gather_dst = (gbuf["dst"] if (gather_in_graph and not db) else
                           [own] + [[torch.empty_like(t) for t in src] for _ in range(1, info.world)])
             host_out = [[[torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in src] for _ in range(info.world)]
                         for _ in range(2)]
-        staged = db and d2h_stage is not None and info.world == 1
+        staged = db and d2h_stage is not None and (info.world == 1 or gather_in_graph)
         if not gather_in_graph and not staged:  # (one rank with a staged D2H: nothing to gather)
             ex.gather(src, gather_dst if info.is_main else None)
         k = it[0] % 2
         if info.is_main:
             if staged:
-                # the replay already copied its results into stage[j] (graph-side D2D): the D2H runs on
-                # the copy stream beside the next replay, which writes the other stage
+                # the replay already copied (one rank) or gathered (RCCL, in the graph) its results into
+                # stage[j]: the D2H runs on the copy stream beside the next replay, which writes the other
                 j = (runner.t - 1) % 2
                 d2h_stream.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(d2h_stream):
-                    for h, d in zip(host_out[k][0], d2h_stage[j]):
-                        h.copy_(d, non_blocking=True)
+                    per_rank = [d2h_stage[j]] if info.world == 1 else d2h_stage[j]
+                    for r, stage_r in enumerate(per_rank):
+                        for h, d in zip(host_out[k][r], stage_r):
+                            h.copy_(d, non_blocking=True)
                     out_ready[k].record(d2h_stream)
                     d2h_free[j].record(d2h_stream)
             else:
@@ -679,6 +687,8 @@ def main():
                 out_ready[k].record()
         else:
             out_ready[k].record()
+            if staged:
+                d2h_free[(runner.t - 1) % 2].record()  # (workers: the gather's sends are in the replay)
         # detections of the previous step are on rank 0's host now; this step's
         # D2H completes while the next step is issued
         if it[0] > 0:
@@ -714,7 +724,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             return allreduce_max(info, 1e3 * e0.elapsed_time(e1) / reps)
-        comm_us = {"gather": round(_time_us(lambda: ex.gather(last_src[0], gather_dst if info.is_main else None)), 1),
+        comm_us = {"gather": round(_time_us(lambda: ex.gather(last_src[0], gather_dst if info.is_main else None)), 1)
+                   if not (gather_in_graph and db) else None,
                    "gather_bytes_per_rank": int(sum(t.numel() * t.element_size() for t in last_src[0])),
                    "gather_in_graph": gather_in_graph}
         if args.ingest == "rccl":

@@ -140,3 +140,44 @@ def test_native_gather_plan_in_step_graph():
         torch.cuda.synchronize()
     finally:
         comm.abort()
+
+
+@pytest.mark.gpu
+def test_native_gather_plan_in_two_double_buffered_graphs():
+    """The bench's default double-buffered step with the gather inside: two graphs,
+    one per input set, each capturing its own copy of the grouped plan over the ONE
+    communicator and gathering into its own receive buffers, replayed alternately
+    (what every rank does, in the same order) — each replay delivers its own step."""
+    from triton_client_amd.parallel.rccl import RECV, SEND, NativeComm
+    from triton_client_amd.pipelines.graph import GraphRunner
+
+    torch.cuda.set_device(0)
+    comm = NativeComm(0, 1)
+    try:
+        inputs = [torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda")]
+        src = [torch.zeros((32, 300, 4), device="cuda"), torch.zeros((32,), dtype=torch.int32, device="cuda")]
+        dst = [[torch.empty_like(t) for t in src] for _ in range(2)]
+
+        def step(k):
+            def fn():
+                src[0].copy_(inputs[k].expand_as(src[0]))
+                src[1].copy_(inputs[k].to(torch.int32).expand_as(src[1]))
+                comm.group_p2p([(RECV, d, 0) for d in dst[k]] + [(SEND, s, 0) for s in src])
+                return src
+            return fn
+        runs = [GraphRunner(step(0)), GraphRunner(step(1))]
+        for r in runs:
+            r.capture()
+        for t, v in enumerate((2.0, 5.0, 9.0, 13.0)):
+            k = t % 2
+            inputs[k].fill_(v)
+            runs[k]()
+            torch.cuda.synchronize()
+            assert float(dst[k][0].reshape(-1)[0]) == v and int(dst[k][1][0]) == int(v)
+            if t:  # the other set still holds the previous step's gather
+                prev = (2.0, 5.0, 9.0, 13.0)[t - 1]
+                assert float(dst[1 - k][0].reshape(-1)[-1]) == prev
+        del runs
+        torch.cuda.synchronize()
+    finally:
+        comm.abort()

@@ -6,7 +6,7 @@ O=$R/gpurun_out/r4
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests/test_draw.py tests/test_live.py tests/test_dp_gpu.py tests/test_dp_drivers.py \
-  tests/test_centerpoint.py tests/test_drivers_gpu.py tests/test_graph_capture_gpu.py -v -m gpu --timeout 300 --timeout-method thread \
+  tests/test_centerpoint.py tests/test_drivers_gpu.py tests/test_graph_capture_gpu.py tests/test_rccl.py -v -m gpu --timeout 300 --timeout-method thread \
   > $O/pytest.log 2>&1; rc=$?
 grep -E 'PASSED|FAILED|ERROR' $O/pytest.log | tail -60; tail -3 $O/pytest.log
 [ $rc -eq 0 ] || { echo TESTS_RC=$rc; grep -E '^E ' $O/pytest.log | head -40; }
