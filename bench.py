@@ -507,8 +507,7 @@ def main():
             # tensor cost ~11 us each at the end of the step: 9 copyBuffer nodes, ~100 us)
             from triton_client_amd import _native
             pairs = [(d, t) for d, t in zip(dst_, src_) if t.numel()]
-            if (os.environ.get("TCA_STAGE_COPY", "1") == "0"
-                    or not all(d.is_contiguous() and t.is_contiguous() for d, t in pairs)):
+            if not all(d.is_contiguous() and t.is_contiguous() for d, t in pairs):
                 for d, t in pairs:
                     d.copy_(t, non_blocking=True)
                 return

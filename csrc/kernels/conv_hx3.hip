@@ -22,7 +22,6 @@ struct Hx3Args {
   int N, ldo, co_off, ldr, r_off;
   int act;  // 0 none, 1 relu, 2 silu, 3 leaky(0.1); | 16: act after the residual add
   const unsigned char* occ;  // stride 2 only: uint8 [B, H, W] input occupancy (0: read as zeros) or null
-  int dbg;                   // wx3 ablation bits (TCA_WX3_DBG, measurement only; 0 in production)
 };
 
 constexpr unsigned kOutOfRange = 0x80000000u;  // buffer offset past any num_records (< 2^31): reads zeros
@@ -528,332 +527,13 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
   hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
 }
 
-// ---- Winograd F(2,3) along the fragment axis ("wx3"), 3x3 stride 1 pad 1.
-//
-// hx3 spends 9 split-product fragment pairs per output pixel and 32-channel chunk.  Along the
-// fragment axis two neighbouring outputs y(2t), y(2t + 1) of one tap row kl are
-//   y0 = M0 + M1 + M2,  y1 = M1 - M2 - M3,   M_xi = U_xi . V_xi,
-//   V = (d0 - d2, d1 + d2, d2 - d1, d1 - d3)   over inputs d_k = x(2t - 1 + k),
-//   U = (g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2)   over the row's taps g,
-// so a pixel pair costs 4 products per tap row: 6 per pixel instead of 9.  The output
-// transform is linear, so M_xi is summed over the 3 tap rows and all input channels first
-// and transformed once per tile.  Numerics: V is formed in fp32 from the pair inputs (exact
-// joins, one rounding per add) and split to hi / lo like any activation; U is formed in fp64
-// on the host and split (ops/conv.py wx_weights); every product is the usual bf16 x3 with
-// fp32 accumulation.
-//
-// Tiling: 8 waves, TH = 6 output lines x 32 fragment-axis positions (16 pixel pairs) x 128
-// channels (WM = 1: each wave owns 16 channels for all 6 lines; WM = 2 for N = 64 layers:
-// two wave rows of 3 lines x four wave columns), weights streamed to registers per wave as in
-// hx3.  Each wave also transforms one of the 8 halo lines per chunk: lane (t, q) loads its 4
-// input pixels x 8 channels straight from global (buffer loads, zero padding by the range
-// check) and writes V_0..3 (hi / lo) into a double-buffered LDS image [line][xi][pair
-// tile][128 B], read back as the MFMA B operand (conflict-free both ways under vswz).
-//
-// Persistent (one 512-thread workgroup per CU, 128 KiB LDS): a workgroup walks tiles
-// blockIdx, + grid, ... as one flat sequence of (tile, chunk) steps, so the V transform of
-// step s + 1 (possibly the next tile's first chunk) runs inside step s and the epilogue of a
-// tile (output transform in registers, lane pairs l / l ^ 16 swapping halves so each lane
-// owns 8 channels of one pixel, 32-B pair stores) overlaps the next tile's MFMAs: one
-// barrier per step, no per-tile prologue.  Waves 0-3 transform after group 0, waves 4-7
-// (the other wave of each SIMD) after group 2, so a SIMD's MFMA pipe is fed while either
-// of its waves does VALU work.
-__device__ __forceinline__ int vswz(int t) { return (t & 7) ^ (t >> 3); }
-
-template <int TH, int WM, bool CM>
-__global__ void __launch_bounds__(512) conv_wx3_kernel(Hx3Args a) {
-  constexpr int NW = 8, TF = 32, HL = TH + 2, WN = NW / WM, BN = 16 * WN, FM = TH / WM;
-  static_assert(HL == NW, "one halo line per wave");
-  static_assert(TH % WM == 0, "wave rows");
-  constexpr int VLINE = 4 * 16 * 128;  // 4 xi x 16 pair tiles x 32 channels (pairs)
-  constexpr int VBUF = HL * VLINE;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * VBUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
-  constexpr int EX = CM ? TH : TF, EY = CM ? TF : TH;
-  const int tx_n = (a.Wo + EX - 1) / EX, ty_n = (a.Ho + EY - 1) / EY;
-  const int nnt = a.N / BN, ntile = a.B * ty_n * tx_n * nnt;
-  const int G = gridDim.x, nmine = (ntile - (int)blockIdx.x + G - 1) / G;
-  const int nc = a.Cin / 32, S = nmine * nc;
-  if (S <= 0) return;  // (the launcher never makes more workgroups than tiles)
-  // step cursor (wave-uniform, SGPRs): chunk c of this workgroup's k-th tile; the divisions
-  // run once per tile, not per step
-  struct Step { int k, c, b, oy0, ox0, n0; };
-  auto set_tile = [&](Step& x) {
-    const int T = (int)blockIdx.x + x.k * G;
-    const int mt = T / nnt, nt = T - mt * nnt;
-    x.b = mt / (ty_n * tx_n);
-    const int rem = mt - x.b * (ty_n * tx_n);
-    x.oy0 = (rem / tx_n) * EY;
-    x.ox0 = (rem - (rem / tx_n) * tx_n) * EX;
-    x.n0 = nt * BN;
-  };
-  auto advance = [&](Step& x) {  // to the next step (stays on the last step at the end)
-    if (x.k * nc + x.c + 1 >= S) return;
-    if (++x.c == nc) {
-      x.c = 0;
-      ++x.k;
-      set_tile(x);
-    }
-  };
-
-  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  // transform unit of this lane: halo line wid, pixel pair t, channels 8 q .. 8 q + 7
-  const int t = lane & 15, q = lane >> 4;
-  // raw inputs: the lane's own pixels 2t, 2t + 1 (d1, d2) plus, on the row's edge lanes only,
-  // pixel -1 (t = 0) or 32 (t = 15); d0 / d3 come from the neighbouring lanes by DPP row shifts
-  u32x4 rr[3][2];  // [own 2t, own 2t + 1, edge][hi | lo]
-  auto raw_load = [&](const Step& T) {
-    const int c = T.c;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int p = k < 2 ? 2 * t + k : (t == 0 ? -1 : 32);  // fragment-axis position in the tile
-      const int iy = CM ? T.oy0 + p : T.oy0 - 1 + wid;
-      const int ix = CM ? T.ox0 - 1 + wid : T.ox0 + p;
-      const bool live = k < 2 || t == 0 || t == 15;
-      const unsigned off = (live && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                               ? (unsigned)((((T.b * a.H + iy) * a.W + ix) * a.ldi + a.ci_off) * 4 + 32 * q)
-                               : kOutOfRange;
-      rr[k][0] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, c * 128, 0);
-      rr[k][1] = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16, c * 128, 0);
-    }
-  };
-  auto transform = [&](int buf) {
-    unsigned char* vb = smem + buf * VBUF + (wid * 64 + t) * 128;
-    const int o_hi = ((2 * q) ^ vswz(t)) << 4, o_lo = ((2 * q + 1) ^ vswz(t)) << 4;
-    u32x4 src[4][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        src[1][h][j] = rr[0][h][j];
-        src[2][h][j] = rr[1][h][j];
-        // row_shr:1 -- lane t takes lane t - 1's pixel 2t - 1; row_shl:1 -- lane t + 1's pixel 2t + 2;
-        // the row's first / last lane keeps its edge load (bound_ctrl off: "old" stays)
-        src[0][h][j] = (unsigned)__builtin_amdgcn_update_dpp((int)rr[2][h][j], (int)rr[1][h][j], 0x111, 0xf, 0xf, false);
-        src[3][h][j] = (unsigned)__builtin_amdgcn_update_dpp((int)rr[2][h][j], (int)rr[0][h][j], 0x101, 0xf, 0xf, false);
-      }
-    float d[4][8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const unsigned h = src[k][0][j], l = src[k][1][j];
-        d[k][2 * j] = __uint_as_float(h << 16) + __uint_as_float(l << 16);
-        d[k][2 * j + 1] = __uint_as_float(h & 0xffff0000u) + __uint_as_float(l & 0xffff0000u);
-      }
-#pragma unroll
-    for (int xi = 0; xi < 4; ++xi) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] = xi == 0 ? d[0][e] - d[2][e] : xi == 1 ? d[1][e] + d[2][e] : xi == 2 ? d[2][e] - d[1][e] : d[1][e] - d[3][e];
-      uint4 hi, lo;
-      pair_split8(v, hi, lo);
-      *reinterpret_cast<uint4*>(vb + xi * 2048 + o_hi) = hi;
-      *reinterpret_cast<uint4*>(vb + xi * 2048 + o_lo) = lo;
-    }
-  };
-
-  // weights: fragment image of U, K step (kl * 4 + xi) * nc + c (ops/conv.py wx_weights)
-  const int NG = a.N / 16;
-  const __bf16* wf = reinterpret_cast<const __bf16*>(a.w) + (long)wn * 1024 + lane * 8;
-  auto gload = [&](const Step& T, int xi, bf16x8 (&dst)[3][2]) {  // group xi of step T
-    const int c = T.c;
-    const __bf16* w0 = wf + (long)(T.n0 / 16) * 1024;
-#pragma unroll
-    for (int kl = 0; kl < 3; ++kl) {
-      const __bf16* p = w0 + (long)((kl * 4 + xi) * nc + c) * NG * 1024;
-      dst[kl][0] = *reinterpret_cast<const bf16x8*>(p);
-      dst[kl][1] = *reinterpret_cast<const bf16x8*>(p + 512);
-    }
-  };
-
-  f32x4 acc[FM][4];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int x = 0; x < 4; ++x) acc[i][x] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  const int o_hi = ((2 * fq) ^ vswz(fr)) << 4, o_lo = ((2 * fq + 1) ^ vswz(fr)) << 4;
-  // group xi of the current step; prefetches group xi + 1 (xi = 3: group 0 of step nx)
-  auto group = [&](auto XI, int buf, bf16x8 (&wu)[3][2], bf16x8 (&wl)[3][2], const Step& cur, const Step& nx) {
-    constexpr int xi = decltype(XI)::value;
-    if (!(a.dbg & 16)) {
-      if constexpr (xi < 3) gload(cur, xi + 1, wl);
-      else gload(nx, 0, wl);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* vp = smem + buf * VBUF + (xi * 16 + fr) * 128 + wm * FM * VLINE;
-#pragma unroll
-    for (int L = 0; L < FM + 2; ++L) {
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(vp + L * VLINE + o_hi);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(vp + L * VLINE + o_lo);
-#pragma unroll
-      for (int kl = 0; kl < 3; ++kl) {
-        const int i = L - kl;
-        if (i < 0 || i >= FM) continue;
-        mfma3(acc[i][xi], wu[kl][0], wu[kl][1], ah, al);
-      }
-    }
-  };
-  auto next_transform = [&](int s, const Step& s2) {  // V of step s + 1 into the other buffer, raw of s + 2
-    if (s + 1 < S) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (!(a.dbg & 1)) transform((s + 1) & 1);
-      if (s + 2 < S && !(a.dbg & 2)) raw_load(s2);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  // epilogue of one tile: y0 / y1 per lane (pixel pair fr, channels 4 fq .. + 3 of the wave's
-  // 16), bias + act, lanes l / l ^ 16 swap halves (even fq: pixel 2 fr, odd: 2 fr + 1; 8
-  // channels each), residual, 32-B pair stores
-  const int act = a.act & 15;
-  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
-  const int eact = post_res ? 0 : act;
-  const bool odd = (fq & 1) != 0;
-  auto epilogue = [&](const Step& T) {
-    const int nl = wn * 16 + fq * 4;
-    const float4 bv = a.bias ? *reinterpret_cast<const float4*>(a.bias + T.n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-    const int n = T.n0 + wn * 16 + (fq >> 1) * 8;
-    const int pos = 2 * fr + (odd ? 1 : 0);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      float y0[4], y1[4], v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        y0[r] = (acc[i][0][r] + acc[i][1][r]) + acc[i][2][r] + bb[r];
-        y1[r] = (acc[i][1][r] - acc[i][2][r]) - acc[i][3][r] + bb[r];
-        if (eact == 1) {
-          y0[r] = fmaxf(y0[r], 0.f);
-          y1[r] = fmaxf(y1[r], 0.f);
-        } else if (eact != 0) {
-          y0[r] = act_fn(y0[r], eact);
-          y1[r] = act_fn(y1[r], eact);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float got = __shfl_xor(odd ? y0[r] : y1[r], 16);
-        v[r] = odd ? got : y0[r];
-        v[4 + r] = odd ? y1[r] : got;
-      }
-      const int line = wm * FM + i;
-      const int oy = T.oy0 + (CM ? pos : line), ox = T.ox0 + (CM ? line : pos);
-      if (oy < a.Ho && ox < a.Wo && !(a.dbg & 4)) {
-        const long pix = ((long)T.b * a.Ho + oy) * a.Wo + ox;
-        if (a.res_f) {
-          float rv[8];
-          pair_join8(a.res_f + pix * a.ldr + a.r_off + n, rv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + rv[e], act) : v[e] + rv[e];
-        }
-        const long o = pix * a.ldo + a.co_off + n;
-        uint4 hi, lo;
-        pair_split8(v, hi, lo);
-        *reinterpret_cast<uint4*>(a.out_f + o) = hi;
-        *reinterpret_cast<uint4*>(a.out_f + o + 4) = lo;
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) acc[i][x] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  bf16x8 wA[3][2], wB[3][2];
-  Step cur{0, 0, 0, 0, 0, 0};
-  set_tile(cur);
-  Step s1 = cur, s2;
-  advance(s1);
-  s2 = s1;
-  advance(s2);
-  raw_load(cur);
-  gload(cur, 0, wA);
-  transform(0);
-  if (S > 1) raw_load(s1);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  const bool early = wid < 4;
-  for (int s = 0; s < S; ++s) {
-    const int buf = s & 1;
-    group(IC<0>{}, buf, wA, wB, cur, s1);
-    if (early) next_transform(s, s2);
-    group(IC<1>{}, buf, wB, wA, cur, s1);
-    group(IC<2>{}, buf, wA, wB, cur, s1);
-    if (!early) next_transform(s, s2);
-    group(IC<3>{}, buf, wB, wA, cur, s1);
-    if (cur.c == nc - 1) epilogue(cur);
-    cur = s1;
-    s1 = s2;
-    advance(s2);
-    if (s + 1 < S && !(a.dbg & 8)) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  }
-}
-
-// wx3 orientation: 0 auto (the smaller padding of a 32-position fragment axis, rows first on a
-// tie), 1 row-major (fragment axis = x), 2 column-major (fragment axis = y)
-int wx3_pick(const Hx3Args& a, int tile) {
-  if (tile != 0) return tile;
-  const long rm = (long)((a.Wo + 31) / 32 * 32) * ((a.Ho + 5) / 6 * 6);
-  const long cm = (long)((a.Ho + 31) / 32 * 32) * ((a.Wo + 5) / 6 * 6);
-  return cm < rm ? 2 : 1;
-}
-
-int num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
-
-int wx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
-  const bool cm = tile == 2;
-  const int bn = a.N % 128 == 0 ? 128 : 64;
-  if (a.N % bn) return (int)hipErrorInvalidValue;
-  const int ex = cm ? 6 : 32, ey = cm ? 32 : 6;
-  const long ntile = (long)a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / bn);
-  if (ntile <= 0) return 0;
-  // persistent: at most one workgroup per CU, every workgroup owns >= 1 tile; the tile
-  // count per workgroup differs by at most one
-  const int grid = (int)(ntile < num_cus() ? ntile : num_cus());
-  if (bn == 128) {
-    if (cm) conv_wx3_kernel<6, 1, true><<<grid, 512, 0, stream>>>(a);
-    else conv_wx3_kernel<6, 1, false><<<grid, 512, 0, stream>>>(a);
-  } else {
-    if (cm) conv_wx3_kernel<6, 2, true><<<grid, 512, 0, stream>>>(a);
-    else conv_wx3_kernel<6, 2, false><<<grid, 512, 0, stream>>>(a);
-  }
-  return (int)hipGetLastError();
-}
-
-// TCA_HX3_PAIRS=0: the single-chunk loop with register copies (A/B measurement)
-bool hx3_no_pairs() {
-  static const bool off = [] {
-    const char* e = getenv("TCA_HX3_PAIRS");
-    return e && e[0] == '0';
-  }();
-  return off;
-}
 
 template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
 int launch_hx3(const Hx3Args& a, hipStream_t stream) {
   if (a.N % BN) return (int)hipErrorInvalidValue;
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
-  if ((a.Cin / 32) % 2 == 0 && !hx3_no_pairs())
+  if ((a.Cin / 32) % 2 == 0)
     conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, true><<<nwg, WM * WN * 64, 0, stream>>>(a);
   else
     conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, false><<<nwg, WM * WN * 64, 0, stream>>>(a);
@@ -930,39 +610,11 @@ TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi
   if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
-  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = nullptr; a.dbg = 0;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = nullptr;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   return hx3_launch(a, tile, stream);
-}
-
-// fp32 mode, pair activations in and out, 3x3 stride 1 pad 1 as a Winograd F(2,3) along one axis
-// (conv_wx3_kernel).  w_rm / w_cm: the transformed weight images of the two orientations
-// (ops/conv.py wx_weights: [12 * Cin / 32][N / 16][hi | lo][64 lanes][8 bf16], K step
-// (kl * 4 + xi) * Cin / 32 + chunk); N % 64 == 0 (128-channel tiles when N % 128 == 0), Cin % 32 == 0.  tile: 0 auto, 1 row-major
-// (w_rm), 2 column-major (w_cm).  Residual and act as tca_conv_hx3p.
-TCA_API int tca_conv_wx3p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* w_rm,
-                          const void* w_cm, const float* bias, int N, float* out, int ldo, int co_off, int act,
-                          const float* res, int ldr, int r_off, int tile, hipStream_t stream) {
-  if (B <= 0) return 0;
-  if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
-  if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
-  if (tile < 0 || tile > 2) return (int)hipErrorInvalidValue;
-  Hx3Args a;
-  a.in_f = in; a.res_f = res; a.out_f = out; a.bias = bias; a.occ = nullptr; a.dbg = 0;
-  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
-  a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
-  if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
-  tile = wx3_pick(a, tile);
-  a.w = tile == 2 ? w_cm : w_rm;
-  static const int dbg = [] {
-    const char* e = getenv("TCA_WX3_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  a.dbg = dbg;
-  if (!a.w) return (int)hipErrorInvalidValue;
-  return wx3_launch(a, tile, stream);
 }
 
 // fp32 mode, pair activations in and out, 3x3 stride 2 pad 1 (conv_hx3s2_kernel), same weight
@@ -976,7 +628,7 @@ TCA_API int tca_conv_hx3s2p(const float* in, int B, int H, int W, int Cin, int l
   if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
-  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = occ; a.dbg = 0;
+  a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = occ;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets

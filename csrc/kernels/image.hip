@@ -858,16 +858,12 @@ TCA_API int tca_yolo_stem_fused(const void* src, long src_batch_stride, int src_
   a.w0 = (const __hip_bfloat16*)w0; a.b0 = bias0; a.w1 = (const __hip_bfloat16*)w1; a.b1 = bias1;
   a.act0 = act0; a.act1 = act1; a.out = out; a.ldo = ldo; a.co_off = co_off;
   a.B = batch; a.H0 = dst_h / 2; a.W0 = dst_w / 2; a.H1 = dst_h / 4; a.W1 = dst_w / 4;
-  // 8-row tiles (44 KiB LDS, three workgroups per CU); TCA_STEM_TY=4 takes 4-row tiles (23 KiB, more
-  // workgroups per CU but 11 / 4 instead of 19 / 8 sampled rows per output row): measured 244 vs 204 us
-  static const int ty = [] {
-    const char* e = getenv("TCA_STEM_TY");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
+  // 8-row tiles (44 KiB LDS, three workgroups per CU; 4-row tiles measured 244 vs 204 us: more
+  // workgroups per CU but 11 / 4 instead of 19 / 8 sampled rows per output row)
+  constexpr int ty = 8;
   const long tiles = (long)batch * ((a.H1 + ty - 1) / ty) * ((a.W1 + 15) / 16);
   if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
-  if (ty == 8) yolo_stem_fused_kernel<8><<<(unsigned)tiles, 256, 0, stream>>>(a);
-  else yolo_stem_fused_kernel<4><<<(unsigned)tiles, 256, 0, stream>>>(a);
+  yolo_stem_fused_kernel<ty><<<(unsigned)tiles, 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -579,16 +579,10 @@ TCA_API int tca_nms_reduce(const int* order, const int* sorted_n, const uint64_t
   OutXform xf{1.f, 1.f, 0.f, 0.f, 0.f, 0.f, 0};
   if (xform) { xf = OutXform{xform[0], xform[1], xform[2], xform[3], xform[4], xform[5], 1}; }
   if (max_out > kSortCap) return (int)hipErrorInvalidValue;
-  // RB 64-row blocks per memory round (TCA_NMS_RB=8: half the dependent rounds, 128 VGPRs of block words)
-  static const int rb = [] { const char* e = getenv("TCA_NMS_RB"); return e && atoi(e) == 8 ? 8 : 4; }();
-  if (rb == 8)
-    nms_reduce_wave_kernel<8><<<batch, 64, 0, stream>>>(order, sorted_n, mask, pre_max, mask_words, boxes, box_dim,
-                                                        scores, cls, cap, max_out, xf, out_box, out_score, out_cls,
-                                                        out_count);
-  else
-    nms_reduce_wave_kernel<4><<<batch, 64, 0, stream>>>(order, sorted_n, mask, pre_max, mask_words, boxes, box_dim,
-                                                        scores, cls, cap, max_out, xf, out_box, out_score, out_cls,
-                                                        out_count);
+  // 4 64-row blocks per memory round (8 measured within noise: profiles/r3/lpipe/README.md)
+  nms_reduce_wave_kernel<4><<<batch, 64, 0, stream>>>(order, sorted_n, mask, pre_max, mask_words, boxes, box_dim,
+                                                      scores, cls, cap, max_out, xf, out_box, out_score, out_cls,
+                                                      out_count);
   TCA_LAUNCH_CHECK();
 }
 

@@ -63,8 +63,6 @@ _KERNEL_SIGS = {
     "tca_conv_hx3p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, I, P],
     # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, res, ldr, r_off, occ, tile, stream
     "tca_conv_hx3s2p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, P, I, P],
-    # in, B, H, W, Cin, ldi, ci_off, w_rm, w_cm, bias, N, out, ldo, co_off, act, res, ldr, r_off, tile, stream
-    "tca_conv_wx3p": [P, I, I, I, I, I, I, P, P, P, I, P, I, I, I, P, I, I, I, P],
     # n, dst[], src[], nbytes[], stream (csrc/kernels/copy.hip)
     "tca_copy_segments": [I, P, P, P, P],
     # coords, nump, vcount, B, V, P, nz, ny, nx, flags, stream

@@ -110,11 +110,6 @@ HX3 = os.environ.get("TCA_HX3", "1") != "0"
 HX3S2 = HX3 and os.environ.get("TCA_HX3S2", "1") != "0"
 HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
-# conv_wx3 (conv_hx3.hip: Winograd F(2,3) along one axis, 6 split products per pixel instead of 9)
-# for the 3x3 stride-1 pair layers (N % 64 == 0); TCA_WX3=1 makes it the default for them.
-# Tiles 130 (auto orientation), 131 (row-major), 132 (column-major).
-WX3 = os.environ.get("TCA_WX3", "0") != "0"
-WX3_TILES = (130, 131, 132)
 
 
 def frag_weights(W: torch.Tensor) -> torch.Tensor:
@@ -127,20 +122,6 @@ def frag_weights(W: torch.Tensor) -> torch.Tensor:
     hi, lo = split_bf16(W)
     t = torch.stack([hi, lo], 0).reshape(2, N // 16, 16, Kp // 32, 4, 8)  # h, g, fr, ks, fq, e
     return t.permute(3, 1, 0, 4, 2, 5).contiguous()  # ks, g, h, fq, fr, e
-
-
-def wx_weights(W: torch.Tensor, cin_p: int, cm: bool) -> torch.Tensor:
-    """[N, 9 * cin_p] fp32 3x3 GEMM weights (K order ky, kx, ci) -> the fragment image of the
-    Winograd F(2,3) weights of conv_wx3 (conv_hx3.hip): along the fragment axis (x row-major,
-    y column-major) each tap row g = (g0, g1, g2) becomes U = (g0, (g0 + g1 + g2) / 2,
-    (g0 - g1 + g2) / 2, g2), formed in fp64 and split; GEMM K index (kl * 4 + xi) * cin_p + ci."""
-    N = W.shape[0]
-    W4 = W[:, : 9 * cin_p].double().reshape(N, 3, 3, cin_p)  # n, ky, kx, ci
-    if cm:
-        W4 = W4.permute(0, 2, 1, 3)  # n, kl = kx, kf = ky, ci
-    g0, g1, g2 = W4[:, :, 0], W4[:, :, 1], W4[:, :, 2]  # [N, 3 (kl), cin]
-    U = torch.stack([g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2], 2)  # n, kl, xi, ci
-    return frag_weights(U.reshape(N, 12 * cin_p).float())
 
 
 def act_dtype(precision: str) -> torch.dtype:
@@ -231,9 +212,6 @@ class FusedConv:
         self.b_gemm = self.bias.to(self.device).contiguous()
         # fragment-order weights of the hx3 kernel (built here, never inside a graph capture)
         self._w_frag = frag_weights(W).to(self.device) if self.hx3_ok() and self.device.type == "cuda" else None
-        self._w_wx = None
-        if WX3 and self.wx3_ok() and self.device.type == "cuda":
-            self.wx3_weights()
         # fp32 copies for the CPU path
         self.w_f32, self.b_f32 = w, b
 
@@ -274,14 +252,6 @@ class FusedConv:
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp, _native.ptr(occ),
                              tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
                 return out
-            if (out.pair and x.occ is None and self.wx3_ok() and
-                    (tile in WX3_TILES or (tile == 0 and WX3))):
-                w_rm, w_cm = self.wx3_weights()
-                _native.call("tca_conv_wx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
-                             _native.ptr(w_rm), _native.ptr(w_cm), _native.ptr(self.b_gemm), self.N,
-                             _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp,
-                             tile - 130 if tile in WX3_TILES else 0, _native.stream_ptr(stream))
-                return out
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
                 _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
@@ -310,17 +280,6 @@ class FusedConv:
         """conv_hx3.hip takes this conv: fp32, 3x3 stride 1 or 2, pad 1, Cin % 32, N % 64."""
         return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s in (1, 2) and self.p == 1
                 and self.cin_p % 32 == 0 and self.K == self.Kp and self.N % 64 == 0)
-
-    def wx3_ok(self) -> bool:
-        """conv_wx3 takes this conv: an hx3 stride-1 layer (N % 64 == 0)."""
-        return self.hx3_ok() and self.s == 1
-
-    def wx3_weights(self):
-        """(row-major, column-major) Winograd weight images, built on first use (outside captures:
-        the plans run every layer once eagerly before capturing)."""
-        if self._w_wx is None:
-            self._w_wx = tuple(wx_weights(self.w_f32_gemm, self.cin_p, cm).to(self.device) for cm in (False, True))
-        return self._w_wx
 
     def hx3_weights(self) -> torch.Tensor:
         if self._w_frag is None:

@@ -73,9 +73,8 @@ class FusedNeckHead:
         self.nbr = len(self.ups)
         self.nh = head.N
         # persistent kernel: one workgroup per CU (a multiple of 8: tiles are split per XCD)
-        if grid <= 0:  # TCA_NECK_GRID: fewer persistent workgroups (for running beside other work)
-            grid = int(os.environ.get("TCA_NECK_GRID", "0")) or \
-                torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+        if grid <= 0:
+            grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
         # fp32 tiling variant (bev_neck.hip tca_bev_neck_head_x3v): 0 auto, 1 <8 waves, 3 stages>,
         # 2 <4 waves, 2 stages, two workgroups per CU>, 3 <8 waves, 2 stages>

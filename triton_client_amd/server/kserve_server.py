@@ -459,8 +459,7 @@ class KServeServer:
         self.repo = repo
         self.address = address
         if switch_interval_s is None:
-            import os
-            switch_interval_s = float(os.environ.get("TCA_GIL_SWITCH_S", "2e-4"))
+            switch_interval_s = 2e-4  # GIL hand-off between the gRPC threads and the batchers
         self.switch_interval_s = switch_interval_s
         metrics = None
         if metrics_port is not None:
