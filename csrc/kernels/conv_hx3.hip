@@ -39,8 +39,9 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 // fragment reads at the three tap shifts
 __device__ __forceinline__ int hswz(int hx) { return (0xb29108 >> (3 * (hx >> 1))) & 7; }
 
-// x * w ~= xh*wh + xh*wl + xl*wh on the bf16 MFMA (fp32 accumulate), same order as conv_mfma.hip
-__device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
+// x * w ~= xh*wh + xh*wl + xl*wh on the bf16 MFMA (fp32 accumulate), same order as conv_mfma.hip.
+// (The kernels below issue these three products product-major over their accumulators.)
+[[maybe_unused]] __device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
                                       const bf16x8& al) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
@@ -67,16 +68,24 @@ __device__ __forceinline__ void pair_join8(const float* p, float* v) {
   for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
 }
 
-// epilogue (as hx): bias + act from the accumulators into an fp32 LDS tile (tile row
-// ml = line * 16 + position along the fragment axis), then 16-B pair stores (+ residual)
+// epilogue: bias + act from the accumulators into an fp32 LDS tile (tile row ml = line * 16 +
+// position along the fragment axis), then 16-B pair stores (+ residual).  The tile rows are
+// BN floats with the 16-B quads XOR-swizzled by the row (quad q of row ml at q ^ (ml & 15)):
+// the accumulator writes (ds_write_b128, 8-lane groups = 8 rows, one quad column) and the
+// row-major reads (ds_read_b128 of two quads per lane, 16-lane groups over two to four rows)
+// are both bank-conflict free (checked for BN = 64 and 128 with the MI355X_MICROARCH.md
+// lane groups).  (The former BN + 4 padding was conflict-free for the writes only: the reads went
+// 2- to 4-way, ~1.7M extra LDS cycles per BEV conv dispatch, profiles/r3/pmc_lidar_r3.)
 template <int TH, int BN, int WM, int WN, bool CM>
 __device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* smem,
                                              const f32x4 (&acc)[TH / WM][BN / WN / 16], int b, int oy0, int ox0,
                                              int n0) {
-  constexpr int BM = TH * 16, NT = WM * WN * 64, FM = TH / WM, FN = BN / WN / 16, LD = BN + 4;
+  constexpr int BM = TH * 16, NT = WM * WN * 64, FM = TH / WM, FN = BN / WN / 16, LD = BN;
+  static_assert(BN % 64 == 0, "the quad swizzle needs >= 16 quads per row");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
   float* st = reinterpret_cast<float*>(smem);
+  auto quad = [](int ml, int q) { return ml * LD + ((q ^ (ml & 15)) << 2); };
   const int act = a.act & 15;
   const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
   const int eact = post_res ? 0 : act;  // wave-uniform: one branch per fragment, not per element
@@ -93,18 +102,18 @@ __device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* sm
       } else if (eact != 0) {
         q.x = act_fn(q.x, eact); q.y = act_fn(q.y, eact); q.z = act_fn(q.z, eact); q.w = act_fn(q.w, eact);
       }
-      *reinterpret_cast<float4*>(st + ml * LD + nl) = q;
+      *reinterpret_cast<float4*>(st + quad(ml, nl >> 2)) = q;
     }
   }
   __syncthreads();
-  constexpr int V8 = BN / 8;
+  constexpr int V8 = BN / 8;  // 8 channels (two quads) per lane and pass
   for (int id = tid; id < BM * V8; id += NT) {
     const int ml = id / V8, c8 = (id - (id / V8) * V8) * 8;
     const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15)), n = n0 + c8;
     if (oy >= a.Ho || ox >= a.Wo) continue;
     float v[8];
-    const float4 v0 = *reinterpret_cast<const float4*>(st + ml * LD + c8);
-    const float4 v1 = *reinterpret_cast<const float4*>(st + ml * LD + c8 + 4);
+    const float4 v0 = *reinterpret_cast<const float4*>(st + quad(ml, c8 >> 2));
+    const float4 v1 = *reinterpret_cast<const float4*>(st + quad(ml, (c8 >> 2) + 1));
     v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
     const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
     if (a.res_f) {
@@ -262,12 +271,23 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
     for (int L = 0; L < FM + 2; ++L) {
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
+      // the three split products, product-major: the MFMAs of one product over every
+      // (tap, channel group) accumulator of this line are independent, so a dependent
+      // accumulator chain never issues back to back; each accumulator still sums its
+      // products in mfma3's order (bit-identical results)
 #pragma unroll
-      for (int kl = 0; kl < 3; ++kl) {
-        const int i = L - kl;
-        if (i < 0 || i >= FM) continue;
+      for (int pr = 0; pr < 3; ++pr) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wu[kl][j][0], wu[kl][j][1], ah, al);
+        for (int kl = 0; kl < 3; ++kl) {
+          const int i = L - kl;
+          if (i < 0 || i >= FM) continue;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const bf16x8& b = pr == 0 ? wu[kl][j][1] : wu[kl][j][0];
+            const bf16x8& x = pr == 1 ? al : ah;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, x, acc[i][j], 0, 0, 0);
+          }
+        }
       }
     }
   };
@@ -504,11 +524,18 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_hi);
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(colp + L * HWD * 128 + o_lo);
 #pragma unroll
-      for (int li = 0; li < S::NL; ++li) {
-        const int i = L - S::loff(li);
-        if (i < 0 || i >= FM) continue;
+      for (int pr = 0; pr < 3; ++pr) {  // product-major, as the stride-1 kernel (same per-accumulator order)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wu[li][j][0], wu[li][j][1], ah, al);
+        for (int li = 0; li < S::NL; ++li) {
+          const int i = L - S::loff(li);
+          if (i < 0 || i >= FM) continue;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const bf16x8& b = pr == 0 ? wu[li][j][1] : wu[li][j][0];
+            const bf16x8& x = pr == 1 ? al : ah;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, x, acc[i][j], 0, 0, 0);
+          }
+        }
       }
     }
     if constexpr (S::LAST_OF_PHASE) phase_end(S::PH, c);
