@@ -76,6 +76,9 @@ def _stamp_changed(name: str, flags: List[str], link: List[str]) -> bool:
     return not same
 
 
+LAST = {}  # what the last build() did: compiled objects and relinked libraries (build provenance)
+
+
 def _build_lib(name: str, sources: List[str], flags: List[str], link: List[str], jobs: int, force: bool) -> str:
     out = os.path.join(LIBDIR, name)
     force = _stamp_changed(name, flags, link) or force
@@ -90,11 +93,14 @@ def _build_lib(name: str, sources: List[str], flags: List[str], link: List[str],
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             list(ex.map(lambda so: _compile(so[0], so[1], flags), todo))
-    if force or todo or _stale(out, objs):
+    relinked = bool(force or todo or _stale(out, objs))
+    if relinked:
         os.makedirs(LIBDIR, exist_ok=True)
         tmp = out + ".tmp"
         _run([HIPCC, "-shared", *flags, "-o", tmp, *objs, *link])
         os.replace(tmp, out)
+    LAST[name] = {"compiled": [os.path.relpath(s_, ROOT) for s_, _ in todo], "sources": len(sources),
+                  "relinked": relinked, "forced": bool(force)}
     return out
 
 
@@ -109,7 +115,29 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     if verbose:
         for o in outs:
             print(f"[tca-build] {os.path.relpath(o, ROOT)} ({os.path.getsize(o) // 1024} KiB)", file=sys.stderr)
+    _write_provenance(outs)
     return outs
+
+
+def _write_provenance(outs: List[str]) -> dict:
+    """build/native/last_build.json: arch, compiler, which sources this build compiled,
+    whether each library was relinked, and each library's sha256 (what the tests load)."""
+    import hashlib
+    import time
+
+    rec = {"time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "arch": ARCH, "hipcc": HIPCC,
+           "libs": {}}
+    for o in outs:
+        name = os.path.basename(o)
+        with open(o, "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+        rec["libs"][name] = dict(LAST.get(name, {}), sha256=digest, bytes=os.path.getsize(o))
+    rec["build_mode"] = ("full" if all(v.get("forced") for v in rec["libs"].values()) else
+                         "incremental" if any(v.get("compiled") for v in rec["libs"].values()) else "up-to-date")
+    os.makedirs(BUILDDIR, exist_ok=True)
+    with open(os.path.join(BUILDDIR, "last_build.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    return rec
 
 
 if __name__ == "__main__":
