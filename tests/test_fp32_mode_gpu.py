@@ -222,8 +222,11 @@ def _camera_parity(cuda, precision, B=4, iou_min=0.99, tol=0.05, hw=(360, 640), 
 
 
 def _lidar_parity(cuda, precision, B=2, iou_min=0.99, tol=0.02, spec=None, max_points=32768, target=1000.0,
-                  check=None):
-    """check: the frames of the batch compared with the reference (default all)."""
+                  check=None, piped=False):
+    """check: the frames of the batch compared with the reference (default all).  piped: the
+    result comes from the bench's default step (--lidar-pipeline 3): two LidarPipelines over
+    one model, batch t's unpack / voxelise / VFE / down blocks on one stream beside the other
+    pipeline's neck + head + decode + NMS on another, the batch finished one step later."""
     from triton_client_amd.models.pointpillars import pillar_point_features, scatter_to_bev
     from triton_client_amd.ops.lidar import AnchorPostprocess, PointLayout, Voxelizer, pc2_unpack
     from triton_client_amd.ops.golden import rotated_iou_bev
@@ -238,7 +241,28 @@ def _lidar_parity(cuda, precision, B=2, iou_min=0.99, tol=0.02, spec=None, max_p
         lid.data[b * lid.frame_bytes: b * lid.frame_bytes + raw.numel()].copy_(raw)
         lid.frame_n[b] = c.shape[0]
     lid.calibrate_detection_density(target)
-    got = lid.step()
+    if piped:
+        other = LidarPipeline(model=lid.model, batch=B, max_points=max_points, device=cuda, precision=precision)
+        for lp in (lid, other):
+            lp.build_fast()
+        for b, c in enumerate(clouds[::-1]):  # the other batch in flight: different frames
+            raw = torch.from_numpy(c.view(np.uint8).reshape(-1))
+            other.data[b * other.frame_bytes: b * other.frame_bytes + raw.numel()].copy_(raw)
+            other.frame_n[b] = c.shape[0]
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        other.step_front(neck_back=True)  # the previous step's front half
+        main = torch.cuda.current_stream()
+        s1.wait_stream(main)
+        s2.wait_stream(main)
+        with torch.cuda.stream(s1):
+            lid.step_front(neck_back=True)  # this batch's front ...
+        with torch.cuda.stream(s2):
+            other.step_back()  # ... beside the previous batch's back half
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+        got = lid.step_back()  # the next step finishes this batch
+    else:
+        got = lid.step()
     torch.cuda.synchronize()
     check = list(range(B)) if check is None else list(check)
     # reference: CPU unpack + CPU voxeliser (spconv order) -> fp32 PyTorch PointPillars -> CPU postprocess
@@ -297,22 +321,20 @@ def test_pipeline_fp32_detection_parity(cuda, branch):
 def test_pipeline_fp32_detection_parity_headline_shape(cuda, branch):
     """The same gates at the headline's shapes (bench.py defaults): B = 32 per step,
     720x1280 camera frames, 64 x 1875-point sweeps, 100 / 2000 candidates per frame
-    reaching NMS (the 3D kept set saturates the 500-box cap).  The whole batch runs
-    on the GPU; 4 of its frames (first, last, two inside) are checked against the
-    fp32 modules + CPU reference post (a frame's result does not depend on the
-    others)."""
+    reaching NMS (the 3D kept set saturates the 500-box cap), every frame of the batch
+    checked against the fp32 modules + CPU reference post.  The LiDAR result comes from
+    the step the bench times (the two-pipeline split step, ``piped``)."""
     from triton_client_amd.utils.synthetic import LidarSpec
 
-    check = (0, 9, 22, 31)
     if branch == "camera":
-        stats = _camera_parity(cuda, "fp32", B=32, hw=(720, 1280), target=100.0, check=check)
+        stats = _camera_parity(cuda, "fp32", B=32, hw=(720, 1280), target=100.0)
     else:
         spec = LidarSpec(sensor_height=3.23)  # 64 x 1875, the bench's sweep
         maxp = ((spec.points_per_sweep + 1023) // 1024) * 1024
-        stats = _lidar_parity(cuda, "fp32", B=32, spec=spec, max_points=maxp, target=2000.0, check=check)
+        stats = _lidar_parity(cuda, "fp32", B=32, spec=spec, max_points=maxp, target=2000.0, piped=True)
     frac, n_r, n_g = _totals(stats)
     print(branch, "fp32 headline shape", stats, f"matched {frac:.4f}")
-    assert n_r >= 10 * len(check), stats  # a synthetic frame may legitimately keep nothing
+    assert len(stats) == 32 and n_r >= 10 * 32, stats  # a synthetic frame may legitimately keep nothing
     assert frac >= 0.99 and abs(n_r - n_g) <= max(1, n_r // 100), stats
 
 
