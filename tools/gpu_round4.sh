@@ -13,3 +13,7 @@ grep -E 'PASSED|FAILED|ERROR' $O/pytest.log | tail -60; tail -3 $O/pytest.log
 timeout -k 10 300 python -u tools/driver_bench.py --camera 1024 --lidar 1024 --batch 32 --workers 3 \
   > $O/driver_bench.json 2> $O/driver_bench.err || { echo DRIVER_BENCH_FAILED; tail -30 $O/driver_bench.err; exit 1; }
 cat $O/driver_bench.json
+for br in camera lidar; do
+  timeout -k 10 240 python -u tools/layer_times.py --branch $br > $O/layers_$br.json 2> $O/layers_$br.txt || { echo LAYERS_FAILED $br; tail -20 $O/layers_$br.txt; exit 1; }
+  head -25 $O/layers_$br.txt
+done
