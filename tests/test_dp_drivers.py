@@ -139,13 +139,21 @@ def _bag_messages(path, topic):
 
 
 def _replay_pair(tmp_path, device, env=None):
+    """One rank calibrates the random-init heads on its first frame and exports the
+    weights; the two-rank run loads them (--weights) -- the way a deployment pins a
+    model across launches: head calibration on the GPU is not bit-reproducible from one
+    process to the next (MIOpen / PyTorch reductions), so two separate launches would
+    otherwise each calibrate their own prior."""
     out = {}
+    w2, w3 = str(tmp_path / "w2.pt"), str(tmp_path / "w3.pt")
     for ranks in (1, 2):
         ob2, ob3 = str(tmp_path / f"cam{ranks}.bag"), str(tmp_path / f"pc{ranks}.bag")
+        wflag2 = ["--export-weights", w2] if ranks == 1 else ["--weights", w2]
+        wflag3 = ["--export-weights", w3] if ranks == 1 else ["--weights", w3]
         _run(["triton_client_amd.cli.bag2d", "--bag", FIX, "--engine", "local", "--device", device, "--out", "",
-              "--out-bag", ob2, "--frames-per-step", "2"], ranks, device, env)
+              "--out-bag", ob2, "--frames-per-step", "2"] + wflag2, ranks, device, env)
         _run(["triton_client_amd.cli.bag3d", "--bag", FIX, "--engine", "local", "--device", device, "--out-bag", ob3,
-              "--labels", "all", "--score-thresh", "0", "--frames-per-step", "1"], ranks, device, env)
+              "--labels", "all", "--score-thresh", "0", "--frames-per-step", "1"] + wflag3, ranks, device, env)
         out[ranks] = (_bag_messages(ob2, "/aver_01/camera_color/detection/detections"),
                       _bag_messages(ob2, "/aver_01/camera_color/detection"),
                       _bag_messages(ob3, "/detections_3d"))
@@ -194,8 +202,7 @@ def _dp_camera_worker(rank, world, port, q):
 
         info = init_distributed("gloo")
         det = LocalDetector2D(batch=3, device=info.device, letterbox=True, names=[f"c{i}" for i in range(80)])
-        det.calibrate_synthetic(0)
-        dp = DataParallelDetector2D(det, info)
+        dp = DataParallelDetector2D(det, info)  # rank 0 calibrates on the first frame and broadcasts
         if info.is_main:
             jp = []
             for i in range(7):

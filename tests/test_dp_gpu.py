@@ -38,8 +38,7 @@ def _worker(rank, world, port, q):
         info = init_distributed("gloo")
         d2 = LocalDetector2D(batch=2, device=info.device)
         d3 = LocalDetector3D(batch=2, device=info.device, max_points=32768)
-        d2.calibrate_synthetic(0)
-        d3.calibrate_synthetic(0)
+        # no per-rank calibration: rank 0 calibrates on the first frame and broadcasts
         if rank != 0:
             def no_host(*a, **k):
                 raise AssertionError("worker rank used the host detect() path")
@@ -120,7 +119,6 @@ def _family_worker(rank, world, port, q, family):
             det = LocalDetector2D(batch=2, device=info.device, family=family, img=(640, 480) if family != "yolov4"
                                   else 512, nc=80)
             dp = DataParallelDetector2D(det, info, max_det=300)
-        det.calibrate_synthetic(0)
         if rank != 0:
             def no_host(*a, **k):
                 raise AssertionError("worker rank used the host detect() path")

@@ -56,3 +56,34 @@ def test_pack_task_segments_matches_per_image():
             np.testing.assert_array_equal(lab[i, :k].numpy(), want[i]["pred_labels"][:k])
             assert (s[i, k:] == 0).all()
     assert list(DET3D_ORDER) == [0, 1, 2, 3, 4, 5, 7, 8, 6]
+
+
+def test_export_weights_reproduces_calibrated_engine(tmp_path):
+    """export_weights (fused, calibrated) -> --weights: the reloaded engines give the
+    same detections bit for bit, with no re-calibration (camera and LiDAR)."""
+    from triton_client_amd.inference.engines import LocalDetector2D, LocalDetector3D, export_weights
+    from triton_client_amd.ros.compat import create_cloud_xyzi
+    from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+
+    frames = [camera_frame(120, 160, 3 + i) for i in range(2)]
+    a = LocalDetector2D(img=128, batch=2, device="cpu", graph=False)
+    want = a.detect(frames)
+    export_weights(a.model, str(tmp_path / "cam.pt"))
+    b = LocalDetector2D(img=128, batch=2, device="cpu", graph=False, weights=str(tmp_path / "cam.pt"))
+    assert b.calibrate_target is None
+    got = b.detect(frames)
+    assert sum(len(d) for d in want) > 0
+    for x, y in zip(want, got):
+        np.testing.assert_array_equal(x, y)
+
+    spec = LidarSpec(rings=16, azimuth_steps=512, sensor_height=3.23)
+    clouds = [create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, 40).tobytes(), np.float32).reshape(-1, 4))]
+    a3 = LocalDetector3D(batch=1, device="cpu", graph=False, max_points=16384)
+    want3 = a3.detect(clouds)
+    export_weights(a3.model, str(tmp_path / "pc.pt"))
+    b3 = LocalDetector3D(batch=1, device="cpu", graph=False, max_points=16384, weights=str(tmp_path / "pc.pt"))
+    got3 = b3.detect(clouds)
+    for x, y in zip(want3, got3):
+        assert x.keys() == y.keys()
+        for k in x:
+            np.testing.assert_array_equal(np.asarray(x[k]), np.asarray(y[k]))

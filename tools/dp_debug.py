@@ -37,8 +37,7 @@ def worker(rank, world, port, dump, three_d):
         det = LocalDetector3D(batch=2, device=info.device, max_points=32768)
     else:
         det = LocalDetector2D(batch=2, device=info.device)
-    det.calibrate_synthetic(0)
-    log(rank, "calibrated")
+    # no per-rank calibration: rank 0 calibrates on its first frame and broadcasts
     dp = (DataParallelDetector3D if three_d else DataParallelDetector2D)(det, info)
     log(rank, f"ring {dp.ring.name} attached")
     if info.is_main:

@@ -6,7 +6,7 @@ import os
 import sys
 
 from .common import DATA, add_framework_flags, add_reference_flags, load_params, setup_logging
-from .engines import engine_2d, maybe_data_parallel
+from .engines import engine_2d, export_if_asked, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -40,6 +40,7 @@ def main(argv=None) -> int:
                          out_bag=flags.out_bag, batch=max(1, flags.frames_per_step), save_png=bool(flags.out),
                          start_seq=flags.start_seq, max_frames=flags.max_frames)
     n = drv.start_inference()
+    export_if_asked(flags, engine)
     if info is not None:
         engine.close()
         from ..parallel.dp import shutdown

@@ -6,7 +6,7 @@ import os
 import sys
 
 from .common import DATA, add_framework_flags, add_reference_flags, labels_arg, load_params, setup_logging
-from .engines import engine_3d, maybe_data_parallel
+from .engines import engine_3d, export_if_asked, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -41,6 +41,7 @@ def main(argv=None) -> int:
                          max_frames=flags.max_frames, verbose=flags.verbose, jsk=not flags.detection3d,
                          labels=labels_arg(flags.labels), score_thresh=flags.score_thresh)
     n = drv.start_inference()
+    export_if_asked(flags, engine)
     if info is not None:
         engine.close()
         from ..parallel.dp import shutdown

@@ -62,6 +62,9 @@ def add_framework_flags(p: argparse.ArgumentParser, params_default: str, three_d
     g.add_argument("--timeout", type=float, default=None, help="per-RPC deadline (s); default none")
     g.add_argument("--retries", type=int, default=2, help="retries on UNAVAILABLE/DEADLINE_EXCEEDED")
     g.add_argument("--weights", default=None, help="state_dict for the local engine: path, file://, http(s):// or s3:// URI (loaded with torch.load weights_only)")
+    g.add_argument("--export-weights", default=None,
+                   help="local engine: after the run, save its fused, calibrated weights here (reload with --weights "
+                        "to reproduce them exactly, e.g. on every rank or host of a deployment)")
     g.add_argument("--play", default=None, help="replay this bag onto the in-process topic bus (no rospy)")
     g.add_argument("--spin-timeout", type=float, default=None, help="stop spinning after N seconds")
     g.add_argument("--metrics-port", type=int, default=None, help="Prometheus exporter port for client metrics")

@@ -96,6 +96,17 @@ def engine_3d(flags, params):
     return eng, ch, client
 
 
+def export_if_asked(flags, engine) -> None:
+    """``--export-weights``: the local engine's fused, calibrated model as a checkpoint
+    (rank 0 under data parallelism; the replicas hold the same weights)."""
+    path = getattr(flags, "export_weights", None)
+    if not path or flags.engine != "local":
+        return
+    from ..inference.engines import export_weights
+
+    export_weights(getattr(engine, "local", engine).model, path)
+
+
 def maybe_data_parallel(engine, three_d: bool = False):
     """Under torchrun (WORLD_SIZE > 1) wrap a *local* engine so rank 0's frames
     are sharded over every GPU (RCCL scatter/gather).  Returns (engine, info);
@@ -107,8 +118,8 @@ def maybe_data_parallel(engine, three_d: bool = False):
     from ..parallel.dp import DataParallelDetector2D, DataParallelDetector3D, init_distributed
 
     info = init_distributed()
-    # random-init weights: every rank calibrates the head prior from the same frame, the node
-    # batch's first (what one GPU does); the DP gather checks that the replicas' weights agree
+    # random-init weights: rank 0 calibrates the head prior on the node batch's first frame
+    # (what one GPU does) and broadcasts the result; the gather checks that the replicas agree
     # rank-failure detection: heartbeats over the c10d store; a dead rank's
     # shards are re-split over the survivors (TCA_DP_HEARTBEAT=0 disables)
     monitor = None

@@ -7,7 +7,7 @@ import sys
 
 from .common import (DATA, add_framework_flags, add_reference_flags, image_files, load_params, play_bag,
                      setup_logging)
-from .engines import engine_2d, maybe_data_parallel
+from .engines import engine_2d, export_if_asked, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -44,6 +44,7 @@ def main(argv=None) -> int:
                        batch=flags.live_batch, workers=flags.live_workers)
     if flags.image_src == "local":
         rc = _run_local_images(drv, flags, params)
+        export_if_asked(flags, engine)
         if info is not None:
             engine.close()
             from ..parallel.dp import shutdown
@@ -53,6 +54,7 @@ def main(argv=None) -> int:
         play_bag(flags.play, bus, topics=[params["sub_topic"]])
     drv.start_inference(spin=True, timeout=flags.spin_timeout)
     drv.stop()
+    export_if_asked(flags, engine)
     if info is not None:
         engine.close()
         from ..parallel.dp import shutdown

@@ -6,7 +6,7 @@ import os
 import sys
 
 from .common import DATA, add_framework_flags, add_reference_flags, labels_arg, load_params, play_bag, setup_logging
-from .engines import engine_3d, maybe_data_parallel
+from .engines import engine_3d, export_if_asked, maybe_data_parallel
 
 
 def parse_args(argv=None):
@@ -42,6 +42,7 @@ def main(argv=None) -> int:
         play_bag(flags.play, bus, topics=[params["sub_topic"]])
     drv.start_inference(spin=True, timeout=flags.spin_timeout)
     drv.stop()
+    export_if_asked(flags, engine)
     if info is not None:
         engine.close()
         from ..parallel.dp import shutdown

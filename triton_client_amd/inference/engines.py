@@ -49,6 +49,31 @@ def _device(device) -> torch.device:
     return torch.device(device)
 
 
+FUSED_MARK = "_tca_fused_calibrated"
+
+
+def load_weights(model, uri: str):
+    """Load a checkpoint into ``model``: a plain state_dict of the module, or one written
+    by :func:`export_weights` (BN folded, head prior calibrated), which is loaded into the
+    model after folding its BN the same way."""
+    from ..models.common import fuse_model
+
+    sd = load_state_dict(uri)
+    if FUSED_MARK in sd:
+        sd = {k: v for k, v in sd.items() if k != FUSED_MARK}
+        model = fuse_model(model.eval())
+    model.load_state_dict(sd)
+    return model
+
+
+def export_weights(model, path: str) -> None:
+    """The engine's model as a fused, calibrated checkpoint (fp32, CPU): loading it with
+    ``--weights`` reproduces this engine's weights exactly (no re-calibration)."""
+    sd = {k: v.detach().float().cpu().contiguous() for k, v in model.state_dict().items()}
+    sd[FUSED_MARK] = torch.ones(1)
+    torch.save(sd, path)
+
+
 def _empty2d() -> np.ndarray:
     return np.zeros((0, 6), np.float32)
 
@@ -148,7 +173,7 @@ class LocalDetector2D(Detector2D):
             self.model = build_detectron(self.det_cfg, seed)
             self.max_det = min(max_det, self.det_cfg.max_detections)
         if weights:
-            self.model.load_state_dict(load_state_dict(weights))
+            self.model = load_weights(self.model, weights)
             calibrate_target = None
         if calibrate_target == "auto":
             calibrate_target = 300.0 if family in ("retinanet", "fcos") else 100.0
@@ -335,7 +360,7 @@ class LocalDetector3D(Detector3D):
         self.z_offset = self.Z_OFFSET[family] if z_offset is None else z_offset
         self.graph = graph and self.device.type == "cuda"
         if weights:
-            self.model.load_state_dict(load_state_dict(weights))
+            self.model = load_weights(self.model, weights)
             calibrate_target = None
         self.calibrate_target = self.FAMILIES[family] if calibrate_target == "auto" else calibrate_target
         self.max_points = max_points

@@ -56,6 +56,7 @@ from .host_ring import MAX_ITEMS, HostRing
 KIND_STOP, KIND_JPEG, KIND_FRAMES, KIND_CLOUDS = -1, 1, 2, 3
 # header ints
 H_SEQ, H_KIND, H_N, H_GEN, H_SLOT, H_MASK, H_PER, H_DRAW, H_KEY = 0, 1, 2, 3, 4, 5, 6, 7, 8
+H_CALIB = 60  # 1: rank 0 broadcasts its freshly calibrated weights in this step (every rank joins)
 # item ints: in_off, in_size, out_off, out_size, meta0, meta1
 I_IN, I_INSZ, I_OUT, I_OUTSZ, I_M0, I_M1 = range(6)
 _ALIGN = 4096
@@ -154,7 +155,8 @@ class _RingDP:
         weakref.finalize(view, release)
 
     def _write_step(self, kind: int, payloads: Sequence, metas: Sequence[Tuple[int, int]], out_sizes: Sequence[int],
-                    key: Sequence[int], draw: bool, parts: List[int], per: int) -> Tuple[int, int, np.ndarray]:
+                    key: Sequence[int], draw: bool, parts: List[int], per: int,
+                    calib: bool = False) -> Tuple[int, int, np.ndarray]:
         """Payloads + item table into the next slot, then publish. -> (seq, slot, items)."""
         from ..inference.live import gather_copy
 
@@ -192,6 +194,7 @@ class _RingDP:
         hdr[H_SEQ], hdr[H_KIND], hdr[H_N], hdr[H_GEN], hdr[H_SLOT] = seq, kind, n, ring.gen, data.slot_bytes
         hdr[H_MASK], hdr[H_PER], hdr[H_DRAW] = mask, per, int(draw)
         hdr[H_KEY:H_KEY + len(key)] = key
+        hdr[H_CALIB] = int(calib)
         ring.publish(s, seq)
         self._slot_use[s] = (seq, list(parts))
         return seq, s, items[:n].copy()
@@ -276,6 +279,8 @@ class _RingDP:
             if hdr[H_KIND] == KIND_STOP:
                 ring.ack(s, self.info.rank, seq)
                 return done
+            if hdr[H_CALIB]:  # rank 0 calibrated its random-init weights: take them (every rank)
+                self._adopt_weights(hdr)
             mask = int(hdr[H_MASK])
             if (mask >> self.info.rank) & 1:
                 data = ring.use_generation(int(hdr[H_GEN]), int(hdr[H_SLOT]))
@@ -294,9 +299,32 @@ class _RingDP:
         me = wk.index(self.info.rank)
         return min(n, me * per), min(n, (me + 1) * per)
 
-    def _run_step(self, kind, payloads, metas, out_sizes, key, draw, assemble):
+    def _needs_calibration(self) -> bool:
+        """A device engine whose random-init head prior is still to be set.  The GPU
+        calibration (LSUV statistics through the PyTorch modules) is not bit-reproducible
+        across processes, so on the device path only rank 0 calibrates — on the node
+        batch's first frame, as one GPU does — and broadcasts the resulting weights."""
+        return self.gpu and self.info.world > 1 and getattr(self.local, "calibrate_target", None) is not None
+
+    def _broadcast_weights(self) -> None:
+        from ..models.common import broadcast_parameters
+        broadcast_parameters(self.local.model)
+        self._sig = None
+
+    def _adopt_weights(self, hdr) -> None:
+        """Peers: fold the model the way rank 0's pipeline did (without calibrating), then
+        receive rank 0's weights; engines are built only after this."""
+        self.local.calibrate_target = None
+        self._model_like_rank0(hdr)
+        self._broadcast_weights()
+
+    def _run_step(self, kind, payloads, metas, out_sizes, key, draw, assemble, prebuild=None):
         """Rank 0: one node step with retries; ``assemble(dst, wk, per, items,
-        slot_view, own)`` builds the results."""
+        slot_view, own)`` builds the results.  ``prebuild()``: builds (and so calibrates)
+        rank 0's engine for this step before it is published."""
+        calib = self._needs_calibration()
+        if calib:
+            prebuild()
         while True:
             parts = self._participants()
             n = len(payloads)
@@ -304,7 +332,10 @@ class _RingDP:
             if self._cap_per(per) < per:
                 raise _Rechunk()
             wk = parts[:-(-n // per)]
-            seq, s, items = self._write_step(kind, payloads, metas, out_sizes, key, draw, wk, per)
+            seq, s, items = self._write_step(kind, payloads, metas, out_sizes, key, draw, wk, per, calib)
+            if calib:  # every rank joins this collective as soon as it reads the header
+                self._broadcast_weights()
+                calib = False
             slot_view = self.ring.data.slot(s)
             try:
                 hdr = self.ring.header(s).copy()
@@ -427,9 +458,17 @@ class DataParallelDetector2D(_RingDP):
         frame = H * W * 3
         out_sizes = [frame] * len(payloads) if draw else []
         metas = [(0, 0)] * len(payloads)
+
+        def prebuild():
+            live = self.local.live()
+            live._engine(live._key(messages[0]), draw, tuple(self.names), messages[0])
         return self._run_step(kind, payloads, metas, out_sizes, (H, W), draw,
                               lambda dst, wk, per, items, view, own, s: self._assemble(
-                                  dst, wk, per, items, view, own, s, messages, H, W, draw))
+                                  dst, wk, per, items, view, own, s, messages, H, W, draw), prebuild)
+
+    def _model_like_rank0(self, hdr) -> None:
+        p = self.local._calibrated_pipeline((int(hdr[H_KEY]), int(hdr[H_KEY + 1])), None)
+        del p  # only its BN folding / device placement of the shared model is wanted
 
     # ------------------------------------------------------------------ every rank
     def _shard_items(self, hdr, items, view, lo, hi):
@@ -580,9 +619,12 @@ class DataParallelDetector3D(_RingDP):
 
         with self._lock:
             groups: Dict[tuple, List[int]] = {}
+            lays = {}
             for i, c in enumerate(clouds):
                 lay = cloud_layout(c, self.FIELDS)
-                groups.setdefault((lay.point_step, *lay.offsets, *lay.dtypes), []).append(i)
+                k = (lay.point_step, *lay.offsets, *lay.dtypes)
+                lays[k] = lay
+                groups.setdefault(k, []).append(i)
             out: List[Optional[dict]] = [None] * len(clouds)
             for key, idx in groups.items():
                 while idx:
@@ -591,9 +633,12 @@ class DataParallelDetector3D(_RingDP):
                     npts = [int(x.width * x.height) for x in cs]
                     payloads = [memoryview(x.data)[:k * key[0]] for x, k in zip(cs, npts)]
                     maxp = max(npts)
+
+                    def prebuild(lay=lays[key], maxp=maxp, c0=cs[0]):
+                        self.local.live()._engine(lay, maxp, c0)
                     try:
                         res = self._run_step(KIND_CLOUDS, payloads, [(k, 0) for k in npts], [], (*key, maxp), False,
-                                             self._assemble)
+                                             self._assemble, prebuild)
                     except _Rechunk:
                         continue
                     for i, r in zip(chunk, res):
@@ -653,6 +698,16 @@ class DataParallelDetector3D(_RingDP):
         return (None, None), src, [box, score, lab, cnt, self._tag(0)], None
 
     _after_gather = DataParallelDetector2D._after_gather
+
+    def _model_like_rank0(self, hdr) -> None:
+        from ..ops.lidar import PointLayout
+        layout = PointLayout(int(hdr[H_KEY]), tuple(int(v) for v in hdr[H_KEY + 1:H_KEY + 5]),
+                             tuple(int(v) for v in hdr[H_KEY + 5:H_KEY + 9]))
+        maxp = self.local.max_points
+        while maxp < int(hdr[H_KEY + 9]):
+            maxp *= 2
+        p = self.local._calibrated_pipeline(layout, maxp, None)
+        del p
 
     def _serve_step(self, hdr, items, view) -> None:
         wk = self._workers(int(hdr[H_MASK]))
