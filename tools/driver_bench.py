@@ -10,7 +10,13 @@ from raw pinned bytes to device detections; this tool times the drivers
 the in-process topic bus, including JPEG decode, micro-batching, the ordered
 re-publisher, GPU annotation and building the published messages.
 
-    python tools/driver_bench.py [--camera N] [--lidar N] [--batch B] [--workers W]
+    python tools/driver_bench.py [--camera N] [--lidar N] [--batch B] [--workers W] [--gpus N]
+
+``--gpus N`` (N > 1) runs the drivers data-parallel the way ``torchrun main.py
+--engine local`` does (``parallel/ring_dp.py``): rank 0 subscribes and publishes, the
+node batch goes through the shared host ring, every rank decodes / detects its shard
+on its own GPU.  Launched without torchrun it starts ``torch.distributed.run`` as a
+child process; ``TCA_DIST_BACKEND=gloo`` rehearses N ranks on one GPU.
 
 Messages are published paced so the latest-wins windows never drop (every
 message is detected and published); throughput = messages / wall time from the
@@ -19,6 +25,7 @@ first publish to the last published result.  Prints one JSON line.
 import argparse
 import io
 import json
+import os
 import sys
 import threading
 import time
@@ -81,7 +88,18 @@ def main():
     ap.add_argument("--hw", default="720,1280")
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--gpus", type=int, default=1, help="data-parallel ranks (one process per GPU)")
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:  # self-launch (a child: nothing has touched the GPU)
+        import socket
+        import subprocess
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", __file__] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     import torch
     from PIL import Image
@@ -93,9 +111,28 @@ def main():
     from triton_client_amd.ros.bus import TopicBus
     from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
 
+    from triton_client_amd.cli.engines import maybe_data_parallel
+
     H, W = (int(v) for v in a.hw.split(","))
-    out = {"tool": "driver_bench", "batch": a.batch, "workers": a.workers,
-           "device": torch.cuda.get_device_name(0) if a.device == "cuda" else a.device}
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.device == "cuda" and world > 1:
+        a.device = f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())}"
+    os.environ.setdefault("TCA_DP_HEARTBEAT", "0")
+    # every rank builds both engines (and their DP wrappers) in the same order
+    eng2, info = maybe_data_parallel(LocalDetector2D(batch=a.batch, device=a.device, letterbox=True)) \
+        if a.camera else (None, None)
+    eng3, info3 = maybe_data_parallel(LocalDetector3D(batch=a.batch, device=a.device), three_d=True) \
+        if a.lidar else (None, None)
+    info = info or info3
+    if info is not None and not info.is_main:  # worker rank: serve shards until rank 0 is done
+        for e in (eng2, eng3):
+            if e is not None:
+                e.serve()
+        from triton_client_amd.parallel.dp import shutdown
+        shutdown(info)
+        return
+    out = {"tool": "driver_bench", "batch": a.batch, "workers": a.workers, "gpus": world,
+           "device": torch.cuda.get_device_name(0) if a.device.startswith("cuda") else a.device}
     bus = TopicBus()
     window = 2 * a.batch * a.workers
     if a.camera:
@@ -109,15 +146,16 @@ def main():
         warm = 2 * a.batch
         msgs_in = [msgs.CompressedImage(header=msgs.Header(seq=i + 1, frame_id="cam"), format="jpeg",
                                         data=jpegs[i % 8]) for i in range(warm + a.camera)]
-        eng = LocalDetector2D(batch=a.batch, device=a.device, letterbox=True)
         st = _Stages()
-        drv = RosInference(engine=eng, params={"sub_topic": "/cam", "pub_topic": "/cam_out"}, bus=bus,
+        drv = RosInference(engine=eng2, params={"sub_topic": "/cam", "pub_topic": "/cam_out"}, bus=bus,
                            batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
         drv.start_inference(spin=False)
         _run(bus, "/cam", "/cam_out", msgs.Image, msgs_in[:warm], window, a.timeout)  # warm-up + graphs
         st.sum.clear(), st.n.clear()
         n, dt, ok = _run(bus, "/cam", "/cam_out", msgs.Image, msgs_in[warm:], window, a.timeout)
         drv.stop()
+        if info is not None:
+            eng2.close()
         out["camera"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
                          "input": f"CompressedImage JPEG {W}x{H} q90", "output": "annotated Image + Detection2DArray",
                          "stages": st.summary()}
@@ -133,20 +171,24 @@ def main():
                                             width=c.width, fields=c.fields, is_bigendian=False,
                                             point_step=c.point_step, row_step=c.row_step, data=c.data,
                                             is_dense=True))
-        eng = LocalDetector3D(batch=a.batch, device=a.device)
         st = _Stages()
-        drv = RosInference3D(engine=eng, params={"sub_topic": "/pc", "pub_topic": "/pc_out"}, bus=bus,
+        drv = RosInference3D(engine=eng3, params={"sub_topic": "/pc", "pub_topic": "/pc_out"}, bus=bus,
                              batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
         drv.start_inference(spin=False)
         _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, msgs_in[:warm], window, a.timeout)
         st.sum.clear(), st.n.clear()
         n, dt, ok = _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, msgs_in[warm:], window, a.timeout)
         drv.stop()
+        if info is not None:
+            eng3.close()
         out["lidar"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
                         "input": f"PointCloud2 {clouds[0].width} points x {clouds[0].point_step} B",
                         "output": "jsk BoundingBoxArray (label 2, score > 0.5)", "stages": st.summary()}
     bus.close()
     print(json.dumps(out), flush=True)
+    if info is not None:
+        from triton_client_amd.parallel.dp import shutdown
+        shutdown(info)
 
 
 if __name__ == "__main__":
