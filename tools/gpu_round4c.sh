@@ -6,11 +6,12 @@ O=$R/gpurun_out/r4
 mkdir -p $O
 cd $R
 fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2: stopping"; exit $1;; esac; }
-for v in two_comms one_comm_prewarm; do
+for v in two_comms one_comm_prewarm one_comm; do
   echo "== rccl $v"
   timeout -k 5 90 python -u tools/rccl_two_graphs.py --variant $v > $O/rccl_$v.log 2>&1; rc=$?
-  grep -v "^RCCL\|^HIP\|^ROCm\|^Hostname\|^Librccl" $O/rccl_$v.log | tail -12
+  grep -v "^RCCL\|^HIP\|^ROCm\|^Hostname\|^Librccl" $O/rccl_$v.log | tail -30
   fatal $rc rccl_$v
+  grep -q "^Timeout" $O/rccl_$v.log && { echo "rccl_$v hung (faulthandler): stopping"; exit 1; }
 done
 echo "== driver bench"
 timeout -k 10 300 python -u tools/driver_bench.py --camera 1024 --lidar 1024 --batch 32 --workers 3 \
@@ -30,7 +31,3 @@ for br in camera lidar; do
   fatal $rc layers_$br
   head -30 $O/layers_$br.txt
 done
-echo "== rccl one_comm (the arrangement that hung in test_rccl; last on purpose)"
-timeout -k 5 60 python -u tools/rccl_two_graphs.py --variant one_comm > $O/rccl_one_comm.log 2>&1; rc=$?
-grep -v "^RCCL\|^HIP\|^ROCm\|^Hostname\|^Librccl" $O/rccl_one_comm.log | tail -12
-echo "one_comm rc=$rc"

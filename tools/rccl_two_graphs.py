@@ -10,6 +10,7 @@ one_comm_prewarm: both sets warmed up eagerly before either graph is captured.
 two_comms: one communicator per input set (each graph owns its comm).
 """
 import argparse
+import os
 import sys
 import time
 
@@ -23,7 +24,11 @@ def log(msg):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variant", default="one_comm", choices=["one_comm", "one_comm_prewarm", "two_comms"])
+    ap.add_argument("--teardown", default="reset", choices=["reset", "del"])
+    ap.add_argument("--close", default="abort", choices=["abort", "close"])
     a = ap.parse_args()
+    import faulthandler
+    faulthandler.dump_traceback_later(45, exit=True)
     import torch
 
     from triton_client_amd.parallel.rccl import RECV, SEND, NativeComm
@@ -66,12 +71,25 @@ def main():
         got = float(dst[k][0].reshape(-1)[0])
         log(f"replay {t} (set {k}): got {got} want {v}")
         ok &= got == v and int(dst[k][1][0]) == int(v)
+    import gc
+    graphs = [r.graph for r in runs]
     del runs
+    gc.collect()
+    log(f"runners released; graph refcounts {[sys.getrefcount(g) - 2 for g in graphs]}")
+    if a.teardown == "reset":
+        for g in graphs:
+            g.reset()
+        log("graphs reset")
+    del graphs
+    gc.collect()
     torch.cuda.synchronize()
-    for c in comms:
-        c.abort()
+    log("synchronized")
+    for i, c in enumerate(comms):
+        getattr(c, a.close)()
+        log(f"comm {i} {a.close}ed")
     log("OK" if ok else "MISMATCH")
-    sys.exit(0 if ok else 1)
+    sys.stdout.flush()
+    os._exit(0 if ok else 1)
 
 
 if __name__ == "__main__":
