@@ -829,6 +829,13 @@ def main():
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     shutdown(info)
+    if native is not None:
+        # the step graphs hold RCCL work over the native communicator: leave without running
+        # their destructors against it at interpreter exit (GraphRunner.release documents the
+        # teardown order; the OS reclaims the communicator and the graphs together)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -136,8 +136,7 @@ def test_native_gather_plan_in_step_graph():
             torch.cuda.synchronize()
             for k, (d, s) in enumerate(zip(dst, src)):
                 assert torch.equal(d, s) and float(d.reshape(-1)[0]) == v + k
-        del run  # the graph holds RCCL work: release it before the communicator goes
-        torch.cuda.synchronize()
+        run.release()  # the graph holds RCCL work: release it before the communicator goes
     finally:
         comm.abort()
 
@@ -153,6 +152,7 @@ def test_native_gather_plan_in_two_double_buffered_graphs():
 
     torch.cuda.set_device(0)
     comm = NativeComm(0, 1)
+    runs = []
     try:
         inputs = [torch.zeros(1, device="cuda"), torch.zeros(1, device="cuda")]
         src = [torch.zeros((32, 300, 4), device="cuda"), torch.zeros((32,), dtype=torch.int32, device="cuda")]
@@ -165,9 +165,9 @@ def test_native_gather_plan_in_two_double_buffered_graphs():
                 comm.group_p2p([(RECV, d, 0) for d in dst[k]] + [(SEND, s, 0) for s in src])
                 return src
             return fn
-        runs = [GraphRunner(step(0)), GraphRunner(step(1))]
-        for r in runs:
-            r.capture()
+        runs += [GraphRunner(step(0)), GraphRunner(step(1))]
+        for run in runs:
+            run.capture()
         for t, v in enumerate((2.0, 5.0, 9.0, 13.0)):
             k = t % 2
             inputs[k].fill_(v)
@@ -177,7 +177,7 @@ def test_native_gather_plan_in_two_double_buffered_graphs():
             if t:  # the other set still holds the previous step's gather
                 prev = (2.0, 5.0, 9.0, 13.0)[t - 1]
                 assert float(dst[1 - k][0].reshape(-1)[-1]) == prev
-        del runs
-        torch.cuda.synchronize()
     finally:
+        for r in runs:  # the graphs go before the communicator (GraphRunner.release)
+            r.release()
         comm.abort()

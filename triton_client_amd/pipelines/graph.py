@@ -205,3 +205,14 @@ class GraphRunner:
                 return self.out
         self.graph.replay()
         return self.out
+
+    def release(self) -> None:
+        """Destroy the captured graph now (the next call re-captures).  A graph holding
+        RCCL work must be released BEFORE its communicator is aborted / destroyed: the
+        graph's teardown hands RCCL's persistent plan back to the communicator, so a
+        graph outliving it (a stray reference, a loop variable) blocks in that teardown
+        (tools/rccl_two_graphs.py: the two-graph gather replays correctly either way)."""
+        if self.graph is not None:
+            torch.cuda.synchronize()
+            self.graph.reset()
+            self.graph = None
