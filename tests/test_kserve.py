@@ -198,6 +198,99 @@ def test_dynamic_batching_concurrent_requests_and_isolation():
     assert m._batcher is None
 
 
+class _PipelinedEcho(_PickyEcho):
+    """A model that claims a GPU and issues batches asynchronously: issue() returns at
+    once, finish() blocks until the test releases that batch (the device's work)."""
+
+    def __init__(self, name):
+        super().__init__(name)
+        import threading
+        import types
+        self.device = types.SimpleNamespace(type="cuda")
+        self.pipeline_depth = 2
+        self.sizes, self.sets, self.gates, self.in_flight, self.max_in_flight = [], [], [], 0, 0
+        self.mu = threading.Lock()
+
+    def stream_context(self, k=0):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def execute_batch_async(self, batch, requested, dsts=None, inst=0):
+        import threading
+        if any(float(x["INPUT0"].reshape(-1)[0]) == 7777.0 for x in batch):
+            raise RuntimeError("issue failed")  # the whole batch falls back to per-request execute
+        gate = threading.Event()
+        with self.mu:
+            self.sizes.append(len(batch))
+            self.sets.append(inst)
+            self.gates.append(gate)
+            self.in_flight += 1
+            self.max_in_flight = max(self.max_in_flight, self.in_flight)
+        outs = []
+        for x in batch:
+            try:
+                outs.append(super().execute(x, requested))
+            except Exception as e:  # noqa: BLE001 - a per-request error entry, as the GPU plans return
+                outs.append(e)
+
+        def finish():
+            assert gate.wait(10)
+            with self.mu:
+                self.in_flight -= 1
+            return outs
+        return finish
+
+
+def test_pipelined_batcher_overlaps_batches_and_isolates_failures():
+    """DynamicBatcher._run_pipelined: batch k + 1 is issued on the other plan set while batch k
+    is still in flight (two at most), every caller gets its own result, a per-request error
+    entry fails only that request, and a batch whose issue raises is re-run request by request."""
+    import threading
+    import time as _t
+
+    from triton_client_amd.server.model import InferError
+
+    m = _PipelinedEcho("pecho")
+    m.dynamic_batch, m.batch_delay_s = 4, 0.01
+    m.load()
+    assert m.pipelined() and m.plan_set_count() == 2
+    n = 24
+    res, errs = [None] * n, [None] * n
+
+    def call(i):
+        v = -1.0 if i == 5 else (7777.0 if i == 11 else float(i))
+        try:
+            res[i] = m({"INPUT0": np.full((3,), v, np.float32)}, ["OUTPUT0"], encode=lambda o: o["OUTPUT0"].copy())
+        except (InferError, RuntimeError) as e:
+            errs[i] = e
+
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    released = 0
+    deadline = _t.time() + 20
+    while any(t.is_alive() for t in ts) and _t.time() < deadline:
+        with m.mu:
+            gates = list(m.gates)
+        if released < len(gates):
+            _t.sleep(0.02)  # let the batcher issue the next batch before releasing this one
+            gates[released].set()
+            released += 1
+        else:
+            _t.sleep(0.002)
+    for t in ts:
+        t.join(5)
+    assert isinstance(errs[5], InferError)
+    assert res[11] is not None and np.array_equal(res[11], np.full((3,), 7777.0, np.float32))  # isolated re-run
+    for i in range(n):
+        if i not in (5, 11):
+            assert errs[i] is None and np.array_equal(res[i], np.full((3,), float(i), np.float32)), i
+    assert m.max_in_flight == 2, m.max_in_flight  # overlapped, never more than the plan sets
+    assert set(m.sets) == {0, 1}
+    m.unload()
+    assert m._batcher is None
+
+
 def test_dynamic_batching_over_grpc():
     import concurrent.futures as cf
 

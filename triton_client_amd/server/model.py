@@ -162,11 +162,18 @@ class DynamicBatcher:
         self.stopped = False
         self.batches = 0
         self.forming = threading.Lock()
-        # one batcher thread per model instance (Triton instance_group count): instance k runs
-        # its batches on its own plans, stream and lock, so one instance stages / encodes while
-        # another's graph runs on the GPU
-        self.threads = [threading.Thread(target=self._run, args=(k,), name=f"batcher-{model.name}-{k}", daemon=True)
-                        for k in range(max(1, model.instances))]
+        self.sets = model.plan_set_count() if model.pipelined() else 1
+        if self.sets > 1:
+            # pipelined: ONE batcher thread issues batch k + 1 on the next plan set (its own stream)
+            # as soon as batch k is queued on the GPU; a finisher thread waits for each batch in
+            # order and answers its requests (batches keep their full size: nothing splits them)
+            self.threads = [threading.Thread(target=self._run_pipelined, name=f"batcher-{model.name}", daemon=True)]
+        else:
+            # one batcher thread per model instance (Triton instance_group count): instance k runs
+            # its batches on its own plans, stream and lock, so one instance stages / encodes while
+            # another's graph runs on the GPU
+            self.threads = [threading.Thread(target=self._run, args=(k,), name=f"batcher-{model.name}-{k}",
+                                             daemon=True) for k in range(max(1, model.instances))]
         for t in self.threads:
             t.start()
 
@@ -232,6 +239,87 @@ class DynamicBatcher:
             finally:
                 GPU_PHASE.release_shared()
 
+    def _run_pipelined(self) -> None:
+        import queue
+        m = self.model
+        jobs: "queue.Queue" = queue.Queue()
+        fin = threading.Thread(target=self._finisher, args=(jobs,), name=f"finisher-{m.name}", daemon=True)
+        fin.start()
+        k = 0
+        try:
+            while True:
+                items = self._take()
+                if items is None:
+                    return
+                with self.cv:
+                    self.batches += 1
+                s = k % self.sets
+                k += 1
+                GPU_PHASE.acquire_shared()
+                lock = m.instance_lock(s)
+                lock.acquire()  # plan set s is free once the finisher is done with its previous batch
+                t0 = time.perf_counter()
+                try:
+                    dsts = [it.out_dst for it in items]
+                    with m.stream_context(s):
+                        finish = m.execute_batch_async([it.inputs for it in items], items[0].requested,
+                                                       dsts=dsts if m.accepts_out_dst and any(dsts) else None, inst=s)
+                except Exception:  # noqa: BLE001 - isolate the failing request(s) below
+                    lock.release()
+                    GPU_PHASE.release_shared()
+                    self._isolate(m, items)
+                    continue
+                jobs.put((items, finish, lock, t0))
+        finally:
+            jobs.put(None)
+            fin.join()
+
+    def _finisher(self, jobs) -> None:
+        m = self.model
+        while True:
+            job = jobs.get()
+            if job is None:
+                return
+            items, finish, lock, t0 = job
+            try:
+                outs = finish()
+                t1 = time.perf_counter()
+                for it, o in zip(items, outs):
+                    if isinstance(o, BaseException):
+                        it.exc = o
+                        it.done.set()
+                    else:
+                        self._finish(it, o)
+                if PROFILE.on:
+                    PROFILE.add(f"{m.name}.execute_batch", t1 - t0)
+                    PROFILE.add(f"{m.name}.batch_items", float(len(items)))
+                    PROFILE.add(f"{m.name}.encode_in_batcher", time.perf_counter() - t1, len(items))
+                failed = False
+            except Exception:  # noqa: BLE001
+                failed = True
+            finally:
+                lock.release()
+                GPU_PHASE.release_shared()
+            if failed:
+                self._isolate(m, items)
+
+    def _isolate(self, m: "ServedModel", items) -> None:
+        """Run a failed batch's unanswered requests one by one (one bad request cannot
+        fail its neighbours)."""
+        GPU_PHASE.acquire_shared()
+        try:
+            with m.instance_lock(0):
+                for it in items:
+                    if it.done.is_set():
+                        continue
+                    try:
+                        self._finish(it, m.execute(it.inputs, it.requested))
+                    except Exception as e:  # noqa: BLE001 - handed to the waiting request thread
+                        it.exc = e
+                        it.done.set()
+        finally:
+            GPU_PHASE.release_shared()
+
     def _execute(self, m: "ServedModel", items, k: int = 0) -> None:
         with m.instance_lock(k):
             try:
@@ -289,6 +377,9 @@ class ServedModel(ABC):
     # Triton instance_group count: dynamic-batching executions in flight at once (a model with
     # instances > 1 takes execute_batch(..., inst=k) and keeps per-instance plans)
     instances = 1
+    # batches in flight on one batcher (models with execute_batch_async(..., inst=k) -> finish():
+    # plan set k issues on its own stream, finish() waits for that batch only)
+    pipeline_depth = 1
 
     def __init__(self, name: str, version: str = "1"):
         self.name = name
@@ -300,6 +391,16 @@ class ServedModel(ABC):
         self._batcher: Optional[DynamicBatcher] = None
         self._streams: Dict[int, object] = {}  # HIP streams of this model's own (per instance)
         self._inst_locks: Dict[int, threading.Lock] = {0: self._lock}
+
+    def pipelined(self) -> bool:
+        """Dynamic batches run pipelined (DynamicBatcher._run_pipelined)."""
+        dev = getattr(self, "device", None)
+        return (self.pipeline_depth > 1 and callable(getattr(self, "execute_batch_async", None))
+                and getattr(dev, "type", None) == "cuda")
+
+    def plan_set_count(self) -> int:
+        """Plan sets a GPU model builds: one per batch in flight (pipelined) or per instance."""
+        return max(1, self.instances, self.pipeline_depth if self.pipelined() else 1)
 
     def instance_lock(self, k: int = 0) -> threading.Lock:
         """Lock of instance k (instance 0: the model lock of direct executions)."""
@@ -356,7 +457,7 @@ class ServedModel(ABC):
         # no execution of this model (batched or direct) is mid-run past this point
         GPU_PHASE.acquire_exclusive()
         try:
-            locks = [self.instance_lock(k) for k in range(max(1, self.instances))]
+            locks = [self.instance_lock(k) for k in range(self.plan_set_count())]
             for lk in locks:
                 lk.acquire()
             try:

@@ -211,6 +211,15 @@ def _instances(n: Optional[int]) -> int:
     return max(1, int(n))
 
 
+def _depth(d: Optional[int]) -> int:
+    """Batches in flight per served GPU model (DynamicBatcher pipelining): the explicit value,
+    else TCA_SERVE_PIPELINE, else 2 -- batch k + 1 is staged, DMA'd and replayed on the other
+    plan set's stream while batch k's D2H runs and its responses are encoded."""
+    if d is None:
+        d = int(os.environ.get("TCA_SERVE_PIPELINE", "2"))
+    return max(1, int(d))
+
+
 def _pick(plans: Dict[int, object], n: int):
     return plans[min(b for b in plans if b >= n)]
 
@@ -254,6 +263,12 @@ class _YoloPlan:
         shared-memory slice}; a slice inside a page-locked region receives its output
         by DMA straight from the device, a device region (device shared memory) by the
         segment-copy kernel (the response encoder then has nothing to copy)."""
+        return self.issue(images, dsts)()
+
+    def issue(self, images: Sequence[np.ndarray], dsts=None):
+        """Stage, DMA, replay and queue the D2H on the current stream without waiting:
+        returns finish() -> the outputs (waits for this batch's work only).  The plan's
+        buffers stay in use until finish() returns."""
         n, img = len(images), self.img
         clk = _PlanClock("YOLOv5")
         segs, host = _Segs(), []
@@ -295,10 +310,15 @@ class _YoloPlan:
         if rest:
             _copy_all([outs[i] for i in rest], [self.dec_slots[i] for i in rest])
         clk.mark("d2h")
-        torch.cuda.current_stream().synchronize()
-        clk.mark("sync")
-        clk.done()
-        return [{"output": o} for o in outs]
+        done = torch.cuda.Event()
+        done.record()
+
+        def finish():
+            done.synchronize()
+            clk.mark("sync")
+            clk.done()
+            return [{"output": o} for o in outs]
+        return finish
 
 
 def check_voxel_shapes(inputs, P: int, max_voxels: int) -> int:
@@ -417,6 +437,11 @@ class _PointPillarsPlan:
         return True
 
     def run(self, batch: Sequence[Dict[str, np.ndarray]]) -> List[Dict[str, np.ndarray]]:
+        return self.issue(batch)()
+
+    def issue(self, batch: Sequence[Dict[str, np.ndarray]]):
+        """As _YoloPlan.issue: everything queued on the current stream, finish() waits
+        for this batch and reads its results out of the pinned outputs."""
         n = len(batch)
         self.pin_vcount_np[:] = 0
         segs = _Segs()
@@ -465,27 +490,33 @@ class _PointPillarsPlan:
         clk.mark("graph")
         torch._foreach_copy_(self.d2h_dst, self.d2h_src, non_blocking=True)  # all B slots: one call
         clk.mark("d2h")
-        torch.cuda.current_stream().synchronize()
-        clk.mark("sync")
-        cnt, box, score, cls = self.pin_np
-        bad = self.pin_flags_np
-        res = [InferError(f"voxel_coords outside the {self.grid[2]}x{self.grid[1]}x{self.grid[0]} (z, y, x) grid "
-                          f"or voxel_num_points outside [1, {self.P}]") if bad[i] else
-               {"pred_boxes": box[i, :k], "pred_scores": score[i, :k],
-                "pred_labels": cls[i, :k].astype(np.int64, copy=False)}
-               for i, k in enumerate(cnt[:n].tolist())]
-        clk.mark("result")
-        clk.done()
-        return res
+        done = torch.cuda.Event()
+        done.record()
+
+        def finish():
+            done.synchronize()
+            clk.mark("sync")
+            cnt, box, score, cls = self.pin_np
+            bad = self.pin_flags_np
+            res = [InferError(f"voxel_coords outside the {self.grid[2]}x{self.grid[1]}x{self.grid[0]} (z, y, x) "
+                              f"grid or voxel_num_points outside [1, {self.P}]") if bad[i] else
+                   {"pred_boxes": box[i, :k], "pred_scores": score[i, :k],
+                    "pred_labels": cls[i, :k].astype(np.int64, copy=False)}
+                   for i, k in enumerate(cnt[:n].tolist())]
+            clk.mark("result")
+            clk.done()
+            return res
+        return finish
 
 
 class YoloV5Model(ServedModel):
     def __init__(self, name: str = "YOLOv5nCOCO", variant: str = "n", nc: int = 80, img: int = 640,
                  device="auto", weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 100.0,
-                 batch: int = 16, instances: Optional[int] = None):
+                 batch: int = 16, instances: Optional[int] = None, pipeline_depth: Optional[int] = None):
         super().__init__(name)
         self.batch = batch  # dynamic batching: concurrent requests run as one captured batch-`batch` graph
         self.instances = _instances(instances)
+        self.pipeline_depth = _depth(pipeline_depth)
         self.variant, self.nc, self.img = variant, nc, img
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -520,7 +551,7 @@ class YoloV5Model(ServedModel):
             # pipeline), all over the calibrated module
             sizes = sorted({b for b in PLAN_SIZES if b <= max(1, self.batch)} | {max(1, self.batch)})
             self.plan_sets = [{b: _YoloPlan(self.pipe, b, self.img, self.device) for b in sizes}
-                              for _ in range(self.instances)]
+                              for _ in range(self.plan_set_count())]
             self.plans = self.plan_sets[0]
             self.dynamic_batch = max(sizes)
         else:
@@ -553,14 +584,20 @@ class YoloV5Model(ServedModel):
             return [self.execute(x, requested) for x in batch]
         return _pick(self.plan_sets[inst], len(batch)).run([x["images"] for x in batch], dsts)
 
+    @torch.no_grad()
+    def execute_batch_async(self, batch, requested, dsts=None, inst: int = 0):
+        """Plan set ``inst`` issues the batch on the current stream; returns finish()."""
+        return _pick(self.plan_sets[inst], len(batch)).issue([x["images"] for x in batch], dsts)
+
 
 class PointPillarsModel(ServedModel):
     def __init__(self, name: str = "pointpillar_kitti", cfg: Optional[PointPillarsConfig] = None, device="auto",
                  weights: Optional[str] = None, seed: int = 0, calibrate_target: float = 2000.0,
-                 batch: int = 16, instances: Optional[int] = None):
+                 batch: int = 16, instances: Optional[int] = None, pipeline_depth: Optional[int] = None):
         super().__init__(name)
         self.batch = batch  # dynamic batching: concurrent requests share one batch-`batch` pass
         self.instances = _instances(instances)
+        self.pipeline_depth = _depth(pipeline_depth)
         self.cfg = cfg or PointPillarsConfig()
         self.device = _device(device)
         self.weights, self.seed, self.calibrate_target = weights, seed, calibrate_target
@@ -608,7 +645,7 @@ class PointPillarsModel(ServedModel):
             self.model = self.pipe.model
             sizes = sorted({b for b in PLAN_SIZES if b <= max(1, self.batch)} | {max(1, self.batch)})
             self.plan_sets = [{b: _PointPillarsPlan(self.model, self.cfg, b, self.device) for b in sizes}
-                              for _ in range(self.instances)]
+                              for _ in range(self.plan_set_count())]
             self.plans = self.plan_sets[0]
             self.dynamic_batch = max(sizes)
         else:
@@ -637,6 +674,10 @@ class PointPillarsModel(ServedModel):
         if self.device.type != "cuda":
             return [self.execute(x, requested) for x in batch]
         return _pick(self.plan_sets[inst], len(batch)).run(batch)  # an out-of-range request's entry is its InferError
+
+    @torch.no_grad()
+    def execute_batch_async(self, batch, requested, dsts=None, inst: int = 0):
+        return _pick(self.plan_sets[inst], len(batch)).issue(batch)
 
     @torch.no_grad()
     def execute(self, inputs, requested):
