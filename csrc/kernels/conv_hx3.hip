@@ -130,65 +130,6 @@ __device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* sm
   }
 }
 
-// direct epilogue: bias + act straight from the accumulators to global pair storage, no LDS
-// round trip and no barrier.  Lane (fr, fq) of fragment (i, j) holds channels fq * 4 .. + 3 of
-// one pixel: in pair storage those are 8 B of the 8-channel group's hi half and 8 B of its lo
-// half, so the lane stores (and reads its residual as) two 8-B pieces; the four lanes of a
-// pixel cover 64 contiguous bytes.  Same arithmetic in the same order as hx3_epilogue
-// (bit-identical outputs).
-template <int TH, int BN, int WM, int WN, bool CM>
-__device__ __forceinline__ void hx3_epilogue_direct(const Hx3Args& a, const f32x4 (&acc)[TH / WM][BN / WN / 16],
-                                                    int b, int oy0, int ox0, int n0) {
-  constexpr int FM = TH / WM, FN = BN / WN / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
-  const int act = a.act & 15;
-  const bool post_res = (a.act & 16) != 0 && a.res_f != nullptr;
-  const int eact = post_res ? 0 : act;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + (wn * FN + j) * 16 + fq * 4;
-    const int coff = (n & ~7) + ((n & 7) >> 1);  // float offset of the 4 channels' hi bf16s in the pair group
-    const float4 bv = a.bias ? *reinterpret_cast<const float4*>(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int line = wm * FM + i;
-      const int oy = oy0 + (CM ? fr : line), ox = ox0 + (CM ? line : fr);
-      if (oy >= a.Ho || ox >= a.Wo) continue;
-      float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
-      if (eact == 1) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      } else if (eact != 0) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_fn(v[e], eact);
-      }
-      const long pix = ((long)b * a.Ho + oy) * a.Wo + ox;
-      if (a.res_f) {
-        const float* rp = a.res_f + pix * a.ldr + a.r_off + coff;
-        const uint2 rh = *reinterpret_cast<const uint2*>(rp);
-        const uint2 rl = *reinterpret_cast<const uint2*>(rp + 4);
-        const __bf16* h = reinterpret_cast<const __bf16*>(&rh);
-        const __bf16* l = reinterpret_cast<const __bf16*>(&rl);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float r = (float)h[e] + (float)l[e];
-          v[e] = post_res ? act_fn(v[e] + r, act) : v[e] + r;
-        }
-      }
-      __bf16 h[4], l[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        h[e] = (__bf16)v[e];
-        l[e] = (__bf16)(v[e] - (float)h[e]);
-      }
-      float* o = a.out_f + pix * a.ldo + a.co_off + coff;
-      *reinterpret_cast<uint2*>(o) = *reinterpret_cast<const uint2*>(h);
-      *reinterpret_cast<uint2*>(o + 4) = *reinterpret_cast<const uint2*>(l);
-    }
-  }
-}
-
 // ---- x3 pair, halo-tiled 3x3 stride 1, v3 ("hx3"): weights streamed to registers.
 //
 // PMC of hx (profiles/r2/pmc_lidar_end/summary.md): waves 34% parked at the per-step
@@ -211,7 +152,7 @@ template <int V> struct IC { static constexpr int value = V; };
 
 // PAIRS: two chunks per loop iteration (even chunk counts), the tap groups alternating
 // between two static weight register sets: no register copy between groups
-template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2, bool PAIRS = false, bool DIRECT = false>
+template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2, bool PAIRS = false>
 __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a) {
   constexpr int TW = 16, BM = TH * TW, NW = WM * WN, NT = NW * 64;
   constexpr int FM = TH / WM, FN = BN / WN / 16;
@@ -221,7 +162,7 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   constexpr int HPIECES = HP * 8;                    // 16-B pieces of one 32-channel pair chunk
   constexpr int HPL = (HPIECES + NT - 1) / NT;       // halo loads per lane per chunk
   constexpr int HBYTES = HP * 128;
-  constexpr int EPI = DIRECT ? 0 : BM * BN * 4;  // the LDS epilogue tile reuses the halo buffers
+  constexpr int EPI = BM * (BN + 4) * 4;
   constexpr int LDS = (HB * HBYTES > EPI) ? HB * HBYTES : EPI;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
 
@@ -397,14 +338,11 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
       chunk_end(c);
     }
   }
-  if constexpr (DIRECT) {
-    hx3_epilogue_direct<TH, BN, WM, WN, CM>(a, acc, b, oy0, ox0, n0);
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
-    asm volatile("" ::: "memory");
-    hx3_epilogue<TH, BN, WM, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
+  asm volatile("" ::: "memory");
+
+  hx3_epilogue<TH, BN, WM, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
 }
 
 // ---- stride 2 ("hx3s2"): the 3x3 stride-2 pad-1 conv as four phase sub-convolutions.
@@ -433,7 +371,7 @@ template <int G> struct S2Group {
   __device__ static constexpr int loff(int li) { return PL == 0 ? 1 : li; }     // its halo line shift
 };
 
-template <int TH, int BN, int WN, bool CM, int MINW, bool OCC, bool DIRECT = false>
+template <int TH, int BN, int WN, bool CM, int MINW, bool OCC>
 __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
   constexpr int TW = 16, NT = WN * 64;
   constexpr int FM = TH, FN = BN / WN / 16;
@@ -442,7 +380,7 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
   constexpr int HPIECES = HP * 8;
   constexpr int HPL = (HPIECES + NT - 1) / NT;
   constexpr int HBYTES = HP * 128;
-  constexpr int EPI = DIRECT ? 0 : TH * TW * BN * 4;
+  constexpr int EPI = TH * TW * (BN + 4) * 4;
   constexpr int LDS = (2 * HBYTES > EPI) ? 2 * HBYTES : EPI;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
 
@@ -544,8 +482,7 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
 #pragma unroll
     for (int k = 0; k < HPL; ++k) mine |= h_ph[k];
     if (!__syncthreads_or(mine != 0u)) {
-      if constexpr (DIRECT) hx3_epilogue_direct<TH, BN, 1, WN, CM>(a, acc, b, oy0, ox0, n0);
-      else hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
+      hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
       return;
     }
   }
@@ -611,26 +548,22 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
     group(IC<4>{}, c, w0, w1);
     group(IC<5>{}, c, w1, w0);
   }
-  if constexpr (DIRECT) {
-    hx3_epilogue_direct<TH, BN, 1, WN, CM>(a, acc, b, oy0, ox0, n0);
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
-    asm volatile("" ::: "memory");
-    hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the epilogue reuses the halo LDS
+  asm volatile("" ::: "memory");
+  hx3_epilogue<TH, BN, 1, WN, CM>(a, smem, acc, b, oy0, ox0, n0);
 }
 
 
-template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2, bool DIRECT = false>
+template <int TH, int BN, int WM, int WN, bool CM, int HB, int MINW = 2>
 int launch_hx3(const Hx3Args& a, hipStream_t stream) {
   if (a.N % BN) return (int)hipErrorInvalidValue;
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
   if ((a.Cin / 32) % 2 == 0)
-    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, true, DIRECT><<<nwg, WM * WN * 64, 0, stream>>>(a);
+    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, true><<<nwg, WM * WN * 64, 0, stream>>>(a);
   else
-    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, false, DIRECT><<<nwg, WM * WN * 64, 0, stream>>>(a);
+    conv_hx3_kernel<TH, BN, WM, WN, CM, HB, MINW, false><<<nwg, WM * WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -657,23 +590,18 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     // <= 168 VGPRs -> 3 workgroups (12 waves) per CU
     case 5: return launch_hx3<8, 64, 1, 4, false, 2, 3>(a, stream);
     case 6: return launch_hx3<8, 64, 1, 4, true, 2, 3>(a, stream);
-    // | 16: the same tiles with the direct (LDS-free) epilogue
-    case 16 | 1: return launch_hx3<8, 128, 1, 4, false, 2, 2, true>(a, stream);
-    case 16 | 2: return launch_hx3<8, 128, 1, 4, true, 2, 2, true>(a, stream);
-    case 16 | 5: return launch_hx3<8, 64, 1, 4, false, 2, 3, true>(a, stream);
-    case 16 | 6: return launch_hx3<8, 64, 1, 4, true, 2, 3, true>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }
 
 
-template <int TH, int BN, int WN, bool CM, int MINW, bool DIRECT = false>
+template <int TH, int BN, int WN, bool CM, int MINW>
 int launch_hx3s2(const Hx3Args& a, hipStream_t stream) {
   if (a.N % BN) return (int)hipErrorInvalidValue;
   const int ex = CM ? TH : 16, ey = CM ? 16 : TH;
   const int nwg = a.B * ((a.Ho + ey - 1) / ey) * ((a.Wo + ex - 1) / ex) * (a.N / BN);
-  if (a.occ) conv_hx3s2_kernel<TH, BN, WN, CM, MINW, true, DIRECT><<<nwg, WN * 64, 0, stream>>>(a);
-  else conv_hx3s2_kernel<TH, BN, WN, CM, MINW, false, DIRECT><<<nwg, WN * 64, 0, stream>>>(a);
+  if (a.occ) conv_hx3s2_kernel<TH, BN, WN, CM, MINW, true><<<nwg, WN * 64, 0, stream>>>(a);
+  else conv_hx3s2_kernel<TH, BN, WN, CM, MINW, false><<<nwg, WN * 64, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -692,10 +620,6 @@ int hx3s2_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     case 2: return launch_hx3s2<8, 128, 4, true, 2>(a, stream);
     case 3: return launch_hx3s2<8, 64, 4, false, 3>(a, stream);
     case 4: return launch_hx3s2<8, 64, 4, true, 3>(a, stream);
-    case 16 | 1: return launch_hx3s2<8, 128, 4, false, 2, true>(a, stream);
-    case 16 | 2: return launch_hx3s2<8, 128, 4, true, 2, true>(a, stream);
-    case 16 | 3: return launch_hx3s2<8, 64, 4, false, 3, true>(a, stream);
-    case 16 | 4: return launch_hx3s2<8, 64, 4, true, 3, true>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

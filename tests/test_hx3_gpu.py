@@ -158,34 +158,3 @@ def test_hx3s2_occupancy_reads_unmarked_pixels_as_zero(cuda, tile):
     ref = torch.relu(conv((xin * occ[..., None].double()).permute(0, 3, 1, 2)))
     assert rel_l2(out.nchw(), ref) < 5e-5, rel_l2(out.nchw(), ref)
     assert rel_l2(dflt.nchw(), ref) < 5e-5
-
-
-# direct (LDS-free) epilogue twins: bit-identical to the LDS epilogue of the same tile
-DIRECT_TWINS = [(151, 111, 1), (152, 112, 1), (155, 115, 1), (156, 116, 1),
-                (161, 121, 2), (162, 122, 2), (163, 123, 2), (164, 124, 2)]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("post_res", [False, True])
-@pytest.mark.parametrize("direct,twin,stride", DIRECT_TWINS)
-def test_hx3_direct_epilogue_bit_identical(cuda, direct, twin, stride, post_res):
-    """Channel-offset input / output / residual slices, partial tiles in both axes, ReLU
-    after (or before) the residual add, and (stride 2) a sparse occupancy map: the direct
-    epilogue writes exactly the LDS epilogue's bits and leaves the other channels alone."""
-    torch.manual_seed(direct + 7 * post_res)
-    cout = 128 if direct in (151, 152, 161, 162) else 64
-    B, H, W, cin = 2, 37, 45, 64
-    conv = nn.Conv2d(cin, cout, 3, stride, 1, bias=True)
-    fc = FusedConv(conv, act=1, device=cuda, precision="fp32", post_res=post_res)
-    Ho, Wo = fc.out_hw(H, W)
-    occ = (torch.rand(B, H, W) < 0.3).to(torch.uint8).to(cuda) if stride == 2 else None
-    x = NHWC(to_pairs(torch.randn(B, H, W, cin + 8)).to(cuda), 8, cin, pair=True, occ=occ)
-    r = NHWC(to_pairs(torch.randn(B, Ho, Wo, cout + 16)).to(cuda), 16, cout, pair=True)
-    outs = []
-    for t in (direct, twin):
-        out = torch.full((B, Ho, Wo, cout + 24), 7.0, dtype=torch.float32, device=cuda)
-        fc(x, out=NHWC(out, 16, cout, pair=True), res=r, tile=t)
-        torch.cuda.synchronize()
-        assert (out[..., :16] == 7.0).all() and (out[..., 16 + cout:] == 7.0).all()
-        outs.append(out)
-    assert torch.equal(outs[0], outs[1])

@@ -110,22 +110,6 @@ HX3 = os.environ.get("TCA_HX3", "1") != "0"
 HX3S2 = HX3 and os.environ.get("TCA_HX3S2", "1") != "0"
 HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
-# the same tiles with the direct (LDS-free) epilogue: 150 + t (hx3 t = 1, 2, 5, 6), 160 + t (hx3s2 t = 1-4)
-HX3D_TILES = (151, 152, 155, 156)
-HX3S2D_TILES = (161, 162, 163, 164)
-
-
-def _hx3_tile(tile: int) -> int:
-    """Python tile number -> the kernel's hx3_launch / hx3s2_launch tile (| 16: direct epilogue)."""
-    if tile in HX3_TILES:
-        return tile - 110
-    if tile in HX3S2_TILES:
-        return tile - 120
-    if tile in HX3D_TILES:
-        return (tile - 150) | 16
-    if tile in HX3S2D_TILES:
-        return (tile - 160) | 16
-    return 0
 
 
 def frag_weights(W: torch.Tensor) -> torch.Tensor:
@@ -259,22 +243,21 @@ class FusedConv:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
-            if out.pair and self.hx3_ok() and self.s == 2 and (tile in HX3S2_TILES + HX3S2D_TILES
-                                                                 or (tile == 0 and HX3S2)):
+            if out.pair and self.hx3_ok() and self.s == 2 and (tile in HX3S2_TILES or (tile == 0 and HX3S2)):
                 occ = x.occ
                 if occ is not None:
                     assert occ.dtype == torch.uint8 and tuple(occ.shape) == (B, H, W), (occ.shape, (B, H, W))
                 _native.call("tca_conv_hx3s2p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp, _native.ptr(occ),
-                             _hx3_tile(tile), _native.stream_ptr(stream))
+                             tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
                 return out
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
-                    (tile in HX3_TILES + HX3D_TILES or (tile == 0 and HX3))):
+                    (tile in HX3_TILES or (tile == 0 and HX3))):
                 _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp,
-                             _hx3_tile(tile), _native.stream_ptr(stream))
+                             tile - 110 if tile in HX3_TILES else 0, _native.stream_ptr(stream))
                 return out
             args = (_native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off, _native.ptr(self.w_gemm),
                     _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p, self.Kp, _native.ptr(out.t), gh,

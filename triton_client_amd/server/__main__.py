@@ -57,6 +57,27 @@ def main(argv=None):
             children.append(subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", *argv_child,
                                               "--child", "--metrics-port", "0"],
                                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True))
+    # SIGTERM ends the children and writes the stage clock; installed before any child can
+    # bind the port, so a request served by a child never races the parent's handler
+    from .model import PROFILE
+    state = {"srv": None}
+    if PROFILE.on or children:
+        import os
+        import signal
+
+        def _term(*_):
+            for c in children:
+                c.terminate()
+            if PROFILE.on:
+                if args.child:  # one stage clock per process
+                    PROFILE.path = f"{PROFILE.path}.{os.getpid()}"
+                PROFILE.dump()
+            if state["srv"] is not None:
+                state["srv"].stop(0)
+            for c in children:
+                c.wait(30)
+            __import__("sys").exit(0)
+        signal.signal(signal.SIGTERM, _term)
     if args.model_repository:
         repo = ModelRepository.from_directory(args.model_repository, args.device)
     else:
@@ -79,26 +100,9 @@ def main(argv=None):
         c.stdin.flush()
     srv = KServeServer(repo, f"{args.host}:{args.port}", max_workers=args.workers,
                        metrics_port=args.metrics_port if args.metrics_port > 0 else None).start()
+    state["srv"] = srv
     logging.info("KServe-v2 server on %s, models: %s%s", srv.target, [m.name for m in repo.models()],
                  f" ({args.procs} processes)" if children else "")
-    from .model import PROFILE
-    if PROFILE.on or children:  # TCA_SERVER_PROFILE: write the stage clock when terminated
-        import os
-        import signal
-        import sys
-
-        def _term(*_):
-            for c in children:
-                c.terminate()
-            if PROFILE.on:
-                if args.child:  # one stage clock per process
-                    PROFILE.path = f"{PROFILE.path}.{os.getpid()}"
-                PROFILE.dump()
-            srv.stop(0)
-            for c in children:
-                c.wait(30)
-            sys.exit(0)
-        signal.signal(signal.SIGTERM, _term)
     srv.wait()
 
 

@@ -162,6 +162,7 @@ class DynamicBatcher:
         self.stopped = False
         self.batches = 0
         self.forming = threading.Lock()
+        self.inflight = 0  # pipelined: batches issued and not yet finished
         self.sets = model.plan_set_count() if model.pipelined() else 1
         if self.sets > 1:
             # pipelined: ONE batcher thread issues batch k + 1 on the next plan set (its own stream)
@@ -215,6 +216,12 @@ class DynamicBatcher:
                 return None
             deadline = time.perf_counter() + self.delay_s
             while len(self.q) < self.max_batch and not self.stopped:
+                if self.inflight:
+                    # pipelined, a batch on the GPU: issue the next one early only when it is full;
+                    # otherwise keep gathering until the GPU frees up (the finisher notifies), so
+                    # overlapping never splits the arriving requests into small batches
+                    self.cv.wait()
+                    continue
                 left = deadline - time.perf_counter()
                 if left <= 0:
                     break
@@ -269,6 +276,8 @@ class DynamicBatcher:
                     GPU_PHASE.release_shared()
                     self._isolate(m, items)
                     continue
+                with self.cv:
+                    self.inflight += 1
                 jobs.put((items, finish, lock, t0))
         finally:
             jobs.put(None)
@@ -300,6 +309,9 @@ class DynamicBatcher:
             finally:
                 lock.release()
                 GPU_PHASE.release_shared()
+                with self.cv:
+                    self.inflight -= 1
+                    self.cv.notify_all()
             if failed:
                 self._isolate(m, items)
 
