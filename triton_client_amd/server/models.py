@@ -213,10 +213,13 @@ def _instances(n: Optional[int]) -> int:
 
 def _depth(d: Optional[int]) -> int:
     """Batches in flight per served GPU model (DynamicBatcher pipelining): the explicit value,
-    else TCA_SERVE_PIPELINE, else 2 -- batch k + 1 is staged, DMA'd and replayed on the other
-    plan set's stream while batch k's D2H runs and its responses are encoded."""
+    else TCA_SERVE_PIPELINE, else 1.  At 2, batch k + 1 is staged, DMA'd and replayed on the
+    other plan set's stream while batch k's D2H runs and its responses are encoded.  Measured
+    with 4 + 4 client processes (profiles/r4/served/): 683 vs 741 pairs/s over shm, 266 vs 252
+    raw -- the served path is bound by host work per request (gRPC + Python), not by the GPU,
+    so one batch in flight (half the plan memory) stays the default."""
     if d is None:
-        d = int(os.environ.get("TCA_SERVE_PIPELINE", "2"))
+        d = int(os.environ.get("TCA_SERVE_PIPELINE", "1"))
     return max(1, int(d))
 
 
