@@ -91,6 +91,21 @@ class _C3Plan:
         self.a = [bufs.new(B, H, W, c_), bufs.new(B, H, W, c_)]
         self.tmp = bufs.new(B, H, W, c_)
         self.out_c = self.cv3.N
+        # c3_fused.hip (c_ = 32 / 64 / 128): fragment-order split weights, built here (never in a capture)
+        self._fw = None
+        convs = [self.cv12, self.cv3] + [c for b1, b2, _ in self.m for c in (b1, b2)] if self.cv12 is not None else []
+        if (C3_FUSED and self.cv12 is not None and c_ in (32, 64, 128) and torch.device(device).type == "cuda"
+                and all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) and c.K == c.Kp
+                        for c in convs)
+                and self.cv12.k == 1 and self.cv12.N == 2 * c_ and self.cv12.cin_p % 32 == 0
+                and self.cv3.k == 1 and self.cv3.cin_p == 2 * c_ and self.cv3.N % 64 == 0
+                and all(b1.k == 1 and b1.cin_p == c_ and b1.N == c_ and b2.k == 3 and b2.s == 1 and b2.p == 1
+                        and b2.cin_p == c_ and b2.N == c_ for b1, b2, _ in self.m)):
+            from ..ops.conv import frag_weights
+            dev = torch.device(device)
+            self._fw = (frag_weights(self.cv12.w_f32_gemm).to(dev), frag_weights(self.cv3.w_f32_gemm).to(dev),
+                        [(frag_weights(b1.w_f32_gemm).to(dev), frag_weights(b2.w_f32_gemm).to(dev))
+                         for b1, b2, _ in self.m])
 
     def fused_ok(self, x: NHWC, out: NHWC) -> bool:
         """yolo_c3s_fused (csrc/kernels/image.hip) takes this block: fp32, 32 -> 32 channels,
@@ -107,8 +122,48 @@ class _C3Plan:
                 and not x.pair and not out.pair and x.c == 32 and out.c == 32 and x.t.dtype == torch.float32
                 and x.t.is_cuda)
 
+    def fused2_ok(self, x: NHWC, out: NHWC) -> bool:
+        """c3_fused.hip takes this block (c_ = 32 / 64 / 128, plain fp32 in and out)."""
+        return (self._fw is not None and C3_FUSED and x.t.is_cuda and not x.pair and not out.pair
+                and x.t.dtype == torch.float32 and out.t.dtype == torch.float32 and x.c == self.cv12.cin_p
+                and out.c == self.cv3.N and x.off % 4 == 0 and out.off % 4 == 0
+                and x.t.shape[-1] % 4 == 0 and out.t.shape[-1] % 4 == 0)
+
+    def _fused2(self, x: NHWC, out: NHWC) -> NHWC:
+        """The block as 1 (n = 1) or n (FIRST, MID..., LAST) c3_fused launches."""
+        import ctypes
+        B, H, W, _ = x.shape
+        c_, n = self.c_, len(self.m)
+        w12, w3, wm = self._fw
+        cat_b = (self.cat.t, 2 * c_, c_)
+
+        def launch(mode, i, xin=None, ain=None, bin_=None, y=None, aout=None, bout=None):
+            b1, b2, add = self.m[i]
+            t = lambda v: v[0] if v is not None else None  # noqa: E731
+            ptrs = [t(xin), t(ain), t(bin_), t(y), t(aout), t(bout), w12, self.cv12.b_gemm, wm[i][0], b1.b_gemm,
+                    wm[i][1], b2.b_gemm, w3, self.cv3.b_gemm]
+            pa = (ctypes.c_void_p * 14)(*[_native.ptr(p) for p in ptrs])
+            ld = lambda v: (v[1], v[2]) if v is not None else (0, 0)  # noqa: E731
+            iv = [mode, c_, self.cv12.cin_p, self.cv3.N, int(bool(add)), B, H, W, *ld(xin), *ld(ain), *ld(bin_),
+                  *ld(y), *ld(aout), *ld(bout), self.cv12.act, b1.act, b2.act, self.cv3.act]
+            ia = (ctypes.c_int * 24)(*iv)
+            _native.call("tca_c3_fused", ctypes.addressof(pa), ctypes.addressof(ia), _native.stream_ptr(None))
+
+        xv, yv = (x.t, x.t.shape[-1], x.off), (out.t, out.t.shape[-1], out.off)
+        if n == 1:
+            launch(0, 0, xin=xv, y=yv)
+            return out
+        av = [(t.t, c_, 0) for t in self.a]
+        launch(1, 0, xin=xv, aout=av[0], bout=cat_b)
+        for i in range(1, n - 1):
+            launch(2, i, ain=av[(i - 1) % 2], aout=av[i % 2])
+        launch(3, n - 1, ain=av[(n - 2) % 2], bin_=cat_b, y=yv)
+        return out
+
     def __call__(self, x: NHWC, out: NHWC) -> NHWC:
         c_ = self.c_
+        if self.fused2_ok(x, out):
+            return self._fused2(x, out)
         if self.fused_ok(x, out):
             b1, b2, add = self.m[0]
             B, H, W, _ = x.shape
