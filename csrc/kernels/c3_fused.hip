@@ -6,7 +6,7 @@
 //
 // Unfused (models/fast.py _C3Plan) a C3 is 4 + 2n launches; at batch 32 each is a 12-60 us
 // kernel bound by its own latency and by moving the block's intermediates through HBM (an
-// 80 x 80 block moves ~470 MB).  Here a workgroup owns a 16 x TH pixel tile of the block's
+// 80 x 80 block moves ~470 MB).  Here a workgroup owns a 16 x 4 pixel tile of the block's
 // output: it reads x (or, between bottlenecks, a) once, keeps a / u / b in LDS, and writes y.
 //
 // Modes (n bottlenecks, each needing a one-pixel halo):
@@ -14,6 +14,11 @@
 //   FIRST (n > 1)  x -> a, b -> u -> a'  ; writes a' and b to global (the block's a / cat buffers)
 //   MID            a (global, halo) -> u -> a'  ; writes a'
 //   LAST           a (global, halo), b (global) -> u -> a' -> y = cv3([a'|b])
+//
+// Every phase is a small GEMM blocked per wave as FM pixel tiles x FN 16-channel groups, so a
+// weight fragment (streamed from L2 in MFMA fragment order, prefetched one K step ahead) feeds
+// FM tiles and an activation fragment FN groups; the K loops are compile-time (cin = 2 c_ or
+// 4 c_, cout = 2 c_: every C3 of the model), fully unrolled where short.
 //
 // LDS images are chunk-major: [C / 4][HPP][4] fp32 for a, [C / 8][HPP][8] bf16 (hi and lo
 // planes) for u and b, HPP = the halo pixel count padded to 16.  An MFMA A fragment is 16
@@ -39,13 +44,13 @@ struct C3fArgs {
   const float* x;     // [B, H, W, ldx], channels [x_off, x_off + cin)          (FULL / FIRST)
   const float* a_in;  // [B, H, W, lda], channels [a_off, a_off + C)            (MID / LAST)
   const float* b_in;  // [B, H, W, ldb], channels [b_off, b_off + C)            (LAST)
-  float* y;           // [B, H, W, ldy], channels [y_off, y_off + cout)         (FULL / LAST)
+  float* y;           // [B, H, W, ldy], channels [y_off, y_off + 2C)           (FULL / LAST)
   float* a_out;       // [B, H, W, ldao], channels [ao_off, ao_off + C)         (FIRST / MID)
   float* b_out;       // [B, H, W, ldbo], channels [bo_off, bo_off + C)         (FIRST)
   const __bf16 *w12, *wm1, *wm2, *w3;  // fragment-order split weights (ops/conv.py frag_weights)
   const float *b12, *bm1, *bm2, *b3;
   int act12, actm1, actm2, act3, add;
-  int B, H, W, cin, cout;
+  int B, H, W;
   int ldx, x_off, lda, a_off, ldb, b_off, ldy, y_off, ldao, ao_off, ldbo, bo_off;
 };
 
@@ -74,18 +79,72 @@ __device__ __forceinline__ void split8(const float4& u, const float4& v, bf16x8&
   }
 }
 
-// fragment-order weight image [K / 32][N / 16][hi | lo][64 lanes][8]: fragment (ks, g) of this lane
-__device__ __forceinline__ void wfrag(const __bf16* w, int ng, int ks, int g, int lane, bf16x8& h, bf16x8& l) {
-  const __bf16* p = w + ((long)(ks * ng + g) * 2) * 512 + lane * 8;
-  h = *reinterpret_cast<const bf16x8*>(p);
-  l = *reinterpret_cast<const bf16x8*>(p + 512);
+__device__ __forceinline__ void split4(const float* v, uint2& h2, uint2& l2) {
+  __bf16 h[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    h[r] = (__bf16)v[r];
+    l[r] = (__bf16)(v[r] - (float)h[r]);
+  }
+  h2 = *reinterpret_cast<const uint2*>(h);
+  l2 = *reinterpret_cast<const uint2*>(l);
 }
 
-template <int C, int MODE, int TH>
+// Weight fragments (ks, g0 .. g0 + FN - 1) of this lane from a fragment-order image
+// [K / 32][NG][hi | lo][64 lanes][8] (one contiguous 1 KiB per fragment and half).
+template <int FN>
+__device__ __forceinline__ void wload(const __bf16* w, int ng, int ks, int g0, int lane, bf16x8 (&h)[FN],
+                                      bf16x8 (&l)[FN]) {
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const __bf16* p = w + ((long)(ks * ng + g0 + j) * 2) * 512 + lane * 8;
+    h[j] = *reinterpret_cast<const bf16x8*>(p);
+    l[j] = *reinterpret_cast<const bf16x8*>(p + 512);
+  }
+}
+
+// acc[i][j] += A(ks, i) . W(ks, g0 + j) over the K steps, the weights prefetched one step ahead
+// (two register sets, unrolled by two: no dynamically indexed register arrays).  MV: valid tiles.
+template <int FM, int FN, int KS, class AF>
+__device__ __forceinline__ void gemm(f32x4 (&acc)[FM][FN], const __bf16* w, int ng, int g0, int lane, int mv,
+                                     AF&& afrag) {
+  bf16x8 h0[FN], l0[FN], h1[FN], l1[FN];
+  auto step = [&](int ks, const bf16x8 (&wh)[FN], const bf16x8 (&wl)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (i >= mv) break;
+      bf16x8 xh, xl;
+      afrag(ks, i, xh, xl);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wh[j], wl[j], xh, xl);
+    }
+  };
+  wload<FN>(w, ng, 0, g0, lane, h0, l0);
+  constexpr int UN = KS <= 8 ? 4 : 1;
+#pragma unroll UN
+  for (int ks = 0; ks < KS; ks += 2) {
+    wload<FN>(w, ng, ks + 1 < KS ? ks + 1 : KS - 1, g0, lane, h1, l1);
+    step(ks, h0, l0);
+    if (ks + 1 < KS) {
+      wload<FN>(w, ng, ks + 2 < KS ? ks + 2 : KS - 1, g0, lane, h0, l0);
+      step(ks + 1, h1, l1);
+    }
+  }
+}
+
+template <int FM, int FN>
+__device__ __forceinline__ void zero(f32x4 (&acc)[FM][FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int C, int CINM, int MODE>
 __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs a) {
-  constexpr int TW = 16, HW_ = TW + 2, HP = (TH + 2) * HW_, HPP = (HP + 15) / 16 * 16;
-  constexpr int MTH = HPP / 16, MTI = TH;  // halo M tiles; interior M tiles (one tile row each)
-  constexpr int NW = 4;
+  constexpr int TH = 4, TW = 16, HW_ = TW + 2, HP = (TH + 2) * HW_, HPP = (HP + 15) / 16 * 16;
+  constexpr int MTH = HPP / 16, MTI = TH;  // halo M tiles (7); tile M tiles (4: one tile row each)
+  constexpr int CIN = CINM * C, COUT = 2 * C, NG = C / 16;
   constexpr bool HAS_B = MODE == kFull;
   constexpr int A_BYTES = C * HPP * 4, U_BYTES = C * HPP * 2, B_BYTES = HAS_B ? C * TH * TW * 2 : 0;
   __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + 2 * U_BYTES + 2 * B_BYTES];
@@ -102,13 +161,19 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
   const int b = bid / (nty * ntx), rem = bid - b * (nty * ntx);
   const int y0 = (rem / ntx) * TH, x0 = (rem - (rem / ntx) * ntx) * TW;
 
-  auto halo_in = [&](int p, int& iy, int& ix) {  // halo pixel p -> image pixel, inside?
+  auto halo_in = [&](int p, long& pix) {  // halo pixel p inside the image? (and its pixel index)
     const int hy = p / HW_, hx = p - (p / HW_) * HW_;
-    iy = y0 - 1 + hy;
-    ix = x0 - 1 + hx;
-    return p < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const bool in = p < HP && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    pix = in ? ((long)b * a.H + iy) * a.W + ix : 0;
+    return in;
   };
-  auto gpix = [&](int iy, int ix) { return ((long)b * a.H + iy) * a.W + ix; };
+  auto tile_in = [&](int mt, long& pix) {  // this lane's pixel of tile row mt
+    const int iy = y0 + mt, ix = x0 + fr;
+    const bool in = iy < a.H && ix < a.W;
+    pix = in ? ((long)b * a.H + iy) * a.W + ix : 0;
+    return in;
+  };
   // A fragment from an fp32 NHWC global tensor (zero when the pixel is outside)
   auto gfrag = [&](const float* base, int ld, int off, bool in, long pix, int k0, bf16x8& h, bf16x8& l) {
     float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
@@ -126,78 +191,71 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
     split8(u, v, h, l);
   };
 
-  // ---- P1: a = act(cv1 x) on the halo; b = act(cv2 x) on the tile (FULL, FIRST)
+  // ---- P1: a = act(cv1 x) on the halo (waves 0, 1), b = act(cv2 x) on the tile (waves 2, 3);
   //      or a loaded from a_in on the halo (MID, LAST)
   if constexpr (MODE == kFull || MODE == kFirst) {
-    const int ks_n = a.cin / 32, ng12 = 2 * C / 16;
-    constexpr int FN = C / 16 >= 4 ? 4 : C / 16;  // 16-channel fragments per work item
-    constexpr int NGB = C / 16 / FN;
-    // a on the halo tiles, then b on the interior tiles
-    for (int item = wid; item < (MTH + MTI) * NGB; item += NW) {
-      const bool is_a = item < MTH * NGB;
-      const int it = is_a ? item : item - MTH * NGB;
-      const int mt = it / NGB, g0 = (it - (it / NGB) * NGB) * FN + (is_a ? 0 : C / 16);
-      int p, iy, ix;
-      bool in;
-      if (is_a) {
-        p = mt * 16 + fr;
-        in = halo_in(p, iy, ix);
-      } else {
-        p = (mt + 1) * HW_ + fr + 1;
-        iy = y0 + mt;
-        ix = x0 + fr;
-        in = iy < a.H && ix < a.W;
-      }
-      const long pix = in ? gpix(iy, ix) : 0;
-      f32x4 acc[FN];
+    constexpr int FN = NG / 2;  // each wave: half of the C channels of its half of cv1 | cv2
+    constexpr int KS = CIN / 32;
+    const int g0 = (wid & 1) * FN;
+    if (wid < 2) {
+      long pix[MTH];
+      bool in[MTH];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int ks = 0; ks < ks_n; ++ks) {
-        bf16x8 xh, xl;
-        gfrag(a.x, a.ldx, a.x_off, in, pix, ks * 32 + fq * 8, xh, xl);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          bf16x8 wh, wl;
-          wfrag(a.w12, ng12, ks, g0 + j, lane, wh, wl);
-          mfma3(acc[j], wh, wl, xh, xl);
-        }
-      }
+      for (int i = 0; i < MTH; ++i) in[i] = halo_in(i * 16 + fr, pix[i]);
+      f32x4 acc[MTH][FN];
+      zero(acc);
+      gemm<MTH, FN, KS>(acc, a.w12, 2 * NG, g0, lane, MTH, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+        gfrag(a.x, a.ldx, a.x_off, in[i], pix[i], ks * 32 + fq * 8, h, l);
+      });
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = (g0 + j) * 16 + fq * 4;  // merged cv1 | cv2 channel
-        float v[4];
+        const int n = (g0 + j) * 16 + fq * 4;
+        const float4 bv = a.b12 ? *reinterpret_cast<const float4*>(a.b12 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = actf(acc[j][r] + (a.b12 ? a.b12[n + r] : 0.f), a.act12);
-        if (is_a) {
-          if (p < HPP)
-            *reinterpret_cast<float4*>(af + ((n >> 2) * HPP + p) * 4) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          const int c = n - C;  // b channel
+        for (int i = 0; i < MTH; ++i) {
+          const int p = i * 16 + fr;
+          *reinterpret_cast<float4*>(af + ((n >> 2) * HPP + p) * 4) =
+              make_float4(actf(acc[i][j][0] + bv.x, a.act12), actf(acc[i][j][1] + bv.y, a.act12),
+                          actf(acc[i][j][2] + bv.z, a.act12), actf(acc[i][j][3] + bv.w, a.act12));
+        }
+      }
+    } else {
+      long pix[MTI];
+      bool in[MTI];
+#pragma unroll
+      for (int i = 0; i < MTI; ++i) in[i] = tile_in(i, pix[i]);
+      f32x4 acc[MTI][FN];
+      zero(acc);
+      gemm<MTI, FN, KS>(acc, a.w12, 2 * NG, NG + g0, lane, MTI, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+        gfrag(a.x, a.ldx, a.x_off, in[i], pix[i], ks * 32 + fq * 8, h, l);
+      });
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = (g0 + j) * 16 + fq * 4;  // b channel
+        const float4 bv = a.b12 ? *reinterpret_cast<const float4*>(a.b12 + C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < MTI; ++i) {
+          float v[4] = {actf(acc[i][j][0] + bv.x, a.act12), actf(acc[i][j][1] + bv.y, a.act12),
+                        actf(acc[i][j][2] + bv.z, a.act12), actf(acc[i][j][3] + bv.w, a.act12)};
           if constexpr (MODE == kFull) {
-            const int q = mt * TW + fr;
-            __bf16 h[4], l[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              h[r] = (__bf16)v[r];
-              l[r] = (__bf16)(v[r] - (float)h[r]);
-            }
-            const int o = ((c >> 3) * (TH * TW) + q) * 8 + (c & 7);
-            *reinterpret_cast<uint2*>(bh + o) = *reinterpret_cast<const uint2*>(h);
-            *reinterpret_cast<uint2*>(bl + o) = *reinterpret_cast<const uint2*>(l);
-          } else if (in) {
-            *reinterpret_cast<float4*>(a.b_out + pix * a.ldbo + a.bo_off + c) = make_float4(v[0], v[1], v[2], v[3]);
+            uint2 h2, l2;
+            split4(v, h2, l2);
+            const int o = ((c >> 3) * (TH * TW) + i * TW + fr) * 8 + (c & 7);
+            *reinterpret_cast<uint2*>(bh + o) = h2;
+            *reinterpret_cast<uint2*>(bl + o) = l2;
+          } else if (in[i]) {
+            *reinterpret_cast<float4*>(a.b_out + pix[i] * a.ldbo + a.bo_off + c) = make_float4(v[0], v[1], v[2], v[3]);
           }
         }
       }
     }
   } else {
     // a from a_in on the halo (zeros outside the image: they only reach masked u)
-    for (int g = tid; g < HPP * (C / 4); g += NW * 64) {
+    for (int g = tid; g < HPP * (C / 4); g += 256) {
       const int p = g % HPP, c4 = g / HPP;
-      int iy, ix;
+      long pix;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (halo_in(p, iy, ix)) v = *reinterpret_cast<const float4*>(a.a_in + gpix(iy, ix) * a.lda + a.a_off + c4 * 4);
+      if (halo_in(p, pix)) v = *reinterpret_cast<const float4*>(a.a_in + pix * a.lda + a.a_off + c4 * 4);
       *reinterpret_cast<float4*>(af + (c4 * HPP + p) * 4) = v;
     }
   }
@@ -205,40 +263,33 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
 
   // ---- P2: u = act(m.cv1 a) on the halo, zero outside the image (the 3x3's padding)
   {
-    constexpr int FN = C / 16 >= 4 ? 4 : C / 16;
-    constexpr int NGB = C / 16 / FN, KS = C / 32, NG = C / 16;
-    for (int item = wid; item < MTH * NGB; item += NW) {
-      const int mt = item / NGB, g0 = (item - (item / NGB) * NGB) * FN;
-      const int p = mt * 16 + fr;
-      int iy, ix;
-      const bool in = halo_in(p, iy, ix);
-      f32x4 acc[FN];
+    // C 32: 2 tile blocks (4 + 3) x 2 groups; 64: 7 tiles x 1 group per wave; 128: 7 x 2
+    constexpr int MB = NG >= 4 ? 1 : 2, FM = MB == 1 ? MTH : 4, FN = NG >= 4 ? NG / 4 : 1;
+    const int mb = MB == 1 ? 0 : wid >> 1, g0 = (MB == 1 ? wid : (wid & 1)) * FN;
+    const int m0 = mb * FM, mv = MTH - m0 < FM ? MTH - m0 : FM;
+    f32x4 acc[FM][FN];
+    zero(acc);
+    gemm<FM, FN, C / 32>(acc, a.wm1, NG, g0, lane, mv, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      afrag((m0 + i) * 16 + fr, ks * 32 + fq * 8, h, l);
+    });
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) {
+      const int n = (g0 + j) * 16 + fq * 4;
+      const float4 bv = a.bm1 ? *reinterpret_cast<const float4*>(a.bm1 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 xh, xl;
-        afrag(p, ks * 32 + fq * 8, xh, xl);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          bf16x8 wh, wl;
-          wfrag(a.wm1, NG, ks, g0 + j, lane, wh, wl);
-          mfma3(acc[j], wh, wl, xh, xl);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = (g0 + j) * 16 + fq * 4;
-        __bf16 h[4], l[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = in ? actf(acc[j][r] + (a.bm1 ? a.bm1[n + r] : 0.f), a.actm1) : 0.f;
-          h[r] = (__bf16)v;
-          l[r] = (__bf16)(v - (float)h[r]);
-        }
+      for (int i = 0; i < FM; ++i) {
+        if (i >= mv) break;
+        const int p = (m0 + i) * 16 + fr;
+        long pix;
+        const bool in = halo_in(p, pix);
+        float v[4] = {actf(acc[i][j][0] + bv.x, a.actm1), actf(acc[i][j][1] + bv.y, a.actm1),
+                      actf(acc[i][j][2] + bv.z, a.actm1), actf(acc[i][j][3] + bv.w, a.actm1)};
+        if (!in) v[0] = v[1] = v[2] = v[3] = 0.f;
+        uint2 h2, l2;
+        split4(v, h2, l2);
         const int o = ((n >> 3) * HPP + p) * 8 + (n & 7);
-        *reinterpret_cast<uint2*>(uh + o) = *reinterpret_cast<const uint2*>(h);
-        *reinterpret_cast<uint2*>(ul + o) = *reinterpret_cast<const uint2*>(l);
+        *reinterpret_cast<uint2*>(uh + o) = h2;
+        *reinterpret_cast<uint2*>(ul + o) = l2;
       }
     }
   }
@@ -246,118 +297,97 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
 
   // ---- P3: a' = act(m.cv2 u) (+ a) on the tile: 3x3 over the u halo, K = 9 C in tap-major order
   {
-    constexpr int FN = C / 16 >= 2 ? 2 : 1;
-    constexpr int NGB = C / 16 / FN, KS = 9 * C / 32, NG = C / 16;
-    for (int item = wid; item < MTI * NGB; item += NW) {
-      const int mt = item / NGB, g0 = (item - (item / NGB) * NGB) * FN;
-      f32x4 acc[FN];
+    // C 32: 2 tile blocks (2 rows) x 2 groups; 64: 4 rows x 1 group per wave; 128: 4 x 2
+    constexpr int MB = NG >= 4 ? 1 : 2, FM = MB == 1 ? MTI : 2, FN = NG >= 4 ? NG / 4 : 1;
+    const int mb = MB == 1 ? 0 : wid >> 1, g0 = (MB == 1 ? wid : (wid & 1)) * FN;
+    const int m0 = mb * FM;
+    f32x4 acc[FM][FN];
+    zero(acc);
+    gemm<FM, FN, 9 * C / 32>(acc, a.wm2, NG, g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      const int k0 = ks * 32, tap = k0 / C, ci = k0 - tap * C + fq * 8;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+      const int o = ((ci >> 3) * HPP + (m0 + i + ky) * HW_ + fr + kx) * 8;
+      h = *reinterpret_cast<const bf16x8*>(uh + o);
+      l = *reinterpret_cast<const bf16x8*>(ul + o);
+    });
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 3
-      for (int ks = 0; ks < KS; ++ks) {
-        const int k0 = ks * 32, tap = k0 / C, ci = k0 - tap * C + fq * 8;
-        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-        const int p = (mt + ky) * HW_ + fr + kx;
-        const int o = ((ci >> 3) * HPP + p) * 8;
-        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(uh + o);
-        const bf16x8 xl = *reinterpret_cast<const bf16x8*>(ul + o);
+    for (int j = 0; j < FN; ++j) {
+      const int n = (g0 + j) * 16 + fq * 4;
+      const float4 bv = a.bm2 ? *reinterpret_cast<const float4*>(a.bm2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          bf16x8 wh, wl;
-          wfrag(a.wm2, NG, ks, g0 + j, lane, wh, wl);
-          mfma3(acc[j], wh, wl, xh, xl);
-        }
-      }
-      const int p = (mt + 1) * HW_ + fr + 1;  // halo index of this lane's tile pixel
-      const int iy = y0 + mt, ix = x0 + fr;
-      const bool in = iy < a.H && ix < a.W;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = (g0 + j) * 16 + fq * 4;
+      for (int i = 0; i < FM; ++i) {
+        const int mt = m0 + i, p = (mt + 1) * HW_ + fr + 1;  // halo index of this lane's tile pixel
         float* ap = af + ((n >> 2) * HPP + p) * 4;
         const float4 r0 = *reinterpret_cast<const float4*>(ap);
-        const float rv[4] = {r0.x, r0.y, r0.z, r0.w};
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = actf(acc[j][r] + (a.bm2 ? a.bm2[n + r] : 0.f), a.actm2);
-          if (a.add) v[r] += rv[r];
+        float v[4] = {actf(acc[i][j][0] + bv.x, a.actm2), actf(acc[i][j][1] + bv.y, a.actm2),
+                      actf(acc[i][j][2] + bv.z, a.actm2), actf(acc[i][j][3] + bv.w, a.actm2)};
+        if (a.add) {
+          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         }
         if constexpr (MODE == kFull || MODE == kLast) {
           *reinterpret_cast<float4*>(ap) = make_float4(v[0], v[1], v[2], v[3]);  // a' over a (same lane)
-        } else if (in) {
-          *reinterpret_cast<float4*>(a.a_out + gpix(iy, ix) * a.ldao + a.ao_off + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          long pix;
+          if (tile_in(mt, pix))
+            *reinterpret_cast<float4*>(a.a_out + pix * a.ldao + a.ao_off + n) = make_float4(v[0], v[1], v[2], v[3]);
         }
       }
     }
   }
 
-  // ---- P4: y = act(cv3 [a' | b]) on the tile
+  // ---- P4: y = act(cv3 [a' | b]) on the tile: 4 rows x cout / 4 channels per wave
   if constexpr (MODE == kFull || MODE == kLast) {
     __syncthreads();
-    const int ng3 = a.cout / 16;
-    constexpr int FN = 4;
-    const int ngb = ng3 / FN;  // cout % 64 == 0
-    constexpr int KA = C / 32, KS = 2 * C / 32;
-    for (int item = wid; item < MTI * ngb; item += NW) {
-      const int mt = item / ngb, g0 = (item - (item / ngb) * ngb) * FN;
-      const int p = (mt + 1) * HW_ + fr + 1;
-      const int iy = y0 + mt, ix = x0 + fr;
-      const bool in = iy < a.H && ix < a.W;
-      const long pix = in ? gpix(iy, ix) : 0;
-      f32x4 acc[FN];
+    constexpr int FN = COUT / 16 / 4, KA = C / 32;
+    const int g0 = wid * FN;
+    long pix[MTI];
+    bool in[MTI];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-      for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 xh, xl;
-        if (ks < KA) {
-          afrag(p, ks * 32 + fq * 8, xh, xl);
-        } else if constexpr (MODE == kFull) {
-          const int c = (ks - KA) * 32 + fq * 8, q = mt * TW + fr;
-          const int o = ((c >> 3) * (TH * TW) + q) * 8;
-          xh = *reinterpret_cast<const bf16x8*>(bh + o);
-          xl = *reinterpret_cast<const bf16x8*>(bl + o);
-        } else {
-          gfrag(a.b_in, a.ldb, a.b_off, in, pix, (ks - KA) * 32 + fq * 8, xh, xl);
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          bf16x8 wh, wl;
-          wfrag(a.w3, ng3, ks, g0 + j, lane, wh, wl);
-          mfma3(acc[j], wh, wl, xh, xl);
-        }
+    for (int i = 0; i < MTI; ++i) in[i] = tile_in(i, pix[i]);
+    f32x4 acc[MTI][FN];
+    zero(acc);
+    gemm<MTI, FN, 2 * C / 32>(acc, a.w3, COUT / 16, g0, lane, MTI, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      if (ks < KA) {
+        afrag((i + 1) * HW_ + fr + 1, ks * 32 + fq * 8, h, l);
+      } else if constexpr (MODE == kFull) {
+        const int c = (ks - KA) * 32 + fq * 8;
+        const int o = ((c >> 3) * (TH * TW) + i * TW + fr) * 8;
+        h = *reinterpret_cast<const bf16x8*>(bh + o);
+        l = *reinterpret_cast<const bf16x8*>(bl + o);
+      } else {
+        gfrag(a.b_in, a.ldb, a.b_off, in[i], pix[i], (ks - KA) * 32 + fq * 8, h, l);
       }
-      if (!in) continue;
-      float* o = a.y + pix * a.ldy + a.y_off;
+    });
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = (g0 + j) * 16 + fq * 4;
-        float v[4];
+    for (int j = 0; j < FN; ++j) {
+      const int n = (g0 + j) * 16 + fq * 4;
+      const float4 bv = a.b3 ? *reinterpret_cast<const float4*>(a.b3 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = actf(acc[j][r] + (a.b3 ? a.b3[n + r] : 0.f), a.act3);
-        *reinterpret_cast<float4*>(o + n) = make_float4(v[0], v[1], v[2], v[3]);
+      for (int i = 0; i < MTI; ++i) {
+        if (!in[i]) continue;
+        *reinterpret_cast<float4*>(a.y + pix[i] * a.ldy + a.y_off + n) =
+            make_float4(actf(acc[i][j][0] + bv.x, a.act3), actf(acc[i][j][1] + bv.y, a.act3),
+                        actf(acc[i][j][2] + bv.z, a.act3), actf(acc[i][j][3] + bv.w, a.act3));
       }
     }
   }
 }
 
-template <int C, int MODE>
+template <int C, int CINM, int MODE>
 int launch_c3f(const C3fArgs& a, hipStream_t stream) {
-  constexpr int TH = 4;
-  const long tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + 15) / 16);
+  const long tiles = (long)a.B * ((a.H + 3) / 4) * ((a.W + 15) / 16);
   if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
-  c3_fused_kernel<C, MODE, TH><<<(unsigned)tiles, 256, 0, stream>>>(a);
+  c3_fused_kernel<C, CINM, MODE><<<(unsigned)tiles, 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
-template <int C>
+template <int C, int CINM>
 int dispatch_mode(int mode, const C3fArgs& a, hipStream_t stream) {
   switch (mode) {
-    case kFull: return launch_c3f<C, kFull>(a, stream);
-    case kFirst: return launch_c3f<C, kFirst>(a, stream);
-    case kMid: return launch_c3f<C, kMid>(a, stream);
-    case kLast: return launch_c3f<C, kLast>(a, stream);
+    case kFull: return launch_c3f<C, CINM, kFull>(a, stream);
+    case kFirst: return launch_c3f<C, CINM, kFirst>(a, stream);
+    case kMid: return launch_c3f<C, 2, kMid>(a, stream);  // (no x: cin unused)
+    case kLast: return launch_c3f<C, 2, kLast>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -367,8 +397,9 @@ int dispatch_mode(int mode, const C3fArgs& a, hipStream_t stream) {
 // One fused C3 pass (c3_fused_kernel).  ptrs: x, a_in, b_in, y, a_out, b_out, w12, b12, wm1, bm1,
 // wm2, bm2, w3, b3 (unused ones null).  ints: mode, C, cin, cout, add, B, H, W, ldx, x_off, lda,
 // a_off, ldb, b_off, ldy, y_off, ldao, ao_off, ldbo, bo_off, act12, actm1, actm2, act3.
-// Weights: fragment-order split images of the FusedConvs' fp32 GEMM weights: cv1|cv2 merged
-// [2C, cin], m.cv1 [C, C], m.cv2 [C, 9C] (tap-major K), cv3 [cout, 2C].
+// C in {32, 64, 128}, cin in {2C, 4C}, cout = 2C.  Weights: fragment-order split images of the
+// FusedConvs' fp32 GEMM weights: cv1|cv2 merged [2C, cin], m.cv1 [C, C], m.cv2 [C, 9C] (tap-major
+// K), cv3 [2C, 2C].  Biases fp32 (16-B aligned).
 TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stream) {
   C3fArgs a;
   a.x = (const float*)ptrs[0]; a.a_in = (const float*)ptrs[1]; a.b_in = (const float*)ptrs[2];
@@ -377,26 +408,29 @@ TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stre
   a.wm1 = (const __bf16*)ptrs[8]; a.bm1 = (const float*)ptrs[9];
   a.wm2 = (const __bf16*)ptrs[10]; a.bm2 = (const float*)ptrs[11];
   a.w3 = (const __bf16*)ptrs[12]; a.b3 = (const float*)ptrs[13];
-  const int mode = v[0], C = v[1];
-  a.cin = v[2]; a.cout = v[3]; a.add = v[4]; a.B = v[5]; a.H = v[6]; a.W = v[7];
+  const int mode = v[0], C = v[1], cin = v[2], cout = v[3];
+  a.add = v[4]; a.B = v[5]; a.H = v[6]; a.W = v[7];
   a.ldx = v[8]; a.x_off = v[9]; a.lda = v[10]; a.a_off = v[11]; a.ldb = v[12]; a.b_off = v[13];
   a.ldy = v[14]; a.y_off = v[15]; a.ldao = v[16]; a.ao_off = v[17]; a.ldbo = v[18]; a.bo_off = v[19];
   a.act12 = v[20]; a.actm1 = v[21]; a.actm2 = v[22]; a.act3 = v[23];
   if (a.B <= 0) return 0;
-  // the contract every mode relies on: 16-B aligned channel slices, K multiples of 32, cout of 64
+  // the contract every mode relies on: 16-B aligned channel slices and biases
   const bool full_or_first = mode == kFull || mode == kFirst, uses_y = mode == kFull || mode == kLast;
-  if ((full_or_first && (!a.x || (a.cin & 31) || (a.ldx & 3) || (a.x_off & 3) || a.ldx < a.x_off + a.cin)) ||
+  auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; };
+  if ((full_or_first && (!a.x || (a.ldx & 3) || (a.x_off & 3) || a.ldx < a.x_off + cin)) ||
       (!full_or_first && (!a.a_in || (a.lda & 3) || (a.a_off & 3) || a.lda < a.a_off + C)) ||
       (mode == kLast && (!a.b_in || (a.ldb & 3) || (a.b_off & 3) || a.ldb < a.b_off + C)) ||
-      (uses_y && (!a.y || !a.w3 || (a.cout & 63) || (a.ldy & 3) || (a.y_off & 3) || a.ldy < a.y_off + a.cout)) ||
+      (uses_y && (!a.y || !a.w3 || cout != 2 * C || (a.ldy & 3) || (a.y_off & 3) || a.ldy < a.y_off + cout)) ||
       (!uses_y && (!a.a_out || (a.ldao & 3) || (a.ao_off & 3) || a.ldao < a.ao_off + C)) ||
       (mode == kFirst && (!a.b_out || (a.ldbo & 3) || (a.bo_off & 3) || a.ldbo < a.bo_off + C)) ||
-      (full_or_first && !a.w12) || !a.wm1 || !a.wm2)
+      (full_or_first && (!a.w12 || (cin != 2 * C && cin != 4 * C))) || !a.wm1 || !a.wm2 ||
+      !al(a.b12) || !al(a.bm1) || !al(a.bm2) || !al(a.b3) || mode < 0 || mode > 3)
     return (int)hipErrorInvalidValue;
+  const bool c4 = cin == 4 * C;
   switch (C) {
-    case 32: return dispatch_mode<32>(mode, a, stream);
-    case 64: return dispatch_mode<64>(mode, a, stream);
-    case 128: return dispatch_mode<128>(mode, a, stream);
+    case 32: return c4 ? dispatch_mode<32, 4>(mode, a, stream) : dispatch_mode<32, 2>(mode, a, stream);
+    case 64: return c4 ? dispatch_mode<64, 4>(mode, a, stream) : dispatch_mode<64, 2>(mode, a, stream);
+    case 128: return c4 ? dispatch_mode<128, 4>(mode, a, stream) : dispatch_mode<128, 2>(mode, a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -35,12 +35,12 @@ def test_c3_fused_matches_chain(cuda, cam, monkeypatch, name, hw):
     outs = []
     for fused in (True, False):
         monkeypatch.setattr(fast, "C3_FUSED", fused)
-        out = NHWC(torch.full((B, H, W, cout + 12), 7.0, device=cuda), 4, cout)
+        out = NHWC(torch.full((B, H, W, cout + 16), 7.0, device=cuda), 8, cout)
         assert plan.fused2_ok(x, out) == fused
         plan(x, out)
         torch.cuda.synchronize()
-        assert (out.t[..., :4] == 7.0).all() and (out.t[..., 4 + cout:] == 7.0).all()
-        outs.append(out.t[..., 4:4 + cout].double())
+        assert (out.t[..., :8] == 7.0).all() and (out.t[..., 8 + cout:] == 7.0).all()
+        outs.append(out.t[..., 8:8 + cout].double())
     got, want = outs
     assert torch.isfinite(got).all()
     rel = ((got - want).norm() / want.norm()).item()
