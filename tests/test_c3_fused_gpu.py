@@ -29,6 +29,7 @@ def test_c3_fused_matches_chain(cuda, cam, monkeypatch, name, hw):
     torch.manual_seed(hw[0] * 7 + len(name))
     B, (H, W) = 2, hw
     blk = getattr(cam.model, name)
+    monkeypatch.setattr(fast, "FUSED_C3_WIDTHS", (32, 64, 128))  # every width the kernel takes
     plan = fast._C3Plan(blk, B, H, W, fast._Buffers(cuda, "fp32"), cuda)
     cin, cout = plan.cv12.cin_p, plan.cv3.N
     x = NHWC(torch.randn(B, H, W, cin + 8, device=cuda) * 2, 8, cin)  # channel-offset input slice
@@ -57,7 +58,7 @@ def test_camera_step_fused_c3_same_detections(cuda, monkeypatch):
         c.frames[b].copy_(torch.from_numpy(camera_frame(720, 1280, b)))
     c.calibrate_detection_density(50.0)
     f = c.build_fast()
-    assert all(p._fw is not None for p in (f.c3_4, f.c3_6, f.c3_8, f.c3_13, f.c3_17, f.c3_20, f.c3_23))
+    assert all(p._fw is not None for p in (f.c3_4, f.c3_6, f.c3_13, f.c3_17, f.c3_20))
     r1 = c.step()
     torch.cuda.synchronize()
     n1, b1 = r1.count.clone(), r1.box.clone()
