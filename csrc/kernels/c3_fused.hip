@@ -1,6 +1,7 @@
 // YOLOv5 C3 blocks fused into LDS-resident kernels, fp32 mode (split-product MFMA), for the
-// blocks with c_ = 32 / 64 / 128 hidden channels (YOLOv5n: b4, b6, b8 and the four head C3s;
-// the c_ = 16 block b2 is image.hip yolo_c3s_fused).  Reference block: C3 = cv3(cat(m(cv1(x)),
+// blocks with c_ = 32 / 64 hidden channels (YOLOv5n: b4, b6, h13, h17, h20; the c_ = 16 block b2
+// is image.hip yolo_c3s_fused; the 20 x 20 c_ = 128 blocks measured faster unfused: one
+// workgroup of ~150 KiB LDS per CU over 320 tiles).  Reference block: C3 = cv3(cat(m(cv1(x)),
 // cv2(x))) with m = n x Bottleneck(1x1, 3x3, + shortcut) (the YOLOv5 model the reference serves,
 // examples/YOLOv5/config.pbtxt).
 //
@@ -20,10 +21,11 @@
 // FM tiles and an activation fragment FN groups; the K loops are compile-time (cin = 2 c_ or
 // 4 c_, cout = 2 c_: every C3 of the model), fully unrolled where short.
 //
-// LDS images are chunk-major: [C / 4][HPP][4] fp32 for a, [C / 8][HPP][8] bf16 (hi and lo
-// planes) for u and b, HPP = the halo pixel count padded to 16.  An MFMA A fragment is 16
-// consecutive pixels (one output row of the tile, or 16 consecutive halo pixels) x 8
-// channels; the lane quads fq = 0..3 read channel chunks 2 fq, 2 fq + 1 (fp32) or fq (bf16),
+// LDS images are chunk-major pair planes, [C / 8][HPP][8] bf16 hi and lo, for a and u on the
+// halo and b on the tile (HPP = the halo pixel count padded to 16), so every MFMA operand is
+// read as stored (no split on the read path); the residual a of the tile pixels also stays in
+// fp32.  An A fragment is 16 consecutive pixels (one output row of the tile, or 16
+// consecutive halo pixels) x 8 channels; the lane quads fq = 0..3 read channel chunk fq,
 // whose planes lie HPP * 16 B = 0 mod 256 B apart, so every 16-lane ds_read_b128 group covers
 // the 64 banks once (conflict-free for the halo rows and for every 3x3 tap shift).
 //
@@ -132,6 +134,8 @@ __device__ __forceinline__ void gemm(f32x4 (&acc)[FM][FN], const __bf16* w, int 
   }
 }
 
+template <int V> struct IC { static constexpr int value = V; };
+
 template <int FM, int FN>
 __device__ __forceinline__ void zero(f32x4 (&acc)[FM][FN]) {
 #pragma unroll
@@ -140,19 +144,24 @@ __device__ __forceinline__ void zero(f32x4 (&acc)[FM][FN]) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-template <int C, int CINM, int MODE>
-__global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs a) {
+template <int C, int CINM, int MODE, bool RES>
+__global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
   constexpr int TH = 4, TW = 16, HW_ = TW + 2, HP = (TH + 2) * HW_, HPP = (HP + 15) / 16 * 16;
   constexpr int MTH = HPP / 16, MTI = TH;  // halo M tiles (7); tile M tiles (4: one tile row each)
   constexpr int CIN = CINM * C, COUT = 2 * C, NG = C / 16;
   constexpr bool HAS_B = MODE == kFull;
-  constexpr int A_BYTES = C * HPP * 4, U_BYTES = C * HPP * 2, B_BYTES = HAS_B ? C * TH * TW * 2 : 0;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + 2 * U_BYTES + 2 * B_BYTES];
-  float* const af = reinterpret_cast<float*>(smem);                   // [C/4][HPP][4]
-  __bf16* const uh = reinterpret_cast<__bf16*>(smem + A_BYTES);        // [C/8][HPP][8]
-  __bf16* const ul = reinterpret_cast<__bf16*>(smem + A_BYTES + U_BYTES);
-  __bf16* const bh = reinterpret_cast<__bf16*>(smem + A_BYTES + 2 * U_BYTES);  // [C/8][TH*TW][8]
-  __bf16* const bl = reinterpret_cast<__bf16*>(smem + A_BYTES + 2 * U_BYTES + B_BYTES);
+  constexpr int NI = TH * TW;
+  // a on the halo as hi / lo planes (MFMA operands as stored), its tile pixels also in fp32 (the
+  // residual); u on the halo; b on the tile (FULL).  a' (FULL / LAST) overwrites a's tile pixels.
+  constexpr int P_BYTES = C * HPP * 2, R_BYTES = RES ? C * NI * 4 : 0, B_BYTES = HAS_B ? C * NI * 2 : 0;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * P_BYTES + R_BYTES + 2 * B_BYTES];
+  __bf16* const ah = reinterpret_cast<__bf16*>(smem);                  // [C/8][HPP][8]
+  __bf16* const al = reinterpret_cast<__bf16*>(smem + P_BYTES);
+  __bf16* const uh = reinterpret_cast<__bf16*>(smem + 2 * P_BYTES);    // [C/8][HPP][8]
+  __bf16* const ul = reinterpret_cast<__bf16*>(smem + 3 * P_BYTES);
+  float* const ar = reinterpret_cast<float*>(smem + 4 * P_BYTES);      // [C/4][NI][4]
+  __bf16* const bh = reinterpret_cast<__bf16*>(smem + 4 * P_BYTES + R_BYTES);  // [C/8][NI][8]
+  __bf16* const bl = reinterpret_cast<__bf16*>(smem + 4 * P_BYTES + R_BYTES + B_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -184,63 +193,58 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
     }
     split8(u, v, h, l);
   };
-  // A fragment from the fp32 a image (halo pixel p, channels k0 .. k0 + 7)
-  auto afrag = [&](int p, int k0, bf16x8& h, bf16x8& l) {
-    const float4 u = *reinterpret_cast<const float4*>(af + ((k0 >> 2) * HPP + p) * 4);
-    const float4 v = *reinterpret_cast<const float4*>(af + (((k0 >> 2) + 1) * HPP + p) * 4);
-    split8(u, v, h, l);
+  // A fragment from a pair image [C/8][npix][8] (pixel p, channels k0 .. k0 + 7)
+  auto pfrag = [&](const __bf16* ph, const __bf16* pl, int npix, int p, int k0, bf16x8& h, bf16x8& l) {
+    const int o = ((k0 >> 3) * npix + p) * 8;
+    h = *reinterpret_cast<const bf16x8*>(ph + o);
+    l = *reinterpret_cast<const bf16x8*>(pl + o);
+  };
+  // 4 channels n .. n + 3 of a at halo pixel p: the pair planes, and the fp32 residual on the tile
+  auto put_a = [&](int p, int n, const float* v, bool residual) {
+    uint2 h2, l2;
+    split4(v, h2, l2);
+    const int o = ((n >> 3) * HPP + p) * 8 + (n & 7);
+    *reinterpret_cast<uint2*>(ah + o) = h2;
+    *reinterpret_cast<uint2*>(al + o) = l2;
+    if (RES && residual) {
+      const int hy = p / HW_, hx = p - (p / HW_) * HW_;
+      if (hy >= 1 && hy <= TH && hx >= 1 && hx <= TW)
+        *reinterpret_cast<float4*>(ar + ((n >> 2) * NI + (hy - 1) * TW + hx - 1) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+    }
   };
 
-  // ---- P1: a = act(cv1 x) on the halo (waves 0, 1), b = act(cv2 x) on the tile (waves 2, 3);
+  // ---- P1: a = act(cv1 x) on the halo, b = act(cv2 x) on the tile (FULL, FIRST);
   //      or a loaded from a_in on the halo (MID, LAST)
   if constexpr (MODE == kFull || MODE == kFirst) {
-    constexpr int FN = NG / 2;  // each wave: half of the C channels of its half of cv1 | cv2
     constexpr int KS = CIN / 32;
-    const int g0 = (wid & 1) * FN;
-    if (wid < 2) {
-      long pix[MTH];
-      bool in[MTH];
+    // cv1 on FM halo tiles from m0 for FN groups from g0 (a) or cv2 on the 4 tile rows (b)
+    auto run = [&](auto FMc, auto FNc, bool is_a, int m0, int g0) {
+      constexpr int FM = decltype(FMc)::value, FN = decltype(FNc)::value;
+      long pix[FM];
+      bool in[FM];
 #pragma unroll
-      for (int i = 0; i < MTH; ++i) in[i] = halo_in(i * 16 + fr, pix[i]);
-      f32x4 acc[MTH][FN];
+      for (int i = 0; i < FM; ++i) in[i] = is_a ? halo_in((m0 + i) * 16 + fr, pix[i]) : tile_in(i, pix[i]);
+      f32x4 acc[FM][FN];
       zero(acc);
-      gemm<MTH, FN, KS>(acc, a.w12, 2 * NG, g0, lane, MTH, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      gemm<FM, FN, KS>(acc, a.w12, 2 * NG, (is_a ? 0 : NG) + g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
         gfrag(a.x, a.ldx, a.x_off, in[i], pix[i], ks * 32 + fq * 8, h, l);
       });
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int n = (g0 + j) * 16 + fq * 4;
-        const float4 bv = a.b12 ? *reinterpret_cast<const float4*>(a.b12 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int c = (g0 + j) * 16 + fq * 4;  // a or b channel
+        const float4 bv = a.b12 ? *reinterpret_cast<const float4*>(a.b12 + (is_a ? 0 : C) + c)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int i = 0; i < MTH; ++i) {
-          const int p = i * 16 + fr;
-          *reinterpret_cast<float4*>(af + ((n >> 2) * HPP + p) * 4) =
-              make_float4(actf(acc[i][j][0] + bv.x, a.act12), actf(acc[i][j][1] + bv.y, a.act12),
-                          actf(acc[i][j][2] + bv.z, a.act12), actf(acc[i][j][3] + bv.w, a.act12));
-        }
-      }
-    } else {
-      long pix[MTI];
-      bool in[MTI];
-#pragma unroll
-      for (int i = 0; i < MTI; ++i) in[i] = tile_in(i, pix[i]);
-      f32x4 acc[MTI][FN];
-      zero(acc);
-      gemm<MTI, FN, KS>(acc, a.w12, 2 * NG, NG + g0, lane, MTI, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-        gfrag(a.x, a.ldx, a.x_off, in[i], pix[i], ks * 32 + fq * 8, h, l);
-      });
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = (g0 + j) * 16 + fq * 4;  // b channel
-        const float4 bv = a.b12 ? *reinterpret_cast<const float4*>(a.b12 + C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < MTI; ++i) {
-          float v[4] = {actf(acc[i][j][0] + bv.x, a.act12), actf(acc[i][j][1] + bv.y, a.act12),
-                        actf(acc[i][j][2] + bv.z, a.act12), actf(acc[i][j][3] + bv.w, a.act12)};
-          if constexpr (MODE == kFull) {
+        for (int i = 0; i < FM; ++i) {
+          const float v[4] = {actf(acc[i][j][0] + bv.x, a.act12), actf(acc[i][j][1] + bv.y, a.act12),
+                              actf(acc[i][j][2] + bv.z, a.act12), actf(acc[i][j][3] + bv.w, a.act12)};
+          if (is_a) {
+            const int p = (m0 + i) * 16 + fr;
+            if (p < HPP) put_a(p, c, v, true);
+          } else if constexpr (MODE == kFull) {
             uint2 h2, l2;
             split4(v, h2, l2);
-            const int o = ((c >> 3) * (TH * TW) + i * TW + fr) * 8 + (c & 7);
+            const int o = ((c >> 3) * NI + i * TW + fr) * 8 + (c & 7);
             *reinterpret_cast<uint2*>(bh + o) = h2;
             *reinterpret_cast<uint2*>(bl + o) = l2;
           } else if (in[i]) {
@@ -248,6 +252,17 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
           }
         }
       }
+    };
+    if constexpr (NG == 2) {
+      // c_ 32: 7 x 2 (a) + 4 x 2 (b) tile-groups: a tiles 0-3 per group on waves 0, 1, a tiles 4-6 on
+      // wave 3, b on wave 2 (at most 4 activation fragments per wave and K step)
+      if (wid < 2) run(IC<4>{}, IC<1>{}, true, 0, wid);
+      else if (wid == 3) run(IC<3>{}, IC<2>{}, true, 4, 0);
+      else run(IC<4>{}, IC<2>{}, false, 0, 0);
+    } else {
+      // waves 0, 1: a on all halo tiles, half the groups each; waves 2, 3: b, half each
+      if (wid < 2) run(IC<MTH>{}, IC<NG / 2>{}, true, 0, (wid & 1) * (NG / 2));
+      else run(IC<MTI>{}, IC<NG / 2>{}, false, 0, (wid & 1) * (NG / 2));
     }
   } else {
     // a from a_in on the halo (zeros outside the image: they only reach masked u)
@@ -256,7 +271,8 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
       long pix;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (halo_in(p, pix)) v = *reinterpret_cast<const float4*>(a.a_in + pix * a.lda + a.a_off + c4 * 4);
-      *reinterpret_cast<float4*>(af + (c4 * HPP + p) * 4) = v;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      put_a(p, c4 * 4, vv, true);
     }
   }
   __syncthreads();
@@ -270,7 +286,7 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
     f32x4 acc[FM][FN];
     zero(acc);
     gemm<FM, FN, C / 32>(acc, a.wm1, NG, g0, lane, mv, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-      afrag((m0 + i) * 16 + fr, ks * 32 + fq * 8, h, l);
+      pfrag(ah, al, HPP, (m0 + i) * 16 + fr, ks * 32 + fq * 8, h, l);
     });
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -317,15 +333,14 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int mt = m0 + i, p = (mt + 1) * HW_ + fr + 1;  // halo index of this lane's tile pixel
-        float* ap = af + ((n >> 2) * HPP + p) * 4;
-        const float4 r0 = *reinterpret_cast<const float4*>(ap);
         float v[4] = {actf(acc[i][j][0] + bv.x, a.actm2), actf(acc[i][j][1] + bv.y, a.actm2),
                       actf(acc[i][j][2] + bv.z, a.actm2), actf(acc[i][j][3] + bv.w, a.actm2)};
-        if (a.add) {
+        if constexpr (RES) {  // the shortcut (RES == add)
+          const float4 r0 = *reinterpret_cast<const float4*>(ar + ((n >> 2) * NI + mt * TW + fr) * 4);
           v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         }
         if constexpr (MODE == kFull || MODE == kLast) {
-          *reinterpret_cast<float4*>(ap) = make_float4(v[0], v[1], v[2], v[3]);  // a' over a (same lane)
+          put_a(p, n, v, false);  // a' over a's tile pixels (P2 is done with them)
         } else {
           long pix;
           if (tile_in(mt, pix))
@@ -348,12 +363,9 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
     zero(acc);
     gemm<MTI, FN, 2 * C / 32>(acc, a.w3, COUT / 16, g0, lane, MTI, [&](int ks, int i, bf16x8& h, bf16x8& l) {
       if (ks < KA) {
-        afrag((i + 1) * HW_ + fr + 1, ks * 32 + fq * 8, h, l);
+        pfrag(ah, al, HPP, (i + 1) * HW_ + fr + 1, ks * 32 + fq * 8, h, l);
       } else if constexpr (MODE == kFull) {
-        const int c = (ks - KA) * 32 + fq * 8;
-        const int o = ((c >> 3) * (TH * TW) + i * TW + fr) * 8;
-        h = *reinterpret_cast<const bf16x8*>(bh + o);
-        l = *reinterpret_cast<const bf16x8*>(bl + o);
+        pfrag(bh, bl, NI, i * TW + fr, (ks - KA) * 32 + fq * 8, h, l);
       } else {
         gfrag(a.b_in, a.ldb, a.b_off, in[i], pix[i], (ks - KA) * 32 + fq * 8, h, l);
       }
@@ -373,21 +385,21 @@ __global__ void __launch_bounds__(256, C == 128 ? 1 : 2) c3_fused_kernel(C3fArgs
   }
 }
 
-template <int C, int CINM, int MODE>
+template <int C, int CINM, int MODE, bool RES>
 int launch_c3f(const C3fArgs& a, hipStream_t stream) {
   const long tiles = (long)a.B * ((a.H + 3) / 4) * ((a.W + 15) / 16);
   if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
-  c3_fused_kernel<C, CINM, MODE><<<(unsigned)tiles, 256, 0, stream>>>(a);
+  c3_fused_kernel<C, CINM, MODE, RES><<<(unsigned)tiles, 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
 template <int C, int CINM>
 int dispatch_mode(int mode, const C3fArgs& a, hipStream_t stream) {
-  switch (mode) {
-    case kFull: return launch_c3f<C, CINM, kFull>(a, stream);
-    case kFirst: return launch_c3f<C, CINM, kFirst>(a, stream);
-    case kMid: return launch_c3f<C, 2, kMid>(a, stream);  // (no x: cin unused)
-    case kLast: return launch_c3f<C, 2, kLast>(a, stream);
+  switch (mode) {  // a multi-bottleneck block's bottlenecks all have the shortcut (YOLOv5 backbone C3s)
+    case kFull: return a.add ? launch_c3f<C, CINM, kFull, true>(a, stream) : launch_c3f<C, CINM, kFull, false>(a, stream);
+    case kFirst: return a.add ? launch_c3f<C, CINM, kFirst, true>(a, stream) : (int)hipErrorInvalidValue;
+    case kMid: return a.add ? launch_c3f<C, 2, kMid, true>(a, stream) : (int)hipErrorInvalidValue;  // (no x)
+    case kLast: return a.add ? launch_c3f<C, 2, kLast, true>(a, stream) : (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -397,7 +409,7 @@ int dispatch_mode(int mode, const C3fArgs& a, hipStream_t stream) {
 // One fused C3 pass (c3_fused_kernel).  ptrs: x, a_in, b_in, y, a_out, b_out, w12, b12, wm1, bm1,
 // wm2, bm2, w3, b3 (unused ones null).  ints: mode, C, cin, cout, add, B, H, W, ldx, x_off, lda,
 // a_off, ldb, b_off, ldy, y_off, ldao, ao_off, ldbo, bo_off, act12, actm1, actm2, act3.
-// C in {32, 64, 128}, cin in {2C, 4C}, cout = 2C.  Weights: fragment-order split images of the
+// C in {32, 64}, cin in {2C, 4C}, cout = 2C; FIRST / MID / LAST need the shortcut (add).  Weights: fragment-order split images of the
 // FusedConvs' fp32 GEMM weights: cv1|cv2 merged [2C, cin], m.cv1 [C, C], m.cv2 [C, 9C] (tap-major
 // K), cv3 [2C, 2C].  Biases fp32 (16-B aligned).
 TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stream) {
@@ -430,7 +442,6 @@ TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stre
   switch (C) {
     case 32: return c4 ? dispatch_mode<32, 4>(mode, a, stream) : dispatch_mode<32, 2>(mode, a, stream);
     case 64: return c4 ? dispatch_mode<64, 4>(mode, a, stream) : dispatch_mode<64, 2>(mode, a, stream);
-    case 128: return c4 ? dispatch_mode<128, 4>(mode, a, stream) : dispatch_mode<128, 2>(mode, a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

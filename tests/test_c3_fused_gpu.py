@@ -1,4 +1,4 @@
-"""c3_fused.hip (YOLOv5 C3 blocks with c_ = 32 / 64 / 128 as LDS-resident kernels: FULL for one
+"""c3_fused.hip (YOLOv5 C3 blocks with c_ = 32 / 64 as LDS-resident kernels: FULL for one
 bottleneck, FIRST / MID / LAST for two or three) against the unfused _C3Plan chain of
 fused 1x1 / 3x3 convs it replaces: the same split operands in the same K order, so the
 block outputs agree to fp32 rounding; and the camera step's detections are unchanged."""
@@ -9,8 +9,8 @@ from triton_client_amd.ops.conv import NHWC
 from triton_client_amd.pipelines import CameraPipeline
 from triton_client_amd.utils.synthetic import camera_frame
 
-# YOLOv5n's C3 blocks: (module name, bottlenecks, shortcut)
-BLOCKS = ["b4", "b6", "b8", "h13", "h17", "h20", "h23"]
+# YOLOv5n's C3 blocks with c_ = 32 / 64 (b4: two bottlenecks, b6: three, the head C3s: one, no shortcut)
+BLOCKS = ["b4", "b6", "h13", "h17", "h20"]
 
 
 @pytest.fixture(scope="module")
@@ -29,7 +29,6 @@ def test_c3_fused_matches_chain(cuda, cam, monkeypatch, name, hw):
     torch.manual_seed(hw[0] * 7 + len(name))
     B, (H, W) = 2, hw
     blk = getattr(cam.model, name)
-    monkeypatch.setattr(fast, "FUSED_C3_WIDTHS", (32, 64, 128))  # every width the kernel takes
     plan = fast._C3Plan(blk, B, H, W, fast._Buffers(cuda, "fp32"), cuda)
     cin, cout = plan.cv12.cin_p, plan.cv3.N
     x = NHWC(torch.randn(B, H, W, cin + 8, device=cuda) * 2, 8, cin)  # channel-offset input slice
@@ -59,6 +58,7 @@ def test_camera_step_fused_c3_same_detections(cuda, monkeypatch):
     c.calibrate_detection_density(50.0)
     f = c.build_fast()
     assert all(p._fw is not None for p in (f.c3_4, f.c3_6, f.c3_13, f.c3_17, f.c3_20))
+    assert f.c3_8._fw is None and f.c3_23._fw is None  # c_ = 128: the chain
     r1 = c.step()
     torch.cuda.synchronize()
     n1, b1 = r1.count.clone(), r1.box.clone()

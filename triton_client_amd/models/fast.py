@@ -33,7 +33,7 @@ from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 STEM_FUSED = os.environ.get("TCA_STEM_FUSED", "1") != "0"
 # fused YOLOv5n first C3 block (_C3Plan.fused_ok) and the c3_fused.hip blocks (_C3Plan.fused2_ok)
 C3_FUSED = os.environ.get("TCA_C3_FUSED", "1") != "0"
-FUSED_C3_WIDTHS = (32, 64)  # c_ of the blocks c3_fused.hip runs (it also takes 128: measured slower there)
+FUSED_C3_WIDTHS = (32, 64)  # c_ of the blocks c3_fused.hip takes
 
 
 def _fc(m: ConvBNAct, device, precision: str = "bf16", **kw) -> FusedConv:
@@ -92,13 +92,13 @@ class _C3Plan:
         self.a = [bufs.new(B, H, W, c_), bufs.new(B, H, W, c_)]
         self.tmp = bufs.new(B, H, W, c_)
         self.out_c = self.cv3.N
-        # c3_fused.hip: fragment-order split weights, built here (never in a capture).  The kernel takes
-        # c_ = 32 / 64 / 128; the plan uses it where it measured faster than the chain: c_ = 32 (80 x 80:
-        # 128 vs 176-244 us at batch 32) and 64 (40 x 40: 84-165 vs 119-232 us), not 128 (20 x 20 at one
-        # 147 KiB workgroup per CU: 165-171 vs 118 us; profiles/r4/layers_camera_c3f*.json)
+        # c3_fused.hip (c_ = 32 / 64): fragment-order split weights, built here (never in a capture).
+        # The 20 x 20 c_ = 128 blocks stay on the chain (measured 118 vs 165-171 us at batch 32 for a
+        # first version of the kernel that took them; profiles/r4/layers_camera_c3f_v2.json)
         self._fw = None
         convs = [self.cv12, self.cv3] + [c for b1, b2, _ in self.m for c in (b1, b2)] if self.cv12 is not None else []
         if (C3_FUSED and self.cv12 is not None and c_ in FUSED_C3_WIDTHS and torch.device(device).type == "cuda"
+                and (len(self.m) == 1 or all(add for _, _, add in self.m))
                 and all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) and c.K == c.Kp
                         for c in convs)
                 and self.cv12.k == 1 and self.cv12.N == 2 * c_ and self.cv12.cin_p % 32 == 0
