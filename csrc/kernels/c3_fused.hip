@@ -105,12 +105,13 @@ __device__ __forceinline__ void wload(const __bf16* w, int ng, int ks, int g0, i
   }
 }
 
-// acc[i][j] += A(ks, i) . W(ks, g0 + j) over the K steps, the weights prefetched one step ahead
-// (two register sets, unrolled by two: no dynamically indexed register arrays).  MV: valid tiles.
+// acc[i][j] += A(ks, i) . W(ks, g0 + j) over the K steps, the weights prefetched two steps ahead
+// through a 3-deep register ring (unrolled by three: no dynamically indexed register arrays;
+// an L2 hit outlives one step of FM x FN x 3 MFMAs).  mv: valid tiles.
 template <int FM, int FN, int KS, class AF>
 __device__ __forceinline__ void gemm(f32x4 (&acc)[FM][FN], const __bf16* w, int ng, int g0, int lane, int mv,
                                      AF&& afrag) {
-  bf16x8 h0[FN], l0[FN], h1[FN], l1[FN];
+  bf16x8 h0[FN], l0[FN], h1[FN], l1[FN], h2[FN], l2[FN];
   auto step = [&](int ks, const bf16x8 (&wh)[FN], const bf16x8 (&wl)[FN]) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -121,15 +122,21 @@ __device__ __forceinline__ void gemm(f32x4 (&acc)[FM][FN], const __bf16* w, int 
       for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wh[j], wl[j], xh, xl);
     }
   };
+  auto clamp = [](int k) { return k < KS ? k : KS - 1; };
   wload<FN>(w, ng, 0, g0, lane, h0, l0);
-  constexpr int UN = KS <= 8 ? 4 : 1;
+  wload<FN>(w, ng, clamp(1), g0, lane, h1, l1);
+  constexpr int UN = KS <= 9 ? 3 : 1;
 #pragma unroll UN
-  for (int ks = 0; ks < KS; ks += 2) {
-    wload<FN>(w, ng, ks + 1 < KS ? ks + 1 : KS - 1, g0, lane, h1, l1);
+  for (int ks = 0; ks < KS; ks += 3) {
+    wload<FN>(w, ng, clamp(ks + 2), g0, lane, h2, l2);
     step(ks, h0, l0);
     if (ks + 1 < KS) {
-      wload<FN>(w, ng, ks + 2 < KS ? ks + 2 : KS - 1, g0, lane, h0, l0);
+      wload<FN>(w, ng, clamp(ks + 3), g0, lane, h0, l0);
       step(ks + 1, h1, l1);
+    }
+    if (ks + 2 < KS) {
+      wload<FN>(w, ng, clamp(ks + 4), g0, lane, h1, l1);
+      step(ks + 2, h2, l2);
     }
   }
 }
@@ -216,19 +223,66 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
   // ---- P1: a = act(cv1 x) on the halo, b = act(cv2 x) on the tile (FULL, FIRST);
   //      or a loaded from a_in on the halo (MID, LAST)
   if constexpr (MODE == kFull || MODE == kFirst) {
-    constexpr int KS = CIN / 32;
-    // cv1 on FM halo tiles from m0 for FN groups from g0 (a) or cv2 on the 4 tile rows (b)
+    // x streams through LDS one 32-channel chunk at a time, split into hi / lo planes once
+    // ([4][HPP][8] bf16 each, in the u planes' space, free until P2), the next chunk's loads in
+    // flight while this chunk's MFMAs run; every wave then reads its A fragments as stored.
+    constexpr int KS = CIN / 32, XB = C >= 64 ? 2 : 1;  // staging buffers (one is 128 B per halo pixel)
+    constexpr int XP = HPP * 8, XPL = (XP + 255) / 256;  // 16-B pieces per chunk, per thread
+    __bf16* const xs = uh;  // buffer k: hi planes at xs + k * 2 * 4 * HPP * 8, lo planes after them
+    float4 xr[XPL];
+    int xo[XPL];
+    long xg[XPL];
+#pragma unroll
+    for (int k = 0; k < XPL; ++k) {
+      const int q = tid + k * 256, p = q >> 3, f4 = q & 7;
+      long pix;
+      const bool in = q < XP && halo_in(p, pix);
+      xg[k] = in ? pix * a.ldx + a.x_off + f4 * 4 : -1;
+      xo[k] = q < XP ? ((f4 >> 1) * HPP + p) * 8 + (f4 & 1) * 4 : -1;
+    }
+    auto xload = [&](int c) {
+#pragma unroll
+      for (int k = 0; k < XPL; ++k)
+        xr[k] = xg[k] >= 0 ? *reinterpret_cast<const float4*>(a.x + xg[k] + c * 32) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto xstore = [&](int buf) {
+      __bf16* hb = xs + buf * 2 * 4 * HPP * 8;
+#pragma unroll
+      for (int k = 0; k < XPL; ++k) {
+        if (xo[k] < 0) continue;
+        const float v[4] = {xr[k].x, xr[k].y, xr[k].z, xr[k].w};
+        uint2 h2, l2;
+        split4(v, h2, l2);
+        *reinterpret_cast<uint2*>(hb + xo[k]) = h2;
+        *reinterpret_cast<uint2*>(hb + 4 * HPP * 8 + xo[k]) = l2;
+      }
+    };
+    // this wave's share: cv1 on FM halo tiles from m0 (a), or cv2 on the 4 tile rows (b), FN groups from g0
     auto run = [&](auto FMc, auto FNc, bool is_a, int m0, int g0) {
       constexpr int FM = decltype(FMc)::value, FN = decltype(FNc)::value;
-      long pix[FM];
-      bool in[FM];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) in[i] = is_a ? halo_in((m0 + i) * 16 + fr, pix[i]) : tile_in(i, pix[i]);
+      const int gw = (is_a ? 0 : NG) + g0;
       f32x4 acc[FM][FN];
       zero(acc);
-      gemm<FM, FN, KS>(acc, a.w12, 2 * NG, (is_a ? 0 : NG) + g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-        gfrag(a.x, a.ldx, a.x_off, in[i], pix[i], ks * 32 + fq * 8, h, l);
-      });
+      xload(0);
+#pragma unroll
+      for (int c = 0; c < KS; ++c) {
+        const int buf = XB == 2 ? (c & 1) : 0;
+        if (XB == 1 && c > 0) __syncthreads();  // every wave done with the previous chunk
+        xstore(buf);
+        if (c + 1 < KS) xload(c + 1);
+        bf16x8 wh[FN], wl[FN];
+        wload<FN>(a.w12, 2 * NG, c, gw, lane, wh, wl);
+        __syncthreads();
+        const __bf16* hb = xs + buf * 2 * 4 * HPP * 8;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int p = is_a ? (m0 + i) * 16 + fr : (i + 1) * HW_ + fr + 1;
+          bf16x8 xh, xl;
+          pfrag(hb, hb + 4 * HPP * 8, HPP, p, fq * 8, xh, xl);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mfma3(acc[i][j], wh[j], wl[j], xh, xl);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = (g0 + j) * 16 + fq * 4;  // a or b channel
@@ -247,15 +301,17 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
             const int o = ((c >> 3) * NI + i * TW + fr) * 8 + (c & 7);
             *reinterpret_cast<uint2*>(bh + o) = h2;
             *reinterpret_cast<uint2*>(bl + o) = l2;
-          } else if (in[i]) {
-            *reinterpret_cast<float4*>(a.b_out + pix[i] * a.ldbo + a.bo_off + c) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            long pix;
+            if (tile_in(i, pix))
+              *reinterpret_cast<float4*>(a.b_out + pix * a.ldbo + a.bo_off + c) = make_float4(v[0], v[1], v[2], v[3]);
           }
         }
       }
     };
     if constexpr (NG == 2) {
       // c_ 32: 7 x 2 (a) + 4 x 2 (b) tile-groups: a tiles 0-3 per group on waves 0, 1, a tiles 4-6 on
-      // wave 3, b on wave 2 (at most 4 activation fragments per wave and K step)
+      // wave 3, b on wave 2
       if (wid < 2) run(IC<4>{}, IC<1>{}, true, 0, wid);
       else if (wid == 3) run(IC<3>{}, IC<2>{}, true, 4, 0);
       else run(IC<4>{}, IC<2>{}, false, 0, 0);
@@ -265,14 +321,22 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
       else run(IC<MTI>{}, IC<NG / 2>{}, false, 0, (wid & 1) * (NG / 2));
     }
   } else {
-    // a from a_in on the halo (zeros outside the image: they only reach masked u)
-    for (int g = tid; g < HPP * (C / 4); g += 256) {
-      const int p = g % HPP, c4 = g / HPP;
+    // a from a_in on the halo (zeros outside the image: they only reach masked u); every load of
+    // this thread issued before the first store
+    constexpr int AP = HPP * (C / 4), APL = (AP + 255) / 256;
+    float4 v[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      const int g = tid + k * 256, p = g % HPP, c4 = g / HPP;
       long pix;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (halo_in(p, pix)) v = *reinterpret_cast<const float4*>(a.a_in + pix * a.lda + a.a_off + c4 * 4);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-      put_a(p, c4 * 4, vv, true);
+      v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (g < AP && halo_in(p, pix)) v[k] = *reinterpret_cast<const float4*>(a.a_in + pix * a.lda + a.a_off + c4 * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      const int g = tid + k * 256, p = g % HPP, c4 = g / HPP;
+      const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      if (g < AP) put_a(p, c4 * 4, vv, true);
     }
   }
   __syncthreads();
