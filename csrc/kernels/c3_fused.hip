@@ -375,6 +375,24 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
   }
   __syncthreads();
 
+  // LAST: this lane's b fragments of P4 (4 tile rows x C / 32 K steps x 8 channels), loaded now so
+  // the global latency hides behind P3
+  constexpr int KB = MODE == kLast ? C / 32 : 1;
+  float4 breg[MTI][KB][2];
+  if constexpr (MODE == kLast) {
+#pragma unroll
+    for (int i = 0; i < MTI; ++i) {
+      long pix;
+      const bool in = tile_in(i, pix);
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const float* q = a.b_in + pix * a.ldb + a.b_off + k * 32 + fq * 8;
+        breg[i][k][0] = in ? *reinterpret_cast<const float4*>(q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        breg[i][k][1] = in ? *reinterpret_cast<const float4*>(q + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+
   // ---- P3: a' = act(m.cv2 u) (+ a) on the tile: 3x3 over the u halo, K = 9 C in tap-major order
   {
     // C 32: 2 tile blocks (2 rows) x 2 groups; 64: 4 rows x 1 group per wave; 128: 4 x 2
@@ -431,7 +449,7 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
       } else if constexpr (MODE == kFull) {
         pfrag(bh, bl, NI, i * TW + fr, (ks - KA) * 32 + fq * 8, h, l);
       } else {
-        gfrag(a.b_in, a.ldb, a.b_off, in[i], pix[i], (ks - KA) * 32 + fq * 8, h, l);
+        split8(breg[i][ks - KA][0], breg[i][ks - KA][1], h, l);
       }
     });
 #pragma unroll
