@@ -1,0 +1,17 @@
+# Round-4 GPU check, part 6: fused C3 tests / layer table / benches, neck tiling variants, and the
+# bench.py multi-rank rehearsal (gloo, 2 and 4 ranks on the one card).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r4
+mkdir -p $O
+cd $R
+fatal() { case $1 in 124|134|137|139) echo "FATAL rc=$1 in $2: stopping"; exit $1;; esac; }
+bash tools/gpu_c3f.sh; rc=$?
+fatal $rc c3f
+echo "== neck variants"
+timeout -k 10 300 python -u tools/bench_neck.py 32 1,2,3,4,5 > $O/neck_variants.jsonl 2>&1; rc=$?
+cat $O/neck_variants.jsonl | tail -8
+fatal $rc neck
+echo "== bench.py rehearsal"
+timeout -k 10 900 bash tools/gpu_dp_rehearsal.sh; rc=$?
+fatal $rc dp_rehearsal
