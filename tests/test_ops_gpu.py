@@ -7,6 +7,7 @@ import torch
 
 from triton_client_amd.config.lidar import KITTI_PILLARS, KITTI_SECOND_VOXELS, NUSC_PILLARS, PointPillarsConfig
 from triton_client_amd.ops import golden
+from triton_client_amd.ops import lidar as lidar_ops
 from triton_client_amd.ops.image import preprocess
 from triton_client_amd.ops.lidar import (AnchorPostprocess, PillarEncoder, PointLayout, Voxelizer, pc2_unpack,
                                          pillar_features_reference, voxelize_np)
@@ -197,7 +198,7 @@ def test_voxelize_gpu_exact(cuda, vcfg, hash_mode, monkeypatch):
     """Order-exact vs the NumPy spconv golden, with the cell rows as the dense grid and as the
     per-frame hash table (voxelize.hip hash_slot; auto: hash for SECOND's 90 M-cell grid)."""
     if hash_mode != "auto":
-        monkeypatch.setenv("TCA_VOX_HASH", hash_mode)
+        monkeypatch.setattr(lidar_ops, "VOX_HASH_FORCE", hash_mode)
     cfg = dataclasses.replace(vcfg, max_voxels=2000)
     B, N = 2, 20000
     nf = cfg.num_point_features
@@ -227,7 +228,7 @@ def test_voxelize_gpu_dense_voxels(cuda, vcfg, hash_mode, monkeypatch):
     (wave bitonic top-P) path of the CSR slot sort; slot order must still be
     the first P points in point order (spconv)."""
     if hash_mode != "auto":
-        monkeypatch.setenv("TCA_VOX_HASH", hash_mode)
+        monkeypatch.setattr(lidar_ops, "VOX_HASH_FORCE", hash_mode)
     cfg = dataclasses.replace(vcfg, max_voxels=3000)
     rng = np.random.default_rng(7)
     r = np.asarray(cfg.point_cloud_range, np.float32)

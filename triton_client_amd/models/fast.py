@@ -19,7 +19,6 @@ neck's three up-sampled scales), so no concat kernel ever runs.
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -30,9 +29,10 @@ from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, to_pairs, upsam
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 # fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
-STEM_FUSED = os.environ.get("TCA_STEM_FUSED", "1") != "0"
-# fused YOLOv5n first C3 block (_C3Plan.fused_ok) and the c3_fused.hip blocks (_C3Plan.fused2_ok)
-C3_FUSED = os.environ.get("TCA_C3_FUSED", "1") != "0"
+STEM_FUSED = True
+# fused YOLOv5n first C3 block (_C3Plan.fused_ok) and the c3_fused.hip blocks (_C3Plan.fused2_ok);
+# False: the unfused chain (tests compare the two)
+C3_FUSED = True
 FUSED_C3_WIDTHS = (32, 64)  # c_ of the blocks c3_fused.hip takes
 
 
@@ -113,7 +113,7 @@ class _C3Plan:
 
     def fused_ok(self, x: NHWC, out: NHWC) -> bool:
         """yolo_c3s_fused (csrc/kernels/image.hip) takes this block: fp32, 32 -> 32 channels,
-        c_ = 16, one bottleneck (1x1 then 3x3), plain fp32 activations.  TCA_C3_FUSED=0: unfused."""
+        c_ = 16, one bottleneck (1x1 then 3x3), plain fp32 activations.  C3_FUSED False: unfused."""
         if not (C3_FUSED and self.cv12 is not None and len(self.m) == 1 and self.c_ == 16):
             return False
         b1, b2, _ = self.m[0]
@@ -276,7 +276,7 @@ class FastYOLOv5:
     def stem_fused_ok(self) -> bool:
         """The fused K1 + stem + b1 kernel (ops/image.py yolo_stem_fused) takes this plan:
         fp32, s2d stem 16 -> 16, b1 3x3 stride 2 16 -> 32, image sides divisible by 4.
-        TCA_STEM_FUSED=0 keeps the three-kernel chain."""
+        STEM_FUSED False keeps the three-kernel chain."""
         b0, b1 = self.b0, self.b1
         return (STEM_FUSED and self.s2d and self.precision == "fp32" and b0.N == 16 and b0.cin_p == 16
                 and b0.Kp == 160 and b0.k == 3 and b0.s == 1 and b1.cin_p == 16 and b1.N == 32 and b1.Kp == 160

@@ -19,7 +19,6 @@ on the GPU-less host).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -102,12 +101,11 @@ PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73
 
 
 # conv_hx3.hip (3x3 stride-1 / stride-2 pair convs with register-streamed fragment-order
-# weights): on by default for every eligible layer; TCA_HX3=0 falls back to the conv_mfma.hip
-# tiles (TCA_HX3S2=0: only the stride-2 layers do).  Tiles 110 (auto) and 111-116
-# (hx3_launch tiles 1-6) select the stride-1 kernel explicitly, 120 and 121-124
-# (hx3s2_launch tiles 1-4) the stride-2 one.
-HX3 = os.environ.get("TCA_HX3", "1") != "0"
-HX3S2 = HX3 and os.environ.get("TCA_HX3S2", "1") != "0"
+# weights): the default for every eligible layer (HX3 / HX3S2 False: the conv_mfma.hip tiles,
+# for A/B runs).  Tiles 110 (auto) and 111-116 (hx3_launch tiles 1-6) select the stride-1
+# kernel explicitly, 120 and 121-124 (hx3s2_launch tiles 1-4) the stride-2 one.
+HX3 = True
+HX3S2 = True
 HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
 

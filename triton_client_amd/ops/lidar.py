@@ -8,7 +8,6 @@ semantics (tested against ``golden``).
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -125,11 +124,15 @@ def voxelize_np(points: np.ndarray, cfg: VoxelConfig, nfeat: Optional[int] = Non
     return voxels, coords, num, slots
 
 
+# "1" / "0": force the voxeliser's hash-table cell rows on / off (tests); None: by grid size
+VOX_HASH_FORCE = None
+
+
 def voxel_hash_bits(cells: int, max_points: int) -> int:
     """log2 of the voxeliser's per-frame hash table (0: dense cell grid).  Hash when the grid has
     more than 16x as many cells as the table would (2 x max_points, rounded up to a power of 2)."""
     bits = max(10, int(2 * max(1, max_points) - 1).bit_length())
-    force = os.environ.get("TCA_VOX_HASH")
+    force = VOX_HASH_FORCE
     if force == "0":
         return 0
     if force == "1" or cells > 16 * (1 << bits):
@@ -153,7 +156,7 @@ class Voxelizer:
             g = self.ws.get
             # cell rows: the dense grid, or (grids much larger than a frame's points: SECOND's 90 M
             # cells, 720 MB per frame dense) a per-frame hash table of >= 2 x max_points slots
-            # (voxelize.hip hash_slot; TCA_VOX_HASH=1 / 0 forces it on / off)
+            # (voxelize.hip hash_slot; VOX_HASH_FORCE forces it on / off)
             self.hash_bits = voxel_hash_bits(cells, max_points)
             rows = (1 << self.hash_bits) if self.hash_bits else cells
             self.cell_first = g("cell_first", (batch, rows), torch.int32, init=INT_MAX)

@@ -10,7 +10,6 @@ the unfused plan for shapes outside the contract.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Sequence
 
 import torch
@@ -78,7 +77,7 @@ class FusedNeckHead:
         self.grid = max(8, grid // 8 * 8)
         # fp32 tiling variant (bev_neck.hip tca_bev_neck_head_x3v): 0 auto, 1 <8 waves, 3 stages>,
         # 2 <4 waves, 2 stages, two workgroups per CU>, 3 <8 waves, 2 stages>
-        self.variant = int(os.environ.get("TCA_NECK_VARIANT", "0"))
+        self.variant = 0
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
             self.wh = split_pairs(wh).to(device)
