@@ -590,6 +590,10 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     // <= 168 VGPRs -> 3 workgroups (12 waves) per CU
     case 5: return launch_hx3<8, 64, 1, 4, false, 2, 3>(a, stream);
     case 6: return launch_hx3<8, 64, 1, 4, true, 2, 3>(a, stream);
+    // 16-line tiles for N = 64 (halo 18 x 18: 1.27 input pixels per output instead of 1.41, and
+    // 18 line fragments per 16 instead of 10 per 8), one halo buffer (64 KiB: two workgroups per CU)
+    case 7: return launch_hx3<16, 64, 1, 4, false, 1, 2>(a, stream);
+    case 8: return launch_hx3<16, 64, 1, 4, true, 1, 2>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }
