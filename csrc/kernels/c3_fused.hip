@@ -161,14 +161,18 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
   // a on the halo as hi / lo planes (MFMA operands as stored), its tile pixels also in fp32 (the
   // residual); u on the halo; b on the tile (FULL).  a' (FULL / LAST) overwrites a's tile pixels.
   constexpr int P_BYTES = C * HPP * 2, R_BYTES = RES ? C * NI * 4 : 0, B_BYTES = HAS_B ? C * NI * 2 : 0;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * P_BYTES + R_BYTES + 2 * B_BYTES];
+  // x staging (P1) overlays the u planes, which come last: one 32-channel chunk needs 128 B per halo
+  // pixel, the u planes hold 4 C (c_ = 16: extended)
+  constexpr int U_REGION = 4 * C * HPP >= 128 * HPP ? 2 * P_BYTES : 128 * HPP;
+  constexpr int U_OFF = 2 * P_BYTES + R_BYTES + 2 * B_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[U_OFF + U_REGION];
   __bf16* const ah = reinterpret_cast<__bf16*>(smem);                  // [C/8][HPP][8]
   __bf16* const al = reinterpret_cast<__bf16*>(smem + P_BYTES);
-  __bf16* const uh = reinterpret_cast<__bf16*>(smem + 2 * P_BYTES);    // [C/8][HPP][8]
-  __bf16* const ul = reinterpret_cast<__bf16*>(smem + 3 * P_BYTES);
-  float* const ar = reinterpret_cast<float*>(smem + 4 * P_BYTES);      // [C/4][NI][4]
-  __bf16* const bh = reinterpret_cast<__bf16*>(smem + 4 * P_BYTES + R_BYTES);  // [C/8][NI][8]
-  __bf16* const bl = reinterpret_cast<__bf16*>(smem + 4 * P_BYTES + R_BYTES + B_BYTES);
+  float* const ar = reinterpret_cast<float*>(smem + 2 * P_BYTES);      // [C/4][NI][4]
+  __bf16* const bh = reinterpret_cast<__bf16*>(smem + 2 * P_BYTES + R_BYTES);  // [C/8][NI][8]
+  __bf16* const bl = reinterpret_cast<__bf16*>(smem + 2 * P_BYTES + R_BYTES + B_BYTES);
+  __bf16* const uh = reinterpret_cast<__bf16*>(smem + U_OFF);          // [C/8][HPP][8]
+  __bf16* const ul = reinterpret_cast<__bf16*>(smem + U_OFF + P_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
@@ -276,7 +280,7 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
         const __bf16* hb = xs + buf * 2 * 4 * HPP * 8;
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const int p = is_a ? (m0 + i) * 16 + fr : (i + 1) * HW_ + fr + 1;
+          const int p = is_a ? (m0 + i) * 16 + fr : (m0 + i + 1) * HW_ + fr + 1;
           bf16x8 xh, xl;
           pfrag(hb, hb + 4 * HPP * 8, HPP, p, fq * 8, xh, xl);
 #pragma unroll
@@ -298,18 +302,23 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
           } else if constexpr (MODE == kFull) {
             uint2 h2, l2;
             split4(v, h2, l2);
-            const int o = ((c >> 3) * NI + i * TW + fr) * 8 + (c & 7);
+            const int o = ((c >> 3) * NI + (m0 + i) * TW + fr) * 8 + (c & 7);
             *reinterpret_cast<uint2*>(bh + o) = h2;
             *reinterpret_cast<uint2*>(bl + o) = l2;
           } else {
             long pix;
-            if (tile_in(i, pix))
+            if (tile_in(m0 + i, pix))
               *reinterpret_cast<float4*>(a.b_out + pix * a.ldbo + a.bo_off + c) = make_float4(v[0], v[1], v[2], v[3]);
           }
         }
       }
     };
-    if constexpr (NG == 2) {
+    if constexpr (NG == 1) {
+      // c_ 16: 7 (a) + 4 (b) tiles: a tiles 0-3 / 4-6 on waves 0 / 1, b rows 0-1 / 2-3 on waves 2 / 3
+      if (wid == 0) run(IC<4>{}, IC<1>{}, true, 0, 0);
+      else if (wid == 1) run(IC<3>{}, IC<1>{}, true, 4, 0);
+      else run(IC<2>{}, IC<1>{}, false, (wid - 2) * 2, 0);
+    } else if constexpr (NG == 2) {
       // c_ 32: 7 x 2 (a) + 4 x 2 (b) tile-groups: a tiles 0-3 per group on waves 0, 1, a tiles 4-6 on
       // wave 3, b on wave 2
       if (wid < 2) run(IC<4>{}, IC<1>{}, true, 0, wid);
@@ -343,14 +352,20 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
 
   // ---- P2: u = act(m.cv1 a) on the halo, zero outside the image (the 3x3's padding)
   {
-    // C 32: 2 tile blocks (4 + 3) x 2 groups; 64: 7 tiles x 1 group per wave; 128: 7 x 2
-    constexpr int MB = NG >= 4 ? 1 : 2, FM = MB == 1 ? MTH : 4, FN = NG >= 4 ? NG / 4 : 1;
-    const int mb = MB == 1 ? 0 : wid >> 1, g0 = (MB == 1 ? wid : (wid & 1)) * FN;
+    // c_ 16: 4 tile blocks (2 + 2 + 2 + 1); 32: 2 blocks (4 + 3) x 2 groups; 64: 7 tiles x 1 group per wave
+    constexpr int MB = NG >= 4 ? 1 : 4 / NG, WPB = 4 / MB, FM = (MTH + MB - 1) / MB, FN = NG >= 4 ? NG / 4 : 1;
+    const int mb = wid / WPB, g0 = (wid % WPB) * FN;
     const int m0 = mb * FM, mv = MTH - m0 < FM ? MTH - m0 : FM;
     f32x4 acc[FM][FN];
     zero(acc);
-    gemm<FM, FN, C / 32>(acc, a.wm1, NG, g0, lane, mv, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-      pfrag(ah, al, HPP, (m0 + i) * 16 + fr, ks * 32 + fq * 8, h, l);
+    gemm<FM, FN, (C + 31) / 32>(acc, a.wm1, NG, g0, lane, mv, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      const int k0 = ks * 32 + fq * 8;
+      if (k0 < C) {
+        pfrag(ah, al, HPP, (m0 + i) * 16 + fr, k0, h, l);
+      } else {  // K padding (c_ 16): zero weights, zero operands
+        h = bf16x8{};
+        l = bf16x8{};
+      }
     });
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -377,7 +392,7 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
 
   // LAST: this lane's b fragments of P4 (4 tile rows x C / 32 K steps x 8 channels), loaded now so
   // the global latency hides behind P3
-  constexpr int KB = MODE == kLast ? C / 32 : 1;
+  constexpr int KB = MODE == kLast ? (C + 31) / 32 : 1;
   float4 breg[MTI][KB][2];
   if constexpr (MODE == kLast) {
 #pragma unroll
@@ -395,18 +410,23 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
 
   // ---- P3: a' = act(m.cv2 u) (+ a) on the tile: 3x3 over the u halo, K = 9 C in tap-major order
   {
-    // C 32: 2 tile blocks (2 rows) x 2 groups; 64: 4 rows x 1 group per wave; 128: 4 x 2
-    constexpr int MB = NG >= 4 ? 1 : 2, FM = MB == 1 ? MTI : 2, FN = NG >= 4 ? NG / 4 : 1;
-    const int mb = MB == 1 ? 0 : wid >> 1, g0 = (MB == 1 ? wid : (wid & 1)) * FN;
+    // c_ 16: one row per wave; 32: 2 row blocks x 2 groups; 64: 4 rows x 1 group per wave
+    constexpr int MB = NG >= 4 ? 1 : 4 / NG, WPB = 4 / MB, FM = MTI / MB, FN = NG >= 4 ? NG / 4 : 1;
+    const int mb = wid / WPB, g0 = (wid % WPB) * FN;
     const int m0 = mb * FM;
     f32x4 acc[FM][FN];
     zero(acc);
-    gemm<FM, FN, 9 * C / 32>(acc, a.wm2, NG, g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-      const int k0 = ks * 32, tap = k0 / C, ci = k0 - tap * C + fq * 8;
-      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-      const int o = ((ci >> 3) * HPP + (m0 + i + ky) * HW_ + fr + kx) * 8;
-      h = *reinterpret_cast<const bf16x8*>(uh + o);
-      l = *reinterpret_cast<const bf16x8*>(ul + o);
+    gemm<FM, FN, (9 * C + 31) / 32>(acc, a.wm2, NG, g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      const int k = ks * 32 + fq * 8, tap = k / C, ci = k - tap * C;  // tap-major K (c_ 16: two taps per step)
+      if (tap < 9) {
+        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+        const int o = ((ci >> 3) * HPP + (m0 + i + ky) * HW_ + fr + kx) * 8;
+        h = *reinterpret_cast<const bf16x8*>(uh + o);
+        l = *reinterpret_cast<const bf16x8*>(ul + o);
+      } else {  // K padding
+        h = bf16x8{};
+        l = bf16x8{};
+      }
     });
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -432,24 +452,27 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
     }
   }
 
-  // ---- P4: y = act(cv3 [a' | b]) on the tile: 4 rows x cout / 4 channels per wave
+  // ---- P4: y = act(cv3 [a' | b]) on the tile: 4 rows x cout / 4 channels per wave (c_ 16: one row x
+  //      all 32 channels per wave)
   if constexpr (MODE == kFull || MODE == kLast) {
     __syncthreads();
-    constexpr int FN = COUT / 16 / 4, KA = C / 32;
-    const int g0 = wid * FN;
-    long pix[MTI];
-    bool in[MTI];
+    constexpr bool ROWS = COUT / 16 >= 4;
+    constexpr int FN = ROWS ? COUT / 16 / 4 : COUT / 16, FM = ROWS ? MTI : 1;
+    const int g0 = ROWS ? wid * FN : 0, m0 = ROWS ? 0 : wid;
+    long pix[FM];
+    bool in[FM];
 #pragma unroll
-    for (int i = 0; i < MTI; ++i) in[i] = tile_in(i, pix[i]);
-    f32x4 acc[MTI][FN];
+    for (int i = 0; i < FM; ++i) in[i] = tile_in(m0 + i, pix[i]);
+    f32x4 acc[FM][FN];
     zero(acc);
-    gemm<MTI, FN, 2 * C / 32>(acc, a.w3, COUT / 16, g0, lane, MTI, [&](int ks, int i, bf16x8& h, bf16x8& l) {
-      if (ks < KA) {
-        pfrag(ah, al, HPP, (i + 1) * HW_ + fr + 1, ks * 32 + fq * 8, h, l);
+    gemm<FM, FN, 2 * C / 32>(acc, a.w3, COUT / 16, g0, lane, FM, [&](int ks, int i, bf16x8& h, bf16x8& l) {
+      const int k = ks * 32 + fq * 8;  // [a' | b] channel (per lane: c_ 16 splits one step)
+      if (k < C) {
+        pfrag(ah, al, HPP, (m0 + i + 1) * HW_ + fr + 1, k, h, l);
       } else if constexpr (MODE == kFull) {
-        pfrag(bh, bl, NI, i * TW + fr, (ks - KA) * 32 + fq * 8, h, l);
+        pfrag(bh, bl, NI, (m0 + i) * TW + fr, k - C, h, l);
       } else {
-        split8(breg[i][ks - KA][0], breg[i][ks - KA][1], h, l);
+        split8(breg[i][(k - C) >> 5][0], breg[i][(k - C) >> 5][1], h, l);
       }
     });
 #pragma unroll
@@ -457,7 +480,7 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
       const int n = (g0 + j) * 16 + fq * 4;
       const float4 bv = a.b3 ? *reinterpret_cast<const float4*>(a.b3 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int i = 0; i < MTI; ++i) {
+      for (int i = 0; i < FM; ++i) {
         if (!in[i]) continue;
         *reinterpret_cast<float4*>(a.y + pix[i] * a.ldy + a.y_off + n) =
             make_float4(actf(acc[i][j][0] + bv.x, a.act3), actf(acc[i][j][1] + bv.y, a.act3),
@@ -491,7 +514,7 @@ int dispatch_mode(int mode, const C3fArgs& a, hipStream_t stream) {
 // One fused C3 pass (c3_fused_kernel).  ptrs: x, a_in, b_in, y, a_out, b_out, w12, b12, wm1, bm1,
 // wm2, bm2, w3, b3 (unused ones null).  ints: mode, C, cin, cout, add, B, H, W, ldx, x_off, lda,
 // a_off, ldb, b_off, ldy, y_off, ldao, ao_off, ldbo, bo_off, act12, actm1, actm2, act3.
-// C in {32, 64}, cin in {2C, 4C}, cout = 2C; FIRST / MID / LAST need the shortcut (add).  Weights: fragment-order split images of the
+// C in {16, 32, 64} (16: cin 2C), cin in {2C, 4C}, cout = 2C; FIRST / MID / LAST need the shortcut (add).  Weights: fragment-order split images of the
 // FusedConvs' fp32 GEMM weights: cv1|cv2 merged [2C, cin], m.cv1 [C, C], m.cv2 [C, 9C] (tap-major
 // K), cv3 [2C, 2C].  Biases fp32 (16-B aligned).
 TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stream) {
@@ -522,6 +545,9 @@ TCA_API int tca_c3_fused(const void* const* ptrs, const int* v, hipStream_t stre
     return (int)hipErrorInvalidValue;
   const bool c4 = cin == 4 * C;
   switch (C) {
+    case 16:  // (YOLOv5's c_ = 16 block has one bottleneck)
+      if (c4 || mode != kFull) return (int)hipErrorInvalidValue;
+      return a.add ? launch_c3f<16, 2, kFull, true>(a, stream) : launch_c3f<16, 2, kFull, false>(a, stream);
     case 32: return c4 ? dispatch_mode<32, 4>(mode, a, stream) : dispatch_mode<32, 2>(mode, a, stream);
     case 64: return c4 ? dispatch_mode<64, 4>(mode, a, stream) : dispatch_mode<64, 2>(mode, a, stream);
     default: return (int)hipErrorInvalidValue;

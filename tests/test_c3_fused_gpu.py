@@ -9,8 +9,9 @@ from triton_client_amd.ops.conv import NHWC
 from triton_client_amd.pipelines import CameraPipeline
 from triton_client_amd.utils.synthetic import camera_frame
 
-# YOLOv5n's C3 blocks with c_ = 32 / 64 (b4: two bottlenecks, b6: three, the head C3s: one, no shortcut)
-BLOCKS = ["b4", "b6", "h13", "h17", "h20"]
+# YOLOv5n's C3 blocks with c_ = 16 / 32 / 64 (b2: c_ 16; b4: two bottlenecks, b6: three; the head
+# C3s: one, no shortcut)
+BLOCKS = ["b2", "b4", "b6", "h13", "h17", "h20"]
 
 
 @pytest.fixture(scope="module")
@@ -57,7 +58,7 @@ def test_camera_step_fused_c3_same_detections(cuda, monkeypatch):
         c.frames[b].copy_(torch.from_numpy(camera_frame(720, 1280, b)))
     c.calibrate_detection_density(50.0)
     f = c.build_fast()
-    assert all(p._fw is not None for p in (f.c3_4, f.c3_6, f.c3_13, f.c3_17, f.c3_20))
+    assert all(p._fw is not None for p in (f.c3_2, f.c3_4, f.c3_6, f.c3_13, f.c3_17, f.c3_20))
     assert f.c3_8._fw is None and f.c3_23._fw is None  # c_ = 128: the chain
     r1 = c.step()
     torch.cuda.synchronize()

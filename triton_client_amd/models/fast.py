@@ -33,7 +33,7 @@ STEM_FUSED = True
 # fused YOLOv5n first C3 block (_C3Plan.fused_ok) and the c3_fused.hip blocks (_C3Plan.fused2_ok);
 # False: the unfused chain (tests compare the two)
 C3_FUSED = True
-FUSED_C3_WIDTHS = (32, 64)  # c_ of the blocks c3_fused.hip takes
+FUSED_C3_WIDTHS = (16, 32, 64)  # c_ of the blocks c3_fused.hip takes
 
 
 def _fc(m: ConvBNAct, device, precision: str = "bf16", **kw) -> FusedConv:
@@ -92,17 +92,16 @@ class _C3Plan:
         self.a = [bufs.new(B, H, W, c_), bufs.new(B, H, W, c_)]
         self.tmp = bufs.new(B, H, W, c_)
         self.out_c = self.cv3.N
-        # c3_fused.hip (c_ = 32 / 64): fragment-order split weights, built here (never in a capture).
+        # c3_fused.hip (c_ = 16 / 32 / 64): fragment-order split weights, built here (never in a capture).
         # The 20 x 20 c_ = 128 blocks stay on the chain (measured 118 vs 165-171 us at batch 32 for a
         # first version of the kernel that took them; profiles/r4/layers_camera_c3f_v2.json)
         self._fw = None
         convs = [self.cv12, self.cv3] + [c for b1, b2, _ in self.m for c in (b1, b2)] if self.cv12 is not None else []
         if (C3_FUSED and self.cv12 is not None and c_ in FUSED_C3_WIDTHS and torch.device(device).type == "cuda"
-                and (len(self.m) == 1 or all(add for _, _, add in self.m))
-                and all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) and c.K == c.Kp
-                        for c in convs)
+                and (len(self.m) == 1 or all(add for _, _, add in self.m)) and (c_ >= 32 or len(self.m) == 1)
+                and all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) for c in convs)
                 and self.cv12.k == 1 and self.cv12.N == 2 * c_ and self.cv12.cin_p % 32 == 0
-                and self.cv3.k == 1 and self.cv3.cin_p == 2 * c_ and self.cv3.N % 64 == 0
+                and self.cv3.k == 1 and self.cv3.cin_p == 2 * c_ and self.cv3.N == 2 * c_
                 and all(b1.k == 1 and b1.cin_p == c_ and b1.N == c_ and b2.k == 3 and b2.s == 1 and b2.p == 1
                         and b2.cin_p == c_ and b2.N == c_ for b1, b2, _ in self.m)):
             from ..ops.conv import frag_weights
