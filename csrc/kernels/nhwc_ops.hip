@@ -65,6 +65,48 @@ __global__ void __launch_bounds__(256) upsample2x_kernel(const T* __restrict__ i
   }
 }
 
+// YOLOv5 SPPF's three chained k x k stride-1 max-pools in one launch: y1 = pool(y0), y2 = pool(y1),
+// y3 = pool(y2) (the same clipped-window maxes as three maxpool_kernel launches, so the same bits).
+// A workgroup owns one image and 4 16-B channel vectors; the plane lives in LDS and each pool is a
+// row pass then a column pass (separable max), written out after each round.
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) sppf_pool3_kernel(const T* __restrict__ in, int H, int W, int C, int ldi,
+                                                         int ci_off, int k, T* __restrict__ out, int ldo, int o1,
+                                                         int o2, int o3) {
+  constexpr int E = 16 / sizeof(T);
+  extern __shared__ uint4 lds[];  // [2][H * W][NV]
+  const int HW = H * W, nvg = C / (E * NV);
+  const int b = blockIdx.x / nvg, v0 = (blockIdx.x - (blockIdx.x / nvg) * nvg) * NV;
+  uint4* A = lds;
+  uint4* Tm = lds + HW * NV;
+  const int r = k / 2;
+  for (int i = threadIdx.x; i < HW * NV; i += blockDim.x) {
+    const int p = i / NV, v = i - (i / NV) * NV;
+    A[i] = *reinterpret_cast<const uint4*>(in + ((long)b * HW + p) * ldi + ci_off + (v0 + v) * E);
+  }
+  __syncthreads();
+  const int offs[3] = {o1, o2, o3};
+  for (int round = 0; round < 3; ++round) {
+    for (int i = threadIdx.x; i < HW * NV; i += blockDim.x) {  // rows
+      const int p = i / NV, v = i - (i / NV) * NV, y = p / W, x = p - (p / W) * W;
+      const int x0 = x - r < 0 ? 0 : x - r, x1 = x + r >= W ? W - 1 : x + r;
+      uint4 acc = A[(y * W + x0) * NV + v];
+      for (int xx = x0 + 1; xx <= x1; ++xx) vec_max<T>(acc, A[(y * W + xx) * NV + v]);
+      Tm[i] = acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < HW * NV; i += blockDim.x) {  // columns
+      const int p = i / NV, v = i - (i / NV) * NV, y = p / W, x = p - (p / W) * W;
+      const int y0 = y - r < 0 ? 0 : y - r, y1 = y + r >= H ? H - 1 : y + r;
+      uint4 acc = Tm[(y0 * W + x) * NV + v];
+      for (int yy = y0 + 1; yy <= y1; ++yy) vec_max<T>(acc, Tm[(yy * W + x) * NV + v]);
+      A[i] = acc;
+      *reinterpret_cast<uint4*>(out + ((long)b * HW + p) * ldo + offs[round] + (v0 + v) * E) = acc;
+    }
+    __syncthreads();
+  }
+}
+
 int grid_for(long work) { return (int)min((work + 255) / 256, (long)4096); }
 
 bool slices_ok(int C, int ldi, int ci_off, int ldo, int co_off, int dtype) {
@@ -118,5 +160,28 @@ TCA_API int tca_upsample2x_nhwc(const void* in, int B, int H, int W, int C, int 
   else
     upsample2x_kernel<__hip_bfloat16><<<g, 256, 0, stream>>>((const __hip_bfloat16*)in, B, H, W, C, ldi, ci_off,
                                                              (__hip_bfloat16*)out, ldo, co_off);
+  TCA_LAUNCH_CHECK();
+}
+
+// SPPF: the three chained k x k stride-1 max-pools of channels [ci_off, ci_off + C) of in into the
+// slices at o1, o2, o3 of out (one launch; sppf_pool3_kernel).  Needs the image plane of 4 channel
+// vectors twice in LDS (H * W * 128 B <= 64 KiB); returns hipErrorInvalidValue when it does not fit
+// (ops/conv.py sppf_pools then runs three tca_maxpool_nhwc).
+TCA_API int tca_sppf_pool3(const void* in, int B, int H, int W, int C, int ldi, int ci_off, int k, void* out, int ldo,
+                           int o1, int o2, int o3, int dtype, hipStream_t stream) {
+  if (B <= 0) return 0;
+  constexpr int NV = 4;
+  const int E = dtype == kF32 ? 4 : 8;
+  if (!slices_ok(C, ldi, ci_off, ldo, o1, dtype) || (o2 % E) || (o3 % E) || (C % (E * NV)) || k < 1 || !(k & 1))
+    return (int)hipErrorInvalidValue;
+  const long lds = 2L * H * W * NV * 16;
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;  // (the default dynamic-LDS limit of a launch)
+  const int grid = B * (C / (E * NV));
+  if (dtype == kF32)
+    sppf_pool3_kernel<float, NV><<<grid, 256, lds, stream>>>((const float*)in, H, W, C, ldi, ci_off, k, (float*)out,
+                                                            ldo, o1, o2, o3);
+  else
+    sppf_pool3_kernel<__hip_bfloat16, NV><<<grid, 256, lds, stream>>>((const __hip_bfloat16*)in, H, W, C, ldi, ci_off,
+                                                                     k, (__hip_bfloat16*)out, ldo, o1, o2, o3);
   TCA_LAUNCH_CHECK();
 }

@@ -63,11 +63,11 @@ def main():
 
     orig_call = convmod.FusedConv.__call__
     convmod.FusedConv.__call__ = timed(conv_label, orig_call)
-    for name in ("maxpool_nhwc", "upsample2x_nhwc"):
+    for name in ("maxpool_nhwc", "upsample2x_nhwc", "sppf_pools"):
         f = getattr(convmod, name)
         setattr(convmod, name, timed(lambda x, out, *r, _n=name, **k: (_n, x.shape[1], x.shape[2], x.c), f))
     import triton_client_amd.models.fast as fast
-    for name in ("maxpool_nhwc", "upsample2x_nhwc"):
+    for name in ("maxpool_nhwc", "upsample2x_nhwc", "sppf_pools"):
         setattr(fast, name, getattr(convmod, name))
     fast._C3Plan.__call__ = timed(lambda self, x, out: ("c3", id(self), x.c, self.c_, x.shape[1], x.shape[2],
                                                         self.fused_ok(x, out) or self.fused2_ok(x, out)),

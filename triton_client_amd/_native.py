@@ -89,6 +89,8 @@ _KERNEL_SIGS = {
     "tca_group_norm_nhwc": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, P],
     "tca_group_norm_nhwc_dt": [P, I, I, I, I, I, I, F, P, P, I, P, P, I, I, I, P],
     "tca_yolov4_decode": [P, P, P, I, I, I, P, P, P, F, F, I, I, P, P, P, P, P, P, P, I, P],
+    # in, B, H, W, C, ldi, ci_off, k, out, ldo, o1, o2, o3, dtype, stream
+    "tca_sppf_pool3": [P, I, I, I, I, I, I, I, P, I, I, I, I, I, P],
     "tca_maxpool_nhwc": [P, I, I, I, I, I, I, I, P, I, I, I, P],
     "tca_upsample2x_nhwc": [P, I, I, I, I, I, I, P, I, I, I, P],
     "tca_vox_slots_csr": [P, I, P, I, P, P, I, I, P, P, P, P, P, P, P, P, I, P],

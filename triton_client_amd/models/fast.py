@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, to_pairs, upsample2x_nhwc
+from ..ops.conv import NHWC, FusedConv, act_dtype, maxpool_nhwc, sppf_pools, to_pairs, upsample2x_nhwc
 from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 # fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
@@ -322,9 +322,7 @@ class FastYOLOv5:
         t = self.c3_8(t, out=self.t8)
         cs = self.sp1.N
         y0 = self.sp1(t, out=NHWC(self.spcat.t, 0, cs))
-        y1 = maxpool_nhwc(y0, NHWC(self.spcat.t, cs, cs), self.k)
-        y2 = maxpool_nhwc(y1, NHWC(self.spcat.t, 2 * cs, cs), self.k)
-        maxpool_nhwc(y2, NHWC(self.spcat.t, 3 * cs, cs), self.k)
+        sppf_pools(y0, self.spcat.t, cs, self.k)
         t9 = self.sp2(self.spcat, out=self.t9)
         h10 = self.h10(t9, out=self.h10_out)
         upsample2x_nhwc(h10, NHWC(self.cat13.t, 0, self.h10.N))

@@ -304,6 +304,22 @@ class FusedConv:
         return out
 
 
+def sppf_pools(y0: NHWC, dst: torch.Tensor, cs: int, k: int = 5, stream=None) -> None:
+    """YOLOv5 SPPF: y1 = pool(y0), y2 = pool(y1), y3 = pool(y2) (k x k, stride 1) into the channel
+    slices [cs, 2cs), [2cs, 3cs), [3cs, 4cs) of dst.  One launch (nhwc_ops.hip tca_sppf_pool3) when
+    the image plane fits its LDS, else three max-pools; the same bits either way."""
+    B, H, W, C = y0.shape
+    e = 4 if y0.t.dtype == torch.float32 else 8
+    if (y0.t.is_cuda and C % (4 * e) == 0 and 2 * H * W * 64 <= 64 * 1024 and y0.off % e == 0
+            and y0.t.shape[-1] % e == 0 and dst.shape[-1] % e == 0 and cs % e == 0):
+        _native.call("tca_sppf_pool3", _native.ptr(y0.t), B, H, W, C, y0.t.shape[-1], y0.off, k, _native.ptr(dst),
+                     dst.shape[-1], cs, 2 * cs, 3 * cs, nhwc_dtype_code(y0.t), _native.stream_ptr(stream))
+        return
+    y1 = maxpool_nhwc(y0, NHWC(dst, cs, cs), k, stream)
+    y2 = maxpool_nhwc(y1, NHWC(dst, 2 * cs, cs), k, stream)
+    maxpool_nhwc(y2, NHWC(dst, 3 * cs, cs), k, stream)
+
+
 def maxpool_nhwc(x: NHWC, out: NHWC, k: int = 5, stream=None) -> NHWC:
     """k x k max-pool, stride 1, pad k//2 (SPPF), slice → slice."""
     B, H, W, C = x.shape
