@@ -22,3 +22,8 @@ fatal $rc neck
 echo "== bench.py rehearsal"
 timeout -k 10 900 bash tools/gpu_dp_rehearsal.sh; rc=$?
 fatal $rc dp_rehearsal
+echo "== served (shm / raw, one and two server processes)"
+NOTEST=1 SPROCS=1 TAG=_r4f timeout -k 10 400 bash tools/gpu_served3.sh; rc=$?
+fatal $rc served1
+NOTEST=1 SPROCS=2 TAG=_r4f timeout -k 10 400 bash tools/gpu_served3.sh; rc=$?
+fatal $rc served2
