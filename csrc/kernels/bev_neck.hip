@@ -694,11 +694,9 @@ TCA_API int tca_bev_neck_head(int nbr, const void* const* x, const int* ldx, con
 // fp32 mode: x[i] fp32, w[i] split [s_i*s_i*128, 2*cin[i]] bf16, wh split [80, 2*nbr*128]
 // (32-chunk permuted, then split), out fp32 [B, H, W, ldo].  Other arguments as tca_bev_neck_head.
 namespace {
-// variant 1: <8 waves, 3 stages> one workgroup per CU; 2: <4 waves, 2 stages> two per CU; 3: <8, 2>
-// auto: <8, 2> (tools/bench_neck.py at batch 32 on MI355X: 1157 us vs 1348 for <8, 3> and 2000 for <4, 2>;
-// profiles/r2/neck_variants.json)
-constexpr int kNeckX3Auto = 3;
-
+// tiling: <8 waves, 2 stages>, one workgroup per CU.  Measured at batch 32 on MI355X against <8, 3>,
+// <4, 2> (two per CU) and the 64-pixel-wave <4, 3, FM 4> / <4, 2, FM 4>: 1008 us vs 1192-1483
+// (profiles/r4/neck_variants.jsonl, profiles/r2/neck_variants.json); the others were removed.
 template <int NWV, int STAGES, int FM = 2>
 void launch_neck_x3(NeckArgsX3& a, long np, int grid, bool pair, hipStream_t stream) {
   using T = NeckX3<NWV, STAGES, FM>;
@@ -713,8 +711,7 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   if (B <= 0) return 0;
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
-  if (variant == 0) variant = kNeckX3Auto;
-  if (variant < 1 || variant > 5) return (int)hipErrorInvalidValue;
+  if (variant != 0 && variant != 3) return (int)hipErrorInvalidValue;  // 0 / 3: the one tiling
   NeckArgsX3 a;
   int S = 1, nsteps = 0;
   for (int i = 0; i < nbr; ++i) {
@@ -741,16 +738,8 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   if (pair)
     for (int i = 0; i < nbr; ++i)
       if ((ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;
-  // grid: workgroup slots of the persistent kernel for one per CU; variant 2 runs two per CU
-  switch (variant) {
-    case 1: launch_neck_x3<8, 3>(a, B * nq, grid, pair, stream); break;
-    case 2: launch_neck_x3<4, 2>(a, B * nq, 2 * grid, pair, stream); break;
-    // 4 waves of 64 pixels (FM 4) at one wave per SIMD: each B fragment read from LDS feeds
-    // four fragment pairs (half the LDS read bytes per MFMA of the 32-pixel waves)
-    case 4: launch_neck_x3<4, 3, 4>(a, B * nq, grid, pair, stream); break;
-    case 5: launch_neck_x3<4, 2, 4>(a, B * nq, grid, pair, stream); break;
-    default: launch_neck_x3<8, 2>(a, B * nq, grid, pair, stream); break;
-  }
+  // grid: workgroup slots of the persistent kernel, one per CU
+  launch_neck_x3<8, 2>(a, B * nq, grid, pair, stream);
   TCA_LAUNCH_CHECK();
 }
 }  // namespace
@@ -770,8 +759,8 @@ TCA_API int tca_bev_neck_head_x3p(int nbr, const void* const* x, const int* ldx,
   return neck_x3(nbr, x, ldx, offx, cin, s, w, bias, wh, bh, nh, out, ldo, B, H, W, grid, true, 0, stream);
 }
 
-// Same with an explicit tiling variant (0 auto, 1 <8 waves, 3 stages>, 2 <4 waves, 2 stages, two
-// workgroups per CU>, 3 <8 waves, 2 stages>) and input storage (pair != 0: pair storage).
+// Same with the input storage as an argument (pair != 0: pair storage); variant: 0 (the one tiling,
+// also accepted as 3, its former number).
 TCA_API int tca_bev_neck_head_x3v(int nbr, const void* const* x, const int* ldx, const int* offx, const int* cin,
                                   const int* s, const void* const* w, const float* const* bias, const void* wh,
                                   const float* bh, int nh, void* out, int ldo, int B, int H, int W, int grid,

@@ -570,7 +570,8 @@ int launch_hx3(const Hx3Args& a, hipStream_t stream) {
 // hx3 tiles.  0 = auto: N % 128 == 0 -> 8 x 16 tiles, 4 waves of 128 pixels x 32 channels
 // (row- or column-major by the smaller padding); N == 64 -> 8 x 16 tiles, 4 waves of 128
 // pixels x 16 channels (3 workgroups per CU).  Every variant: 2 waves per SIMD (<= 256 VGPRs, no spill), two
-// workgroups per CU (<= 80 KiB LDS).
+// workgroups per CU (<= 80 KiB LDS).  (16-line N = 64 tiles measured on par: 361-371 vs 365 us for
+// pp.b1.conv at batch 32, profiles/r4/hx3_16line_tiles_removed.jsonl.)
 int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
   if (tile == 0) {
     const long rm8 = (long)((a.Wo + 15) / 16 * 16) * ((a.Ho + 7) / 8 * 8);
@@ -590,10 +591,6 @@ int hx3_launch(const Hx3Args& a, int tile, hipStream_t stream) {
     // <= 168 VGPRs -> 3 workgroups (12 waves) per CU
     case 5: return launch_hx3<8, 64, 1, 4, false, 2, 3>(a, stream);
     case 6: return launch_hx3<8, 64, 1, 4, true, 2, 3>(a, stream);
-    // 16-line tiles for N = 64 (halo 18 x 18: 1.27 input pixels per output instead of 1.41, and
-    // 18 line fragments per 16 instead of 10 per 8), one halo buffer (64 KiB: two workgroups per CU)
-    case 7: return launch_hx3<16, 64, 1, 4, false, 1, 2>(a, stream);
-    case 8: return launch_hx3<16, 64, 1, 4, true, 1, 2>(a, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -530,245 +530,6 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
   }
 }
 
-// ---- YOLOv5n's first C3 (b2: 32 -> 32 channels, c_ = 16, one bottleneck) in one kernel.
-//
-// Unfused (models/fast.py _C3Plan) the block is four launches at 160 x 160 that move ~790 MB
-// through HBM at batch 32: cv1|cv2 (1x1, 32 -> 16 | 16) into the concat buffer, the
-// bottleneck's 1x1 (16 -> 16) and 3x3 (16 -> 16, + a), cv3 (1x1, 32 -> 32).  Here a workgroup
-// owns a 16 x 16 pixel tile: x on the 18 x 18 halo (split hi / lo) -> a = cv1(x) on the halo
-// (fp32, the residual) and b = cv2(x) inside -> u = m.cv1(a) on the halo (zero outside the
-// image: the 3x3's padding) -> a' = m.cv2(u) + a inside -> y = cv3([a' | b]).  Every
-// intermediate stays in LDS (78.6 KiB: two workgroups per CU); only x is read and y written.
-// Each MFMA operand is the bf16 hi / lo split of the same fp32 value the unfused chain
-// stores, and the K steps run in the same order, so y matches the four-kernel chain.
-struct C3sArgs {
-  const float* x;  // [B, H, W, ldx], channels [x_off, x_off + 32)
-  float* y;        // [B, H, W, ldy], channels [y_off, y_off + 32)
-  const __hip_bfloat16 *w12, *wm1, *wm2, *w3;  // split_pairs images: [32, 2*32], [16, 2*32], [16, 2*160], [32, 2*32]
-  const float *b12, *bm1, *bm2, *b3;
-  int act12, actm1, actm2, act3, add;
-  int B, H, W, ldx, x_off, ldy, y_off;
-};
-
-__global__ void __launch_bounds__(256, 2) yolo_c3s_fused_kernel(C3sArgs a) {
-  constexpr int T = 16, HS = T + 2, NH = HS * HS, NHT = (NH + 15) / 16;  // halo 18 x 18 (21 M tiles)
-  constexpr int NI = T * T;
-  // LDS: X hi | X lo (halo, 32 ch, 64 B per pixel each), A (halo, 16 ch fp32, 64 B), Bh | Bl (inside,
-  // 16 ch, 32 B each); U hi | lo (halo, 16 ch, 32 B each) overlays X once a and b exist
-  constexpr int XB = NH * 64, AB = NH * 64, BB = NI * 32;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * XB + AB + 2 * BB];
-  unsigned char* const xh = smem;
-  unsigned char* const xl = smem + XB;
-  unsigned char* const uh = smem;            // overlays X
-  unsigned char* const ul = smem + NH * 32;
-  float* const aimg = reinterpret_cast<float*>(smem + 2 * XB);
-  unsigned char* const bh_ = smem + 2 * XB + AB;
-  unsigned char* const bl_ = bh_ + BB;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int ntx = (a.W + T - 1) / T, nty = (a.H + T - 1) / T;
-  const int tile = blockIdx.x;
-  const int b = tile / (nty * ntx), rem = tile - b * nty * ntx;
-  const int y0 = (rem / ntx) * T, x0 = (rem - (rem / ntx) * ntx) * T;
-
-  // x halo -> hi / lo images (zeros outside the image; those pixels only feed masked u)
-  for (int g = tid; g < NH * 8; g += 256) {
-    const int p = g >> 3, c4 = g & 7;
-    const int hy = p / HS, hx = p - (p / HS) * HS;
-    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-      v = *reinterpret_cast<const float4*>(a.x + (((long)b * a.H + iy) * a.W + ix) * a.ldx + a.x_off + c4 * 4);
-    const float vv[4] = {v.x, v.y, v.z, v.w};
-    __bf16 h[4], l[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      h[e] = (__bf16)vv[e];
-      l[e] = (__bf16)(vv[e] - (float)h[e]);
-    }
-    *reinterpret_cast<uint2*>(xh + p * 64 + c4 * 8) = *reinterpret_cast<const uint2*>(h);
-    *reinterpret_cast<uint2*>(xl + p * 64 + c4 * 8) = *reinterpret_cast<const uint2*>(l);
-  }
-  __syncthreads();
-
-  auto wfrag = [&](const __hip_bfloat16* w, int kp, int n, int k0, bf16x8_t& wh, bf16x8_t& wl) {
-    const __hip_bfloat16* q = w + n * 2 * kp + (k0 >> 3) * 16;
-    wh = *reinterpret_cast<const bf16x8_t*>(q);
-    wl = *reinterpret_cast<const bf16x8_t*>(q + 8);
-  };
-  auto split8 = [&](const float* v, bf16x8_t& h, bf16x8_t& l) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      h[e] = (__bf16)v[e];
-      l[e] = (__bf16)(v[e] - (float)h[e]);
-    }
-  };
-  auto inside = [&](int p) {  // halo pixel p inside the image
-    const int hy = p / HS, hx = p - (p / HS) * HS;
-    return (unsigned)(y0 - 1 + hy) < (unsigned)a.H && (unsigned)(x0 - 1 + hx) < (unsigned)a.W;
-  };
-  auto interior = [&](int p) {  // halo pixel p -> interior index, or -1
-    const int hy = p / HS, hx = p - (p / HS) * HS;
-    return (hy >= 1 && hy <= T && hx >= 1 && hx <= T) ? (hy - 1) * T + hx - 1 : -1;
-  };
-
-  // a = act(cv1 x) on the halo (fp32 into A), b = act(cv2 x) inside (split into B)
-  {
-    bf16x8_t wh[2], wl[2];
-    wfrag(a.w12, 32, fr, fq * 8, wh[0], wl[0]);
-    wfrag(a.w12, 32, 16 + fr, fq * 8, wh[1], wl[1]);
-    float ba[4], bb[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      ba[r] = a.b12 ? a.b12[fq * 4 + r] : 0.f;
-      bb[r] = a.b12 ? a.b12[16 + fq * 4 + r] : 0.f;
-    }
-    for (int mt = wid; mt < NHT; mt += 4) {
-      const int p = mt * 16 + fr;
-      bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
-      if (p < NH) {
-        ah = *reinterpret_cast<const bf16x8_t*>(xh + p * 64 + fq * 16);
-        al = *reinterpret_cast<const bf16x8_t*>(xl + p * 64 + fq * 16);
-      }
-      f32x4_t c0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, c1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      stem_mfma3(c0, wh[0], wl[0], ah, al);
-      stem_mfma3(c1, wh[1], wl[1], ah, al);
-      // D layout: lane holds pixel mt * 16 + fr, channels fq * 4 .. + 3
-      if (p < NH) {
-        float va[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) va[r] = stem_act(c0[r] + ba[r], a.act12);
-        *reinterpret_cast<float4*>(aimg + p * 16 + fq * 4) = make_float4(va[0], va[1], va[2], va[3]);
-        const int q = interior(p);
-        if (q >= 0) {
-          __bf16 h[4], l[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = stem_act(c1[r] + bb[r], a.act12);
-            h[r] = (__bf16)v;
-            l[r] = (__bf16)(v - (float)h[r]);
-          }
-          *reinterpret_cast<uint2*>(bh_ + q * 32 + fq * 8) = *reinterpret_cast<const uint2*>(h);
-          *reinterpret_cast<uint2*>(bl_ + q * 32 + fq * 8) = *reinterpret_cast<const uint2*>(l);
-        }
-      }
-    }
-  }
-  __syncthreads();  // a, b written; X no longer read: U may overlay it
-
-  // u = act(m.cv1 a) on the halo, zero outside the image (K 16, padded to one 32-deep step)
-  {
-    bf16x8_t wh, wl;
-    wfrag(a.wm1, 32, fr, fq * 8, wh, wl);
-    float bu[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bu[r] = a.bm1 ? a.bm1[fq * 4 + r] : 0.f;
-    for (int mt = wid; mt < NHT; mt += 4) {
-      const int p = mt * 16 + fr;
-      bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
-      if (p < NH && fq < 2) {
-        const float4 v0 = *reinterpret_cast<const float4*>(aimg + p * 16 + fq * 8);
-        const float4 v1 = *reinterpret_cast<const float4*>(aimg + p * 16 + fq * 8 + 4);
-        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        split8(v, ah, al);
-      }
-      f32x4_t c = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      stem_mfma3(c, wh, wl, ah, al);
-      if (p < NH) {
-        const bool in = inside(p);
-        __bf16 h[4], l[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = in ? stem_act(c[r] + bu[r], a.actm1) : 0.f;
-          h[r] = (__bf16)v;
-          l[r] = (__bf16)(v - (float)h[r]);
-        }
-        *reinterpret_cast<uint2*>(uh + p * 32 + fq * 8) = *reinterpret_cast<const uint2*>(h);
-        *reinterpret_cast<uint2*>(ul + p * 32 + fq * 8) = *reinterpret_cast<const uint2*>(l);
-      }
-    }
-  }
-  __syncthreads();
-
-  // a' = act(m.cv2 u) (+ a) inside: wave wid owns tile rows 4 wid .. 4 wid + 3 (3x3 over U, K 144 -> 160)
-  {
-    f32x4_t c[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int st = 0; st < 5; ++st) {
-      const int k0 = st * 32 + fq * 8, tap = k0 >> 4, ci0 = k0 & 15;
-      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-      bf16x8_t wh, wl;
-      wfrag(a.wm2, 160, fr, k0, wh, wl);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        bf16x8_t ah = bf16x8_t{}, al = bf16x8_t{};
-        if (tap < 9) {
-          const int p = (4 * wid + i + ky) * HS + fr + kx;
-          ah = *reinterpret_cast<const bf16x8_t*>(uh + p * 32 + ci0 * 2);
-          al = *reinterpret_cast<const bf16x8_t*>(ul + p * 32 + ci0 * 2);
-        }
-        stem_mfma3(c[i], wh, wl, ah, al);
-      }
-    }
-    float bm[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bm[r] = a.bm2 ? a.bm2[fq * 4 + r] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = (4 * wid + i + 1) * HS + fr + 1;  // halo index of the interior pixel
-      float* ap = aimg + p * 16 + fq * 4;
-      const float4 r0 = *reinterpret_cast<const float4*>(ap);
-      const float rv[4] = {r0.x, r0.y, r0.z, r0.w};
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = stem_act(c[i][r] + bm[r], a.actm2);
-        if (a.add) v[r] += rv[r];
-      }
-      *reinterpret_cast<float4*>(ap) = make_float4(v[0], v[1], v[2], v[3]);  // a' over a (same lane)
-    }
-  }
-  __syncthreads();
-
-  // y = act(cv3 [a' | b]) inside: K 32 = a' channels 0-15 (fq 0, 1) | b channels 0-15 (fq 2, 3), N 32
-  {
-    bf16x8_t wh[2], wl[2];
-    wfrag(a.w3, 32, fr, fq * 8, wh[0], wl[0]);
-    wfrag(a.w3, 32, 16 + fr, fq * 8, wh[1], wl[1]);
-    const int ox = x0 + fr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ty = 4 * wid + i, q = ty * T + fr;
-      bf16x8_t ah, al;
-      if (fq < 2) {
-        const float* ap = aimg + ((ty + 1) * HS + fr + 1) * 16 + fq * 8;
-        const float4 v0 = *reinterpret_cast<const float4*>(ap);
-        const float4 v1 = *reinterpret_cast<const float4*>(ap + 4);
-        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        split8(v, ah, al);
-      } else {
-        ah = *reinterpret_cast<const bf16x8_t*>(bh_ + q * 32 + (fq - 2) * 16);
-        al = *reinterpret_cast<const bf16x8_t*>(bl_ + q * 32 + (fq - 2) * 16);
-      }
-      f32x4_t c0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, c1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      stem_mfma3(c0, wh[0], wl[0], ah, al);
-      stem_mfma3(c1, wh[1], wl[1], ah, al);
-      const int oy = y0 + ty;
-      if (oy >= a.H || ox >= a.W) continue;
-      float* o = a.y + (((long)b * a.H + oy) * a.W + ox) * a.ldy + a.y_off;
-      float v0[4], v1[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v0[r] = stem_act(c0[r] + (a.b3 ? a.b3[fq * 4 + r] : 0.f), a.act3);
-        v1[r] = stem_act(c1[r] + (a.b3 ? a.b3[16 + fq * 4 + r] : 0.f), a.act3);
-      }
-      *reinterpret_cast<float4*>(o + fq * 4) = make_float4(v0[0], v0[1], v0[2], v0[3]);
-      *reinterpret_cast<float4*>(o + 16 + fq * 4) = make_float4(v1[0], v1[1], v1[2], v1[3]);
-    }
-  }
-}
 }  // namespace
 
 // fp32 NCHW [B, 3, H, W] -> dst NHWC x 8 (layout 1) or space-to-depth [B, H/2, W/2, 16]
@@ -864,29 +625,5 @@ TCA_API int tca_yolo_stem_fused(const void* src, long src_batch_stride, int src_
   const long tiles = (long)batch * ((a.H1 + ty - 1) / ty) * ((a.W1 + 15) / 16);
   if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
   yolo_stem_fused_kernel<ty><<<(unsigned)tiles, 256, 0, stream>>>(a);
-  return (int)hipGetLastError();
-}
-
-// YOLOv5n's first C3 block fused (yolo_c3s_fused_kernel): x fp32 [B, H, W, ldx] (32 channels at
-// x_off) -> y fp32 [B, H, W, ldy] (32 channels at y_off).  Weights: the FusedConvs' split_pairs
-// images (cv1|cv2 merged [32, 64], m.cv1 [16, 64] (K 16 padded to 32), m.cv2 [16, 320], cv3 [32, 64]).
-TCA_API int tca_yolo_c3s_fused(const float* x, int B, int H, int W, int ldx, int x_off, const void* w12,
-                               const float* b12, int act12, const void* wm1, const float* bm1, int actm1,
-                               const void* wm2, const float* bm2, int actm2, const void* w3, const float* b3, int act3,
-                               int add, float* y, int ldy, int y_off, hipStream_t stream) {
-  if (B <= 0) return 0;
-  if ((ldx & 3) || (x_off & 3) || (ldy & 3) || (y_off & 3) || ldx < x_off + 32 || ldy < y_off + 32 || !w12 || !wm1 ||
-      !wm2 || !w3 || !x || !y)
-    return (int)hipErrorInvalidValue;
-  C3sArgs a;
-  a.x = x; a.y = y;
-  a.w12 = (const __hip_bfloat16*)w12; a.wm1 = (const __hip_bfloat16*)wm1; a.wm2 = (const __hip_bfloat16*)wm2;
-  a.w3 = (const __hip_bfloat16*)w3;
-  a.b12 = b12; a.bm1 = bm1; a.bm2 = bm2; a.b3 = b3;
-  a.act12 = act12; a.actm1 = actm1; a.actm2 = actm2; a.act3 = act3; a.add = add;
-  a.B = B; a.H = H; a.W = W; a.ldx = ldx; a.x_off = x_off; a.ldy = ldy; a.y_off = y_off;
-  const long tiles = (long)B * ((H + 15) / 16) * ((W + 15) / 16);
-  if (tiles >= (1L << 31)) return (int)hipErrorInvalidValue;
-  yolo_c3s_fused_kernel<<<(unsigned)tiles, 256, 0, stream>>>(a);
   return (int)hipGetLastError();
 }

@@ -54,31 +54,3 @@ def test_camera_step_fused_stem_same_detections(cuda, monkeypatch):
     for b in range(4):
         n = int(n1[b])
         assert torch.allclose(b1[b, :n], r2.box[b, :n], atol=1e-3)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("hw", [(160, 160), (40, 36), (23, 50)])
-def test_c3_fused_matches_chain(cuda, monkeypatch, hw):
-    """yolo_c3s_fused (YOLOv5n's first C3: cv1|cv2, bottleneck 1x1 + 3x3 + shortcut, cv3) against
-    the four-launch _C3Plan chain, partial tiles at the image edges included."""
-    import triton_client_amd.models.fast as fast
-
-    torch.manual_seed(hw[0])
-    cam = CameraPipeline(batch=2, src_hw=(64, 64), img_hw=(64, 64), device=cuda)
-    f = cam.build_fast()
-    B, (H, W) = 2, hw
-    plan = fast._C3Plan(cam.model.b2, B, H, W, fast._Buffers(cuda, "fp32"), cuda)
-    x = NHWC(torch.randn(B, H, W, 48, device=cuda), 8, 32)  # channel-offset input slice
-    out_f = NHWC(torch.full((B, H, W, 40), 7.0, device=cuda), 8, 32)
-    assert plan.fused_ok(x, out_f)
-    plan(x, out_f)
-    monkeypatch.setattr(fast, "C3_FUSED", False)
-    assert not plan.fused_ok(x, out_f)
-    out_u = NHWC(torch.full((B, H, W, 40), 7.0, device=cuda), 8, 32)
-    plan(x, out_u)
-    torch.cuda.synchronize()
-    got, want = out_f.t[..., 8:40].double(), out_u.t[..., 8:40].double()
-    assert (out_f.t[..., :8] == 7.0).all()
-    rel = ((got - want).norm() / want.norm()).item()
-    assert rel < 1e-6, rel
-    del f

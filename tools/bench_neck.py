@@ -1,6 +1,7 @@
-"""fp32 fused BEV neck + head (K15) tiling variants on the PointPillars KITTI
-shapes at the headline batch: pair-storage branch inputs (the LiDAR pipeline's
-form), µs per call and bit-identity across variants.
+"""fp32 fused BEV neck + head (K15) on the PointPillars KITTI shapes at the headline
+batch: pair-storage branch inputs (the LiDAR pipeline's form), µs per call.  (The
+tiling variants this tool compared were removed in round 4, after
+profiles/r4/neck_variants.jsonl; variant 0 is the one tiling.)
 
     python tools/bench_neck.py [batch] [variants,comma,separated]
 """
@@ -20,7 +21,7 @@ from triton_client_amd.ops.conv import NHWC, to_pairs  # noqa: E402
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
-    variants = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 3]
+    variants = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
     dev = torch.device("cuda")
     m = build_pointpillars(PointPillarsConfig())
     randomize_bn(m, 3)

@@ -70,7 +70,7 @@ def main():
     for name in ("maxpool_nhwc", "upsample2x_nhwc", "sppf_pools"):
         setattr(fast, name, getattr(convmod, name))
     fast._C3Plan.__call__ = timed(lambda self, x, out: ("c3", id(self), x.c, self.c_, x.shape[1], x.shape[2],
-                                                        self.fused_ok(x, out) or self.fused2_ok(x, out)),
+                                                        self.fused2_ok(x, out)),
                                             fast._C3Plan.__call__)
 
     B = a.batch

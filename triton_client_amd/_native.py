@@ -35,8 +35,6 @@ _KERNEL_SIGS = {
     "tca_image_preprocess": [P, L, I, I, I, I, I, P, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P],
     # src, batch stride, src_h, src_w, row stride, src_c, swap_rb, dst_h, dst_w, B, top, left, reg_h, reg_w, pad,
     # quantize, sc0-2, b0-2, w0, bias0, act0, w1, bias1, act1, out, ldo, co_off, stream
-    # x, B, H, W, ldx, x_off, w12, b12, act12, wm1, bm1, actm1, wm2, bm2, actm2, w3, b3, act3, add, y, ldy, y_off, stream
-    "tca_yolo_c3s_fused": [P, I, I, I, I, I, P, P, I, P, P, I, P, P, I, P, P, I, I, P, I, I, P],
     # ptrs[14], ints[24], stream (csrc/kernels/c3_fused.hip)
     "tca_c3_fused": [P, P, P],
     "tca_yolo_stem_fused": [P, L, I, I, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P, P, I, P, P, I, P, I,

@@ -30,8 +30,7 @@ from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 # fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
 STEM_FUSED = True
-# fused YOLOv5n first C3 block (_C3Plan.fused_ok) and the c3_fused.hip blocks (_C3Plan.fused2_ok);
-# False: the unfused chain (tests compare the two)
+# the c3_fused.hip C3 blocks (_C3Plan.fused2_ok); False: the unfused chain (tests compare the two)
 C3_FUSED = True
 FUSED_C3_WIDTHS = (16, 32, 64)  # c_ of the blocks c3_fused.hip takes
 
@@ -110,21 +109,6 @@ class _C3Plan:
                         [(frag_weights(b1.w_f32_gemm).to(dev), frag_weights(b2.w_f32_gemm).to(dev))
                          for b1, b2, _ in self.m])
 
-    def fused_ok(self, x: NHWC, out: NHWC) -> bool:
-        """yolo_c3s_fused (csrc/kernels/image.hip) takes this block: fp32, 32 -> 32 channels,
-        c_ = 16, one bottleneck (1x1 then 3x3), plain fp32 activations.  C3_FUSED False: unfused."""
-        if not (C3_FUSED and self.cv12 is not None and len(self.m) == 1 and self.c_ == 16):
-            return False
-        b1, b2, _ = self.m[0]
-        convs = (self.cv12, b1, b2, self.cv3)
-        return (all(c.precision == "fp32" and not c.transpose and c.act in (0, 1, 2, 3) for c in convs)
-                and self.cv12.cin_p == 32 and self.cv12.N == 32 and self.cv12.k == 1 and self.cv12.Kp == 32
-                and b1.cin_p == 16 and b1.N == 16 and b1.k == 1 and b1.Kp == 32
-                and b2.cin_p == 16 and b2.N == 16 and b2.k == 3 and b2.s == 1 and b2.p == 1 and b2.Kp == 160
-                and self.cv3.cin_p == 32 and self.cv3.N == 32 and self.cv3.k == 1 and self.cv3.Kp == 32
-                and not x.pair and not out.pair and x.c == 32 and out.c == 32 and x.t.dtype == torch.float32
-                and x.t.is_cuda)
-
     def fused2_ok(self, x: NHWC, out: NHWC) -> bool:
         """c3_fused.hip takes this block (c_ = 32 / 64 / 128, plain fp32 in and out)."""
         return (self._fw is not None and C3_FUSED and x.t.is_cuda and not x.pair and not out.pair
@@ -167,16 +151,6 @@ class _C3Plan:
         c_ = self.c_
         if self.fused2_ok(x, out):
             return self._fused2(x, out)
-        if self.fused_ok(x, out):
-            b1, b2, add = self.m[0]
-            B, H, W, _ = x.shape
-            _native.call("tca_yolo_c3s_fused", _native.ptr(x.t), B, H, W, x.t.shape[-1], x.off,
-                         _native.ptr(self.cv12.w_gemm), _native.ptr(self.cv12.b_gemm), self.cv12.act,
-                         _native.ptr(b1.w_gemm), _native.ptr(b1.b_gemm), b1.act, _native.ptr(b2.w_gemm),
-                         _native.ptr(b2.b_gemm), b2.act, _native.ptr(self.cv3.w_gemm), _native.ptr(self.cv3.b_gemm),
-                         self.cv3.act, int(bool(add)), _native.ptr(out.t), out.t.shape[-1], out.off,
-                         _native.stream_ptr(None))
-            return out
         if self.cv12 is not None:
             self.cv12(x, out=NHWC(self.cat.t, 0, 2 * c_))
             cur = NHWC(self.cat.t, 0, c_)

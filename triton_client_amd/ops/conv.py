@@ -106,7 +106,7 @@ PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73
 # kernel explicitly, 120 and 121-124 (hx3s2_launch tiles 1-4) the stride-2 one.
 HX3 = True
 HX3S2 = True
-HX3_TILES = (110, 111, 112, 113, 114, 115, 116, 117, 118)
+HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
 
 

@@ -75,8 +75,7 @@ class FusedNeckHead:
         if grid <= 0:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
-        # fp32 tiling variant (bev_neck.hip tca_bev_neck_head_x3v): 0 auto, 1 <8 waves, 3 stages>,
-        # 2 <4 waves, 2 stages, two workgroups per CU>, 3 <8 waves, 2 stages>
+        # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = the one measured-best tiling
         self.variant = 0
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
