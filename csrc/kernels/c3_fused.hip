@@ -1,7 +1,6 @@
 // YOLOv5 C3 blocks fused into LDS-resident kernels, fp32 mode (split-product MFMA), for the
-// blocks with c_ = 32 / 64 hidden channels (YOLOv5n: b4, b6, h13, h17, h20; the c_ = 16 block b2
-// is image.hip yolo_c3s_fused; the 20 x 20 c_ = 128 blocks measured faster unfused: one
-// workgroup of ~150 KiB LDS per CU over 320 tiles).  Reference block: C3 = cv3(cat(m(cv1(x)),
+// blocks with c_ = 16 / 32 / 64 hidden channels (YOLOv5n: b2, b4, b6, h13, h17, h20; the 20 x 20
+// c_ = 128 blocks measured faster unfused: one workgroup of ~150 KiB LDS per CU over 320 tiles).  Reference block: C3 = cv3(cat(m(cv1(x)),
 // cv2(x))) with m = n x Bottleneck(1x1, 3x3, + shortcut) (the YOLOv5 model the reference serves,
 // examples/YOLOv5/config.pbtxt).
 //
