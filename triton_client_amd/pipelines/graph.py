@@ -37,6 +37,14 @@ class GraphCaptureError(RuntimeError):
 
 
 _TL = threading.local()
+
+# Process-wide: one graph capture at a time, and no executor submitting work while one runs.  A
+# thread_local-mode capture lets other host threads keep calling HIP, but their device-wide
+# calls (synchronize, pinned host allocation and the caching allocators' event queries) interleaved
+# with another thread's capture were seen to stall two live drivers building their engines at
+# once (tests/test_live.py::test_live_drivers_publish_engine_results); serialising the capture
+# against the other threads' issue costs only host time at engine build.
+CAPTURE_LOCK = threading.RLock()
 _SPY_LOCK = threading.Lock()
 _SPY = {"installed": False}
 
@@ -166,6 +174,10 @@ class GraphRunner:
     def capture(self) -> None:
         if not self.enabled:
             return
+        with CAPTURE_LOCK:
+            self._capture()
+
+    def _capture(self) -> None:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

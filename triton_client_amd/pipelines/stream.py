@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from .graph import GraphRunner
+from .graph import CAPTURE_LOCK, GraphRunner
 
 
 def flatten_tensors(obj) -> List[torch.Tensor]:
@@ -137,13 +137,13 @@ class StreamExecutor:
         # capture every set now, over whatever the inputs hold: the eager warm-up
         # runs of a capture must not see (and, for an in-place annotator, modify)
         # a real batch
-        with torch.cuda.stream(self.compute):
+        with CAPTURE_LOCK, torch.cuda.stream(self.compute):
             for k, r in enumerate(self.runners):
                 if r.enabled:
                     r.capture()
                 else:
                     r()  # eager: one run allocates the stage buffers
-        self.compute.synchronize()
+            self.compute.synchronize()
 
     @property
     def sets(self) -> int:
@@ -184,7 +184,7 @@ class StreamExecutor:
         (e.g. the annotated frames of set k) into fresh pinned tensors, or
         into ``extras_dst[i]`` (page-locked host tensors, e.g. slots of the
         data-parallel host ring) where given."""
-        with self.lock:
+        with CAPTURE_LOCK, self.lock:  # (no submission while another thread captures)
             k = self.next
             self.next = (k + 1) % self.sets
             for ev in self.set_free[k]:  # set k's inputs / stage are still being read back
