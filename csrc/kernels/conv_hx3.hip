@@ -22,6 +22,12 @@ struct Hx3Args {
   int N, ldo, co_off, ldr, r_off;
   int act;  // 0 none, 1 relu, 2 silu, 3 leaky(0.1); | 16: act after the residual add
   const unsigned char* occ;  // stride 2 only: uint8 [B, H, W] input occupancy (0: read as zeros) or null
+  // stride 1 only, optional: uint8 [B, Ho, Wo] uniform depth (tca_bev_uniform_depth) and the pair
+  // storage [N] of this layer's output on a uniform pixel.  A tile whose in-image pixels all have
+  // depth >= uni_min is written from uni_val without running the K loop.
+  const unsigned char* uni;
+  const float* uni_val;
+  int uni_min;
 };
 
 constexpr unsigned kOutOfRange = 0x80000000u;  // buffer offset past any num_records (< 2^31): reads zeros
@@ -180,6 +186,27 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
   const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
   const int n0 = nt * BN;
+
+  if (a.uni) {
+    // uniform tile (every input it reads is the previous layer's constant vector, inside the
+    // image): the dense K loop would produce uni_val on every pixel, so store it directly
+    bool bad = false;
+    for (int ml = tid; ml < BM; ml += NT) {
+      const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
+      if (oy < a.Ho && ox < a.Wo) bad |= a.uni[((long)b * a.Ho + oy) * a.Wo + ox] < a.uni_min;
+    }
+    if (!__syncthreads_or(bad)) {
+      constexpr int Q = BN / 4;  // 16-B pieces per pixel
+      for (int id = tid; id < BM * Q; id += NT) {
+        const int ml = id / Q, q = id - (id / Q) * Q;
+        const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
+        if (oy >= a.Ho || ox >= a.Wo) continue;
+        const long o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n0 + q * 4;
+        *reinterpret_cast<uint4*>(a.out_f + o) = *reinterpret_cast<const uint4*>(a.uni_val + n0 + q * 4);
+      }
+      return;
+    }
+  }
 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
@@ -639,6 +666,7 @@ TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
   a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = nullptr;
+  a.uni = nullptr; a.uni_val = nullptr; a.uni_min = 0;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
@@ -657,8 +685,100 @@ TCA_API int tca_conv_hx3s2p(const float* in, int B, int H, int W, int Cin, int l
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
   a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = occ;
+  a.uni = nullptr; a.uni_val = nullptr; a.uni_min = 0;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
   return hx3s2_launch(a, tile, stream);
+}
+
+// tca_conv_hx3p with uniform-tile skipping (Hx3Args::uni): uni uint8 [B, H, W] uniform depth
+// (tca_bev_uniform_depth), uni_min the depth this layer's output needs to be the constant
+// uni_val (pair storage [N], the dense kernel's own output on such a pixel).  No residual.
+TCA_API int tca_conv_hx3p_uni(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
+                              const float* bias, int N, float* out, int ldo, int co_off, int act,
+                              const unsigned char* uni, int uni_min, const float* uni_val, int tile,
+                              hipStream_t stream) {
+  if (B <= 0) return 0;
+  if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
+  if (!uni || !uni_val || uni_min < 1) return (int)hipErrorInvalidValue;
+  Hx3Args a;
+  a.in_f = in; a.res_f = nullptr; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = nullptr;
+  a.uni = uni; a.uni_val = uni_val; a.uni_min = uni_min;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = H; a.Wo = W;
+  a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = 0; a.r_off = 0; a.act = act;
+  if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;
+  return hx3_launch(a, tile, stream);
+}
+
+// ---- uniform depth of a sparse BEV canvas behind a 3x3 stride-2 pad-1 conv.
+//
+// u(p) (output pixel p of that first conv, [Ho, Wo] = [(H + 1) / 2, (W + 1) / 2]): its 3 x 3
+// stride-2 input window holds no occupied canvas cell, so its accumulators are exactly 0 and it
+// holds act(bias), the same vector everywhere.  A following 3x3 stride-1 pad-1 conv maps a pixel
+// whose 9 neighbours are all inside the image and uniform to one constant again, and so on: the
+// j-th conv of the chain (the stride-2 one is j = 1) outputs its constant at p iff every pixel
+// within Chebyshev radius j - 1 of p is inside the image and has u.  depth(p) = the largest such
+// j, capped at maxd (0: p itself is not uniform).  One workgroup per 16 x 64 output tile: u of
+// the tile plus a (maxd - 1) halo into LDS, then a ring scan per pixel.
+namespace {
+
+constexpr int UD_TY = 16, UD_TX = 64, UD_MAXR = 7;
+
+__global__ void __launch_bounds__(256) bev_uniform_depth_kernel(const unsigned char* __restrict__ occ, int H, int W,
+                                                                 int Ho, int Wo, int maxd,
+                                                                 unsigned char* __restrict__ depth) {
+  constexpr int LY = UD_TY + 2 * UD_MAXR, LX = UD_TX + 2 * UD_MAXR;
+  __shared__ unsigned char u[LY * LX];
+  const int b = blockIdx.z, ty0 = blockIdx.y * UD_TY, tx0 = blockIdx.x * UD_TX;
+  const int R = maxd - 1;
+  const int ry = UD_TY + 2 * R, rx = UD_TX + 2 * R;
+  const unsigned char* oc = occ + (long)b * H * W;
+  for (int id = threadIdx.x; id < ry * rx; id += blockDim.x) {
+    const int ly = id / rx, lx = id - (id / rx) * rx;
+    const int Y = ty0 - R + ly, X = tx0 - R + lx;
+    unsigned char good = 0;
+    if (Y >= 0 && X >= 0 && Y < Ho && X < Wo) {
+      good = 1;
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int iy = 2 * Y + dy, ix = 2 * X + dx;
+          if (iy >= 0 && ix >= 0 && iy < H && ix < W && oc[(long)iy * W + ix]) good = 0;
+        }
+    }
+    u[ly * LX + lx] = good;
+  }
+  __syncthreads();
+  for (int id = threadIdx.x; id < UD_TY * UD_TX; id += blockDim.x) {
+    const int py = id / UD_TX, px = id - (id / UD_TX) * UD_TX;
+    const int Y = ty0 + py, X = tx0 + px;
+    if (Y >= Ho || X >= Wo) continue;
+    const int cy = py + R, cx = px + R;
+    int d = 0;
+    if (u[cy * LX + cx]) {
+      d = 1;
+      for (int k = 1; k <= R; ++k) {  // ring of radius k
+        bool ok = true;
+        for (int t = -k; t <= k && ok; ++t)
+          ok = u[(cy - k) * LX + cx + t] && u[(cy + k) * LX + cx + t] && u[(cy + t) * LX + cx - k] &&
+               u[(cy + t) * LX + cx + k];
+        if (!ok) break;
+        d = k + 1;
+      }
+    }
+    depth[((long)b * Ho + Y) * Wo + X] = (unsigned char)d;
+  }
+}
+
+}  // namespace
+
+// occ: uint8 [B, H, W] canvas occupancy; depth: uint8 [B, (H + 1) / 2, (W + 1) / 2]; 1 <= maxd <= 8.
+TCA_API int tca_bev_uniform_depth(const unsigned char* occ, int B, int H, int W, int maxd, unsigned char* depth,
+                                  hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (maxd < 1 || maxd > UD_MAXR + 1) return (int)hipErrorInvalidValue;
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  dim3 grid((unsigned)((Wo + UD_TX - 1) / UD_TX), (unsigned)((Ho + UD_TY - 1) / UD_TY), (unsigned)B);
+  bev_uniform_depth_kernel<<<grid, 256, 0, stream>>>(occ, H, W, Ho, Wo, maxd, depth);
+  TCA_LAUNCH_CHECK();
 }

@@ -30,6 +30,9 @@ from .common import ACT_NONE, ACT_RELU, ACT_SILU, ConvBNAct
 
 # fused K1 + YOLOv5 stem + b1 kernel for the frame-input camera step (FastYOLOv5.stem_fused_ok)
 STEM_FUSED = True
+# PointPillars first block: skip the tiles of the stride-1 convs whose receptive field is empty
+# canvas (_BEVBackbonePlan.forward_blocks; False: dense, for A/B runs)
+BEV_UNIFORM = True
 # the c3_fused.hip C3 blocks (_C3Plan.fused2_ok); False: the unfused chain (tests compare the two)
 C3_FUSED = True
 FUSED_C3_WIDTHS = (16, 32, 64)  # c_ of the blocks c3_fused.hip takes
@@ -348,13 +351,52 @@ class _BEVBackbonePlan:
             assert u.fused, "call fuse_model() first"
             self.ups.append((fc, off, c))
             off += c
+        self.ny, self.nx = ny, nx
+        self.uni_vals = self._uniform_values(device) if BEV_UNIFORM else None
+        self.depth = None
+        if self.uni_vals is not None:
+            _, _, H1, W1 = self.blocks[0]
+            self.depth = torch.zeros((B, H1, W1), dtype=torch.uint8, device=device)
+
+    def _uniform_eligible(self) -> bool:
+        convs = self.blocks[0][0]
+        return (self.pair and len(convs) >= 2 and convs[0].s == 2 and convs[0].hx3_ok()
+                and all(c.s == 1 and c.hx3_ok() for c in convs[1:]) and len(convs) <= 8)
+
+    @torch.no_grad()
+    def _uniform_values(self, device) -> Optional[List[torch.Tensor]]:
+        """Pair storage of each first-block conv's output on a uniform pixel (see conv_hx3.hip
+        tca_bev_uniform_depth): one image of the canvas shape with nothing occupied, run through
+        the same kernels (same tile choice: the shapes match), and read at the centre.  Built
+        here, outside any graph capture; the plan's weights are fixed from here on."""
+        if not self._uniform_eligible() or torch.cuda.is_current_stream_capturing():
+            return None
+        convs = self.blocks[0][0]
+        x = NHWC(torch.zeros((1, self.ny, self.nx, convs[0].cin_p), dtype=torch.float32, device=device), pair=True,
+                 occ=torch.zeros((1, self.ny, self.nx), dtype=torch.uint8, device=device))
+        vals = []
+        for cv in convs:
+            Ho, Wo = cv.out_hw(x.t.shape[1], x.t.shape[2])
+            x = cv(x, out=NHWC(torch.zeros((1, Ho, Wo, cv.N), dtype=torch.float32, device=device), pair=True))
+            vals.append(x.t[0, Ho // 2, Wo // 2].clone())
+        torch.cuda.synchronize(device)
+        return vals
 
     def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
-        """The down blocks only: each block's output (the deblocks' inputs)."""
+        """The down blocks only: each block's output (the deblocks' inputs).  With the canvas
+        occupancy, the first block's stride-1 convs store their constant on the tiles whose
+        receptive field holds no occupied cell (tca_bev_uniform_depth); bit-identical."""
         x, outs = canvas, []
-        for convs, pp, H, W in self.blocks:
+        uni = self.uni_vals is not None and canvas.occ is not None and BEV_UNIFORM
+        if uni:
+            B, ny, nx = canvas.occ.shape
+            assert (ny, nx) == (self.ny, self.nx) and B == self.depth.shape[0], (canvas.occ.shape, self.depth.shape)
+            _native.call("tca_bev_uniform_depth", _native.ptr(canvas.occ), B, ny, nx, len(self.blocks[0][0]),
+                         _native.ptr(self.depth), _native.stream_ptr(None))
+        for bi, (convs, pp, H, W) in enumerate(self.blocks):
             for i, cv in enumerate(convs):
-                x = cv(x, out=pp[i % 2])
+                u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 and i > 0 else None
+                x = cv(x, out=pp[i % 2], uni=u)
             outs.append(x)
         return outs
 

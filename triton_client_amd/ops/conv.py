@@ -222,7 +222,10 @@ class FusedConv:
         return self.cout_real if self.transpose else self.N
 
     def __call__(self, x: NHWC, out: Optional[NHWC] = None, res: Optional[NHWC] = None, tile: int = 0,
-                 stream=None) -> NHWC:
+                 stream=None, uni=None) -> NHWC:
+        """uni: optional (depth uint8 [B, Ho, Wo], min depth, pair value [N]) — hx3 tiles whose
+        pixels all reach the depth store the value instead of computing it (conv_hx3.hip
+        tca_conv_hx3p_uni; see _BEVBackbonePlan)."""
         B, H, W, C = x.shape
         Ho, Wo = self.out_hw(H, W)
         if out is None:
@@ -252,6 +255,16 @@ class FusedConv:
                 return out
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
+                if uni is not None and res is None:
+                    depth, dmin, val = uni
+                    assert depth.dtype == torch.uint8 and tuple(depth.shape) == (B, Ho, Wo), depth.shape
+                    assert val.dtype == torch.float32 and val.numel() == self.N, (val.dtype, val.shape)
+                    _native.call("tca_conv_hx3p_uni", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                                 _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
+                                 _native.ptr(out.t), out.t.shape[-1], out.off, act, _native.ptr(depth), dmin,
+                                 _native.ptr(val), tile - 110 if tile in HX3_TILES else 0,
+                                 _native.stream_ptr(stream))
+                    return out
                 _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp,
