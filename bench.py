@@ -70,6 +70,9 @@ def parse():
                     help="DP scatter/gather: the C++ RCCL communicator (default) or torch batch_isend_irecv")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-prefetch", action="store_true", help="serial H2D ingest (no copy-stream prefetch)")
+    ap.add_argument("--unfused-detect", action="store_true",
+                    help="YOLOv5 Detect convs + tca_yolo_decode_filter instead of the fused kernel "
+                         "(models/fast.py DETECT_FUSED; A/B)")
     ap.add_argument("--dense-bev", action="store_true",
                     help="PointPillars first block without uniform-tile skipping (models/fast.py BEV_UNIFORM; A/B)")
     ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3],
@@ -189,9 +192,11 @@ def main():
         raise SystemExit("bench.py needs a GPU")
     from triton_client_amd.pipelines import CameraPipeline, GraphRunner, LidarPipeline
     from triton_client_amd.utils.synthetic import LidarSpec, camera_frame, lidar_sweep
+    import triton_client_amd.models.fast as fast_plans
     if args.dense_bev:
-        import triton_client_amd.models.fast as fast_plans
         fast_plans.BEV_UNIFORM = False
+    if args.unfused_detect:
+        fast_plans.DETECT_FUSED = False
 
     B = args.batch
     H0, W0 = (int(v) for v in args.cam.split("x"))

@@ -11,7 +11,7 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
             "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   rm -rf /tmp/pmc$i
-  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/pmc$i -o run -- python $CMD > gpurun_out/pmc/${TAG}_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/${TAG}_p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d /tmp/pmc$i -o run -- python $CMD > gpurun_out/pmc/${TAG}_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/${TAG}_p$i.log; exit 1; }
   f=$(find /tmp/pmc$i -name "*counter_collection.csv" | head -1)
   cp $f gpurun_out/pmc/${TAG}_p$i.csv
 done

@@ -39,6 +39,9 @@ _KERNEL_SIGS = {
     "tca_c3_fused": [P, P, P],
     "tca_yolo_stem_fused": [P, L, I, I, I, I, I, I, I, I, I, I, I, I, F, I, F, F, F, F, F, F, P, P, I, P, P, I, P, I,
                             I, P],
+    # x[3], ldx[3], x_off[3], cin[3], hw[6], w[3], bias[3], strides[3], anchors, B, na, nc, conf, class_mask,
+    # cand box, score, cls, key, count, cap, stream
+    "tca_yolo_detect_filter": [P, P, P, P, P, P, P, P, P, I, I, I, F, P, P, P, P, P, P, I, P],
     "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
     "tca_topk_sort": [P, P, I, I, I, P, P, P],
     "tca_nms_mask": [I, P, I, P, P, P, I, I, I, F, I, P, I, P],

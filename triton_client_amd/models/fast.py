@@ -33,6 +33,8 @@ STEM_FUSED = True
 # PointPillars first block: skip the tiles of the stride-1 convs whose receptive field is empty
 # canvas (_BEVBackbonePlan.forward_blocks; False: dense, for A/B runs)
 BEV_UNIFORM = True
+# YOLOv5 Detect convs fused with the decode + candidate filter (FastYOLOv5.detect_fused_ok)
+DETECT_FUSED = True
 # the c3_fused.hip C3 blocks (_C3Plan.fused2_ok); False: the unfused chain (tests compare the two)
 C3_FUSED = True
 FUSED_C3_WIDTHS = (16, 32, 64)  # c_ of the blocks c3_fused.hip takes
@@ -283,8 +285,20 @@ class FastYOLOv5:
             self.x.t.zero_()
             self.x.t[..., :3].copy_(x.permute(0, 2, 3, 1))
 
-    def forward(self, from_t1: bool = False) -> List[NHWC]:
-        """from_t1: b1's output is already in ``t1`` (the fused K1 + stem + b1 kernel ran)."""
+    def detect_fused_ok(self) -> bool:
+        """The fused Detect convs + decode + filter kernel (ops/yolo.py YoloPostprocess.detect_fused,
+        yolo_detect.hip) takes this plan's head: fp32, 1x1 stride-1 convs without activation over
+        fp32 NHWC inputs with cin in {64, 128, 256}, 256 output rows.  DETECT_FUSED False keeps the
+        convs + tca_yolo_decode_filter."""
+        return (DETECT_FUSED and self.precision == "fp32" and self.device.type == "cuda"
+                and all(d.k == 1 and d.s == 1 and d.p == 0 and not d.transpose and d.act == ACT_NONE
+                        and d.cin_p in (64, 128, 256) and d.K == d.Kp and d.N == 256
+                        and d.w_gemm.shape == (256, 2 * d.cin_p) and o.c == d.cin_p and not o.pair
+                        for d, o in zip(self.det, (self.o3, self.o4, self.o5))))
+
+    def forward(self, from_t1: bool = False, heads: bool = True) -> List[NHWC]:
+        """from_t1: b1's output is already in ``t1`` (the fused K1 + stem + b1 kernel ran).
+        heads False: stop before the Detect convs and return their inputs (o3, o4, o5)."""
         if from_t1:
             t = self.t1
         else:
@@ -311,6 +325,8 @@ class FastYOLOv5:
         o4 = self.c3_20(self.cat20, out=self.o4)
         self.h21(o4, out=NHWC(self.cat23.t, 0, self.h21.N))
         o5 = self.c3_23(self.cat23, out=self.o5)
+        if not heads:
+            return [o3, o4, o5]
         outs = []
         for d, o, dst in zip(self.det, (o3, o4, o5), self.dout):
             d(o, out=dst)

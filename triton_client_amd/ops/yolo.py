@@ -84,6 +84,43 @@ class YoloPostprocess:
             res = self._merge(cand, res, xf, stream)
         return (res, decoded) if decoded_out else res
 
+    def detect_fused_ok(self, plan) -> bool:
+        """The plan's Detect convs can run fused with this filter (single-label, head width
+        na * (5 + nc) <= 256)."""
+        return (not self.multi_label and self.na * (self.nc + 5) <= 256 and self.na <= 4
+                and self.device.type == "cuda" and plan.detect_fused_ok() and plan.no_real == self.na * (self.nc + 5))
+
+    def detect_fused(self, plan, feats, xform: Optional[FrameXform] = None, stream=None):
+        """Detect convs + decode + filter in one kernel (yolo_detect.hip) from the head inputs
+        ``feats`` (plan.forward(heads=False)), then sort / NMS as :meth:`__call__`.  The logits
+        are bit-identical to the plan's convs, so the candidates are those of the unfused path."""
+        B = feats[0].t.shape[0]
+        cap = min(self.num_anchors_total, 1 << 20)
+        cand = Candidates.alloc(self.ws, "yolo_", B, cap, 4)
+        args = getattr(plan, "_detect_args", None)
+        if args is None:
+            P = ctypes.c_void_p
+            args = plan._detect_args = dict(
+                x=(P * 3)(*[_native.ptr(o.t) + o.off * o.t.element_size() for o in feats]),
+                ldx=(ctypes.c_int * 3)(*[o.t.shape[-1] for o in feats]),
+                xoff=(ctypes.c_int * 3)(0, 0, 0),
+                cin=(ctypes.c_int * 3)(*[d.cin_p for d in plan.det]),
+                w=(P * 3)(*[_native.ptr(d.w_gemm) for d in plan.det]),
+                b=(P * 3)(*[_native.ptr(d.b_gemm) for d in plan.det]),
+                key=tuple(_native.ptr(o.t) + o.off * o.t.element_size() for o in feats))
+        assert args["key"] == tuple(_native.ptr(o.t) + o.off * o.t.element_size() for o in feats)
+        _native.call("tca_yolo_detect_filter", ctypes.addressof(args["x"]), args["ldx"], args["xoff"], args["cin"],
+                     self.hw, ctypes.addressof(args["w"]), ctypes.addressof(args["b"]), self.strides, self.anc, B,
+                     self.na, self.nc, float(self.conf_thres), _native.ptr(self._class_mask), _native.ptr(cand.box),
+                     _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count),
+                     cap, _native.stream_ptr(stream))
+        xf = xform.as_list() if xform is not None else None
+        res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
+                           None if self.merge else xf, prefix="yolo_nms_", stream=stream)
+        if self.merge:
+            res = self._merge(cand, res, xf, stream)
+        return res
+
     def _merge(self, cand, kept: NmsResult, xf, stream=None) -> NmsResult:
         B, md = kept.score.shape
         out = NmsResult(self.ws.get("yolo_merge_box", (B, md, 4), torch.float32),

@@ -104,6 +104,8 @@ class CameraPipeline:
             f = self.fast or self.build_fast()
             if f.stem_fused_ok():  # one kernel: frames -> b1's output
                 yolo_stem_fused(self.frames, self.img_hw, self.mode, f.b0, f.b1, f.t1, "COCO", swap_rb=self.swap_rb)
+                if self.post.detect_fused_ok(f):  # one kernel: head inputs -> candidates
+                    return self.post.detect_fused(f, f.forward(from_t1=True, heads=False), self.xform)
                 return self.post(f.forward(from_t1=True), self.xform)
             if f.s2d:
                 preprocess(self.frames, self.img_hw, self.mode, "COCO", f.x.t.dtype, "S2D",
@@ -111,6 +113,8 @@ class CameraPipeline:
             else:
                 preprocess(self.frames, self.img_hw, self.mode, "COCO", f.x.t.dtype, "NHWC", f.IN_CHANNELS,
                            swap_rb=self.swap_rb, out=f.x.t.permute(0, 3, 1, 2))
+            if self.post.detect_fused_ok(f):
+                return self.post.detect_fused(f, f.forward(heads=False), self.xform)
             return self.post(f.forward(), self.xform)
         preprocess(self.frames, self.img_hw, self.mode, "COCO", self.dtype, "NHWC", 3, swap_rb=self.swap_rb,
                    out=self.inp)
