@@ -158,3 +158,34 @@ def test_hx3s2_occupancy_reads_unmarked_pixels_as_zero(cuda, tile):
     ref = torch.relu(conv((xin * occ[..., None].double()).permute(0, 3, 1, 2)))
     assert rel_l2(out.nchw(), ref) < 5e-5, rel_l2(out.nchw(), ref)
     assert rel_l2(dflt.nchw(), ref) < 5e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [120, 123, 124])
+@pytest.mark.parametrize("pattern", ["random", "arcs"])
+def test_hx3s2_occupancy_skips_are_exact(cuda, tile, pattern):
+    """Occupancy-gated stride-2 conv (empty tiles and empty line fragments skipped) against the
+    same kernel reading the zero-masked input without occupancy: bit-identical."""
+    torch.manual_seed(12)
+    B, H, W, cin, cout = 2, 96, 80, 64, 64
+    conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True)
+    fc = FusedConv(conv, act=1, device=cuda, precision="fp32")
+    if pattern == "random":
+        occ = (torch.rand(B, H, W) < 0.08).to(torch.uint8)
+    else:  # thin rings around a corner, like a LiDAR's ground returns: most line fragments empty
+        yy, xx = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+        r = ((yy - 5.0) ** 2 + (xx + 3.0) ** 2).sqrt()
+        occ = ((r % 23.0) < 1.2).to(torch.uint8).expand(B, H, W).contiguous()
+        occ[1, 40:, :] = 0
+    xin = torch.randn(B, H, W, cin) * occ[..., None]
+    stored = torch.where(occ.bool()[..., None], xin, torch.full_like(xin, 3e4))
+    x_occ = NHWC(to_pairs(stored).to(cuda), pair=True, occ=occ.to(cuda))
+    x_dense = NHWC(to_pairs(xin).to(cuda), pair=True)
+    Ho, Wo = fc.out_hw(H, W)
+    outs = []
+    for x in (x_occ, x_dense):
+        o = NHWC(torch.full((B, Ho, Wo, cout), float("nan"), device=cuda), pair=True)
+        fc(x, out=o, tile=tile)
+        outs.append(o.t)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
