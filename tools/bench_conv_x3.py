@@ -41,6 +41,14 @@ SHAPES = [
     ("y.c3c.1x1", B, 40, 40, 128, 64, 1, 1, 2),
     ("y.c3c.3x3", B, 40, 40, 64, 64, 3, 1, 2),
     ("y.b7", B, 40, 40, 128, 256, 3, 2, 2),
+    # the c_ = 128 C3 blocks (b8 / h23, unfused) and the SPPF / neck 1x1s at 20 x 20, the PAN downsamples
+    ("y.c3d.cv12", B, 20, 20, 256, 256, 1, 1, 2),
+    ("y.c3d.m1", B, 20, 20, 128, 128, 1, 1, 2),
+    ("y.c3d.m2", B, 20, 20, 128, 128, 3, 1, 2),
+    ("y.sp1", B, 20, 20, 256, 128, 1, 1, 2),
+    ("y.sp2", B, 20, 20, 512, 256, 1, 1, 2),
+    ("y.h19", B, 80, 80, 64, 64, 3, 2, 2),
+    ("y.h22", B, 40, 40, 128, 128, 3, 2, 2),
     # Detect heads (1x1, 255 -> 256 outputs, no activation): short K, output-write bound
     ("y.det80", B, 80, 80, 64, 256, 1, 1, 0),
     ("y.det40", B, 40, 40, 128, 256, 1, 1, 0),
