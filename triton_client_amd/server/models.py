@@ -63,7 +63,7 @@ def _device(device) -> torch.device:
     return torch.device(device)
 
 
-PLAN_SIZES = (1, 4, 8, 16)  # captured batch sizes per served model; a dynamic batch runs on the smallest >= n
+PLAN_SIZES = (1, 2, 4, 6, 8, 12, 16)  # captured batch sizes per served model; a dynamic batch runs on the smallest >= n
 
 
 def _direct(a, dtype) -> Optional[torch.Tensor]:
