@@ -185,6 +185,119 @@ TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const v
 }
 
 // ============================================================================
+// K3 on a *decoded* prediction — the remote client's postprocess
+// (reference clients/postprocess/yolov5_postprocess.py:36-92 applied to the
+// ModelInfer response, communicator/ros_inference.py:148).  The server's output
+// lands in device memory by one H2D of the response bytes and is filtered here;
+// candidates feed the same sort + bitmask NMS as the local pipeline.
+//   kind 0 (YOLOv5 ONNX): pred [B, N, ld] rows (cx, cy, w, h, obj, cls[nc]) in
+//          model-input pixels; obj > t, then best (cls * obj) > t, or every
+//          class with cls * obj > t (multi_label); tie key = row (* nc + class).
+//   kind 1 (YOLOv4 ONNX, examples/YOLOv4/config.pbtxt): boxes [B, N, 4]
+//          normalised x1y1x2y2 (pred) + confs [B, N, nc] (conf); best conf > t
+//          (tools/utils.py:166-233), boxes scaled to img_w x img_h.
+// One thread per row: the row's first gate is one load (obj, kind 0), the
+// class scan only runs for rows that pass it.  The products are fp32 like the
+// reference's NumPy float32 ``x[:, 5:] *= x[:, 4:5]``, so the kept sets match.
+// ============================================================================
+namespace {
+
+__global__ void __launch_bounds__(256) yolo_filter_decoded_kernel(
+    const float* __restrict__ pred, const float* __restrict__ confs, int kind, int N, int ld, int nc,
+    float conf_thres, int multi_label, const uint32_t* __restrict__ class_mask, float img_w, float img_h,
+    float* __restrict__ cand_box, float* __restrict__ cand_score, int* __restrict__ cand_cls,
+    uint64_t* __restrict__ cand_key, int* __restrict__ cand_count, int cap) {
+  __shared__ int s_cnt, s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  bool pass = false;
+  float box[4] = {0.f, 0.f, 0.f, 0.f}, best = 0.f;
+  int best_c = 0;
+  if (r < N) {
+    if (kind == 0) {
+      const float* row = pred + ((long)b * N + r) * ld;
+      const float obj = row[4];
+      if (obj > conf_thres) {
+        const float cx = row[0], cy = row[1], hw = row[2] * 0.5f, hh = row[3] * 0.5f;
+        box[0] = cx - hw; box[1] = cy - hh; box[2] = cx + hw; box[3] = cy + hh;
+        if (!multi_label) {
+          float m = -INFINITY;
+          for (int c = 0; c < nc; ++c) {
+            if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+            const float v = row[5 + c] * obj;
+            if (v > m) { m = v; best_c = c; }
+          }
+          best = m;
+          pass = m > conf_thres;
+        } else {
+          for (int c = 0; c < nc; ++c) {
+            if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+            const float s = row[5 + c] * obj;
+            if (s > conf_thres) {
+              const int slot = atomicAdd(&cand_count[b], 1);
+              if (slot < cap) {
+                const long o = (long)b * cap + slot;
+                cand_box[o * 4 + 0] = box[0]; cand_box[o * 4 + 1] = box[1];
+                cand_box[o * 4 + 2] = box[2]; cand_box[o * 4 + 3] = box[3];
+                cand_score[o] = s; cand_cls[o] = c; cand_key[o] = make_score_key(s, (uint32_t)(r * nc + c));
+              }
+            }
+          }
+        }
+      }
+    } else {
+      const float* cf = confs + ((long)b * N + r) * nc;
+      float m = -INFINITY;
+      for (int c = 0; c < nc; ++c) {
+        const float v = cf[c];
+        if (v > m) { m = v; best_c = c; }
+      }
+      if (m > conf_thres) {
+        const float* bx = pred + ((long)b * N + r) * 4;
+        box[0] = bx[0] * img_w; box[1] = bx[1] * img_h; box[2] = bx[2] * img_w; box[3] = bx[3] * img_h;
+        best = m;
+        pass = true;
+      }
+    }
+  }
+  if (multi_label && kind == 0) return;  // compacted above, one atomic per candidate
+  int my = -1;
+  if (pass) my = atomicAdd(&s_cnt, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&cand_count[b], s_cnt) : 0;
+  __syncthreads();
+  if (pass) {
+    const int slot = s_base + my;
+    if (slot < cap) {
+      const long o = (long)b * cap + slot;
+      cand_box[o * 4 + 0] = box[0]; cand_box[o * 4 + 1] = box[1];
+      cand_box[o * 4 + 2] = box[2]; cand_box[o * 4 + 3] = box[3];
+      cand_score[o] = best; cand_cls[o] = best_c; cand_key[o] = make_score_key(best, (uint32_t)r);
+    }
+  }
+}
+
+}  // namespace
+
+TCA_API int tca_yolo_filter_decoded(const float* pred, const float* confs, int kind, int batch, int N, int ld, int nc,
+                                    float conf_thres, int multi_label, const uint32_t* class_mask, float img_w,
+                                    float img_h, float* cand_box, float* cand_score, int* cand_cls, uint64_t* cand_key,
+                                    int* cand_count, int cap, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (N <= 0 || nc <= 0 || (kind == 0 && ld < nc + 5) || (kind == 1 && confs == nullptr) || kind < 0 || kind > 1)
+    return (int)hipErrorInvalidValue;
+  int e = zero_i32_async(cand_count, batch, stream);
+  if (e) return e;
+  dim3 grid((unsigned)((N + 255) / 256), (unsigned)batch);
+  yolo_filter_decoded_kernel<<<grid, 256, 0, stream>>>(pred, confs, kind, N, ld, nc, conf_thres, multi_label,
+                                                       class_mask, img_w, img_h, cand_box, cand_score, cand_cls,
+                                                       cand_key, cand_count, cap);
+  TCA_LAUNCH_CHECK();
+}
+
+// ============================================================================
 // K5 — YOLOv4 head decode (reference tools/yolo_layer.py:148-288,
 // yolo_forward_dynamic) fused with the post-processing filter
 // (tools/utils.py:166-233: max/argmax over conf = sigmoid(cls) * sigmoid(obj),

@@ -76,38 +76,103 @@ def test_host_ring_cross_process():
     assert not os.path.exists(ring.ctl_path) and not os.path.exists(ring.data_path(1))
 
 
+def _fake_sysfs(tmp_path, devices, kfd_nodes=()):
+    pci = tmp_path / "pci"
+    for bdf, vendor, cls, cpus, node in devices:
+        d = pci / bdf
+        d.mkdir(parents=True)
+        (d / "vendor").write_text(vendor + "\n")
+        (d / "class").write_text(cls + "\n")
+        (d / "local_cpulist").write_text(cpus + "\n")
+        (d / "numa_node").write_text(f"{node}\n")
+    kfd = tmp_path / "kfd"
+    kfd.mkdir()
+    for i, props in enumerate(kfd_nodes):
+        n = kfd / str(i)
+        n.mkdir()
+        (n / "properties").write_text("".join(f"{k} {v}\n" for k, v in props.items()))
+    return str(pci), str(kfd)
+
+
 def test_numa_binding_from_sysfs(tmp_path, monkeypatch):
     from triton_client_amd.parallel import numa
 
     assert numa.parse_cpulist("0-3,8,10-11") == {0, 1, 2, 3, 8, 10, 11}
-    for bdf, vendor, cls, cpus in (("0000:05:00.0", "0x1002", "0x038000", "0-1"),
-                                   ("0000:15:00.0", "0x1002", "0x038000", "2-3"),
-                                   ("0000:16:00.0", "0x8086", "0x038000", "4-5"),   # not AMD
-                                   ("0000:17:00.0", "0x1002", "0x020000", "6-7")):  # not a GPU
-        d = tmp_path / bdf
-        d.mkdir()
-        (d / "vendor").write_text(vendor + "\n")
-        (d / "class").write_text(cls + "\n")
-        (d / "local_cpulist").write_text(cpus + "\n")
-    root = str(tmp_path)
-    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
-    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
-    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
-    assert [os.path.basename(d) for d in numa.amd_gpus(root)] == ["0000:05:00.0", "0000:15:00.0"]
-    assert numa.gpu_cpus(1, root) == {2, 3}
+    root, kfd = _fake_sysfs(tmp_path, (
+        ("0000:05:00.0", "0x1002", "0x038000", "0-1", 0),
+        ("0000:15:00.0", "0x1002", "0x120000", "2-3", 1),   # Instinct: processing accelerator
+        ("0000:16:00.0", "0x8086", "0x038000", "4-5", 0),   # not AMD
+        ("0000:17:00.0", "0x1002", "0x020000", "6-7", 0)))  # not a GPU
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    # no KFD topology: PCI class order
+    assert [os.path.basename(d) for d in numa.gpu_devices(root, kfd)] == ["0000:05:00.0", "0000:15:00.0"]
+    assert numa.gpu_cpus(1, root, kfd) == {2, 3}
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
-    assert numa.gpu_cpus(0, root) == {2, 3}
-    before = os.sched_getaffinity(0)
-    try:
-        got = numa.bind_to_gpu(0, root)
-        want = {2, 3} & before
-        assert got == (want if want and want != before else None)
-        if got:
-            assert os.sched_getaffinity(0) == want
-    finally:
-        os.sched_setaffinity(0, before)
+    assert numa.gpu_cpus(0, root, kfd) == {2, 3}
+    info = numa.describe(0, root, kfd)
+    assert info["gpu_pci"] == "0000:15:00.0" and info["numa_node"] == 1 and info["local_cpus"] == 2
     monkeypatch.setenv("TCA_NUMA_BIND", "0")
-    assert numa.bind_to_gpu(0, root) is None
+    assert numa.bind_to_gpu(0, root, kfd) is None
+
+
+def test_numa_kfd_topology_order(tmp_path, monkeypatch):
+    """KFD GPU nodes (simd_count > 0) name the PCI functions in HSA agent order, which
+    need not be bus order; CPU nodes are skipped."""
+    from triton_client_amd.parallel import numa
+
+    root, kfd = _fake_sysfs(tmp_path, (
+        ("0000:05:00.0", "0x1002", "0x120000", "0-1", 0),
+        ("0000:85:00.0", "0x1002", "0x120000", "2-3", 1)),
+        kfd_nodes=({"cpu_cores_count": 64, "simd_count": 0},
+                   {"simd_count": 1024, "location_id": 0x8500, "domain": 0},
+                   {"simd_count": 1024, "location_id": 0x0500, "domain": 0}))
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert [os.path.basename(d) for d in numa.gpu_devices(root, kfd)] == ["0000:85:00.0", "0000:05:00.0"]
+    assert numa.gpu_cpus(0, root, kfd) == {2, 3}
+
+
+_BIND_CHILD = r"""
+import os, sys, threading, json
+from triton_client_amd.parallel import numa
+root, kfd = sys.argv[1], sys.argv[2]
+seen = {}
+go, done = threading.Event(), threading.Event()
+def early():
+    go.wait()
+    seen["early"] = sorted(os.sched_getaffinity(0))
+    done.set()
+t = threading.Thread(target=early)
+t.start()                      # started before the binding
+before = sorted(os.sched_getaffinity(0))
+got = numa.bind_to_gpu(0, root, kfd)
+go.set(); done.wait(10); t.join()
+print(json.dumps({"before": before, "got": sorted(got) if got else None, "main": sorted(os.sched_getaffinity(0)),
+                  "early": seen["early"]}))
+"""
+
+
+def test_numa_binding_covers_existing_threads(tmp_path):
+    """bind_to_gpu binds every thread of the process, including one started earlier
+    (run in a child process so the test runner keeps its CPU set)."""
+    import json
+    import subprocess
+    import sys
+
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 2:
+        pytest.skip("needs 2 CPUs")
+    local = f"{cpus[0]}"
+    root, kfd = _fake_sysfs(tmp_path, (("0000:05:00.0", "0x1002", "0x120000", local, 0),))
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
+                                                           "CUDA_VISIBLE_DEVICES", "TCA_NUMA_BIND")}
+    env["PYTHONPATH"] = ROOT
+    out = subprocess.run([sys.executable, "-c", _BIND_CHILD, root, kfd], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["got"] == [cpus[0]] and r["main"] == [cpus[0]] and r["early"] == [cpus[0]], r
 
 
 # ------------------------------------------------------------------ bag replays, 1 rank vs 2 ranks
@@ -256,3 +321,87 @@ def test_dp_camera_jpeg_annotated_two_ranks(cuda):
             p.kill()
     # 7 frames, batch 3 per rank: steps of 6 (3 + 3) and 1 (rank 0 alone), twice
     assert res == {0: "ok", 1: "served 2"}, res
+
+
+# ------------------------------------------------------------------ slot reuse vs a slow non-participant
+class _NullEngine:
+    names = []
+
+    def detect(self, frames):
+        return [np.zeros((0, 6), np.float32) for _ in frames]
+
+
+def _slow_peer_worker(rank, world, port, q, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TCA_NUMA_BIND="0")
+    try:
+        import time
+
+        from triton_client_amd.parallel.dp import init_distributed
+        from triton_client_amd.parallel.ring_dp import DataParallelDetector2D
+        from triton_client_amd.ros import compat, msgs
+
+        info = init_distributed("gloo")
+        dp = DataParallelDetector2D(_NullEngine(), info, nslots=3)
+        if info.is_main:
+            frame = np.zeros((8, 8, 3), np.uint8)
+            for i in range(steps):  # one message per step: rank 0 is the only participant
+                m = compat.numpy_to_imgmsg(frame, "rgb8", header=msgs.Header(seq=i))
+                assert len(dp.process([m], draw=False)) == 1
+            dp.close()
+            q.put((0, dp.steps))
+        else:
+            orig = dp.ring.wait_ready
+
+            def slow(s, seq, timeout_ms):  # a peer that reads every header late
+                time.sleep(0.02)
+                return orig(s, seq, timeout_ms)
+            dp.ring.wait_ready = slow
+            q.put((rank, dp.serve()))
+            dp.ring.close()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_ring_slot_reuse_waits_for_slow_non_participant():
+    """Single-message steps have only rank 0 as participant, but every peer reads every
+    slot header: rank 0 must not rewrite a slot a slow peer has not acked yet (it would
+    read a newer header and end its serve loop with a RingStepError)."""
+    _runtime_or_skip()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    steps = 15
+    procs = [ctx.Process(target=_slow_peer_worker, args=(r, 2, port, q, steps)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert res == {0: steps, 1: 0}, res
+
+
+def test_ring_data_area_reserved_or_clear_error(monkeypatch):
+    """Ring files are fully backed when created (no SIGBUS later on a full /dev/shm);
+    when /dev/shm cannot hold one, creation fails with RingSpaceError and leaves no file."""
+    import errno
+
+    from triton_client_amd.parallel import host_ring
+
+    name = f"tca_test_space_{os.getpid()}"
+    ring = host_ring.HostRing(name, nslots=2, world=1, create=True, pin=False)
+    try:
+        d = ring.new_generation(1 << 20)
+        assert os.stat(d.path).st_blocks * 512 >= 2 << 20  # allocated, not sparse
+        def full(fd, off, size):
+            raise OSError(errno.ENOSPC, "No space left on device")
+        monkeypatch.setattr(host_ring.os, "posix_fallocate", full)
+        with pytest.raises(host_ring.RingSpaceError, match="shm-size"):
+            ring.new_generation(4 << 20)
+        assert not os.path.exists(ring.data_path(ring.gen + 1)) and ring.data is d and os.path.exists(d.path)
+    finally:
+        monkeypatch.undo()
+        ring.close()

@@ -312,3 +312,61 @@ def test_live_drivers_publish_engine_results(cuda):
         idx = select_boxes(r, (2,), 0.5)
         np.testing.assert_array_equal(m.boxes.columns["value"], r["pred_scores"][idx])
         np.testing.assert_array_equal(m.boxes.columns["position"], r["pred_boxes"][idx, :3].astype(np.float64))
+
+
+@pytest.mark.gpu
+def test_engines_build_while_another_streams(cuda):
+    """Two live camera engines of new geometries build (pipeline, warm-ups, two graph
+    captures each) while a third streams: the streaming engine's submissions keep
+    completing during the builds -- only the capture windows exclude them
+    (pipelines/graph.py CaptureGate) -- and every thread finishes."""
+    import threading
+    import time
+
+    from triton_client_amd.inference import LocalDetector2D
+    from triton_client_amd.pipelines.graph import capture_gate
+    from triton_client_amd.utils.synthetic import camera_frame
+
+    eng = LocalDetector2D(batch=4, device=cuda, letterbox=True, calibrate_target=100.0)
+    names = [f"c{i}" for i in range(80)]
+    live = eng.live()
+    base = [compat.numpy_to_imgmsg(camera_frame(360, 640, s), "rgb8", msgs.Header(seq=s)) for s in range(4)]
+    want = live.process(base, draw=True, names=names)
+    stop, stamps, errors = threading.Event(), [], []
+
+    def stream():
+        try:
+            while not stop.is_set():
+                got = live.process(base, draw=True, names=names)
+                for (_, d), (_, w) in zip(got, want):
+                    np.testing.assert_array_equal(d, w)
+                stamps.append(time.monotonic())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def build(hw, seed):
+        try:
+            m = [compat.numpy_to_imgmsg(camera_frame(hw[0], hw[1], seed), "rgb8", msgs.Header(seq=seed))]
+            assert len(live.process(m, draw=True, names=names)) == 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    st = threading.Thread(target=stream)
+    st.start()
+    time.sleep(0.3)
+    caps0 = capture_gate(cuda).captures
+    t0 = time.monotonic()
+    builders = [threading.Thread(target=build, args=(hw, 9 + i)) for i, hw in enumerate([(480, 848), (300, 500)])]
+    for b in builders:
+        b.start()
+    for b in builders:
+        b.join(300)
+    t1 = time.monotonic()
+    stop.set()
+    st.join(60)
+    assert not errors, errors
+    assert not st.is_alive() and not any(b.is_alive() for b in builders)
+    assert capture_gate(cuda).captures - caps0 >= 4  # two graphs per new engine
+    during = [s for s in stamps if t0 < s < t1]
+    gaps = np.diff([t0] + during + [t1])
+    assert len(during) >= 3 and gaps.max() < 0.8 * (t1 - t0), (len(during), float(gaps.max()), t1 - t0)

@@ -1,0 +1,91 @@
+"""How many GPUs can rank 0 feed through the shared host ring?
+
+In the data-parallel live drivers (``parallel/ring_dp.py``) rank 0 copies every
+payload of a node step into the ring slot itself (``tca_host_gather_copy`` on
+C++ threads, ``_write_step``).  At the one-GPU rate of the headline (32 camera
+frames + 32 LiDAR sweeps per ~7.3 ms step) a node of G GPUs needs
+G x 32 x (2.76 MB raw 1280x720 frame + 1.92 MB 120k-point cloud) per step.
+This measures the copy rate into a ring data area (a /dev/shm mapping, as in
+production) for 32 x 2.76 MB frames and 32 x 1.92 MB clouds at several thread
+counts, and from it the largest G whose copy still fits in one step.
+
+    python tools/fanout_bench.py --threads 4,8,16,32 --json out.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+FRAME = 720 * 1280 * 3      # raw rgb8 frame
+CLOUD = 64 * 1875 * 16      # 120k points x 16 B (x, y, z, intensity)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--threads", default="4,8,16,32")
+    ap.add_argument("--items", type=int, default=32, help="frames and clouds per GPU per step")
+    ap.add_argument("--step-ms", type=float, default=7.3, help="one-GPU step time to feed")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--gpus", type=int, default=8, help="node size for the feed estimate")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args(argv)
+
+    from triton_client_amd.inference.live import gather_copy
+    from triton_client_amd.parallel.host_ring import HostRing
+
+    rng = np.random.default_rng(0)
+    n = a.items
+    # sources: bytes objects, like deserialised ROS message payloads
+    srcs = [rng.integers(0, 255, FRAME, np.uint8).tobytes() for _ in range(n)] + \
+        [rng.integers(0, 255, CLOUD, np.uint8).tobytes() for _ in range(n)]
+    sizes = [len(s) for s in srcs]
+    total = sum(sizes)
+    ring = HostRing(f"tca_fanout_{os.getpid()}", nslots=1, world=1, create=True, pin=False)
+    try:
+        data = ring.new_generation(total + 4096 * len(srcs))
+        offs, o = [], 0
+        for z in sizes:
+            offs.append(o)
+            o += (z + 4095) // 4096 * 4096
+        dst = [data.base + x for x in offs]
+        rows = []
+        for t in [int(v) for v in a.threads.split(",")]:
+            for _ in range(3):  # first touch of the mapping, thread pool warm-up
+                gather_copy(dst, srcs, sizes, t)
+            ts = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                gather_copy(dst, srcs, sizes, t)
+                ts.append(time.perf_counter() - t0)
+            med = float(np.median(ts))
+            gbs = total / med / 1e9
+            feed = (a.step_ms / 1e3) / med  # GPUs whose per-step payload rank 0 copies within one step
+            rows.append({"threads": t, "bytes_per_gpu_step": total, "median_ms": med * 1e3,
+                         "min_ms": min(ts) * 1e3, "GBps": gbs, "gpus_fed_at_1gpu_rate": feed})
+            print(f"threads {t:3d}: {med * 1e3:7.2f} ms per GPU-step of {total / 1e6:.1f} MB = {gbs:6.1f} GB/s "
+                  f"-> rank 0 feeds {feed:4.1f} GPUs at {a.step_ms} ms/step", flush=True)
+        best = max(rows, key=lambda r: r["GBps"])
+        out = {"tool": "tools/fanout_bench.py", "items_per_gpu": n, "frame_bytes": FRAME, "cloud_bytes": CLOUD,
+               "step_ms": a.step_ms, "cpus_allowed": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+               "rows": rows, "best": best, "node_gpus": a.gpus,
+               "node_step_copy_ms_at_best": best["median_ms"] * a.gpus,
+               "feeds_node": best["gpus_fed_at_1gpu_rate"] >= a.gpus}
+        print(json.dumps({"best_GBps": best["GBps"], "gpus_fed": best["gpus_fed_at_1gpu_rate"],
+                          "cpus_allowed": out["cpus_allowed"]}))
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump(out, f, indent=1)
+    finally:
+        ring.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

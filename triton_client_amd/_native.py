@@ -43,6 +43,9 @@ _KERNEL_SIGS = {
     # cand box, score, cls, key, count, cap, stream
     "tca_yolo_detect_filter": [P, P, P, P, P, P, P, P, P, I, I, I, F, P, P, P, P, P, P, I, P],
     "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
+    # pred, confs, kind, B, N, ld, nc, conf, multi_label, class_mask, img_w, img_h, cand box/score/cls/key/count,
+    # cap, stream (the remote client's postprocess of a decoded response, csrc/kernels/yolo.hip)
+    "tca_yolo_filter_decoded": [P, P, I, I, I, I, I, F, I, P, F, F, P, P, P, P, P, I, P],
     "tca_topk_sort": [P, P, I, I, I, P, P, P],
     "tca_nms_mask": [I, P, I, P, P, P, I, I, I, F, I, P, I, P],
     "tca_nms_mask_rot": [P, I, P, P, P, I, I, I, F, I, P, P, P],

@@ -49,7 +49,9 @@ def add_framework_flags(p: argparse.ArgumentParser, params_default: str, three_d
     g.add_argument("--client", choices=["auto", "yolov5", "fcos", "pointpillars"], default="auto",
                    help="model-family client (auto: from the model's config)")
     g.add_argument("--server", default=None, help="override grpc_channel host:port")
-    g.add_argument("--device", default="auto", help="GPU for the local engine / preprocessing (cuda:N, cpu)")
+    g.add_argument("--device", default="auto",
+                   help="where the engine runs: the local pipeline, or the remote client's decode / preprocess / "
+                        "postprocess HIP kernels (auto: the first GPU if there is one; cuda:N; cpu)")
     g.add_argument("--frames-per-step", type=int, default=8, help="micro-batch for bag replay / local engine")
     g.add_argument("--live-batch", type=int, default=1,
                    help="live topic: run up to N pending frames per engine call (latest-wins window, "
@@ -101,21 +103,34 @@ def make_channel(params: dict, flags):
     return GRPCChannel(params, flags, timeout_s=getattr(flags, "timeout", None), retries=getattr(flags, "retries", 2))
 
 
+def resolve_device(flag: Optional[str]) -> str:
+    """``--device``: "auto" is the first visible GPU when there is one, else the CPU
+    (config 1, the CPU-only client); anything else is taken as given."""
+    if flag in (None, "", "auto"):
+        import torch
+
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    return flag
+
+
 def make_client(flags, channel=None):
+    """The model-family client, its pre/postprocess on ``--device`` (the remote
+    engine's HIP path on a GPU client)."""
     from ..clients import FCOS_client, Pointpillars_client, Yolov5client, client_for_model
 
+    dev = resolve_device(getattr(flags, "device", "cpu"))
     c = getattr(flags, "client", "auto")
     if c == "yolov5":
-        return Yolov5client()
+        return Yolov5client(dev)
     if c == "fcos":
-        return FCOS_client()
+        return FCOS_client(dev)
     if c == "pointpillars":
-        return Pointpillars_client()
+        return Pointpillars_client(dev)
     cfg = None
     if channel is not None:
         cr = channel.get_metadata().get("config_response")
         cfg = getattr(cr, "config", cr)
-    return client_for_model(flags.model_name, cfg)
+    return client_for_model(flags.model_name, cfg, dev)
 
 
 def rpc_mode(flags) -> str:

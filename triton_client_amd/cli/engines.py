@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import os
 
-from .common import DATA, make_channel, make_client, rpc_mode
+from .common import DATA, make_channel, make_client, resolve_device, rpc_mode
 
 
 def yolo_spec(model_name: str, classes: int):
@@ -66,7 +66,7 @@ def engine_2d(flags, params, letterbox=None, conf_thres=None):
     client = make_client(flags, ch)
     eng = RemoteDetector2D(ch, client, letterbox=lb, conf_thres=conf, mode=rpc_mode(flags), wire=flags.wire,
                            scaling=flags.scaling if flags.scaling != "COCO" else None,
-                           device=flags.device if flags.device != "auto" else "cpu")
+                           device=resolve_device(flags.device))
     return eng, ch, client
 
 
@@ -92,7 +92,8 @@ def engine_3d(flags, params):
 
     ch = make_channel(params, flags)
     client = make_client(flags, ch)
-    eng = RemoteDetector3D(ch, client, z_offset=flags.z_offset, mode=rpc_mode(flags), wire=flags.wire)
+    eng = RemoteDetector3D(ch, client, z_offset=flags.z_offset, mode=rpc_mode(flags), wire=flags.wire,
+                           device=resolve_device(flags.device))
     return eng, ch, client
 
 

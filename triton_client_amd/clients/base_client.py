@@ -54,19 +54,20 @@ class Client(ABC):
                 input_metadata.datatype)
 
 
-def client_for_model(model_name: str, model_config=None) -> Client:
+def client_for_model(model_name: str, model_config=None, device="cpu") -> Client:
     """Pick the client by model family (fixes SURVEY Appendix A1: the
-    reference hard-codes Yolov5client regardless of ``-m``)."""
+    reference hard-codes Yolov5client regardless of ``-m``).  ``device``: where the
+    client's pre/postprocess runs (a GPU: the HIP kernels; "cpu": config 1)."""
     n = model_name.lower()
     outs = len(model_config.output) if model_config is not None else 0
     if "pointpillar" in n or "second" in n or "centerpoint" in n or (model_config is not None and len(model_config.input) == 3):
         from .detector_3d_client import Pointpillars_client
-        return Pointpillars_client()
+        return Pointpillars_client(device)
     if "fcos" in n or "retina" in n or "detectron" in n or n == "test_model" or outs == 4:
         from .detectron_client import FCOS_client
-        return FCOS_client()
+        return FCOS_client(device)
     if "yolov4" in n or outs == 2:
         from .yolov4_client import Yolov4client
-        return Yolov4client()
+        return Yolov4client(device)
     from .yolov5_client import Yolov5client
-    return Yolov5client()
+    return Yolov5client(device)

@@ -32,8 +32,26 @@ class FCOSpostprocess(Postprocess):
         keep = scores >= conf_thres
         return [np.concatenate([boxes[keep], scores[keep, None], classes[keep, None].astype(np.float32)], 1)]
 
+    def extract_boxes_device(self, responses, conf_thres: float = 0.0, iou_thres=None, xform=None, device="cuda",
+                             **_):
+        """Final server detections of several responses -> one device NmsResult (boxes
+        in original-frame pixels with ``xform``) for the GPU annotator."""
+        from .postprocess.device import pack_host_detections
+
+        per = []
+        for r in responses:
+            d = self.extract_boxes(r, conf_thres)[0]
+            if xform is not None and len(d):
+                d[:, :4] = xform.unmap_boxes(d[:, :4])
+            per.append(d)
+        return pack_host_detections(per, device)
+
 
 class FCOS_client(Client):
+    def __init__(self, device="cpu"):
+        super().__init__()
+        self.device = device
+
     def get_preprocess(self):
         return FCOSpreprocess()
 

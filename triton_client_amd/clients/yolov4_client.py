@@ -8,6 +8,7 @@ import os
 from typing import List, Optional
 
 import numpy as np
+import torch
 
 from .base_client import Client
 from .postprocess.base_postprocess import Postprocess
@@ -19,8 +20,10 @@ class Yolov4preprocess(Yolov5preprocess):
 
 
 class Yolov4postprocess(Postprocess):
-    def __init__(self, input_hw=(512, 512)):
+    def __init__(self, input_hw=(512, 512), device="cpu"):
         self.input_hw = tuple(input_hw)
+        self.device = torch.device(device)
+        self._pp, self._up = {}, None
 
     def load_class_names(self, namesfile: Optional[str] = None) -> List[str]:
         return Postprocess.load_class_names(namesfile or os.path.join(DATA, "coco.names"))
@@ -44,11 +47,37 @@ class Yolov4postprocess(Postprocess):
             out.append(d)
         return out
 
+    def extract_boxes_device(self, responses, conf_thres: float = 0.4, iou_thres: float = 0.6, xform=None,
+                             stream=None, **_):
+        """Several responses -> one device NmsResult: ``boxes`` / ``confs`` of every
+        response uploaded by one pinned H2D each, then the filter (K3,
+        ``tca_yolo_filter_decoded`` kind 1) and per-class NMS (K4) on the GPU."""
+        from ..ops.yolov4 import Yolov4Postprocess
+        from .postprocess.device import ResponseUpload
+
+        names = self.output_names(responses[0])
+        ci = names.index("confs") if "confs" in names else 0
+        bi = names.index("boxes") if "boxes" in names else 1
+        confs = [np.asarray(self.output_array(r, ci), np.float32) for r in responses]
+        boxes = [np.asarray(self.output_array(r, bi), np.float32) for r in responses]
+        nc = confs[0].shape[-1]
+        confs = [c.reshape(-1, nc) for c in confs]
+        boxes = [b.reshape(-1, 4) for b in boxes]
+        if self._up is None:
+            self._up = (ResponseUpload(self.device), ResponseUpload(self.device))
+        dc, db = self._up[0](confs, np.float32, stream), self._up[1](boxes, np.float32, stream)
+        key = (nc, float(conf_thres), float(iou_thres))
+        pp = self._pp.get(key)
+        if pp is None:
+            pp = self._pp[key] = Yolov4Postprocess(nc, self.input_hw, conf_thres, iou_thres, device=self.device)
+        return pp.filter_decoded(db, dc, xform, stream)
+
 
 class Yolov4client(Client):
-    def __init__(self):
+    def __init__(self, device="cpu"):
         super().__init__()
         self.input_hw = (512, 512)
+        self.device = device
 
     def parse_model(self, model_metadata, model_config):
         r = super().parse_model(model_metadata, model_config)
@@ -59,4 +88,4 @@ class Yolov4client(Client):
         return Yolov4preprocess()
 
     def get_postprocess(self):
-        return Yolov4postprocess(self.input_hw)
+        return Yolov4postprocess(self.input_hw, self.device)

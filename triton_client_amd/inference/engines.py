@@ -809,6 +809,18 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
 
     _TORCH_OF = {"FP32": torch.float32, "FP16": torch.float16, "UINT8": torch.uint8}
 
+    def live(self):
+        """The drivers' device path on a GPU client (``inference/remote_live.py``):
+        GPU JPEG decode, K1 preprocess, one KServe request per frame, K3/K4 on the
+        response, GPU annotation, zero-copy publish.  None on a CPU client (config 1)
+        and for the shared-memory wires, which keep :meth:`detect`."""
+        if self.device.type != "cuda" or self.wire not in ("raw", "proto"):
+            return None
+        if getattr(self, "_live", None) is None:
+            from .remote_live import RemoteLiveCamera
+            self._live = RemoteLiveCamera(self)
+        return self._live
+
     def _gpu_staging(self, hw):
         """Per source geometry: pinned frame upload buffer, device input, and
         the pinned staging the model input lands in (one D2H DMA)."""

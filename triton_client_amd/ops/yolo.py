@@ -163,6 +163,32 @@ class YoloPostprocess:
                      _native.ptr(cand.count), cap, _native.ptr(decoded), _native.stream_ptr(stream))
         return cand, decoded
 
+    def filter_decoded(self, pred: torch.Tensor, xform: Optional[FrameXform] = None, stream=None) -> NmsResult:
+        """K3 + K4 on a *decoded* prediction already on the GPU: pred [B, N, >=5+nc] fp32
+        (a KServe YOLOv5 response uploaded by the remote client) -> NmsResult on the
+        device, boxes in original-frame pixels if ``xform`` is given, else model pixels.
+        Same kept sets as :meth:`postprocess_decoded` (the CPU path of ``--device cpu``)."""
+        if pred.device.type != "cuda":
+            return self.postprocess_decoded(pred.numpy(), xform)
+        if pred.dim() != 3 or pred.dtype != torch.float32 or pred.stride(2) != 1 or pred.shape[2] < self.nc + 5:
+            raise ValueError(f"pred must be fp32 [B, N, >= {self.nc + 5}] with unit inner stride, "
+                             f"got {tuple(pred.shape)} {pred.dtype}")
+        pred = pred if pred.stride(1) == pred.shape[2] and pred.stride(0) == pred.shape[1] * pred.shape[2] \
+            else pred.contiguous()
+        B, N, ld = pred.shape
+        cap = min(N * (self.nc if self.multi_label else 1), 1 << 20)
+        cand = Candidates.alloc(self.ws, "yolod_", B, cap, 4)
+        _native.call("tca_yolo_filter_decoded", _native.ptr(pred), None, 0, B, N, ld, self.nc, float(self.conf_thres),
+                     int(self.multi_label), _native.ptr(self._class_mask), 0.0, 0.0, _native.ptr(cand.box),
+                     _native.ptr(cand.score), _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count),
+                     cap, _native.stream_ptr(stream))
+        xf = xform.as_list() if xform is not None else None
+        res = sort_and_nms(self.ws, cand, 0, self.iou_thres, self.max_nms, self.max_det, self.agnostic,
+                           None if self.merge else xf, prefix="yolod_nms_", stream=stream)
+        if self.merge:
+            res = self._merge(cand, res, xf, stream)
+        return res
+
     def decode(self, heads: List[torch.Tensor], stream=None) -> torch.Tensor:
         """Decoded [B, N, 5+nc] fp32 (the ONNX YOLOv5 output contract)."""
         if not _on_gpu(heads[0]):

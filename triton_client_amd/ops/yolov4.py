@@ -57,11 +57,42 @@ class Yolov4Postprocess:
                            xform.as_list() if xform is not None else None, prefix="y4_nms_", stream=stream)
         return (res, ob, oc) if full else res
 
+    def filter_decoded(self, boxes: torch.Tensor, confs: torch.Tensor, xform: Optional[FrameXform] = None,
+                       stream=None) -> NmsResult:
+        """The served model's decoded outputs (``boxes`` [B, N, 1, 4] normalised x1y1x2y2,
+        ``confs`` [B, N, nc]) already on the GPU -> per-class NMS detections on the device
+        (the remote client's postprocess, ``tools/utils.py:166-233``); CPU tensors take
+        :meth:`decoded_cpu`."""
+        if boxes.device.type != "cuda":
+            return self.decoded_cpu(boxes.numpy(), confs.numpy(), xform)
+        B, N = confs.shape[:2]
+        if confs.shape[2] != self.nc or boxes.numel() != B * N * 4:
+            raise ValueError(f"boxes {tuple(boxes.shape)} / confs {tuple(confs.shape)} do not match nc={self.nc}")
+        boxes, confs = boxes.float().contiguous(), confs.float().contiguous()
+        cand = Candidates.alloc(self.ws, "y4d_", B, self.cap, 4)
+        H, W = self.img_hw
+        _native.call("tca_yolo_filter_decoded", _native.ptr(boxes), _native.ptr(confs), 1, B, N, 4, self.nc,
+                     float(self.conf_thres), 0, None, float(W), float(H), _native.ptr(cand.box), _native.ptr(cand.score),
+                     _native.ptr(cand.cls), _native.ptr(cand.key), _native.ptr(cand.count), self.cap,
+                     _native.stream_ptr(stream))
+        return sort_and_nms(self.ws, cand, 0, self.nms_thres, self.cap, self.max_out, False,
+                            xform.as_list() if xform is not None else None, prefix="y4d_nms_", stream=stream)
+
+    def decoded_cpu(self, boxes: np.ndarray, confs: np.ndarray, xform=None) -> NmsResult:
+        from ..models.yolov4 import post_processing
+
+        B = confs.shape[0]
+        return self._pack(post_processing(np.asarray(boxes).reshape(B, -1, 1, 4), np.asarray(confs), self.conf_thres,
+                                          self.nms_thres), xform)
+
     def cpu(self, heads, xform=None, full=False):
         from ..models.yolov4 import decode_reference, post_processing
 
         boxes, confs = decode_reference(heads, self.nc, self.sxy)
-        per = post_processing(boxes.numpy(), confs.numpy(), self.conf_thres, self.nms_thres)
+        res = self._pack(post_processing(boxes.numpy(), confs.numpy(), self.conf_thres, self.nms_thres), xform)
+        return (res, boxes, confs) if full else res
+
+    def _pack(self, per, xform=None) -> NmsResult:
         B, mo = len(per), self.max_out
         H, W = self.img_hw
         box = np.zeros((B, mo, 4), np.float32)
@@ -75,5 +106,4 @@ class Yolov4Postprocess:
                 bx = xform.unmap_boxes(bx)
             k = len(d)
             box[b, :k], score[b, :k], cls[b, :k], cnt[b] = bx, d[:, 4], d[:, 5], k
-        res = NmsResult(torch.from_numpy(box), torch.from_numpy(score), torch.from_numpy(cls), torch.from_numpy(cnt))
-        return (res, boxes, confs) if full else res
+        return NmsResult(torch.from_numpy(box), torch.from_numpy(score), torch.from_numpy(cls), torch.from_numpy(cnt))

@@ -55,17 +55,52 @@ def _rt():
     return _native.runtime()
 
 
+class RingSpaceError(RuntimeError):
+    """/dev/shm cannot hold a ring file (Docker's default /dev/shm is 64 MB)."""
+
+
+def _reserve(fd: int, path: str, size: int) -> None:
+    """Back the whole file with tmpfs pages now: a sparse file that later runs out of
+    /dev/shm space would SIGBUS inside the payload copy or a D2H into the mapping."""
+    try:
+        os.posix_fallocate(fd, 0, size)
+    except OSError as e:
+        import errno
+        if e.errno in (errno.ENOSPC, errno.EFBIG, errno.ENOMEM):
+            free = None
+            try:
+                st = os.statvfs(os.path.dirname(path))
+                free = st.f_bavail * st.f_frsize
+            except OSError:
+                pass
+            raise RingSpaceError(
+                f"{path}: cannot reserve {size / 2**20:.1f} MiB in {os.path.dirname(path)} "
+                f"({'unknown' if free is None else f'{free / 2**20:.1f} MiB'} free); the data-parallel drivers need "
+                "about 4 x 1.25 x (one node batch of payloads + annotated frames) -- give the container a larger "
+                "/dev/shm (docker run --shm-size=...)") from e
+        if e.errno not in (errno.EOPNOTSUPP, errno.EINVAL):  # filesystems without fallocate: stay sparse
+            raise
+        os.ftruncate(fd, size)
+
+
 def _open(path: str, size: int, create: bool) -> mmap.mmap:
     flags = os.O_RDWR | (os.O_CREAT | os.O_TRUNC if create else 0)
     fd = os.open(path, flags, 0o600)
     try:
         if create:
-            os.ftruncate(fd, size)
+            try:
+                _reserve(fd, path, size)
+            except BaseException:
+                os.close(fd)
+                fd = -1
+                os.unlink(path)
+                raise
         elif os.fstat(fd).st_size < size:
             raise RuntimeError(f"{path}: {os.fstat(fd).st_size} bytes, expected {size}")
         return mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
     finally:
-        os.close(fd)
+        if fd >= 0:
+            os.close(fd)
 
 
 def _host_register(mm: mmap.mmap, size: int) -> bool:
@@ -146,6 +181,7 @@ class HostRing:
         self.data: Optional[DataRing] = None
         self.gen = -1
         self.owner = create
+        self.generation_switches = {"grow": 0, "leased": 0}  # rank 0: why a new data area was made
 
     # ------------------------------------------------------------------ layout
     def _blk(self, s: int) -> int:
@@ -171,9 +207,9 @@ class HostRing:
     def new_generation(self, slot_bytes: int) -> DataRing:
         """Rank 0: a (larger) data area; the caller has drained every slot."""
         old = self.data
-        self.gen += 1
         slot_bytes = (int(slot_bytes) + 4095) // 4096 * 4096
-        self.data = DataRing(self.data_path(self.gen), self.nslots, slot_bytes, True, self.pin)
+        self.data = DataRing(self.data_path(self.gen + 1), self.nslots, slot_bytes, True, self.pin)
+        self.gen += 1  # only once the new area exists: a failed reservation keeps the old one in use
         if old is not None:
             old.close(unlink=True)
         return self.data

@@ -39,6 +39,7 @@ Reference: none — the reference runs one blocking RPC per frame
 """
 from __future__ import annotations
 
+import logging
 import os
 import threading
 import time
@@ -60,6 +61,8 @@ H_CALIB = 60  # 1: rank 0 broadcasts its freshly calibrated weights in this step
 # item ints: in_off, in_size, out_off, out_size, meta0, meta1
 I_IN, I_INSZ, I_OUT, I_OUTSZ, I_M0, I_M1 = range(6)
 _ALIGN = 4096
+
+log = logging.getLogger("triton_client_amd.ring_dp")
 
 
 def _align(n: int) -> int:
@@ -104,8 +107,10 @@ class _RingDP:
             dist.barrier()
         if not info.is_main:
             self.ring = HostRing(name[0])
-        # rank 0: per slot, (seq, participants) of its last use; open output leases per
-        # (data generation, slot): published Image messages still viewing the slot's output area
+        # rank 0: per slot, (seq, every live rank) of its last use -- every peer reads every
+        # slot's header in sequence and acks it, participant or not, so a slot is rewritten
+        # only once all of them have; open output leases per (data generation, slot):
+        # published Image messages still viewing the slot's output area
         self._slot_use: List[Optional[Tuple[int, List[int]]]] = [None] * nslots
         self._leases: Dict[Tuple[int, int], int] = {}
         self._lease_lock = threading.Lock()
@@ -115,7 +120,9 @@ class _RingDP:
         return self.monitor.alive() if self.monitor is not None else list(range(self.info.world))
 
     def _drain(self, s: int) -> bool:
-        """Wait until slot s's last step's participants have acked.  Returns False
+        """Wait until every rank live at slot s's last step has acked it (peers that
+        did not take part still read its header: rewriting it earlier could hand a slow
+        peer a newer or half-written header).  Returns False
         if published messages still view the slot's output area in the current
         data generation (the caller then moves to a fresh generation; the old
         mapping lives on under those messages)."""
@@ -170,6 +177,13 @@ class _RingDP:
         need = sum(_align(z) for z in sizes) + sum(_align(z) for z in out_sizes)
         ring = self.ring
         if ring.data is None or need > ring.data.slot_bytes or not free:
+            if ring.data is not None:
+                why = "leased" if need <= ring.data.slot_bytes else "grow"
+                ring.generation_switches[why] += 1
+                if why == "leased":  # a consumer holds published Images of this slot
+                    log.warning("host ring %s: slot %d still viewed by published messages: new data generation "
+                                "(%d so far; re-pins the ring on every rank)", ring.name, s,
+                                ring.generation_switches["leased"])
             for t in range(self.nslots):  # every slot acked before the data area is replaced
                 self._drain(t)
             size = max(need + need // 4, 1 << 20, ring.data.slot_bytes if ring.data is not None else 0)
@@ -196,7 +210,7 @@ class _RingDP:
         hdr[H_KEY:H_KEY + len(key)] = key
         hdr[H_CALIB] = int(calib)
         ring.publish(s, seq)
-        self._slot_use[s] = (seq, list(parts))
+        self._slot_use[s] = (seq, self._participants())
         return seq, s, items[:n].copy()
 
     def close(self) -> None:
@@ -352,8 +366,7 @@ class _RingDP:
                         raise RingStepError(f"step {seq}: rank {r} answered for step {int(tag[0])}")
                     if (int(tag[2]), int(tag[3])) != (int(dst[0][-1][2]), int(dst[0][-1][3])):
                         raise ReplicaMismatch(f"rank {r} runs different weights than rank 0")
-                self._wait_acks(s, [r for r in wk if r != 0], seq)
-                self._slot_use[s] = None
+                self._wait_acks(s, [r for r in wk if r != 0], seq)  # their outputs are in the slot
                 self.steps += 1
                 return assemble(dst, wk, per, items, slot_view, own, s)
             except (RuntimeError, RingStepError):

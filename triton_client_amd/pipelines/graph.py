@@ -25,6 +25,7 @@ replay — raises the same error.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 from typing import Callable, Dict, Optional, Set
@@ -38,13 +39,106 @@ class GraphCaptureError(RuntimeError):
 
 _TL = threading.local()
 
-# Process-wide: one graph capture at a time, and no executor submitting work while one runs.  A
-# thread_local-mode capture lets other host threads keep calling HIP, but their device-wide
-# calls (synchronize, pinned host allocation and the caching allocators' event queries) interleaved
-# with another thread's capture were seen to stall two live drivers building their engines at
-# once (tests/test_live.py::test_live_drivers_publish_engine_results); serialising the capture
-# against the other threads' issue costs only host time at engine build.
-CAPTURE_LOCK = threading.RLock()
+class CaptureGate:
+    """Reader/writer gate of one device between graph captures and stream work.
+
+    ``shared()``: stream work that must not interleave with a capture window --
+    executor submissions (pinned result allocation, H2D / D2H enqueue, replays) and
+    capture warm-ups.  Any number of threads hold it together: two engines' submissions
+    no longer serialise against each other.
+    ``exclusive()``: the capture window itself (``torch.cuda.graph`` begin..end); it waits
+    for the current shared holders and blocks new ones (writer preference, so a steady
+    stream of submissions cannot starve an engine build).
+
+    Why a capture window is exclusive -- the mechanism, from the code on these paths: a
+    thread_local-mode capture restricts only the capturing thread, and the calls other
+    threads make here are legal on their own streams; the two that are device- or
+    process-wide are (a) ``hipHostMalloc`` / ``hipHostFree`` behind ``torch.empty(...,
+    pin_memory=True)`` in :meth:`~triton_client_amd.pipelines.stream.StreamExecutor.submit`
+    (the caching host allocator calls them with the GIL held), and (b) the old warm-up's
+    ``torch.cuda.synchronize()`` (hipDeviceSynchronize over every stream of the device).
+    A capture also needs the GIL to run the Python step it records.  A thread blocked in a
+    device-wide call with the GIL held while another thread sits inside a capture window
+    therefore stalls both -- the intermittent stall of two live drivers building engines
+    at once (round 4).  The warm-up now waits on its own stream only, runs under the
+    shared side, and only the capture window is exclusive.
+
+    Reentrant per thread; a thread holding the shared side that asks for the exclusive
+    side gives its shared holds up while it waits (a first-use capture inside a
+    submission), and gets them back after."""
+
+    def __init__(self):
+        self._cv = threading.Condition(threading.Lock())
+        self._readers = 0
+        self._writer: Optional[int] = None
+        self._writer_depth = 0
+        self._writers_waiting = 0
+        self._tl = threading.local()
+        self.captures = 0
+
+    def _shared_depth(self) -> int:
+        return getattr(self._tl, "shared", 0)
+
+    @contextlib.contextmanager
+    def shared(self):
+        me = threading.get_ident()
+        with self._cv:
+            if self._writer != me and self._shared_depth() == 0:
+                while self._writer is not None or self._writers_waiting:
+                    self._cv.wait()
+            self._readers += 1
+            self._tl.shared = self._shared_depth() + 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._readers -= 1
+                self._tl.shared -= 1
+                self._cv.notify_all()
+
+    @contextlib.contextmanager
+    def exclusive(self):
+        me = threading.get_ident()
+        with self._cv:
+            if self._writer == me:
+                self._writer_depth += 1
+            else:
+                held = self._shared_depth()
+                self._readers -= held  # give up this thread's shared holds while waiting
+                self._writers_waiting += 1
+                self._cv.notify_all()
+                while self._writer is not None or self._readers > 0:
+                    self._cv.wait()
+                self._writers_waiting -= 1
+                self._writer, self._writer_depth = me, 1
+                self._readers += held
+                self.captures += 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._writer_depth -= 1
+                if self._writer_depth == 0:
+                    self._writer = None
+                self._cv.notify_all()
+
+
+_GATES: Dict[int, CaptureGate] = {}
+_GATES_LOCK = threading.Lock()
+
+
+def capture_gate(device=None) -> CaptureGate:
+    """The :class:`CaptureGate` of ``device`` (default: the current device)."""
+    idx = torch.device(device).index if device is not None else None
+    if idx is None:
+        idx = torch.cuda.current_device() if torch.cuda.is_available() else -1
+    with _GATES_LOCK:
+        g = _GATES.get(idx)
+        if g is None:
+            g = _GATES[idx] = CaptureGate()
+        return g
+
+
 _SPY_LOCK = threading.Lock()
 _SPY = {"installed": False}
 
@@ -174,17 +268,19 @@ class GraphRunner:
     def capture(self) -> None:
         if not self.enabled:
             return
-        with CAPTURE_LOCK:
+        gate = capture_gate()
+        with gate.shared():  # warm-up: ordinary stream work beside other threads' submissions
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    self.out = self.fn()
+            torch.cuda.current_stream().wait_stream(s)
+            s.synchronize()  # this stream only: no device-wide sync (see CaptureGate)
+        with gate.exclusive():
             self._capture()
 
     def _capture(self) -> None:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(self.warmup):
-                self.out = self.fn()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
         _install_stream_spy()
         g = torch.cuda.CUDAGraph()
         unjoined: Dict[int, object] = {}

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from .graph import CAPTURE_LOCK, GraphRunner
+from .graph import GraphRunner, capture_gate
 
 
 def flatten_tensors(obj) -> List[torch.Tensor]:
@@ -137,7 +137,8 @@ class StreamExecutor:
         # capture every set now, over whatever the inputs hold: the eager warm-up
         # runs of a capture must not see (and, for an in-place annotator, modify)
         # a real batch
-        with CAPTURE_LOCK, torch.cuda.stream(self.compute):
+        self.gate = capture_gate(self.device)
+        with torch.cuda.stream(self.compute):
             for k, r in enumerate(self.runners):
                 if r.enabled:
                     r.capture()
@@ -184,7 +185,7 @@ class StreamExecutor:
         (e.g. the annotated frames of set k) into fresh pinned tensors, or
         into ``extras_dst[i]`` (page-locked host tensors, e.g. slots of the
         data-parallel host ring) where given."""
-        with CAPTURE_LOCK, self.lock:  # (no submission while another thread captures)
+        with self.gate.shared(), self.lock:  # (no submission inside another thread's capture window)
             k = self.next
             self.next = (k + 1) % self.sets
             for ev in self.set_free[k]:  # set k's inputs / stage are still being read back
