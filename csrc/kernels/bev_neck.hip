@@ -349,11 +349,27 @@ __device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x
   }
 }
 
+// max(x, 0) as ONE v_max_i32 on the bits (a negative float is a negative int; -0 -> +0): fmaxf in
+// IEEE mode costs a canonicalizing v_max_f32 per input on top of the max
+__device__ __forceinline__ float relu_bits(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 __device__ __forceinline__ void mfma3(f32x4& acc, const bf16x8& bh, const bf16x8& bl, const bf16x8& ah,
                                       const bf16x8& al) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+}
+
+constexpr unsigned kOutOfRange = 0x80000000u;  // >= any num_records the launcher accepts (< 2^31): reads zeros
+
+// one 16-B-per-lane LDS DMA through a buffer resource: voffset per lane, soffset scalar
+__device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, const void* l, unsigned soff) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+               : "memory");
 }
 
 template <int N>
@@ -427,21 +443,50 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
       }
     }
   };
-  int a_off[Y_A_INS];  // per (tile, branch) element offsets of the lane's A rows (-1: zero page)
-  const float* a_base = nullptr;
+  // LDS DMA through buffer resources (conv_mfma.hip "xb"): every lane's 32-bit byte offset
+  // of a DMA is formed once per (tile, branch) -- A rows, B rows, bias -- or once per kernel
+  // (head weight pieces); a K step only advances the scalar soffset, so the K loop's DMA
+  // issue needs no VALU.  A row outside the image is offset kOutOfRange: the descriptor's
+  // range check reads zeros.
+  unsigned a_vo[Y_A_INS], b_vo[Y_B_INS], bias_vo = 0;
+  __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)a.x[0], (short)0, 0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs_w = rs_a, rs_bias = rs_a;
   auto row_sources = [&]() {  // once per (tile, branch): the K steps only add their channel offset
     const int s = a.s[i_br], f = S / s;
-    const int Wi = a.W / s;
+    const int Hi = a.H / s, Wi = a.W / s;
     const int sy = i_cy / s, sx = i_cx / s;
-    a_base = a.x[i_br] + a.offx[i_br];
-    const int ldx = a.ldx[i_br];
+    const int ldx = a.ldx[i_br], cin = a.cin[i_br];
+    rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)a.x[i_br], (short)0, a.B * Hi * Wi * ldx * 4, 0x00020000);
+    rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w[i_br], (short)0, s * s * CB * cin * 4, 0x00020000);
+    rs_bias = __builtin_amdgcn_make_buffer_rsrc((void*)a.bias[i_br], (short)0, s * s * CB * 4, 0x00020000);
 #pragma unroll
     for (int j = 0; j < Y_A_INS; ++j) {
       const int row = (wid * Y_A_INS + j) * 8 + lrow;
       const int yg = r_yx[j] >> 16, x = r_yx[j] & 0xFFFF;
-      a_off[j] = r_yx[j] < 0 ? -1 : ((yg * f + sy) * Wi + x * f + sx) * ldx + (lslot ^ swz3(row)) * 4;
+      a_vo[j] = r_yx[j] < 0 ? kOutOfRange
+                            : (unsigned)((((yg * f + sy) * Wi + x * f + sx) * ldx + a.offx[i_br] +
+                                          (lslot ^ swz3(row)) * 4) * 4);
     }
+    const int sub = (i_cy % s) * s + (i_cx % s);
+#pragma unroll
+    for (int j = 0; j < Y_B_INS; ++j) {
+      const int row = (wid * Y_B_INS + j) * 8 + lrow;
+      b_vo[j] = (unsigned)(((sub * CB + row) * 2 * cin + (lslot ^ swz3(row)) * 8) * 2);
+    }
+    bias_vo = (unsigned)((sub * CB + wid * (4 * T::BIAS_LANES) + lane * 4) * 4);
   };
+  // head weight pieces of this wave (p = wid + k * NW): per-lane byte offsets, fixed for the kernel
+  constexpr int HP_MAX = (Y_HEAD_PIECES + NW - 1) / NW;
+  unsigned h_vo[HP_MAX];
+  int h_lds[HP_MAX];
+#pragma unroll
+  for (int k = 0; k < HP_MAX; ++k) {
+    const int p = wid + k * NW;
+    const int c = p / (NH / 8), r8 = p - c * (NH / 8), h = r8 * 8 + lrow;
+    h_vo[k] = (unsigned)((h * ldwh + c * 64 + (lslot ^ swz3(h)) * 8) * 2);
+    h_lds[k] = p < Y_HEAD_PIECES ? c * NH * X_ROWB + r8 * 1024 : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rs_wh = __builtin_amdgcn_make_buffer_rsrc((void*)a.wh, (short)0, NH * ldwh * 2, 0x00020000);
   auto issue = [&](int buf) -> int {
     unsigned char* sa = smem + buf * Y_STAGE;
     unsigned char* sb = sa + Y_A_BYTES;
@@ -450,34 +495,24 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
     int n = 0;
     if (i_kc < nkc) {
       if (i_kc == 0) row_sources();
-      const int ci0 = i_kc * 32;
+      const unsigned so = (unsigned)(i_kc * 32 * 4);  // fp32 inputs and split weights: 4 B per channel
 #pragma unroll
-      for (int j = 0; j < Y_A_INS; ++j) {
-        const void* g = a_off[j] >= 0 ? (const void*)(a_base + a_off[j] + ci0) : (const void*)g_neck_zero_page;
-        glds16_asm(g, sa + (wid * Y_A_INS + j) * 1024);
-      }
-      const int s = a.s[i_br];
-      const int sub = (i_cy % s) * s + (i_cx % s);
-      const int cin2 = 2 * a.cin[i_br];
-      const __hip_bfloat16* wb = a.w[i_br] + (long)sub * CB * cin2 + ci0 * 2;
+      for (int j = 0; j < Y_A_INS; ++j) bdma16(a_vo[j], rs_a, sa + (wid * Y_A_INS + j) * 1024, so);
 #pragma unroll
-      for (int j = 0; j < Y_B_INS; ++j) {
-        const int row = (wid * Y_B_INS + j) * 8 + lrow;
-        glds16_asm(wb + (long)row * cin2 + (lslot ^ swz3(row)) * 8, sb + (wid * Y_B_INS + j) * 1024);
-      }
-      if (lane < T::BIAS_LANES)
-        glds16_asm(a.bias[i_br] + sub * CB + wid * (4 * T::BIAS_LANES) + lane * 4, sbias + wid * (16 * T::BIAS_LANES));
+      for (int j = 0; j < Y_B_INS; ++j) bdma16(b_vo[j], rs_w, sb + (wid * Y_B_INS + j) * 1024, so);
+      if (lane < T::BIAS_LANES) bdma16(bias_vo, rs_bias, sbias + wid * (16 * T::BIAS_LANES), 0u);
       n = Y_DC_LOADS;
     } else {
       // head step t: rows h < 80 of the split head weights, channels [br*CB + 64t, +64)
       // as two 32-channel blocks [80][128 B] in the A slot
       const int t = i_kc - nkc;
-      const __hip_bfloat16* whb = a.wh + (i_br * CB + 64 * t) * 2;
-      for (int p = wid; p < Y_HEAD_PIECES; p += NW) {
-        const int c = p / (NH / 8), r8 = p - c * (NH / 8), h = r8 * 8 + lrow;
-        glds16_asm(whb + (long)h * ldwh + c * 64 + (lslot ^ swz3(h)) * 8, sa + c * NH * X_ROWB + r8 * 1024);
-        ++n;
-      }
+      const unsigned so = (unsigned)((i_br * CB + 64 * t) * 2 * 2);
+#pragma unroll
+      for (int k = 0; k < HP_MAX; ++k)
+        if (h_lds[k] >= 0) {  // wave-uniform
+          bdma16(h_vo[k], rs_wh, sa + h_lds[k], so);
+          ++n;
+        }
     }
     if (++i_kc == nkc + Y_HEAD_STEPS) {
       i_kc = 0;
@@ -530,8 +565,9 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
     bf16x8 xh[Y_FM], xl[Y_FM];
 #pragma unroll
     for (int i = 0; i < Y_FM; ++i) {
-      const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];
-      split8(make_float4(p0[0], p0[1], p0[2], p0[3]), make_float4(p1[0], p1[1], p1[2], p1[3]), xh[i], xl[i]);
+      const f32x4 p0 = acc1[i][2 * q], p1 = acc1[i][2 * q + 1];  // ReLU'd here, chunk by chunk
+      split8(make_float4(relu_bits(p0[0]), relu_bits(p0[1]), relu_bits(p0[2]), relu_bits(p0[3])),
+             make_float4(relu_bits(p1[0]), relu_bits(p1[1]), relu_bits(p1[2]), relu_bits(p1[3])), xh[i], xl[i]);
     }
 #pragma unroll
     for (int u = 0; u < NH / 16; ++u) {
@@ -545,12 +581,19 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
   for (int c_k = 0; c_k < my_tiles; ++c_k) {
     for (int c_br = 0; c_br < a.nbr; ++c_br) {
       const int nkc = a.cin[c_br] / 32;
-      const unsigned char* last = smem;
       for (int c_kc = 0; c_kc < nkc; ++c_kc) {
         // ---- deconv K step: 2 x 8 fragment pairs, three MFMAs each
         const unsigned char* sa = begin_step();
         const unsigned char* sb = sa + Y_A_BYTES;
-        last = sa;
+        if (c_kc == 0) {  // the branch's accumulators start at its deconv bias (staged with every K step)
+          const float* bias = reinterpret_cast<const float*>(sb + Y_B_BYTES);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
+#pragma unroll
+            for (int i = 0; i < Y_FM; ++i) acc1[i][j] = f32x4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
         bf16x8 ah[Y_FM], al[Y_FM];
 #pragma unroll
         for (int i = 0; i < Y_FM; ++i) {
@@ -584,20 +627,7 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
         }
         __builtin_amdgcn_s_setprio(0);
       }
-      {  // branch GEMM done: bias + ReLU from the last deconv stage (not refilled before the next step)
-        const float* bias = reinterpret_cast<const float*>(last + Y_A_BYTES + Y_B_BYTES);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 bv = *reinterpret_cast<const float4*>(bias + j * 16 + fq * 4);
-#pragma unroll
-          for (int i = 0; i < Y_FM; ++i) {
-            acc1[i][j][0] = fmaxf(acc1[i][j][0] + bv.x, 0.f);
-            acc1[i][j][1] = fmaxf(acc1[i][j][1] + bv.y, 0.f);
-            acc1[i][j][2] = fmaxf(acc1[i][j][2] + bv.z, 0.f);
-            acc1[i][j][3] = fmaxf(acc1[i][j][3] + bv.w, 0.f);
-          }
-        }
-      }
+      // branch GEMM done (its bias was the accumulators' start); the head chunks apply the ReLU
       // ---- head steps: branch channels 64t..64t+63 (acc1[.][4t .. 4t+3]) x 80 head rows
       static_assert(Y_HEAD_STEPS == 2, "head steps unrolled below");
       {
@@ -616,10 +646,6 @@ __global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a
         head_chunk(IC<3>{}, sa + NH * X_ROWB);
         __builtin_amdgcn_s_setprio(0);
       }
-#pragma unroll
-      for (int i = 0; i < Y_FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     {  // ---- tile done: head bias, fp32 store (lane: pixel fr, head rows 16u + 4fq .. +3)
       const int ct = t_lo + slot + c_k * nslot;
@@ -728,19 +754,35 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
     a.x[i] = nullptr; a.ldx[i] = a.offx[i] = a.cin[i] = 0; a.s[i] = 1; a.w[i] = nullptr; a.bias[i] = nullptr;
   }
   if ((H % S) || (W % S)) return (int)hipErrorInvalidValue;
-  // the kernel packs q-grid rows as (Yg << 16 | X) and addresses branch inputs with 32-bit element offsets
-  if ((long)B * (H / S) >= 32768 || W / S >= 65536) return (int)hipErrorInvalidValue;
-  for (int i = 0; i < nbr; ++i)
-    if ((long)B * (H / s[i]) * (W / s[i]) * ldx[i] >= (1L << 31)) return (int)hipErrorInvalidValue;
-  a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.out = (float*)out; a.ldo = ldo; a.nh = nh;
-  a.B = B; a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
+  // the kernel packs q-grid rows as (Yg << 16 | X) and reads branch inputs / weights through buffer
+  // resources with 32-bit byte offsets (< kOutOfRange): batches whose inputs exceed that run in chunks
+  if (W / S >= 65536 || (long)NH * 2 * nbr * CB * 2 >= (1L << 31)) return (int)hipErrorInvalidValue;
+  long per_frame_max = 0;
+  for (int i = 0; i < nbr; ++i) {
+    const long fb = (long)(H / s[i]) * (W / s[i]) * ldx[i] * 4;
+    per_frame_max = fb > per_frame_max ? fb : per_frame_max;
+    if ((long)s[i] * s[i] * CB * cin[i] * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;
+  }
+  int chunk = (int)(((1L << 31) - 1) / per_frame_max);
+  if ((long)(H / S) * chunk >= 32768) chunk = 32767 / (H / S);
+  if (chunk < 1) return (int)hipErrorInvalidValue;
+  a.wh = (const __hip_bfloat16*)wh; a.bh = bh; a.ldo = ldo; a.nh = nh;
+  a.H = H; a.W = W; a.S = S; a.nbr = nbr; a.nsteps = nsteps;
   const int nq = (H / S) * (W / S);
   if (pair)
     for (int i = 0; i < nbr; ++i)
       if ((ldx[i] & 7) || (offx[i] & 7)) return (int)hipErrorInvalidValue;
-  // grid: workgroup slots of the persistent kernel, one per CU
-  launch_neck_x3<8, 2>(a, B * nq, grid, pair, stream);
-  TCA_LAUNCH_CHECK();
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = B - b0 < chunk ? B - b0 : chunk;
+    for (int i = 0; i < nbr; ++i) a.x[i] = (const float*)x[i] + (long)b0 * (H / s[i]) * (W / s[i]) * ldx[i];
+    a.out = (float*)out + (long)b0 * H * W * ldo;
+    a.B = nb;
+    // grid: workgroup slots of the persistent kernel, one per CU
+    launch_neck_x3<8, 2>(a, (long)nb * nq, grid, pair, stream);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 }  // namespace
 

@@ -89,6 +89,13 @@ def main():
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--gpus", type=int, default=1, help="data-parallel ranks (one process per GPU)")
+    ap.add_argument("--engine", choices=["local", "remote"], default="local",
+                    help="remote: the reference's architecture -- the drivers are KServe clients (RemoteDetector2D / "
+                         "3D with their HIP pre/post on this GPU, main.py's default) of a server process started here "
+                         "with YOLOv5nCOCO + pointpillar_kitti on the same GPU")
+    ap.add_argument("--mode", choices=["sync", "async"], default="sync",
+                    help="remote: RPC mode (sync = the reference's blocking ModelInfer; async = -a)")
+    ap.add_argument("--wire", choices=["raw", "proto"], default="raw", help="remote: request codec")
     a = ap.parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:  # self-launch (a child: nothing has touched the GPU)
         import socket
@@ -114,6 +121,8 @@ def main():
     from triton_client_amd.cli.engines import maybe_data_parallel
 
     H, W = (int(v) for v in a.hw.split(","))
+    if a.engine == "remote":
+        return _remote(a, H, W)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.device == "cuda" and world > 1:
         a.device = f"cuda:{int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())}"
@@ -189,6 +198,122 @@ def main():
     if info is not None:
         from triton_client_amd.parallel.dp import shutdown
         shutdown(info)
+
+
+def _camera_messages(H, W, n):
+    from PIL import Image
+
+    from triton_client_amd.ros import msgs
+    from triton_client_amd.utils.synthetic import camera_frame
+
+    jpegs = []
+    for s in range(8):
+        buf = io.BytesIO()
+        Image.fromarray(camera_frame(H, W, s)).save(buf, format="JPEG", quality=90)
+        jpegs.append(buf.getvalue())
+    return [msgs.CompressedImage(header=msgs.Header(seq=i + 1, frame_id="cam"), format="jpeg", data=jpegs[i % 8])
+            for i in range(n)]
+
+
+def _cloud_messages(n):
+    from triton_client_amd.ros import compat, msgs
+    from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+
+    spec = LidarSpec(sensor_height=3.23)
+    clouds = [compat.create_cloud_xyzi(np.frombuffer(lidar_sweep(spec, s).tobytes(), np.float32).reshape(-1, 4))
+              for s in range(8)]
+    out = []
+    for i in range(n):
+        c = clouds[i % 8]
+        out.append(msgs.PointCloud2(header=msgs.Header(seq=i + 1, frame_id="os"), height=c.height, width=c.width,
+                                    fields=c.fields, is_bigendian=False, point_step=c.point_step, row_step=c.row_step,
+                                    data=c.data, is_dense=True))
+    return out
+
+
+def _remote(a, H, W):
+    """--engine remote: a KServe server process on this GPU; the drivers as its clients
+    (RemoteDetector2D / RemoteDetector3D on the GPU: main.py / main3d.py's default path)."""
+    import socket
+    import subprocess
+    from types import SimpleNamespace
+
+    import torch
+
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+    from triton_client_amd.clients import client_for_model
+    from triton_client_amd.inference.engines import RemoteDetector2D, RemoteDetector3D
+    from triton_client_amd.inference.ros_inference import RosInference
+    from triton_client_amd.inference.ros_inference3d import RosInference3D
+    from triton_client_amd.ros import msgs
+    from triton_client_amd.ros.bus import TopicBus
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    target = f"127.0.0.1:{port}"
+    proc = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+                             str(port), "--metrics-port", "0", "--models", "YOLOv5nCOCO,pointpillar_kitti"])
+    out = {"tool": "driver_bench", "engine": "remote", "mode": a.mode, "wire": a.wire, "batch": a.batch,
+           "workers": a.workers, "device": torch.cuda.get_device_name(0) if a.device.startswith("cuda") else a.device,
+           "server": "separate process, same GPU: YOLOv5nCOCO + pointpillar_kitti (fp32)"}
+    try:
+        def channel(model):
+            f = SimpleNamespace(model_name=model, model_version="", batch_size=1, verbose=False)
+            return GRPCChannel({"grpc_channel": target}, f, wait_ready_s=600.0)
+
+        bus = TopicBus()
+        window = 2 * a.batch * a.workers
+        if a.camera:
+            ch = channel("YOLOv5nCOCO")
+            cr = ch.get_metadata()["config_response"]
+            client = client_for_model("YOLOv5nCOCO", getattr(cr, "config", cr), a.device)
+            eng = RemoteDetector2D(ch, client, letterbox=False, conf_thres=0.3, mode=a.mode, wire=a.wire,
+                                   device=a.device)
+            warm = 2 * a.batch
+            ms = _camera_messages(H, W, warm + a.camera)
+            st = _Stages()
+            drv = RosInference(ch, client, engine=eng, params={"sub_topic": "/cam", "pub_topic": "/cam_out"},
+                               bus=bus, batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
+            drv.start_inference(spin=False)
+            _run(bus, "/cam", "/cam_out", msgs.Image, ms[:warm], window, a.timeout)
+            st.sum.clear(), st.n.clear()
+            n, dt, ok = _run(bus, "/cam", "/cam_out", msgs.Image, ms[warm:], window, a.timeout)
+            drv.stop()
+            live = eng.live()
+            out["camera"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
+                             "device_path": live is not None and live.stats["frames"] > 0,
+                             "input": f"CompressedImage JPEG {W}x{H} q90", "output": "annotated Image + Detection2DArray",
+                             "stages": st.summary()}
+            ch.close()
+        if a.lidar:
+            ch = channel("pointpillar_kitti")
+            cr = ch.get_metadata()["config_response"]
+            client = client_for_model("pointpillar_kitti", getattr(cr, "config", cr), a.device)
+            eng = RemoteDetector3D(ch, client, z_offset=1.5, mode=a.mode, wire=a.wire, device=a.device)
+            warm = 2 * a.batch
+            ms = _cloud_messages(warm + a.lidar)
+            st = _Stages()
+            drv = RosInference3D(ch, client, engine=eng, params={"sub_topic": "/pc", "pub_topic": "/pc_out"},
+                                 bus=bus, batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
+            drv.start_inference(spin=False)
+            _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, ms[:warm], window, a.timeout)
+            st.sum.clear(), st.n.clear()
+            n, dt, ok = _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, ms[warm:], window, a.timeout)
+            drv.stop()
+            out["lidar"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
+                            "device_voxeliser": str(getattr(eng.pre, "device", "cpu")),
+                            "input": f"PointCloud2 {ms[0].width} points x {ms[0].point_step} B",
+                            "output": "jsk BoundingBoxArray (label 2, score > 0.5)", "stages": st.summary()}
+            ch.close()
+        bus.close()
+        print(json.dumps(out), flush=True)
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(60)
+        except subprocess.TimeoutExpired:
+            proc.kill()
 
 
 if __name__ == "__main__":

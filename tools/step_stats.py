@@ -42,8 +42,26 @@ def main():
             tot[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             cnt[k] += 1
     ksum = sum(tot.values()) / n
+    # GPU-busy time: the union of the step's kernel intervals (any kernel running), and the
+    # idle gaps (no kernel on the device at all) inside the step
+    busy = []
+    for s, e in zip(starts[:-1], starts[1:]):
+        t_end = int(rows[e]["Start_Timestamp"])
+        iv = sorted((int(r["Start_Timestamp"]), min(int(r["End_Timestamp"]), t_end)) for r in rows[s:e])
+        u, cs, ce = 0, None, None
+        for b_, e_ in iv:
+            if cs is None or b_ > ce:
+                if cs is not None:
+                    u += ce - cs
+                cs, ce = b_, e_
+            else:
+                ce = max(ce, e_)
+        if cs is not None:
+            u += ce - cs
+        busy.append(u / 1e3)
     print(f"# {n} steps (marker {a.marker!r}); step span mean {sum(spans) / n:.1f} us "
-          f"(min {min(spans):.1f}, max {max(spans):.1f}); kernel time sum {ksum:.1f} us/step")
+          f"(min {min(spans):.1f}, max {max(spans):.1f}); kernel time sum {ksum:.1f} us/step; "
+          f"GPU busy (union of kernels) {sum(busy) / n:.1f} us/step = {100 * sum(busy) / sum(spans):.1f}% of the span")
     print(f"{'us/step':>9} {'share':>6} {'calls':>6}  kernel")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[: a.top]:
         print(f"{v / n:9.1f} {100 * v / n / ksum:5.1f}% {cnt[k] / n:6.1f}  {k}")

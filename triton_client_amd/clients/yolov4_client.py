@@ -5,6 +5,7 @@ re-implemented here per SURVEY Appendix A13)."""
 from __future__ import annotations
 
 import os
+import threading
 from typing import List, Optional
 
 import numpy as np
@@ -24,6 +25,7 @@ class Yolov4postprocess(Postprocess):
         self.input_hw = tuple(input_hw)
         self.device = torch.device(device)
         self._pp, self._up = {}, None
+        self.lock = threading.RLock()  # the device path's workspaces: one caller at a time
 
     def load_class_names(self, namesfile: Optional[str] = None) -> List[str]:
         return Postprocess.load_class_names(namesfile or os.path.join(DATA, "coco.names"))

@@ -3,6 +3,7 @@
 from __future__ import annotations
 
 import os
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -50,6 +51,9 @@ class Yolov5postprocess(Postprocess):
         self.device = torch.device(device)
         self._pp = {}
         self._up = None
+        # the device path's workspaces (candidates, NMS buffers) are reused: one caller at a time,
+        # held until its results have been read (RemoteLiveCamera holds it across the annotation)
+        self.lock = threading.RLock()
 
     def load_class_names(self, namesfile: Optional[str] = None) -> List[str]:
         return Postprocess.load_class_names(namesfile or os.path.join(DATA, "coco.names"))
@@ -80,9 +84,10 @@ class Yolov5postprocess(Postprocess):
         list entry means no detections (the reference returned the exception)."""
         pred = self._pred(prediction)
         if self.device.type == "cuda":
-            res = self.extract_boxes_device([pred], conf_thres, iou_thres, classes=classes, agnostic=agnostic,
-                                            multi_label=multi_label, max_det=max_det)
-            return detections_nx6(res)
+            with self.lock:
+                res = self.extract_boxes_device([pred], conf_thres, iou_thres, classes=classes, agnostic=agnostic,
+                                                multi_label=multi_label, max_det=max_det)
+                return detections_nx6(res)
         pp = self._post(pred.shape[2] - 5, conf_thres, iou_thres, classes, agnostic, multi_label, max_det, "cpu")
         return detections_nx6(pp.postprocess_decoded(pred))
 

@@ -692,6 +692,10 @@ class _RemoteBase:
         if wire not in ("raw", "proto", "shm", "devshm"):
             raise ValueError(f"wire {wire!r}")
         self.channel, self.client, self.mode, self.wire, self.window = channel, client, mode, wire, window
+        # the client's staging (pinned buffers, shared-memory slots) is reused from call to call:
+        # concurrent driver workers take turns on it; their RPCs still overlap
+        self._stage_lock = threading.Lock()
+        self._shm_lock = threading.Lock()
         md = channel.get_metadata()
         cfg = md["config_response"]
         self.model_metadata = md["metadata_response"]
@@ -982,24 +986,28 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         from ..utils.trace import trace_range
         timer = getattr(self, "timer", None)
         if self.wire in ("shm", "devshm"):
-            return self._detect_shm(frames)
+            with self._shm_lock:
+                return self._detect_shm(frames)
         if self.wire == "raw" and self.mode != "stream":
             # prepare + encode frame by frame: the staging buffer is reused, each
             # request's bytes are complete before the next frame is prepared
             xfs, raws = [], []
             for i, f in enumerate(frames):
-                with trace_range("preprocess"), _stage(timer, "preprocess"):
-                    a, xf = self._prep(f)
-                with _stage(timer, "encode"):
-                    raws.append(self._encode([(self.input_name, self.dtype, a)], self.requested, str(i)))
+                with self._stage_lock:
+                    with trace_range("preprocess"), _stage(timer, "preprocess"):
+                        a, xf = self._prep(f)
+                    with _stage(timer, "encode"):
+                        raws.append(self._encode([(self.input_name, self.dtype, a)], self.requested, str(i)))
                 xfs.append(xf)
             with trace_range("rpc"), _stage(timer, "rpc"):
                 resps = self._send(raws)
             preps = [(None, xf) for xf in xfs]
         else:
-            with trace_range("preprocess"):
-                preps = [self._prep(f) for f in frames]
-            preps = [(a.numpy() if isinstance(a, torch.Tensor) else a, xf) for a, xf in preps]
+            preps = []
+            for f in frames:
+                with self._stage_lock, trace_range("preprocess"):
+                    a, xf = self._prep(f)
+                    preps.append((a.numpy().copy() if isinstance(a, torch.Tensor) else a, xf))
             with trace_range("rpc"):
                 resps = self._run([[(self.input_name, self.dtype, a)] for a, _ in preps], self.requested)
         out = []
@@ -1058,13 +1066,14 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
         dts = {key: spec["dtype"] for key, spec in zip(keys, self.inputs)}
         raws, keep = [], []
         for i, c in enumerate(clouds):
-            with _stage(timer, "preprocess"):
-                d = self.pre.filter_cloud_gpu(c, self.normalize, self.z_offset, dts)
-            if d["voxels"].shape[0] == 0:
-                continue
-            with _stage(timer, "encode"):
-                raws.append(self._encode([(spec["name"], spec["dtype"], d[key]) for key, spec in zip(keys, self.inputs)],
-                                         self.out_names, str(i)))
+            with self._stage_lock:  # the voxeliser's pinned staging is read by the encoder
+                with _stage(timer, "preprocess"):
+                    d = self.pre.filter_cloud_gpu(c, self.normalize, self.z_offset, dts)
+                if d["voxels"].shape[0] == 0:
+                    continue
+                with _stage(timer, "encode"):
+                    raws.append(self._encode([(spec["name"], spec["dtype"], d[key])
+                                              for key, spec in zip(keys, self.inputs)], self.out_names, str(i)))
             keep.append(i)
         with _stage(timer, "rpc"):
             resps = self._send(raws)
@@ -1152,7 +1161,8 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
         if self.wire == "devshm" and not gpu_pre:
             raise ValueError("wire='devshm' needs the GPU preprocess (device='cuda')")
         if self.wire in ("shm", "devshm") and gpu_pre:
-            keep, resps = self._detect_gpu_shm(clouds)
+            with self._shm_lock:
+                keep, resps = self._detect_gpu_shm(clouds)
             return self._outputs(clouds, keep, resps)
         if self.wire == "raw" and self.mode != "stream" and gpu_pre:
             keep, resps = self._detect_gpu_raw(clouds)
@@ -1160,7 +1170,8 @@ class RemoteDetector3D(_RemoteBase, Detector3D):
         batches, empty = [], []
         for c in clouds:
             pts = cloud_to_numpy(c, normalize_intensity=self.normalize, z_offset=self.z_offset)
-            d = self.pre.filter_pc(pts)
+            with self._stage_lock:
+                d = self.pre.filter_pc(pts)
             empty.append(len(d["voxels"]) == 0)
             batches.append([(spec["name"], spec["dtype"],
                              np.ascontiguousarray(d[_voxel_key(spec["name"], k)].astype(_NP_OF[spec["dtype"]])))

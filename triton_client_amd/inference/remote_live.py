@@ -188,7 +188,7 @@ class RemoteLiveCamera:
             torch.cuda.current_stream(self.device).synchronize()  # the inputs are in host memory
         with trace_range("remote_rpc"):
             responses = self._rpc(inputs)
-        with self.lock, trace_range("remote_postprocess"):
+        with getattr(self.det.post, "lock", self.lock), trace_range("remote_postprocess"):
             res = self._post(responses, xf)
             if draw:
                 draw_annotations_(frames, res.box, res.score, res.cls, res.count, self._names_dev(names),
