@@ -737,7 +737,8 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   if (B <= 0) return 0;
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
-  if (variant != 0 && variant != 3) return (int)hipErrorInvalidValue;  // 0 / 3: the one tiling
+  // 0 (also accepted as 3, its former number): <8 waves, 2 stages>; 1: <8, 3> (two K steps in flight)
+  if (variant != 0 && variant != 3 && variant != 1) return (int)hipErrorInvalidValue;
   NeckArgsX3 a;
   int S = 1, nsteps = 0;
   for (int i = 0; i < nbr; ++i) {
@@ -778,7 +779,8 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
     a.out = (float*)out + (long)b0 * H * W * ldo;
     a.B = nb;
     // grid: workgroup slots of the persistent kernel, one per CU
-    launch_neck_x3<8, 2>(a, (long)nb * nq, grid, pair, stream);
+    if (variant == 1) launch_neck_x3<8, 3>(a, (long)nb * nq, grid, pair, stream);
+    else launch_neck_x3<8, 2>(a, (long)nb * nq, grid, pair, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
   }

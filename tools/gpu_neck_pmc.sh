@@ -9,8 +9,8 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
             "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   rm -rf /tmp/npmc$i
-  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/npmc$i -o run -- python tools/bench_neck.py 32 3 > gpurun_out/pmc/neck_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/neck_p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/npmc$i -o run -- python tools/bench_neck.py 32 0 > gpurun_out/pmc/neck_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/neck_p$i.log; exit 1; }
   f=$(find /tmp/npmc$i -name "*counter_collection.csv" | head -1)
-  cp $f gpurun_out/pmc/neck_v3_p$i.csv
+  cp $f gpurun_out/pmc/neck_r5_p$i.csv
 done
-python tools/pmc_summary.py bev_neck_head_x3 gpurun_out/pmc/neck_v3_p*.csv > gpurun_out/pmc_neck_v3.md && tail -6 gpurun_out/pmc_neck_v3.md
+python tools/pmc_summary.py bev_neck_head_x3 gpurun_out/pmc/neck_r5_p*.csv > gpurun_out/pmc_neck_r5.md && tail -6 gpurun_out/pmc_neck_v3.md
