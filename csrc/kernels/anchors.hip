@@ -145,6 +145,67 @@ __global__ void __launch_bounds__(256) anchor_decode_kernel(
   }
 }
 
+// Pixel-major form of the same filter for an fp32 NHWC head (the fused neck's output):
+// one thread per BEV pixel loads all A * C class logits of the pixel with 16-B loads
+// (A * C = 18 for KITTI's 3 classes x 2 rotations: four float4 + one float2), so each
+// thread has every load of its pixel in flight at once instead of a dependent chain of
+// C scalar loads per anchor; the per-anchor max / sigmoid / threshold and the LDS-staged
+// compaction + decode are the anchor kernel's, so the candidate set is identical.
+template <int A, int C>
+__global__ void __launch_bounds__(256) anchor_decode_px_kernel(
+    const float* __restrict__ cls, const float* __restrict__ box, const float* __restrict__ dir, int H, int W,
+    int bins, int ld_cls, int ld_box, int ld_dir, AnchorTable tb, float x0, float xs, float y0, float ys,
+    float dir_offset, float dir_limit_offset, float score_thresh, float* __restrict__ cand_box,
+    float* __restrict__ cand_score, int* __restrict__ cand_label, uint64_t* __restrict__ cand_key,
+    int* __restrict__ cand_count, int cap) {
+  constexpr int N = A * C, NV = N / 4;
+  static_assert(256 * A <= kStage, "stage");
+  __shared__ int s_idx[256 * A];
+  __shared__ float s_score[256 * A];
+  __shared__ int s_label[256 * A];
+  __shared__ int s_cnt, s_base;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int px = blockIdx.x * 256 + threadIdx.x;
+  if (px < H * W) {
+    const float* src = cls + ((long)b * H * W + px) * ld_cls;
+    float v[N];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const float4 t = reinterpret_cast<const float4*>(src)[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+#pragma unroll
+    for (int q = 4 * NV; q < N; ++q) v[q] = src[q];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      float best = -INFINITY;
+      int bc = 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (v[a * C + c] > best) { best = v[a * C + c]; bc = c; }
+      const float score = sigmoidf_(best);
+      if (score < score_thresh) continue;
+      const int slot = atomicAdd(&s_cnt, 1);  // < 256 * A: every anchor of the block fits
+      s_idx[slot] = px * A + a;
+      s_score[slot] = score;
+      s_label[slot] = bc + 1;
+    }
+  }
+  __syncthreads();
+  const int n = s_cnt;
+  if (threadIdx.x == 0) s_base = n ? atomicAdd(&cand_count[b], n) : 0;
+  __syncthreads();
+  const int base_slot = s_base;
+  for (int k = threadIdx.x; k < n; k += 256) {
+    const int slot = base_slot + k;
+    if (slot >= cap) break;
+    decode_write(box, dir, 1, H, W, A, bins, ld_box, ld_dir, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset, b,
+                 s_idx[k], s_score[k], s_label[k], (long)b * cap + slot, cand_box, cand_score, cand_label, cand_key);
+  }
+}
+
 // ---- exact top-k threshold over all anchors (proposal layers) -------------------
 // SECONDHead's proposal layer keeps the top NMS_PRE_MAXSIZE (1024) of all
 // 211,200 anchors by max class logit, with no score threshold.  Decoding and
@@ -295,6 +356,15 @@ static int anchor_decode_launch(const void* cls, const void* box, const void* di
     for (int k = 0; k < 6; ++k) tb.v[a][k] = a < A ? table[a * 6 + k] : 0.f;
   int e = zero_i32_async(cand_count, batch, stream);
   if (e) return e;
+  const int ldc = ld_cls > 0 ? ld_cls : A * C;
+  if (dtype == kF32 && layout == 1 && !key_thr && A == 6 && C == 3 && (ldc & 3) == 0 &&
+      ((uintptr_t)cls & 15) == 0) {  // KITTI PointPillars / SECOND head, fp32 NHWC
+    anchor_decode_px_kernel<6, 3><<<dim3((H * W + 255) / 256, batch), 256, 0, stream>>>(
+        (const float*)cls, (const float*)box, (const float*)dir, H, W, bins, ldc, ld_box > 0 ? ld_box : A * 7,
+        ld_dir > 0 ? ld_dir : A * bins, tb, x0, xs, y0, ys, dir_offset, dir_limit_offset, score_thresh, cand_box,
+        cand_score, cand_label, cand_key, cand_count, cap);
+    TCA_LAUNCH_CHECK();
+  }
   dim3 grid((H * W * A + kAnchorsPerBlock - 1) / kAnchorsPerBlock, batch);
 #define LAUNCH(T)                                                                                              \
   anchor_decode_kernel<T><<<grid, 256, 0, stream>>>((const T*)cls, (const T*)box, (const T*)dir, layout, H, W, A, C, \

@@ -460,18 +460,22 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
     }
   }
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 hreg[HPL];
-  auto halo_load = [&](int ph, int c) {  // ph: runtime-uniform phase
+  // two register sets: phase-chunk q's halo lives in hreg[q & 1] (= its phase's parity, a compile-time
+  // index below), loaded three phases ahead so each load has two phases of MFMAs to land in
+  u32x4 hreg[2][HPL];
+  auto halo_load = [&](int ph, int c, auto SL) {  // ph: runtime-uniform phase
+    constexpr int sl = decltype(SL)::value;
     const int so = c * 128 + (ph >> 1) * dl + (ph & 1) * df;
 #pragma unroll
     for (int k = 0; k < HPL; ++k)
-      hreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, ((h_ph[k] >> ph) & 1u) ? h_off[k] : kOutOfRange, so, 0);
+      hreg[sl][k] = __builtin_amdgcn_raw_buffer_load_b128(rin, ((h_ph[k] >> ph) & 1u) ? h_off[k] : kOutOfRange, so, 0);
   };
-  auto halo_write = [&](int buf) {
+  auto halo_write = [&](int buf, auto SL) {
+    constexpr int sl = decltype(SL)::value;
     unsigned char* dst = smem + buf * HBYTES;
 #pragma unroll
     for (int k = 0; k < HPL; ++k)
-      if (k + 1 < HPL || h_lds[k] >= 0) *reinterpret_cast<u32x4*>(dst + h_lds[k]) = hreg[k];
+      if (k + 1 < HPL || h_lds[k] >= 0) *reinterpret_cast<u32x4*>(dst + h_lds[k]) = hreg[sl][k];
   };
 
   const int NG = a.N / 16, g0 = (n0 + wn * FN * 16) / 16;
@@ -514,22 +518,24 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
     }
   }
   bf16x8 w0[2][FN][2], w1[2][FN][2];
-  halo_load(0, 0);
+  halo_load(0, 0, IC<0>{});
   gload(IC<0>{}, 0, w0);
-  halo_write(0);
-  halo_load(1, 0);
+  halo_write(0, IC<0>{});
+  halo_load(1, 0, IC<1>{});                                    // q = 1
+  halo_load(4 * nc > 2 ? 2 : 4 * nc - 1, 0, IC<0>{});          // q = 2 (nc >= 1: 4 phases per chunk)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
   const int fr = lane & 15, fq = lane >> 4;
-  // phase-chunk q = 4 c + ph lives in halo buffer q & 1 = ph & 1
-  auto phase_end = [&](int ph, int c) {
+  // phase-chunk q = 4 c + ph lives in halo buffer q & 1 = ph & 1 and, before that, in register set ph & 1
+  auto phase_end = [&](auto PH, int c) {
+    constexpr int ph = decltype(PH)::value;
     const int q = 4 * c + ph;
     if (q + 1 < 4 * nc) {
-      halo_write((ph + 1) & 1);
-      const int q2 = q + 2 < 4 * nc ? q + 2 : 4 * nc - 1;
-      halo_load(q2 & 3, q2 >> 2);
+      halo_write((ph + 1) & 1, IC<(ph + 1) & 1>{});
+      const int q3 = q + 3 < 4 * nc ? q + 3 : 4 * nc - 1;
+      halo_load(q3 & 3, q3 >> 2, IC<(ph + 1) & 1>{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -565,7 +571,7 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
         }
       }
     }
-    if constexpr (S::LAST_OF_PHASE) phase_end(S::PH, c);
+    if constexpr (S::LAST_OF_PHASE) phase_end(IC<S::PH>{}, c);
   };
   for (int c = 0; c < nc; ++c) {
     group(IC<0>{}, c, w0, w1);

@@ -317,6 +317,41 @@ def test_anchor_postprocess_gpu_vs_cpu(cuda):
     np.testing.assert_array_equal(got.cls[0, :k].cpu().numpy(), ref.cls[0, :k].numpy())
 
 
+def test_anchor_postprocess_merged_head_fast_path(cuda):
+    """The merged fp32 NHWC head (the fused neck's output, cls / box / dir channel slices of
+    one [B, H, W, 72] buffer) takes the pixel-major decode (anchors.hip
+    anchor_decode_px_kernel): same candidates as the anchor-major kernel on the same data,
+    and the same detections as the CPU reference."""
+    from triton_client_amd.ops.conv import NHWC
+
+    cfg = PointPillarsConfig()
+    ap_c = AnchorPostprocess(cfg, 2, device="cpu")
+    ap_g = AnchorPostprocess(cfg, 2, device=cuda)
+    H, W, A, C = ap_c.H, ap_c.W, ap_c.A, ap_c.C
+    g = torch.Generator().manual_seed(1)
+    head = torch.cat([torch.randn(2, H, W, A * C, generator=g) - 3.5, torch.randn(2, H, W, A * 7, generator=g) * 0.1,
+                      torch.randn(2, H, W, A * 2, generator=g)], -1)
+    assert head.shape[-1] == 72
+    hd = head.to(cuda)
+    views = (NHWC(hd, 0, A * C), NHWC(hd, A * C, A * 7), NHWC(hd, A * 8, A * 2))
+    fast = ap_g(*views)
+    torch.cuda.synchronize()
+    fast = [t.clone() for t in (fast.box, fast.score, fast.cls, fast.count)]
+    # the anchor-major kernel on the same data: separate channels_last tensors (ld = A * C, no fast path)
+    nchw = head.permute(0, 3, 1, 2)
+    slow = ap_g(*(nchw[:, a:b].to(cuda).contiguous(memory_format=torch.channels_last)
+                  for a, b in ((0, A * C), (A * C, A * 8), (A * 8, A * 10))))
+    torch.cuda.synchronize()
+    for x, y in zip(fast, (slow.box, slow.score, slow.cls, slow.count)):
+        assert torch.equal(x, y)
+    ref = ap_c.cpu(nchw[:, :A * C], nchw[:, A * C:A * 8], nchw[:, A * 8:])
+    for b in range(2):
+        n_r, n_g = int(ref.count[b]), int(fast[3][b])
+        assert n_r > 10 and abs(n_r - n_g) <= 2
+        k = min(n_r, n_g, 50)
+        np.testing.assert_allclose(fast[0][b, :k].cpu().numpy(), ref.box[b, :k].numpy(), rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("cin,cout,k,s,p,act", [
     (16, 32, 3, 2, 1, 2), (32, 32, 3, 1, 1, 2), (64, 64, 3, 1, 1, 1), (64, 128, 3, 2, 1, 1),
     (128, 256, 1, 1, 0, 2), (24, 16, 1, 1, 0, 0), (8, 16, 6, 2, 2, 2), (256, 72, 1, 1, 0, 0)])

@@ -13,4 +13,4 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   f=$(find /tmp/npmc$i -name "*counter_collection.csv" | head -1)
   cp $f gpurun_out/pmc/neck_r5_p$i.csv
 done
-python tools/pmc_summary.py bev_neck_head_x3 gpurun_out/pmc/neck_r5_p*.csv > gpurun_out/pmc_neck_r5.md && tail -6 gpurun_out/pmc_neck_v3.md
+python tools/pmc_summary.py bev_neck_head_x3 gpurun_out/pmc/neck_r5_p*.csv > gpurun_out/pmc_neck_r5.md && tail -6 gpurun_out/pmc_neck_r5.md

@@ -34,7 +34,7 @@ def main():
     d = []
     if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "GRBM_GUI_ACTIVE" in m:
         d.append(f"MFMA busy: {100 * m['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * m['GRBM_GUI_ACTIVE'] / 8):.1f}%")
-    if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
+    if "SQ_INSTS_VALU" in m and m.get("SQ_INSTS_MFMA"):
         d.append(f"non-MFMA VALU per MFMA: {(m['SQ_INSTS_VALU'] - m['SQ_INSTS_MFMA']) / m['SQ_INSTS_MFMA']:.2f}")
     if all(k in m for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES")):
         w = m["SQ_WAVE_CYCLES"]

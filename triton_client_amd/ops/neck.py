@@ -75,8 +75,9 @@ class FusedNeckHead:
         if grid <= 0:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
-        # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = the one measured-best tiling
-        self.variant = 0
+        # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 1 = <8 waves, 3 stages> (977 vs 1061 us for
+        # 0 = <8, 2> at batch 32 once the DMA issue moved to buffer resources, profiles/r5/neck_ab.log)
+        self.variant = 1
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
             self.wh = split_pairs(wh).to(device)
