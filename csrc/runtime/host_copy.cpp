@@ -7,9 +7,19 @@
 // the pinned slot the H2D DMA reads — split into ~1 MiB chunks over a few
 // std::threads so one batch (32 x 1.9 MB clouds) is not one core's memcpy,
 // and called through ctypes, i.e. without the GIL.
+//
+// Large pieces are copied with non-temporal (streaming) stores: the destination is
+// a page-locked staging slot that only the DMA engine reads next, so filling the CPU
+// caches with it (and reading every destination line first, the write-allocate of an
+// ordinary store) only costs memory bandwidth -- the budget rank 0 spends feeding the
+// node's GPUs through the shared host ring (tools/fanout_bench.py).  TCA_HOST_COPY_NT=0
+// turns it off (plain memcpy) for A/B runs.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -18,7 +28,37 @@
 
 namespace {
 constexpr int64_t kChunk = 1 << 20;
+constexpr int64_t kStreamMin = 64 << 10;  // pieces below this keep memcpy
+
+__attribute__((target("avx2"))) void copy_stream(char* d, const char* s, int64_t n) {
+  int64_t head = (int64_t)((32 - ((uintptr_t)d & 31)) & 31);
+  if (head > n) head = n;
+  std::memcpy(d, s, (size_t)head);
+  d += head;
+  s += head;
+  n -= head;
+  const int64_t body = n & ~(int64_t)127;
+  for (int64_t i = 0; i < body; i += 128) {
+    const __m256i a0 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+    const __m256i a1 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+    const __m256i a2 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+    const __m256i a3 = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a0);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), a1);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), a2);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), a3);
+  }
+  std::memcpy(d + body, s + body, (size_t)(n - body));
 }
+
+bool use_stream() {
+  static const bool on = [] {
+    const char* e = std::getenv("TCA_HOST_COPY_NT");
+    return !(e && e[0] == '0') && __builtin_cpu_supports("avx2");
+  }();
+  return on;
+}
+}  // namespace
 
 // n copies dst[i] <- src[i] of nbytes[i]; returns 0, or -1 on a bad argument.
 TCA_API int tca_host_gather_copy(int n, void* const* dst, const void* const* src, const int64_t* nbytes,
@@ -40,8 +80,18 @@ TCA_API int tca_host_gather_copy(int n, void* const* dst, const void* const* src
   const int t = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(nthreads, 1),
                                                               (int64_t)pieces.size(), total / (4 * kChunk) + 1}));
   std::atomic<size_t> next{0};
+  const bool nt = use_stream();
   auto work = [&] {
-    for (size_t k; (k = next.fetch_add(1)) < pieces.size();) std::memcpy(pieces[k].d, pieces[k].s, pieces[k].len);
+    bool streamed = false;
+    for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+      if (nt && pieces[k].len >= kStreamMin) {
+        copy_stream(pieces[k].d, pieces[k].s, pieces[k].len);
+        streamed = true;
+      } else {
+        std::memcpy(pieces[k].d, pieces[k].s, pieces[k].len);
+      }
+    }
+    if (streamed) _mm_sfence();  // this thread's streaming stores are globally visible before it joins
   };
   std::vector<std::thread> pool;
   pool.reserve(t - 1);

@@ -333,18 +333,19 @@ def test_anchor_postprocess_merged_head_fast_path(cuda):
                       torch.randn(2, H, W, A * 2, generator=g)], -1)
     assert head.shape[-1] == 72
     hd = head.to(cuda)
-    views = (NHWC(hd, 0, A * C), NHWC(hd, A * C, A * 7), NHWC(hd, A * 8, A * 2))
+    cb, cd = A * C, A * C + A * 7  # channel offsets of box and dir in the merged head
+    views = (NHWC(hd, 0, A * C), NHWC(hd, cb, A * 7), NHWC(hd, cd, A * 2))
     fast = ap_g(*views)
     torch.cuda.synchronize()
     fast = [t.clone() for t in (fast.box, fast.score, fast.cls, fast.count)]
     # the anchor-major kernel on the same data: separate channels_last tensors (ld = A * C, no fast path)
     nchw = head.permute(0, 3, 1, 2)
     slow = ap_g(*(nchw[:, a:b].to(cuda).contiguous(memory_format=torch.channels_last)
-                  for a, b in ((0, A * C), (A * C, A * 8), (A * 8, A * 10))))
+                  for a, b in ((0, cb), (cb, cd), (cd, cd + A * 2))))
     torch.cuda.synchronize()
     for x, y in zip(fast, (slow.box, slow.score, slow.cls, slow.count)):
         assert torch.equal(x, y)
-    ref = ap_c.cpu(nchw[:, :A * C], nchw[:, A * C:A * 8], nchw[:, A * 8:])
+    ref = ap_c.cpu(nchw[:, :cb], nchw[:, cb:cd], nchw[:, cd:])
     for b in range(2):
         n_r, n_g = int(ref.count[b]), int(fast[3][b])
         assert n_r > 10 and abs(n_r - n_g) <= 2

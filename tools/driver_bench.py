@@ -273,7 +273,7 @@ def _remote(a, H, W):
             warm = 2 * a.batch
             ms = _camera_messages(H, W, warm + a.camera)
             st = _Stages()
-            drv = RosInference(ch, client, engine=eng, params={"sub_topic": "/cam", "pub_topic": "/cam_out"},
+            drv = RosInference(None, client, engine=eng, params={"sub_topic": "/cam", "pub_topic": "/cam_out"},
                                bus=bus, batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
             drv.start_inference(spin=False)
             _run(bus, "/cam", "/cam_out", msgs.Image, ms[:warm], window, a.timeout)
@@ -294,7 +294,7 @@ def _remote(a, H, W):
             warm = 2 * a.batch
             ms = _cloud_messages(warm + a.lidar)
             st = _Stages()
-            drv = RosInference3D(ch, client, engine=eng, params={"sub_topic": "/pc", "pub_topic": "/pc_out"},
+            drv = RosInference3D(None, client, engine=eng, params={"sub_topic": "/pc", "pub_topic": "/pc_out"},
                                  bus=bus, batch=a.batch, workers=a.workers, metrics=st, queue_size=window)
             drv.start_inference(spin=False)
             _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, ms[:warm], window, a.timeout)
