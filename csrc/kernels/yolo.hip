@@ -138,7 +138,82 @@ __global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layo
   }
 }
 
+// Decode only (the ONNX YOLOv5 output [B, N, 5 + nc], what a served YOLOv5 returns): every
+// output element is a function of one head element, so thread = 4 consecutive output floats
+// (one 16-B store; consecutive threads write consecutive bytes) and the reads walk each row's
+// channels in order.  yolo_filter_kernel's decoded path (thread = row) wrote 85 floats per
+// thread at a 340-B stride across the wave, one cache line per lane per store.
+template <typename T>
+__global__ void __launch_bounds__(256) yolo_decode_kernel(YoloHeads hd, int layout, int na, int nc, long total4,
+                                                          float* __restrict__ decoded) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total4) return;
+  const int no = nc + 5, C = na * no;
+  const int n0 = na * hd.h[0] * hd.w[0], n1 = na * hd.h[1] * hd.w[1], n2 = na * hd.h[2] * hd.w[2];
+  const long N = (long)n0 + n1 + n2;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long f = q * 4 + e;
+    const long row = f / no;
+    const int c = (int)(f - row * no);
+    const int b = (int)(row / N);
+    int rem = (int)(row - (long)b * N), l = 0;
+    if (rem >= n0) { rem -= n0; l = 1; if (rem >= n1) { rem -= n1; l = 2; } }
+    const int H = hd.h[l], W = hd.w[l];
+    const int a = rem / (H * W), yx = rem - a * (H * W);
+    const T* hp = (const T*)hd.head[l];
+    const long idx = layout == 0 ? ((long)b * C + (long)a * no + c) * H * W + yx
+                                 : ((long)b * H * W + yx) * hd.ldc[l] + (long)a * no + c;
+    const float s = sigmoidf_(ld(hp, idx));
+    const float st = (float)hd.stride[l];
+    const int y = yx / W, x = yx - y * W;
+    switch (c) {
+      case 0: v[e] = (s * 2.f - 0.5f + (float)x) * st; break;
+      case 1: v[e] = (s * 2.f - 0.5f + (float)y) * st; break;
+      case 2: v[e] = (s * 2.f) * (s * 2.f) * hd.anchor[l][a][0]; break;
+      case 3: v[e] = (s * 2.f) * (s * 2.f) * hd.anchor[l][a][1]; break;
+      default: v[e] = s;
+    }
+  }
+  *reinterpret_cast<float4*>(decoded + q * 4) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 }  // namespace
+
+TCA_API int tca_yolo_decode(const void* head0, const void* head1, const void* head2, int dtype, int layout, int batch,
+                            int na, int nc, const int* hw /*[6]*/, const int* strides /*[3]*/,
+                            const int* ldc /*[3] or null*/, const float* anchors /*[3][na][2] host*/, float* decoded,
+                            hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (na > 4 || na <= 0) return (int)hipErrorInvalidValue;
+  YoloHeads hd;
+  hd.head[0] = head0; hd.head[1] = head1; hd.head[2] = head2;
+  long N = 0;
+  for (int l = 0; l < 3; ++l) {
+    hd.h[l] = hw[2 * l]; hd.w[l] = hw[2 * l + 1]; hd.stride[l] = strides[l];
+    hd.ldc[l] = ldc ? ldc[l] : na * (nc + 5);
+    for (int a = 0; a < 4; ++a) {
+      hd.anchor[l][a][0] = a < na ? anchors[(l * na + a) * 2] : 0.f;
+      hd.anchor[l][a][1] = a < na ? anchors[(l * na + a) * 2 + 1] : 0.f;
+    }
+    N += (long)na * hd.h[l] * hd.w[l];
+  }
+  const long total = (long)batch * N * (nc + 5);
+  if (total % 4 != 0 || ((uintptr_t)decoded & 15) != 0) return (int)hipErrorInvalidValue;  // 16-B stores
+  const long total4 = total / 4;
+  const int bs = 256;
+  const unsigned grid = (unsigned)((total4 + bs - 1) / bs);
+  switch (dtype) {
+    case kF32: yolo_decode_kernel<float><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded); break;
+    case kF16: yolo_decode_kernel<__half><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded); break;
+    case kBF16:
+      yolo_decode_kernel<__hip_bfloat16><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded);
+      break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  TCA_LAUNCH_CHECK();
+}
 
 TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const void* head2, int dtype, int layout,
                                    int batch, int na, int nc, const int* hw /*[6]*/, const int* strides /*[3]*/,

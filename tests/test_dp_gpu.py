@@ -156,7 +156,7 @@ def _family_worker(rank, world, port, q, family):
         os._exit(1)
 
 
-@pytest.mark.parametrize("family", ["centerpoint", "retinanet", "fcos", "yolov4"])
+@pytest.mark.parametrize("family", ["centerpoint", "second_iou", "retinanet", "fcos", "yolov4"])
 def test_dp_families_two_ranks(cuda, family):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -167,6 +167,8 @@ def test_yolo_postprocess_gpu_vs_cpu(cuda):
         res, dec = pp_gpu(hg, decoded_out=True)
         torch.cuda.synchronize()
         np.testing.assert_allclose(dec.cpu().numpy(), pp_cpu.decode_cpu(hs).numpy(), rtol=1e-4, atol=1e-3)
+        dec = dec.clone()
+        assert torch.equal(pp_gpu.decode(hg), dec)  # decode-only kernel (served output): same formulas
         for b in range(B):
             n = int(ref.count[b])
             assert int(res.count[b]) == n and n > 0

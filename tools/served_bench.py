@@ -60,6 +60,9 @@ def main(argv=None):
     ap.add_argument("--target", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--server-procs", type=int, default=1, help="server processes sharing the port (--procs)")
+    ap.add_argument("--client-hw-queues", type=int, default=0,
+                    help="multi-process runs: GPU_MAX_HW_QUEUES of each client process (0: HIP's default); fewer "
+                         "queues per client leave more of the hardware scheduler's mapped queues to the server")
     ap.add_argument("--server-profile", default=None, metavar="JSON",
                     help="multi-process runs: the server's stage clock (TCA_SERVER_PROFILE) written here")
     a = ap.parse_args(argv)
@@ -261,11 +264,13 @@ def multi_proc(a) -> int:
               "--cam", a.cam, "--rings", str(a.rings), "--columns", str(a.columns), "--wire", a.wire,
               "--target", target] + (["--burst"] if a.burst else [])
     clients = []
+    cenv = dict(os.environ, **({"GPU_MAX_HW_QUEUES": str(a.client_hw_queues)} if a.client_hw_queues > 0 else {}))
     try:
         for p in range(a.client_procs):
             for role in ("camera", "lidar"):
                 clients.append(subprocess.Popen([sys.executable, here, "--role", role, "--seed", str(p)] + common,
-                                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True))
+                                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                                                env=cenv))
         for c in clients:
             line = c.stdout.readline()
             if line.strip() != "READY":
@@ -328,7 +333,8 @@ def multi_proc(a) -> int:
             "host_cpu_cores_busy": round(cpu_cores, 2), "host_cpus_in_affinity": cpu_avail,
             "topology": (f"{a.server_procs} server process{'es' if a.server_procs > 1 else ''} + {a.client_procs} camera "
                          f"and {a.client_procs} LiDAR client processes"),
-            "wire": a.wire, "window_mode": "burst" if a.burst else "sliding",
+            "wire": a.wire, "window_mode": "burst" if a.burst else "sliding", "server_workers": a.workers,
+            "client_hw_queues": a.client_hw_queues or None,
             "path": {"raw": "tensors inside the gRPC messages (C++ codec both ends)",
                      "shm": "GPU preprocess -> page-locked /dev/shm slot -> region references in the message -> "
                             "server DMA from / into the client's slot",

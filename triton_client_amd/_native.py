@@ -42,6 +42,7 @@ _KERNEL_SIGS = {
     # x[3], ldx[3], x_off[3], cin[3], hw[6], w[3], bias[3], strides[3], anchors, B, na, nc, conf, class_mask,
     # cand box, score, cls, key, count, cap, stream
     "tca_yolo_detect_filter": [P, P, P, P, P, P, P, P, P, I, I, I, F, P, P, P, P, P, P, I, P],
+    "tca_yolo_decode": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
     "tca_yolo_decode_filter": [P, P, P, I, I, I, I, I, P, P, P, P, F, I, P, P, P, P, P, P, I, P, P],
     # pred, confs, kind, B, N, ld, nc, conf, multi_label, class_mask, img_w, img_h, cand box/score/cls/key/count,
     # cap, stream (the remote client's postprocess of a decoded response, csrc/kernels/yolo.hip)

@@ -135,7 +135,8 @@ class YoloPostprocess:
                      _native.ptr(out.count), _native.stream_ptr(stream))
         return out
 
-    def _filter(self, heads, decoded_out: bool, stream=None):
+    def _heads(self, heads):
+        """-> (head pointers, NHWC channel strides or None, layout, dtype code, batch)."""
         from .conv import NHWC
         ldc = None
         if isinstance(heads[0], NHWC):  # slices of padded NHWC buffers (fused-conv plan)
@@ -150,6 +151,10 @@ class YoloPostprocess:
                 lay = 0
             ptrs = [_native.ptr(h) for h in hs]
             dt, B = dtype_code(hs[0]), hs[0].shape[0]
+        return ptrs, ldc, lay, dt, B
+
+    def _filter(self, heads, decoded_out: bool, stream=None):
+        ptrs, ldc, lay, dt, B = self._heads(heads)
         cap = self.num_anchors_total * (self.nc if self.multi_label else 1)
         cap = min(cap, 1 << 20)
         cand = Candidates.alloc(self.ws, "yolo_", B, cap, 4)
@@ -193,7 +198,11 @@ class YoloPostprocess:
         """Decoded [B, N, 5+nc] fp32 (the ONNX YOLOv5 output contract)."""
         if not _on_gpu(heads[0]):
             return self.decode_cpu(heads)
-        return self._filter(heads, True, stream)[1]
+        ptrs, ldc, lay, dt, B = self._heads(heads)
+        decoded = self.ws.get("decoded", (B, self.num_anchors_total, self.nc + 5), torch.float32)
+        _native.call("tca_yolo_decode", ptrs[0], ptrs[1], ptrs[2], dt, lay, B, self.na, self.nc, self.hw, self.strides,
+                     ldc, self.anc, _native.ptr(decoded), _native.stream_ptr(stream))
+        return decoded
 
     # -------------------------------------------------------------- CPU
     def decode_cpu(self, heads: List[torch.Tensor]) -> torch.Tensor:
