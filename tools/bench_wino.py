@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""hx3 (direct, conv_hx3.hip) vs wino (F(2,3), conv_wino.hip) on the PointPillars backbone's
+stride-1 layer shapes at batch 32 (pair storage in and out, ReLU): us per call, TFLOP/s of the
+direct conv's work (x3 split products), one JSON line per shape."""
+import copy
+import json
+import os
+import sys
+
+import torch
+import torch.nn as nn
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from triton_client_amd.ops.conv import NHWC, FusedConv, to_pairs  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    B = int(os.environ.get("B", 32))
+    for (H, W, c) in [(248, 216, 64), (124, 108, 128), (62, 54, 256)]:
+        torch.manual_seed(0)
+        conv = nn.Conv2d(c, c, 3, 1, 1, bias=True)
+        fc = FusedConv(copy.deepcopy(conv), act=1, device=dev, precision="fp32")
+        x = NHWC(to_pairs(torch.relu(torch.randn(B, H, W, c))).to(dev), pair=True)
+        outs = {t: NHWC(torch.empty(B, H, W, c, device=dev), pair=True) for t in (110, 130)}
+        res = {"shape": [B, H, W, c]}
+        for t in (110, 130, 131, 132, 133, 134):
+            if t in (131, 132) and c % 128:
+                continue
+            o = outs[110 if t == 110 else 130]
+            for _ in range(3):
+                fc(x, out=o, tile=t)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 20
+            e0.record()
+            for _ in range(n):
+                fc(x, out=o, tile=t)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / n
+            flops = 2.0 * B * H * W * c * c * 9 * 3
+            res[str(t)] = {"us": round(us, 1), "tflops_x3": round(flops / us / 1e6, 1)}
+        d = (outs[110].nchw() - outs[130].nchw()).norm() / outs[110].nchw().norm()
+        res["rel_l2_wino_vs_hx3"] = float(d)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -108,6 +108,36 @@ HX3 = True
 HX3S2 = True
 HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
+# conv_wino.hip (3x3 stride-1 by 1-D Winograd F(2,3), 1.5x fewer MFMAs than hx3): the default for
+# every eligible stride-1 layer (WINO False: hx3).  Tiles 130 (auto) and 131-134 select it explicitly.
+WINO = True
+WINO_TILES = (130, 131, 132, 133, 134)
+
+
+def wino_tile(H: int, W: int, N: int) -> int:
+    """conv_wino.hip wino_launch tile for an H x W output with N channels: F(2,3) along the axis
+    that pads less to 32 (tiles 2 / 4: along y), 32 (1, 2) or 16 (3, 4) channels per wave."""
+    cm = (H + 31) // 32 * 32 * W <= (W + 31) // 32 * 32 * H
+    return (2 if cm else 1) if N % 128 == 0 else (4 if cm else 3)
+
+
+def wino_taps(W: torch.Tensor, cin: int, cm: bool) -> torch.Tensor:
+    """[N, 9 * cin] GEMM weights (K order (ky * 3 + kx) * cin + ci) -> the F(2,3)-transformed taps
+    [N, 3 line taps kl, 4 positions p, cin] in fp64.  The Winograd axis is y when ``cm`` (line taps
+    kl = kx), else x (kl = ky): V0 = g0, V1 = (g0 + g1 + g2) / 2, V2 = (g0 - g1 + g2) / 2, V3 = g2."""
+    N = W.shape[0]
+    g = W[:, :9 * cin].double().reshape(N, 3, 3, cin)  # n, ky, kx, ci
+    if cm:
+        g = g.permute(0, 2, 1, 3)  # n, kl = kx, kf = ky, ci
+    g0, g1, g2 = g[:, :, 0], g[:, :, 1], g[:, :, 2]
+    return torch.stack([g0, (g0 + g1 + g2) / 2, (g0 - g1 + g2) / 2, g2], 2)
+
+
+def wino_weights(W: torch.Tensor, cin: int, cm: bool) -> torch.Tensor:
+    """The conv_wino.hip weight image: wino_taps in fragment order (frag_weights over
+    K = (kl * 4 + p) * cin + ci)."""
+    N = W.shape[0]
+    return frag_weights(wino_taps(W, cin, cm).reshape(N, 12 * cin).float())
 
 
 def frag_weights(W: torch.Tensor) -> torch.Tensor:
@@ -253,6 +283,9 @@ class FusedConv:
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp, _native.ptr(occ),
                              tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
                 return out
+            if (out.pair and x.occ is None and res is None and self.wino_ok() and
+                    (tile in WINO_TILES or (tile == 0 and WINO))):
+                return self._wino(x, out, tile, stream, uni)
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
                 if uni is not None and res is None:
@@ -291,6 +324,29 @@ class FusedConv:
         """conv_hx3.hip takes this conv: fp32, 3x3 stride 1 or 2, pad 1, Cin % 32, N % 64."""
         return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s in (1, 2) and self.p == 1
                 and self.cin_p % 32 == 0 and self.K == self.Kp and self.N % 64 == 0)
+
+    def wino_ok(self) -> bool:
+        """conv_wino.hip takes this conv: hx3's shapes at stride 1, ReLU or no activation."""
+        return self.hx3_ok() and self.s == 1 and self.act in (ACT_NONE, ACT_RELU)
+
+    def _wino(self, x: NHWC, out: NHWC, tile: int, stream, uni) -> NHWC:
+        B, H, W, _ = x.shape
+        t = tile - 130 if tile in WINO_TILES[1:] else wino_tile(H, W, self.N)
+        cm = t in (2, 4)
+        if not hasattr(self, "_w_wino"):
+            self._w_wino = {}
+        wf = self._w_wino.get(cm)
+        if wf is None:  # built on first use, never inside a graph capture (the plans warm up first)
+            wf = self._w_wino[cm] = wino_weights(self.w_f32_gemm, self.cin_p, cm).to(self.device)
+        depth, dmin, val = uni if uni is not None else (None, 0, None)
+        if uni is not None:
+            assert depth.dtype == torch.uint8 and tuple(depth.shape) == (B, H, W), depth.shape
+            assert val.dtype == torch.float32 and val.numel() == self.N, (val.dtype, val.shape)
+        _native.call("tca_conv_wino", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off, int(x.pair),
+                     _native.ptr(wf), _native.ptr(self.b_gemm), self.N, _native.ptr(out.t), out.t.shape[-1], out.off,
+                     int(out.pair), self.act, _native.ptr(depth), dmin, _native.ptr(val), t,
+                     _native.stream_ptr(stream))
+        return out
 
     def hx3_weights(self) -> torch.Tensor:
         if self._w_frag is None:
