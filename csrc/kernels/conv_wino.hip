@@ -21,8 +21,8 @@
 //      TH + 2 U lines once and feeds each to the three line taps kl (output line u - kl), with
 //      the transformed weights V_p[kl] streamed from L2 into registers one group ahead (hx3's
 //      fragment-order image; ops/conv.py wino_weights).
-// The transform of chunk c + 1 runs in the middle of chunk c (double-buffered image), its raw
-// loads one chunk ahead.  Epilogue: y0 = m0 + m1 + m2, y1 = m1 - m2 - m3 per lane (the lane
+// The raw halo of chunk c + 1 lands by LDS DMA during chunk c's MFMAs; its transform runs between
+// chunks (one image, two workgroups per CU, so one's transform overlaps the other's MFMAs).  Epilogue: y0 = m0 + m1 + m2, y1 = m1 - m2 - m3 per lane (the lane
 // holds all four positions of its tile), bias + act, an LDS staging tile, 16-B stores.
 #include "tca_common.h"
 
@@ -82,14 +82,42 @@ __device__ __forceinline__ void join8(const u32x4& p0, const u32x4& p1, float* d
 
 template <int P> struct PosC { static constexpr int value = P; };
 
+// one 16-B-per-lane LDS DMA through a buffer resource: voffset per lane, soffset scalar; the wave's
+// 64 pieces land contiguously at the wave-uniform LDS address l (lane i at l + 16 i)
+__device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, const void* l, unsigned soff) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+               : "memory");
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// raw-halo slot of (pixel fi along F, 16-B piece slot = cq * 2 + hl): XOR swizzle by fi / 2 so the
+// transform's reads (16 lanes = 16 tiles at pixels 2t + j) spread over 8 bank groups per half
+__device__ __forceinline__ int raw_slot(int fi, int slot) { return slot ^ ((fi >> 1) & 7); }
+
 template <int TH, int WN, int FN, bool CM, bool PIN, bool POUT>
-__global__ void __launch_bounds__(WN * 64, 1) conv_wino_kernel(WinoArgs a) {
+__global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
   constexpr int NT = WN * 64, BN = WN * FN * 16, TF = 32, NU = TH + 2;
   constexpr int NITEM = NU * 64, IPT = (NITEM + NT - 1) / NT;
   constexpr int UB = NU * 8192;  // one U image: NU lines x 4 positions x 4 groups x 2 x 16 tiles x 16 B
+  // raw halo of one chunk: NU lines x 34 pixels x 8 pieces of 16 B, staged by LDS DMA (whole
+  // wave-instructions of 64 pieces; the pieces past the halo read zeros into padding)
+  constexpr int NPIECE = NU * 34 * 8, NINS = (NPIECE + 63) / 64, DPW = (NINS + WN - 1) / WN;
+  constexpr int RAWB = DPW * WN * 1024;
   constexpr int EPI = TH * TF * BN * 4;
-  constexpr int LDS = 2 * UB > EPI ? 2 * UB : EPI;
+  constexpr int LDS = (UB + RAWB) > EPI ? UB + RAWB : EPI;
+  static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+  unsigned char* const raw = smem + UB;
 
   const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
   const int FH = CM ? a.H : a.W, LW = CM ? a.W : a.H;
@@ -132,45 +160,43 @@ __global__ void __launch_bounds__(WN * 64, 1) conv_wino_kernel(WinoArgs a) {
 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
-  // transform items of this lane: item id = (u * 4 + cq) * 16 + t
-  unsigned ioff[IPT][4];
-  int iwr[IPT];  // LDS byte offset of the item's (position 0, hi) slot; -1: none
+  // DMA pieces of this lane: piece q = (instruction wn * DPW + k) * 64 + lane = (u * 34 + fi) * 8 + phys
+  unsigned dvo[DPW];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int id = tid + k * NT;
-    const int u = id >> 6, cq = (id >> 4) & 3, t = id & 15;
-    iwr[k] = id < NITEM ? ((u * 4 * 4 + cq) * 2 * 16 + t) * 16 : -1;
-    const int l = l0 - 1 + u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int y, x;
-      pix_yx(f0 + 2 * t - 1 + j, l, y, x);
-      ioff[k][j] = (id < NITEM && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                       ? (unsigned)(((((long)b * a.H + y) * a.W + x) * a.ldi + a.ci_off + cq * 8) * 4)
-                       : kOutOfRange;
-    }
+  for (int k = 0; k < DPW; ++k) {
+    const int q = (wn * DPW + k) * 64 + lane;
+    const int u = q / 272, fi = (q / 8) % 34, slot = raw_slot(fi, q & 7);
+    int y, x;
+    pix_yx(f0 - 1 + fi, l0 - 1 + u, y, x);
+    dvo[k] = (q < NPIECE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                 ? (unsigned)(((((long)b * a.H + y) * a.W + x) * a.ldi + a.ci_off + (slot >> 1) * 8) * 4 + (slot & 1) * 16)
+                 : kOutOfRange;
   }
-  u32x4 raw[IPT][4][2];
-  auto raw_load = [&](int c) {
+  auto raw_dma = [&](int c) {
 #pragma unroll
-    for (int k = 0; k < IPT; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        raw[k][j][0] = __builtin_amdgcn_raw_buffer_load_b128(rin, ioff[k][j], c * 128, 0);
-        raw[k][j][1] = __builtin_amdgcn_raw_buffer_load_b128(rin, ioff[k][j] + 16, c * 128, 0);
-      }
+    for (int k = 0; k < DPW; ++k) bdma16(dvo[k], rin, raw + (wn * DPW + k) * 1024, (unsigned)(c * 128));
   };
-  auto transform = [&](int buf) {
-    unsigned char* ub = smem + buf * UB;
+  // transform: item id = (u * 4 + cq) * 16 + t -> the 4 positions' hi / lo slots of (u, cq, t)
+  auto transform = [&]() {
+    unsigned char* ub = smem;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-      if (NITEM % NT != 0 && iwr[k] < 0) continue;
+      const int id = tid + k * NT;
+      if (NITEM % NT != 0 && id >= NITEM) continue;
+      const int u = id >> 6, cq = (id >> 4) & 3, t = id & 15;
       float d[4][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) join8<PIN>(raw[k][j][0], raw[k][j][1], d[j]);
+      for (int j = 0; j < 4; ++j) {
+        const int fi = 2 * t + j;
+        const unsigned char* rp = raw + (u * 34 + fi) * 128;
+        const u32x4 p0 = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2) * 16);
+        const u32x4 p1 = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2 + 1) * 16);
+        join8<PIN>(p0, p1, d[j]);
+      }
+      // image slot: ((((u * 4 + p) * 4 + cq) * 2 + hl) * 16 + t) * 16
+      unsigned char* wp = ub + ((u * 16 + cq) * 32 + t) * 16;
       float uv[8];
       u32x4 hi, lo;
-      // position stride in the image: 4 groups x 2 x 16 tiles x 16 B = 2 KiB; hi -> lo: 256 B
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
 #pragma unroll
@@ -178,26 +204,25 @@ __global__ void __launch_bounds__(WN * 64, 1) conv_wino_kernel(WinoArgs a) {
           uv[e] = p == 0 ? d[0][e] - d[2][e] : p == 1 ? d[1][e] + d[2][e] : p == 2 ? d[2][e] - d[1][e]
                                                                                   : d[1][e] - d[3][e];
         split8(uv, hi, lo);
-        *reinterpret_cast<u32x4*>(ub + iwr[k] + p * 2048) = hi;
-        *reinterpret_cast<u32x4*>(ub + iwr[k] + p * 2048 + 256) = lo;
+        *reinterpret_cast<u32x4*>(wp + p * 2048) = hi;
+        *reinterpret_cast<u32x4*>(wp + p * 2048 + 256) = lo;
       }
     }
   };
 
-  // weights: block (ks, g, hl) = 64 lanes x 8 bf16, ks = (kl * 4 + p) * nc + c
+  // weights: block (ks, g, hl) = 64 lanes x 8 bf16, ks = (kl * 4 + p) * nc + c.  Streamed per
+  // step (c, p, kl) through a 3-deep register ring (set = kl), two steps ahead.
   const int NG = a.N / 16, g0 = n0 / 16 + wn * FN;
   const bf16x8* wf = reinterpret_cast<const bf16x8*>(a.w) + (long)g0 * 128 + lane;
-  const int nc = a.Cin / 32, G = 4 * nc;
-  auto gload = [&](int gs, bf16x8 (&dst)[3][FN][2]) {  // group gs: chunk gs / 4, position gs % 4
-    const int c = gs >> 2, p = gs & 3;
+  const int nc = a.Cin / 32, NS = 12 * nc;
+  auto wload = [&](int s, bf16x8 (&dst)[FN][2]) {  // step s = (c * 4 + p) * 3 + kl
+    s = s < NS ? s : NS - 1;
+    const int kl = s % 3, p = (s / 3) & 3, c = s / 12;
+    const bf16x8* q = wf + (long)((kl * 4 + p) * nc + c) * NG * 128;
 #pragma unroll
-    for (int kl = 0; kl < 3; ++kl) {
-      const bf16x8* q = wf + (long)((kl * 4 + p) * nc + c) * NG * 128;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        dst[kl][j][0] = q[j * 128];
-        dst[kl][j][1] = q[j * 128 + 64];
-      }
+    for (int j = 0; j < FN; ++j) {
+      dst[j][0] = q[j * 128];
+      dst[j][1] = q[j * 128 + 64];
     }
   };
 
@@ -211,53 +236,67 @@ __global__ void __launch_bounds__(WN * 64, 1) conv_wino_kernel(WinoArgs a) {
 
   const int fr = lane & 15, fq = lane >> 4;
   const int rd = (fq * 2 * 16 + fr) * 16;  // this lane's B-fragment slot (hi) inside a (line, position) block
-  auto group = [&](auto PC, const unsigned char* ub, bf16x8 (&wu)[3][FN][2], bf16x8 (&wl)[3][FN][2], int gs_next) {
-    constexpr int p = decltype(PC)::value;
-    gload(gs_next < G ? gs_next : G - 1, wl);
+  bf16x8 w[3][FN][2];
+  // one step: line tap kl of position p over the TH output lines (U lines i + kl), two lines at a time
+  auto step = [&](auto PC, auto KC, const unsigned char* ub, int s_next) {
+    constexpr int p = decltype(PC)::value, kl = decltype(KC)::value;
+    wload(s_next, w[(kl + 2) % 3]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int L = 0; L < NU; ++L) {
-      const unsigned char* s = ub + (L * 4 + p) * 2048 + rd;
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(s + 256);
+    for (int i0 = 0; i0 < TH; i0 += 2) {
+      bf16x8 ah[2], al[2];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const unsigned char* s = ub + ((i0 + ii + kl) * 4 + p) * 2048 + rd;
+        ah[ii] = *reinterpret_cast<const bf16x8*>(s);
+        al[ii] = *reinterpret_cast<const bf16x8*>(s + 256);
+      }
 #pragma unroll
       for (int pr = 0; pr < 3; ++pr)
 #pragma unroll
-        for (int kl = 0; kl < 3; ++kl) {
-          const int i = L - kl;
-          if (i < 0 || i >= TH) continue;
+        for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
-            const bf16x8& w = pr == 0 ? wu[kl][j][1] : wu[kl][j][0];
-            const bf16x8& x = pr == 1 ? al : ah;
-            acc[i][p][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, acc[i][p][j], 0, 0, 0);
+            const bf16x8& wv = pr == 0 ? w[kl][j][1] : w[kl][j][0];
+            const bf16x8& x = pr == 1 ? al[ii] : ah[ii];
+            acc[i0 + ii][p][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, x, acc[i0 + ii][p][j], 0, 0, 0);
           }
-        }
     }
   };
+  auto position = [&](auto PC, const unsigned char* ub, int s0) {
+    step(PC, PosC<0>{}, ub, s0 + 2);
+    step(PC, PosC<1>{}, ub, s0 + 3);
+    step(PC, PosC<2>{}, ub, s0 + 4);
+  };
 
-  bf16x8 wc[3][FN][2], wx[3][FN][2];
-  raw_load(0);
-  gload(0, wc);
-  transform(0);
-  raw_load(nc > 1 ? 1 : 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
+  // one U image and one raw halo: two workgroups per CU overlap one's transform with the
+  // other's MFMAs.  Chunk c: MFMAs on U(c) while the DMA of raw(c + 1) lands; then
+  // transform raw(c + 1) -> U(c + 1) between two barriers and start the DMA of raw(c + 2).
+  raw_dma(0);
+  wload(0, w[0]);
+  wload(1, w[1]);
+  wait_vmcnt0();
+  lds_barrier();
+  transform();
+  lds_barrier();  // the image is visible and every wave is done with the raw halo
+  if (nc > 1) raw_dma(1);
+  const unsigned char* ub = smem;
   for (int c = 0; c < nc; ++c) {
-    const unsigned char* ub = smem + (c & 1) * UB;
-    group(PosC<0>{}, ub, wc, wx, 4 * c + 1);
-    group(PosC<1>{}, ub, wx, wc, 4 * c + 2);
-    if (c + 1 < nc) {  // the next chunk's image (its buffer was last read in chunk c - 1)
-      transform((c + 1) & 1);
-      raw_load(c + 2 < nc ? c + 2 : nc - 1);
+    const int s0 = c * 12;
+    position(PosC<0>{}, ub, s0);
+    position(PosC<1>{}, ub, s0 + 3);
+    position(PosC<2>{}, ub, s0 + 6);
+    position(PosC<3>{}, ub, s0 + 9);
+    if (c + 1 < nc) {
+      wait_vmcnt0();
+      lds_barrier();  // raw(c + 1) landed for every wave; every wave is done reading U(c)
+      transform();
+      lds_barrier();
+      if (c + 2 < nc) raw_dma(c + 2);
     }
-    group(PosC<2>{}, ub, wc, wx, 4 * c + 3);
-    group(PosC<3>{}, ub, wx, wc, 4 * c + 4);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
   }
+  wait_vmcnt0();  // the clamped tail prefetches
+  lds_barrier();  // the epilogue reuses the image
 
   // ---- epilogue: output transform + bias + act -> fp32 staging tile [TH * 32 rows][BN] (16-B
   // quads XOR-swizzled by the row, as hx3_epilogue) -> 16-B stores

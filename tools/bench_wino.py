@@ -18,14 +18,17 @@ from triton_client_amd.ops.conv import NHWC, FusedConv, to_pairs  # noqa: E402
 def main():
     dev = torch.device("cuda")
     B = int(os.environ.get("B", 32))
-    for (H, W, c) in [(248, 216, 64), (124, 108, 128), (62, 54, 256)]:
+    shapes = [(248, 216, 64), (124, 108, 128), (62, 54, 256)]
+    only = os.environ.get("SHAPE")  # e.g. SHAPE=1: the 128-channel layer only
+    tiles = [int(t) for t in os.environ.get("TILES", "110,130,131,132,133,134").split(",")]
+    for (H, W, c) in ([shapes[int(only)]] if only else shapes):
         torch.manual_seed(0)
         conv = nn.Conv2d(c, c, 3, 1, 1, bias=True)
         fc = FusedConv(copy.deepcopy(conv), act=1, device=dev, precision="fp32")
         x = NHWC(to_pairs(torch.relu(torch.randn(B, H, W, c))).to(dev), pair=True)
         outs = {t: NHWC(torch.empty(B, H, W, c, device=dev), pair=True) for t in (110, 130)}
         res = {"shape": [B, H, W, c]}
-        for t in (110, 130, 131, 132, 133, 134):
+        for t in tiles:
             if t in (131, 132) and c % 128:
                 continue
             o = outs[110 if t == 110 else 130]
@@ -42,8 +45,9 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / n
             flops = 2.0 * B * H * W * c * c * 9 * 3
             res[str(t)] = {"us": round(us, 1), "tflops_x3": round(flops / us / 1e6, 1)}
-        d = (outs[110].nchw() - outs[130].nchw()).norm() / outs[110].nchw().norm()
-        res["rel_l2_wino_vs_hx3"] = float(d)
+        if 110 in tiles and any(t >= 130 for t in tiles):
+            d = (outs[110].nchw() - outs[130].nchw()).norm() / outs[110].nchw().norm()
+            res["rel_l2_wino_vs_hx3"] = float(d)
         print(json.dumps(res), flush=True)
 
 
