@@ -129,6 +129,11 @@ __device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* sm
       for (int e = 0; e < 8; ++e) v[e] = post_res ? act_fn(v[e] + r[e], act) : v[e] + r[e];
     }
     const long o = pix * a.ldo + a.co_off + n;
+    if (a.act & 32) {  // fp32 storage out (the input of an F(2,3) layer, conv_wino.hip)
+      *reinterpret_cast<float4*>(a.out_f + o) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(a.out_f + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      continue;
+    }
     uint4 hi, lo;
     pair_split8(v, hi, lo);
     *reinterpret_cast<uint4*>(a.out_f + o) = hi;
@@ -680,13 +685,14 @@ TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi
 }
 
 // fp32 mode, pair activations in and out, 3x3 stride 2 pad 1 (conv_hx3s2_kernel), same weight
-// image as tca_conv_hx3p.  Output [B, Ho, Wo, ldo] with Ho = (H + 1) / 2, Wo = (W + 1) / 2.
+// image as tca_conv_hx3p.  act | 32: fp32 storage out instead of pairs (no residual).  Output [B, Ho, Wo, ldo] with Ho = (H + 1) / 2, Wo = (W + 1) / 2.
 // occ: optional uint8 [B, H, W] input occupancy (a pixel marked 0 is read as zeros).
 // tile: 0 auto, 1-4 (hx3s2_launch).
 TCA_API int tca_conv_hx3s2p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
                             const float* bias, int N, float* out, int ldo, int co_off, int act, const float* res,
                             int ldr, int r_off, const unsigned char* occ, int tile, hipStream_t stream) {
   if (B <= 0) return 0;
+  if ((act & 32) && res) return (int)hipErrorInvalidValue;
   if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;

@@ -94,6 +94,10 @@ __device__ __forceinline__ void bdma16(unsigned voff, __amdgpu_buffer_rsrc_t rsr
 }
 
 __device__ __forceinline__ void wait_vmcnt0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+template <int N>
+__device__ __forceinline__ void wait_vm() {  // at most this wave's N youngest vector-memory ops in flight
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -212,17 +216,19 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
 
   // weights: block (ks, g, hl) = 64 lanes x 8 bf16, ks = (kl * 4 + p) * nc + c.  Streamed per
   // step (c, p, kl) through a 3-deep register ring (set = kl), two steps ahead.
+  // Buffer loads: the lane part of the address is fixed, the step part is scalar (no VALU per load).
   const int NG = a.N / 16, g0 = n0 / 16 + wn * FN;
-  const bf16x8* wf = reinterpret_cast<const bf16x8*>(a.w) + (long)g0 * 128 + lane;
   const int nc = a.Cin / 32, NS = 12 * nc;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, NS * NG * 2048, 0x00020000);
+  const unsigned wvo = (unsigned)(g0 * 2048 + lane * 16);
   auto wload = [&](int s, bf16x8 (&dst)[FN][2]) {  // step s = (c * 4 + p) * 3 + kl
     s = s < NS ? s : NS - 1;
     const int kl = s % 3, p = (s / 3) & 3, c = s / 12;
-    const bf16x8* q = wf + (long)((kl * 4 + p) * nc + c) * NG * 128;
+    const unsigned so = (unsigned)(((kl * 4 + p) * nc + c) * NG * 2048);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      dst[j][0] = q[j * 128];
-      dst[j][1] = q[j * 128 + 64];
+      dst[j][0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wvo + j * 2048, so, 0));
+      dst[j][1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wvo + j * 2048 + 1024, so, 0));
     }
   };
 
@@ -288,8 +294,8 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
     position(PosC<2>{}, ub, s0 + 6);
     position(PosC<3>{}, ub, s0 + 9);
     if (c + 1 < nc) {
-      wait_vmcnt0();
-      lds_barrier();  // raw(c + 1) landed for every wave; every wave is done reading U(c)
+      wait_vm<4 * FN>();  // all but the next chunk's two prefetched weight steps: raw(c + 1) landed
+      lds_barrier();      // ... for every wave; every wave is done reading U(c)
       transform();
       lds_barrier();
       if (c + 2 < nc) raw_dma(c + 2);

@@ -83,14 +83,21 @@ def test_hx3_post_residual_act_and_no_bias(cuda):
 
 
 @pytest.mark.gpu
-def test_hx3_is_the_default_for_pair_backbone_layers(cuda):
-    """tile 0 routes an eligible pair conv to hx3 (the same bits as tile 110)."""
+def test_wino_is_the_default_for_pair_backbone_layers(cuda, monkeypatch):
+    """tile 0 routes an eligible stride-1 pair conv to conv_wino.hip F(2,3) (the same bits as
+    tile 130), and to hx3 (tile 110) with ops.conv.WINO off."""
+    from triton_client_amd.ops import conv as conv_mod
     torch.manual_seed(5)
     B, H, W, cin, cout = 2, 20, 24, 128, 128
     fc = FusedConv(nn.Conv2d(cin, cout, 3, 1, 1), act=1, device=cuda, precision="fp32")
     x = NHWC(to_pairs(torch.randn(B, H, W, cin)).to(cuda), pair=True)
     a = NHWC(torch.empty(B, H, W, cout, device=cuda), pair=True)
     b = NHWC(torch.empty(B, H, W, cout, device=cuda), pair=True)
+    fc(x, out=a, tile=0)
+    fc(x, out=b, tile=130)
+    torch.cuda.synchronize()
+    assert torch.equal(a.t, b.t)
+    monkeypatch.setattr(conv_mod, "WINO", False)
     fc(x, out=a, tile=0)
     fc(x, out=b, tile=110)
     torch.cuda.synchronize()

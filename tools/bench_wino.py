@@ -25,7 +25,10 @@ def main():
         torch.manual_seed(0)
         conv = nn.Conv2d(c, c, 3, 1, 1, bias=True)
         fc = FusedConv(copy.deepcopy(conv), act=1, device=dev, precision="fp32")
-        x = NHWC(to_pairs(torch.relu(torch.randn(B, H, W, c))).to(dev), pair=True)
+        xr = torch.relu(torch.randn(B, H, W, c))
+        x = NHWC(to_pairs(xr).to(dev), pair=True)
+        x32 = NHWC(xr.to(dev), pair=False)  # fp32 storage (the chain inside a block)
+        o32 = NHWC(torch.empty(B, H, W, c, device=dev), pair=False)
         outs = {t: NHWC(torch.empty(B, H, W, c, device=dev), pair=True) for t in (110, 130)}
         res = {"shape": [B, H, W, c]}
         for t in tiles:
@@ -45,6 +48,16 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / n
             flops = 2.0 * B * H * W * c * c * 9 * 3
             res[str(t)] = {"us": round(us, 1), "tflops_x3": round(flops / us / 1e6, 1)}
+            if t == 130:  # fp32 storage in and out
+                for _ in range(3):
+                    fc(x32, out=o32, tile=t)
+                e0.record()
+                for _ in range(n):
+                    fc(x32, out=o32, tile=t)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / n
+                res["130_fp32io"] = {"us": round(us, 1), "tflops_x3": round(flops / us / 1e6, 1)}
         if 110 in tiles and any(t >= 130 for t in tiles):
             d = (outs[110].nchw() - outs[130].nchw()).norm() / outs[110].nchw().norm()
             res["rel_l2_wino_vs_hx3"] = float(d)

@@ -33,6 +33,10 @@ STEM_FUSED = True
 # PointPillars first block: skip the tiles of the stride-1 convs whose receptive field is empty
 # canvas (_BEVBackbonePlan.forward_blocks; False: dense, for A/B runs)
 BEV_UNIFORM = True
+# fp32-mode BEV blocks: a conv whose successor is an F(2,3) layer (ops/conv.py WINO) writes fp32
+# storage instead of pairs (conv_wino.hip then skips the pair join); the last conv of a block
+# writes pairs (the next block's stride-2 conv and the deblock read them)
+WINO_F32_CHAIN = True
 # YOLOv5 Detect convs fused with the decode + candidate filter (FastYOLOv5.detect_fused_ok)
 DETECT_FUSED = True
 # the c3_fused.hip C3 blocks (_C3Plan.fused2_ok); False: the unfused chain (tests compare the two)
@@ -374,6 +378,15 @@ class _BEVBackbonePlan:
             _, _, H1, W1 = self.blocks[0]
             self.depth = torch.zeros((B, H1, W1), dtype=torch.uint8, device=device)
 
+    def out_pair(self, convs, i: int) -> bool:
+        """Storage of conv i's output in its block: fp32 when the next conv is an F(2,3) layer and
+        this conv can write fp32 (an F(2,3) layer, or the stride-2 hx3 kernel), else pairs."""
+        from ..ops import conv as conv_mod
+        if not (self.pair and WINO_F32_CHAIN and conv_mod.WINO) or i + 1 >= len(convs):
+            return True
+        cv, nxt = convs[i], convs[i + 1]
+        return not (nxt.wino_ok() and (cv.wino_ok() or (cv.s == 2 and cv.hx3_ok() and conv_mod.HX3S2)))
+
     def _uniform_eligible(self) -> bool:
         convs = self.blocks[0][0]
         return (self.pair and len(convs) >= 2 and convs[0].s == 2 and convs[0].hx3_ok()
@@ -391,9 +404,10 @@ class _BEVBackbonePlan:
         x = NHWC(torch.zeros((1, self.ny, self.nx, convs[0].cin_p), dtype=torch.float32, device=device), pair=True,
                  occ=torch.zeros((1, self.ny, self.nx), dtype=torch.uint8, device=device))
         vals = []
-        for cv in convs:
+        for i, cv in enumerate(convs):
             Ho, Wo = cv.out_hw(x.t.shape[1], x.t.shape[2])
-            x = cv(x, out=NHWC(torch.zeros((1, Ho, Wo, cv.N), dtype=torch.float32, device=device), pair=True))
+            x = cv(x, out=NHWC(torch.zeros((1, Ho, Wo, cv.N), dtype=torch.float32, device=device),
+                               pair=self.out_pair(convs, i)))
             vals.append(x.t[0, Ho // 2, Wo // 2].clone())
         torch.cuda.synchronize(device)
         return vals
@@ -412,7 +426,8 @@ class _BEVBackbonePlan:
         for bi, (convs, pp, H, W) in enumerate(self.blocks):
             for i, cv in enumerate(convs):
                 u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 and i > 0 else None
-                x = cv(x, out=pp[i % 2], uni=u)
+                o = pp[i % 2] if self.out_pair(convs, i) else NHWC(pp[i % 2].t, pair=False)
+                x = cv(x, out=o, uni=u)
             outs.append(x)
         return outs
 

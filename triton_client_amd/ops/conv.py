@@ -270,22 +270,26 @@ class FusedConv:
         act = self.act | (16 if (self.post_res and res is not None) else 0)
         rp = (_native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
               res.off if res is not None else 0)
+        if (x.occ is None and res is None and self.wino_ok() and not self.transpose and
+                (tile in WINO_TILES or (tile == 0 and WINO))):
+            # F(2,3) stride-1 kernel: pair or fp32 storage on either side
+            return self._wino(x, out, tile, stream, uni)
         if x.pair or out.pair:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
-            if out.pair and self.hx3_ok() and self.s == 2 and (tile in HX3S2_TILES or (tile == 0 and HX3S2)):
+            if ((out.pair or res is None) and self.hx3_ok() and self.s == 2 and
+                    (tile in HX3S2_TILES or (tile == 0 and HX3S2))):
                 occ = x.occ
                 if occ is not None:
                     assert occ.dtype == torch.uint8 and tuple(occ.shape) == (B, H, W), (occ.shape, (B, H, W))
+                # act | 32: fp32 storage out (the input of an F(2,3) layer)
                 _native.call("tca_conv_hx3s2p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
-                             _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp, _native.ptr(occ),
+                             _native.ptr(out.t), out.t.shape[-1], out.off, act | (0 if out.pair else 32), *rp,
+                             _native.ptr(occ),
                              tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
                 return out
-            if (out.pair and x.occ is None and res is None and self.wino_ok() and
-                    (tile in WINO_TILES or (tile == 0 and WINO))):
-                return self._wino(x, out, tile, stream, uni)
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
                 if uni is not None and res is None:
