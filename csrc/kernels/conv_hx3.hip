@@ -141,6 +141,31 @@ __device__ __forceinline__ void hx3_epilogue(const Hx3Args& a, unsigned char* sm
   }
 }
 
+// Uniform-tile skipping (Hx3Args::uni): every output pixel of the BM-pixel tile (16-pixel
+// fragment lines, CM as the kernels) has uniform depth >= uni_min, i.e. every input the dense K
+// loop would read is the previous layer's constant (or, for the stride-2 conv on the sparse
+// canvas, its window is empty): store uni_val (this layer's own output on such a pixel, in its
+// output storage) and skip the K loop.  Workgroup-uniform result.
+template <int BM, int BN, bool CM, int NT>
+__device__ __forceinline__ bool uni_tile_store(const Hx3Args& a, int b, int oy0, int ox0, int n0) {
+  const int tid = threadIdx.x;
+  bool bad = false;
+  for (int ml = tid; ml < BM; ml += NT) {
+    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
+    if (oy < a.Ho && ox < a.Wo) bad |= a.uni[((long)b * a.Ho + oy) * a.Wo + ox] < a.uni_min;
+  }
+  if (__syncthreads_or(bad)) return false;
+  constexpr int Q = BN / 4;  // 16-B pieces per pixel
+  for (int id = tid; id < BM * Q; id += NT) {
+    const int ml = id / Q, q = id - (id / Q) * Q;
+    const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    const long o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n0 + q * 4;
+    *reinterpret_cast<uint4*>(a.out_f + o) = *reinterpret_cast<const uint4*>(a.uni_val + n0 + q * 4);
+  }
+  return true;
+}
+
 // ---- x3 pair, halo-tiled 3x3 stride 1, v3 ("hx3"): weights streamed to registers.
 //
 // PMC of hx (profiles/r2/pmc_lidar_end/summary.md): waves 34% parked at the per-step
@@ -192,26 +217,7 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_hx3_kernel(Hx3Args a)
   const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
   const int n0 = nt * BN;
 
-  if (a.uni) {
-    // uniform tile (every input it reads is the previous layer's constant vector, inside the
-    // image): the dense K loop would produce uni_val on every pixel, so store it directly
-    bool bad = false;
-    for (int ml = tid; ml < BM; ml += NT) {
-      const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
-      if (oy < a.Ho && ox < a.Wo) bad |= a.uni[((long)b * a.Ho + oy) * a.Wo + ox] < a.uni_min;
-    }
-    if (!__syncthreads_or(bad)) {
-      constexpr int Q = BN / 4;  // 16-B pieces per pixel
-      for (int id = tid; id < BM * Q; id += NT) {
-        const int ml = id / Q, q = id - (id / Q) * Q;
-        const int oy = oy0 + (CM ? (ml & 15) : ml / 16), ox = ox0 + (CM ? ml / 16 : (ml & 15));
-        if (oy >= a.Ho || ox >= a.Wo) continue;
-        const long o = (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldo + a.co_off + n0 + q * 4;
-        *reinterpret_cast<uint4*>(a.out_f + o) = *reinterpret_cast<const uint4*>(a.uni_val + n0 + q * 4);
-      }
-      return;
-    }
-  }
+  if (a.uni && uni_tile_store<TH * TW, BN, CM, NT>(a, b, oy0, ox0, n0)) return;
 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
@@ -429,6 +435,7 @@ __global__ void __launch_bounds__(WN * 64, MINW) conv_hx3s2_kernel(Hx3Args a) {
   const int b = mt / (ty_n * tx_n), rem = mt - b * (ty_n * tx_n);
   const int oy0 = (rem / tx_n) * EY, ox0 = (rem - (rem / tx_n) * tx_n) * EX;
   const int n0 = nt * BN;
+  if (a.uni && uni_tile_store<TH * TW, BN, CM, NT>(a, b, oy0, ox0, n0)) return;
 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
@@ -687,17 +694,21 @@ TCA_API int tca_conv_hx3p(const float* in, int B, int H, int W, int Cin, int ldi
 // fp32 mode, pair activations in and out, 3x3 stride 2 pad 1 (conv_hx3s2_kernel), same weight
 // image as tca_conv_hx3p.  act | 32: fp32 storage out instead of pairs (no residual).  Output [B, Ho, Wo, ldo] with Ho = (H + 1) / 2, Wo = (W + 1) / 2.
 // occ: optional uint8 [B, H, W] input occupancy (a pixel marked 0 is read as zeros).
+// uni / uni_min / uni_val: optional uniform-tile skipping on the output grid (tca_conv_hx3p_uni;
+// uni_min 1 = the stride-2 window holds no occupied cell, tca_bev_uniform_depth).
 // tile: 0 auto, 1-4 (hx3s2_launch).
 TCA_API int tca_conv_hx3s2p(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
                             const float* bias, int N, float* out, int ldo, int co_off, int act, const float* res,
-                            int ldr, int r_off, const unsigned char* occ, int tile, hipStream_t stream) {
+                            int ldr, int r_off, const unsigned char* occ, const unsigned char* uni, int uni_min,
+                            const float* uni_val, int tile, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((act & 32) && res) return (int)hipErrorInvalidValue;
   if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 63) || (ldo & 7) || (co_off & 7)) return (int)hipErrorInvalidValue;
   if (res && ((ldr & 7) || (r_off & 7))) return (int)hipErrorInvalidValue;
   Hx3Args a;
+  if (uni && (!uni_val || uni_min < 1 || res)) return (int)hipErrorInvalidValue;
   a.in_f = in; a.res_f = res; a.out_f = out; a.w = wfrag; a.bias = bias; a.occ = occ;
-  a.uni = nullptr; a.uni_val = nullptr; a.uni_min = 0;
+  a.uni = uni; a.uni_val = uni_val; a.uni_min = uni ? uni_min : 0;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.ldr = ldr; a.r_off = r_off; a.act = act;
   if ((long)B * H * W * ldi * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;  // 32-bit buffer offsets

@@ -243,7 +243,9 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
   const int fr = lane & 15, fq = lane >> 4;
   const int rd = (fq * 2 * 16 + fr) * 16;  // this lane's B-fragment slot (hi) inside a (line, position) block
   bf16x8 w[3][FN][2];
-  // one step: line tap kl of position p over the TH output lines (U lines i + kl), two lines at a time
+  // one step: line tap kl of position p over the TH output lines (U lines i + kl), two lines at a
+  // time, its weights streamed two steps ahead.  (Reading the position's NU lines into registers
+  // once for its three taps measured ~10 % slower: profiles/r5/wino_ab.md.)
   auto step = [&](auto PC, auto KC, const unsigned char* ub, int s_next) {
     constexpr int p = decltype(PC)::value, kl = decltype(KC)::value;
     wload(s_next, w[(kl + 2) % 3]);
@@ -253,9 +255,9 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
       bf16x8 ah[2], al[2];
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
-        const unsigned char* s = ub + ((i0 + ii + kl) * 4 + p) * 2048 + rd;
-        ah[ii] = *reinterpret_cast<const bf16x8*>(s);
-        al[ii] = *reinterpret_cast<const bf16x8*>(s + 256);
+        const unsigned char* sp = ub + ((i0 + ii + kl) * 4 + p) * 2048 + rd;
+        ah[ii] = *reinterpret_cast<const bf16x8*>(sp);
+        al[ii] = *reinterpret_cast<const bf16x8*>(sp + 256);
       }
 #pragma unroll
       for (int pr = 0; pr < 3; ++pr)

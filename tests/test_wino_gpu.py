@@ -12,6 +12,13 @@ import torch.nn as nn
 from triton_client_amd.ops.conv import NHWC, FusedConv, from_pairs, to_pairs, wino_taps, wino_tile
 
 
+@pytest.fixture(autouse=True)
+def _wino_all_widths(monkeypatch):
+    """The kernel serves N = 64 too (the default routes only N >= 128 layers to it)."""
+    from triton_client_amd.ops import conv as conv_mod
+    monkeypatch.setattr(conv_mod, "WINO_MIN_N", 64)
+
+
 def rel_l2(got, ref):
     got, ref = got.double().cpu(), ref.double().cpu()
     return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()

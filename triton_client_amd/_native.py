@@ -74,7 +74,7 @@ _KERNEL_SIGS = {
     # occ, B, H, W, maxd, depth, stream
     "tca_bev_uniform_depth": [P, I, I, I, I, P, P],
     # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, res, ldr, r_off, occ, tile, stream
-    "tca_conv_hx3s2p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, P, I, P],
+    "tca_conv_hx3s2p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, P, P, I, P, I, P],
     # n, dst[], src[], nbytes[], stream (csrc/kernels/copy.hip)
     "tca_copy_segments": [I, P, P, P, P],
     # coords, nump, vcount, B, V, P, nz, ny, nx, flags, stream

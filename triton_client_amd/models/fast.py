@@ -425,7 +425,8 @@ class _BEVBackbonePlan:
                          _native.ptr(self.depth), _native.stream_ptr(None))
         for bi, (convs, pp, H, W) in enumerate(self.blocks):
             for i, cv in enumerate(convs):
-                u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 and i > 0 else None
+                # the stride-2 conv skips tiles whose windows hold no occupied cell (depth >= 1)
+                u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 else None
                 o = pp[i % 2] if self.out_pair(convs, i) else NHWC(pp[i % 2].t, pair=False)
                 x = cv(x, out=o, uni=u)
             outs.append(x)

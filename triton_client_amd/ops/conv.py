@@ -19,6 +19,8 @@ on the GPU-less host).
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Optional
 
@@ -110,7 +112,8 @@ HX3_TILES = (110, 111, 112, 113, 114, 115, 116)
 HX3S2_TILES = (120, 121, 122, 123, 124)
 # conv_wino.hip (3x3 stride-1 by 1-D Winograd F(2,3), 1.5x fewer MFMAs than hx3): the default for
 # every eligible stride-1 layer (WINO False: hx3).  Tiles 130 (auto) and 131-134 select it explicitly.
-WINO = True
+WINO = os.environ.get("TCA_WINO", "1") != "0"  # TCA_WINO=0: hx3 for A/B runs
+WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
 WINO_TILES = (130, 131, 132, 133, 134)
 
 
@@ -287,7 +290,7 @@ class FusedConv:
                 _native.call("tca_conv_hx3s2p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act | (0 if out.pair else 32), *rp,
-                             _native.ptr(occ),
+                             _native.ptr(occ), *self._uni_args(uni, B, Ho, Wo, res),
                              tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
                 return out
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
@@ -329,9 +332,18 @@ class FusedConv:
         return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s in (1, 2) and self.p == 1
                 and self.cin_p % 32 == 0 and self.K == self.Kp and self.N % 64 == 0)
 
+    def _uni_args(self, uni, B, Ho, Wo, res=None):
+        """(depth, uni_min, value) pointers of an optional uniform-tile skip (see _BEVBackbonePlan)."""
+        if uni is None or res is not None:
+            return None, 0, None
+        depth, dmin, val = uni
+        assert depth.dtype == torch.uint8 and tuple(depth.shape) == (B, Ho, Wo), depth.shape
+        assert val.dtype == torch.float32 and val.numel() == self.N, (val.dtype, val.shape)
+        return _native.ptr(depth), dmin, _native.ptr(val)
+
     def wino_ok(self) -> bool:
         """conv_wino.hip takes this conv: hx3's shapes at stride 1, ReLU or no activation."""
-        return self.hx3_ok() and self.s == 1 and self.act in (ACT_NONE, ACT_RELU)
+        return self.hx3_ok() and self.s == 1 and self.act in (ACT_NONE, ACT_RELU) and self.N >= WINO_MIN_N
 
     def _wino(self, x: NHWC, out: NHWC, tile: int, stream, uni) -> NHWC:
         B, H, W, _ = x.shape
