@@ -30,6 +30,8 @@ def main():
         x32 = NHWC(xr.to(dev), pair=False)  # fp32 storage (the chain inside a block)
         o32 = NHWC(torch.empty(B, H, W, c, device=dev), pair=False)
         outs = {t: NHWC(torch.empty(B, H, W, c, device=dev), pair=True) for t in (110, 130)}
+        if os.environ.get("F32"):  # fp32 storage in and out for every wino tile (PMC runs)
+            x, outs[130] = x32, o32
         res = {"shape": [B, H, W, c]}
         for t in tiles:
             if t in (131, 132) and c % 128:

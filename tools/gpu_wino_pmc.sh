@@ -10,7 +10,7 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
             "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   rm -rf /tmp/wpmc$i
-  SHAPE=$S TILES=$T timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/wpmc$i -o run -- python tools/bench_wino.py > gpurun_out/pmc/wino_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/wino_p$i.log; exit 1; }
+  F32=${F32:-} SHAPE=$S TILES=$T timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d /tmp/wpmc$i -o run -- python tools/bench_wino.py > gpurun_out/pmc/wino_p$i.log 2>&1 || { echo "PASS $i FAILED"; tail -5 gpurun_out/pmc/wino_p$i.log; exit 1; }
   f=$(find /tmp/wpmc$i -name "*counter_collection.csv" | head -1)
   cp $f gpurun_out/pmc/wino_s${S}_t${T}_p$i.csv
 done
