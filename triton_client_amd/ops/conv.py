@@ -99,7 +99,7 @@ def _ceil(x, m):
 PRECISIONS = ("fp32", "bf16")
 # split-product tiles with pair-storage instantiations (conv_mfma.hip launch_glds_x3p: global_load_lds
 # kernels 20-42, buffer-descriptor DMA kernels 68-79)
-PAIR_TILES = (20, 22, 24, 25, 26, 30, 32, 35, 37, 41, 42, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 90, 91, 92, 93, 94, 95, 96, 97, 102)
+PAIR_TILES = (20, 22, 24, 25, 26, 32, 37, 41, 42, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 90, 91, 92, 93, 94, 95, 96, 97, 102)
 
 
 # conv_hx3.hip (3x3 stride-1 / stride-2 pair convs with register-streamed fragment-order
