@@ -752,22 +752,31 @@ __global__ void __launch_bounds__(256) bev_uniform_depth_kernel(const unsigned c
                                                                  int Ho, int Wo, int maxd,
                                                                  unsigned char* __restrict__ depth) {
   constexpr int LY = UD_TY + 2 * UD_MAXR, LX = UD_TX + 2 * UD_MAXR;
+  constexpr int OY = 2 * LY + 1, OX = 2 * LX + 1;  // the canvas window behind the u region
   __shared__ unsigned char u[LY * LX];
+  __shared__ unsigned char os[OY * OX];
   const int b = blockIdx.z, ty0 = blockIdx.y * UD_TY, tx0 = blockIdx.x * UD_TX;
   const int R = maxd - 1;
   const int ry = UD_TY + 2 * R, rx = UD_TX + 2 * R;
   const unsigned char* oc = occ + (long)b * H * W;
+  // the occupancy window once into LDS (coalesced byte rows; each canvas byte feeds up to 4 u
+  // cells' 3 x 3 stride-2 windows), outside the canvas as occupied-free
+  const int iy0 = 2 * (ty0 - R) - 1, ix0 = 2 * (tx0 - R) - 1, oy = 2 * ry + 1, ox = 2 * rx + 1;
+  for (int id = threadIdx.x; id < oy * ox; id += blockDim.x) {
+    const int r = id / ox, c = id - (id / ox) * ox;
+    const int iy = iy0 + r, ix = ix0 + c;
+    os[r * OX + c] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? oc[(long)iy * W + ix] : 0;
+  }
+  __syncthreads();
   for (int id = threadIdx.x; id < ry * rx; id += blockDim.x) {
     const int ly = id / rx, lx = id - (id / rx) * rx;
     const int Y = ty0 - R + ly, X = tx0 - R + lx;
     unsigned char good = 0;
     if (Y >= 0 && X >= 0 && Y < Ho && X < Wo) {
-      good = 1;
-      for (int dy = -1; dy <= 1; ++dy)
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int iy = 2 * Y + dy, ix = 2 * X + dx;
-          if (iy >= 0 && ix >= 0 && iy < H && ix < W && oc[(long)iy * W + ix]) good = 0;
-        }
+      const unsigned char* w = os + (2 * ly) * OX + 2 * lx;  // window rows 2 ly .. 2 ly + 2
+      const unsigned any = w[0] | w[1] | w[2] | w[OX] | w[OX + 1] | w[OX + 2] | w[2 * OX] | w[2 * OX + 1] |
+                           w[2 * OX + 2];
+      good = any ? 0 : 1;
     }
     u[ly * LX + lx] = good;
   }
