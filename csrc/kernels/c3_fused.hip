@@ -235,9 +235,14 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
     float4 xr[XPL];
     int xo[XPL];
     long xg[XPL];
+    // 16-B piece q -> (pixel p, float4 f4): 16 consecutive lanes take 8 pixels x both 8-B halves of
+    // one hi / lo plane chunk, so each 16-lane ds_write_b64 group writes 128 contiguous bytes (the
+    // pixel-major order wrote the four planes at one bank offset: 4-way); a wave still reads 8
+    // whole 128-B pixel chunks from global
 #pragma unroll
     for (int k = 0; k < XPL; ++k) {
-      const int q = tid + k * 256, p = q >> 3, f4 = q & 7;
+      const int q = tid + k * 256;
+      const int p = (q >> 6) * 8 + ((q >> 1) & 7), f4 = ((q >> 4) & 3) * 2 + (q & 1);
       long pix;
       const bool in = q < XP && halo_in(p, pix);
       xg[k] = in ? pix * a.ldx + a.x_off + f4 * 4 : -1;
@@ -332,17 +337,29 @@ __global__ void __launch_bounds__(256, 2) c3_fused_kernel(C3fArgs a) {
     // a from a_in on the halo (zeros outside the image: they only reach masked u); every load of
     // this thread issued before the first store
     constexpr int AP = HPP * (C / 4), APL = (AP + 255) / 256;
+    // piece g -> (pixel p, 4-channel group c4): lane pairs take the two halves of one pixel's
+    // 8-channel group, so 16 lanes write 128 contiguous LDS bytes (pixel-major: 2-way) and each
+    // pair reads 32 contiguous global bytes
+    auto piece = [&](int g, int& p, int& c4) {
+      const int h = g >> 1;
+      p = h % HPP;
+      c4 = (h / HPP) * 2 + (g & 1);
+    };
     float4 v[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
-      const int g = tid + k * 256, p = g % HPP, c4 = g / HPP;
+      const int g = tid + k * 256;
+      int p, c4;
+      piece(g, p, c4);
       long pix;
       v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (g < AP && halo_in(p, pix)) v[k] = *reinterpret_cast<const float4*>(a.a_in + pix * a.lda + a.a_off + c4 * 4);
     }
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
-      const int g = tid + k * 256, p = g % HPP, c4 = g / HPP;
+      const int g = tid + k * 256;
+      int p, c4;
+      piece(g, p, c4);
       const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
       if (g < AP) put_a(p, c4 * 4, vv, true);
     }

@@ -349,10 +349,13 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
       h[c] = (__bf16)v[c];
       l[c] = (__bf16)(v[c] - (float)h[c]);
     }
-    *reinterpret_cast<uint4*>(himg + g * 32) = reinterpret_cast<const uint4*>(h)[0];
-    *reinterpret_cast<uint4*>(himg + g * 32 + 16) = reinterpret_cast<const uint4*>(h)[1];
-    *reinterpret_cast<uint4*>(limg + g * 32) = reinterpret_cast<const uint4*>(l)[0];
-    *reinterpret_cast<uint4*>(limg + g * 32 + 16) = reinterpret_cast<const uint4*>(l)[1];
+    // 32-B pixel stride: the two 16-B halves go in an order alternating every 4 pixels, so each
+    // 8-lane ds_write_b128 group covers the 32 banks once (in one order: 2-way)
+    const int q0 = (g >> 2) & 1;
+    *reinterpret_cast<uint4*>(himg + g * 32 + q0 * 16) = reinterpret_cast<const uint4*>(h)[q0];
+    *reinterpret_cast<uint4*>(himg + g * 32 + (q0 ^ 1) * 16) = reinterpret_cast<const uint4*>(h)[q0 ^ 1];
+    *reinterpret_cast<uint4*>(limg + g * 32 + q0 * 16) = reinterpret_cast<const uint4*>(l)[q0];
+    *reinterpret_cast<uint4*>(limg + g * 32 + (q0 ^ 1) * 16) = reinterpret_cast<const uint4*>(l)[q0 ^ 1];
   };
   if (half) {
     // all of this thread's source blocks are requested before any is used (one memory latency
