@@ -95,8 +95,6 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
   };
   const bool vec4 = (pstride & 3) == 0;
   const int rs = min(r, P - 1);
-  // Two-deep pipeline: slot rows are loaded two pillars ahead and points one
-  // pillar ahead, so both dependent loads have a whole pillar of compute to land.
   auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[(long)min(vv, nv - 1) * P + rs] : 0; };
   auto gather = [&](int vv, int id, float (&q)[4]) {
     const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
@@ -111,21 +109,34 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
       q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
     }
   };
+  // Three-deep: slot rows three pillars ahead, points two ahead, the pillar's count and
+  // coordinates one ahead (each dependent load has two pillars of compute to land).
+  auto meta = [&](int vv, int& vc_, int4& co_) {
+    const int vq = min(vv, nv - 1);
+    vc_ = FROM_SLOTS ? vcount[vq] : num_points[vq];
+    co_ = *reinterpret_cast<const int4*>(coords + (long)vq * 4);
+  };
   int v = next_valid(__builtin_amdgcn_readfirstlane((int)wave));
   int vn = v < nv ? next_valid(v + step) : nv;
-  float pc[4];
+  int vnn = vn < nv ? next_valid(vn + step) : nv;
+  float pc[4], pn[4];
   gather(v, slot_of(v), pc);
-  int idx_n = slot_of(vn);
+  gather(vn, slot_of(vn), pn);
+  int idx_nn = slot_of(vnn);
+  int vc;
+  int4 co;
+  meta(v, vc, co);
   while (v < nv) {
     const int b = (unsigned)v / (unsigned)max_voxels;
-    const int vc = FROM_SLOTS ? vcount[v] : num_points[v];
-    const int4 co = *reinterpret_cast<const int4*>(coords + (long)v * 4);
     const int n = min(vc, P);
     const bool real = r < n;
-    const int vnn = vn < nv ? next_valid(vn + step) : nv;
-    const int idx_nn = slot_of(vnn);  // two ahead
-    float pn[4];
-    gather(vn, idx_n, pn);            // one ahead
+    const int v3 = vnn < nv ? next_valid(vnn + step) : nv;
+    const int idx_3 = slot_of(v3);     // three ahead
+    float pnn[4];
+    gather(vnn, idx_nn, pnn);          // two ahead
+    int vc_n;
+    int4 co_n;
+    meta(vn, vc_n, co_n);              // one ahead
     float p[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) p[k] = real ? pc[k] : 0.f;
@@ -196,9 +207,15 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     if (occ && lane == 0) occ[((long)b * g.ny + co.z) * g.nx + co.w] = 1;
     v = vn;
     vn = vnn;
-    idx_n = idx_nn;
+    vnn = v3;
+    idx_nn = idx_3;
+    vc = vc_n;
+    co = co_n;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pc[k] = pn[k];
+    for (int k = 0; k < 4; ++k) {
+      pc[k] = pn[k];
+      pn[k] = pnn[k];
+    }
   }
 }
 

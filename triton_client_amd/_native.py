@@ -154,6 +154,8 @@ def _load_hip() -> ctypes.CDLL:
 
 
 def _lib_path(name: str) -> str:
+    if name == "libtca_kernels.so" and os.environ.get("TCA_KERNELS_LIB"):
+        return os.environ["TCA_KERNELS_LIB"]  # A/B runs against another build of the kernels
     return os.path.join(_build.LIBDIR, name)
 
 
