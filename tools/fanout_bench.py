@@ -34,6 +34,9 @@ def main(argv=None) -> int:
     ap.add_argument("--step-ms", type=float, default=7.3, help="one-GPU step time to feed")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--gpus", type=int, default=8, help="node size for the feed estimate")
+    ap.add_argument("--frame-bytes", type=int, default=FRAME,
+                    help="camera payload bytes (default a raw rgb8 1280x720 frame; a JPEG CompressedImage, the "
+                         "reference's camera topic, is ~220 KB at quality 90)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
 
@@ -43,7 +46,7 @@ def main(argv=None) -> int:
     rng = np.random.default_rng(0)
     n = a.items
     # sources: bytes objects, like deserialised ROS message payloads
-    srcs = [rng.integers(0, 255, FRAME, np.uint8).tobytes() for _ in range(n)] + \
+    srcs = [rng.integers(0, 255, a.frame_bytes, np.uint8).tobytes() for _ in range(n)] + \
         [rng.integers(0, 255, CLOUD, np.uint8).tobytes() for _ in range(n)]
     sizes = [len(s) for s in srcs]
     total = sum(sizes)
@@ -72,7 +75,7 @@ def main(argv=None) -> int:
             print(f"threads {t:3d}: {med * 1e3:7.2f} ms per GPU-step of {total / 1e6:.1f} MB = {gbs:6.1f} GB/s "
                   f"-> rank 0 feeds {feed:4.1f} GPUs at {a.step_ms} ms/step", flush=True)
         best = max(rows, key=lambda r: r["GBps"])
-        out = {"tool": "tools/fanout_bench.py", "items_per_gpu": n, "frame_bytes": FRAME, "cloud_bytes": CLOUD,
+        out = {"tool": "tools/fanout_bench.py", "items_per_gpu": n, "frame_bytes": a.frame_bytes, "cloud_bytes": CLOUD,
                "step_ms": a.step_ms, "cpus_allowed": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
                "rows": rows, "best": best, "node_gpus": a.gpus,
                "node_step_copy_ms_at_best": best["median_ms"] * a.gpus,

@@ -65,6 +65,10 @@ _ALIGN = 4096
 log = logging.getLogger("triton_client_amd.ring_dp")
 
 
+# rank 0's ring copy threads: 8 measured fastest on the 256-CPU box (147.5 GB/s vs 137.1 at 16 and 119.6
+# at 32: one socket's memory bandwidth, profiles/r5/fanout/fanout_raw675.json)
+COPY_THREADS = int(os.environ.get("TCA_RING_COPY_THREADS", "8"))
+
 def _align(n: int) -> int:
     return (int(n) + _ALIGN - 1) // _ALIGN * _ALIGN
 
@@ -199,7 +203,7 @@ class _RingDP:
         for i, z in enumerate(out_sizes):
             items[i, I_OUT], items[i, I_OUTSZ] = off, z
             off += _align(z)
-        gather_copy([data.base + base + int(items[i, I_IN]) for i in range(n)], payloads, sizes, 16)
+        gather_copy([data.base + base + int(items[i, I_IN]) for i in range(n)], payloads, sizes, COPY_THREADS)
         hdr = ring.header(s)
         hdr[:] = 0
         mask = 0
