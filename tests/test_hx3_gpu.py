@@ -196,3 +196,25 @@ def test_hx3s2_occupancy_skips_are_exact(cuda, tile, pattern):
         outs.append(o.t)
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [120, 121, 124])
+def test_hx3s2_fp32_storage_out(cuda, tile):
+    """act flag 32: the stride-2 kernel writes fp32 storage (the input of an F(2,3) layer, see
+    models/fast.py _BEVBackbonePlan.out_pair): the same accumulators as the pair output, so the
+    two decode to within the hi / lo split error, and the fp32 tile meets the fp64 budget."""
+    torch.manual_seed(11)
+    B, H, W, cin, cout = 2, 37, 29, 64, 128
+    conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    x = NHWC(to_pairs(torch.randn(B, H, W, cin)).to(cuda), pair=True)
+    Ho, Wo = fc.out_hw(H, W)
+    op = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=True)
+    of = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=False)
+    fc(x, out=op, tile=tile)
+    fc(x, out=of, tile=tile)
+    torch.cuda.synchronize()
+    assert rel_l2(op.nchw(), of.t.permute(0, 3, 1, 2)) < 2e-5
+    ref = torch.relu(conv(from_pairs(x.t).double().cpu().permute(0, 3, 1, 2)))
+    assert rel_l2(of.t.permute(0, 3, 1, 2), ref) < 5e-5
