@@ -45,7 +45,7 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
 }
 
 template <bool FROM_SLOTS, typename CT, int PFIX = 0>
-__global__ void __launch_bounds__(256) pillar_vfe_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) pillar_vfe_kernel(
     const float* __restrict__ pts, int pstride, int max_pts,               // FROM_SLOTS source
     const int* __restrict__ slots, const int* __restrict__ vcount,        // FROM_SLOTS source
     const float* __restrict__ voxels, const int* __restrict__ num_points,  // materialised source [V][P][4]
@@ -60,21 +60,29 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
 
-  // B fragments (weights), hi/lo, two 32-column tiles: lane holds W[c][k=8h+j].
-  bf16x8 bh[2], bl[2];
+  // B fragments (weights), hi/lo, two 32-column tiles: lane holds W[c][k=8h+j].  They stay in
+  // LDS ([t][hi|lo][64 lanes][16 B], 4 KiB, read per pillar, conflict-free) rather than 16 VGPRs:
+  // the kernel then fits 64 VGPRs, 8 waves per SIMD alone and 2 beside the BEV neck.
+  __shared__ bf16x8 wfrag[2][2][64];
+  if (threadIdx.x < 64) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c = 32 * t + r;
+    for (int t = 0; t < 2; ++t) {
+      const int c = 32 * t + r;
+      bf16x8 hv, lv;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;
-      const float w = k < 10 ? W[c * 10 + k] : 0.f;
-      __bf16 hi, lo;
-      split_bf16(w, hi, lo);
-      bh[t][j] = hi;
-      bl[t][j] = lo;
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * h + j;
+        const float w = k < 10 ? W[c * 10 + k] : 0.f;
+        __bf16 hi, lo;
+        split_bf16(w, hi, lo);
+        hv[j] = hi;
+        lv[j] = lo;
+      }
+      wfrag[t][0][lane] = hv;
+      wfrag[t][1][lane] = lv;
     }
   }
+  __syncthreads();
   const float b_my0 = bias[r], b_my1 = bias[32 + r];
 
   // 32-bit pillar indices (B * max_voxels < 2^31): 64-bit div/mod is ~150 VALU.
@@ -174,10 +182,11 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
     float m[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      const bf16x8 bh = wfrag[t][0][lane], bl = wfrag[t][1][lane];
       f32x16 acc = {};
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
       float mm = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -186,6 +195,7 @@ __global__ void __launch_bounds__(256) pillar_vfe_kernel(
       }
       mm = fmaxf(mm, __shfl_xor(mm, 32, 64));
       m[t] = mm;
+      __builtin_amdgcn_sched_barrier(0);  // one tile's 16 accumulators live at a time
     }
     // lanes 0-31 -> channel r (tile 0), lanes 32-63 -> channel 32 + r (tile 1)
     const float val = fmaxf((h == 0 ? m[0] + b_my0 : m[1] + b_my1), 0.f);
