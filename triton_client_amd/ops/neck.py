@@ -10,6 +10,7 @@ the unfused plan for shapes outside the contract.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Sequence
 
 import torch
@@ -75,9 +76,11 @@ class FusedNeckHead:
         if grid <= 0:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
-        # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 1 = <8 waves, 3 stages> (977 vs 1061 us for
-        # 0 = <8, 2> at batch 32 once the DMA issue moved to buffer resources, profiles/r5/neck_ab.log)
-        self.variant = 1
+        # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = <8 waves, 2 stages>, 99.6 KiB LDS; 1 = <8, 3>,
+        # 149 KiB.  Alone, 1 is faster (977 vs 1061 us at batch 32, profiles/r5/neck_ab.log); in the headline
+        # step, where the neck runs beside the VFE and the camera's first kernels, 0 leaves them LDS on every
+        # CU: 4658 vs 4635 frame pairs/s over six same-box pairs (profiles/r5/neck_variant_ab.txt)
+        self.variant = int(os.environ.get("TCA_NECK_VARIANT", "0"))
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
             self.wh = split_pairs(wh).to(device)
