@@ -402,7 +402,7 @@ struct NeckArgsX3 {
 // PAIR: branch inputs in pair storage ({hi 8 | lo 8} per 8 channels, see
 // conv_mfma.hip pair_split8): the A fragments are read as stored, no split.
 template <bool PAIR, int NWV, int STAGES, int FM_ = 2>
-__global__ void __launch_bounds__(NWV * 64) bev_neck_head_x3_kernel(NeckArgsX3 a) {
+__global__ void __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) bev_neck_head_x3_kernel(NeckArgsX3 a) {
   using T = NeckX3<NWV, STAGES, FM_>;
   constexpr int Y_BM = T::BM, Y_FM = T::FM, Y_STAGES = STAGES, Y_STAGE = T::STAGE, Y_A_BYTES = T::A_BYTES;
   constexpr int Y_B_BYTES = T::B_BYTES, Y_BH_OFF = T::BH_OFF, Y_A_INS = T::A_INS, Y_B_INS = T::B_INS;
@@ -737,8 +737,9 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
   if (B <= 0) return 0;
   if (nbr < 1 || nbr > MAXBR || nh <= 0 || nh > NH || (nh & 3) || (ldo & 3) || grid < 8 || (grid & 7))
     return (int)hipErrorInvalidValue;
-  // 0 (also accepted as 3, its former number): <8 waves, 2 stages>; 1: <8, 3> (two K steps in flight)
-  if (variant != 0 && variant != 3 && variant != 1) return (int)hipErrorInvalidValue;
+  // 0: <8 waves, 2 stages>; 1: <8, 3> (two K steps in flight); 2: <4, 2>, 128-pixel tiles, two
+  // workgroups per CU (66 KiB LDS and <= 256 VGPRs each; the grid doubles)
+  if (variant < 0 || variant > 2) return (int)hipErrorInvalidValue;
   NeckArgsX3 a;
   int S = 1, nsteps = 0;
   for (int i = 0; i < nbr; ++i) {
@@ -780,6 +781,7 @@ int neck_x3(int nbr, const void* const* x, const int* ldx, const int* offx, cons
     a.B = nb;
     // grid: workgroup slots of the persistent kernel, one per CU
     if (variant == 1) launch_neck_x3<8, 3>(a, (long)nb * nq, grid, pair, stream);
+    else if (variant == 2) launch_neck_x3<4, 2>(a, (long)nb * nq, 2 * grid, pair, stream);
     else launch_neck_x3<8, 2>(a, (long)nb * nq, grid, pair, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;

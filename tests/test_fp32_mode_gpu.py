@@ -135,10 +135,10 @@ def test_preprocess_s2d_fp32(cuda):
     assert (out.cpu() - ref).abs().mean().item() < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_fused_neck_x3_vs_unfused(cuda, variant):
-    """fp32 fused deconv + head (streamed split head weights) == the fp32 module (the
-    one tiling, under both its numbers)."""
+    """fp32 fused deconv + head (streamed split head weights) == the fp32 module; every
+    tiling (2 / 3 stages, 8 waves; 2 stages, 4 waves, two workgroups per CU) gives the same bits."""
     from triton_client_amd.models.fast import FastBEV
     from test_fast_plans import _small_pp
 

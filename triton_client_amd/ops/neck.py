@@ -79,7 +79,9 @@ class FusedNeckHead:
         # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = <8 waves, 2 stages>, 99.6 KiB LDS; 1 = <8, 3>,
         # 149 KiB.  Alone, 1 is faster (977 vs 1061 us at batch 32, profiles/r5/neck_ab.log); in the headline
         # step, where the neck runs beside the VFE and the camera's first kernels, 0 leaves them LDS on every
-        # CU: 4658 vs 4635 frame pairs/s over six same-box pairs (profiles/r5/neck_variant_ab.txt)
+        # CU: 4658 vs 4635 frame pairs/s over six same-box pairs (profiles/r5/neck_variant_ab.txt).  2 = <4, 2>
+        # (two workgroups per CU) is the fastest alone (883 vs 1056 us) but not in the step: 4617 vs 4652
+        # (profiles/r5/neck_variant2_ab.txt)
         self.variant = int(os.environ.get("TCA_NECK_VARIANT", "0"))
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
