@@ -405,3 +405,139 @@ def test_ring_data_area_reserved_or_clear_error(monkeypatch):
     finally:
         monkeypatch.undo()
         ring.close()
+
+
+# ------------------------------------------------------------------ ingest arena: payloads deserialised into the ring
+def test_ingest_arena_fifo_allocator():
+    """Blocks are handed out in order, freed out of order (the tail advances over freed
+    blocks only), wrap at the end, and a full arena returns None instead of blocking."""
+    import gc
+
+    from triton_client_amd.parallel.host_ring import IngestArena
+
+    path = f"/dev/shm/tca_test_arena_{os.getpid()}"
+    ar = IngestArena(path, 4096, True, pin=False)
+    try:
+        a = ar.alloc(1000)  # 1024 B blocks
+        b = ar.alloc(1000)
+        c = ar.alloc(1000)
+        assert [ar.offset_of(x, 1000) for x in (a, b, c)] == [0, 1024, 2048]
+        a[:] = 1
+        view = memoryview(b)[10:20]  # a view keeps its block alive
+        del b
+        gc.collect()
+        assert ar.in_use() == 3072
+        d = ar.alloc(1000)
+        assert ar.offset_of(d, 1000) == 3072 and ar.alloc(100) is None and ar.stats["full"] == 1
+        del a
+        gc.collect()
+        e = ar.alloc(1000)  # wraps into a's block
+        assert ar.offset_of(e, 1000) == 0
+        del view, c
+        gc.collect()
+        f = ar.alloc(2000)  # b and c freed behind e: the tail moved past them
+        assert ar.offset_of(f, 2000) == 1024
+        assert ar.offset_of(np.zeros(10, np.uint8), 10) is None and ar.offset_of(b"xy", 2) is None
+        del d, e, f
+        gc.collect()
+        assert ar.in_use() == 0
+    finally:
+        ar.close(unlink=True)
+    assert not os.path.exists(path)
+
+
+def test_deserialize_into_caller_buffers(tmp_path):
+    """rosmsg.deserialize / Bag.read_messages put large byte arrays into alloc() buffers
+    (the ring's ingest arena) and leave small ones as bytes; the messages are unchanged."""
+    from triton_client_amd.ros import compat, msgs, rosmsg
+    from triton_client_amd.ros.bag import Bag
+
+    frame = np.random.default_rng(0).integers(0, 255, (120, 200, 3), np.uint8)
+    m = compat.numpy_to_imgmsg(frame, "rgb8", header=msgs.Header(seq=3))
+    small = compat.numpy_to_imgmsg(frame[:4, :4], "rgb8")
+    got = []
+
+    def alloc(n):
+        got.append(n)
+        return np.zeros(n, np.uint8)
+    for msg in (m, small):
+        back = rosmsg.deserialize(rosmsg.serialize(msg), "sensor_msgs/Image", alloc)
+        assert bytes(back.data) == bytes(msg.data) and back.header.seq == msg.header.seq
+    assert got == [frame.nbytes]
+    assert isinstance(rosmsg.deserialize(rosmsg.serialize(m), "sensor_msgs/Image").data, bytes)
+    for kind in ("rosbag", "tca"):
+        path = str(tmp_path / f"x_{kind}.bag")
+        if kind == "rosbag":
+            from triton_client_amd.ros.bag import RosBag
+            w = RosBag(path, "w")
+        else:
+            w = Bag(path, "w")
+        w.write("/cam", m)
+        w.close()
+        got.clear()
+        with Bag(path) as b:
+            (_, back, _), = list(b.read_messages(topics=["/cam"], alloc=alloc))
+        assert got == [frame.nbytes] and isinstance(back.data, memoryview), kind
+        np.testing.assert_array_equal(compat.imgmsg_to_numpy(back, "rgb8"), frame)
+
+
+class _SumEngine:
+    """Host engine whose 'detection' is a checksum of the frame: a peer that read the
+    wrong bytes shows up in the result."""
+    names = []
+
+    def detect(self, frames):
+        return [np.array([[float(f.sum() % 100003), float(f[0, 0, 0]), 0, 0, 1, 0]], np.float32) for f in frames]
+
+
+def _arena_worker(rank, world, port, q, arena_mb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TCA_NUMA_BIND="0")
+    try:
+        from triton_client_amd.parallel.dp import init_distributed
+        from triton_client_amd.parallel.ring_dp import DataParallelDetector2D
+        from triton_client_amd.ros import compat, msgs, rosmsg
+
+        info = init_distributed("gloo")
+        dp = DataParallelDetector2D(_SumEngine(), info, nslots=2, arena_mb=arena_mb)
+        if info.is_main:
+            rng = np.random.default_rng(1)
+            wire = [rosmsg.serialize(compat.numpy_to_imgmsg(rng.integers(0, 255, (160, 256, 3), np.uint8), "rgb8",
+                                                            header=msgs.Header(seq=i))) for i in range(9)]
+            res = []
+            for rep in range(3):  # more steps than slots: blocks are freed and reused
+                ms = [rosmsg.deserialize(w, "sensor_msgs/Image", dp.ingest_buffer) for w in wire]
+                res.append([d for _, d in dp.process(ms, draw=False)])
+                want = _SumEngine().detect([compat.imgmsg_to_numpy(x, "rgb8") for x in ms])
+                for d, w in zip(res[-1], want):
+                    np.testing.assert_array_equal(d, w)
+                del ms
+            q.put((0, (dp.arena_items, dp.copied_items, dp.steps)))
+            dp.close()
+        else:
+            q.put((rank, dp.serve()))
+            dp.ring.close()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("arena_mb", [4, 0])
+def test_ring_payloads_from_ingest_arena_two_ranks(arena_mb):
+    """Frames deserialised into rank 0's ingest arena reach rank 1 without a slot copy
+    (every item read from the arena) and give the same results as the copy path
+    (arena off)."""
+    _runtime_or_skip()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_arena_worker, args=(r, 2, port, q, arena_mb)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert res[1] == 3, res
+    assert res[0] == ((27, 0, 3) if arena_mb else (0, 27, 3)), res

@@ -38,6 +38,9 @@ def main(argv=None) -> int:
                     help="camera payload bytes (default a raw rgb8 1280x720 frame; a JPEG CompressedImage, the "
                          "reference's camera topic, is ~220 KB at quality 90)")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--deserialize", action="store_true",
+                    help="also measure deserialising the node batch's wire messages into bytes (the copy path: the "
+                         "ring copy comes on top) vs into the ring's ingest arena (the only copy)")
     a = ap.parse_args(argv)
 
     from triton_client_amd.inference.live import gather_copy
@@ -75,11 +78,12 @@ def main(argv=None) -> int:
             print(f"threads {t:3d}: {med * 1e3:7.2f} ms per GPU-step of {total / 1e6:.1f} MB = {gbs:6.1f} GB/s "
                   f"-> rank 0 feeds {feed:4.1f} GPUs at {a.step_ms} ms/step", flush=True)
         best = max(rows, key=lambda r: r["GBps"])
+        deser = _deserialize_rows(a, srcs, total) if a.deserialize else None
         out = {"tool": "tools/fanout_bench.py", "items_per_gpu": n, "frame_bytes": a.frame_bytes, "cloud_bytes": CLOUD,
                "step_ms": a.step_ms, "cpus_allowed": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
                "rows": rows, "best": best, "node_gpus": a.gpus,
                "node_step_copy_ms_at_best": best["median_ms"] * a.gpus,
-               "feeds_node": best["gpus_fed_at_1gpu_rate"] >= a.gpus}
+               "feeds_node": best["gpus_fed_at_1gpu_rate"] >= a.gpus, "deserialize": deser}
         print(json.dumps({"best_GBps": best["GBps"], "gpus_fed": best["gpus_fed_at_1gpu_rate"],
                           "cpus_allowed": out["cpus_allowed"]}))
         if a.json:
@@ -88,6 +92,55 @@ def main(argv=None) -> int:
     finally:
         ring.close()
     return 0
+
+
+def _deserialize_rows(a, srcs, total):
+    """Rank 0's ingest with the arena: each wire message (a serialised Image / PointCloud2)
+    deserialised once, its payload written into the arena (``rosmsg.deserialize(.., alloc)``,
+    numpy copies outside the GIL), and nothing copied by the ring step -- against
+    deserialising into ``bytes`` (the copy path, before its ring copy)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from triton_client_amd.parallel.host_ring import IngestArena
+    from triton_client_amd.ros import msgs, rosmsg
+
+    n = a.items
+    wire = []
+    for i, s in enumerate(srcs):
+        if i < n:
+            m = msgs.Image(height=1, width=len(s) // 3, encoding="rgb8", step=len(s), data=s)
+            wire.append((rosmsg.serialize(m), "sensor_msgs/Image"))
+        else:
+            m = msgs.PointCloud2(height=1, width=len(s) // 16, point_step=16, row_step=len(s), data=s)
+            wire.append((rosmsg.serialize(m), "sensor_msgs/PointCloud2"))
+    arena = IngestArena(f"/dev/shm/tca_fanout_in_{os.getpid()}", 3 * (total + 256 * len(srcs)), True, pin=False)
+    rows = []
+    try:
+        for t in [int(v) for v in a.threads.split(",")]:
+            with ThreadPoolExecutor(t) as pool:
+                for mode in ("bytes", "arena"):
+                    alloc = arena.alloc if mode == "arena" else None
+
+                    def one(w, alloc=alloc):
+                        return rosmsg.deserialize(w[0], w[1], alloc)
+                    ts = []
+                    for r in range(a.reps + 3):
+                        t0 = time.perf_counter()
+                        out = list(pool.map(one, wire))
+                        dt = time.perf_counter() - t0
+                        if mode == "arena":
+                            assert all(isinstance(m.data, memoryview) for m in out)
+                        del out
+                        if r >= 3:
+                            ts.append(dt)
+                    med = float(np.median(ts))
+                    rows.append({"threads": t, "mode": mode, "median_ms": med * 1e3, "GBps": total / med / 1e9,
+                                 "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med})
+                    print(f"deserialise into {mode:5s}, {t:3d} threads: {med * 1e3:7.2f} ms per GPU-step = "
+                          f"{total / med / 1e9:6.1f} GB/s", flush=True)
+    finally:
+        arena.close(unlink=True)
+    return rows
 
 
 if __name__ == "__main__":

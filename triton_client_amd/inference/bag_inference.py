@@ -22,6 +22,12 @@ from .ros_inference import RosInference
 from .ros_inference3d import RosInference3D
 
 
+def _ingest(engine):
+    """The data-parallel engine's ingest arena allocator (payloads deserialised
+    straight into the node's host ring), or None."""
+    return getattr(engine, "ingest_buffer", None)
+
+
 def _batches(it, n):
     buf = []
     for item in it:
@@ -51,7 +57,8 @@ class BagInference2D(RosInference):
         count = 0
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
-            it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq))
+            it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
+                                                     alloc=_ingest(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]
@@ -96,7 +103,8 @@ class BagInference3D(RosInference3D):
         count = 0
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
-            it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq))
+            it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
+                                                     alloc=_ingest(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]

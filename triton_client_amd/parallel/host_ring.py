@@ -11,7 +11,7 @@ from the shared pages).  Each rank decodes its own JPEGs on its own (NUMA-
 local) cores.  Annotated frames come back the same way: each rank DMAs them
 into the slot's output area.  Only the detections travel over RCCL.
 
-Two shared-memory files per ring:
+Shared-memory files per ring:
 
 * control ``/dev/shm/<name>_ctl``: a header page, then per slot a 64 KiB
   control block — the slot's ``ready`` sequence word, one ``ack`` word per
@@ -20,6 +20,9 @@ Two shared-memory files per ring:
   area.  When a batch needs more room rank 0 starts a new generation (after
   every slot has drained); the header names the generation and peers attach
   to it on sight.
+* ingest arena ``/dev/shm/<name>_in`` (optional, fixed size): rank 0's
+  deserialisers write message payloads straight into it (:class:`IngestArena`),
+  so the step records offsets there instead of copying payloads into the slot.
 
 Signalling is by 32-bit sequence words with release/acquire ordering and
 futex sleep/wake (``csrc/runtime/host_ring.cpp``): rank 0 writes a slot, then
@@ -35,6 +38,7 @@ from __future__ import annotations
 import ctypes
 import mmap
 import os
+import weakref
 from typing import Iterable, List, Optional
 
 import numpy as np
@@ -152,11 +156,119 @@ class DataRing:
                 pass
 
 
-class HostRing:
-    """Control ring + the current data generation.  Rank 0 ``create``s, the
-    other ranks ``attach`` (after a barrier)."""
+class IngestArena:
+    """Rank 0's deserialisers write message payloads straight into this area.
 
-    def __init__(self, name: str, nslots: int = 4, world: int = 1, create: bool = False, pin: bool = True):
+    Without it a payload is copied twice in rank 0: the wire / bag record into a
+    ``bytes`` object (the deserialiser), then into the ring slot (``_write_step``,
+    one process copying the whole node batch: 6.6 GPUs fed with raw rgb8 frames,
+    ``profiles/r5/fanout/``).  With it the deserialiser's copy *is* the ring copy:
+    ``alloc(n)`` hands out a buffer inside a shared, page-locked mapping that every
+    rank attached at start-up, the message's ``data`` views it, and the step only
+    records the payload's offset (item ``I_SRC`` = 1) -- rank 0's step copies
+    nothing, and the one remaining copy runs in whichever threads deserialise.
+
+    Allocation is a circular first-in-first-out arena: blocks are handed out in
+    order and the tail advances over freed blocks, so frees may come out of order
+    (a held message keeps only the blocks behind it).  A block is free when every
+    view of its array is gone (``weakref.finalize``); rank 0 holds the messages of a
+    step until every participant has acked it, so a peer never reads a freed block.
+    A full arena returns None and the caller keeps an ordinary ``bytes`` payload
+    (the slot-copy path): ingest never blocks on the arena."""
+
+    ALIGN = 256
+
+    def __init__(self, path: str, size: int, create: bool, pin: bool):
+        import collections
+        import threading
+
+        self.path, self.size = path, int(size)
+        self.mm = _open(path, self.size, create)
+        self.buf = np.frombuffer(self.mm, np.uint8)
+        self.base = self.buf.ctypes.data
+        self.pinned = _host_register(self.mm, self.size) if pin else False
+        self._lock = threading.Lock()
+        self._live = collections.deque()  # [offset, bytes, freed] in allocation order
+        self._head = 0
+        self.stats = {"allocs": 0, "bytes": 0, "full": 0}
+
+    def _fit(self, z: int) -> Optional[int]:
+        if not self._live:
+            self._head = 0
+            return 0 if z <= self.size else None
+        tail = self._live[0][0]
+        if self._head > tail:  # live blocks are [tail, head): room after head, else wrap to 0
+            if self._head + z <= self.size:
+                return self._head
+            return 0 if z <= tail else None
+        return self._head if self._head + z <= tail else None  # wrapped: room up to the tail
+
+    def alloc(self, n: int) -> Optional[np.ndarray]:
+        """A writable uint8 array of ``n`` bytes inside the arena, or None when it is full."""
+        n = int(n)
+        z = max(self.ALIGN, (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN)
+        if self.mm is None:
+            return None
+        with self._lock:
+            off = self._fit(z)
+            if off is None:
+                self.stats["full"] += 1
+                return None
+            rec = [off, z, False]
+            self._live.append(rec)
+            self._head = off + z
+            self.stats["allocs"] += 1
+            self.stats["bytes"] += n
+        # a fresh array over the mapping (not a slice of self.buf): numpy collapses view
+        # chains to the last ndarray, so slices and memoryviews of *this* array keep it alive
+        arr = np.frombuffer(self.mm, np.uint8, n, off)
+        weakref.finalize(arr, self._free, rec)
+        return arr
+
+    def _free(self, rec) -> None:
+        with self._lock:
+            rec[2] = True
+            while self._live and self._live[0][2]:
+                self._live.popleft()
+
+    def offset_of(self, payload, nbytes: int) -> Optional[int]:
+        """The arena offset of a payload buffer that lies inside the arena, else None."""
+        if self.mm is None or nbytes <= 0:
+            return None
+        try:
+            addr = np.frombuffer(payload, np.uint8, 1).ctypes.data
+        except (TypeError, ValueError):
+            return None
+        off = addr - self.base
+        return off if 0 <= off and off + nbytes <= self.size else None
+
+    def in_use(self) -> int:
+        with self._lock:
+            return sum(r[1] for r in self._live if not r[2])
+
+    def close(self, unlink: bool = False) -> None:
+        if self.pinned:
+            _host_unregister(self.mm)
+            self.pinned = False
+        self.buf = None
+        try:
+            self.mm.close()
+            self.mm = None
+        except BufferError:  # payload views still alive: the mapping goes with them
+            pass
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+class HostRing:
+    """Control ring + the current data generation (+ the ingest arena, when one was
+    asked for).  Rank 0 ``create``s, the other ranks ``attach`` (after a barrier)."""
+
+    def __init__(self, name: str, nslots: int = 4, world: int = 1, create: bool = False, pin: bool = True,
+                 arena_bytes: int = 0):
         if not name or "/" in name:
             raise ValueError(f"ring name {name!r}")
         if world > 64:
@@ -164,17 +276,29 @@ class HostRing:
         self.name, self.pin = name, pin
         self.ctl_path = os.path.join("/dev/shm", name + "_ctl")
         size = 4096 + nslots * CTL_SLOT
+        self.arena: Optional[IngestArena] = None
+        self.arena_path = os.path.join("/dev/shm", name + "_in")
         if create:
             self.mm = _open(self.ctl_path, size, True)
             hdr = np.frombuffer(self.mm, np.int64, 4, 0)
-            hdr[:] = (MAGIC, nslots, world, 0)
+            arena_bytes = (int(arena_bytes) + 4095) // 4096 * 4096
+            if arena_bytes > 0:
+                try:
+                    self.arena = IngestArena(self.arena_path, arena_bytes, True, pin)
+                except RingSpaceError as e:  # the ring still works: payloads are copied into the slots
+                    import logging
+                    logging.getLogger("triton_client_amd.host_ring").warning("no ingest arena: %s", e)
+                    arena_bytes = 0
+            hdr[:] = (MAGIC, nslots, world, arena_bytes)
         else:
             mm = _open(self.ctl_path, 4096, False)
-            magic, nslots, world, _ = np.frombuffer(mm, np.int64, 4, 0).tolist()
+            magic, nslots, world, arena_bytes = np.frombuffer(mm, np.int64, 4, 0).tolist()
             mm.close()
             if magic != MAGIC:
                 raise RuntimeError(f"{self.ctl_path} is not a host ring")
             self.mm = _open(self.ctl_path, 4096 + nslots * CTL_SLOT, False)
+            if arena_bytes > 0:
+                self.arena = IngestArena(self.arena_path, arena_bytes, False, pin)
         self.nslots, self.world = int(nslots), int(world)
         self.ctl = np.frombuffer(self.mm, np.uint8)
         self.ctl_base = self.ctl.ctypes.data
@@ -251,6 +375,9 @@ class HostRing:
         if self.data is not None:
             self.data.close(unlink=self.owner)
             self.data = None
+        if self.arena is not None:
+            self.arena.close(unlink=self.owner)
+            self.arena = None
         try:
             self.mm.close()
         except BufferError:

@@ -58,8 +58,8 @@ KIND_STOP, KIND_JPEG, KIND_FRAMES, KIND_CLOUDS = -1, 1, 2, 3
 # header ints
 H_SEQ, H_KIND, H_N, H_GEN, H_SLOT, H_MASK, H_PER, H_DRAW, H_KEY = 0, 1, 2, 3, 4, 5, 6, 7, 8
 H_CALIB = 60  # 1: rank 0 broadcasts its freshly calibrated weights in this step (every rank joins)
-# item ints: in_off, in_size, out_off, out_size, meta0, meta1
-I_IN, I_INSZ, I_OUT, I_OUTSZ, I_M0, I_M1 = range(6)
+# item ints: in_off, in_size, out_off, out_size, meta0, meta1, in_src (0: the slot, 1: the ingest arena)
+I_IN, I_INSZ, I_OUT, I_OUTSZ, I_M0, I_M1, I_SRC = range(7)
 _ALIGN = 4096
 
 log = logging.getLogger("triton_client_amd.ring_dp")
@@ -68,6 +68,9 @@ log = logging.getLogger("triton_client_amd.ring_dp")
 # rank 0's ring copy threads: 8 measured fastest on the 256-CPU box (147.5 GB/s vs 137.1 at 16 and 119.6
 # at 32: one socket's memory bandwidth, profiles/r5/fanout/fanout_raw675.json)
 COPY_THREADS = int(os.environ.get("TCA_RING_COPY_THREADS", "8"))
+# rank 0's ingest arena (host_ring.IngestArena) in MiB when world > 1: deserialisers write payloads
+# straight into it and the ring step copies nothing; 0 turns it off (every payload copied into the slot)
+ARENA_MB = int(os.environ.get("TCA_RING_ARENA_MB", "512"))
 
 def _align(n: int) -> int:
     return (int(n) + _ALIGN - 1) // _ALIGN * _ALIGN
@@ -89,7 +92,7 @@ class _RingDP:
     """Shared protocol; subclasses define the message kinds and the local run."""
 
     def __init__(self, local, info: DistInfo, monitor: Optional[HealthMonitor] = None, nslots: int = 4,
-                 comm=None, ack_timeout_s: float = 120.0):
+                 comm=None, ack_timeout_s: float = 120.0, arena_mb: Optional[int] = None):
         self.local, self.info, self.monitor = local, info, monitor
         self.names = list(getattr(local, "names", []) or [])
         self.ex = FrameExchange(info, native=comm)
@@ -97,6 +100,7 @@ class _RingDP:
         self.retries = 0
         self.seq = 0
         self.steps = 0
+        self.arena_items = self.copied_items = 0  # rank 0: payloads read from the arena / copied into slots
         self.ack_timeout_s = ack_timeout_s
         self._lock = threading.Lock()
         self.gpu = (getattr(getattr(local, "device", None), "type", "cpu") == "cuda"
@@ -106,7 +110,8 @@ class _RingDP:
         if info.world > 1:
             dist.broadcast_object_list(name, src=0)
         if info.is_main:
-            self.ring = HostRing(name[0], nslots, info.world, create=True)
+            arena = (ARENA_MB if arena_mb is None else int(arena_mb)) << 20 if info.world > 1 else 0
+            self.ring = HostRing(name[0], nslots, info.world, create=True, arena_bytes=arena)
         if info.world > 1:
             dist.barrier()
         if not info.is_main:
@@ -120,6 +125,22 @@ class _RingDP:
         self._lease_lock = threading.Lock()
 
     # ------------------------------------------------------------------ rank 0
+    def ingest_buffer(self, nbytes: int) -> Optional[np.ndarray]:
+        """Rank 0's deserialisers: a writable ``nbytes`` buffer in the ring's ingest
+        arena for a message payload (``rosmsg.deserialize(..., alloc=)``,
+        ``Bag.read_messages(..., alloc=)``).  A payload there reaches every rank
+        without rank 0 copying it into a slot.  None: no arena (one rank, or
+        ``TCA_RING_ARENA_MB=0``) or full -- keep a ``bytes`` payload."""
+        arena = self.ring.arena if self.info.is_main else None
+        return arena.alloc(nbytes) if arena is not None else None
+
+    def _raw(self, items, i: int, view: np.ndarray) -> np.ndarray:
+        """Item i's input bytes: in the slot (``view``) or in the ingest arena."""
+        off, n = int(items[i, I_IN]), int(items[i, I_INSZ])
+        if int(items[i, I_SRC]) == 1:
+            return self.ring.arena.buf[off:off + n]
+        return view[off:off + n]
+
     def _participants(self) -> List[int]:
         return self.monitor.alive() if self.monitor is not None else list(range(self.info.world))
 
@@ -178,7 +199,9 @@ class _RingDP:
         seq, s = self.seq, self.seq % self.nslots
         free = self._drain(s)
         sizes = [len(p) if not isinstance(p, np.ndarray) else p.nbytes for p in payloads]
-        need = sum(_align(z) for z in sizes) + sum(_align(z) for z in out_sizes)
+        arena = self.ring.arena
+        at = [arena.offset_of(p, z) if arena is not None else None for p, z in zip(payloads, sizes)]
+        need = sum(_align(z) for z, a in zip(sizes, at) if a is None) + sum(_align(z) for z in out_sizes)
         ring = self.ring
         if ring.data is None or need > ring.data.slot_bytes or not free:
             if ring.data is not None:
@@ -197,13 +220,23 @@ class _RingDP:
         items = ring.items(s)
         items[:n] = 0
         off = 0
-        for i, (z, (m0, m1)) in enumerate(zip(sizes, metas)):
-            items[i, I_IN], items[i, I_INSZ], items[i, I_M0], items[i, I_M1] = off, z, m0, m1
-            off += _align(z)
+        copy = []
+        for i, (z, (m0, m1), a) in enumerate(zip(sizes, metas, at)):
+            items[i, I_INSZ], items[i, I_M0], items[i, I_M1] = z, m0, m1
+            if a is not None:  # already in the ingest arena: every rank reads it there
+                items[i, I_IN], items[i, I_SRC] = a, 1
+            else:
+                items[i, I_IN] = off
+                copy.append(i)
+                off += _align(z)
         for i, z in enumerate(out_sizes):
             items[i, I_OUT], items[i, I_OUTSZ] = off, z
             off += _align(z)
-        gather_copy([data.base + base + int(items[i, I_IN]) for i in range(n)], payloads, sizes, COPY_THREADS)
+        if copy:
+            gather_copy([data.base + base + int(items[i, I_IN]) for i in copy], [payloads[i] for i in copy],
+                        [sizes[i] for i in copy], COPY_THREADS)
+        self.arena_items += n - len(copy)
+        self.copied_items += len(copy)
         hdr = ring.header(s)
         hdr[:] = 0
         mask = 0
@@ -401,8 +434,8 @@ class DataParallelDetector2D(_RingDP):
     any engine with ``detect(frames)`` (host path, e.g. CPU)."""
 
     def __init__(self, local, info: DistInfo, max_det: int = 300, monitor: Optional[HealthMonitor] = None,
-                 nslots: int = 4, comm=None):
-        super().__init__(local, info, monitor, nslots, comm)
+                 nslots: int = 4, comm=None, arena_mb: Optional[int] = None):
+        super().__init__(local, info, monitor, nslots, comm, arena_mb=arena_mb)
         self.max_det = max_det
         self.B = int(getattr(local, "B", 0) or 0)
 
@@ -495,7 +528,7 @@ class DataParallelDetector2D(_RingDP):
         kind, H, W = int(hdr[H_KIND]), int(hdr[H_KEY]), int(hdr[H_KEY + 1])
         out = []
         for i in range(lo, hi):
-            raw = view[int(items[i, I_IN]):int(items[i, I_IN]) + int(items[i, I_INSZ])]
+            raw = self._raw(items, i, view)
             if kind == KIND_JPEG:
                 out.append(msgs.CompressedImage(format="jpeg", data=memoryview(raw)))
             else:
@@ -616,8 +649,9 @@ class DataParallelDetector3D(_RingDP):
     FIELDS = ("x", "y", "z", "intensity")
 
     def __init__(self, local, info: DistInfo, max_out: int = 500, box_dim: int = 7,
-                 monitor: Optional[HealthMonitor] = None, nslots: int = 4, comm=None):
-        super().__init__(local, info, monitor, nslots, comm)
+                 monitor: Optional[HealthMonitor] = None, nslots: int = 4, comm=None,
+                 arena_mb: Optional[int] = None):
+        super().__init__(local, info, monitor, nslots, comm, arena_mb=arena_mb)
         self.max_out, self.box_dim = max_out, box_dim
         self.B = int(getattr(local, "B", 0) or 0)
 
@@ -672,7 +706,7 @@ class DataParallelDetector3D(_RingDP):
         fields = [msgs.PointField(k, o, d, 1) for k, o, d in zip(self.FIELDS, offs, dts)]
         out = []
         for i in range(lo, hi):
-            raw = view[int(items[i, I_IN]):int(items[i, I_IN]) + int(items[i, I_INSZ])]
+            raw = self._raw(items, i, view)
             k = int(items[i, I_M0])
             out.append(msgs.PointCloud2(height=1, width=k, fields=fields, point_step=step, row_step=k * step,
                                         data=memoryview(raw), is_dense=False))

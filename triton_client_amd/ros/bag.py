@@ -22,8 +22,9 @@ import struct
 from typing import Iterator, Optional, Sequence, Tuple
 
 import msgpack
+import numpy as np
 
-from . import msgs, rosbag_v2
+from . import msgs, rosbag_v2, rosmsg
 
 MAGIC = b"TCABAG1\n"
 
@@ -54,9 +55,11 @@ class RosBag:
     def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
         self._w.write(topic, msg, t)
 
-    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0):
+    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0, alloc=None):
+        """``alloc(n)``: where large payloads are deserialised to (e.g. the DP ring's
+        ``ingest_buffer``); None keeps ``bytes``."""
         k = 0
-        for topic, m, t in rosbag_v2.read_messages(self._r, topics):
+        for topic, m, t in rosbag_v2.read_messages(self._r, topics, alloc):
             k += 1
             if k <= start_seq:
                 continue
@@ -111,7 +114,8 @@ class TcaBag:
             (n,) = struct.unpack("<Q", hdr)
             yield msgpack.unpackb(self._f.read(n), raw=False)
 
-    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0) -> Iterator[Tuple[str, object, msgs.Time]]:
+    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0,
+                      alloc=None) -> Iterator[Tuple[str, object, msgs.Time]]:
         """Yields (topic, msg, t).  ``start_seq`` resumes a replay after the
         first ``start_seq`` matching messages."""
         k = 0
@@ -123,6 +127,12 @@ class TcaBag:
                 continue
             cls = msgs.MSG_TYPES.get(r["type"])
             m = msgs.from_dict(cls, r["msg"]) if cls else r["msg"]
+            raw = getattr(m, "data", None)
+            if alloc is not None and isinstance(raw, (bytes, bytearray)) and len(raw) >= rosmsg.ALLOC_MIN:
+                buf = alloc(len(raw))
+                if buf is not None:
+                    buf[:] = np.frombuffer(raw, np.uint8)
+                    m.data = memoryview(buf)
             t = msgs.Time(r["t"] // 1_000_000_000, r["t"] % 1_000_000_000)
             yield r["topic"], m, t
 

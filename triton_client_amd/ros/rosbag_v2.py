@@ -249,9 +249,9 @@ class RosBagReader:
             # bag header, index data, chunk info: nothing to replay
 
     @staticmethod
-    def decode(conn: Connection, data: bytes):
+    def decode(conn: Connection, data: bytes, alloc=None):
         if conn.type in rosmsg.DEFS:
-            return rosmsg.deserialize(data, conn.type)
+            return rosmsg.deserialize(data, conn.type, alloc)
         return RawMessage(conn.type, conn.md5sum, data)
 
     def close(self) -> None:
@@ -263,8 +263,9 @@ def is_rosbag(path: str) -> bool:
         return f.read(len(MAGIC)) == MAGIC
 
 
-def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None):
+def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None):
+    """``alloc``: see :func:`rosmsg.deserialize` (large payloads written into caller buffers)."""
     for c, t, data in reader.raw_messages():
         if topics and c.topic not in topics:
             continue
-        yield c.topic, reader.decode(c, data), t
+        yield c.topic, reader.decode(c, data, alloc), t

@@ -19,8 +19,9 @@ from __future__ import annotations
 
 import hashlib
 import struct
+import threading
 from dataclasses import is_dataclass
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from . import msgs
 
@@ -265,6 +266,12 @@ def _read(mv: memoryview, off: int, f: Field):
     else:
         n = f.size
     if f.base in ("uint8", "char"):
+        alloc = getattr(_TLS, "alloc", None)
+        if alloc is not None and n >= ALLOC_MIN:
+            buf = alloc(n)  # e.g. the DP host ring's ingest arena: the payload lands where every rank reads it
+            if buf is not None:
+                buf[:] = mv[off: off + n]
+                return memoryview(buf), off + n
         return bytes(mv[off: off + n]), off + n
     if f.base in BUILTIN:
         fmt = "<%d%s" % (n, BUILTIN[f.base])
@@ -288,9 +295,19 @@ def _build(msg_type: str, d: dict):
     return cls(**{k: v for k, v in d.items() if k in names})
 
 
-def deserialize(data: bytes, msg_type: str):
+_TLS = threading.local()
+ALLOC_MIN = 64 << 10  # byte arrays from this size go to ``alloc`` (image rows, JPEG bytes, PointCloud2 data)
+
+
+def deserialize(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]] = None):
+    """``alloc(n)``: optional destination for large uint8 arrays (a writable buffer of n
+    bytes, or None to keep ``bytes``); the message's field then views that buffer."""
     mv = memoryview(data)
-    msg, off = _read_msg(mv, 0, msg_type)
+    _TLS.alloc = alloc
+    try:
+        msg, off = _read_msg(mv, 0, msg_type)
+    finally:
+        _TLS.alloc = None
     if off != len(data):
         raise ValueError(f"{msg_type}: {len(data) - off} trailing bytes")
     return msg
