@@ -229,6 +229,138 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
   }
 }
 
+// The same PillarVFE + scatter, with the Linear(10->64) folded by linearity so it runs on the
+// VALU in plain fp32 (more accurate than the split-bf16 MFMA above, and ~5x fewer VALU ops
+// per pillar: no operand splits, no accumulator scan).  The ten features are
+// [p, p - mean, p_xyz - centre], so with W = [W1 | W2 | W3]:
+//   W f(p) = A p + d,   A = W1 + [W2 | 0] + [W3 | 0]   (64 x 4, per channel),
+//                       d = -(W2 mean + W3 centre)     (per pillar and channel).
+// max over the real points of (A p) + d, then the padded slots' zero row when n < P, then
+// relu(+ bias) -- exactly OpenPCDet's masked features (padded rows give relu(bias)).
+// One wave per pillar; lane c owns channel c; the pillar's points are staged in LDS
+// (one float4 per slot, broadcast reads) and the per-point loop runs over the n real points
+// only (n is wave-uniform): 3 FMA + 1 MUL + 1 MAX + 3 ADD (the xyz sums for the mean).
+template <bool FROM_SLOTS, typename CT, int PFIX = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) pillar_vfe_lin_kernel(
+    const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ slots,
+    const int* __restrict__ vcount, const float* __restrict__ voxels, const int* __restrict__ num_points,
+    const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P_arg,
+    const float* __restrict__ W /*[64][10]*/, const float* __restrict__ bias /*[64]*/, PillarGeom g,
+    CT* __restrict__ canvas, float* __restrict__ feat_out, uint8_t* __restrict__ occ) {
+  const int P = PFIX ? PFIX : P_arg;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  __shared__ float4 spts[4][32];
+
+  const float* w = W + lane * 10;
+  const float a0 = w[0] + w[4] + w[7], a1 = w[1] + w[5] + w[8], a2 = w[2] + w[6] + w[9], a3 = w[3];
+  const float u0 = w[4], u1 = w[5], u2 = w[6], t0 = w[7], t1 = w[8], t2 = w[9];
+  const float bc = bias[lane];
+
+  const int nv = batch * max_voxels;
+  const int step = __builtin_amdgcn_readfirstlane((int)nwaves);
+  auto next_valid = [&](int vv) {
+    while (vv < nv) {
+      const int bb = (unsigned)vv / (unsigned)max_voxels;
+      if (vv - bb * max_voxels < voxel_count[bb]) break;
+      vv += step;
+    }
+    return vv;
+  };
+  const bool vec4 = (pstride & 3) == 0;
+  const int rs = min(r, P - 1);
+  auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[(long)min(vv, nv - 1) * P + rs] : 0; };
+  auto gather = [&](int vv, int id, float (&q)[4]) {
+    const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
+    const bool real_ = r < min(vc_, P);
+    const int bb = (unsigned)min(vv, nv - 1) / (unsigned)max_voxels;
+    const float* src = FROM_SLOTS ? pts + ((long)bb * max_pts + (real_ ? id : 0)) * pstride
+                                  : voxels + ((long)min(vv, nv - 1) * P + rs) * 4;
+    if (!FROM_SLOTS || vec4) {
+      const float4 t = *reinterpret_cast<const float4*>(src);
+      q[0] = t.x; q[1] = t.y; q[2] = t.z; q[3] = t.w;
+    } else {
+      q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
+    }
+  };
+  auto meta = [&](int vv, int& vc_, int4& co_) {
+    const int vq = min(vv, nv - 1);
+    vc_ = FROM_SLOTS ? vcount[vq] : num_points[vq];
+    co_ = *reinterpret_cast<const int4*>(coords + (long)vq * 4);
+  };
+  // the same three-deep load pipeline as the MFMA kernel
+  int v = next_valid(__builtin_amdgcn_readfirstlane((int)wave));
+  int vn = v < nv ? next_valid(v + step) : nv;
+  int vnn = vn < nv ? next_valid(vn + step) : nv;
+  float pc[4], pn[4];
+  gather(v, slot_of(v), pc);
+  gather(vn, slot_of(vn), pn);
+  int idx_nn = slot_of(vnn);
+  int vc;
+  int4 co;
+  meta(v, vc, co);
+  while (v < nv) {
+    const int b = (unsigned)v / (unsigned)max_voxels;
+    const int n = __builtin_amdgcn_readfirstlane(min(vc, P));
+    const int v3 = vnn < nv ? next_valid(vnn + step) : nv;
+    const int idx_3 = slot_of(v3);
+    float pnn[4];
+    gather(vnn, idx_nn, pnn);
+    int vc_n;
+    int4 co_n;
+    meta(vn, vc_n, co_n);
+    if (h == 0) spts[wid][r] = make_float4(pc[0], pc[1], pc[2], pc[3]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float acc = -INFINITY, sx = 0.f, sy = 0.f, sz = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < n; ++j) {
+      const float4 q = spts[wid][j];
+      acc = fmaxf(acc, fmaf(a0, q.x, fmaf(a1, q.y, fmaf(a2, q.z, a3 * q.w))));
+      sx += q.x;
+      sy += q.y;
+      sz += q.z;
+    }
+    __builtin_amdgcn_wave_barrier();  // this pillar's reads before the next pillar's LDS writes
+    const float inv_n = 1.f / (float)max(n, 1);
+    const float xc = (float)co.w * g.vx + (g.vx * 0.5f + g.r0);
+    const float yc = (float)co.z * g.vy + (g.vy * 0.5f + g.r1);
+    const float zc = (float)co.y * g.vz + (g.vz * 0.5f + g.r2);
+    const float d = -(u0 * (sx * inv_n) + u1 * (sy * inv_n) + u2 * (sz * inv_n) + t0 * xc + t1 * yc + t2 * zc);
+    float mval = acc + d;
+    if (n < P) mval = fmaxf(mval, 0.f);  // a padded slot's all-zero feature row
+    const float val = fmaxf(mval + bc, 0.f);
+    const int ch = lane;
+    if (canvas) {
+      const long cell = ((long)b * g.ny + co.z) * g.nx + co.w;
+      if constexpr (std::is_same<CT, PairTag>::value) {
+        __bf16* c2 = reinterpret_cast<__bf16*>(canvas) + cell * 128 + (ch >> 3) * 16 + (ch & 7);
+        const __bf16 hv = (__bf16)val;
+        c2[0] = hv;
+        c2[8] = (__bf16)(val - (float)hv);
+      } else {
+        canvas[cell * 64 + ch] = from_f32<CT>(val);
+      }
+    }
+    if (feat_out) feat_out[(long)v * 64 + ch] = val;
+    if (occ && lane == 0) occ[((long)b * g.ny + co.z) * g.nx + co.w] = 1;
+    v = vn;
+    vn = vnn;
+    vnn = v3;
+    idx_nn = idx_3;
+    vc = vc_n;
+    co = co_n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pc[k] = pn[k];
+      pn[k] = pnn[k];
+    }
+  }
+}
+
 // Zero exactly the cells the previous frame scattered: one thread per 16-B
 // chunk of a pillar's C channels (C * esize % 16 == 0), frame per grid row.
 __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict__ coords,
@@ -268,27 +400,47 @@ int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, con
                                      batch, max_voxels, P, W, bias, g, canvas, feat_out, dt, occ, stream);
 }
 
+// 0: the fp32 VALU kernel (default), 1: the split-bf16 MFMA kernel (TCA_VFE_MFMA=1 or
+// tca_pillar_vfe_set_variant; kept for A/B and its tests)
+int g_vfe_variant = -1;
+
+int vfe_variant() {
+  if (g_vfe_variant < 0) {
+    const char* e = getenv("TCA_VFE_MFMA");
+    g_vfe_variant = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_vfe_variant;
+}
+
 template <bool FROM_SLOTS, int PFIX>
 int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, const int* vcount, const float* voxels,
                  const int* num_points, const int* coords, const int* voxel_count, int batch, int max_voxels, int P,
                  const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
                  uint8_t* occ, hipStream_t stream) {
-  if (dt == kF32)
-    pillar_vfe_kernel<FROM_SLOTS, float, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
-                                                                   num_points, coords, voxel_count, batch, max_voxels,
-                                                                   P, W, bias, g, (float*)canvas, feat_out, occ);
-  else if (dt == kPair)
-    pillar_vfe_kernel<FROM_SLOTS, PairTag, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels,
-                                                                     num_points, coords, voxel_count, batch,
-                                                                     max_voxels, P, W, bias, g, (PairTag*)canvas,
-                                                                     feat_out, occ);
-  else
-    pillar_vfe_kernel<FROM_SLOTS, __hip_bfloat16, PFIX><<<2048, 256, 0, stream>>>(
-        pts, pstride, max_pts, slots, vcount, voxels, num_points, coords, voxel_count, batch, max_voxels, P, W, bias,
-        g, (__hip_bfloat16*)canvas, feat_out, occ);
+#define TCA_VFE_LAUNCH(KERNEL, CT)                                                                                 \
+  KERNEL<FROM_SLOTS, CT, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels, num_points, \
+                                                        coords, voxel_count, batch, max_voxels, P, W, bias, g,      \
+                                                        (CT*)canvas, feat_out, occ)
+  const bool mfma = vfe_variant() == 1;
+  if (dt == kF32) {
+    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, float); else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, float);
+  } else if (dt == kPair) {
+    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, PairTag); else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, PairTag);
+  } else {
+    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, __hip_bfloat16);
+    else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, __hip_bfloat16);
+  }
+#undef TCA_VFE_LAUNCH
   TCA_LAUNCH_CHECK();
 }
 }  // namespace
+
+// VFE kernel selection: 0 = fp32 VALU (default), 1 = split-bf16 MFMA; returns the previous one.
+TCA_API int tca_pillar_vfe_set_variant(int v) {
+  const int old = vfe_variant();
+  g_vfe_variant = v ? 1 : 0;
+  return old;
+}
 
 // Fused path: source = voxeliser slots + unpacked points.  canvas_dtype: kBF16,
 // kF32 or kPair (fp32 mode's pair storage, see tca_common.h).
