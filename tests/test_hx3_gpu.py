@@ -218,3 +218,58 @@ def test_hx3s2_fp32_storage_out(cuda, tile):
     assert rel_l2(op.nchw(), of.t.permute(0, 3, 1, 2)) < 2e-5
     ref = torch.relu(conv(from_pairs(x.t).double().cpu().permute(0, 3, 1, 2)))
     assert rel_l2(of.t.permute(0, 3, 1, 2), ref) < 5e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin", [32, 64])
+@pytest.mark.parametrize("pattern", ["random", "arcs", "empty"])
+def test_s2sp_sparse_gather_conv(cuda, cin, pattern):
+    """conv_s2sp.hip (tile 140, the default over an occupancy-marked canvas): garbage in the
+    unmarked cells; channel-offset input / output slices; partial 8 x 32 tiles; against fp64 on
+    the masked input; close to the dense hx3s2 kernel (same split products, another order) and
+    bit-identical to it on pixels whose window is empty; bit-reproducible run to run; fp32
+    storage out (act | 32) decodes to the pair output."""
+    torch.manual_seed(13 + cin)
+    B, H, W, cout = 2, 70, 90, 64
+    conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True).double()
+    fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
+    assert fc.s2sp_ok()
+    if pattern == "random":
+        occ = (torch.rand(B, H, W) < 0.05).to(torch.uint8)
+    elif pattern == "arcs":
+        yy, xx = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+        r = ((yy - 5.0) ** 2 + (xx + 3.0) ** 2).sqrt()
+        occ = ((r % 17.0) < 1.5).to(torch.uint8).expand(B, H, W).contiguous()
+        occ[1, :, 50:] = 0
+    else:
+        occ = torch.zeros(B, H, W, dtype=torch.uint8)
+    xin = torch.randn(B, H, W, cin, dtype=torch.float64) * occ[..., None].double()
+    stored = torch.where(occ.bool()[..., None], xin, torch.full_like(xin, 1e6))
+    buf = torch.zeros(B, H, W, cin + 16)
+    buf[..., 8:8 + cin] = stored.float()
+    x = NHWC(to_pairs(buf).to(cuda), 8, cin, pair=True, occ=occ.to(cuda))
+    Ho, Wo = fc.out_hw(H, W)
+    outs = []
+    for t in (140, 140, 0):
+        o = torch.full((B, Ho, Wo, cout + 16), 7.0, dtype=torch.float32, device=cuda)
+        fc(x, out=NHWC(o, 8, cout, pair=True), tile=t)
+        outs.append(o)
+    dense = torch.full((B, Ho, Wo, cout + 16), 7.0, dtype=torch.float32, device=cuda)
+    fc(x, out=NHWC(dense, 8, cout, pair=True), tile=120)
+    of = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=False)
+    fc(x, out=of, tile=140)
+    torch.cuda.synchronize()
+    o = outs[0]
+    assert (o[..., :8] == 7.0).all() and (o[..., 8 + cout:] == 7.0).all()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))  # reproducible
+    assert torch.equal(outs[0].view(torch.int32), outs[2].view(torch.int32))  # the default route
+    ref = torch.relu(conv(xin.permute(0, 3, 1, 2)))
+    got = NHWC(o, 8, cout, pair=True).nchw()
+    assert rel_l2(got, ref) < 5e-5, rel_l2(got, ref)
+    dn = NHWC(dense, 8, cout, pair=True).nchw()
+    assert rel_l2(got, dn) < 2e-6, rel_l2(got, dn)
+    # pixels whose 3 x 3 stride-2 window holds no occupied cell: act(bias), bit for bit
+    win = torch.nn.functional.max_pool2d(occ.float()[:, None], 3, 2, 1)[:, 0] > 0
+    empty = (~win).to(cuda)
+    assert torch.equal(o[..., 8:8 + cout][empty].view(torch.int32), dense[..., 8:8 + cout][empty].view(torch.int32))
+    assert rel_l2(got, of.t.permute(0, 3, 1, 2)) < 2e-5

@@ -113,6 +113,11 @@ HX3S2_TILES = (120, 121, 122, 123, 124)
 # conv_wino.hip (3x3 stride-1 by 1-D Winograd F(2,3), 1.5x fewer MFMAs than hx3): the default for
 # every eligible stride-1 layer (WINO False: hx3).  Tiles 130 (auto) and 131-134 select it explicitly.
 WINO = os.environ.get("TCA_WINO", "1") != "0"  # TCA_WINO=0: hx3 for A/B runs
+# conv_s2sp.hip (the sparse-gather stride-2 conv: only (pixel, tap) pairs whose input cell is
+# occupied): the default for a stride-2 pair conv over an occupancy-marked canvas with N == 64 and
+# Cin 32 / 64 (the first PointPillars BEV conv); S2SP False / TCA_S2SP=0: the dense hx3s2 kernel.
+# Tile 140 selects it explicitly.
+S2SP = os.environ.get("TCA_S2SP", "1") != "0"
 WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
 WINO_TILES = (130, 131, 132, 133, 134)
 
@@ -281,6 +286,14 @@ class FusedConv:
             # pair storage: the global_load_lds split-product kernels (Cin % 32, K == Kp)
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
+            if (res is None and x.occ is not None and self.s2sp_ok() and
+                    (tile == 140 or (tile == 0 and S2SP))):
+                assert x.occ.dtype == torch.uint8 and tuple(x.occ.shape) == (B, H, W), (x.occ.shape, (B, H, W))
+                _native.call("tca_conv_s2sp", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
+                             _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
+                             _native.ptr(out.t), out.t.shape[-1], out.off, self.act | (0 if out.pair else 32),
+                             _native.ptr(x.occ), _native.stream_ptr(stream))
+                return out
             if ((out.pair or res is None) and self.hx3_ok() and self.s == 2 and
                     (tile in HX3S2_TILES or (tile == 0 and HX3S2))):
                 occ = x.occ
@@ -368,6 +381,13 @@ class FusedConv:
         if self._w_frag is None:
             self._w_frag = frag_weights(self.w_f32_gemm).to(self.device)
         return self._w_frag
+
+    def s2sp_ok(self) -> bool:
+        """The sparse-gather stride-2 kernel takes this conv (conv_s2sp.hip: 3x3 stride 2 pad 1,
+        N == 64, Cin 32 / 64, pair weights)."""
+        return (self.precision == "fp32" and not self.transpose and self.k == 3 and self.s == 2 and self.p == 1
+                and self.N == 64 and self.cin_p in (32, 64) and self.K == self.Kp
+                and self.act in (ACT_NONE, ACT_RELU, ACT_SILU, ACT_LEAKY))
 
     def pair_ok(self) -> bool:
         """The pair-storage kernels take this conv (Cin % 32, K == Kp)."""
