@@ -64,6 +64,8 @@ def _fields(d: Dict[str, bytes]) -> bytes:
 
 
 def _parse_fields(b: bytes) -> Dict[str, bytes]:
+    if not isinstance(b, bytes):
+        b = bytes(b)
     d, off = {}, 0
     while off < len(b):
         (n,) = struct.unpack_from("<I", b, off)
@@ -182,13 +184,22 @@ class RosBagReader:
             raise ValueError(f"{path}: not a ROS bag v2.0")
         self.conns: Dict[int, Connection] = {}
 
-    def _read_record(self, f) -> Optional[Tuple[Dict[str, bytes], bytes]]:
+    def _read_record(self, f, alloc=None) -> Optional[Tuple[Dict[str, bytes], bytes]]:
+        """``alloc``: an uncompressed chunk is read straight into ``alloc(n)`` (the DP ring's
+        ingest arena) and its messages are views of it -- no copy between the file and the ring."""
         b = f.read(4)
         if len(b) < 4:
             return None
         (hl,) = struct.unpack("<I", b)
         h = _parse_fields(f.read(hl))
         (dl,) = struct.unpack("<I", f.read(4))
+        if (alloc is not None and dl >= rosmsg.ALLOC_MIN and h.get("op", b"\0")[0] == OP_CHUNK
+                and h.get("compression", b"none") == b"none"):
+            buf = alloc(dl)
+            if buf is not None:
+                if f.readinto(memoryview(buf)) != dl:
+                    raise ValueError("truncated ROS bag chunk")
+                return h, memoryview(buf)
         return h, f.read(dl)
 
     def _conn(self, h, data) -> Connection:
@@ -219,7 +230,7 @@ class RosBagReader:
         n = len(blob)
         while off + 8 <= n:
             (hl,) = struct.unpack_from("<I", blob, off)
-            h = _parse_fields(blob[off + 4: off + 4 + hl])
+            h = _parse_fields(bytes(blob[off + 4: off + 4 + hl]))
             (dl,) = struct.unpack_from("<I", blob, off + 4 + hl)
             data = blob[off + 8 + hl: off + 8 + hl + dl]
             off += 8 + hl + dl
@@ -230,11 +241,12 @@ class RosBagReader:
                 cid = struct.unpack("<I", h["conn"])[0]
                 yield self.conns[cid], _read_time(h["time"]), data
 
-    def raw_messages(self) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
-        """(connection, time, serialised bytes) in file order."""
+    def raw_messages(self, alloc=None) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
+        """(connection, time, serialised bytes) in file order (memoryviews into ``alloc``
+        buffers for uncompressed chunks when ``alloc`` is given)."""
         self.f.seek(len(MAGIC))
         while True:
-            rec = self._read_record(self.f)
+            rec = self._read_record(self.f, alloc)
             if rec is None:
                 return
             h, data = rec
@@ -251,6 +263,8 @@ class RosBagReader:
     @staticmethod
     def decode(conn: Connection, data: bytes, alloc=None):
         if conn.type in rosmsg.DEFS:
+            if isinstance(data, memoryview):  # a view of an arena chunk: payloads stay views of it
+                return rosmsg.deserialize(data, conn.type, zero_copy=True)
             return rosmsg.deserialize(data, conn.type, alloc)
         return RawMessage(conn.type, conn.md5sum, data)
 
@@ -265,7 +279,7 @@ def is_rosbag(path: str) -> bool:
 
 def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None):
     """``alloc``: see :func:`rosmsg.deserialize` (large payloads written into caller buffers)."""
-    for c, t, data in reader.raw_messages():
+    for c, t, data in reader.raw_messages(alloc):
         if topics and c.topic not in topics:
             continue
         yield c.topic, reader.decode(c, data, alloc), t

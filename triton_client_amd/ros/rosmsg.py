@@ -267,6 +267,8 @@ def _read(mv: memoryview, off: int, f: Field):
         n = f.size
     if f.base in ("uint8", "char"):
         alloc = getattr(_TLS, "alloc", None)
+        if alloc is _ZERO_COPY and n >= ALLOC_MIN:
+            return mv[off: off + n], off + n
         if alloc is not None and n >= ALLOC_MIN:
             buf = alloc(n)  # e.g. the DP host ring's ingest arena: the payload lands where every rank reads it
             if buf is not None:
@@ -299,11 +301,16 @@ _TLS = threading.local()
 ALLOC_MIN = 64 << 10  # byte arrays from this size go to ``alloc`` (image rows, JPEG bytes, PointCloud2 data)
 
 
-def deserialize(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]] = None):
+_ZERO_COPY = object()
+
+
+def deserialize(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]] = None, zero_copy: bool = False):
     """``alloc(n)``: optional destination for large uint8 arrays (a writable buffer of n
-    bytes, or None to keep ``bytes``); the message's field then views that buffer."""
+    bytes, or None to keep ``bytes``); the message's field then views that buffer.
+    ``zero_copy``: large uint8 arrays are views of ``data`` itself (which the message
+    then keeps alive)."""
     mv = memoryview(data)
-    _TLS.alloc = alloc
+    _TLS.alloc = _ZERO_COPY if zero_copy else alloc
     try:
         msg, off = _read_msg(mv, 0, msg_type)
     finally:
