@@ -38,7 +38,7 @@ struct S2spArgs {
   int tiles_x, tiles;        // output tiles per row / per image
 };
 
-constexpr int TH = 8, TW = 32, NPIX = TH * TW, N = 64, LDA = N + 4;
+constexpr int TW = 32, N = 64, LDA = N + 4;
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   switch (act) {
@@ -49,9 +49,12 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   }
 }
 
-template <int KC>
+// TH = 8: 256 pixels, one per thread (78 KiB LDS, two workgroups per CU); TH = 4: 128 pixels,
+// threads 0-127 test taps 0-4 and 128-255 taps 5-8 (40 KiB LDS, four workgroups per CU)
+template <int KC, int TH>
 __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
-  __shared__ float acc_s[NPIX * LDA];   // 69.6 KiB: the tile's fp32 accumulators, pixel-major
+  constexpr int NPIX = TH * TW;
+  __shared__ float acc_s[NPIX * LDA];   // the tile's fp32 accumulators, pixel-major
   __shared__ int list_s[9][NPIX];       // per tap: (input cell << 8) | pixel
   __shared__ int cnt_s[9][4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -63,14 +66,16 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
   for (int i = tid; i < NPIX * LDA / 4; i += 256) reinterpret_cast<float4*>(acc_s)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // 1. per-tap lists of occupied (input cell, pixel) entries
-  const int p = tid, oy = oy0 + p / TW, ox = ox0 + p % TW;
+  const int p = tid % NPIX, oy = oy0 + p / TW, ox = ox0 + p % TW;
   const bool in_out = oy < a.Ho && ox < a.Wo;
+  const int tg = tid / NPIX;  // tap group: all taps (TH = 8) or taps 0-4 / 5-8 (TH = 4)
+  auto mine = [&](int t) { return NPIX == 256 || (tg == 0 ? t < 5 : t >= 5); };
   const unsigned char* occ_b = a.occ + (long)b * a.H * a.W;
   unsigned okm = 0;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int iy = 2 * oy - 1 + t / 3, ix = 2 * ox - 1 + t % 3;
-    const bool ok = in_out && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && occ_b[iy * a.W + ix] != 0;
+    const bool ok = mine(t) && in_out && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && occ_b[iy * a.W + ix] != 0;
     okm |= (unsigned)ok << t;
     const unsigned long long m = __ballot(ok);
     if (lane == 0) cnt_s[t][wid] = __popcll(m);
@@ -169,10 +174,10 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
 
 // fp32 mode, pair activations in, 3x3 stride 2 pad 1, N == 64, Cin 32 or 64, no residual:
 // the same arguments and weights as tca_conv_hx3s2p (conv_hx3.hip), occ required.
-// act | 32: fp32 storage out.
+// act | 32: fp32 storage out.  tile: 0 auto (8 x 32 output tiles), 1 (4 x 32).
 TCA_API int tca_conv_s2sp(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
                           const float* bias, int n, float* out, int ldo, int co_off, int act,
-                          const unsigned char* occ, hipStream_t stream) {
+                          const unsigned char* occ, int tile, hipStream_t stream) {
   if (B <= 0) return 0;
   if (!occ || n != N || (Cin != 32 && Cin != 64) || (ldi & 7) || (ci_off & 7) || (ldo & 7) || (co_off & 7))
     return (int)hipErrorInvalidValue;
@@ -181,12 +186,16 @@ TCA_API int tca_conv_s2sp(const float* in, int B, int H, int W, int Cin, int ldi
   a.in = in; a.occ = occ; a.w = reinterpret_cast<const uint4*>(wfrag); a.bias = bias; a.out = out;
   a.B = B; a.H = H; a.W = W; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
   a.ldo = ldo; a.co_off = co_off; a.act = act;
+  const int TH = tile == 1 ? 4 : 8;  // 0 = auto (8 x 32), 1 = 4 x 32
   a.tiles_x = (a.Wo + TW - 1) / TW;
   a.tiles = a.tiles_x * ((a.Ho + TH - 1) / TH);
   const dim3 grid(a.tiles, B);
-  if (Cin == 64)
-    conv_s2sp_kernel<2><<<grid, 256, 0, stream>>>(a);
-  else
-    conv_s2sp_kernel<1><<<grid, 256, 0, stream>>>(a);
+  if (TH == 4) {
+    if (Cin == 64) conv_s2sp_kernel<2, 4><<<grid, 256, 0, stream>>>(a);
+    else conv_s2sp_kernel<1, 4><<<grid, 256, 0, stream>>>(a);
+  } else {
+    if (Cin == 64) conv_s2sp_kernel<2, 8><<<grid, 256, 0, stream>>>(a);
+    else conv_s2sp_kernel<1, 8><<<grid, 256, 0, stream>>>(a);
+  }
   TCA_LAUNCH_CHECK();
 }

@@ -221,9 +221,10 @@ def test_hx3s2_fp32_storage_out(cuda, tile):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tile", [140, 141])
 @pytest.mark.parametrize("cin", [32, 64])
 @pytest.mark.parametrize("pattern", ["random", "arcs", "empty"])
-def test_s2sp_sparse_gather_conv(cuda, cin, pattern):
+def test_s2sp_sparse_gather_conv(cuda, tile, cin, pattern):
     """conv_s2sp.hip (tile 140, the default over an occupancy-marked canvas): garbage in the
     unmarked cells; channel-offset input / output slices; partial 8 x 32 tiles; against fp64 on
     the masked input; close to the dense hx3s2 kernel (same split products, another order) and
@@ -250,14 +251,14 @@ def test_s2sp_sparse_gather_conv(cuda, cin, pattern):
     x = NHWC(to_pairs(buf).to(cuda), 8, cin, pair=True, occ=occ.to(cuda))
     Ho, Wo = fc.out_hw(H, W)
     outs = []
-    for t in (140, 140, 0):
+    for t in (tile, tile, 0 if tile == 140 else tile):
         o = torch.full((B, Ho, Wo, cout + 16), 7.0, dtype=torch.float32, device=cuda)
         fc(x, out=NHWC(o, 8, cout, pair=True), tile=t)
         outs.append(o)
     dense = torch.full((B, Ho, Wo, cout + 16), 7.0, dtype=torch.float32, device=cuda)
     fc(x, out=NHWC(dense, 8, cout, pair=True), tile=120)
     of = NHWC(torch.empty(B, Ho, Wo, cout, device=cuda), pair=False)
-    fc(x, out=of, tile=140)
+    fc(x, out=of, tile=tile)
     torch.cuda.synchronize()
     o = outs[0]
     assert (o[..., :8] == 7.0).all() and (o[..., 8 + cout:] == 7.0).all()

@@ -18,3 +18,4 @@ done
 unset TCA_S2SP
 VAR=TCA_S2SP A= B=0 RUNS=${RUNS:-2} TAG=s2sp_h bash tools/gpu_env_ab.sh || exit 1
 VAR=TCA_S2SP A= B=0 RUNS=1 TAG=s2sp_l EXTRA="--only lidar" bash tools/gpu_env_ab.sh || exit 1
+VAR=TCA_S2SP_TILE A= B=1 RUNS=2 TAG=s2sp_tile_l EXTRA="--only lidar" bash tools/gpu_env_ab.sh || exit 1

@@ -59,7 +59,7 @@ _KERNEL_SIGS = {
     "tca_voxelize": [P, I, I, P, I, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, I, P, I, P],
     "tca_pillar_vfe_slots": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_vfe_set_variant": [I],
-    "tca_conv_s2sp": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, P],  # returns the previous variant (not an error code)
+    "tca_conv_s2sp": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, P],  # returns the previous variant (not an error code)
     "tca_pillar_vfe_voxels": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P],
     "tca_pillar_canvas_clear": [P, P, I, I, I, I, I, P, I, P],
     "tca_pillar_vfe_slots_occ": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P, P],

@@ -116,8 +116,10 @@ WINO = os.environ.get("TCA_WINO", "1") != "0"  # TCA_WINO=0: hx3 for A/B runs
 # conv_s2sp.hip (the sparse-gather stride-2 conv: only (pixel, tap) pairs whose input cell is
 # occupied): the default for a stride-2 pair conv over an occupancy-marked canvas with N == 64 and
 # Cin 32 / 64 (the first PointPillars BEV conv); S2SP False / TCA_S2SP=0: the dense hx3s2 kernel.
-# Tile 140 selects it explicitly.
+# Tiles 140 (auto: 8 x 32 output tiles) and 141 (4 x 32) select it explicitly.
 S2SP = os.environ.get("TCA_S2SP", "1") != "0"
+S2SP_TILES = (140, 141)
+S2SP_TILE = int(os.environ.get("TCA_S2SP_TILE", "0"))
 WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
 WINO_TILES = (130, 131, 132, 133, 134)
 
@@ -287,12 +289,13 @@ class FusedConv:
             if self.precision != "fp32" or not x.pair or (res is not None and res.pair != out.pair):
                 raise TypeError("pair activations: fp32 convs reading pairs (output pairs or fp32)")
             if (res is None and x.occ is not None and self.s2sp_ok() and
-                    (tile == 140 or (tile == 0 and S2SP))):
+                    (tile in S2SP_TILES or (tile == 0 and S2SP))):
                 assert x.occ.dtype == torch.uint8 and tuple(x.occ.shape) == (B, H, W), (x.occ.shape, (B, H, W))
                 _native.call("tca_conv_s2sp", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, self.act | (0 if out.pair else 32),
-                             _native.ptr(x.occ), _native.stream_ptr(stream))
+                             _native.ptr(x.occ), tile - 140 if tile in S2SP_TILES else S2SP_TILE,
+                             _native.stream_ptr(stream))
                 return out
             if ((out.pair or res is None) and self.hx3_ok() and self.s == 2 and
                     (tile in HX3S2_TILES or (tile == 0 and HX3S2))):
