@@ -7,8 +7,8 @@
 // The dense kernel (conv_hx3.hip hx3s2) runs all 9 taps x Cin of every output pixel and masks
 // the loads of empty cells; here only the (output pixel, tap) pairs whose input cell is occupied
 // are computed:
-//   1. per 8 x 32 output tile, every thread (one output pixel) tests its 9 input cells'
-//      occupancy bytes; per tap, a ballot + cross-wave prefix builds the list of
+//   1. per TH x 32 output tile, the threads test the 9 input cells' occupancy bytes of every
+//      output pixel; per tap, a ballot + cross-wave prefix builds the list of
 //      (input cell, pixel) entries in LDS (deterministic order);
 //   2. wave w owns output channels [16 w, 16 w + 16): for tap 0..8 in order it takes the tap's
 //      list 16 entries at a time -- the activation fragment of entry fr is the input cell's
@@ -49,8 +49,8 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   }
 }
 
-// TH = 8: 256 pixels, one per thread (78 KiB LDS, two workgroups per CU); TH = 4: 128 pixels,
-// threads 0-127 test taps 0-4 and 128-255 taps 5-8 (40 KiB LDS, four workgroups per CU)
+// TH = 8: 256 pixels, one per thread (78 KiB LDS, two workgroups per CU); TH = 4: 128 pixels
+// (40 KiB, four per CU); TH = 2: 64 pixels (20 KiB, eight per CU)
 template <int KC, int TH>
 __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
   constexpr int NPIX = TH * TW;
@@ -68,8 +68,10 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
   // 1. per-tap lists of occupied (input cell, pixel) entries
   const int p = tid % NPIX, oy = oy0 + p / TW, ox = ox0 + p % TW;
   const bool in_out = oy < a.Ho && ox < a.Wo;
-  const int tg = tid / NPIX;  // tap group: all taps (TH = 8) or taps 0-4 / 5-8 (TH = 4)
-  auto mine = [&](int t) { return NPIX == 256 || (tg == 0 ? t < 5 : t >= 5); };
+  // 256 / NPIX thread groups share the taps: group g tests taps t with t % G == g
+  constexpr int G = 256 / NPIX;
+  const int tg = tid / NPIX;
+  auto mine = [&](int t) { return G == 1 || t % G == tg; };
   const unsigned char* occ_b = a.occ + (long)b * a.H * a.W;
   unsigned okm = 0;
 #pragma unroll
@@ -95,46 +97,68 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
   }
   __syncthreads();
 
-  // 2. wave wid: output channels [16 wid, 16 wid + 16), taps in order
+  // 2. wave wid: output channels [16 wid, 16 wid + 16); the (tap, 16-entry chunk) items in tap
+  // order, the next item's activation and weight fragments loaded while this one computes
   const int fr = lane & 15, fq = lane >> 4;
   const float* in_b = a.in + (long)b * a.H * a.W * a.ldi + a.ci_off + 8 * fq;
-  for (int t = 0; t < 9; ++t) {
-    const int cnt = cnt_s[t][0] + cnt_s[t][1] + cnt_s[t][2] + cnt_s[t][3];
-    if (cnt == 0) continue;
-    bf16x8 wh[KC], wl[KC];
+  int cnt[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) cnt[t] = cnt_s[t][0] + cnt_s[t][1] + cnt_s[t][2] + cnt_s[t][3];
+  struct Item {
+    uint4 xh[KC], xl[KC], wh[KC], wl[KC];
+    int e;
+    bool valid;
+  };
+  auto load = [&](int t, int c0, Item& it) {
+    it.valid = c0 + fr < cnt[t];
+    it.e = list_s[t][it.valid ? c0 + fr : c0];
+    const float* src = in_b + (long)(it.e >> 8) * a.ldi;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
+      it.xh[kc] = *reinterpret_cast<const uint4*>(src + kc * 32);
+      it.xl[kc] = *reinterpret_cast<const uint4*>(src + kc * 32 + 4);
       const uint4* wf = a.w + ((long)((t * KC + kc) * (N / 16) + wid) * 2) * 64 + lane;
-      const uint4 h = wf[0], l = wf[64];
-      wh[kc] = *reinterpret_cast<const bf16x8*>(&h);
-      wl[kc] = *reinterpret_cast<const bf16x8*>(&l);
+      it.wh[kc] = wf[0];
+      it.wl[kc] = wf[64];
     }
-    for (int c0 = 0; c0 < cnt; c0 += 16) {
-      const bool valid = c0 + fr < cnt;
-      const int e = list_s[t][valid ? c0 + fr : c0];
-      const float* src = in_b + (long)(e >> 8) * a.ldi;
-      uint4 xh[KC], xl[KC];
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        xh[kc] = *reinterpret_cast<const uint4*>(src + kc * 32);
-        xl[kc] = *reinterpret_cast<const uint4*>(src + kc * 32 + 4);
-      }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {  // products in conv_hx3.hip mfma3's order
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&xh[kc]);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(&xl[kc]);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[kc], ah, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kc], al, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[kc], ah, acc, 0, 0, 0);
-      }
-      if (valid) {  // lane: channels 16 wid + 4 fq .. + 4 of entry fr's pixel
-        float4* dst = reinterpret_cast<float4*>(acc_s + (e & 255) * LDA + 16 * wid + 4 * fq);
-        float4 v = *dst;
-        v.x += acc[0]; v.y += acc[1]; v.z += acc[2]; v.w += acc[3];
-        *dst = v;
-      }
+  };
+  // next item after (t, c0): the following chunk of tap t, else the first chunk of the next
+  // tap with entries; t == 9: none
+  auto advance = [&](int& t, int& c0) {
+    c0 += 16;
+    if (t < 9 && c0 < cnt[t]) return;
+    c0 = 0;
+    for (++t; t < 9 && cnt[t] == 0; ++t) {
     }
+  };
+  int t = -1, c0 = 0;
+  advance(t, c0);
+  Item cur, nxt;
+  if (t < 9) load(t, c0, cur);
+  while (t < 9) {
+    int tn = t, cn = c0;
+    advance(tn, cn);
+    if (tn < 9) load(tn, cn, nxt);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {  // products in conv_hx3.hip mfma3's order
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&cur.xh[kc]);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(&cur.xl[kc]);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&cur.wh[kc]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&cur.wl[kc]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+    }
+    if (cur.valid) {  // lane: channels 16 wid + 4 fq .. + 4 of entry fr's pixel
+      float4* dst = reinterpret_cast<float4*>(acc_s + (cur.e & 255) * LDA + 16 * wid + 4 * fq);
+      float4 v = *dst;
+      v.x += acc[0]; v.y += acc[1]; v.z += acc[2]; v.w += acc[3];
+      *dst = v;
+    }
+    cur = nxt;
+    t = tn;
+    c0 = cn;
   }
   __syncthreads();
 
@@ -174,7 +198,7 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
 
 // fp32 mode, pair activations in, 3x3 stride 2 pad 1, N == 64, Cin 32 or 64, no residual:
 // the same arguments and weights as tca_conv_hx3s2p (conv_hx3.hip), occ required.
-// act | 32: fp32 storage out.  tile: 0 auto (8 x 32 output tiles), 1 (4 x 32).
+// act | 32: fp32 storage out.  tile: 0 auto (4 x 32 output tiles), 1 (8 x 32), 2 (2 x 32).
 TCA_API int tca_conv_s2sp(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
                           const float* bias, int n, float* out, int ldo, int co_off, int act,
                           const unsigned char* occ, int tile, hipStream_t stream) {
@@ -186,13 +210,16 @@ TCA_API int tca_conv_s2sp(const float* in, int B, int H, int W, int Cin, int ldi
   a.in = in; a.occ = occ; a.w = reinterpret_cast<const uint4*>(wfrag); a.bias = bias; a.out = out;
   a.B = B; a.H = H; a.W = W; a.ldi = ldi; a.ci_off = ci_off; a.Ho = (H + 1) / 2; a.Wo = (W + 1) / 2;
   a.ldo = ldo; a.co_off = co_off; a.act = act;
-  const int TH = tile == 1 ? 4 : 8;  // 0 = auto (8 x 32), 1 = 4 x 32
+  const int TH = tile == 1 ? 8 : tile == 2 ? 2 : 4;  // 0 = auto (4 x 32), 1 = 8 x 32, 2 = 2 x 32
   a.tiles_x = (a.Wo + TW - 1) / TW;
   a.tiles = a.tiles_x * ((a.Ho + TH - 1) / TH);
   const dim3 grid(a.tiles, B);
   if (TH == 4) {
     if (Cin == 64) conv_s2sp_kernel<2, 4><<<grid, 256, 0, stream>>>(a);
     else conv_s2sp_kernel<1, 4><<<grid, 256, 0, stream>>>(a);
+  } else if (TH == 2) {
+    if (Cin == 64) conv_s2sp_kernel<2, 2><<<grid, 256, 0, stream>>>(a);
+    else conv_s2sp_kernel<1, 2><<<grid, 256, 0, stream>>>(a);
   } else {
     if (Cin == 64) conv_s2sp_kernel<2, 8><<<grid, 256, 0, stream>>>(a);
     else conv_s2sp_kernel<1, 8><<<grid, 256, 0, stream>>>(a);

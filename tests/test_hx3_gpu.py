@@ -221,7 +221,7 @@ def test_hx3s2_fp32_storage_out(cuda, tile):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile", [140, 141])
+@pytest.mark.parametrize("tile", [140, 141, 142])
 @pytest.mark.parametrize("cin", [32, 64])
 @pytest.mark.parametrize("pattern", ["random", "arcs", "empty"])
 def test_s2sp_sparse_gather_conv(cuda, tile, cin, pattern):
