@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(256) conv_s2sp_kernel(S2spArgs a) {
   // tap with entries; t == 9: none
   auto advance = [&](int& t, int& c0) {
     c0 += 16;
-    if (t < 9 && c0 < cnt[t]) return;
+    if (t >= 0 && t < 9 && c0 < cnt[t]) return;
     c0 = 0;
     for (++t; t < 9 && cnt[t] == 0; ++t) {
     }
