@@ -224,8 +224,8 @@ def test_hx3s2_fp32_storage_out(cuda, tile):
 @pytest.mark.parametrize("tile", [140, 141, 142])
 @pytest.mark.parametrize("cin", [32, 64])
 @pytest.mark.parametrize("pattern", ["random", "arcs", "empty"])
-def test_s2sp_sparse_gather_conv(cuda, tile, cin, pattern):
-    """conv_s2sp.hip (tile 140, the default over an occupancy-marked canvas): garbage in the
+def test_s2sp_sparse_gather_conv(cuda, tile, cin, pattern, monkeypatch):
+    """conv_s2sp.hip (tiles 140-142; the route over an occupancy-marked canvas when S2SP): garbage in the
     unmarked cells; channel-offset input / output slices; partial 8 x 32 tiles; against fp64 on
     the masked input; close to the dense hx3s2 kernel (same split products, another order) and
     bit-identical to it on pixels whose window is empty; bit-reproducible run to run; fp32
@@ -235,6 +235,8 @@ def test_s2sp_sparse_gather_conv(cuda, tile, cin, pattern):
     conv = nn.Conv2d(cin, cout, 3, 2, 1, bias=True).double()
     fc = FusedConv(copy.deepcopy(conv).float(), act=1, device=cuda, precision="fp32")
     assert fc.s2sp_ok()
+    from triton_client_amd.ops import conv as conv_mod
+    monkeypatch.setattr(conv_mod, "S2SP", True)
     if pattern == "random":
         occ = (torch.rand(B, H, W) < 0.05).to(torch.uint8)
     elif pattern == "arcs":

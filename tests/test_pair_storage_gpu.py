@@ -207,7 +207,7 @@ def test_conv_pair_occupancy_gated_reads(cuda, tile):
 def test_lidar_pipeline_occupancy_matches_ungated(cuda, monkeypatch, s2sp):
     """The occupancy-gated first conv against the ungated one on the whole canvas: bit-identical
     with the dense gated kernel (masked loads give the same zeros); with the sparse-gather kernel
-    (conv_s2sp.hip, the default) the same detections to within the summation order."""
+    (conv_s2sp.hip, opt-in) the same detections to within the summation order."""
     import numpy as np
 
     from triton_client_amd.ops import conv as conv_mod

@@ -114,10 +114,11 @@ HX3S2_TILES = (120, 121, 122, 123, 124)
 # every eligible stride-1 layer (WINO False: hx3).  Tiles 130 (auto) and 131-134 select it explicitly.
 WINO = os.environ.get("TCA_WINO", "1") != "0"  # TCA_WINO=0: hx3 for A/B runs
 # conv_s2sp.hip (the sparse-gather stride-2 conv: only (pixel, tap) pairs whose input cell is
-# occupied): the default for a stride-2 pair conv over an occupancy-marked canvas with N == 64 and
-# Cin 32 / 64 (the first PointPillars BEV conv); S2SP False / TCA_S2SP=0: the dense hx3s2 kernel.
+# occupied) for a stride-2 pair conv over an occupancy-marked canvas with N == 64 and Cin 32 / 64
+# (the first PointPillars BEV conv).  Opt-in (S2SP True / TCA_S2SP=1): measured no faster than the
+# dense occupancy-masked hx3s2 kernel in the step (profiles/r5/s2sp/), which stays the default.
 # Tiles 140 (auto: 4 x 32 output tiles), 141 (8 x 32) and 142 (2 x 32) select it explicitly.
-S2SP = os.environ.get("TCA_S2SP", "1") != "0"
+S2SP = os.environ.get("TCA_S2SP", "0") == "1"
 S2SP_TILES = (140, 141, 142)
 S2SP_TILE = int(os.environ.get("TCA_S2SP_TILE", "0"))
 WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
