@@ -187,7 +187,8 @@ class IngestArena:
         self.buf = np.frombuffer(self.mm, np.uint8)
         self.base = self.buf.ctypes.data
         self.pinned = _host_register(self.mm, self.size) if pin else False
-        self._lock = threading.Lock()
+        # re-entrant: a block's finalizer can run inside alloc() (cyclic GC on an allocation there)
+        self._lock = threading.RLock()
         self._live = collections.deque()  # [offset, bytes, freed] in allocation order
         self._head = 0
         self.stats = {"allocs": 0, "bytes": 0, "full": 0}
