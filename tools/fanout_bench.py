@@ -38,6 +38,9 @@ def main(argv=None) -> int:
                     help="camera payload bytes (default a raw rgb8 1280x720 frame; a JPEG CompressedImage, the "
                          "reference's camera topic, is ~220 KB at quality 90)")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--bag", action="store_true",
+                    help="also measure replaying a ROS bag (in /dev/shm) of one GPU-step of frames + clouds: "
+                         "messages read into bytes vs uncompressed chunks read straight into the ingest arena")
     ap.add_argument("--deserialize", action="store_true",
                     help="also measure deserialising the node batch's wire messages into bytes (the copy path: the "
                          "ring copy comes on top) vs into the ring's ingest arena (the only copy)")
@@ -79,11 +82,12 @@ def main(argv=None) -> int:
                   f"-> rank 0 feeds {feed:4.1f} GPUs at {a.step_ms} ms/step", flush=True)
         best = max(rows, key=lambda r: r["GBps"])
         deser = _deserialize_rows(a, srcs, total) if a.deserialize else None
+        bag = _bag_rows(a, srcs, total) if a.bag else None
         out = {"tool": "tools/fanout_bench.py", "items_per_gpu": n, "frame_bytes": a.frame_bytes, "cloud_bytes": CLOUD,
                "step_ms": a.step_ms, "cpus_allowed": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
                "rows": rows, "best": best, "node_gpus": a.gpus,
                "node_step_copy_ms_at_best": best["median_ms"] * a.gpus,
-               "feeds_node": best["gpus_fed_at_1gpu_rate"] >= a.gpus, "deserialize": deser}
+               "feeds_node": best["gpus_fed_at_1gpu_rate"] >= a.gpus, "deserialize": deser, "bag": bag}
         print(json.dumps({"best_GBps": best["GBps"], "gpus_fed": best["gpus_fed_at_1gpu_rate"],
                           "cpus_allowed": out["cpus_allowed"]}))
         if a.json:
@@ -140,6 +144,50 @@ def _deserialize_rows(a, srcs, total):
                           f"{total / med / 1e9:6.1f} GB/s", flush=True)
     finally:
         arena.close(unlink=True)
+    return rows
+
+
+def _bag_rows(a, srcs, total):
+    """Bag replay on rank 0 (``Bag.read_messages``): one GPU-step of messages (a.items raw
+    frames + a.items clouds) from a ROS bag v2 in /dev/shm, into bytes vs with ``alloc`` = the
+    ingest arena (uncompressed chunks ``readinto`` the arena, payloads views of them)."""
+    from triton_client_amd.parallel.host_ring import IngestArena
+    from triton_client_amd.ros import msgs
+    from triton_client_amd.ros.bag import Bag, RosBag
+
+    n = a.items
+    path = f"/dev/shm/tca_fanout_{os.getpid()}.bag"
+    w = RosBag(path, "w")
+    for i, s in enumerate(srcs):
+        if i < n:
+            w.write("/cam", msgs.Image(header=msgs.Header(seq=i), height=1, width=len(s) // 3, encoding="rgb8",
+                                       step=len(s), data=s))
+        else:
+            w.write("/pc", msgs.PointCloud2(header=msgs.Header(seq=i), height=1, width=len(s) // 16, point_step=16,
+                                            row_step=len(s), data=s))
+    w.close()
+    arena = IngestArena(f"/dev/shm/tca_fanout_bag_{os.getpid()}", 2 * (total + (64 << 20)), True, pin=False)
+    rows = []
+    try:
+        for mode in ("bytes", "arena"):
+            ts = []
+            for r in range(a.reps + 2):
+                t0 = time.perf_counter()
+                with Bag(path) as b:
+                    out = [m for _, m, _ in b.read_messages(alloc=arena.alloc if mode == "arena" else None)]
+                dt = time.perf_counter() - t0
+                assert len(out) == 2 * n
+                del out
+                if r >= 2:
+                    ts.append(dt)
+            med = float(np.median(ts))
+            rows.append({"mode": mode, "median_ms": med * 1e3, "GBps": total / med / 1e9, "us_per_msg": med / (2 * n) * 1e6,
+                         "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med})
+            print(f"bag replay into {mode:5s}: {med * 1e3:7.2f} ms per GPU-step = {total / med / 1e9:6.1f} GB/s, "
+                  f"{med / (2 * n) * 1e6:.0f} us per message", flush=True)
+    finally:
+        arena.close(unlink=True)
+        os.unlink(path)
     return rows
 
 
