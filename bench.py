@@ -75,13 +75,14 @@ def parse():
                          "(models/fast.py DETECT_FUSED; A/B)")
     ap.add_argument("--dense-bev", action="store_true",
                     help="PointPillars first block without uniform-tile skipping (models/fast.py BEV_UNIFORM; A/B)")
-    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3],
+    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3, 4],
                     help="LiDAR software pipeline over two LidarPipelines sharing one model (double-buffered "
                          "graphs only; every step still runs one full batch through every stage, results come "
                          "out one step later). 0: off. 1: network + NMS of batch t beside preprocessing of "
                          "batch t+1. 2: preprocessing + network of batch t beside decode + NMS of batch t-1. "
                          "3 (default): preprocessing + down blocks of batch t beside the fused neck + head + "
-                         "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/)")
+                         "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/). "
+                         "4: as 3 with the last down block in the back half too")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
@@ -470,6 +471,7 @@ def main():
             lids = [lid, make_lid(B, lid.model)]
             for lp in lids:
                 lp.build_fast()
+            blocks_front = len(lids[0].fast.bb.blocks) - 1 if args.lidar_pipeline == 4 else None
             side2 = torch.cuda.Stream()
             lside = side if side is not None else torch.cuda.Stream()
             # (the canvas clear moved from the front into the back half: 7.60 vs 7.60 ms, not kept;
@@ -484,7 +486,7 @@ def main():
                     side2.wait_stream(main)
                     if post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
                         with torch.cuda.stream(lside):
-                            lids[k].step_front(neck_back=args.lidar_pipeline == 3)
+                            lids[k].step_front(neck_back=args.lidar_pipeline >= 3, blocks_front=blocks_front)
                         with torch.cuda.stream(side2):
                             r3 = lids[1 - k].step_back()
                     else:  # graph k: pipeline k's network / NMS beside pipeline 1-k's preprocessing
@@ -573,7 +575,8 @@ def main():
             db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
         torch.cuda.synchronize()
         if piped:  # prologue: graph 0's first replay finishes a batch of pipeline 0 (mode 1) / 1 (mode 2)
-            lids[1].step_front(neck_back=args.lidar_pipeline == 3) if post_split else lids[0].step_pre()
+            lids[1].step_front(neck_back=args.lidar_pipeline >= 3, blocks_front=blocks_front) if post_split \
+                else lids[0].step_pre()
             torch.cuda.synchronize()
 
         class _DoubleBuffered:
@@ -819,7 +822,7 @@ def main():
                 "branch_streams": (3 if piped else 2) if side is not None else 1,
                 "graph_mode": args.graph_mode if side is not None else "single",
                 "graph_input_sets": 2 if db else 1,
-                "lidar_pipelined": (["off", "pre", "post", "neck"][args.lidar_pipeline] if piped else "off"),
+                "lidar_pipelined": (["off", "pre", "post", "neck", "block3"][args.lidar_pipeline] if piped else "off"),
                 "lidar_pipeline_note": ("two LiDAR pipelines alternate: each timed step runs one full batch through "
                                         "every stage, one batch's first half beside the previous batch's second "
                                         "half (split point: lidar_pipelined); detections leave one step later"

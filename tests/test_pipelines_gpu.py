@@ -92,9 +92,10 @@ def test_lidar_graph_replay_twice_is_stable(cuda):
         assert torch.equal(a[1][b, :n], r2.score[b, :n])
 
 
-@pytest.mark.parametrize("neck_back", [False, True])
-def test_lidar_post_split_pipelining_matches_step(cuda, neck_back):
-    """bench.py --lidar-pipeline 2 / 3: pipeline B's front (preprocessing + network) on one
+@pytest.mark.parametrize("neck_back,blocks_front", [(False, None), (True, None), (True, 2)])
+def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, blocks_front):
+    """bench.py --lidar-pipeline 2 / 3 / 4: pipeline B's front (preprocessing + network; with
+    blocks_front only the first two down blocks, the third runs in the back half) on one
     stream beside pipeline A's back (neck + head / decode + rotated NMS of A's previous
     front) on another gives A exactly the detections of a plain step(); two rounds over
     swapped frames catch a canvas cell left uncleared."""
@@ -120,11 +121,11 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back):
         _load_lidar(la, spec, sa)
         _load_lidar(lb, spec, sb)
         torch.cuda.synchronize()
-        la.step_front(neck_back)
+        la.step_front(neck_back, blocks_front)
         s1.wait_stream(main)
         s2.wait_stream(main)
         with torch.cuda.stream(s1):
-            lb.step_front(neck_back)
+            lb.step_front(neck_back, blocks_front)
         with torch.cuda.stream(s2):
             got[f"a{rnd}"] = snap(la.step_back())
         main.wait_stream(s1)

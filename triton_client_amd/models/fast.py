@@ -412,18 +412,26 @@ class _BEVBackbonePlan:
         torch.cuda.synchronize(device)
         return vals
 
-    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
+    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None, outs: Optional[List[NHWC]] = None) -> List[NHWC]:
         """The down blocks only: each block's output (the deblocks' inputs).  With the canvas
         occupancy, the first block's stride-1 convs store their constant on the tiles whose
-        receptive field holds no occupied cell (tca_bev_uniform_depth); bit-identical."""
-        x, outs = canvas, []
-        uni = self.uni_vals is not None and canvas.occ is not None and BEV_UNIFORM
+        receptive field holds no occupied cell (tca_bev_uniform_depth); bit-identical.
+        stop: run blocks [0, stop) only; outs: the outputs of the blocks already run (continue
+        from the last one -- bench.py --lidar-pipeline 4 runs the last block in the back half)."""
+        outs = list(outs or [])
+        x = outs[-1] if outs else canvas
+        first = len(outs)
+        stop = len(self.blocks) if stop is None else stop
+        uni = (first == 0 and self.uni_vals is not None and canvas is not None and canvas.occ is not None
+               and BEV_UNIFORM)
         if uni:
             B, ny, nx = canvas.occ.shape
             assert (ny, nx) == (self.ny, self.nx) and B == self.depth.shape[0], (canvas.occ.shape, self.depth.shape)
             _native.call("tca_bev_uniform_depth", _native.ptr(canvas.occ), B, ny, nx, len(self.blocks[0][0]),
                          _native.ptr(self.depth), _native.stream_ptr(None))
         for bi, (convs, pp, H, W) in enumerate(self.blocks):
+            if bi < first or bi >= stop:
+                continue
             for i, cv in enumerate(convs):
                 # the stride-2 conv skips tiles whose windows hold no occupied cell (depth >= 1)
                 u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 else None
@@ -502,13 +510,16 @@ class FastBEV:
             self.head(self.bb.forward(canvas), out=self.hout)
         return self.head_maps()
 
-    def forward_blocks(self, canvas: NHWC) -> List[NHWC]:
-        """The down blocks only (pair canvas); forward_neck finishes the batch from their outputs,
-        which stay in this plan's buffers until its next forward_blocks."""
+    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None) -> List[NHWC]:
+        """The down blocks only (pair canvas), or the first ``stop`` of them; forward_neck finishes
+        the batch from their outputs, which stay in this plan's buffers until its next
+        forward_blocks."""
         assert self.neck is not None and canvas.pair == self.pair
-        return self.bb.forward_blocks(canvas)
+        return self.bb.forward_blocks(canvas, stop)
 
     def forward_neck(self, blocks: List[NHWC]):
+        if len(blocks) < len(self.bb.blocks):  # the remaining down blocks first
+            blocks = self.bb.forward_blocks(None, outs=blocks)
         self.neck(blocks, self.hout)
         return self.head_maps()
 

@@ -130,16 +130,17 @@ class LidarPipeline:
         return canvas
 
     @torch.no_grad()
-    def step_front(self, neck_back: bool = False):
+    def step_front(self, neck_back: bool = False, blocks_front: Optional[int] = None):
         """Preprocessing + BEV network; the head maps stay in this pipeline's plan buffers
         for step_back (bench.py --lidar-pipeline 2: the decode / rotated NMS of one batch,
         a few low-occupancy kernels, runs beside the next batch's network).  neck_back
         (--lidar-pipeline 3): stop after the down blocks; step_back runs the fused neck +
-        head as well."""
+        head as well.  blocks_front (--lidar-pipeline 4): only the first blocks_front down
+        blocks here; step_back runs the rest before the neck."""
         canvas = self.step_pre()
         self._blocks = self._head = None
         if self.use_fast and neck_back and self.fast.neck is not None:
-            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc())
+            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc(), blocks_front)
         elif self.use_fast:
             self._head = self.fast.forward(self.enc.canvas_nhwc())
         else:
