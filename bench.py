@@ -82,7 +82,8 @@ def parse():
                          "batch t+1. 2: preprocessing + network of batch t beside decode + NMS of batch t-1. "
                          "3 (default): preprocessing + down blocks of batch t beside the fused neck + head + "
                          "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/). "
-                         "4: as 3 with the last down block in the back half too")
+                         "4: as 3 with the last down block in the back half too (bit-identical; 3241-3267 vs "
+                         "4699-4792 frame pairs/s: its convs starve the camera, profiles/r5/split4/)")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
