@@ -307,9 +307,12 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
   lds_barrier();  // the epilogue reuses the image
 
   // ---- epilogue: output transform + bias + act -> fp32 staging tile [TH * 32 rows][BN] (16-B
-  // quads XOR-swizzled by the row, as hx3_epilogue) -> 16-B stores
+  // quads XOR-swizzled by the row) -> 16-B stores.  A lane writes rows 2 fr and 2 fr + 1 (a tile's
+  // two outputs), so hx3's row swizzle (ml & 15) gave the 8 lanes of a ds_write_b128 group only 4
+  // distinct quads mod 8 (2-way conflicts); bit 3 of the row folded into bit 0 makes them 8, and
+  // rows 2k / 2k + 1 still differ in bit 0 (the ds_read_b128 groups span two rows: conflict-free).
   float* st = reinterpret_cast<float*>(smem);
-  auto quad = [](int ml, int q) { return ml * BN + ((q ^ (ml & 15)) << 2); };
+  auto quad = [](int ml, int q) { return ml * BN + ((q ^ ((ml & 15) ^ ((ml >> 3) & 1))) << 2); };
   const bool relu = a.act == 1;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
