@@ -446,6 +446,37 @@ def test_ingest_arena_fifo_allocator():
     assert not os.path.exists(path)
 
 
+def test_bag_read_ahead_threads_match_sequential(tmp_path):
+    """ROS bag replay with chunks read ahead by threads into alloc buffers: every message in
+    order and equal to the sequential read, a full arena (alloc -> None) falling back."""
+    from triton_client_amd.ros import compat, msgs
+    from triton_client_amd.ros.bag import Bag, RosBag
+
+    rng = np.random.default_rng(3)
+    path = str(tmp_path / "multi.bag")
+    w = RosBag(path, "w")
+    frames = [rng.integers(0, 255, (100, 300, 3), np.uint8) for _ in range(12)]
+    for i, f in enumerate(frames):
+        w.write("/cam", compat.numpy_to_imgmsg(f, "rgb8", header=msgs.Header(seq=i)))
+        w.write("/other", msgs.Header(seq=1000 + i))
+    w.close()
+    with Bag(path) as b:
+        want = [(t, m) for t, m, _ in b.read_messages()]
+    calls = []
+
+    def alloc(n):
+        calls.append(n)
+        return np.empty(n, np.uint8) if len(calls) % 3 else None  # every third: "full"
+    with Bag(path) as b:
+        got = [(t, m) for t, m, _ in b.read_messages(alloc=alloc, readers=4)]
+    assert calls and [t for t, _ in got] == [t for t, _ in want]
+    for (_, a), (_, c) in zip(got, want):
+        if hasattr(c, "data"):
+            assert bytes(a.data) == bytes(c.data) and a.header.seq == c.header.seq
+        else:
+            assert a.seq == c.seq
+
+
 def test_deserialize_into_caller_buffers(tmp_path):
     """rosmsg.deserialize / Bag.read_messages put large byte arrays into alloc() buffers
     (the ring's ingest arena) and leave small ones as bytes; the messages are unchanged."""
@@ -479,6 +510,11 @@ def test_deserialize_into_caller_buffers(tmp_path):
         bufs.clear()
         with Bag(path) as b:
             (_, back, _), = list(b.read_messages(topics=["/cam"], alloc=alloc))
+        with Bag(path) as b:  # chunks read ahead by reader threads: the same message
+            (_, back2, _), = list(b.read_messages(topics=["/cam"], alloc=alloc, readers=3))
+        assert bytes(back2.data) == bytes(back.data) and back2.header.seq == back.header.seq
+        got.pop()
+        bufs.pop()
         assert isinstance(back.data, memoryview), kind
         # ROS bags: the whole uncompressed chunk is read into the buffer and the payload is a view
         # of it; msgpack bags: the payload is copied into a buffer of its own size

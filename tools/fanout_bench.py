@@ -150,7 +150,8 @@ def _deserialize_rows(a, srcs, total):
 def _bag_rows(a, srcs, total):
     """Bag replay on rank 0 (``Bag.read_messages``): one GPU-step of messages (a.items raw
     frames + a.items clouds) from a ROS bag v2 in /dev/shm, into bytes vs with ``alloc`` = the
-    ingest arena (uncompressed chunks ``readinto`` the arena, payloads views of them)."""
+    ingest arena (uncompressed chunks ``readinto`` the arena, payloads views of them), and with
+    4 / 8 / 16 threads reading chunks ahead (``readers``)."""
     from triton_client_amd.parallel.host_ring import IngestArena
     from triton_client_amd.ros import msgs
     from triton_client_amd.ros.bag import Bag, RosBag
@@ -169,12 +170,14 @@ def _bag_rows(a, srcs, total):
     arena = IngestArena(f"/dev/shm/tca_fanout_bag_{os.getpid()}", 2 * (total + (64 << 20)), True, pin=False)
     rows = []
     try:
-        for mode in ("bytes", "arena"):
+        for mode in ("bytes", "arena", "arena_r4", "arena_r8", "arena_r16"):
+            readers = int(mode.split("_r")[1]) if "_r" in mode else 0
             ts = []
             for r in range(a.reps + 2):
                 t0 = time.perf_counter()
                 with Bag(path) as b:
-                    out = [m for _, m, _ in b.read_messages(alloc=arena.alloc if mode == "arena" else None)]
+                    out = [m for _, m, _ in b.read_messages(alloc=arena.alloc if mode != "bytes" else None,
+                                                            readers=readers)]
                 dt = time.perf_counter() - t0
                 assert len(out) == 2 * n
                 del out
@@ -183,7 +186,7 @@ def _bag_rows(a, srcs, total):
             med = float(np.median(ts))
             rows.append({"mode": mode, "median_ms": med * 1e3, "GBps": total / med / 1e9, "us_per_msg": med / (2 * n) * 1e6,
                          "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med})
-            print(f"bag replay into {mode:5s}: {med * 1e3:7.2f} ms per GPU-step = {total / med / 1e9:6.1f} GB/s, "
+            print(f"bag replay into {mode:9s}: {med * 1e3:7.2f} ms per GPU-step = {total / med / 1e9:6.1f} GB/s, "
                   f"{med / (2 * n) * 1e6:.0f} us per message", flush=True)
     finally:
         arena.close(unlink=True)

@@ -28,6 +28,11 @@ def _ingest(engine):
     return getattr(engine, "ingest_buffer", None)
 
 
+def _readers(engine) -> int:
+    """Threads reading the bag's chunks ahead into the ingest arena (with an arena only)."""
+    return 8 if getattr(engine, "ingest_buffer", None) is not None else 0
+
+
 def _batches(it, n):
     buf = []
     for item in it:
@@ -58,7 +63,8 @@ class BagInference2D(RosInference):
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
             it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
-                                                     alloc=_ingest(self.engine)))
+                                                     alloc=_ingest(self.engine),
+                                                     readers=_readers(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]
@@ -104,7 +110,8 @@ class BagInference3D(RosInference3D):
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
             it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
-                                                     alloc=_ingest(self.engine)))
+                                                     alloc=_ingest(self.engine),
+                                                     readers=_readers(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]

@@ -55,11 +55,13 @@ class RosBag:
     def write(self, topic: str, msg, t: Optional[msgs.Time] = None) -> None:
         self._w.write(topic, msg, t)
 
-    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0, alloc=None):
+    def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0, alloc=None,
+                      readers: int = 0):
         """``alloc(n)``: where large payloads are deserialised to (e.g. the DP ring's
-        ``ingest_buffer``); None keeps ``bytes``."""
+        ``ingest_buffer``); None keeps ``bytes``.  ``readers``: threads that read uncompressed
+        chunks ahead into ``alloc`` buffers (0: the calling thread reads)."""
         k = 0
-        for topic, m, t in rosbag_v2.read_messages(self._r, topics, alloc):
+        for topic, m, t in rosbag_v2.read_messages(self._r, topics, alloc, readers):
             k += 1
             if k <= start_seq:
                 continue
@@ -115,7 +117,7 @@ class TcaBag:
             yield msgpack.unpackb(self._f.read(n), raw=False)
 
     def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0,
-                      alloc=None) -> Iterator[Tuple[str, object, msgs.Time]]:
+                      alloc=None, readers: int = 0) -> Iterator[Tuple[str, object, msgs.Time]]:
         """Yields (topic, msg, t).  ``start_seq`` resumes a replay after the
         first ``start_seq`` matching messages."""
         k = 0

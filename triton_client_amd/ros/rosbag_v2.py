@@ -27,6 +27,7 @@ read with the stdlib; lz4 only if the ``lz4`` module is importable.
 from __future__ import annotations
 
 import bz2
+import os
 import struct
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
@@ -241,9 +242,86 @@ class RosBagReader:
                 cid = struct.unpack("<I", h["conn"])[0]
                 yield self.conns[cid], _read_time(h["time"]), data
 
-    def raw_messages(self, alloc=None) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
+    def _records(self) -> Iterator[Tuple[Dict[str, bytes], int, int]]:
+        """(header, data offset, data length) of every record, reading headers only."""
+        f = self.f
+        f.seek(len(MAGIC))
+        while True:
+            b = f.read(4)
+            if len(b) < 4:
+                return
+            (hl,) = struct.unpack("<I", b)
+            h = _parse_fields(f.read(hl))
+            b = f.read(4)
+            if len(b) < 4:
+                return
+            (dl,) = struct.unpack("<I", b)
+            off = f.tell()
+            yield h, off, dl
+            f.seek(off + dl)
+
+    def _prefetched(self, alloc, readers: int, ahead: int):
+        """Records with the data of uncompressed chunks read ahead by ``readers`` threads
+        (``os.preadv`` into ``alloc`` buffers, GIL released) -- a single reader thread bounds bag
+        replay at one core's copy rate otherwise (``tools/fanout_bench.py --bag``)."""
+        import collections
+        from concurrent.futures import ThreadPoolExecutor
+
+        fd = self.f.fileno()
+
+        def read_into(buf, off, n):
+            mv = memoryview(buf)
+            got = 0
+            while got < n:
+                k = os.preadv(fd, [mv[got:]], off + got)
+                if k <= 0:
+                    raise ValueError("truncated ROS bag chunk")
+                got += k
+            return mv
+
+        recs = list(self._records())
+        pending = collections.deque()
+        with ThreadPoolExecutor(readers, thread_name_prefix="bagread") as pool:
+            it = iter(recs)
+
+            def fill():
+                while len(pending) < ahead:
+                    r = next(it, None)
+                    if r is None:
+                        return
+                    h, off, dl = r
+                    fut = None
+                    if (dl >= rosmsg.ALLOC_MIN and h.get("op", b"\0")[0] == OP_CHUNK
+                            and h.get("compression", b"none") == b"none"):
+                        buf = alloc(dl)
+                        if buf is not None:
+                            fut = pool.submit(read_into, buf, off, dl)
+                    pending.append((h, off, dl, fut))
+            fill()
+            while pending:
+                h, off, dl, fut = pending.popleft()
+                if fut is not None:
+                    data = fut.result()
+                else:
+                    data = os.pread(fd, dl, off)
+                fill()
+                yield h, data
+
+    def raw_messages(self, alloc=None, readers: int = 0, ahead: int = 8) -> Iterator[Tuple[Connection, msgs.Time, bytes]]:
         """(connection, time, serialised bytes) in file order (memoryviews into ``alloc``
-        buffers for uncompressed chunks when ``alloc`` is given)."""
+        buffers for uncompressed chunks when ``alloc`` is given; with ``readers`` > 0 those
+        chunks are read ahead by that many threads, up to ``ahead`` records in flight)."""
+        if alloc is not None and readers > 0:
+            for h, data in self._prefetched(alloc, readers, ahead):
+                op = h["op"][0]
+                if op == OP_CHUNK:
+                    yield from self._iter_payload(self._decompress(h["compression"].decode(), data))
+                elif op == OP_CONNECTION:
+                    self._conn(h, data)
+                elif op == OP_MSG:
+                    cid = struct.unpack("<I", h["conn"])[0]
+                    yield self.conns[cid], _read_time(h["time"]), data
+            return
         self.f.seek(len(MAGIC))
         while True:
             rec = self._read_record(self.f, alloc)
@@ -277,9 +355,10 @@ def is_rosbag(path: str) -> bool:
         return f.read(len(MAGIC)) == MAGIC
 
 
-def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None):
-    """``alloc``: see :func:`rosmsg.deserialize` (large payloads written into caller buffers)."""
-    for c, t, data in reader.raw_messages(alloc):
+def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None, readers: int = 0):
+    """``alloc``: see :func:`rosmsg.deserialize` (large payloads written into caller buffers);
+    ``readers``: threads reading uncompressed chunks ahead into ``alloc`` buffers."""
+    for c, t, data in reader.raw_messages(alloc, readers):
         if topics and c.topic not in topics:
             continue
         yield c.topic, reader.decode(c, data, alloc), t
