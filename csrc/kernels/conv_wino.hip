@@ -104,9 +104,17 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// raw-halo slot of (pixel fi along F, 16-B piece slot = cq * 2 + hl): XOR swizzle by fi / 2 so the
-// transform's reads (16 lanes = 16 tiles at pixels 2t + j) spread over 8 bank groups per half
-__device__ __forceinline__ int raw_slot(int fi, int slot) { return slot ^ ((fi >> 1) & 7); }
+// Raw-halo layout of (pixel fi along F, 16-B piece slot = cq * 2 + hl).  A transform read (fixed
+// j and hl) has lane (cq, t) at pixel 2t + j; a ds_read_b128 lane group holds tiles t of two cq
+// ({0-3, 12-15} of one, {4-11} of the other).  With 128 B per pixel all 16 lanes of a group fall
+// in one 128-B half of the 64 banks (2-way at best), so pixel pairs swap places by bit 1 of fi
+// (raw_pos: the half alternates with t), and the slot XOR (raw_slot) takes (fi >> 2) & 3 plus
+// bit 3 of fi / 2 + 4, which separates the two cq's tile sets: conflict-free for j = 0, 1, a few
+// 2-way lanes for j = 2, 3 (was 2-way throughout).
+__device__ __forceinline__ int raw_pos(int fi) { return fi ^ ((fi >> 1) & 1); }
+__device__ __forceinline__ int raw_slot(int fi, int slot) {
+  return slot ^ (((fi >> 2) & 3) | (((((fi >> 1) + 4) >> 3) & 1) << 2));
+}
 
 template <int TH, int WN, int FN, bool CM, bool PIN, bool POUT>
 __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
@@ -169,7 +177,7 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
 #pragma unroll
   for (int k = 0; k < DPW; ++k) {
     const int q = (wn * DPW + k) * 64 + lane;
-    const int u = q / 272, fi = (q / 8) % 34, slot = raw_slot(fi, q & 7);
+    const int u = q / 272, fi = raw_pos((q / 8) % 34), slot = raw_slot(fi, q & 7);
     int y, x;
     pix_yx(f0 - 1 + fi, l0 - 1 + u, y, x);
     dvo[k] = (q < NPIECE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
@@ -192,7 +200,7 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int fi = 2 * t + j;
-        const unsigned char* rp = raw + (u * 34 + fi) * 128;
+        const unsigned char* rp = raw + (u * 34 + raw_pos(fi)) * 128;
         const u32x4 p0 = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2) * 16);
         const u32x4 p1 = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2 + 1) * 16);
         join8<PIN>(p0, p1, d[j]);
