@@ -91,15 +91,16 @@ __global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layo
       if (obj > conf_thres && !multi_label) {
         float m = -INFINITY;
         int mc = 0;
+        // best over ALL classes, then the class filter drops the row (reference
+        // yolov5_postprocess.py:87-92: max first, `classes` filter after)
         for (int c = 0; c < nc; ++c) {
-          if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
           float v = ld(hp, base + (5 + c) * cstride);
           if (v > m) { m = v; mc = c; }
         }
         if (m > -INFINITY) {
           best = sigmoidf_(m) * obj;
           best_c = mc;
-          pass = best > conf_thres;
+          pass = best > conf_thres && !(class_mask && !((class_mask[mc >> 5] >> (mc & 31)) & 1u));
         }
       }
     }
@@ -143,11 +144,13 @@ __global__ void __launch_bounds__(256) yolo_filter_kernel(YoloHeads hd, int layo
 // (one 16-B store; consecutive threads write consecutive bytes) and the reads walk each row's
 // channels in order.  yolo_filter_kernel's decoded path (thread = row) wrote 85 floats per
 // thread at a 340-B stride across the wave, one cache line per lane per store.
+// The last thread of an output whose size is not a multiple of 4 (e.g. img 416 / 608 at batch 1:
+// N = 10647 / 22743 rows of 85) writes its 1-3 leftover floats with scalar stores.
 template <typename T>
-__global__ void __launch_bounds__(256) yolo_decode_kernel(YoloHeads hd, int layout, int na, int nc, long total4,
+__global__ void __launch_bounds__(256) yolo_decode_kernel(YoloHeads hd, int layout, int na, int nc, long total,
                                                           float* __restrict__ decoded) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= total4) return;
+  if (q * 4 >= total) return;
   const int no = nc + 5, C = na * no;
   const int n0 = na * hd.h[0] * hd.w[0], n1 = na * hd.h[1] * hd.w[1], n2 = na * hd.h[2] * hd.w[2];
   const long N = (long)n0 + n1 + n2;
@@ -155,6 +158,7 @@ __global__ void __launch_bounds__(256) yolo_decode_kernel(YoloHeads hd, int layo
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const long f = q * 4 + e;
+    if (f >= total) { v[e] = 0.f; continue; }
     const long row = f / no;
     const int c = (int)(f - row * no);
     const int b = (int)(row / N);
@@ -176,7 +180,11 @@ __global__ void __launch_bounds__(256) yolo_decode_kernel(YoloHeads hd, int layo
       default: v[e] = s;
     }
   }
-  *reinterpret_cast<float4*>(decoded + q * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  if (q * 4 + 4 <= total) {
+    *reinterpret_cast<float4*>(decoded + q * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int e = 0; q * 4 + e < total; ++e) decoded[q * 4 + e] = v[e];
+  }
 }
 
 }  // namespace
@@ -200,15 +208,15 @@ TCA_API int tca_yolo_decode(const void* head0, const void* head1, const void* he
     N += (long)na * hd.h[l] * hd.w[l];
   }
   const long total = (long)batch * N * (nc + 5);
-  if (total % 4 != 0 || ((uintptr_t)decoded & 15) != 0) return (int)hipErrorInvalidValue;  // 16-B stores
-  const long total4 = total / 4;
+  if (((uintptr_t)decoded & 15) != 0) return (int)hipErrorInvalidValue;  // 16-B stores
+  const long total4 = (total + 3) / 4;
   const int bs = 256;
   const unsigned grid = (unsigned)((total4 + bs - 1) / bs);
   switch (dtype) {
-    case kF32: yolo_decode_kernel<float><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded); break;
-    case kF16: yolo_decode_kernel<__half><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded); break;
+    case kF32: yolo_decode_kernel<float><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total, decoded); break;
+    case kF16: yolo_decode_kernel<__half><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total, decoded); break;
     case kBF16:
-      yolo_decode_kernel<__hip_bfloat16><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total4, decoded);
+      yolo_decode_kernel<__hip_bfloat16><<<grid, bs, 0, stream>>>(hd, layout, na, nc, total, decoded);
       break;
     default: return (int)hipErrorInvalidValue;
   }
@@ -272,7 +280,8 @@ TCA_API int tca_yolo_decode_filter(const void* head0, const void* head1, const v
 //          normalised x1y1x2y2 (pred) + confs [B, N, nc] (conf); best conf > t
 //          (tools/utils.py:166-233), boxes scaled to img_w x img_h.
 // One thread per row: the row's first gate is one load (obj, kind 0), the
-// class scan only runs for rows that pass it.  The products are fp32 like the
+// class scan only runs for rows that pass it.  A class filter drops a row whose
+// best class is masked (it never promotes a lower-scoring allowed class).  The products are fp32 like the
 // reference's NumPy float32 ``x[:, 5:] *= x[:, 4:5]``, so the kept sets match.
 // ============================================================================
 namespace {
@@ -299,13 +308,12 @@ __global__ void __launch_bounds__(256) yolo_filter_decoded_kernel(
         box[0] = cx - hw; box[1] = cy - hh; box[2] = cx + hw; box[3] = cy + hh;
         if (!multi_label) {
           float m = -INFINITY;
-          for (int c = 0; c < nc; ++c) {
-            if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+          for (int c = 0; c < nc; ++c) {  // best over all classes, class filter after (see K3)
             const float v = row[5 + c] * obj;
             if (v > m) { m = v; best_c = c; }
           }
           best = m;
-          pass = m > conf_thres;
+          pass = m > conf_thres && !(class_mask && !((class_mask[best_c >> 5] >> (best_c & 31)) & 1u));
         } else {
           for (int c = 0; c < nc; ++c) {
             if (class_mask && !((class_mask[c >> 5] >> (c & 31)) & 1u)) continue;

@@ -194,15 +194,14 @@ __global__ void __launch_bounds__(256, 2) yolo_detect_filter_kernel(DetArgs a) {
       box[0] = cx - bw * 0.5f; box[1] = cy - bh * 0.5f; box[2] = cx + bw * 0.5f; box[3] = cy + bh * 0.5f;
       float m = -INFINITY;
       int mc = 0;
-      for (int c = 0; c < a.nc; ++c) {
-        if (a.class_mask && !((a.class_mask[c >> 5] >> (c & 31)) & 1u)) continue;
+      for (int c = 0; c < a.nc; ++c) {  // best over all classes, then the class filter (reference order)
         const float v = row[5 + c];
         if (v > m) { m = v; mc = c; }
       }
       if (m > -INFINITY) {
         best = sigmoidf_(m) * obj;
         best_c = mc;
-        pass = best > a.conf_thres;
+        pass = best > a.conf_thres && !(a.class_mask && !((a.class_mask[mc >> 5] >> (mc & 31)) & 1u));
       }
     }
   }

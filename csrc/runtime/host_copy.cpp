@@ -14,7 +14,12 @@
 // ordinary store) only costs memory bandwidth -- the budget rank 0 spends feeding the
 // node's GPUs through the shared host ring (tools/fanout_bench.py).  TCA_HOST_COPY_NT=0
 // turns it off (plain memcpy) for A/B runs.
+#if defined(__x86_64__) || defined(__i386__)
 #include <immintrin.h>
+#define TCA_HAVE_NT_COPY 1
+#else
+#define TCA_HAVE_NT_COPY 0  // other hosts: plain memcpy
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -30,6 +35,7 @@ namespace {
 constexpr int64_t kChunk = 1 << 20;
 constexpr int64_t kStreamMin = 64 << 10;  // pieces below this keep memcpy
 
+#if TCA_HAVE_NT_COPY
 __attribute__((target("avx2"))) void copy_stream(char* d, const char* s, int64_t n) {
   int64_t head = (int64_t)((32 - ((uintptr_t)d & 31)) & 31);
   if (head > n) head = n;
@@ -51,6 +57,8 @@ __attribute__((target("avx2"))) void copy_stream(char* d, const char* s, int64_t
   std::memcpy(d + body, s + body, (size_t)(n - body));
 }
 
+void store_fence() { _mm_sfence(); }
+
 bool use_stream() {
   static const bool on = [] {
     const char* e = std::getenv("TCA_HOST_COPY_NT");
@@ -58,6 +66,11 @@ bool use_stream() {
   }();
   return on;
 }
+#else
+void copy_stream(char* d, const char* s, int64_t n) { std::memcpy(d, s, (size_t)n); }
+void store_fence() {}
+bool use_stream() { return false; }
+#endif
 }  // namespace
 
 // n copies dst[i] <- src[i] of nbytes[i]; returns 0, or -1 on a bad argument.
@@ -91,7 +104,7 @@ TCA_API int tca_host_gather_copy(int n, void* const* dst, const void* const* src
         std::memcpy(pieces[k].d, pieces[k].s, pieces[k].len);
       }
     }
-    if (streamed) _mm_sfence();  // this thread's streaming stores are globally visible before it joins
+    if (streamed) store_fence();  // this thread's streaming stores are globally visible before it joins
   };
   std::vector<std::thread> pool;
   pool.reserve(t - 1);

@@ -4,6 +4,8 @@ is exclusive, writers are not starved, and a first-use capture inside a submissi
 import threading
 import time
 
+import pytest
+
 from triton_client_amd.pipelines.graph import CaptureGate
 
 
@@ -75,3 +77,37 @@ def test_reentrant_and_upgrade_inside_shared():
     with g.exclusive():  # the gate is free again
         pass
     assert g._readers == 0 and g._writer is None
+
+
+@pytest.mark.gpu
+def test_two_threads_submit_to_executor_with_lazy_capture(cuda):
+    """Both sets' graphs dropped, so the first submissions capture inside ``submit``
+    (shared -> exclusive while holding the executor lock) while a second thread submits
+    to the same executor: with the lock taken before the gate, neither blocks forever."""
+    import torch
+
+    from triton_client_amd.pipelines.stream import StreamExecutor
+
+    class Owner:
+        x = torch.zeros(1024, device=cuda)
+
+    own = Owner()
+    ex = StreamExecutor(lambda: own.x * 2 + 1, [(own, "x")], cuda)
+    for r in ex.runners:
+        r.graph = None  # the next call of each set re-captures inside submit
+    host = [torch.full((1024,), float(i), pin_memory=True) for i in range(4)]
+    got, errs = {}, []
+
+    def worker(i):
+        try:
+            t = ex.submit(lambda k, i=i: [(ex.inputs[k][0], host[i])]).wait()
+            got[i] = float(t.host[0][0])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts), "submission deadlocked"
+    assert not errs and got == {i: 2.0 * i + 1 for i in range(4)}

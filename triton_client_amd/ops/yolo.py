@@ -238,11 +238,12 @@ class YoloPostprocess:
                     ii, jj = ii[keep], jj[keep]
                 bx, sc, cl, tie = box[ii], cls_conf[ii, jj].astype(np.float32), jj, idx[ii] * nc + jj
             else:
-                if self.classes is not None:
-                    cls_conf = np.where(allowed[None, :], cls_conf, -1.0)
+                # best over all classes, then the class filter (yolov5_postprocess.py:87-92)
                 j = cls_conf.argmax(1) if len(cls_conf) else np.zeros((0,), np.int64)
                 conf = cls_conf[np.arange(len(j)), j].astype(np.float32)
                 sel = conf > self.conf_thres
+                if self.classes is not None:
+                    sel &= allowed[j]
                 bx, sc, cl, tie = box[sel], conf[sel], j[sel], idx[sel]
             from .nms import sort_and_nms_cpu
             keep = sort_and_nms_cpu(bx, sc, cl.astype(np.int32), tie, 0, self.iou_thres, self.max_nms,

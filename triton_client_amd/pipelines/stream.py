@@ -185,7 +185,10 @@ class StreamExecutor:
         (e.g. the annotated frames of set k) into fresh pinned tensors, or
         into ``extras_dst[i]`` (page-locked host tensors, e.g. slots of the
         data-parallel host ring) where given."""
-        with self.gate.shared(), self.lock:  # (no submission inside another thread's capture window)
+        # executor lock first, then the gate's shared side: a thread waiting for the lock holds
+        # no shared hold, so a first-use capture below (shared -> exclusive while holding the
+        # lock) only waits for other executors' submissions, which never need this lock
+        with self.lock, self.gate.shared():  # (no submission inside another thread's capture window)
             k = self.next
             self.next = (k + 1) % self.sets
             for ev in self.set_free[k]:  # set k's inputs / stage are still being read back
