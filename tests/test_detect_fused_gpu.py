@@ -30,10 +30,19 @@ def _sorted_cands(cand):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("img_hw", [(640, 640), (320, 416)])
-@pytest.mark.parametrize("classes", [None, [0, 2, 5, 17, 63]])
+@pytest.mark.parametrize("classes", [None, "common"])
 def test_detect_fused_candidates_identical(cuda, img_hw, classes):
     c = _cam(cuda, img_hw)
     f = c.build_fast()
+    if classes == "common":
+        # a class filter drops rows whose best class is masked: filter on the classes the random-init
+        # heads actually pick (every other one of the most frequent), so both kernels keep candidates
+        p0 = YoloPostprocess(c.model.cfg.nc, c.model.anchors.cpu(), img_hw, 0.3, 0.45, 300, device=cuda)
+        c.step()
+        cand0, _ = p0._filter(f.forward(from_t1=True), False)
+        cls0 = torch.cat([cand0.cls[b, :min(int(cand0.count[b]), cand0.cls.shape[1])] for b in range(2)])
+        freq = torch.bincount(cls0.long(), minlength=c.model.cfg.nc)
+        classes = torch.argsort(freq, descending=True)[:6:2].tolist()
     post = YoloPostprocess(c.model.cfg.nc, c.model.anchors.cpu(), img_hw, 0.3, 0.45, 300, device=cuda,
                            classes=classes)
     assert post.detect_fused_ok(f)

@@ -587,3 +587,83 @@ def test_ring_payloads_from_ingest_arena_two_ranks(arena_mb):
             p.kill()
     assert res[1] == 3, res
     assert res[0] == ((22, 5, 3) if arena_mb else (0, 27, 3)), res
+
+
+def _file_worker(rank, world, port, q, path, shard):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TCA_NUMA_BIND="0", TCA_RING_FILE_SHARD=str(int(shard)))
+    try:
+        from triton_client_amd.parallel.dp import init_distributed
+        from triton_client_amd.parallel.ring_dp import DataParallelDetector2D
+        from triton_client_amd.ros.bag import Bag
+
+        info = init_distributed("gloo")
+        dp = DataParallelDetector2D(_SumEngine(), info, nslots=2, arena_mb=0)
+        if info.is_main:
+            assert dp.file_sharding == shard
+            seqs, dets = [], []
+            with Bag(path) as b:
+                ms = [m for _, m, _ in b.read_messages(topics=["/cam"], mapped=dp.file_sharding)]
+                for k in range(0, len(ms), 4):  # steps of 4 frames over the two ranks
+                    chunk = ms[k:k + 4]
+                    for m, (im, d) in zip(chunk, dp.process(chunk, draw=False)):
+                        seqs.append(im.header.seq)
+                        dets.append(d.tolist())
+                del ms
+            q.put((0, (seqs, dets, dp.file_items, dp.copied_items)))
+            dp.close()
+        else:
+            q.put((rank, dp.serve()))
+            dp.ring.close()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_sharded_bag_replay_reads_payloads_per_rank(tmp_path):
+    """Sharded replay: rank 0 reads the bag mapped (record headers + message prefixes only)
+    and publishes file offsets; rank 1 reads its shard's payloads from its own mapping of the
+    bag.  Same messages, same order and same results as the copy path and as one engine."""
+    _runtime_or_skip()
+    from triton_client_amd.ros import compat, msgs
+    from triton_client_amd.ros.bag import Bag, RosBag
+
+    rng = np.random.default_rng(5)
+    path = str(tmp_path / "cams.bag")
+    w = RosBag(path, "w")
+    frames = []
+    for i in range(10):
+        f = rng.integers(0, 255, (120, 200, 3), np.uint8)
+        frames.append(f)
+        w.write("/cam", compat.numpy_to_imgmsg(f, "rgb8", header=msgs.Header(seq=100 + i)))
+        if i % 3 == 0:  # a non-sensor message type between the frames (flushes the native parse run)
+            w.write("/other", msgs.BoundingBoxArray(header=msgs.Header(seq=i)))
+    w.close()
+    want = [d.tolist() for d in _SumEngine().detect(frames)]
+    out = {}
+    for shard in (True, False):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_file_worker, args=(r, 2, port, q, path, shard)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = dict(q.get(timeout=180) for _ in range(2))
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+        assert isinstance(res[1], int) and res[1] == 3, res
+        out[shard] = res[0]
+    seqs, dets, nfile, ncopy = out[True]
+    assert seqs == list(range(100, 110)) and dets == want
+    assert (nfile, ncopy) == (10, 0)
+    assert out[False][:2] == (seqs, dets) and out[False][2:] == (0, 10)
+    # the mapped reader yields the same messages as the ordinary one
+    with Bag(path) as a, Bag(path) as b:
+        ra, rb = list(a.read_messages()), list(b.read_messages(mapped=True))
+        assert len(ra) == len(rb) == 14
+        for (t1, m1, s1), (t2, m2, s2) in zip(ra, rb):
+            assert (t1, s1) == (t2, s2) and m1.header == m2.header
+            if t1 == "/cam":
+                assert bytes(m1.data) == bytes(m2.data) and isinstance(m2.data, memoryview)

@@ -119,18 +119,29 @@ def _deserialize_rows(a, srcs, total):
             wire.append((rosmsg.serialize(m), "sensor_msgs/PointCloud2"))
     arena = IngestArena(f"/dev/shm/tca_fanout_in_{os.getpid()}", 3 * (total + 256 * len(srcs)), True, pin=False)
     rows = []
+    by_type = {}
+    for w, typ in wire:
+        by_type.setdefault(typ, []).append(w)
     try:
         for t in [int(v) for v in a.threads.split(",")]:
             with ThreadPoolExecutor(t) as pool:
-                for mode in ("bytes", "arena"):
-                    alloc = arena.alloc if mode == "arena" else None
+                # bytes / arena: one deserialize() per message on a pool of t threads (the native parse
+                # for these types); arena_py: the same with the per-field Python reader (round 5's path);
+                # arena_batch: one deserialize_many() per message type, its payload copy on t threads
+                for mode in ("bytes", "arena", "arena_py", "arena_batch"):
+                    alloc = arena.alloc if mode != "bytes" else None
+                    fn = rosmsg.deserialize_py if mode == "arena_py" else rosmsg.deserialize
 
-                    def one(w, alloc=alloc):
-                        return rosmsg.deserialize(w[0], w[1], alloc)
+                    def one(w, alloc=alloc, fn=fn):
+                        return fn(w[0], w[1], alloc)
                     ts = []
                     for r in range(a.reps + 3):
                         t0 = time.perf_counter()
-                        out = list(pool.map(one, wire))
+                        if mode == "arena_batch":
+                            out = [m for typ, ws in by_type.items()
+                                   for m in rosmsg.deserialize_many(ws, typ, alloc=alloc, threads=t)]
+                        else:
+                            out = list(pool.map(one, wire))
                         dt = time.perf_counter() - t0
                         if mode == "arena":
                             assert all(isinstance(m.data, memoryview) for m in out)
@@ -140,7 +151,7 @@ def _deserialize_rows(a, srcs, total):
                     med = float(np.median(ts))
                     rows.append({"threads": t, "mode": mode, "median_ms": med * 1e3, "GBps": total / med / 1e9,
                                  "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med})
-                    print(f"deserialise into {mode:5s}, {t:3d} threads: {med * 1e3:7.2f} ms per GPU-step = "
+                    print(f"deserialise into {mode:11s}, {t:3d} threads: {med * 1e3:7.2f} ms per GPU-step = "
                           f"{total / med / 1e9:6.1f} GB/s", flush=True)
     finally:
         arena.close(unlink=True)
@@ -188,10 +199,77 @@ def _bag_rows(a, srcs, total):
                          "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med})
             print(f"bag replay into {mode:9s}: {med * 1e3:7.2f} ms per GPU-step = {total / med / 1e9:6.1f} GB/s, "
                   f"{med / (2 * n) * 1e6:.0f} us per message", flush=True)
+        rows.append(_sharded_row(a, path, total, n))
     finally:
         arena.close(unlink=True)
         os.unlink(path)
     return rows
+
+
+def _sharded_row(a, path, total, n):
+    """Sharded replay (``Bag.read_messages(mapped=True)`` + ``ring_dp`` file-sourced items):
+    rank 0's part per GPU-step is reading the record headers and message prefixes of the mapped
+    bag, building the messages and locating each payload in the file (``FileMaps.locate``, what
+    ``_write_step`` does per item) -- no payload byte.  Each rank's part is gathering its own
+    shard's payloads from its own mapping into its pinned staging (``gather_copy``, as the live
+    engines do), on its own cores.  GPUs fed = step time / rank 0's time per GPU-step; the
+    per-rank read must fit in one step on that rank's cores."""
+    from triton_client_amd.inference.live import gather_copy
+    from triton_client_amd.parallel.host_ring import FileMaps
+    from triton_client_amd.ros.bag import Bag
+
+    ts = []
+    for r in range(a.reps + 2):
+        t0 = time.perf_counter()
+        with Bag(path) as b:
+            ms = [m for _, m, _ in b.read_messages(mapped=True)]
+            locs = [FileMaps.locate(memoryview(m.data), len(m.data)) for m in ms]
+        dt = time.perf_counter() - t0
+        assert len(ms) == 2 * n and all(x is not None for x in locs)
+        if r >= 2:
+            ts.append(dt)
+        del ms, locs
+    med = float(np.median(ts))
+    # one rank's shard read: its GPU-step of payloads from the file into pinned staging
+    view = FileMaps.view(path)
+    with Bag(path) as b:
+        ms = [m for _, m, _ in b.read_messages(mapped=True)]
+        sizes = [len(m.data) for m in ms]
+        offs = [FileMaps.locate(memoryview(m.data), len(m.data))[1] for m in ms]
+    del ms
+    try:
+        import torch
+        pinned = torch.cuda.is_available()
+        dst = torch.empty(sum(sizes) + 4096 * len(sizes), dtype=torch.uint8, pin_memory=pinned)
+        base = dst.data_ptr()
+    except Exception:  # noqa: BLE001
+        pinned = False
+        dst = np.empty(sum(sizes) + 4096 * len(sizes), np.uint8)
+        base = dst.ctypes.data
+    dptr, o = [], 0
+    for z in sizes:
+        dptr.append(base + o)
+        o += (z + 4095) // 4096 * 4096
+    rt = {}
+    for th in (4, 8, 16):
+        tt = []
+        for r in range(a.reps + 2):
+            t0 = time.perf_counter()
+            gather_copy(dptr, [view[x:x + z] for x, z in zip(offs, sizes)], sizes, th)
+            if r >= 2:
+                tt.append(time.perf_counter() - t0)
+        rt[th] = float(np.median(tt))
+    best_th = min(rt, key=rt.get)
+    row = {"mode": "sharded", "rank0_ms_per_gpu_step": med * 1e3, "us_per_msg_rank0": med / (2 * n) * 1e6,
+           "gpus_fed_by_rank0": (a.step_ms / 1e3) / med,
+           "rank_shard_read_ms": {str(k): v * 1e3 for k, v in rt.items()},
+           "rank_shard_read_GBps": total / rt[best_th] / 1e9, "rank_read_fits_step": rt[best_th] * 1e3 <= a.step_ms,
+           "pinned_staging": pinned, "median_ms": med * 1e3, "GBps": None,
+           "gpus_fed_at_1gpu_rate": (a.step_ms / 1e3) / med}
+    print(f"sharded replay: rank 0 {med * 1e3:7.2f} ms per GPU-step ({med / (2 * n) * 1e6:.1f} us per message) -> "
+          f"feeds {row['gpus_fed_by_rank0']:.1f} GPUs; one rank's shard read {rt[best_th] * 1e3:.2f} ms "
+          f"({total / rt[best_th] / 1e9:.1f} GB/s, {best_th} threads)", flush=True)
+    return row
 
 
 if __name__ == "__main__":

@@ -20,6 +20,10 @@ SIGS = {
     "tca_jpeg_decode_batch": (I, [P, P, I, P, ctypes.c_int64, P, P, P, I]),
     # batched host payload copies into pinned staging (csrc/runtime/host_copy.cpp)
     "tca_host_gather_copy": (I, [I, P, P, P, I]),
+    # ROS1 wire parse of sensor messages / bag chunk record scan (csrc/runtime/ros_wire.cpp)
+    "tca_ros_parse": (I, [I, I, P, P, P]),
+    "tca_bag_scan": (ctypes.c_int64, [P, ctypes.c_int64, ctypes.c_int64, P, P, P, P, P, P, P, P]),
+    "tca_bag_index": (ctypes.c_int64, [P, ctypes.c_int64, P, ctypes.c_int64, P, P, P, P, P, P, P, P]),
     # node host ring signalling (csrc/runtime/host_ring.cpp)
     "tca_ring_publish": (I, [P, ctypes.c_uint32]),
     "tca_ring_load": (ctypes.c_uint32, [P]),

@@ -33,6 +33,16 @@ def _readers(engine) -> int:
     return 8 if getattr(engine, "ingest_buffer", None) is not None else 0
 
 
+def _read_kw(engine) -> dict:
+    """How the bag is read for this engine: a data-parallel engine that shards by file
+    (``ring_dp.file_sharding``) gets messages whose payloads stay in the mapped bag -- rank 0
+    reads record headers and message prefixes, every rank reads its own shard's payloads --
+    else payloads are deserialised into the ingest arena by reader threads."""
+    if getattr(engine, "file_sharding", False):
+        return {"mapped": True}
+    return {"alloc": _ingest(engine), "readers": _readers(engine)}
+
+
 def _batches(it, n):
     buf = []
     for item in it:
@@ -63,8 +73,7 @@ class BagInference2D(RosInference):
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
             it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
-                                                     alloc=_ingest(self.engine),
-                                                     readers=_readers(self.engine)))
+                                                     **_read_kw(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]
@@ -110,8 +119,7 @@ class BagInference3D(RosInference3D):
         t0 = time.perf_counter()
         with Bag(self.bagfile) as bag:
             it = (m for _, m, _ in bag.read_messages(topics=[p["sub_topic"]], start_seq=self.start_seq,
-                                                     alloc=_ingest(self.engine),
-                                                     readers=_readers(self.engine)))
+                                                     **_read_kw(self.engine)))
             for chunk in _batches(it, self.batch):
                 if self.max_frames is not None:
                     chunk = chunk[: max(0, self.max_frames - count)]

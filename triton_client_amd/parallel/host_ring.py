@@ -53,6 +53,8 @@ ITEMS_OFF = 8192
 MAX_ITEMS = (CTL_SLOT - ITEMS_OFF) // (ITEM_INTS * 8)
 ACK_OFF, ACK_STRIDE = 64, 64  # bytes: ack word of rank r at ACK_OFF + r * ACK_STRIDE
 HDR_OFF = ACK_OFF + 64 * ACK_STRIDE
+PATH_OFF = HDR_OFF + HDR_INTS * 8  # the step's source file (sharded replay): <u32 length><utf-8 path>
+PATH_MAX = ITEMS_OFF - PATH_OFF - 4
 
 
 def _rt():
@@ -264,6 +266,64 @@ class IngestArena:
                 pass
 
 
+class FileMaps:
+    """Read-only mappings of files whose payload bytes each rank reads for itself.
+
+    Sharded bag replay: rank 0 maps the bag (:meth:`~triton_client_amd.ros.rosbag_v2.RosBagReader.mapping`)
+    and publishes messages whose payloads are views of the mapping; the ring step records a
+    payload's *file offset* (item ``I_SRC`` = 2) and the file's path instead of copying the
+    bytes, and every rank -- rank 0 included -- maps the same file and gathers its own shard's
+    payloads from it into its own pinned staging, on its own cores.  Rank 0 never touches a
+    payload byte it does not run itself."""
+
+    _lock = __import__("threading").Lock()
+    _maps: list = []  # (path, mmap, base address, size); a file may be mapped more than once
+
+    @classmethod
+    def register(cls, path: str, mm) -> None:
+        base = np.frombuffer(mm, np.uint8).ctypes.data if len(mm) else 0
+        with cls._lock:
+            cls._maps.append((os.path.abspath(path), mm, base, len(mm)))
+
+    @classmethod
+    def unregister(cls, mm) -> None:
+        with cls._lock:
+            cls._maps[:] = [e for e in cls._maps if e[1] is not mm]
+
+    @classmethod
+    def locate(cls, payload, nbytes: int):
+        """(path, file offset) of a payload buffer inside a registered mapping, else None."""
+        if nbytes <= 0 or not cls._maps:
+            return None
+        try:
+            addr = np.frombuffer(payload, np.uint8, 1).ctypes.data
+        except (TypeError, ValueError):
+            return None
+        with cls._lock:
+            for path, _, base, size in cls._maps:
+                off = addr - base
+                if 0 <= off and off + nbytes <= size:
+                    return path, off
+        return None
+
+    @classmethod
+    def view(cls, path: str) -> np.ndarray:
+        """The whole file as a read-only uint8 array (mapped on first use in this process)."""
+        path = os.path.abspath(path)
+        with cls._lock:
+            ent = next((e for e in cls._maps if e[0] == path), None)
+        if ent is None:
+            with open(path, "rb") as f:
+                mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+            try:
+                mm.madvise(mmap.MADV_RANDOM)
+            except (AttributeError, OSError):
+                pass
+            cls.register(path, mm)
+            ent = (path, mm)
+        return np.frombuffer(ent[1], np.uint8)
+
+
 class HostRing:
     """Control ring + the current data generation (+ the ingest arena, when one was
     asked for).  Rank 0 ``create``s, the other ranks ``attach`` (after a barrier)."""
@@ -324,6 +384,20 @@ class HostRing:
     def items(self, s: int) -> np.ndarray:
         return np.frombuffer(self.mm, np.int64, MAX_ITEMS * ITEM_INTS, self._blk(s) + ITEMS_OFF).reshape(
             MAX_ITEMS, ITEM_INTS)
+
+    def set_path(self, s: int, path: str) -> None:
+        """Rank 0: the file slot s's file-sourced items (``I_SRC`` = 2) are read from."""
+        b = path.encode()
+        if len(b) > PATH_MAX:
+            raise ValueError(f"source path longer than {PATH_MAX} bytes")
+        o = self._blk(s) + PATH_OFF
+        self.ctl[o:o + 4] = np.frombuffer(np.uint32(len(b)).tobytes(), np.uint8)
+        self.ctl[o + 4:o + 4 + len(b)] = np.frombuffer(b, np.uint8)
+
+    def path(self, s: int) -> str:
+        o = self._blk(s) + PATH_OFF
+        n = int(np.frombuffer(self.mm, np.uint32, 1, o)[0])
+        return bytes(self.ctl[o + 4:o + 4 + min(n, PATH_MAX)]).decode()
 
     # ------------------------------------------------------------------ data generations
     def data_path(self, gen: int) -> str:

@@ -58,8 +58,11 @@ KIND_STOP, KIND_JPEG, KIND_FRAMES, KIND_CLOUDS = -1, 1, 2, 3
 # header ints
 H_SEQ, H_KIND, H_N, H_GEN, H_SLOT, H_MASK, H_PER, H_DRAW, H_KEY = 0, 1, 2, 3, 4, 5, 6, 7, 8
 H_CALIB = 60  # 1: rank 0 broadcasts its freshly calibrated weights in this step (every rank joins)
-# item ints: in_off, in_size, out_off, out_size, meta0, meta1, in_src (0: the slot, 1: the ingest arena)
+H_FILE = 61  # 1: file-sourced items read from the slot's path (sharded replay)
+# item ints: in_off, in_size, out_off, out_size, meta0, meta1, in_src (0: the slot, 1: the ingest arena,
+# 2: the step's source file -- in_off is then the payload's offset in that file)
 I_IN, I_INSZ, I_OUT, I_OUTSZ, I_M0, I_M1, I_SRC = range(7)
+SRC_SLOT, SRC_ARENA, SRC_FILE = 0, 1, 2
 _ALIGN = 4096
 
 log = logging.getLogger("triton_client_amd.ring_dp")
@@ -71,6 +74,9 @@ COPY_THREADS = int(os.environ.get("TCA_RING_COPY_THREADS", "8"))
 # rank 0's ingest arena (host_ring.IngestArena) in MiB when world > 1: deserialisers write payloads
 # straight into it and the ring step copies nothing; 0 turns it off (every payload copied into the slot)
 ARENA_MB = int(os.environ.get("TCA_RING_ARENA_MB", "512"))
+# sharded replay: payloads that are views of a mapped file (a bag, host_ring.FileMaps) travel as file
+# offsets and every rank reads its own shard from the file; 0 copies them into the slots like any payload
+FILE_SHARD = os.environ.get("TCA_RING_FILE_SHARD", "1") != "0"
 
 def _align(n: int) -> int:
     return (int(n) + _ALIGN - 1) // _ALIGN * _ALIGN
@@ -123,6 +129,14 @@ class _RingDP:
         self._slot_use: List[Optional[Tuple[int, List[int]]]] = [None] * nslots
         self._leases: Dict[Tuple[int, int], int] = {}
         self._lease_lock = threading.Lock()
+        self._path: Optional[str] = None  # the current step's source file (file-sourced items)
+        self.file_items = 0  # rank 0: payloads every rank read from the source file itself
+
+    @property
+    def file_sharding(self) -> bool:
+        """Bag replays should hand this engine messages whose payloads stay in the mapped
+        file (``Bag.read_messages(mapped=True)``): every rank then reads its own shard."""
+        return FILE_SHARD and self.info.world > 1
 
     # ------------------------------------------------------------------ rank 0
     def ingest_buffer(self, nbytes: int) -> Optional[np.ndarray]:
@@ -137,8 +151,12 @@ class _RingDP:
     def _raw(self, items, i: int, view: np.ndarray) -> np.ndarray:
         """Item i's input bytes: in the slot (``view``) or in the ingest arena."""
         off, n = int(items[i, I_IN]), int(items[i, I_INSZ])
-        if int(items[i, I_SRC]) == 1:
+        src = int(items[i, I_SRC])
+        if src == SRC_ARENA:
             return self.ring.arena.buf[off:off + n]
+        if src == SRC_FILE:  # this rank's own mapping of the source file: read by its own staging copy
+            from .host_ring import FileMaps
+            return FileMaps.view(self._path)[off:off + n]
         return view[off:off + n]
 
     def _participants(self) -> List[int]:
@@ -201,6 +219,16 @@ class _RingDP:
         sizes = [len(p) if not isinstance(p, np.ndarray) else p.nbytes for p in payloads]
         arena = self.ring.arena
         at = [arena.offset_of(p, z) if arena is not None else None for p, z in zip(payloads, sizes)]
+        at = [(SRC_ARENA, a) if a is not None else None for a in at]
+        path = None
+        if FILE_SHARD:
+            from .host_ring import FileMaps
+            for i, (p, z) in enumerate(zip(payloads, sizes)):
+                if at[i] is None:
+                    loc = FileMaps.locate(p, z)
+                    if loc is not None and (path is None or loc[0] == path):  # one source file per step
+                        path = loc[0]
+                        at[i] = (SRC_FILE, loc[1])
         need = sum(_align(z) for z, a in zip(sizes, at) if a is None) + sum(_align(z) for z in out_sizes)
         ring = self.ring
         if ring.data is None or need > ring.data.slot_bytes or not free:
@@ -223,8 +251,8 @@ class _RingDP:
         copy = []
         for i, (z, (m0, m1), a) in enumerate(zip(sizes, metas, at)):
             items[i, I_INSZ], items[i, I_M0], items[i, I_M1] = z, m0, m1
-            if a is not None:  # already in the ingest arena: every rank reads it there
-                items[i, I_IN], items[i, I_SRC] = a, 1
+            if a is not None:  # in the ingest arena / the source file: every rank reads it there
+                items[i, I_SRC], items[i, I_IN] = a
             else:
                 items[i, I_IN] = off
                 copy.append(i)
@@ -235,8 +263,13 @@ class _RingDP:
         if copy:
             gather_copy([data.base + base + int(items[i, I_IN]) for i in copy], [payloads[i] for i in copy],
                         [sizes[i] for i in copy], COPY_THREADS)
-        self.arena_items += n - len(copy)
+        nfile = sum(1 for a in at if a is not None and a[0] == SRC_FILE)
+        self.file_items += nfile
+        self.arena_items += n - len(copy) - nfile
         self.copied_items += len(copy)
+        self._path = path
+        if path is not None:
+            ring.set_path(s, path)
         hdr = ring.header(s)
         hdr[:] = 0
         mask = 0
@@ -246,6 +279,7 @@ class _RingDP:
         hdr[H_MASK], hdr[H_PER], hdr[H_DRAW] = mask, per, int(draw)
         hdr[H_KEY:H_KEY + len(key)] = key
         hdr[H_CALIB] = int(calib)
+        hdr[H_FILE] = int(path is not None)
         ring.publish(s, seq)
         self._slot_use[s] = (seq, self._participants())
         return seq, s, items[:n].copy()
@@ -333,6 +367,7 @@ class _RingDP:
             if hdr[H_CALIB]:  # rank 0 calibrated its random-init weights: take them (every rank)
                 self._adopt_weights(hdr)
             mask = int(hdr[H_MASK])
+            self._path = ring.path(s) if hdr[H_FILE] else None
             if (mask >> self.info.rank) & 1:
                 data = ring.use_generation(int(hdr[H_GEN]), int(hdr[H_SLOT]))
                 items = ring.items(s)[:int(hdr[H_N])].copy()

@@ -56,12 +56,13 @@ class RosBag:
         self._w.write(topic, msg, t)
 
     def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0, alloc=None,
-                      readers: int = 0):
+                      readers: int = 0, mapped: bool = False):
         """``alloc(n)``: where large payloads are deserialised to (e.g. the DP ring's
         ``ingest_buffer``); None keeps ``bytes``.  ``readers``: threads that read uncompressed
-        chunks ahead into ``alloc`` buffers (0: the calling thread reads)."""
+        chunks ahead into ``alloc`` buffers (0: the calling thread reads).  ``mapped``: sensor
+        payloads stay in the file, as views of its read-only mapping (sharded DP replay)."""
         k = 0
-        for topic, m, t in rosbag_v2.read_messages(self._r, topics, alloc, readers):
+        for topic, m, t in rosbag_v2.read_messages(self._r, topics, alloc, readers, mapped):
             k += 1
             if k <= start_seq:
                 continue
@@ -117,7 +118,7 @@ class TcaBag:
             yield msgpack.unpackb(self._f.read(n), raw=False)
 
     def read_messages(self, topics: Optional[Sequence[str]] = None, start_seq: int = 0,
-                      alloc=None, readers: int = 0) -> Iterator[Tuple[str, object, msgs.Time]]:
+                      alloc=None, readers: int = 0, mapped: bool = False) -> Iterator[Tuple[str, object, msgs.Time]]:
         """Yields (topic, msg, t).  ``start_seq`` resumes a replay after the
         first ``start_seq`` matching messages."""
         k = 0

@@ -180,10 +180,12 @@ class RosBagWriter:
 
 class RosBagReader:
     def __init__(self, path: str):
+        self.path = os.path.abspath(path)
         self.f = open(path, "rb")
         if self.f.read(len(MAGIC)) != MAGIC:
             raise ValueError(f"{path}: not a ROS bag v2.0")
         self.conns: Dict[int, Connection] = {}
+        self.mm = None
 
     def _read_record(self, f, alloc=None) -> Optional[Tuple[Dict[str, bytes], bytes]]:
         """``alloc``: an uncompressed chunk is read straight into ``alloc(n)`` (the DP ring's
@@ -338,6 +340,101 @@ class RosBagReader:
                 yield self.conns[cid], _read_time(h["time"]), data
             # bag header, index data, chunk info: nothing to replay
 
+    def mapping(self):
+        """The bag file's read-only shared mapping (made on first use; random access advice,
+        so touching a message's first page does not read its payload ahead)."""
+        if self.mm is None:
+            import mmap
+            self.mm = mmap.mmap(self.f.fileno(), 0, access=mmap.ACCESS_READ)
+            try:
+                self.mm.madvise(mmap.MADV_RANDOM)
+            except (AttributeError, OSError):
+                pass
+            from ..parallel.host_ring import FileMaps
+            FileMaps.register(self.path, self.mm)
+        return self.mm
+
+    WINDOW = 64  # messages parsed per native call batch (per type) in mapped_messages
+
+    def mapped_messages(self, topics: Optional[Sequence[str]] = None) -> Iterator[Tuple[Connection, msgs.Time, object]]:
+        """(connection, time, message) in file order, with the sensor messages' payloads left in
+        the file: each ``data`` is a view of :meth:`mapping` and nothing of it is read until a
+        consumer touches it.  One native pass (``tca_bag_index``) walks the top-level records and
+        the records inside uncompressed chunks; windows of up to :attr:`WINDOW` messages are
+        parsed with one native call per message type (``rosmsg.deserialize_many``).  So this
+        reads only record headers and message prefixes.  Sharded data-parallel replay
+        (``parallel/ring_dp.py``): rank 0 orders and publishes these messages, and every rank
+        reads its own shard's payloads from its own mapping of the file.  Compressed chunks
+        (and hosts without the runtime library) take the ordinary path."""
+        import numpy as np
+
+        rt = rosmsg._native_rt()
+        if rt is None or not hasattr(rt, "tca_bag_index"):
+            for c, t, data in self.raw_messages():
+                if not topics or c.topic in topics:
+                    yield c, t, self.decode(c, data)
+            return
+        mm = self.mapping()
+        mv = memoryview(mm)
+        base = np.frombuffer(mm, np.uint8).ctypes.data if len(mm) else 0
+        want = None if not topics else set(topics)
+        cap = 1024
+        cols = [np.empty(cap, t) for t in (np.int32, np.int32, np.uint32, np.uint32, np.int64, np.int64, np.int64,
+                                           np.int64)]
+        ptrs = [c.ctypes.data for c in cols]
+        state = np.array([len(MAGIC), 0], np.int64)
+        pending: List[Tuple[Connection, msgs.Time, int, int]] = []
+        conns = self.conns
+
+        def flush():
+            if not pending:
+                return []
+            groups: Dict[str, List[int]] = {}
+            for i, (c, _, _, _) in enumerate(pending):
+                groups.setdefault(c.type, []).append(i)
+            parsed: List[object] = [None] * len(pending)
+            for typ, idx in groups.items():
+                ms = rosmsg.deserialize_many([mv[pending[i][2]:pending[i][2] + pending[i][3]] for i in idx], typ,
+                                             zero_copy=True)
+                for i, m in zip(idx, ms):
+                    parsed[i] = m
+            out = [(c, t, m) for (c, t, _, _), m in zip(pending, parsed)]
+            pending.clear()
+            return out
+        while True:
+            k = int(rt.tca_bag_index(base, len(mm), state.ctypes.data, cap, *ptrs))
+            if k < 0:
+                raise ValueError(f"{self.path}: malformed record near byte {int(state[0])}")
+            if k == 0:
+                break
+            ops, cids, secs, nsecs, hoffs, hlens, doffs, dlens = (c[:k].tolist() for c in cols)
+            for i in range(k):
+                o = ops[i]
+                if o == OP_MSG:
+                    c = conns[cids[i]]
+                    if want is not None and c.topic not in want:
+                        continue
+                    t = msgs.Time(secs[i], nsecs[i])
+                    if c.type in rosmsg.NATIVE_TYPES:
+                        pending.append((c, t, doffs[i], dlens[i]))
+                        if len(pending) >= self.WINDOW:
+                            yield from flush()
+                    else:
+                        yield from flush()
+                        yield c, t, self.decode(c, mv[doffs[i]:doffs[i] + dlens[i]])
+                elif o == OP_CONNECTION:
+                    if cids[i] not in conns:
+                        h0 = hoffs[i]
+                        self._conn(_parse_fields(bytes(mv[h0:h0 + hlens[i]])), bytes(mv[doffs[i]:doffs[i] + dlens[i]]))
+                elif o == OP_CHUNK:  # compressed: the ordinary path
+                    yield from flush()
+                    h = _parse_fields(bytes(mv[hoffs[i]:hoffs[i] + hlens[i]]))
+                    blob = self._decompress(h["compression"].decode(), bytes(mv[doffs[i]:doffs[i] + dlens[i]]))
+                    for c, t, data in self._iter_payload(blob):
+                        if want is None or c.topic in want:
+                            yield c, t, self.decode(c, data)
+        yield from flush()
+
     @staticmethod
     def decode(conn: Connection, data: bytes, alloc=None):
         if conn.type in rosmsg.DEFS:
@@ -347,6 +444,14 @@ class RosBagReader:
         return RawMessage(conn.type, conn.md5sum, data)
 
     def close(self) -> None:
+        if self.mm is not None:
+            from ..parallel.host_ring import FileMaps
+            FileMaps.unregister(self.mm)
+            try:
+                self.mm.close()
+            except BufferError:  # messages still view the file: the mapping goes with them
+                pass
+            self.mm = None
         self.f.close()
 
 
@@ -355,9 +460,15 @@ def is_rosbag(path: str) -> bool:
         return f.read(len(MAGIC)) == MAGIC
 
 
-def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None, readers: int = 0):
+def read_messages(reader: RosBagReader, topics: Optional[Sequence[str]] = None, alloc=None, readers: int = 0,
+                  mapped: bool = False):
     """``alloc``: see :func:`rosmsg.deserialize` (large payloads written into caller buffers);
-    ``readers``: threads reading uncompressed chunks ahead into ``alloc`` buffers."""
+    ``readers``: threads reading uncompressed chunks ahead into ``alloc`` buffers;
+    ``mapped``: payloads stay in the file (:meth:`RosBagReader.mapped_messages`)."""
+    if mapped:
+        for c, m, t in ((c, m, t) for c, t, m in reader.mapped_messages(topics)):
+            yield c.topic, m, t
+        return
     for c, t, data in reader.raw_messages(alloc, readers):
         if topics and c.topic not in topics:
             continue

@@ -308,7 +308,16 @@ def deserialize(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]
     """``alloc(n)``: optional destination for large uint8 arrays (a writable buffer of n
     bytes, or None to keep ``bytes``); the message's field then views that buffer.
     ``zero_copy``: large uint8 arrays are views of ``data`` itself (which the message
-    then keeps alive)."""
+    then keeps alive).  Image / CompressedImage / PointCloud2 go through the native parse
+    (:func:`deserialize_many`) when the runtime library is built."""
+    if msg_type in NATIVE_TYPES and _native_rt() is not None:
+        return deserialize_many([data], msg_type, alloc, zero_copy)[0]
+    return deserialize_py(data, msg_type, alloc, zero_copy)
+
+
+def deserialize_py(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]] = None, zero_copy: bool = False):
+    """The schema-driven Python reader (every registered type; the reference semantics the
+    native parse is tested against)."""
     mv = memoryview(data)
     _TLS.alloc = _ZERO_COPY if zero_copy else alloc
     try:
@@ -318,3 +327,100 @@ def deserialize(data: bytes, msg_type: str, alloc: Optional[Callable[[int], Any]
     if off != len(data):
         raise ValueError(f"{msg_type}: {len(data) - off} trailing bytes")
     return msg
+
+
+# ------------------------------------------------------------------ native batch parse (sensor messages)
+NATIVE_TYPES = {"sensor_msgs/Image": 1, "sensor_msgs/CompressedImage": 2, "sensor_msgs/PointCloud2": 3}
+COPY_THREADS = 8  # threads of one batch's payload copy into caller buffers
+_STR_CACHE: Dict[bytes, str] = {}
+_FIELDS_CACHE: Dict[bytes, List[msgs.PointField]] = {}
+
+
+def _native_rt():
+    try:
+        from .. import _native
+        return _native.runtime(auto_build=False)
+    except Exception:  # noqa: BLE001 - no runtime library: the Python reader below stays exact
+        return None
+
+
+def _str(a, o: int, n: int) -> str:
+    b = a[o:o + n].tobytes()
+    s = _STR_CACHE.get(b)
+    if s is None:
+        s = b.decode("utf-8", "replace")
+        if len(_STR_CACHE) < 4096:
+            _STR_CACHE[b] = s
+    return s
+
+
+def _point_fields(a, o: int, e: int) -> List[msgs.PointField]:
+    b = a[o:e].tobytes()
+    f = _FIELDS_CACHE.get(b)
+    if f is None:
+        f, _ = _read(memoryview(b), 0, Field("PointField[]", "fields", "sensor_msgs"))
+        if len(_FIELDS_CACHE) < 256:
+            _FIELDS_CACHE[b] = f
+    return [msgs.PointField(x.name, x.offset, x.datatype, x.count) for x in f]
+
+
+def deserialize_many(datas, msg_type: str, alloc: Optional[Callable[[int], Any]] = None, zero_copy: bool = False,
+                     threads: int = COPY_THREADS) -> list:
+    """Deserialise a batch of ``sensor_msgs/Image`` / ``CompressedImage`` / ``PointCloud2``
+    wire buffers with one native parse (``tca_ros_parse``, csrc/runtime/ros_wire.cpp) and one
+    multi-threaded payload copy (``tca_host_gather_copy``), both outside the GIL.  Same
+    result as :func:`deserialize` per message: ``alloc`` puts payloads of ``ALLOC_MIN`` bytes
+    or more into caller buffers (the DP ingest arena), ``zero_copy`` makes every payload a
+    view of its input (a mapped bag file: nothing is read until a consumer touches it)."""
+    import numpy as np
+
+    t = NATIVE_TYPES.get(msg_type)
+    rt = _native_rt() if t is not None else None
+    if rt is None:
+        return [deserialize_py(d, msg_type, alloc, zero_copy) for d in datas]
+    n = len(datas)
+    if n == 0:
+        return []
+    arrs = [np.frombuffer(d, np.uint8) for d in datas]
+    ptrs = np.fromiter((a.ctypes.data for a in arrs), np.uint64, n)
+    lens = np.fromiter((a.size for a in arrs), np.int64, n)
+    meta = np.empty((n, 16), np.int64)
+    rc = rt.tca_ros_parse(t, n, ptrs.ctypes.data, lens.ctypes.data, meta.ctypes.data)
+    if rc != 0:
+        if rc > 0:  # the Python reader names what is wrong with that message
+            deserialize_py(datas[rc - 1], msg_type)
+        raise ValueError(f"{msg_type}: message {rc - 1} does not parse")
+    rows = meta.tolist()
+    out = []
+    cd, cs, cn = [], [], []
+    for i, m in enumerate(rows):
+        a = arrs[i]
+        do, dl = m[11], m[12]
+        data = None
+        if zero_copy and dl >= ALLOC_MIN:
+            data = memoryview(datas[i])[do:do + dl]
+        elif alloc is not None and dl >= ALLOC_MIN:
+            buf = alloc(dl)
+            if buf is not None:
+                cd.append(buf.ctypes.data)
+                cs.append(int(ptrs[i]) + do)
+                cn.append(dl)
+                data = memoryview(buf)
+        if data is None:
+            data = a[do:do + dl].tobytes()
+        hdr = msgs.Header(m[0], msgs.Time(m[1], m[2]), _str(a, m[3], m[4]))
+        if t == 1:
+            out.append(msgs.Image(hdr, m[5], m[6], _str(a, m[7], m[8]), m[9], m[10], data))
+        elif t == 2:
+            out.append(msgs.CompressedImage(hdr, _str(a, m[5], m[6]), data))
+        else:
+            out.append(msgs.PointCloud2(hdr, m[5], m[6], _point_fields(a, m[7], m[8]), bool(m[9]), m[10], m[13],
+                                        data, bool(m[14])))
+    if cd:
+        k = len(cd)
+        d_ = np.asarray(cd, np.uint64)
+        s_ = np.asarray(cs, np.uint64)
+        n_ = np.asarray(cn, np.int64)
+        if rt.tca_host_gather_copy(k, d_.ctypes.data, s_.ctypes.data, n_.ctypes.data, int(threads)) != 0:
+            raise ValueError("tca_host_gather_copy: bad arguments")
+    return out
