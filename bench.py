@@ -162,6 +162,32 @@ class _Split:
         return self.fn()
 
 
+def _preflight(info, dev, rccl_ranks: int, comm_used: str) -> dict:
+    """Before the first step on N GPUs: every rank's peer access to every other visible GPU
+    (``hipDeviceCanAccessPeer``: RCCL's xGMI p2p path), the communicator's rank count, and
+    every rank's NUMA placement (``parallel/numa.py`` describe + the CPUs it runs on), gathered
+    to rank 0 and printed into the result's ``config``."""
+    from triton_client_amd.parallel import numa
+
+    n = torch.cuda.device_count()
+    me = dev.index if dev.index is not None else 0
+    peers = {j: bool(torch.cuda.can_device_access_peer(me, j)) for j in range(n) if j != me}
+    d = numa.describe(info.local_rank)
+    mine = {"rank": info.rank, "device": me, "gpu_pci": d["gpu_pci"], "numa_node": d["numa_node"],
+            "cpus_allowed": len(os.sched_getaffinity(0)), "gpu_local_cpus": d["local_cpus"],
+            "binding": d["reason"], "peer_access": peers}
+    every = [mine]
+    if info.world > 1:
+        import torch.distributed as dist
+        every = [None] * info.world
+        dist.all_gather_object(every, mine)
+    ranks_dev = sorted({e["device"] for e in every})
+    pairs = [(e["device"], j) for e in every for j in ranks_dev if j != e["device"]]
+    ok = all(e["peer_access"].get(j, False) for e in every for j in ranks_dev if j != e["device"])
+    return {"ranks": every, "peer_pairs_checked": len(pairs), "peer_access_all_pairs": ok if pairs else None,
+            "rccl_comm_ranks": rccl_ranks, "comm": comm_used}
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -387,6 +413,7 @@ def main():
         rccl_ranks = dist.get_world_size() if dist.get_backend() == "nccl" else 0
     if info.world > 1 and not gloo_rehearsal and rccl_ranks != args.gpus:
         raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
+    preflight = _preflight(info, dev, rccl_ranks, comm_used)
     ex = FrameExchange(info, native=native)
     # with the native RCCL communicator the detection gather (grouped send / recv of fixed-shape
     # result buffers) is stream work: it is captured inside the step graph(s), so a step is one
@@ -813,6 +840,7 @@ def main():
                 "lidar_sweeps_per_frame": args.sweeps if (use_lid and cp) else None,
                 "distinct_frames_per_rank": nd,
                 "rccl_ranks": rccl_ranks,
+                "preflight": preflight,
                 "vs_reference_equivalent_emulation": round(fps / REFERENCE_EQUIVALENT_FPS, 2),
                 "ingest": args.ingest,
                 "camera_input": args.camera_input if use_cam else None,

@@ -16,11 +16,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _CHILD = r"""
 import json, os
 from triton_client_amd.parallel import numa
-before = len(os.sched_getaffinity(0))
+allowed = set(os.sched_getaffinity(0))
+local = numa.gpu_cpus(0)
+before = len(allowed)
 info = numa.describe(0)
 got = numa.bind_to_gpu(0)
-print(json.dumps({"info": info, "before": before, "after": len(os.sched_getaffinity(0)),
-                  "applied": None if got is None else len(got)}))
+after = set(os.sched_getaffinity(0))
+print(json.dumps({"info": info, "before": before, "after": len(after),
+                  "applied": None if got is None else len(got),
+                  "already_local": local is not None and allowed <= local,
+                  "after_local": local is not None and after <= local}))
 """
 
 
@@ -31,9 +36,19 @@ def test_numa_binding_on_the_box(cuda):
     assert out.returncode == 0, out.stderr
     r = json.loads(out.stdout.strip().splitlines()[-1])
     print(json.dumps(r))
+    keep = os.environ.get("GRAFT_REPO_ROOT")
+    if keep:  # the box's answer, kept with the run's outputs
+        os.makedirs(os.path.join(keep, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(keep, "gpurun_out", "numa_describe.json"), "w") as f:
+            json.dump(r, f, indent=1)
     info = r["info"]
     assert info["kfd_gpus"] + info["pci_gpus"] > 0 and info["gpu_pci"], r
     if info["would_bind"]:
         assert r["applied"] == r["after"] == info["would_bind"] < r["before"], r
     else:
         assert r["after"] == r["before"] and info["reason"], r
+    if info["numa_node"] is not None and info["numa_node"] >= 0:
+        # a GPU with a NUMA node: afterwards the process runs on that node's CPUs only -- by a
+        # shrink, or because its cpuset was already inside them (checked on the sets, not a string)
+        assert r["after_local"], r
+        assert r["after"] < r["before"] or r["already_local"], r

@@ -172,7 +172,44 @@ def test_main_default_flags_remote_on_device(cuda, served, tmp_path, monkeypatch
         assert abs(ng - total) <= max(2, total // 10) and ok >= 0.85 * ng, (ok, ng, total)
 
 
-def test_main3d_default_flags_remote_on_device(cuda, served, tmp_path, monkeypatch):
+@pytest.mark.parametrize("wire", ["devshm", "shm"])
+def test_main_shared_memory_wire_on_device(cuda, served, tmp_path, monkeypatch, wire):
+    """``main.py -m YOLOv5nCOCO --wire devshm|shm``: the device path runs on the shared-memory
+    wires (K1 writes the model input into the registered region, the server writes the output
+    back there; devshm: a GPU allocation shared by HIP IPC handle, K3/K4 read the output in
+    place) and publishes the CPU client's detections."""
+    from triton_client_amd.cli import main as main2d, record
+    from triton_client_amd.inference import remote_live
+
+    cam = str(tmp_path / "cam.bag")
+    assert record.main([cam, "--frames", "6", "--cam", "720x1280", "--raw"]) == 0
+    params = tmp_path / "p.yaml"
+    params.write_text(yaml.safe_dump({"grpc_channel": served.target, "sub_topic": "/camera/color/image_raw",
+                                      "pub_topic": "/det", "gt_topic": "/gt"}))
+    calls = []
+    orig = remote_live.RemoteLiveCamera._rpc_shm
+
+    def counted(self, x, n):
+        calls.append((self.det.wire, n))
+        return orig(self, x, n)
+
+    monkeypatch.setattr(remote_live.RemoteLiveCamera, "_rpc_shm", counted)
+    base = ["-m", "YOLOv5nCOCO", "--params", str(params), "--play", cam, "--spin-timeout", "120"]
+    gpu = _run_main(main2d, base + ["--wire", wire], ["/det", "/det/detections"])
+    assert len(calls) == 6 and {w for w, _ in calls} == {wire}
+    cpu = _run_main(main2d, base + ["--device", "cpu"], ["/det", "/det/detections"])
+    g, c = _dets_by_seq(gpu["/det/detections"]), _dets_by_seq(cpu["/det/detections"])
+    assert sorted(g) == sorted(c) and len(g) == 6
+    assert sum(len(v) for v in c.values()) > 6
+    for s in c:
+        assert g[s].shape == c[s].shape, s
+        np.testing.assert_array_equal(g[s][:, 5], c[s][:, 5])
+        np.testing.assert_allclose(g[s][:, 4], c[s][:, 4], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g[s][:, :4], c[s][:, :4], atol=0.05)
+
+
+@pytest.mark.parametrize("wire", ["raw", "devshm"])
+def test_main3d_default_flags_remote_on_device(cuda, served, tmp_path, monkeypatch, wire):
     """``main3d.py -m pointpillar_kitti`` with default flags: the client unpacks and
     voxelises on the GPU (K6 + K7) and publishes the CPU client's boxes."""
     from triton_client_amd.cli import main3d, record
@@ -194,7 +231,7 @@ def test_main3d_default_flags_remote_on_device(cuda, served, tmp_path, monkeypat
     monkeypatch.setattr(PointpillarPreprocess, "filter_cloud_gpu", counted)
     base = ["-m", "pointpillar_kitti", "--params", str(params), "--play", pc, "--spin-timeout", "120",
             "--labels", "all", "--score-thresh", "0"]
-    gpu = _run_main(main3d, base, ["/det3d"])
+    gpu = _run_main(main3d, base + ["--wire", wire], ["/det3d"])
     assert calls == ["cuda"] * 3
     cpu = _run_main(main3d, base + ["--device", "cpu"], ["/det3d"])
     assert len(calls) == 3

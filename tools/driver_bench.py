@@ -95,7 +95,8 @@ def main():
                          "with YOLOv5nCOCO + pointpillar_kitti on the same GPU")
     ap.add_argument("--mode", choices=["sync", "async"], default="sync",
                     help="remote: RPC mode (sync = the reference's blocking ModelInfer; async = -a)")
-    ap.add_argument("--wire", choices=["raw", "proto"], default="raw", help="remote: request codec")
+    ap.add_argument("--wire", choices=["raw", "proto", "shm", "devshm"], default="raw",
+                    help="remote: request codec / transport (shm, devshm: shared-memory regions, server on this node)")
     a = ap.parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:  # self-launch (a child: nothing has touched the GPU)
         import socket
@@ -281,6 +282,7 @@ def _remote(a, H, W):
             n, dt, ok = _run(bus, "/cam", "/cam_out", msgs.Image, ms[warm:], window, a.timeout)
             drv.stop()
             live = eng.live()
+            eng.release_transport()
             out["camera"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
                              "device_path": live is not None and live.stats["frames"] > 0,
                              "input": f"CompressedImage JPEG {W}x{H} q90", "output": "annotated Image + Detection2DArray",
@@ -301,6 +303,7 @@ def _remote(a, H, W):
             st.sum.clear(), st.n.clear()
             n, dt, ok = _run(bus, "/pc", "/pc_out", msgs.BoundingBoxArray, ms[warm:], window, a.timeout)
             drv.stop()
+            eng.release_transport()
             out["lidar"] = {"messages": n, "complete": ok, "seconds": round(dt, 3), "msgs_per_s": round(n / dt, 1),
                             "device_voxeliser": str(getattr(eng.pre, "device", "cpu")),
                             "input": f"PointCloud2 {ms[0].width} points x {ms[0].point_step} B",

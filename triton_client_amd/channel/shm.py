@@ -9,6 +9,7 @@ from __future__ import annotations
 import mmap
 import os
 import uuid
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -49,6 +50,13 @@ class DeviceShmRegion:
         self.alloc.close()
 
 
+def _unlink_quiet(path: str) -> None:
+    try:
+        os.unlink(path)
+    except FileNotFoundError:
+        pass
+
+
 class ShmRegion:
     def register(self, channel) -> None:
         channel.register_system_shared_memory(self.key, self.key, self.byte_size)
@@ -67,6 +75,8 @@ class ShmRegion:
         finally:
             os.close(fd)
         self.pinned = _host_register(self.mm, self.byte_size) if pin else False
+        # a region nobody closed still leaves no file behind in /dev/shm (at GC or interpreter exit)
+        self._unlink = weakref.finalize(self, _unlink_quiet, self.path)
 
     def view(self, offset: int, dtype, shape) -> np.ndarray:
         dt = np.dtype(dtype)
@@ -86,10 +96,9 @@ class ShmRegion:
             pass
         self.mm = None
         if unlink:
-            try:
-                os.unlink(self.path)
-            except FileNotFoundError:
-                pass
+            self._unlink()
+        else:
+            self._unlink.detach()
 
     def __enter__(self):
         return self

@@ -58,9 +58,11 @@ def add_framework_flags(p: argparse.ArgumentParser, params_default: str, three_d
                         "re-published in header.seq order); 1 = the reference's one frame per callback")
     g.add_argument("--live-workers", type=int, default=1,
                    help="live topic: micro-batches in flight (host work of one overlaps another's GPU work)")
-    g.add_argument("--wire", choices=["raw", "proto", "shm"], default="raw",
+    g.add_argument("--wire", choices=["raw", "proto", "shm", "devshm"], default="raw",
                    help="raw: C++ zero-copy KServe codec; proto: reference-style protobuf request; shm: KServe "
-                        "system shared memory (server on the same host; tensors stay in a /dev/shm region)")
+                        "system shared memory (server on the same host; tensors stay in a /dev/shm region); "
+                        "devshm: KServe device shared memory (server on the same GPU node; the model input and "
+                        "outputs stay in a GPU allocation the server maps by HIP IPC handle -- needs --device cuda)")
     g.add_argument("--timeout", type=float, default=None, help="per-RPC deadline (s); default none")
     g.add_argument("--retries", type=int, default=2, help="retries on UNAVAILABLE/DEADLINE_EXCEEDED")
     g.add_argument("--weights", default=None, help="state_dict for the local engine: path, file://, http(s):// or s3:// URI (loaded with torch.load weights_only)")

@@ -54,6 +54,8 @@ def main(argv=None) -> int:
         play_bag(flags.play, bus, topics=[params["sub_topic"]])
     drv.start_inference(spin=True, timeout=flags.spin_timeout)
     drv.stop()
+    if hasattr(engine, "release_transport"):  # a remote client's shared-memory regions
+        engine.release_transport()
     export_if_asked(flags, engine)
     if info is not None:
         engine.close()

@@ -684,6 +684,16 @@ def _device_output_to_host(a: torch.Tensor, conf_thres: float) -> np.ndarray:
 
 
 class _RemoteBase:
+    def release_transport(self) -> None:
+        """Unregister and free the shared-memory regions this client registered with the server
+        (its own and its device path's): the drivers call it when they stop."""
+        live = getattr(self, "_live", None)
+        if live is not None and hasattr(live, "close"):
+            live.close()
+        close = getattr(self, "close_shm", None)
+        if close is not None:
+            close()
+
     def __init__(self, channel, client, mode: str = "sync", wire: str = "raw", window: int = 8):
         if mode not in ("sync", "async", "stream"):
             raise ValueError(f"mode {mode!r}")
@@ -816,9 +826,11 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
     def live(self):
         """The drivers' device path on a GPU client (``inference/remote_live.py``):
         GPU JPEG decode, K1 preprocess, one KServe request per frame, K3/K4 on the
-        response, GPU annotation, zero-copy publish.  None on a CPU client (config 1)
-        and for the shared-memory wires, which keep :meth:`detect`."""
-        if self.device.type != "cuda" or self.wire not in ("raw", "proto"):
+        response, GPU annotation, zero-copy publish.  None on a CPU client (config 1).
+        The shared-memory wires run it too: ``shm`` with the model input / outputs in a
+        page-locked /dev/shm region, ``devshm`` with both in a device allocation the server maps
+        by HIP IPC handle, so no tensor crosses host memory."""
+        if self.device.type != "cuda":
             return None
         if getattr(self, "_live", None) is None:
             from .remote_live import RemoteLiveCamera
@@ -868,12 +880,8 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
         return a, xf
 
     # ------------------------------------------------------------ shared memory
-    def _shm_setup(self):
-        """Client shm region of `window` slots (input tensor + requested outputs
-        each), registered with the server once."""
-        if getattr(self, "_shm", None) is not None:
-            return self._shm
-        from ..channel.shm import ShmRegion
+    def _shm_layout(self):
+        """One request's slot: (slot bytes, input shape, input dtype, [(output, offset, bytes)])."""
         from ..proto import KSERVE_TO_NP
 
         def nbytes(shape, dt):
@@ -893,6 +901,14 @@ class RemoteDetector2D(_RemoteBase, Detector2D):
             b = nbytes(shape, KSERVE_TO_NP[md[n].datatype])
             layout.append((n, off, b))
             off += align(b)
+        return off, in_shape, in_dt, layout
+
+    def _shm_setup(self):
+        """Client shm region of `window` slots (input tensor + requested outputs
+        each), registered with the server once."""
+        if getattr(self, "_shm", None) is not None:
+            return self._shm
+        off, in_shape, in_dt, layout = self._shm_layout()
         region = _new_region(self.wire, off * self.window, self.device)
         region.register(self.channel)
         self._shm = (region, off, in_shape, in_dt, layout)

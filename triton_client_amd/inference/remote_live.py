@@ -25,6 +25,14 @@ steps to the client's GPU:
   (``tca_draw_annotations``), one D2H of the annotated frames into page-locked
   memory the published ``Image`` wraps without a copy.
 
+Shared-memory wires (``--wire shm`` / ``devshm``, reference
+``communicator/channel/grpc_channel.py:26-30,73-78`` for the RPC it replaces): K1 writes
+each frame's model input straight into its slot of the client's registered region and the
+request carries only region references; the server writes the outputs back into the same
+slot.  With ``devshm`` the region is a device allocation the server maps by HIP IPC handle:
+the input never leaves the GPU, and K3/K4 read the decoded YOLOv5 output where the server
+wrote it -- no tensor crosses host memory.
+
 Several driver workers may call :meth:`RemoteLiveCamera.process` at once: ingest,
 preprocess and the RPCs of one batch overlap another's; only the postprocess +
 annotation (which share the postprocess workspaces) is serialised.
@@ -113,6 +121,111 @@ class RemoteLiveCamera:
         self.lock = threading.Lock()       # postprocess workspaces + annotation
         self._mk = threading.Lock()        # ingest table
         self.stats = {"frames": 0, "batches": 0}
+        self._tl = threading.local()       # shared-memory wires: each worker thread's own region
+        self._regions: list = []
+
+    # ------------------------------------------------------------------ shared-memory wires
+    def _region(self, n: int):
+        """This thread's registered region of >= n request slots (input + requested outputs each)."""
+        from .engines import _new_region
+        st = getattr(self._tl, "shm", None)
+        if st is None or st[-1] < n:
+            d = self.det
+            if st is not None:
+                try:
+                    st[0].unregister(d.channel)
+                finally:
+                    st[0].close()
+                    self._regions.remove(st[0])
+            slot, in_shape, in_dt, layout = d._shm_layout()
+            nslots = max(n, 8)
+            region = _new_region(d.wire, slot * nslots, self.device)
+            region.register(d.channel)
+            self._regions.append(region)
+            st = self._tl.shm = (region, slot, in_shape, in_dt, layout, nslots)
+        return st
+
+    def close(self) -> None:
+        """Unregister and free every worker's shared-memory region."""
+        for r in self._regions:
+            try:
+                r.unregister(self.det.channel)
+            except Exception:  # noqa: BLE001 - the server may be gone already
+                pass
+            r.close()
+        self._regions = []
+        self._tl = threading.local()
+
+    @staticmethod
+    def _slots(region, slot: int, off: int, dtype, shape, n: int) -> torch.Tensor:
+        """[n, *shape] view of the same tensor in n consecutive slots of a device region."""
+        tdt = torch.from_numpy(np.empty(0, np.dtype(dtype))).dtype
+        isz = np.dtype(dtype).itemsize
+        base = region.alloc.tensor.view(tdt)
+        inner = [int(np.prod(shape[i + 1:], dtype=np.int64)) for i in range(len(shape))]
+        return base.as_strided((n,) + tuple(shape), (slot // isz,) + tuple(inner), off // isz)
+
+    def _rpc_shm(self, x: torch.Tensor, n: int):
+        """Model inputs [n, ...] on the GPU -> their slots; one request per frame carrying
+        only region references; -> (region, slot, layout) once every response is in."""
+        from ..channel.shm import shm_params
+        from ..proto import service_pb2 as pb
+
+        d = self.det
+        region, slot, in_shape, in_dt, layout, _ = self._region(n)
+        tdt = d._TORCH_OF.get(d.dtype, torch.float32)
+        with trace_range("remote_shm_input"):
+            xs = x.to(tdt).reshape((n,) + tuple(in_shape))
+            if d.wire == "devshm":
+                self._slots(region, slot, 0, in_dt, in_shape, n).copy_(xs)  # device to device, one kernel
+            else:
+                for k in range(n):  # D2H into the page-locked mapping
+                    torch.from_numpy(region.view(k * slot, in_dt, in_shape)).copy_(xs[k], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()  # complete before the server reads it
+        ch = d.channel
+        nin = int(np.prod(in_shape)) * np.dtype(in_dt).itemsize
+        futs = []
+        for k in range(n):
+            req = pb.ModelInferRequest(model_name=ch.model_name, model_version=ch.model_version, id=str(k))
+            t = req.inputs.add(name=d.input_name, datatype=d.dtype, shape=list(in_shape))
+            shm_params(t, region.key, k * slot, nin)
+            for name, o, b in layout:
+                shm_params(req.outputs.add(name=name), region.key, k * slot + o, b)
+            futs.append(ch._grpc_stub.ModelInferRaw.future(req.SerializeToString(), timeout=ch.timeout_s))
+        resps = [pb.ModelInferResponse.FromString(f.result()) for f in futs]
+        return region, slot, layout, resps
+
+    def _post_shm(self, region, slot: int, layout, resps, n: int, xf):
+        """Detections from the outputs the server wrote into the slots."""
+        from ..channel.wire import ParsedResponse
+        from ..proto import KSERVE_TO_NP
+        from .engines import _device_output_to_host
+
+        d = self.det
+        post = d.post
+        offs = {name: o for name, o, _ in layout}
+        t0 = resps[0].outputs[0] if resps and len(resps[0].outputs) else None
+        if (d.wire == "devshm" and t0 is not None and len(resps[0].outputs) == 1 and t0.datatype == "FP32"
+                and len(t0.shape) == 3 and int(t0.shape[0]) == 1 and hasattr(post, "_post")
+                and all(tuple(r.outputs[0].shape) == tuple(t0.shape) for r in resps)):
+            # YOLOv5: K3 + K4 read the decoded output in the device region (one D2D gather of the slots)
+            N, no = int(t0.shape[1]), int(t0.shape[2])
+            pred = self._slots(region, slot, offs[t0.name], np.float32, (N, no), n).contiguous()
+            pp = post._post(no - 5, d.conf_thres, d.iou_thres, None, False, False, 300, self.device)
+            return pp.filter_decoded(pred, xf)
+        prs = []
+        for k, r in enumerate(resps):
+            pr = ParsedResponse()
+            pr.model_name = r.model_name
+            for t in r.outputs:
+                a = region.view(k * slot + offs[t.name], KSERVE_TO_NP[t.datatype], tuple(t.shape))
+                if isinstance(a, torch.Tensor):
+                    a = _device_output_to_host(a, d.conf_thres)
+                pr.outputs[t.name] = a
+                pr.datatypes[t.name] = t.datatype
+                pr.order.append(t.name)
+            prs.append(pr)
+        return self._post(prs, xf)
 
     # ------------------------------------------------------------------ pieces
     def _key(self, m):
@@ -181,15 +294,27 @@ class RemoteLiveCamera:
     # ------------------------------------------------------------------ one batch
     def run(self, key, batch: Sequence, draw: bool, names: Tuple[str, ...]) -> List[tuple]:
         n, (H, W) = len(batch), key[1]
+        d = self.det
         with trace_range("remote_ingest"):
             frames = self._ingest_for(key)(batch)
-        with trace_range("remote_preprocess"):
-            inputs, xf = self._model_input(frames)
-            torch.cuda.current_stream(self.device).synchronize()  # the inputs are in host memory
-        with trace_range("remote_rpc"):
-            responses = self._rpc(inputs)
+        if d.wire in ("shm", "devshm"):
+            with trace_range("remote_preprocess"):
+                x, xf = preprocess(frames, (d.h, d.w), d.mode2d, d.scaling, torch.float32,
+                                   "NHWC" if d.nhwc else "NCHW")
+                if d.nhwc:
+                    x = x.permute(0, 2, 3, 1)
+            with trace_range("remote_rpc"):
+                region, slot, layout, resps = self._rpc_shm(x, n)
+            post_fn = lambda: self._post_shm(region, slot, layout, resps, n, xf)  # noqa: E731
+        else:
+            with trace_range("remote_preprocess"):
+                inputs, xf = self._model_input(frames)
+                torch.cuda.current_stream(self.device).synchronize()  # the inputs are in host memory
+            with trace_range("remote_rpc"):
+                responses = self._rpc(inputs)
+            post_fn = lambda: self._post(responses, xf)  # noqa: E731
         with getattr(self.det.post, "lock", self.lock), trace_range("remote_postprocess"):
-            res = self._post(responses, xf)
+            res = post_fn()
             if draw:
                 draw_annotations_(frames, res.box, res.score, res.cls, res.count, self._names_dev(names),
                                   thickness=self.thickness)
