@@ -5,7 +5,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${TAG:-ab}
 RUNS=${RUNS:-2}
-mkdir -p $R/gpurun_out/r5
+mkdir -p $R/gpurun_out/r5 $R/gpurun_out/r6
 cd $R
 if [ -n "$TESTS" ]; then
   timeout -k 10 400 python -u -m pytest $TESTS -x -q -m gpu ${KSEL:+-k "$KSEL"} --timeout 200 --timeout-method thread > gpurun_out/r5/${TAG}_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r5/${TAG}_tests.log; exit 1; }
