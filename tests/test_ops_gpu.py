@@ -575,3 +575,73 @@ def test_copy_segments_kernel(cuda):
     for d, s, n in segs:
         ref[d:d + n] = src[s:s + n]
     assert torch.equal(dst, ref)
+
+
+@pytest.mark.parametrize("vcfg", [KITTI_PILLARS, KITTI_SECOND_VOXELS])
+@pytest.mark.parametrize("hash_mode", ["auto", "1"])
+def test_voxelize_gpu_exact_ring_order(cuda, vcfg, hash_mode, monkeypatch):
+    """Points in sensor (ring / azimuth) order: long runs of consecutive points in one cell, so
+    the run-aggregated atomics (voxelize.hip wave_run: one atomicMin / count / cursor reservation
+    per run) carry most points.  Runs cross wave boundaries, are cut by out-of-range points, and
+    the LiDAR sweep of the bench is order-exact against the spconv golden too."""
+    from triton_client_amd.utils.synthetic import LidarSpec, lidar_sweep
+    if hash_mode != "auto":
+        monkeypatch.setattr(lidar_ops, "VOX_HASH_FORCE", hash_mode)
+    cfg = dataclasses.replace(vcfg, max_voxels=20000)
+    nf = cfg.num_point_features
+    sweeps = []
+    for b in range(2):
+        p = lidar_sweep(LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23), 20 + b)
+        p = p[~np.isnan(p).any(1)]
+        p[:, 2] += 1.5
+        sweeps.append(p)
+    rng = np.random.default_rng(3)
+    r = np.asarray(cfg.point_cloud_range, np.float32)
+    runs = np.repeat(rng.uniform(r[:3], r[3:], size=(300, 3)).astype(np.float32), rng.integers(1, 150, 300), 0)
+    runs[::97] = r[3:] + 5  # out of range: cuts a run
+    ordered = np.concatenate([runs, np.zeros((len(runs), 1), np.float32)], 1)
+    sweeps.append(ordered)
+    B, N = len(sweeps), max(len(p) for p in sweeps)
+    pts = np.zeros((B, N, nf), np.float32)
+    cnt = np.array([len(p) for p in sweeps], np.int32)
+    for b, p in enumerate(sweeps):
+        pts[b, :len(p), :4] = p
+    vox = Voxelizer(cfg, B, N, device=cuda, nfeat=nf)
+    for rep in range(2):
+        v, c, n, vc = vox(torch.from_numpy(pts).to(cuda), torch.from_numpy(cnt).to(cuda))
+        torch.cuda.synchronize()
+        for b in range(B):
+            rv, rcoord, rn, _ = voxelize_np(pts[b, :cnt[b]], cfg, nf)
+            k = int(vc[b])
+            assert k == len(rn) and k > 100
+            np.testing.assert_array_equal(c[b, :k, 1:].cpu().numpy(), rcoord)
+            np.testing.assert_array_equal(n[b, :k].cpu().numpy(), rn)
+            np.testing.assert_array_equal(v[b, :k].cpu().numpy(), rv)
+
+
+@pytest.mark.parametrize("shift", [0, 4, 1])
+@pytest.mark.parametrize("out_stride", [4, 5])
+def test_pc2_unpack_gpu_alignments(cuda, shift, out_stride):
+    """The xyzi float32 fast paths (one 16-B load per point with the frame 16-B aligned, dword
+    loads when 4-B aligned, byte loads otherwise) and the 16-B output store give the CPU
+    unpack's points."""
+    clouds = [synth_cloud(n, seed=s) for n, s in ((7000, 4), (3, 5), (20001, 6))]
+    blobs, offs, o = [], [], 0
+    for c in clouds:
+        pad = bytes(shift)
+        blobs.append(pad + c.tobytes())
+        offs.append(o + shift)
+        o += len(pad) + c.nbytes
+    d = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8)
+    ns = np.array([len(c) for c in clouds], np.int32)
+    offs = np.asarray(offs, np.int64)
+    ref, rc = pc2_unpack(None, d, torch.from_numpy(offs), torch.from_numpy(ns), PointLayout.xyzi_f32(), 32768,
+                         True, 1.5, out_stride=out_stride)
+    ws = Workspace(cuda)
+    got, gc = pc2_unpack(ws, d.to(cuda), torch.from_numpy(offs).to(cuda), torch.from_numpy(ns).to(cuda),
+                         PointLayout.xyzi_f32(), 32768, True, 1.5, out_stride=out_stride)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gc.cpu().numpy(), rc.numpy())
+    for b in range(3):
+        n = int(rc[b])
+        np.testing.assert_allclose(got[b, :n].cpu().numpy(), ref[b, :n].numpy(), rtol=1e-6, atol=1e-7)

@@ -103,6 +103,38 @@ def served(cuda):
     srv.stop()
 
 
+@pytest.fixture(scope="module")
+def served_proc(cuda):
+    """The same models in a server PROCESS: device shared memory maps the client's allocation by
+    HIP IPC handle, which a process cannot open on its own allocation."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from triton_client_amd.channel.grpc_channel import GRPCChannel
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    srv = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+                            str(port), "--models", "YOLOv5nCOCO,pointpillar_kitti", "--device", "cuda",
+                            "--metrics-port", "0"], cwd=root)
+
+    class F:
+        model_name, model_version, batch_size = "YOLOv5nCOCO", "", 1
+
+    class S:
+        target = f"127.0.0.1:{port}"
+    try:
+        GRPCChannel({"grpc_channel": S.target}, F(), wait_ready_s=240.0).close()
+        yield S
+    finally:
+        srv.terminate()
+        srv.wait(60)
+
+
 def _run_main(mod, argv, topics):
     """Run an entry point on the in-process topic bus; -> {topic: [messages]}."""
     from triton_client_amd.ros import default_bus, reset_default_bus
@@ -173,7 +205,7 @@ def test_main_default_flags_remote_on_device(cuda, served, tmp_path, monkeypatch
 
 
 @pytest.mark.parametrize("wire", ["devshm", "shm"])
-def test_main_shared_memory_wire_on_device(cuda, served, tmp_path, monkeypatch, wire):
+def test_main_shared_memory_wire_on_device(cuda, served, served_proc, tmp_path, monkeypatch, wire):
     """``main.py -m YOLOv5nCOCO --wire devshm|shm``: the device path runs on the shared-memory
     wires (K1 writes the model input into the registered region, the server writes the output
     back there; devshm: a GPU allocation shared by HIP IPC handle, K3/K4 read the output in
@@ -184,7 +216,8 @@ def test_main_shared_memory_wire_on_device(cuda, served, tmp_path, monkeypatch, 
     cam = str(tmp_path / "cam.bag")
     assert record.main([cam, "--frames", "6", "--cam", "720x1280", "--raw"]) == 0
     params = tmp_path / "p.yaml"
-    params.write_text(yaml.safe_dump({"grpc_channel": served.target, "sub_topic": "/camera/color/image_raw",
+    srv = served_proc if wire == "devshm" else served
+    params.write_text(yaml.safe_dump({"grpc_channel": srv.target, "sub_topic": "/camera/color/image_raw",
                                       "pub_topic": "/det", "gt_topic": "/gt"}))
     calls = []
     orig = remote_live.RemoteLiveCamera._rpc_shm
@@ -194,8 +227,20 @@ def test_main_shared_memory_wire_on_device(cuda, served, tmp_path, monkeypatch, 
         return orig(self, x, n)
 
     monkeypatch.setattr(remote_live.RemoteLiveCamera, "_rpc_shm", counted)
+    errs = []
+    orig_run = remote_live.RemoteLiveCamera.run
+
+    def run(self, *a, **k):  # the bus thread swallows callback errors: keep them for the assert
+        try:
+            return orig_run(self, *a, **k)
+        except BaseException as e:
+            errs.append(e)
+            raise
+    monkeypatch.setattr(remote_live.RemoteLiveCamera, "run", run)
     base = ["-m", "YOLOv5nCOCO", "--params", str(params), "--play", cam, "--spin-timeout", "120"]
     gpu = _run_main(main2d, base + ["--wire", wire], ["/det", "/det/detections"])
+    if errs:
+        raise errs[0]
     assert len(calls) == 6 and {w for w, _ in calls} == {wire}
     cpu = _run_main(main2d, base + ["--device", "cpu"], ["/det", "/det/detections"])
     g, c = _dets_by_seq(gpu["/det/detections"]), _dets_by_seq(cpu["/det/detections"])
@@ -209,7 +254,7 @@ def test_main_shared_memory_wire_on_device(cuda, served, tmp_path, monkeypatch, 
 
 
 @pytest.mark.parametrize("wire", ["raw", "devshm"])
-def test_main3d_default_flags_remote_on_device(cuda, served, tmp_path, monkeypatch, wire):
+def test_main3d_default_flags_remote_on_device(cuda, served, served_proc, tmp_path, monkeypatch, wire):
     """``main3d.py -m pointpillar_kitti`` with default flags: the client unpacks and
     voxelises on the GPU (K6 + K7) and publishes the CPU client's boxes."""
     from triton_client_amd.cli import main3d, record
@@ -218,7 +263,7 @@ def test_main3d_default_flags_remote_on_device(cuda, served, tmp_path, monkeypat
     pc = str(tmp_path / "pc.bag")
     assert record.main([pc, "--frames", "3", "--no-camera", "--lidar"]) == 0
     params = tmp_path / "p3.yaml"
-    params.write_text(yaml.safe_dump({"grpc_channel": served.target,
+    params.write_text(yaml.safe_dump({"grpc_channel": (served_proc if wire == "devshm" else served).target,
                                       "sub_topic": "/ai_test_field/sensors/os_cloud_node/points",
                                       "pub_topic": "/det3d", "gt_topic": "/gt"}))
     calls = []

@@ -131,3 +131,45 @@ def test_bag_scan_matches_python_walker(tmp_path):
         assert arr["conn"][i] == c.id and (arr["sec"][i], arr["nsec"][i]) == (t.secs, t.nsecs)
         assert blob[arr["doff"][i]:arr["doff"][i] + arr["dlen"][i]] == bytes(data)
     assert rt.tca_bag_scan(b.ctypes.data, len(blob) - 3, cap, *[arr[n].ctypes.data for n in arr]) == -1
+
+
+def test_rospy_anymsg_ingest_into_arena(monkeypatch):
+    """With a real ROS master (faked here: rospy is not installed), a data-parallel driver's
+    subscriber takes the raw wire bytes (``rospy.AnyMsg``) and deserialises them natively with
+    the payload in the ingest arena; other types / no arena keep the typed subscription."""
+    _rt()
+    from triton_client_amd.ros import compat
+
+    subs = []
+
+    class AnyMsg:
+        pass
+
+    class _Sub:
+        def __init__(self, topic, t, cb, queue_size=None):
+            subs.append((topic, t, cb))
+
+    FakeRospy = type("FakeRospy", (), {"AnyMsg": AnyMsg, "Subscriber": _Sub})
+
+    monkeypatch.setattr(compat, "HAVE_ROSPY", True)
+    monkeypatch.setattr(compat, "_rospy", FakeRospy)
+    arena = np.zeros(1 << 22, np.uint8)
+    used = []
+
+    def ingest(n):
+        used.append(n)
+        return arena[:n]
+    got = []
+    compat.Subscriber("/cam", msgs.CompressedImage, got.append, ingest=ingest)
+    compat.Subscriber("/dets", msgs.Detection2DArray, got.append, ingest=ingest)
+    compat.Subscriber("/cam2", msgs.CompressedImage, got.append)
+    assert [t for _, t, _ in subs] == [AnyMsg, msgs.Detection2DArray, msgs.CompressedImage]
+    payload = bytes(range(256)) * 600  # >= ALLOC_MIN
+    raw = AnyMsg()
+    raw._buff = rosmsg.serialize(msgs.Image(msgs.Header(7, msgs.Time(1, 2), "cam"), 200, 256, "rgb8", 0, 768,
+                                            payload))
+    raw._connection_header = {"type": "sensor_msgs/Image"}
+    subs[0][2](raw)
+    m = got[-1]
+    assert isinstance(m, msgs.Image) and m.header.seq == 7 and bytes(m.data) == payload
+    assert used == [len(payload)] and np.frombuffer(m.data, np.uint8).ctypes.data == arena.ctypes.data

@@ -84,7 +84,8 @@ class RosInference(BaseInference):
                                            batch=self.batch, workers=self.workers,
                                            capacity=max(self.queue_size or 0, 2 * self.batch * self.workers))
             cb, qs = self.runner.push, None  # the window is the (latest-wins) queue
-        self.sub = compat.Subscriber(p["sub_topic"], msgs.CompressedImage, cb, queue_size=qs, bus=self.bus)
+        self.sub = compat.Subscriber(p["sub_topic"], msgs.CompressedImage, cb, queue_size=qs, bus=self.bus,
+                                     ingest=getattr(self.engine, "ingest_buffer", None))
         if spin:
             compat.spin(self.bus, timeout)
 

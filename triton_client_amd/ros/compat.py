@@ -60,11 +60,37 @@ def logerr(msg, *a):
     (_rospy.logerr if HAVE_ROSPY else log.error)(msg, *a)
 
 
+def _raw_ingest(msg_type, callback, ingest):
+    """rospy ``AnyMsg`` callback: the wire bytes of an Image / CompressedImage / PointCloud2 parsed
+    by the native ROS parser (csrc/runtime/ros_wire.cpp, GIL released) with the payload copied
+    straight into ``ingest(n)`` buffers -- the data-parallel ring's ingest arena -- instead of
+    genpy's per-field Python deserialiser building a ``bytes`` payload that the ring then copies
+    again."""
+    from . import rosmsg
+
+    def cb(raw):
+        # the publisher's actual type (AnyMsg keeps the connection header): an Image topic
+        # subscribed as CompressedImage is parsed as what it is
+        hdr = getattr(raw, "_connection_header", None) or {}
+        return callback(rosmsg.deserialize(raw._buff, hdr.get("type", msg_type), alloc=ingest))
+    return cb
+
+
 class Subscriber:
-    def __init__(self, topic: str, msg_type, callback, queue_size: Optional[int] = None, bus=None):
+    def __init__(self, topic: str, msg_type, callback, queue_size: Optional[int] = None, bus=None, ingest=None):
+        """``ingest(n)``: with a real ROS master, sensor messages are received as raw bytes
+        (``rospy.AnyMsg``) and deserialised natively with their payloads in ``ingest`` buffers
+        (the data-parallel drivers pass the host ring's ``ingest_buffer``)."""
         self.topic = topic
         if HAVE_ROSPY and bus is None:
-            self._impl = _rospy.Subscriber(topic, msg_type, callback, queue_size=queue_size)
+            from . import rosmsg
+            name = msg_type if isinstance(msg_type, str) else (getattr(msg_type, "_type", None)
+                                                               or rosmsg.TYPE_OF.get(msg_type))
+            if ingest is not None and name in rosmsg.NATIVE_TYPES:
+                cb = _raw_ingest(name, callback, ingest)
+                self._impl = _rospy.Subscriber(topic, _rospy.AnyMsg, cb, queue_size=queue_size)
+            else:
+                self._impl = _rospy.Subscriber(topic, msg_type, callback, queue_size=queue_size)
             self._bus = None
         else:
             self._bus = bus or default_bus()
