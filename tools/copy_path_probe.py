@@ -14,7 +14,6 @@ them:
 
     rocprofv3 --kernel-trace --memory-copy-trace --stats -d out -- python tools/copy_path_probe.py
 """
-import ctypes
 import mmap
 import os
 import sys
@@ -42,7 +41,7 @@ def main() -> int:
     os.close(fd)
     reg = _host_register(mm, total)
     shm = np.frombuffer(mm, np.uint8)
-    out = {"registered": bool(reg)}
+    out = {"registered": bool(reg)}  # the mapping stays registered until the process exits
     try:
         d = {k: torch.empty(v, dtype=torch.uint8, device=dev) for k, v in SIZES.items()}
         pin = {k: torch.empty(SIZES[k], dtype=torch.uint8).pin_memory() for k in "AF"}
@@ -69,8 +68,6 @@ def main() -> int:
             out[k] = {"bytes": SIZES[k], "us": round(dt * 1e6, 1), "GBps": round(SIZES[k] / dt / 1e9, 1)}
             print(k, out[k], flush=True)
     finally:
-        if reg:
-            torch.cuda.cudart().cudaHostUnregister(ctypes.c_void_p(ctypes.addressof(ctypes.c_char.from_buffer(mm))))
         del shm
         try:
             mm.close()
