@@ -26,6 +26,11 @@ constexpr int kPtsPerBlock = kPtsPerThread * kBlock;
 struct FieldDesc {
   int off[4];    // byte offset of x, y, z, intensity inside a point record
   int dtype[4];  // sensor_msgs/PointField datatype codes (1..8)
+  // 1: every field float32 at a 4-B aligned offset and step % 4 == 0 (dword loads, not byte loads);
+  // 2: in addition x, y, z, intensity are the 16 B at offsets 0 / 4 / 8 / 12 and step % 16 == 0 (one
+  // 16-B load per point: the Ouster / Velodyne xyzi record).  The frame's byte offset must be as
+  // aligned, checked per block.
+  int fast;
 };
 
 __device__ __forceinline__ float load_field(const uint8_t* rec, int off, int dt) {
@@ -42,11 +47,27 @@ __device__ __forceinline__ float load_field(const uint8_t* rec, int off, int dt)
   }
 }
 
-__device__ __forceinline__ bool load_point(const uint8_t* base, int i, int step, const FieldDesc& fd, float* v) {
+__device__ __forceinline__ bool load_point(const uint8_t* base, int i, int step, const FieldDesc& fd, float* v,
+                                           int fast) {
   const uint8_t* rec = base + (long)i * step;
+  if (fast == 2) {
+    const float4 q = *reinterpret_cast<const float4*>(rec);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else if (fast == 1) {
 #pragma unroll
-  for (int f = 0; f < 4; ++f) v[f] = load_field(rec, fd.off[f], fd.dtype[f]);
+    for (int f = 0; f < 4; ++f) v[f] = *reinterpret_cast<const float*>(rec + fd.off[f]);
+  } else {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) v[f] = load_field(rec, fd.off[f], fd.dtype[f]);
+  }
   return !(isnan(v[0]) || isnan(v[1]) || isnan(v[2]) || isnan(v[3]));
+}
+
+// the fast path this frame can take: its byte offset must keep the records aligned
+__device__ __forceinline__ int frame_fast(const FieldDesc& fd, long off) {
+  if (fd.fast == 2 && (off & 15) == 0) return 2;
+  if (fd.fast >= 1 && (off & 3) == 0) return 1;
+  return 0;
 }
 
 __global__ void __launch_bounds__(kBlock) pc2_count_kernel(const uint8_t* __restrict__ data,
@@ -59,15 +80,17 @@ __global__ void __launch_bounds__(kBlock) pc2_count_kernel(const uint8_t* __rest
   const int b = blockIdx.y, blk = blockIdx.x;
   const int n = frame_n[b];
   const uint8_t* base = data + frame_off[b];
+  const int fast = frame_fast(fd, frame_off[b]);
   int cnt = 0;
   float mx = -INFINITY;
-  const int first = blk * kPtsPerBlock + threadIdx.x * kPtsPerThread;
+  // consecutive lanes read consecutive points (coalesced): point i = first + k * kBlock
+  const int first = blk * kPtsPerBlock + threadIdx.x;
 #pragma unroll
   for (int k = 0; k < kPtsPerThread; ++k) {
-    const int i = first + k;
+    const int i = first + k * kBlock;
     if (i < n) {
       float v[4];
-      if (load_point(base, i, step, fd, v)) { ++cnt; mx = fmaxf(mx, v[3]); }
+      if (load_point(base, i, step, fd, v, fast)) { ++cnt; mx = fmaxf(mx, v[3]); }
     }
   }
   cnt = wave_sum(cnt);
@@ -117,11 +140,12 @@ __global__ void __launch_bounds__(kBlock) pc2_compact_kernel(const uint8_t* __re
   float v[kPtsPerThread][4];
   bool ok[kPtsPerThread];
   int cnt = 0;
+  const int fast = frame_fast(fd, frame_off[b]);
   const int first = blk * kPtsPerBlock + threadIdx.x * kPtsPerThread;
 #pragma unroll
   for (int k = 0; k < kPtsPerThread; ++k) {
     const int i = first + k;
-    ok[k] = i < n && load_point(base, i, step, fd, v[k]);
+    ok[k] = i < n && load_point(base, i, step, fd, v[k], fast);
     cnt += ok[k];
   }
   int total;
@@ -133,11 +157,15 @@ __global__ void __launch_bounds__(kBlock) pc2_compact_kernel(const uint8_t* __re
     if (!ok[k]) continue;
     if (pos < max_points) {
       float* o = ob + (long)pos * out_stride;
-      o[0] = v[k][0];
-      o[1] = v[k][1];
-      o[2] = v[k][2] + z_offset;
-      o[3] = v[k][3] * inv;
-      for (int f = 4; f < out_stride; ++f) o[f] = 0.f;  // e.g. zero time-lag column (voxelize.py:38-39)
+      if (out_stride == 4) {  // one 16-B store
+        *reinterpret_cast<float4*>(o) = make_float4(v[k][0], v[k][1], v[k][2] + z_offset, v[k][3] * inv);
+      } else {
+        o[0] = v[k][0];
+        o[1] = v[k][1];
+        o[2] = v[k][2] + z_offset;
+        o[3] = v[k][3] * inv;
+        for (int f = 4; f < out_stride; ++f) o[f] = 0.f;  // e.g. zero time-lag column (voxelize.py:38-39)
+      }
     }
     ++pos;
   }
@@ -154,7 +182,16 @@ TCA_API int tca_pc2_unpack(const void* data, const long* frame_off, const int* f
   if (batch <= 0) return 0;
   if (out_stride < 4) return (int)hipErrorInvalidValue;
   FieldDesc fd;
-  for (int f = 0; f < 4; ++f) { fd.off[f] = field_off[f]; fd.dtype[f] = field_dtype[f]; }
+  bool f32 = (point_step & 3) == 0;
+  for (int f = 0; f < 4; ++f) {
+    fd.off[f] = field_off[f];
+    fd.dtype[f] = field_dtype[f];
+    f32 = f32 && field_dtype[f] == 7 && (field_off[f] & 3) == 0 && field_off[f] + 4 <= point_step;
+  }
+  fd.fast = !f32 ? 0
+            : (field_off[0] == 0 && field_off[1] == 4 && field_off[2] == 8 && field_off[3] == 12 &&
+               (point_step & 15) == 0) ? 2 : 1;
+  if (((uintptr_t)out & 15) != 0 && out_stride == 4) return (int)hipErrorInvalidValue;  // 16-B stores
   const int bpf = (max_points + kPtsPerBlock - 1) / kPtsPerBlock;
   int e = zero_i32_async((int*)frame_imax, batch, stream);
   if (e) return e;

@@ -69,21 +69,50 @@ __device__ __forceinline__ int cell_of(const float* p, const VoxGeom& g, int& cx
   return (cz * g.ny + cy) * g.nx + cx;
 }
 
+// Runs of equal keys in consecutive lanes.  A sensor's points arrive ring by ring in azimuth
+// order, so neighbouring points mostly fall into the same pillar (at 10 m, ~5 consecutive points of
+// a 1875-step ring share a 16 cm pillar): one atomic per run instead of one per point.  key < 0:
+// no key (never part of a run).  head: the run's first lane (the smallest point index of the run);
+// len: the run's length (valid on the head); rank / head_lane: this lane's place in its run.
+struct Run {
+  bool head;
+  int len, rank, head_lane;
+};
+
+__device__ __forceinline__ Run wave_run(int key) {
+  const int lane = threadIdx.x & 63;
+  const int prev = __shfl_up(key, 1, 64);
+  Run r;
+  r.head = key >= 0 && (lane == 0 || prev != key);
+  const unsigned long long brk = __ballot(key < 0 || r.head);  // every run starts at a break
+  const unsigned long long after = lane == 63 ? 0ull : (brk >> (lane + 1));
+  r.len = after ? (__builtin_ctzll(after) + 1) : (64 - lane);
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  r.head_lane = 63 - __builtin_clzll(brk & upto);  // lane's own break or the last one before it
+  r.rank = lane - r.head_lane;
+  return r;
+}
+
 __global__ void __launch_bounds__(kBlock) vox_cell_kernel(const float* __restrict__ pts, int pstride, int max_pts,
                                                           const int* __restrict__ npts, VoxGeom g,
                                                           int* __restrict__ cell_first, int* __restrict__ point_cell) {
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= max_pts) return;
   int cell = -1;
-  if (i < npts[b]) {
+  if (i < max_pts && i < npts[b]) {
     const float* p = pts + ((long)b * max_pts + i) * pstride;
     int cx, cy, cz;
     cell = cell_of(p, g, cx, cy, cz);
-    if (cell >= 0 && g.keys) cell = hash_slot(g.keys + (long)b * g.cells, g.hbits, cell);
-    if (cell >= 0) atomicMin(&cell_first[(long)b * g.cells + cell], i);
   }
-  point_cell[(long)b * max_pts + i] = cell;
+  // the run head holds the run's smallest index: atomicMin of the others cannot change the cell
+  const Run r = wave_run(cell);
+  if (g.keys) {  // hash mode: the head claims the run's table slot
+    int slot = r.head ? hash_slot(g.keys + (long)b * g.cells, g.hbits, cell) : -1;
+    slot = __shfl(slot, r.head_lane, 64);
+    if (cell >= 0) cell = slot;
+  }
+  if (r.head) atomicMin(&cell_first[(long)b * g.cells + cell], i);
+  if (i < max_pts) point_cell[(long)b * max_pts + i] = cell;
 }
 
 __device__ __forceinline__ int first_flag(const int* pc, const int* cf, long cbase, int i, int n) {
@@ -260,11 +289,13 @@ __global__ void __launch_bounds__(kBlock) vox_count_kernel(const int* __restrict
                                                            const int* __restrict__ cell_vid, int max_voxels,
                                                            int* __restrict__ vcount) {
   const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npts[b] || i >= max_pts) return;
-  const int c = point_cell[(long)b * max_pts + i];
-  if (c < 0) return;
-  const int vid = cell_vid[(long)b * cells + c];
-  if (vid >= 0) atomicAdd(&vcount[(long)b * max_voxels + vid], 1);
+  int vid = -1;
+  if (i < npts[b] && i < max_pts) {
+    const int c = point_cell[(long)b * max_pts + i];
+    if (c >= 0) vid = cell_vid[(long)b * cells + c];
+  }
+  const Run r = wave_run(vid);  // one atomic per run of points in one voxel
+  if (r.head) atomicAdd(&vcount[(long)b * max_voxels + vid], r.len);
 }
 
 constexpr int kScanT = 1024;
@@ -272,29 +303,37 @@ constexpr int kScanT = 1024;
 __global__ void __launch_bounds__(kScanT) vox_scan_kernel(const int* __restrict__ voxel_count, int max_voxels,
                                                           const int* __restrict__ vcount, int* __restrict__ offs,
                                                           int* __restrict__ cursor, int* __restrict__ dense_count) {
+  // chunks of kScanT counts, one per thread, read and written coalesced; a block scan per chunk
   __shared__ int s_w[kScanT / 64];
+  __shared__ int s_carry;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int n = voxel_count[b];
-  const int per = (n + kScanT - 1) / kScanT;
-  const int lo = min(t * per, n), hi = min(lo + per, n);
   const int* vc = vcount + (long)b * max_voxels;
-  int sum = 0;
-  for (int v = lo; v < hi; ++v) sum += vc[v];
-  const int incl = wave_incl_sum(sum);
-  if (lane == 63) s_w[wid] = incl;
-  __syncthreads();
-  int wbase = 0;
-  for (int w = 0; w < wid; ++w) wbase += s_w[w];
-  int run = wbase + incl - sum;
   int* ob = offs + (long)b * (max_voxels + 1);
   int* cb = cursor + (long)b * max_voxels;
-  for (int v = lo; v < hi; ++v) {
-    ob[v] = run;
-    cb[v] = run;
-    run += vc[v];
+  if (t == 0) s_carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += kScanT) {
+    const int v = base + t;
+    const int x = v < n ? vc[v] : 0;
+    const int incl = wave_incl_sum(x);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    int wbase = s_carry;
+    for (int w = 0; w < wid; ++w) wbase += s_w[w];
+    const int excl = wbase + incl - x;
+    if (v < n) {
+      ob[v] = excl;
+      cb[v] = excl;
+    }
+    __syncthreads();  // every thread has read s_w and s_carry
+    if (t == kScanT - 1) s_carry = excl + x;
+    __syncthreads();
   }
-  if (t == kScanT - 1) ob[n] = run;
-  if (t == 0) dense_count[b] = 0;
+  if (t == 0) {
+    ob[n] = s_carry;
+    dense_count[b] = 0;
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) vox_fill_kernel(const int* __restrict__ point_cell, int max_pts,
@@ -302,13 +341,18 @@ __global__ void __launch_bounds__(kBlock) vox_fill_kernel(const int* __restrict_
                                                           const int* __restrict__ cell_vid, int max_voxels,
                                                           int* __restrict__ cursor, int* __restrict__ csr) {
   const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npts[b] || i >= max_pts) return;
-  const int c = point_cell[(long)b * max_pts + i];
-  if (c < 0) return;
-  const int vid = cell_vid[(long)b * cells + c];
-  if (vid < 0) return;
-  const int pos = atomicAdd(&cursor[(long)b * max_voxels + vid], 1);
-  csr[(long)b * max_pts + pos] = i;
+  int vid = -1;
+  if (i < npts[b] && i < max_pts) {
+    const int c = point_cell[(long)b * max_pts + i];
+    if (c >= 0) vid = cell_vid[(long)b * cells + c];
+  }
+  // one cursor atomic per run: the head reserves the run's positions, its lanes take them in order
+  // (a voxel's list is sorted by the next stage, so only the set of positions matters)
+  const Run r = wave_run(vid);
+  int base = 0;
+  if (r.head) base = atomicAdd(&cursor[(long)b * max_voxels + vid], r.len);
+  base = __shfl(base, r.head_lane, 64);
+  if (vid >= 0) csr[(long)b * max_pts + base + r.rank] = i;
 }
 
 __device__ __forceinline__ void cswap(int& a, int& b) {
@@ -400,14 +444,15 @@ __global__ void __launch_bounds__(256) vox_slot_reset_kernel(int max_voxels, int
                                                              int* __restrict__ num_points) {
   const int b = blockIdx.y;
   const int cpv = P >> 2;  // 16-B chunks per voxel
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  const int vid = t / cpv, c = t - vid * cpv;
-  if (vid >= voxel_count[b]) return;
-  const long g = (long)b * max_voxels + vid;
-  reinterpret_cast<int4*>(slots + g * P)[c] = make_int4(kEmpty, kEmpty, kEmpty, kEmpty);
-  if (c == 0) {
-    num_points[g] = min(vcount[g], P);
-    vcount[g] = 0;
+  const int n = voxel_count[b] * cpv;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {  // bounded grid
+    const int vid = t / cpv, c = t - vid * cpv;
+    const long g = (long)b * max_voxels + vid;
+    reinterpret_cast<int4*>(slots + g * P)[c] = make_int4(kEmpty, kEmpty, kEmpty, kEmpty);
+    if (c == 0) {
+      num_points[g] = min(vcount[g], P);
+      vcount[g] = 0;
+    }
   }
 }
 
@@ -416,9 +461,8 @@ __global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const 
                                                              int* __restrict__ cell_first, int* __restrict__ cell_vid,
                                                              int* __restrict__ keys) {
   const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= npts[b]) return;
-  const int c = point_cell[(long)b * max_pts + i];
-  if (c < 0) return;
+  const int c = i < npts[b] && i < max_pts ? point_cell[(long)b * max_pts + i] : -1;
+  if (!wave_run(c).head) return;  // one reset per run of points in one cell
   cell_first[(long)b * cells + c] = kEmpty;
   cell_vid[(long)b * cells + c] = -1;
   if (keys) keys[(long)b * cells + c] = -1;
@@ -471,7 +515,8 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
                                                       vcount, slots);
   }
   if ((mode & 2) && !gather && (P & 3) == 0) {
-    vox_slot_reset_kernel<<<dim3((max_voxels * (P / 4) + 255) / 256, batch), 256, 0, stream>>>(
+    const int need = (max_voxels * (P / 4) + 255) / 256;
+    vox_slot_reset_kernel<<<dim3(need < 32 ? need : 32, batch), 256, 0, stream>>>(
         max_voxels, P, voxel_count, vcount, slots, num_points);
     vox_cell_reset_kernel<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid,
                                                         g.keys);
