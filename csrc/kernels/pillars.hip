@@ -262,27 +262,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
 
   const int nv = batch * max_voxels;
   const int step = __builtin_amdgcn_readfirstlane((int)nwaves);
-  // The walk covers only the real pillars: j in [0, total) over the frames' voxel counts laid end
-  // to end (lane f holds frame f's exclusive prefix; batch <= 64), so no wave steps over the empty
-  // tail of a frame's max_voxels rows and no integer division finds the frame.
-  const int cnt_l = lane < batch ? voxel_count[lane] : 0;
-  const int incl_l = wave_incl_sum(cnt_l);
-  const int excl_l = incl_l - cnt_l;
-  const int total = __builtin_amdgcn_readlane(incl_l, 63);
-  auto locate = [&](int j, int& bb) {  // j -> global row b * max_voxels + local (nv past the end)
-    if (j >= total) {
-      bb = batch - 1;
-      return nv;
+  auto next_valid = [&](int vv) {
+    while (vv < nv) {
+      const int bb = (unsigned)vv / (unsigned)max_voxels;
+      if (vv - bb * max_voxels < voxel_count[bb]) break;
+      vv += step;
     }
-    bb = __builtin_popcountll(__ballot(lane < batch && excl_l <= j)) - 1;
-    return bb * max_voxels + (j - __shfl(excl_l, bb, 64));
+    return vv;
   };
   const bool vec4 = (pstride & 3) == 0;
   const int rs = min(r, P - 1);
   auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[(long)min(vv, nv - 1) * P + rs] : 0; };
-  auto gather = [&](int vv, int bb, int id, float (&q)[4]) {
+  auto gather = [&](int vv, int id, float (&q)[4]) {
     const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
     const bool real_ = r < min(vc_, P);
+    const int bb = (unsigned)min(vv, nv - 1) / (unsigned)max_voxels;
     const float* src = FROM_SLOTS ? pts + ((long)bb * max_pts + (real_ ? id : 0)) * pstride
                                   : voxels + ((long)min(vv, nv - 1) * P + rs) * 4;
     if (!FROM_SLOTS || vec4) {
@@ -298,27 +292,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
     co_ = *reinterpret_cast<const int4*>(coords + (long)vq * 4);
   };
   // the same three-deep load pipeline as the MFMA kernel
-  const int j0 = __builtin_amdgcn_readfirstlane((int)wave);
-  int b, bn, bnn;
-  int v = locate(j0, b);
-  int vn = locate(j0 + step, bn);
-  int vnn = locate(j0 + 2 * step, bnn);
-  int j3 = j0 + 3 * step;
+  int v = next_valid(__builtin_amdgcn_readfirstlane((int)wave));
+  int vn = v < nv ? next_valid(v + step) : nv;
+  int vnn = vn < nv ? next_valid(vn + step) : nv;
   float pc[4], pn[4];
-  gather(v, b, slot_of(v), pc);
-  gather(vn, bn, slot_of(vn), pn);
+  gather(v, slot_of(v), pc);
+  gather(vn, slot_of(vn), pn);
   int idx_nn = slot_of(vnn);
   int vc;
   int4 co;
   meta(v, vc, co);
   while (v < nv) {
+    const int b = (unsigned)v / (unsigned)max_voxels;
     const int n = __builtin_amdgcn_readfirstlane(min(vc, P));
-    int b3;
-    const int v3 = locate(j3, b3);
-    j3 += step;
+    const int v3 = vnn < nv ? next_valid(vnn + step) : nv;
     const int idx_3 = slot_of(v3);
     float pnn[4];
-    gather(vnn, bnn, idx_nn, pnn);
+    gather(vnn, idx_nn, pnn);
     int vc_n;
     int4 co_n;
     meta(vn, vc_n, co_n);
@@ -360,9 +350,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
     v = vn;
     vn = vnn;
     vnn = v3;
-    b = bn;
-    bn = bnn;
-    bnn = b3;
     idx_nn = idx_3;
     vc = vc_n;
     co = co_n;
@@ -409,7 +396,6 @@ int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, con
                const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
                uint8_t* occ, hipStream_t stream) {
   if (P > 32 || (dt != kBF16 && dt != kF32 && dt != kPair)) return (int)hipErrorInvalidValue;
-  if (batch > 64) return (int)hipErrorInvalidValue;  // the VALU kernel keeps one frame per lane
   if (P == 32) return launch_vfe_t<FROM_SLOTS, 32>(pts, pstride, max_pts, slots, vcount, voxels, num_points, coords,
                                                     voxel_count, batch, max_voxels, P, W, bias, g, canvas, feat_out,
                                                     dt, occ, stream);

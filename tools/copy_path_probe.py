@@ -41,7 +41,8 @@ def main() -> int:
     os.close(fd)
     reg = _host_register(mm, total)
     shm = np.frombuffer(mm, np.uint8)
-    out = {"registered": bool(reg)}  # the mapping stays registered until the process exits
+    out = {"registered": bool(reg)}
+    src_b = dst_e = None
     try:
         d = {k: torch.empty(v, dtype=torch.uint8, device=dev) for k, v in SIZES.items()}
         pin = {k: torch.empty(SIZES[k], dtype=torch.uint8).pin_memory() for k in "AF"}
@@ -68,7 +69,10 @@ def main() -> int:
             out[k] = {"bytes": SIZES[k], "us": round(dt * 1e6, 1), "GBps": round(SIZES[k] / dt / 1e9, 1)}
             print(k, out[k], flush=True)
     finally:
-        del shm
+        torch.cuda.synchronize()
+        if reg:  # unregister before the mapping goes: the runtime's exit path walks registered ranges
+            torch.cuda.cudart().cudaHostUnregister(int(shm.ctypes.data))
+        del src_b, dst_e, shm
         try:
             mm.close()
         except BufferError:

@@ -20,3 +20,15 @@ for k in $(seq 1 $RUNS); do
     echo "$L run $k: lidar $(tail -1 gpurun_out/r5/${TAG}_l_${L}_$k.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d[\"value\"], d[\"ms_per_step\"])") headline $(tail -1 gpurun_out/r5/${TAG}_h_${L}_$k.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d[\"value\"], d[\"ms_per_step\"])")"
   done
 done
+if [ -n "$STATS" ]; then  # same-box LiDAR step kernel tables of both builds
+  cd /tmp && export TMPDIR=/tmp && cd $R
+  for L in new base; do
+    if [ $L = base ]; then export TCA_KERNELS_LIB=$BASE; else unset TCA_KERNELS_LIB; fi
+    rm -rf /tmp/ab_sp
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/ab_sp -o run -- python bench.py --only lidar --steps 8 --warmup 3 > gpurun_out/r6/${TAG}_sp_$L.log 2>&1 || { echo PROF_FAILED $L; tail -20 gpurun_out/r6/${TAG}_sp_$L.log; exit 1; }
+    f=$(find /tmp/ab_sp -name "*kernel_trace.csv" | head -1)
+    python tools/step_stats.py $f --marker pc2_count --steps 6 > gpurun_out/r6/${TAG}_stats_$L.txt || exit 1
+    echo "== $L"; head -24 gpurun_out/r6/${TAG}_stats_$L.txt
+  done
+  unset TCA_KERNELS_LIB
+fi
