@@ -747,6 +747,7 @@ TCA_API int tca_conv_hx3p_uni(const float* in, int B, int H, int W, int Cin, int
 namespace {
 
 constexpr int UD_TY = 16, UD_TX = 64, UD_MAXR = 7;
+static_assert(UD_TX + 2 * UD_MAXR < 128, "u rows are walked 128 columns at a time");
 
 __global__ void __launch_bounds__(256) bev_uniform_depth_kernel(const unsigned char* __restrict__ occ, int H, int W,
                                                                  int Ho, int Wo, int maxd,
@@ -762,14 +763,21 @@ __global__ void __launch_bounds__(256) bev_uniform_depth_kernel(const unsigned c
   // the occupancy window once into LDS (coalesced byte rows; each canvas byte feeds up to 4 u
   // cells' 3 x 3 stride-2 windows), outside the canvas as occupied-free
   const int iy0 = 2 * (ty0 - R) - 1, ix0 = 2 * (tx0 - R) - 1, oy = 2 * ry + 1, ox = 2 * rx + 1;
-  for (int id = threadIdx.x; id < oy * ox; id += blockDim.x) {
-    const int r = id / ox, c = id - (id / ox) * ox;
-    const int iy = iy0 + r, ix = ix0 + c;
-    os[r * OX + c] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? oc[(long)iy * W + ix] : 0;
+  // rows by wave, columns by lane: no per-element integer division (a runtime divisor costs ~40
+  // VALU instructions per element)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int r = wv; r < oy; r += nw) {
+    const int iy = iy0 + r;
+    const bool row_in = (unsigned)iy < (unsigned)H;
+    for (int c = lane; c < ox; c += 64) {
+      const int ix = ix0 + c;
+      os[r * OX + c] = (row_in && (unsigned)ix < (unsigned)W) ? oc[(long)iy * W + ix] : 0;
+    }
   }
   __syncthreads();
-  for (int id = threadIdx.x; id < ry * rx; id += blockDim.x) {
-    const int ly = id / rx, lx = id - (id / rx) * rx;
+  for (int id = threadIdx.x; id < ry * 128; id += blockDim.x) {  // rx <= UD_TX + 2 * UD_MAXR < 128
+    const int ly = id >> 7, lx = id & 127;
+    if (lx >= rx) continue;
     const int Y = ty0 - R + ly, X = tx0 - R + lx;
     unsigned char good = 0;
     if (Y >= 0 && X >= 0 && Y < Ho && X < Wo) {

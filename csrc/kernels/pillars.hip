@@ -262,21 +262,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
 
   const int nv = batch * max_voxels;
   const int step = __builtin_amdgcn_readfirstlane((int)nwaves);
-  auto next_valid = [&](int vv) {
-    while (vv < nv) {
-      const int bb = (unsigned)vv / (unsigned)max_voxels;
-      if (vv - bb * max_voxels < voxel_count[bb]) break;
-      vv += step;
+  // Waves are spread over the frames (waves_per_frame of them each, frames b, b + fstep, ...), and
+  // a wave walks its frame's real pillars with a fixed stride: the scalar unit (one per CU, shared
+  // by the CU's 32 waves) no longer steps over the empty tail of every frame's max_voxels rows with
+  // an integer division per row -- that scalar work bounded the kernel (PMC: 2x the VALU count in
+  // SALU instructions, profiles/r6/vfe_pmc/).
+  const int wave_u = __builtin_amdgcn_readfirstlane((int)wave);
+  const int wpf = max(1, step / batch);
+  const int fstep = max(1, step / wpf);
+  const int loc0 = wave_u % wpf;
+  auto first_at = [&](int bb) {
+    while (bb < batch && loc0 >= voxel_count[bb]) bb += fstep;
+    return bb;
+  };
+  int cb = first_at(wave_u / wpf), cl = loc0;  // the next pillar this wave takes
+  auto take = [&](int& bb) {
+    bb = min(cb, batch - 1);
+    if (cb >= batch) return nv;
+    const int row = cb * max_voxels + cl;
+    cl += wpf;
+    if (cl >= voxel_count[cb]) {
+      cb = first_at(cb + fstep);
+      cl = loc0;
     }
-    return vv;
+    return row;
   };
   const bool vec4 = (pstride & 3) == 0;
   const int rs = min(r, P - 1);
-  auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[(long)min(vv, nv - 1) * P + rs] : 0; };
-  auto gather = [&](int vv, int id, float (&q)[4]) {
+  auto slot_of = [&](int vv) { return FROM_SLOTS ? slots[min(vv, nv - 1) * P + rs] : 0; };
+  auto gather = [&](int vv, int bb, int id, float (&q)[4]) {
     const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
     const bool real_ = r < min(vc_, P);
-    const int bb = (unsigned)min(vv, nv - 1) / (unsigned)max_voxels;
     const float* src = FROM_SLOTS ? pts + ((long)bb * max_pts + (real_ ? id : 0)) * pstride
                                   : voxels + ((long)min(vv, nv - 1) * P + rs) * 4;
     if (!FROM_SLOTS || vec4) {
@@ -289,26 +305,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
   auto meta = [&](int vv, int& vc_, int4& co_) {
     const int vq = min(vv, nv - 1);
     vc_ = FROM_SLOTS ? vcount[vq] : num_points[vq];
-    co_ = *reinterpret_cast<const int4*>(coords + (long)vq * 4);
+    co_ = *reinterpret_cast<const int4*>(coords + vq * 4);
   };
   // the same three-deep load pipeline as the MFMA kernel
-  int v = next_valid(__builtin_amdgcn_readfirstlane((int)wave));
-  int vn = v < nv ? next_valid(v + step) : nv;
-  int vnn = vn < nv ? next_valid(vn + step) : nv;
+  int b, bn, bnn;
+  int v = take(b);
+  int vn = take(bn);
+  int vnn = take(bnn);
   float pc[4], pn[4];
-  gather(v, slot_of(v), pc);
-  gather(vn, slot_of(vn), pn);
+  gather(v, b, slot_of(v), pc);
+  gather(vn, bn, slot_of(vn), pn);
   int idx_nn = slot_of(vnn);
   int vc;
   int4 co;
   meta(v, vc, co);
   while (v < nv) {
-    const int b = (unsigned)v / (unsigned)max_voxels;
     const int n = __builtin_amdgcn_readfirstlane(min(vc, P));
-    const int v3 = vnn < nv ? next_valid(vnn + step) : nv;
+    int b3;
+    const int v3 = take(b3);
     const int idx_3 = slot_of(v3);
     float pnn[4];
-    gather(vnn, idx_nn, pnn);
+    gather(vnn, bnn, idx_nn, pnn);
     int vc_n;
     int4 co_n;
     meta(vn, vc_n, co_n);
@@ -350,6 +367,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
     v = vn;
     vn = vnn;
     vnn = v3;
+    b = bn;
+    bn = bnn;
+    bnn = b3;
     idx_nn = idx_3;
     vc = vc_n;
     co = co_n;
@@ -371,9 +391,10 @@ __global__ void __launch_bounds__(256) canvas_clear_kernel(const int* __restrict
                                                            uint8_t* __restrict__ occ) {
   const int b = blockIdx.y;
   const int cpp = C * esize >> 4;
+  const int sh = __builtin_ctz(cpp);  // cpp is a power of two (checked by the launcher): no division
   const int n = voxel_count[b] * cpp;
   for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
-    const int vid = t / cpp, c = t - vid * cpp;
+    const int vid = t >> sh, c = t & (cpp - 1);
     const int* co = coords + ((long)b * max_voxels + vid) * 4;
     const long cell = ((long)b * ny + co[2]) * nx + co[3];
     canvas[cell * cpp + c] = make_uint4(0u, 0u, 0u, 0u);
@@ -498,12 +519,38 @@ int canvas_clear(const int* coords, const int* voxel_count, int batch, int max_v
   const int esize = (canvas_dtype == kF32 || canvas_dtype == kPair) ? 4 : 2;
   if ((C * esize) & 15 || (canvas_dtype != kBF16 && canvas_dtype != kF32 && canvas_dtype != kPair))
     return (int)hipErrorInvalidValue;
+  const int cpp = C * esize / 16;
+  if (cpp & (cpp - 1)) return (int)hipErrorInvalidValue;  // 16-B chunks per pillar: a power of two
   const int need = (max_voxels * (C * esize / 16) + 255) / 256;
   canvas_clear_kernel<<<dim3(need < 64 ? need : 64, batch), 256, 0, stream>>>(
       coords, voxel_count, max_voxels, nx, ny, C, esize, (uint4*)canvas, occ);
   TCA_LAUNCH_CHECK();
 }
+// Occupancy-gated canvas (every reader of the features skips unoccupied cells: the first BEV conv
+// gates its loads on occ): the previous frame's features may stay, only its occupancy bytes go.
+// One thread per pillar, a bounded grid per frame.
+__global__ void __launch_bounds__(256) occ_clear_kernel(const int* __restrict__ coords,
+                                                        const int* __restrict__ voxel_count, int max_voxels, int nx,
+                                                        int ny, uint8_t* __restrict__ occ) {
+  const int b = blockIdx.y;
+  const int n = voxel_count[b];
+  for (int vid = blockIdx.x * 256 + threadIdx.x; vid < n; vid += gridDim.x * 256) {
+    const int4 co = *reinterpret_cast<const int4*>(coords + ((long)b * max_voxels + vid) * 4);
+    occ[((long)b * ny + co.z) * nx + co.w] = 0;
+  }
+}
 }  // namespace
+
+// Clear only the occupancy bytes of the cells the previous frame wrote (see occ_clear_kernel).
+TCA_API int tca_pillar_occ_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx, int ny,
+                                 uint8_t* occ, hipStream_t stream) {
+  if (batch <= 0) return 0;
+  if (!occ) return (int)hipErrorInvalidValue;
+  const int need = (max_voxels + 255) / 256;
+  occ_clear_kernel<<<dim3(need < 16 ? need : 16, batch), 256, 0, stream>>>(coords, voxel_count, max_voxels, nx, ny,
+                                                                           occ);
+  TCA_LAUNCH_CHECK();
+}
 
 TCA_API int tca_pillar_canvas_clear(const int* coords, const int* voxel_count, int batch, int max_voxels, int nx,
                                     int ny, int C, void* canvas, int canvas_dtype, hipStream_t stream) {

@@ -445,8 +445,10 @@ __global__ void __launch_bounds__(256) vox_slot_reset_kernel(int max_voxels, int
   const int b = blockIdx.y;
   const int cpv = P >> 2;  // 16-B chunks per voxel
   const int n = voxel_count[b] * cpv;
+  const bool pow2 = (cpv & (cpv - 1)) == 0;
+  const int sh = __builtin_ctz(cpv);
   for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {  // bounded grid
-    const int vid = t / cpv, c = t - vid * cpv;
+    const int vid = pow2 ? t >> sh : t / cpv, c = t - vid * cpv;
     const long g = (long)b * max_voxels + vid;
     reinterpret_cast<int4*>(slots + g * P)[c] = make_int4(kEmpty, kEmpty, kEmpty, kEmpty);
     if (c == 0) {

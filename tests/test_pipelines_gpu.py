@@ -140,3 +140,28 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, blocks_front)
             assert n == int(g[2][b]), (name, b)
             assert torch.equal(r[0][b, :n], g[0][b, :n]), (name, b)
             assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)
+
+
+def test_lidar_occupancy_only_clear_matches_fresh_pipeline(cuda):
+    """With the fast plan's first conv gating its canvas loads on the occupancy bytes, a frame's
+    clear resets only the previous frame's occupancy (not its features): a pipeline that ran other
+    sweeps first gives exactly the detections and the (masked) dense canvas of a fresh one."""
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    la = LidarPipeline(batch=2, max_points=32768, device=cuda)
+    _load_lidar(la, spec, [5, 6])
+    la.calibrate_detection_density(500.0)
+    la.step()
+    assert la.enc.occ_gated and la.enc.pair
+    _load_lidar(la, spec, [7, 8])
+    ra = la.step()
+    lf = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
+    _load_lidar(lf, spec, [7, 8])
+    rf = lf.step()
+    torch.cuda.synchronize()
+    assert int(ra.count.min()) > 0
+    for a, f in zip((ra.box, ra.score, ra.count), (rf.box, rf.score, rf.count)):
+        assert torch.equal(a, f)
+    assert torch.equal(la.enc.canvas_nchw(), lf.enc.canvas_nchw())
+    # the old cells of frames 5 / 6 hold stale features: only the occupancy hides them
+    stale = (la.enc.occ == 0) & (la.enc.canvas.abs().amax(-1) > 0)
+    assert int(stale.sum()) > 0

@@ -65,6 +65,7 @@ _KERNEL_SIGS = {
     "tca_pillar_vfe_slots_occ": [P, I, I, P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P, P],
     "tca_pillar_vfe_voxels_occ": [P, P, P, P, I, I, I, P, P, P, P, I, I, P, P, I, P, P],
     "tca_pillar_canvas_clear_occ": [P, P, I, I, I, I, I, P, I, P, P],
+    "tca_pillar_occ_clear": [P, P, I, I, I, I, P, P],
     "tca_conv_nhwc": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, P],
     "tca_conv_nhwc_x3p": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P],

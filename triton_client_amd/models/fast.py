@@ -496,6 +496,13 @@ class FastBEV:
             if neck_head_supported(ups, si, cins, self.head, H0, W0):
                 self.neck = FusedNeckHead(ups, si, self.head, self.device)
 
+    def first_conv_gated(self) -> bool:
+        """The plan's only reader of the pillar canvas is its first conv, and (pair storage with the
+        occupancy bytes) that conv loads only occupied cells: a non-transposed conv of at most 32
+        taps over pairs takes an occupancy-gated kernel (ops/conv.py: s2sp, hx3s2, x3p_occ)."""
+        cv = self.blocks[0][0][0]
+        return bool(self.pair and not cv.transpose and cv.k * cv.k <= 32)
+
     def forward(self, canvas: NHWC):
         if self.pair and not canvas.pair:
             if self.canvas_pairs is None or self.canvas_pairs.t.shape != canvas.tensor().shape:

@@ -326,6 +326,10 @@ class PillarEncoder:
             # pair mode: per-cell occupancy bytes written by the scatter, cleared with the cells;
             # the first BEV conv skips the reads of unoccupied cells (most of the canvas)
             self.occ = None
+            # occupancy-gated: every reader of the canvas features skips unoccupied cells (the
+            # fast BEV plan's first conv gates its loads on occ), so a frame's clear resets only
+            # the occupancy bytes of the previous frame's cells (set_occ_gated)
+            self.occ_gated = False
             self._range = _carr(ctypes.c_float, cfg.point_cloud_range)
             self._vsize = _carr(ctypes.c_float, cfg.voxel_size)
 
@@ -342,15 +346,30 @@ class PillarEncoder:
             # the canvas was written without occupancy until now: mark nothing, the
             # first frame after the switch rewrites its cells (and the canvas was cleared by cells)
 
+    def set_occ_gated(self, gated: bool) -> None:
+        """The canvas's only feature reader gates on the occupancy bytes (pair storage with its
+        occupancy): clear just those per frame, not the 256 B of features of every old pillar.
+        Turning it off zeroes the canvas once (stale features outside the occupied cells)."""
+        gated = bool(gated) and self.pair and self.occ is not None
+        if self.occ_gated and not gated:
+            self.canvas.zero_()
+        self.occ_gated = gated
+
     def canvas_nhwc(self):
         from .conv import NHWC
         return NHWC(self.canvas, pair=self.pair, occ=self.occ if self.pair else None)
 
     def canvas_nchw(self) -> torch.Tensor:
+        """Dense fp32 view for the PyTorch modules (calibration, the non-fused path); with an
+        occupancy-gated canvas the unoccupied cells are masked to zero (a copy)."""
         if self.pair:
             from .conv import from_pairs
-            return from_pairs(self.canvas).permute(0, 3, 1, 2)
-        return self.canvas.permute(0, 3, 1, 2)  # channels_last view
+            c = from_pairs(self.canvas)
+        else:
+            c = self.canvas
+        if self.occ_gated:
+            c = c * self.occ[..., None].to(c.dtype)
+        return c.permute(0, 3, 1, 2)  # channels_last view
 
     def clear(self, vox: Voxelizer, stream=None) -> None:
         """Zero the cells written for the voxels currently in ``vox`` (call
@@ -361,7 +380,10 @@ class PillarEncoder:
         """coords [B, V, 4] (b, z, y, x), voxel_count [B]."""
         args = (_native.ptr(coords), _native.ptr(voxel_count), coords.shape[0], coords.shape[1], self.nx, self.ny,
                 self.C, _native.ptr(self.canvas), self._dt)
-        if self.occ is not None:
+        if self.occ is not None and self.occ_gated:
+            _native.call("tca_pillar_occ_clear", _native.ptr(coords), _native.ptr(voxel_count), coords.shape[0],
+                         coords.shape[1], self.nx, self.ny, _native.ptr(self.occ), _native.stream_ptr(stream))
+        elif self.occ is not None:
             _native.call("tca_pillar_canvas_clear_occ", *args, _native.ptr(self.occ), _native.stream_ptr(stream))
         else:
             _native.call("tca_pillar_canvas_clear", *args, _native.stream_ptr(stream))

@@ -19,6 +19,8 @@ materialised (the VFE kernel gathers from the voxeliser's slot lists).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -29,6 +31,10 @@ from ..models.pointpillars import PointPillars, build_pointpillars
 from ..ops._ws import Workspace
 from ..ops.conv import act_dtype
 from ..ops.lidar import AnchorPostprocess, PillarEncoder, PointLayout, Voxelizer, pc2_unpack
+
+# the per-frame canvas clear resets only the previous frame's occupancy bytes when the fast plan's
+# first conv gates its loads on them (TCA_LAZY_CANVAS=0: clear the features too, for A/B runs)
+LAZY_CANVAS_CLEAR = os.environ.get("TCA_LAZY_CANVAS", "1") != "0"
 
 
 class LidarPipeline:
@@ -64,8 +70,10 @@ class LidarPipeline:
     def build_fast(self):
         from ..models.fast import FastBEV
         self.fast = FastBEV(self.model, self.B, self.device, precision=self.precision)
-        # fp32 mode: the scatter writes the pair storage the plan reads
+        # fp32 mode: the scatter writes the pair storage the plan reads; the plan's first conv
+        # gates its canvas loads on the occupancy bytes, so a frame's clear resets only those
         self.enc.set_pair(self.fast.pair)
+        self.enc.set_occ_gated(LAZY_CANVAS_CLEAR and self.fast.first_conv_gated())
         return self.fast
 
     @torch.no_grad()
