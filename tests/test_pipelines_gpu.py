@@ -148,13 +148,15 @@ def test_lidar_occupancy_only_clear_matches_fresh_pipeline(cuda):
     sweeps first gives exactly the detections and the (masked) dense canvas of a fresh one."""
     spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
     la = LidarPipeline(batch=2, max_points=32768, device=cuda)
+    # built before the calibration too: a pipeline takes the VFE weights at construction and the
+    # calibration's LSUV pass rescales the model
+    lf = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
     _load_lidar(la, spec, [5, 6])
     la.calibrate_detection_density(500.0)
     la.step()
     assert la.enc.occ_gated and la.enc.pair
     _load_lidar(la, spec, [7, 8])
     ra = la.step()
-    lf = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
     _load_lidar(lf, spec, [7, 8])
     rf = lf.step()
     torch.cuda.synchronize()
