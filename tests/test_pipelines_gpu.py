@@ -142,28 +142,47 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, blocks_front)
             assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)
 
 
-def test_lidar_occupancy_only_clear_matches_fresh_pipeline(cuda):
+@pytest.mark.parametrize("lazy", [True, False], ids=["occ_clear", "full_clear"])
+def test_lidar_occupancy_only_clear_matches_fresh_pipeline(cuda, monkeypatch, lazy):
     """With the fast plan's first conv gating its canvas loads on the occupancy bytes, a frame's
     clear resets only the previous frame's occupancy (not its features): a pipeline that ran other
-    sweeps first gives exactly the detections and the (masked) dense canvas of a fresh one."""
+    sweeps first gives exactly the voxels, occupancy, (masked) dense canvas, head maps and
+    detections of a fresh one -- and so does the full clear."""
+    import triton_client_amd.pipelines.lidar as lidar_mod
+    monkeypatch.setattr(lidar_mod, "LAZY_CANVAS_CLEAR", lazy)
     spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
     la = LidarPipeline(batch=2, max_points=32768, device=cuda)
-    # built before the calibration too: a pipeline takes the VFE weights at construction and the
-    # calibration's LSUV pass rescales the model
+    # built before the calibration too: both pipelines take the same weights
     lf = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
     _load_lidar(la, spec, [5, 6])
     la.calibrate_detection_density(500.0)
     la.step()
-    assert la.enc.occ_gated and la.enc.pair
+    assert la.enc.occ_gated == lazy and la.enc.pair
     _load_lidar(la, spec, [7, 8])
     ra = la.step()
     _load_lidar(lf, spec, [7, 8])
     rf = lf.step()
     torch.cuda.synchronize()
+    same = {}
+    vc = la.vox.voxel_count
+    same["voxel_count"] = torch.equal(vc, lf.vox.voxel_count)
+    for b in range(2):
+        k = int(vc[b])
+        same[f"coords{b}"] = torch.equal(la.vox.coords[b, :k], lf.vox.coords[b, :k])
+        same[f"num_points{b}"] = torch.equal(la.vox.num_points[b, :k], lf.vox.num_points[b, :k])
+    same["occ"] = torch.equal(la.enc.occ, lf.enc.occ)
+    same["canvas"] = torch.equal(la.enc.canvas_nchw(), lf.enc.canvas_nchw())
+    occ = la.enc.occ.bool()
+    same["canvas_occupied"] = torch.equal(la.enc.canvas[occ], lf.enc.canvas[occ])
+    same["depth"] = torch.equal(la.fast.bb.depth, lf.fast.bb.depth) if la.fast.bb.depth is not None else True
+    same["hout"] = torch.equal(la.fast.hout.t, lf.fast.hout.t)
+    same["count"] = torch.equal(ra.count, rf.count)
+    for b in range(2):  # rows past a frame's count are scratch (a reused pipeline keeps older ones)
+        k = int(ra.count[b])
+        same[f"box{b}"] = torch.equal(ra.box[b, :k], rf.box[b, :k])
+        same[f"score{b}"] = torch.equal(ra.score[b, :k], rf.score[b, :k])
+    assert all(same.values()), {k: v for k, v in same.items() if not v}
     assert int(ra.count.min()) > 0
-    for a, f in zip((ra.box, ra.score, ra.count), (rf.box, rf.score, rf.count)):
-        assert torch.equal(a, f)
-    assert torch.equal(la.enc.canvas_nchw(), lf.enc.canvas_nchw())
-    # the old cells of frames 5 / 6 hold stale features: only the occupancy hides them
-    stale = (la.enc.occ == 0) & (la.enc.canvas.abs().amax(-1) > 0)
-    assert int(stale.sum()) > 0
+    if lazy:  # the old cells of frames 5 / 6 hold stale features: only the occupancy hides them
+        stale = (la.enc.occ == 0) & (la.enc.canvas.abs().amax(-1) > 0)
+        assert int(stale.sum()) > 0
