@@ -177,7 +177,13 @@ def kernels(auto_build: bool = True) -> ctypes.CDLL:
             raise NativeError(f"{path} is missing: run `python -m triton_client_amd._build` (hipcc, gfx950)")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, args in _KERNEL_SIGS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                # an older build (TCA_KERNELS_LIB A/B runs): a call of this entry fails loudly
+                # (AttributeError) instead of the whole library failing to load
+                if not os.environ.get("TCA_KERNELS_LIB"):
+                    raise NativeError(f"{path}: no symbol {name}: rebuild (python -m triton_client_amd._build)")
+                continue
             fn.argtypes = args
             fn.restype = I
         _KERNELS = lib
