@@ -12,7 +12,7 @@ them:
   E  device -> hipHostRegister'd /dev/shm mapping       (a system shared-memory output slice)
   F  device -> torch pinned
 
-    rocprofv3 --kernel-trace --memory-copy-trace --stats -d out -- python tools/copy_path_probe.py
+    python tools/copy_path_probe.py   (device events per kind via torch.profiler; a rocprofv3 run crashed at exit)
 """
 import mmap
 import os
@@ -26,6 +26,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SIZES = {"A": 3 << 20, "B": (3 << 20) + 4096, "C": (3 << 20) + 8192, "D": (3 << 20) + 12288,
          "E": (3 << 20) + 16384, "F": (3 << 20) + 20480}
+
+
+def _device_events(fn) -> dict:
+    """Names of the device-side events one call of ``fn`` produces (blit kernel vs DMA copy), via torch.profiler:
+    in-process, so nothing depends on the tracer's exit path."""
+    from torch.profiler import ProfilerActivity, profile
+
+    try:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            fn()
+            torch.cuda.synchronize()
+    except Exception as e:  # profiler unavailable: the timings still stand
+        return {"error": repr(e)}
+    names = {}
+    for ev in prof.events():
+        if getattr(ev, "device_type", None) is not None and "CUDA" in str(ev.device_type):
+            names[ev.name] = names.get(ev.name, 0) + 1
+    return names
 
 
 def main() -> int:
@@ -61,6 +79,7 @@ def main() -> int:
         for k, fn in kinds.items():
             fn()
             torch.cuda.synchronize()
+            out.setdefault("device_events", {})[k] = _device_events(fn)
             t0 = time.perf_counter()
             for _ in range(reps):
                 fn()
