@@ -11,6 +11,22 @@ import sys
 from collections import defaultdict
 
 
+def _short(name: str) -> str:
+    """'void (anonymous namespace)::conv_wino_kernel<4, 4, 2, true, false, false>(float const*, ...)' ->
+    'conv_wino_kernel<4, 4, 2, true, false, false>' (splitting at the first '(' kept only 'void ')."""
+    for p in ("void ", "(anonymous namespace)::"):
+        name = name.replace(p, "")
+    depth = 0
+    for i, c in enumerate(name):
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == "(" and depth == 0:
+            return name[:i][:80]
+    return name[:80]
+
+
 def main():
     args = sys.argv[1:]
     min_waves = 64
@@ -23,7 +39,7 @@ def main():
     for fn in args:
         with open(fn) as f:
             for r in csv.DictReader(f):
-                k = r["Kernel_Name"].split("(")[0][:80]
+                k = _short(r["Kernel_Name"])
                 vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
     rows = []
