@@ -381,6 +381,170 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
   }
 }
 
+// pillar_vfe_lin_kernel, two pillars per wave iteration: lanes 0-31 gather pillar A's slots and
+// lanes 32-63 pillar B's (the one-pillar kernel loads the same 32 points into both halves), so a
+// wave walks its chain of dependent loads (take -> slot index -> point gather) half as many times.
+// That chain is what the one-pillar kernel waits on (PMC: 53% of wave time waiting,
+// profiles/r6/vfe/).  Per pillar the arithmetic and its order are those of the one-pillar kernel,
+// so the two write bit-identical canvases.
+template <bool FROM_SLOTS, typename CT, int PFIX = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) pillar_vfe_lin2_kernel(
+    const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ slots,
+    const int* __restrict__ vcount, const float* __restrict__ voxels, const int* __restrict__ num_points,
+    const int* __restrict__ coords, const int* __restrict__ voxel_count, int batch, int max_voxels, int P_arg,
+    const float* __restrict__ W /*[64][10]*/, const float* __restrict__ bias /*[64]*/, PillarGeom g,
+    CT* __restrict__ canvas, float* __restrict__ feat_out, uint8_t* __restrict__ occ) {
+  const int P = PFIX ? PFIX : P_arg;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  __shared__ float4 spts[4][64];  // [wave][half * 32 + slot]
+
+  const float* w = W + lane * 10;
+  const float a0 = w[0] + w[4] + w[7], a1 = w[1] + w[5] + w[8], a2 = w[2] + w[6] + w[9], a3 = w[3];
+  const float u0 = w[4], u1 = w[5], u2 = w[6], t0 = w[7], t1 = w[8], t2 = w[9];
+  const float bc = bias[lane];
+
+  const int nv = batch * max_voxels;
+  const int step = __builtin_amdgcn_readfirstlane((int)nwaves);
+  // the one-pillar kernel's per-frame walk: consecutive takes are this wave's next pillars
+  const int wave_u = __builtin_amdgcn_readfirstlane((int)wave);
+  const int wpf = max(1, step / batch);
+  const int fstep = max(1, step / wpf);
+  const int loc0 = wave_u % wpf;
+  auto first_at = [&](int bb) {
+    while (bb < batch && loc0 >= voxel_count[bb]) bb += fstep;
+    return bb;
+  };
+  int cb = first_at(wave_u / wpf), cl = loc0;
+  auto take = [&](int& bb) {
+    bb = min(cb, batch - 1);
+    if (cb >= batch) return nv;
+    const int row = cb * max_voxels + cl;
+    cl += wpf;
+    if (cl >= voxel_count[cb]) {
+      cb = first_at(cb + fstep);
+      cl = loc0;
+    }
+    return row;
+  };
+  const bool vec4 = (pstride & 3) == 0;
+  const int rs = min(r, P - 1);
+  // lane half h works on pillar h of the pair (vA, vB)
+  auto slot_of = [&](int vA, int vB) {
+    const int vv = h ? vB : vA;
+    return FROM_SLOTS ? slots[min(vv, nv - 1) * P + rs] : 0;
+  };
+  auto gather = [&](int vA, int vB, int bA, int bB, int id, float (&q)[4]) {
+    const int vv = h ? vB : vA, bb = h ? bB : bA;
+    const int vc_ = vv < nv ? (FROM_SLOTS ? vcount[vv] : num_points[vv]) : 0;
+    const bool real_ = r < min(vc_, P);
+    const float* src = FROM_SLOTS ? pts + ((long)bb * max_pts + (real_ ? id : 0)) * pstride
+                                  : voxels + ((long)min(vv, nv - 1) * P + rs) * 4;
+    if (!FROM_SLOTS || vec4) {
+      const float4 t = *reinterpret_cast<const float4*>(src);
+      q[0] = t.x; q[1] = t.y; q[2] = t.z; q[3] = t.w;
+    } else {
+      q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
+    }
+  };
+  auto meta = [&](int vA, int vB, int& vc_, int4& co_) {
+    const int vq = min(h ? vB : vA, nv - 1);
+    vc_ = FROM_SLOTS ? vcount[vq] : num_points[vq];
+    co_ = *reinterpret_cast<const int4*>(coords + vq * 4);
+  };
+  // one pillar's output: the one-pillar kernel's expressions
+  auto emit = [&](int n, float acc, float sx, float sy, float sz, int b, int cz, int cy, int cx, int v) {
+    const float inv_n = 1.f / (float)max(n, 1);
+    const float xc = (float)cx * g.vx + (g.vx * 0.5f + g.r0);
+    const float yc = (float)cy * g.vy + (g.vy * 0.5f + g.r1);
+    const float zc = (float)cz * g.vz + (g.vz * 0.5f + g.r2);
+    const float d = -(u0 * (sx * inv_n) + u1 * (sy * inv_n) + u2 * (sz * inv_n) + t0 * xc + t1 * yc + t2 * zc);
+    float mval = acc + d;
+    if (n < P) mval = fmaxf(mval, 0.f);
+    const float val = fmaxf(mval + bc, 0.f);
+    const int ch = lane;
+    const long cell = ((long)b * g.ny + cy) * g.nx + cx;
+    if (canvas) {
+      if constexpr (std::is_same<CT, PairTag>::value) {
+        __bf16* c2 = reinterpret_cast<__bf16*>(canvas) + cell * 128 + (ch >> 3) * 16 + (ch & 7);
+        const __bf16 hv = (__bf16)val;
+        c2[0] = hv;
+        c2[8] = (__bf16)(val - (float)hv);
+      } else {
+        canvas[cell * 64 + ch] = from_f32<CT>(val);
+      }
+    }
+    if (feat_out) feat_out[(long)v * 64 + ch] = val;
+    if (occ && lane == 0) occ[cell] = 1;
+  };
+  auto points_max = [&](const float4* sp, int n, float& acc, float& sx, float& sy, float& sz) {
+    acc = -INFINITY;
+    sx = sy = sz = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < n; ++j) {
+      const float4 q = sp[j];
+      acc = fmaxf(acc, fmaf(a0, q.x, fmaf(a1, q.y, fmaf(a2, q.z, a3 * q.w))));
+      sx += q.x;
+      sy += q.y;
+      sz += q.z;
+    }
+  };
+  int bA, bB, bAn, bBn, bAnn, bBnn;
+  int vA = take(bA), vB = take(bB);
+  int vAn = take(bAn), vBn = take(bBn);
+  int vAnn = take(bAnn), vBnn = take(bBnn);
+  float pc[4], pn[4];
+  gather(vA, vB, bA, bB, slot_of(vA, vB), pc);
+  gather(vAn, vBn, bAn, bBn, slot_of(vAn, vBn), pn);
+  int idx_nn = slot_of(vAnn, vBnn);
+  int vc;
+  int4 co;
+  meta(vA, vB, vc, co);
+  while (vA < nv) {
+    const int mv = min(vc, P);
+    const int nA = __builtin_amdgcn_readlane(mv, 0);
+    const int nB = vB < nv ? __builtin_amdgcn_readlane(mv, 32) : 0;
+    const int zA = __builtin_amdgcn_readlane(co.y, 0), yA = __builtin_amdgcn_readlane(co.z, 0),
+              xA = __builtin_amdgcn_readlane(co.w, 0);
+    const int zB = __builtin_amdgcn_readlane(co.y, 32), yB = __builtin_amdgcn_readlane(co.z, 32),
+              xB = __builtin_amdgcn_readlane(co.w, 32);
+    int bA3, bB3;
+    const int vA3 = take(bA3), vB3 = take(bB3);
+    const int idx_3 = slot_of(vA3, vB3);
+    float pnn[4];
+    gather(vAnn, vBnn, bAnn, bBnn, idx_nn, pnn);
+    int vc_n;
+    int4 co_n;
+    meta(vAn, vBn, vc_n, co_n);
+    spts[wid][lane] = make_float4(pc[0], pc[1], pc[2], pc[3]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float accA, sxA, syA, szA, accB, sxB, syB, szB;
+    points_max(&spts[wid][0], nA, accA, sxA, syA, szA);
+    points_max(&spts[wid][32], nB, accB, sxB, syB, szB);
+    __builtin_amdgcn_wave_barrier();  // this pair's reads before the next pair's LDS writes
+    emit(nA, accA, sxA, syA, szA, bA, zA, yA, xA, vA);
+    if (nB > 0) emit(nB, accB, sxB, syB, szB, bB, zB, yB, xB, vB);
+    vA = vAn; vB = vBn;
+    vAn = vAnn; vBn = vBnn;
+    vAnn = vA3; vBnn = vB3;
+    bA = bAn; bB = bBn;
+    bAn = bAnn; bBn = bBnn;
+    bAnn = bA3; bBnn = bB3;
+    idx_nn = idx_3;
+    vc = vc_n;
+    co = co_n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pc[k] = pn[k];
+      pn[k] = pnn[k];
+    }
+  }
+}
+
 // Zero exactly the cells the previous frame scattered: one thread per 16-B
 // chunk of a pillar's C channels (C * esize % 16 == 0), frame per grid row.
 // A bounded grid walks each frame's pillars (grid-stride): dispatching B x max_voxels worth of
@@ -424,14 +588,16 @@ int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, con
                                      batch, max_voxels, P, W, bias, g, canvas, feat_out, dt, occ, stream);
 }
 
-// 0: the fp32 VALU kernel (default), 1: the split-bf16 MFMA kernel (TCA_VFE_MFMA=1 or
-// tca_pillar_vfe_set_variant; kept for A/B and its tests)
+// 0: the fp32 VALU kernel, one pillar per wave iteration; 1: the split-bf16 MFMA kernel
+// (TCA_VFE_MFMA=1; kept for A/B and its tests); 2: the fp32 VALU kernel, two pillars per wave
+// iteration (TCA_VFE_LIN2=1).  tca_pillar_vfe_set_variant switches at run time.
 int g_vfe_variant = -1;
 
 int vfe_variant() {
   if (g_vfe_variant < 0) {
     const char* e = getenv("TCA_VFE_MFMA");
-    g_vfe_variant = (e && e[0] == '1') ? 1 : 0;
+    const char* e2 = getenv("TCA_VFE_LIN2");
+    g_vfe_variant = (e && e[0] == '1') ? 1 : (e2 && e2[0] == '1') ? 2 : 0;
   }
   return g_vfe_variant;
 }
@@ -445,13 +611,18 @@ int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, c
   KERNEL<FROM_SLOTS, CT, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels, num_points, \
                                                         coords, voxel_count, batch, max_voxels, P, W, bias, g,      \
                                                         (CT*)canvas, feat_out, occ)
-  const bool mfma = vfe_variant() == 1;
+  const int var = vfe_variant();
   if (dt == kF32) {
-    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, float); else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, float);
+    if (var == 1) TCA_VFE_LAUNCH(pillar_vfe_kernel, float);
+    else if (var == 2) TCA_VFE_LAUNCH(pillar_vfe_lin2_kernel, float);
+    else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, float);
   } else if (dt == kPair) {
-    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, PairTag); else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, PairTag);
+    if (var == 1) TCA_VFE_LAUNCH(pillar_vfe_kernel, PairTag);
+    else if (var == 2) TCA_VFE_LAUNCH(pillar_vfe_lin2_kernel, PairTag);
+    else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, PairTag);
   } else {
-    if (mfma) TCA_VFE_LAUNCH(pillar_vfe_kernel, __hip_bfloat16);
+    if (var == 1) TCA_VFE_LAUNCH(pillar_vfe_kernel, __hip_bfloat16);
+    else if (var == 2) TCA_VFE_LAUNCH(pillar_vfe_lin2_kernel, __hip_bfloat16);
     else TCA_VFE_LAUNCH(pillar_vfe_lin_kernel, __hip_bfloat16);
   }
 #undef TCA_VFE_LAUNCH
@@ -459,10 +630,11 @@ int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, c
 }
 }  // namespace
 
-// VFE kernel selection: 0 = fp32 VALU (default), 1 = split-bf16 MFMA; returns the previous one.
+// VFE kernel selection: 0 = fp32 VALU, 1 = split-bf16 MFMA, 2 = fp32 VALU two pillars per wave
+// iteration; returns the previous one.
 TCA_API int tca_pillar_vfe_set_variant(int v) {
   const int old = vfe_variant();
-  g_vfe_variant = v ? 1 : 0;
+  g_vfe_variant = (v == 1 || v == 2) ? v : 0;
   return old;
 }
 

@@ -263,17 +263,62 @@ def test_voxelize_gpu_dense_voxels(cuda, vcfg, hash_mode, monkeypatch):
             np.testing.assert_array_equal(v[b, :k].cpu().numpy(), rv)
 
 
-@pytest.mark.parametrize("variant", [0, 1], ids=["valu_fp32", "mfma_split"])
+@pytest.mark.parametrize("variant", [0, 1, 2], ids=["valu_fp32", "mfma_split", "valu_fp32_two_pillars"])
 def test_pillar_vfe_gpu_vs_fp32(cuda, variant):
-    """Both VFE kernels against the fp32 PyTorch reference: 0 = the linearity-folded fp32 VALU
-    kernel (default; tight tolerance), 1 = the split-bf16 MFMA kernel."""
+    """The VFE kernels against the fp32 PyTorch reference: 0 = the linearity-folded fp32 VALU
+    kernel (tight tolerance), 1 = the split-bf16 MFMA kernel, 2 = the VALU kernel taking two
+    pillars per wave iteration."""
     from triton_client_amd import _native
 
     old = _native.kernels().tca_pillar_vfe_set_variant(variant)
     try:
-        _pillar_vfe_check(cuda, 1e-4 if variant == 0 else 2e-3)
+        _pillar_vfe_check(cuda, 2e-3 if variant == 1 else 1e-4)
     finally:
         _native.kernels().tca_pillar_vfe_set_variant(old)
+
+
+@pytest.mark.parametrize("pair", [False, True], ids=["fp32_canvas", "pair_canvas"])
+@pytest.mark.parametrize("batch", [1, 3])
+def test_pillar_vfe_two_pillar_walk_bit_identical(cuda, pair, batch):
+    """The two-pillars-per-iteration VALU kernel writes exactly the one-pillar kernel's features,
+    canvas and occupancy (same per-pillar arithmetic; every pillar of every frame, odd counts
+    leaving a half-empty last pair)."""
+    from triton_client_amd import _native
+
+    cfg = dataclasses.replace(KITTI_PILLARS, max_voxels=5000)
+    N = 20000
+    pts = np.stack([synth_cloud(N, seed=40 + b, nan_frac=0.0, pcr=cfg.point_cloud_range) for b in range(batch)])
+    pts[..., 3] /= 255.0
+    cnt = np.array([N - 977 * b for b in range(batch)], np.int32)  # frames of different pillar counts
+    torch.manual_seed(1)
+    W = torch.randn(64, 10) * 0.3
+    bias = torch.randn(64) * 0.1
+    pg, cg = torch.from_numpy(pts).to(cuda), torch.from_numpy(cnt).to(cuda)
+    outs = []
+    k = _native.kernels()
+    old = k.tca_pillar_vfe_set_variant(0)
+    try:
+        for variant in (0, 2):
+            k.tca_pillar_vfe_set_variant(variant)
+            vox = Voxelizer(cfg, batch, N, device=cuda)
+            enc = PillarEncoder(cfg, W, bias, batch, device=cuda, dtype=torch.float32)
+            enc.set_pair(pair)
+            feat = torch.zeros(batch, cfg.max_voxels, 64, device=cuda)
+            vox.assign(pg, cg)
+            enc.encode_from_slots(pg, vox, feat_out=feat)
+            torch.cuda.synchronize()
+            vc = vox.voxel_count.cpu()
+            outs.append((vc, [feat[b, :int(vc[b])].cpu() for b in range(batch)], enc.canvas.cpu(),
+                         None if enc.occ is None else enc.occ.cpu()))
+    finally:
+        k.tca_pillar_vfe_set_variant(old)
+    (vc0, f0, c0, o0), (vc2, f2, c2, o2) = outs
+    assert torch.equal(vc0, vc2) and int(vc0.min()) > 100
+    for a, b_ in zip(f0, f2):
+        assert torch.equal(a, b_)
+    assert torch.equal(c0, c2)
+    if pair:
+        assert torch.equal(o0, o2) and int(o0.sum()) == int(vc0.sum())
 
 
 def _pillar_vfe_check(cuda, tol):
