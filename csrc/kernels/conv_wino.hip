@@ -189,7 +189,9 @@ __global__ void __launch_bounds__(WN * 64, 2) conv_wino_kernel(WinoArgs a) {
     for (int k = 0; k < DPW; ++k) bdma16(dvo[k], rin, raw + (wn * DPW + k) * 1024, (unsigned)(c * 128));
   };
   // transform: item id = (u * 4 + cq) * 16 + t -> the 4 positions' hi / lo slots of (u, cq, t)
-  auto transform = [&]() {
+  // always inlined: with pair input the inliner kept it a function (a call per chunk, its
+  // captures passed through scratch memory)
+  auto transform = [&]() __attribute__((always_inline)) {
     unsigned char* ub = smem;
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {

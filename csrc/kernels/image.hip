@@ -40,6 +40,10 @@ __device__ __forceinline__ void coord(float dst, float scale, int src_n, int& i0
   i1 = min(s + 1, src_n - 1);
 }
 
+// Channel c of a 3-channel sample, red and blue swapped when `swap`: two constant-index reads and a
+// select (o[swap ? 2 - c : c] is a run-time index, which puts the whole array in scratch memory).
+__device__ __forceinline__ float rgb_at(const float (&o)[3], int c, bool swap) { return swap ? o[2 - c] : o[c]; }
+
 template <typename T>
 __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ src, T* __restrict__ dst, PrepParams p,
                                                    int batch) {
@@ -95,10 +99,9 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
     const bool full = q * 4 + 3 < p.dst_w && ((p.dst_w & 3) == 0);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const int sc_c = p.swap_rb ? 2 - c : c;
       T v4[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v4[k] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+      for (int k = 0; k < 4; ++k) v4[k] = from_f32<T>(rgb_at(out[k], c, p.swap_rb) * sc[c] + bi[c]);
       T* o = d + base + (long)c * plane;
       if (full) {
         if constexpr (sizeof(T) == 4) {
@@ -123,8 +126,7 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
       T px[8];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const int sc_c = p.swap_rb ? 2 - c : c;
-        px[c] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+        px[c] = from_f32<T>(rgb_at(out[k], c, p.swap_rb) * sc[c] + bi[c]);
       }
 #pragma unroll
       for (int c = 3; c < 8; ++c) px[c] = from_f32<T>(0.f);
@@ -139,8 +141,7 @@ __global__ void __launch_bounds__(256) prep_kernel(const uint8_t* __restrict__ s
       T px[4];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const int sc_c = p.swap_rb ? 2 - c : c;
-        px[c] = from_f32<T>(out[k][sc_c] * sc[c] + bi[c]);
+        px[c] = from_f32<T>(rgb_at(out[k], c, p.swap_rb) * sc[c] + bi[c]);
       }
       px[3] = from_f32<T>(0.f);
       T* o = d + base + (long)k * p.dst_c;
@@ -205,7 +206,7 @@ __global__ void __launch_bounds__(256) prep_s2d_kernel(const uint8_t* __restrict
     float o[3];
     sample_px(p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) px[d * 3 + c] = from_f32<T>(o[p.swap_rb ? 2 - c : c] * sc[c] + bi[c]);
+    for (int c = 0; c < 3; ++c) px[d * 3 + c] = from_f32<T>(rgb_at(o, c, p.swap_rb) * sc[c] + bi[c]);
   }
 #pragma unroll
   for (int c = 12; c < 16; ++c) px[c] = from_f32<T>(0.f);
@@ -343,19 +344,31 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
                     !(a.p.reg_top & 1) && !(a.p.reg_left & 1) && !(a.p.reg_h & 1) && !(a.p.reg_w & 1) &&
                     !(a.p.src_row_stride & 3) && !(a.p.src_batch_stride & 3);
   auto put = [&](int g, const float (&v)[16]) {
-    __bf16 h[16], l[16];
+    // hi / lo bf16 of the 16 channels packed straight into 32-bit words (no private arrays: a
+    // run-time choice between halves of an array kept it in scratch memory, 80 B per lane
+    // written and read back per pixel)
+    unsigned hw[8], lw[8];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      h[c] = (__bf16)v[c];
-      l[c] = (__bf16)(v[c] - (float)h[c]);
+    for (int c = 0; c < 8; ++c) {
+      const __bf16 h0 = (__bf16)v[2 * c], h1 = (__bf16)v[2 * c + 1];
+      const __bf16 l0 = (__bf16)(v[2 * c] - (float)h0), l1 = (__bf16)(v[2 * c + 1] - (float)h1);
+      hw[c] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+      lw[c] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
     }
+    const uint4 hA = make_uint4(hw[0], hw[1], hw[2], hw[3]), hB = make_uint4(hw[4], hw[5], hw[6], hw[7]);
+    const uint4 lA = make_uint4(lw[0], lw[1], lw[2], lw[3]), lB = make_uint4(lw[4], lw[5], lw[6], lw[7]);
     // 32-B pixel stride: the two 16-B halves go in an order alternating every 4 pixels, so each
     // 8-lane ds_write_b128 group covers the 32 banks once (in one order: 2-way)
-    const int q0 = (g >> 2) & 1;
-    *reinterpret_cast<uint4*>(himg + g * 32 + q0 * 16) = reinterpret_cast<const uint4*>(h)[q0];
-    *reinterpret_cast<uint4*>(himg + g * 32 + (q0 ^ 1) * 16) = reinterpret_cast<const uint4*>(h)[q0 ^ 1];
-    *reinterpret_cast<uint4*>(limg + g * 32 + q0 * 16) = reinterpret_cast<const uint4*>(l)[q0];
-    *reinterpret_cast<uint4*>(limg + g * 32 + (q0 ^ 1) * 16) = reinterpret_cast<const uint4*>(l)[q0 ^ 1];
+    const bool q0 = (g >> 2) & 1;
+    uint4 f, s2;
+    f.x = q0 ? hB.x : hA.x; f.y = q0 ? hB.y : hA.y; f.z = q0 ? hB.z : hA.z; f.w = q0 ? hB.w : hA.w;
+    s2.x = q0 ? hA.x : hB.x; s2.y = q0 ? hA.y : hB.y; s2.z = q0 ? hA.z : hB.z; s2.w = q0 ? hA.w : hB.w;
+    *reinterpret_cast<uint4*>(himg + g * 32 + q0 * 16) = f;
+    *reinterpret_cast<uint4*>(himg + g * 32 + (!q0) * 16) = s2;
+    f.x = q0 ? lB.x : lA.x; f.y = q0 ? lB.y : lA.y; f.z = q0 ? lB.z : lA.z; f.w = q0 ? lB.w : lA.w;
+    s2.x = q0 ? lA.x : lB.x; s2.y = q0 ? lA.y : lB.y; s2.z = q0 ? lA.z : lB.z; s2.w = q0 ? lA.w : lB.w;
+    *reinterpret_cast<uint4*>(limg + g * 32 + q0 * 16) = f;
+    *reinterpret_cast<uint4*>(limg + g * 32 + (!q0) * 16) = s2;
   };
   if (half) {
     // all of this thread's source blocks are requested before any is used (one memory latency
@@ -405,7 +418,7 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
       for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          v[d * 3 + c] = state[u] ? o[d][a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c] : 0.f;
+          v[d * 3 + c] = state[u] ? rgb_at(o[d], c, a.p.swap_rb) * sc[c] + bi[c] : 0.f;
 #pragma unroll
       for (int c = 12; c < 16; ++c) v[c] = 0.f;
       put(g, v);
@@ -423,7 +436,7 @@ __global__ void __launch_bounds__(256) yolo_stem_fused_kernel(StemArgs a) {
           float o[3];
           sample_px(a.p, s, 2 * Y + (d >> 1), 2 * X + (d & 1), o);
 #pragma unroll
-          for (int c = 0; c < 3; ++c) v[d * 3 + c] = o[a.p.swap_rb ? 2 - c : c] * sc[c] + bi[c];
+          for (int c = 0; c < 3; ++c) v[d * 3 + c] = rgb_at(o, c, a.p.swap_rb) * sc[c] + bi[c];
         }
       }
       put(g, v);

@@ -385,8 +385,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) p
 // lanes 32-63 pillar B's (the one-pillar kernel loads the same 32 points into both halves), so a
 // wave walks its chain of dependent loads (take -> slot index -> point gather) half as many times.
 // That chain is what the one-pillar kernel waits on (PMC: 53% of wave time waiting,
-// profiles/r6/vfe/).  Per pillar the arithmetic and its order are those of the one-pillar kernel,
-// so the two write bit-identical canvases.
+// profiles/r6/vfe/).  Per pillar the expressions are those of the one-pillar kernel (the same
+// values to fp32 rounding: the compiler may contract them into FMAs differently).
 template <bool FROM_SLOTS, typename CT, int PFIX = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) pillar_vfe_lin2_kernel(
     const float* __restrict__ pts, int pstride, int max_pts, const int* __restrict__ slots,

@@ -279,10 +279,11 @@ def test_pillar_vfe_gpu_vs_fp32(cuda, variant):
 
 @pytest.mark.parametrize("pair", [False, True], ids=["fp32_canvas", "pair_canvas"])
 @pytest.mark.parametrize("batch", [1, 3])
-def test_pillar_vfe_two_pillar_walk_bit_identical(cuda, pair, batch):
-    """The two-pillars-per-iteration VALU kernel writes exactly the one-pillar kernel's features,
-    canvas and occupancy (same per-pillar arithmetic; every pillar of every frame, odd counts
-    leaving a half-empty last pair)."""
+def test_pillar_vfe_two_pillar_walk_matches_one_pillar(cuda, pair, batch):
+    """The two-pillars-per-iteration VALU kernel writes the one-pillar kernel's features and canvas
+    within the fp32 test bound (same per-pillar expressions; the compiler contracts them into FMAs
+    differently: ~1e-5 apart) and exactly its occupancy: every pillar of every frame, odd counts
+    leaving a half-empty last pair."""
     from triton_client_amd import _native
 
     cfg = dataclasses.replace(KITTI_PILLARS, max_voxels=5000)
@@ -314,9 +315,13 @@ def test_pillar_vfe_two_pillar_walk_bit_identical(cuda, pair, batch):
         k.tca_pillar_vfe_set_variant(old)
     (vc0, f0, c0, o0), (vc2, f2, c2, o2) = outs
     assert torch.equal(vc0, vc2) and int(vc0.min()) > 100
+    tol = 1e-4 * max(1.0, max(float(a.abs().max()) for a in f0))  # the vs-fp32 test's bound
     for a, b_ in zip(f0, f2):
-        assert torch.equal(a, b_)
-    assert torch.equal(c0, c2)
+        torch.testing.assert_close(b_, a, rtol=0.0, atol=tol)
+    if pair:
+        from triton_client_amd.ops.conv import from_pairs
+        c0, c2 = from_pairs(c0), from_pairs(c2)
+    torch.testing.assert_close(c2, c0, rtol=0.0, atol=tol)
     if pair:
         assert torch.equal(o0, o2) and int(o0.sum()) == int(vc0.sum())
 

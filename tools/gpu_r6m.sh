@@ -1,5 +1,5 @@
 # Round 6: PillarVFE two pillars per wave iteration (TCA_VFE_LIN2=1, variant 2): the VFE tests (numerics
-# vs fp32 and bit-identity vs the one-pillar kernel), standalone VFE times of the three variants
+# vs fp32 and vs the one-pillar kernel), standalone VFE times of the three variants
 # (tools/bench_vfe.py), then same-box LiDAR-only and headline A/Bs of the switch.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
