@@ -416,299 +416,6 @@ int wino_launch(const WinoArgs& a, int tile, bool pin, bool pout, hipStream_t st
   }
 }
 
-
-// ---- persistent F(2,3) kernel ("winop"): one 4-wave workgroup per CU (151 KB of LDS), fp32 storage in and
-// out, N % 128 == 0, Cin >= 64.  Why: the two-workgroups-per-CU kernel above holds 252 VGPRs per wave, so
-// its weight stream is prefetched only two steps ahead, every chunk stops the workgroup for a transform
-// phase between two barriers, and every 128-pixel tile pays its own halo prologue and store epilogue
-// (profiles/r6/wino/experiments.md: the 128-channel layer runs at ~48 % MFMA busy and ~40 % of the HBM
-// rate, neither saturated).  Here one wave per SIMD owns the register file (the accumulators go to
-// AGPRs), so:
-//   - tiles come from a work queue (wq[0], one atomic per tile, taken three chunks ahead) and the chunk
-//     stream runs across tile boundaries: the raw halo of chunk s + 2 lands by LDS DMA (double-buffered
-//     raw images) while chunk s computes, and chunk s + 1's input transform (double-buffered U images)
-//     is interleaved into chunk s's MFMA steps in ten pieces: one barrier per chunk, no transform phase;
-//   - the transformed weights stream through a 3-deep register ring (two steps ahead), and each step
-//     reads the next step's B fragments from LDS before its own MFMAs (double-buffered registers);
-//   - the epilogue stores each lane's fragments straight from the accumulators (no LDS staging), and
-//     the next tile's first chunk is already transformed.
-// The last workgroup to finish resets the queue (wq[1] counts finished workgroups), so the kernel is
-// graph-replay safe; every workgroup leaves through that exit.  Same products and summation order per
-// accumulator as conv_wino_kernel (bit-identical outputs, tests/test_wino_gpu.py).
-template <bool CM>
-__global__ void __launch_bounds__(256, 1) conv_winop_kernel(WinoArgs a, int* __restrict__ wq) {
-  constexpr int TH = 4, WN = 4, FN = 2, NT = 256, BN = 128, TF = 32, NU = TH + 2;
-  constexpr int UB = NU * 8192;
-  constexpr int NPIECE = NU * 34 * 8, NINS = (NPIECE + 63) / 64, DPW = (NINS + WN - 1) / WN;
-  constexpr int RAWB = NINS * 1024;
-  constexpr int RING = 4, PD = RING - 1;  // weight register sets; prefetch distance in steps
-  static_assert(12 % RING == 0, "the ring index of a step is the same in every chunk");
-  constexpr int NITEM = NU * 64;  // transform items: tid (every thread) and tid + NT (tid < NITEM - NT)
-  static_assert(NITEM > NT && NITEM <= 2 * NT, "two transform items per thread at most");
-  static_assert(2 * UB + 2 * RAWB + 64 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * UB + 2 * RAWB + 64];
-  int* const tq = reinterpret_cast<int*>(smem + 2 * UB + 2 * RAWB);  // tile ids, slot k & 3 for tile k
-
-  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
-  const int FH = CM ? a.H : a.W, LW = CM ? a.W : a.H;
-  const int nF = (FH + TF - 1) / TF, nL = (LW + TH - 1) / TH;
-  const int nnt = a.N / BN, ntile = a.B * nF * nL * nnt;
-  const int nc = a.Cin / 32;
-  auto pix_yx = [&](int f, int l, int& y, int& x) {
-    y = CM ? f : l;
-    x = CM ? l : f;
-  };
-  auto decode = [&](int t, int& b, int& f0, int& l0, int& n0) {
-    const int mt = t / nnt, nt = t - mt * nnt;
-    b = mt / (nF * nL);
-    const int rem = mt - b * (nF * nL);
-    f0 = (rem / nL) * TF;
-    l0 = (rem - (rem / nL) * nL) * TH;
-    n0 = nt * BN;
-  };
-
-  if (tid == 0) {
-    tq[0] = atomicAdd(wq, 1);
-    tq[1] = atomicAdd(wq, 1);
-  }
-  __syncthreads();
-  if (tq[0] < ntile) {
-    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.in_f, (short)0, a.B * a.H * a.W * a.ldi * 4, 0x00020000);
-    // this lane's DMA pieces (tile independent): pixel fi along F, halo line u, byte offset in the pixel
-    unsigned meta[DPW];
-#pragma unroll
-    for (int k = 0; k < DPW; ++k) {
-      const int q = (k * WN + wn) * 64 + lane;
-      const int u = q / 272, fi = raw_pos((q / 8) % 34), slot = raw_slot(fi, q & 7);
-      meta[k] = q < NPIECE ? (unsigned)(fi | (u << 8) | (((slot >> 1) * 32 + (slot & 1) * 16) << 16)) : 0xFFFFFFFFu;
-    }
-    auto dma_at = [&](int b, int f0, int l0, int c, unsigned char* rbuf) {
-#pragma unroll
-      for (int k = 0; k < DPW; ++k) {
-        if (NINS % WN != 0 && k * WN + wn >= NINS) continue;
-        const unsigned m = meta[k];
-        int y, x;
-        pix_yx(f0 - 1 + (int)(m & 255u), l0 - 1 + (int)((m >> 8) & 255u), y, x);
-        const unsigned vo = (m != 0xFFFFFFFFu && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                                ? (unsigned)((((b * a.H + y) * a.W + x) * a.ldi + a.ci_off) * 4) + (m >> 16)
-                                : kOutOfRange;
-        bdma16(vo, rin, rbuf + (k * WN + wn) * 1024, (unsigned)(c * 128));
-      }
-    };
-    unsigned char* const U0 = smem;
-    unsigned char* const R0 = smem + 2 * UB;
-
-    // input transform of one item (u, cq, t) in pieces: phase 0 loads its four raw pixels, phase
-    // 1 + p writes position p's hi / lo slots
-    auto tpiece = [&](auto KC, auto PH, const unsigned char* raw, unsigned char* ub, u32x4 (&pr)[4][2])
-        __attribute__((always_inline)) {
-      constexpr int k = decltype(KC)::value, ph = decltype(PH)::value;
-      // threads past NITEM repeat item id - (NITEM - NT) of their own half (same values to the same
-      // address): no branch, so the pieces stay in the MFMA steps' basic blocks
-      const int id = k == 0 ? tid : (tid + NT < NITEM ? tid + NT : tid + 2 * NT - NITEM);
-      const int u = id >> 6, cq = (id >> 4) & 3, t = id & 15;
-      if constexpr (ph == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int fi = 2 * t + j;
-          const unsigned char* rp = raw + (u * 34 + raw_pos(fi)) * 128;
-          pr[j][0] = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2) * 16);
-          pr[j][1] = *reinterpret_cast<const u32x4*>(rp + raw_slot(fi, cq * 2 + 1) * 16);
-        }
-      } else {
-        constexpr int p = ph - 1;
-        float uv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          auto dv = [&](int j) { return __uint_as_float(pr[j][e >> 2][e & 3]); };
-          uv[e] = p == 0 ? fsub1(dv(0), dv(2)) : p == 1 ? fadd1(dv(1), dv(2)) : p == 2 ? fsub1(dv(2), dv(1))
-                                                                                        : fsub1(dv(1), dv(3));
-        }
-        u32x4 hi, lo;
-        split8(uv, hi, lo);
-        unsigned char* wp = ub + ((u * 16 + cq) * 32 + t) * 16 + p * 2048;
-        *reinterpret_cast<u32x4*>(wp) = hi;
-        *reinterpret_cast<u32x4*>(wp + 256) = lo;
-      }
-    };
-
-    // weights: as conv_wino_kernel, a 3-deep ring; step (c, j = p * 3 + kl) of a chunk sits at scalar offset
-    // (kl * 4 + p) * S1 + c * S0, the lane part at (n0 / 16 + wn * FN) * 2048 + lane * 16
-    const int NG = a.N / 16;
-    const unsigned S0 = (unsigned)NG * 2048u, S1 = (unsigned)nc * S0;
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, 12 * nc * NG * 2048, 0x00020000);
-    bf16x8 w[RING][FN][2];
-    auto wload = [&](unsigned so, unsigned wvo, bf16x8 (&dst)[FN][2]) {
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) {
-        dst[jj][0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wvo + jj * 2048, so, 0));
-        dst[jj][1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, wvo + jj * 2048 + 1024, so, 0));
-      }
-    };
-    auto wvo_of = [&](int n0) { return (unsigned)((n0 / 16 + wn * FN) * 2048 + lane * 16); };
-
-    const int fr = lane & 15, fq = lane >> 4;
-    const int rd = (fq * 2 * 16 + fr) * 16;
-    f32x4 acc[TH][4][FN];
-    auto acc_init = [&](int n0) {
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) {
-        const f32x4 bv = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n0 + (wn * FN + jj) * 16 + fq * 4)
-                                : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < TH; ++i)
-#pragma unroll
-          for (int p = 0; p < 4; ++p) acc[i][p][jj] = p == 1 ? bv : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-
-    // prologue: chunks 0 and 1 of the first tile land, chunk 0 is transformed, two weight steps fly
-    int t0 = tq[0], b, f0, l0, n0;
-    decode(t0, b, f0, l0, n0);
-    unsigned wvo = wvo_of(n0);
-    dma_at(b, f0, l0, 0, R0);
-    dma_at(b, f0, l0, 1, R0 + RAWB);
-    wload(0 * S1, wvo, w[0]);  // (c 0, p 0, kl 0)
-    wload(4 * S1, wvo, w[1]);  // kl 1
-    if constexpr (PD > 2) wload(8 * S1, wvo, w[2]);  // kl 2
-    wait_vmcnt0();
-    lds_barrier();
-    {
-      u32x4 pr[4][2];
-      tpiece(PosC<0>{}, PosC<0>{}, R0, U0, pr);
-      tpiece(PosC<0>{}, PosC<1>{}, R0, U0, pr);
-      tpiece(PosC<0>{}, PosC<2>{}, R0, U0, pr);
-      tpiece(PosC<0>{}, PosC<3>{}, R0, U0, pr);
-      tpiece(PosC<0>{}, PosC<4>{}, R0, U0, pr);
-      tpiece(PosC<1>{}, PosC<0>{}, R0, U0, pr);
-      tpiece(PosC<1>{}, PosC<1>{}, R0, U0, pr);
-      tpiece(PosC<1>{}, PosC<2>{}, R0, U0, pr);
-      tpiece(PosC<1>{}, PosC<3>{}, R0, U0, pr);
-      tpiece(PosC<1>{}, PosC<4>{}, R0, U0, pr);
-    }
-    acc_init(n0);
-    const float lo = a.act == 1 ? 0.f : -__builtin_inff();
-    int s = 0;
-    for (int k = 0;; ++k) {  // tiles of this workgroup: tile k is (b, f0, l0, n0)
-      int t1 = ntile, b1 = 0, f1 = 0, l1 = 0, n1 = 0;  // tile k + 1, decoded at chunk nc - 2
-      for (int c = 0; c < nc; ++c, ++s) {  // chunks of tile k; s counts chunks over the tiles
-        if (s > 0) {
-          if (c == 0) wait_vm<4 * PD + 2 * TH * FN>();  // the previous tile's stores are younger
-          else wait_vm<4 * PD>();  // this wave's DMA pieces of chunk s + 1 landed (only the prefetched weights fly)
-        }
-        lds_barrier();  // U(s) complete, raw(s + 1) landed, U(s + 1) / raw(s + 2) buffers free, tq visible
-        // tile (s + 3) / nc when chunk s + 3 starts it (tiles 0 and 1 came with the prologue)
-        if (tid == 0 && (s + 3) % nc == 0 && s + 3 >= 2 * nc) tq[((s + 3) / nc) & 3] = atomicAdd(wq, 1);
-        if (c == nc - 2) {  // tile k + 1 was taken at chunk (k + 1) * nc - 3
-          t1 = tq[(k + 1) & 3];
-          if (t1 < ntile) decode(t1, b1, f1, l1, n1);
-        }
-        if (c + 2 < nc) dma_at(b, f0, l0, c + 2, R0 + (s & 1) * RAWB);
-        else if (t1 < ntile) dma_at(b1, f1, l1, c + 2 - nc, R0 + (s & 1) * RAWB);
-        const unsigned cs = (unsigned)c * S0;
-        const unsigned cs_next = c + 1 < nc ? cs + S0 : 0u;
-        const unsigned wvo_next = c + 1 < nc ? wvo : wvo_of(t1 < ntile ? n1 : n0);
-        const unsigned char* ub = U0 + (s & 1) * UB;
-        unsigned char* ubn = U0 + ((s + 1) & 1) * UB;
-        const unsigned char* rn = R0 + ((s + 1) & 1) * RAWB;
-        u32x4 pr[4][2];
-        bf16x8 bsets[2][2 * TH];
-        auto bread = [&](auto JC, bf16x8 (&dst)[2 * TH]) __attribute__((always_inline)) {
-          constexpr int j = decltype(JC)::value, p = j / 3, kl = j % 3;
-#pragma unroll
-          for (int i = 0; i < TH; ++i) {
-            const unsigned char* sp = ub + ((i + kl) * 4 + p) * 2048 + rd;
-            dst[2 * i] = *reinterpret_cast<const bf16x8*>(sp);
-            dst[2 * i + 1] = *reinterpret_cast<const bf16x8*>(sp + 256);
-          }
-        };
-        auto step = [&](auto JC) __attribute__((always_inline)) {
-          constexpr int j = decltype(JC)::value, p = j / 3, kl = j % 3;
-          constexpr int jn = (j + PD) % 12, kpn = (jn % 3) * 4 + jn / 3;
-          // weights of step j + PD (the next chunk's first steps for j >= 12 - PD)
-          if constexpr (j + PD < 12) wload(kpn * S1 + cs, wvo, w[(j + PD) % RING]);
-          else wload(kpn * S1 + cs_next, wvo_next, w[(j + PD) % RING]);
-          // transform pieces of chunk s + 1 (unconditional: past the last chunk they fill the idle
-          // buffer): item 0 in steps 0-4, item 1 in steps 5-9
-          if constexpr (j < 5) tpiece(PosC<0>{}, PosC<j>{}, rn, ubn, pr);
-          else if constexpr (j < 10) tpiece(PosC<1>{}, PosC<j - 5>{}, rn, ubn, pr);
-          // B fragments: this step's were read during the previous step; read the next step's now
-          // (not across the chunk's end: U(s + 1) is complete only after the next barrier)
-          bf16x8 (&cur)[2 * TH] = bsets[j & 1];
-          if constexpr (j < 11) bread(PosC<j + 1>{}, bsets[(j + 1) & 1]);
-#pragma unroll
-          for (int prd = 0; prd < 3; ++prd)
-#pragma unroll
-            for (int i = 0; i < TH; ++i)
-#pragma unroll
-              for (int jj = 0; jj < FN; ++jj) {
-                const bf16x8& wv = prd == 0 ? w[j % RING][jj][1] : w[j % RING][jj][0];
-                const bf16x8& x = prd == 1 ? cur[2 * i + 1] : cur[2 * i];
-                acc[i][p][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, x, acc[i][p][jj], 0, 0, 0);
-              }
-        };
-        bread(PosC<0>{}, bsets[0]);
-        step(PosC<0>{}); step(PosC<1>{}); step(PosC<2>{}); step(PosC<3>{});
-        step(PosC<4>{}); step(PosC<5>{}); step(PosC<6>{}); step(PosC<7>{});
-        step(PosC<8>{}); step(PosC<9>{}); step(PosC<10>{}); step(PosC<11>{});
-      }
-      // output transform + act, stored from the fragments: lane (fr, fq) holds pixels 2 fr, 2 fr + 1
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) {
-        const int ch = n0 + (wn * FN + jj) * 16 + fq * 4;
-#pragma unroll
-        for (int i = 0; i < TH; ++i) {
-          float4 y0, y1;
-          float* y0p = &y0.x;
-          float* y1p = &y1.x;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float m0 = acc[i][0][jj][r], m1 = acc[i][1][jj][r], m2 = acc[i][2][jj][r], m3 = acc[i][3][jj][r];
-            y0p[r] = fmaxf((m0 + m1) + m2, lo);
-            y1p[r] = fmaxf((m1 - m2) - m3, lo);
-          }
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            int y, x;
-            pix_yx(f0 + 2 * fr + e, l0 + i, y, x);
-            if (y < a.H && x < a.W)
-              *reinterpret_cast<float4*>(a.out_f + ((long)(b * a.H + y) * a.W + x) * a.ldo + a.co_off + ch) = e ? y1 : y0;
-          }
-        }
-      }
-      if (t1 >= ntile) break;
-      b = b1; f0 = f1; l0 = l1; n0 = n1;
-      wvo = wvo_of(n0);
-      acc_init(n0);
-    }
-    wait_vmcnt0();
-  }
-  __syncthreads();
-  if (tid == 0 && atomicAdd(wq + 1, 1) == (int)gridDim.x - 1) {  // the last workgroup resets the queue
-    atomicExch(wq, 0);
-    atomicExch(wq + 1, 0);
-  }
-}
-
-// grid: one workgroup per CU (the LDS allows no second one), fewer for small layers
-int launch_winop(const WinoArgs& a, bool cm, int* wq, hipStream_t stream) {
-  if (a.N % 128 || a.Cin < 64 || !wq || a.uni) return (int)hipErrorInvalidValue;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      ncu = 256;
-  }
-  const int FH = cm ? a.H : a.W, LW = cm ? a.W : a.H;
-  const long ntile = (long)a.B * ((FH + 31) / 32) * ((LW + 3) / 4) * (a.N / 128);
-  if (ntile <= 0 || ntile >= (1L << 30)) return (int)hipErrorInvalidValue;
-  const unsigned grid = (unsigned)(ntile < ncu ? ntile : ncu);
-  if (cm) conv_winop_kernel<true><<<grid, 256, 0, stream>>>(a, wq);
-  else conv_winop_kernel<false><<<grid, 256, 0, stream>>>(a, wq);
-  return (int)hipGetLastError();
-}
-
 }  // namespace
 
 // fp32 mode, 3x3 stride 1 pad 1 by F(2,3) (conv_wino_kernel).  in / out: pair storage
@@ -731,22 +438,4 @@ TCA_API int tca_conv_wino(const float* in, int B, int H, int W, int Cin, int ldi
   a.N = N; a.ldo = ldo; a.co_off = co_off; a.act = act;
   a.uni = uni; a.uni_val = uni_val; a.uni_min = uni ? uni_min : 0;
   return wino_launch(a, tile, pair_in != 0, pair_out != 0, stream);
-}
-
-// persistent F(2,3) (conv_winop_kernel): fp32 storage in and out, N % 128 == 0, Cin >= 64, no uniform
-// skipping.  wq: two int32 on the device, zero before the first launch (the kernel leaves them zero);
-// one queue per call site that may run concurrently with another.  cm: F(2,3) along y (1) or x (0).
-TCA_API int tca_conv_winop(const float* in, int B, int H, int W, int Cin, int ldi, int ci_off, const void* wfrag,
-                           const float* bias, int N, float* out, int ldo, int co_off, int act, int cm, int* wq,
-                           hipStream_t stream) {
-  if (B <= 0) return 0;
-  if ((Cin & 31) || (ldi & 7) || (ci_off & 7) || (N & 127) || (ldo & 3) || (co_off & 3)) return (int)hipErrorInvalidValue;
-  if (act != 0 && act != 1) return (int)hipErrorInvalidValue;
-  if ((long)B * H * W * ldi * 4 >= (1L << 31) || (long)B * H * W * ldo >= (1L << 31)) return (int)hipErrorInvalidValue;
-  WinoArgs a;
-  a.in_f = in; a.out_f = out; a.w = wfrag; a.bias = bias;
-  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.ldi = ldi; a.ci_off = ci_off;
-  a.N = N; a.ldo = ldo; a.co_off = co_off; a.act = act;
-  a.uni = nullptr; a.uni_val = nullptr; a.uni_min = 0;
-  return launch_winop(a, cm != 0, wq, stream);
 }

@@ -71,7 +71,6 @@ _KERNEL_SIGS = {
     "tca_conv_nhwc_x3p": [P, I, I, I, I, I, I, P, P, I, I, I, I, I, I, P, I, I, I, I, I, P, I, I, I, I, I, P],
     # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, res, ldr, r_off, tile, stream
     "tca_conv_wino": [P, I, I, I, I, I, I, I, P, P, I, P, I, I, I, I, P, I, P, I, P],
-    "tca_conv_winop": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, I, P, P],
     "tca_conv_hx3p": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, I, I, P],
     # in, B, H, W, Cin, ldi, ci_off, wfrag, bias, N, out, ldo, co_off, act, uni, uni_min, uni_val, tile, stream
     "tca_conv_hx3p_uni": [P, I, I, I, I, I, I, P, P, I, P, I, I, I, P, I, P, I, P],

@@ -123,12 +123,6 @@ S2SP_TILES = (140, 141, 142)
 S2SP_TILE = int(os.environ.get("TCA_S2SP_TILE", "0"))
 WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
 WINO_TILES = (130, 131, 132, 133, 134)
-# the persistent F(2,3) kernel (conv_wino.hip conv_winop_kernel: one workgroup per CU, work queue,
-# double-buffered halo / transform, the transform interleaved into the MFMA steps) for the fp32-storage
-# layers inside a block (N % 128 == 0, Cin >= 64); tiles 137 (F along x) / 138 (along y) select it
-# explicitly, TCA_WINOP=1 routes the auto tile there.
-WINOP = os.environ.get("TCA_WINOP", "0") == "1"
-WINOP_TILES = (137, 138)
 
 
 def wino_tile(H: int, W: int, N: int) -> int:
@@ -288,7 +282,7 @@ class FusedConv:
         rp = (_native.ptr(res.t if res is not None else None), res.t.shape[-1] if res is not None else 0,
               res.off if res is not None else 0)
         if (x.occ is None and res is None and self.wino_ok() and not self.transpose and
-                (tile in WINO_TILES or tile in WINOP_TILES or (tile == 0 and WINO))):
+                (tile in WINO_TILES or (tile == 0 and WINO))):
             # F(2,3) stride-1 kernel: pair or fp32 storage on either side
             return self._wino(x, out, tile, stream, uni)
         if x.pair or out.pair:
@@ -370,8 +364,6 @@ class FusedConv:
 
     def _wino(self, x: NHWC, out: NHWC, tile: int, stream, uni) -> NHWC:
         B, H, W, _ = x.shape
-        if tile in WINOP_TILES or (WINOP and tile not in WINO_TILES[1:] and self.winop_ok(x, out, uni)):
-            return self._winop(x, out, tile, stream)
         t = tile - 130 if tile in WINO_TILES[1:] else wino_tile(H, W, self.N)
         cm = t in (2, 4)
         if not hasattr(self, "_w_wino"):
@@ -387,28 +379,6 @@ class FusedConv:
                      _native.ptr(wf), _native.ptr(self.b_gemm), self.N, _native.ptr(out.t), out.t.shape[-1], out.off,
                      int(out.pair), self.act, _native.ptr(depth), dmin, _native.ptr(val), t,
                      _native.stream_ptr(stream))
-        return out
-
-    def winop_ok(self, x: NHWC, out: NHWC, uni=None) -> bool:
-        """The persistent F(2,3) kernel takes this call: fp32 storage in and out, no uniform-tile map,
-        N % 128 == 0, Cin >= 64, 16-B aligned output slices."""
-        return (not x.pair and not out.pair and uni is None and self.N % 128 == 0 and self.cin_p >= 64
-                and out.t.shape[-1] % 4 == 0 and out.off % 4 == 0)
-
-    def _winop(self, x: NHWC, out: NHWC, tile: int, stream) -> NHWC:
-        B, H, W, _ = x.shape
-        assert self.winop_ok(x, out), "tca_conv_winop: fp32 storage, N % 128 == 0, Cin >= 64"
-        cm = tile == 138 if tile in WINOP_TILES else wino_tile(H, W, self.N) in (2, 4)
-        if not hasattr(self, "_w_wino"):
-            self._w_wino = {}
-        wf = self._w_wino.get(cm)
-        if wf is None:
-            wf = self._w_wino[cm] = wino_weights(self.w_f32_gemm, self.cin_p, cm).to(self.device)
-        if getattr(self, "_wq", None) is None:  # the work queue: zero, and left zero by every launch
-            self._wq = torch.zeros(2, dtype=torch.int32, device=self.device)
-        _native.call("tca_conv_winop", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
-                     _native.ptr(wf), _native.ptr(self.b_gemm), self.N, _native.ptr(out.t), out.t.shape[-1], out.off,
-                     self.act, int(cm), _native.ptr(self._wq), _native.stream_ptr(stream))
         return out
 
     def hx3_weights(self) -> torch.Tensor:
