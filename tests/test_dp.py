@@ -138,7 +138,8 @@ def _fault_worker(rank, world, port, q):
         from triton_client_amd.parallel.dp import DataParallelDetector2D, HealthMonitor, init_distributed
 
         info = init_distributed("gloo")
-        mon = HealthMonitor(info, interval=0.1, timeout=1.0)
+        # a 2 s heartbeat timeout: a loaded CI host can hold a healthy rank's 0.1 s beat past 1 s
+        mon = HealthMonitor(info, interval=0.1, timeout=2.0)
         dp = DataParallelDetector2D(FakeDetector(), info, max_det=8, monitor=mon)
         frames = [np.full((8, 12, 3), 7 * i, np.uint8) for i in range(9)]
         want = FakeDetector().detect(frames)
@@ -147,7 +148,7 @@ def _fault_worker(rank, world, port, q):
             assert all(np.array_equal(a, b) for a, b in zip(got, want))
             assert mon.alive() == [0, 1, 2]
             q.put((2, "wait"))  # let rank 2 die before the next batch
-            time.sleep(2.5)
+            time.sleep(4.5)
             for _ in range(2):
                 got = dp.detect(frames)
                 assert all(np.array_equal(a, b) for a, b in zip(got, want))
