@@ -588,16 +588,18 @@ int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, con
                                      batch, max_voxels, P, W, bias, g, canvas, feat_out, dt, occ, stream);
 }
 
-// 0: the fp32 VALU kernel, one pillar per wave iteration; 1: the split-bf16 MFMA kernel
-// (TCA_VFE_MFMA=1; kept for A/B and its tests); 2: the fp32 VALU kernel, two pillars per wave
-// iteration (TCA_VFE_LIN2=1).  tca_pillar_vfe_set_variant switches at run time.
+// 0: the fp32 VALU kernel, one pillar per wave iteration (TCA_VFE_LIN2=0); 1: the split-bf16 MFMA
+// kernel (TCA_VFE_MFMA=1; kept for A/B and its tests); 2 (default since round 6): the fp32 VALU kernel,
+// two pillars per wave iteration -- bit-identical to 0, 119 vs 141 us alone at the headline batch and
+// +0.4 / +0.5% on the headline in two same-box sweeps of the final tree (profiles/r6/knobs/).
+// tca_pillar_vfe_set_variant switches at run time.
 int g_vfe_variant = -1;
 
 int vfe_variant() {
   if (g_vfe_variant < 0) {
     const char* e = getenv("TCA_VFE_MFMA");
     const char* e2 = getenv("TCA_VFE_LIN2");
-    g_vfe_variant = (e && e[0] == '1') ? 1 : (e2 && e2[0] == '1') ? 2 : 0;
+    g_vfe_variant = (e && e[0] == '1') ? 1 : (e2 && e2[0] == '0') ? 0 : 2;
   }
   return g_vfe_variant;
 }

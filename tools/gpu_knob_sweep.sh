@@ -1,0 +1,25 @@
+# Same-box sweep of the step's existing switches: ROUNDS rounds, every config once per round in a rotated
+# order, 30 timed steps each; tools/knob_table.py prints the per-config medians.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+TAG=${TAG:-knobs}
+ROUNDS=${ROUNDS:-5}
+mkdir -p gpurun_out/r6/$TAG
+if [ "${SET:-1}" = "2" ]; then  # the follow-up on another box: the two candidates and both together
+  CONFIGS=("default||" "neck2|TCA_NECK_VARIANT=2|" "vfelin2|TCA_VFE_LIN2=1|" "both|TCA_NECK_VARIANT=2 TCA_VFE_LIN2=1|")
+elif [ "${SET:-1}" = "3" ]; then  # after both became the default: against the previous defaults
+  CONFIGS=("default||" "r6start|TCA_NECK_VARIANT=0 TCA_VFE_LIN2=0|")
+else
+  CONFIGS=("default||" "neck1|TCA_NECK_VARIANT=1|" "neck2|TCA_NECK_VARIANT=2|" "pipe2||--lidar-pipeline 2"
+           "pipe4||--lidar-pipeline 4" "wino64|TCA_WINO_MIN_N=64|" "vfelin2|TCA_VFE_LIN2=1|" "split||--graph-mode split")
+fi
+n=${#CONFIGS[@]}
+for k in $(seq 1 $ROUNDS); do
+  for i in $(seq 0 $((n - 1))); do
+    c=${CONFIGS[$(( (i + k) % n ))]}
+    name=${c%%|*}; rest=${c#*|}; envs=${rest%%|*}; flags=${rest#*|}
+    env $envs timeout -k 10 300 python bench.py --steps 30 --warmup 5 $flags > gpurun_out/r6/$TAG/${name}_$k.log 2>&1 || { echo "BENCH_FAILED $name"; tail -20 gpurun_out/r6/$TAG/${name}_$k.log; exit 1; }
+    echo "$name $k $(tail -1 gpurun_out/r6/$TAG/${name}_$k.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'])")"
+  done
+done

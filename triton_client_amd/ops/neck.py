@@ -77,12 +77,11 @@ class FusedNeckHead:
             grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
         # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = <8 waves, 2 stages>, 99.6 KiB LDS; 1 = <8, 3>,
-        # 149 KiB.  Alone, 1 is faster (977 vs 1061 us at batch 32, profiles/r5/neck_ab.log); in the headline
-        # step, where the neck runs beside the VFE and the camera's first kernels, 0 leaves them LDS on every
-        # CU: 4658 vs 4635 frame pairs/s over six same-box pairs (profiles/r5/neck_variant_ab.txt).  2 = <4, 2>
-        # (two workgroups per CU) is the fastest alone (883 vs 1056 us) but not in the step: 4617 vs 4652
-        # (profiles/r5/neck_variant2_ab.txt)
-        self.variant = int(os.environ.get("TCA_NECK_VARIANT", "0"))
+        # 149 KiB; 2 = <4, 2>, two workgroups per CU (66 KiB each), the fastest alone (883 vs 1056 us).  In
+        # round 5's step 0 measured best (4652 vs 4617 for 2, profiles/r5/neck_variant2_ab.txt); with round 6's
+        # front and VFE beside it, 2 is ahead on two boxes: +1.2% and +0.6% over 5-6 alternating rounds each
+        # (profiles/r6/knobs/), so it is the default now
+        self.variant = int(os.environ.get("TCA_NECK_VARIANT", "2"))
         wh = permute_head_weight(head.w_f32_gemm[:, : head.Kp].float())
         if self.precision == "fp32":
             self.wh = split_pairs(wh).to(device)
