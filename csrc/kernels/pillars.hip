@@ -595,6 +595,17 @@ int launch_vfe(const float* pts, int pstride, int max_pts, const int* slots, con
 // tca_pillar_vfe_set_variant switches at run time.
 int g_vfe_variant = -1;
 
+// workgroups of the encoder launch: 2048 (8 per CU), TCA_VFE_GRID overrides for sweeps
+int vfe_grid() {
+  static int g = 0;
+  if (!g) {
+    const char* e = getenv("TCA_VFE_GRID");
+    g = e ? atoi(e) : 0;
+    g = g >= 64 && g <= 65536 ? g : 2048;
+  }
+  return g;
+}
+
 int vfe_variant() {
   if (g_vfe_variant < 0) {
     const char* e = getenv("TCA_VFE_MFMA");
@@ -610,7 +621,7 @@ int launch_vfe_t(const float* pts, int pstride, int max_pts, const int* slots, c
                  const float* W, const float* bias, const PillarGeom& g, void* canvas, float* feat_out, int dt,
                  uint8_t* occ, hipStream_t stream) {
 #define TCA_VFE_LAUNCH(KERNEL, CT)                                                                                 \
-  KERNEL<FROM_SLOTS, CT, PFIX><<<2048, 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels, num_points, \
+  KERNEL<FROM_SLOTS, CT, PFIX><<<vfe_grid(), 256, 0, stream>>>(pts, pstride, max_pts, slots, vcount, voxels, num_points, \
                                                         coords, voxel_count, batch, max_voxels, P, W, bias, g,      \
                                                         (CT*)canvas, feat_out, occ)
   const int var = vfe_variant();

@@ -10,6 +10,10 @@ if [ "${SET:-1}" = "2" ]; then  # the follow-up on another box: the two candidat
   CONFIGS=("default||" "neck2|TCA_NECK_VARIANT=2|" "vfelin2|TCA_VFE_LIN2=1|" "both|TCA_NECK_VARIANT=2 TCA_VFE_LIN2=1|")
 elif [ "${SET:-1}" = "3" ]; then  # after both became the default: against the previous defaults
   CONFIGS=("default||" "r6start|TCA_NECK_VARIANT=0 TCA_VFE_LIN2=0|")
+elif [ "${SET:-1}" = "4" ]; then  # launch shapes and tiles (TCA_VFE_GRID, TCA_NECK_GRID, TCA_*_TILE)
+  CONFIGS=("default||" "vfeg1024|TCA_VFE_GRID=1024|" "vfeg4096|TCA_VFE_GRID=4096|" "neckg192|TCA_NECK_GRID=192|"
+           "neckg224|TCA_NECK_GRID=224|" "hx3t5|TCA_HX3_TILE=5|" "hx3t4|TCA_HX3_TILE=4|" "winot1|TCA_WINO_TILE=1|"
+           "lazy0|TCA_LAZY_CANVAS=0|" "s2sp|TCA_S2SP=1|")
 else
   CONFIGS=("default||" "neck1|TCA_NECK_VARIANT=1|" "neck2|TCA_NECK_VARIANT=2|" "pipe2||--lidar-pipeline 2"
            "pipe4||--lidar-pipeline 4" "wino64|TCA_WINO_MIN_N=64|" "vfelin2|TCA_VFE_LIN2=1|" "split||--graph-mode split")

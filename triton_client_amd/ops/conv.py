@@ -123,6 +123,11 @@ S2SP_TILES = (140, 141, 142)
 S2SP_TILE = int(os.environ.get("TCA_S2SP_TILE", "0"))
 WINO_MIN_N = int(os.environ.get("TCA_WINO_MIN_N", "128"))  # narrower layers stay on hx3 (A/B: profiles/r5/wino_ab.md)
 WINO_TILES = (130, 131, 132, 133, 134)
+# sweep overrides of the auto tile choice (tools/gpu_knob_sweep.sh): hx3_launch / hx3s2_launch / wino_launch tile
+# numbers applied where the caller asked for tile 0; unset = the kernels' own choice
+HX3_TILE_AUTO = int(os.environ.get("TCA_HX3_TILE", "0"))
+HX3S2_TILE_AUTO = int(os.environ.get("TCA_HX3S2_TILE", "0"))
+WINO_TILE_AUTO = int(os.environ.get("TCA_WINO_TILE", "0"))
 
 
 def wino_tile(H: int, W: int, N: int) -> int:
@@ -308,7 +313,7 @@ class FusedConv:
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act | (0 if out.pair else 32), *rp,
                              _native.ptr(occ), *self._uni_args(uni, B, Ho, Wo, res),
-                             tile - 120 if tile in HX3S2_TILES else 0, _native.stream_ptr(stream))
+                             tile - 120 if tile in HX3S2_TILES else HX3S2_TILE_AUTO, _native.stream_ptr(stream))
                 return out
             if (out.pair and x.occ is None and self.hx3_ok() and self.s == 1 and
                     (tile in HX3_TILES or (tile == 0 and HX3))):
@@ -319,13 +324,13 @@ class FusedConv:
                     _native.call("tca_conv_hx3p_uni", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                                  _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                                  _native.ptr(out.t), out.t.shape[-1], out.off, act, _native.ptr(depth), dmin,
-                                 _native.ptr(val), tile - 110 if tile in HX3_TILES else 0,
+                                 _native.ptr(val), tile - 110 if tile in HX3_TILES else HX3_TILE_AUTO,
                                  _native.stream_ptr(stream))
                     return out
                 _native.call("tca_conv_hx3p", _native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off,
                              _native.ptr(self.hx3_weights()), _native.ptr(self.b_gemm), self.N,
                              _native.ptr(out.t), out.t.shape[-1], out.off, act, *rp,
-                             tile - 110 if tile in HX3_TILES else 0, _native.stream_ptr(stream))
+                             tile - 110 if tile in HX3_TILES else HX3_TILE_AUTO, _native.stream_ptr(stream))
                 return out
             args = (_native.ptr(x.t), B, H, W, self.cin_p, x.t.shape[-1], x.off, _native.ptr(self.w_gemm),
                     _native.ptr(self.b_gemm), self.N, self.k, self.k, self.s, self.p, self.Kp, _native.ptr(out.t), gh,
@@ -364,7 +369,7 @@ class FusedConv:
 
     def _wino(self, x: NHWC, out: NHWC, tile: int, stream, uni) -> NHWC:
         B, H, W, _ = x.shape
-        t = tile - 130 if tile in WINO_TILES[1:] else wino_tile(H, W, self.N)
+        t = tile - 130 if tile in WINO_TILES[1:] else (WINO_TILE_AUTO or wino_tile(H, W, self.N))
         cm = t in (2, 4)
         if not hasattr(self, "_w_wino"):
             self._w_wino = {}

@@ -74,7 +74,8 @@ class FusedNeckHead:
         self.nh = head.N
         # persistent kernel: one workgroup per CU (a multiple of 8: tiles are split per XCD)
         if grid <= 0:
-            grid = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+            grid = int(os.environ.get("TCA_NECK_GRID", "0")) or \
+                torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
         self.grid = max(8, grid // 8 * 8)
         # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = <8 waves, 2 stages>, 99.6 KiB LDS; 1 = <8, 3>,
         # 149 KiB; 2 = <4, 2>, two workgroups per CU (66 KiB each), the fastest alone (883 vs 1056 us).  In
