@@ -75,7 +75,7 @@ def parse():
                          "(models/fast.py DETECT_FUSED; A/B)")
     ap.add_argument("--dense-bev", action="store_true",
                     help="PointPillars first block without uniform-tile skipping (models/fast.py BEV_UNIFORM; A/B)")
-    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3, 4],
+    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3, 4, 5],
                     help="LiDAR software pipeline over two LidarPipelines sharing one model (double-buffered "
                          "graphs only; every step still runs one full batch through every stage, results come "
                          "out one step later). 0: off. 1: network + NMS of batch t beside preprocessing of "
@@ -83,7 +83,10 @@ def parse():
                          "3 (default): preprocessing + down blocks of batch t beside the fused neck + head + "
                          "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/). "
                          "4: as 3 with the last down block in the back half too (bit-identical; 3241-3267 vs "
-                         "4699-4792 frame pairs/s: its convs starve the camera, profiles/r5/split4/)")
+                         "4699-4792 frame pairs/s: its convs starve the camera, profiles/r5/split4/). 5: the "
+                         "down blocks of batch t alone beside the fused neck + head + decode + NMS of batch t-1 "
+                         "and then the preprocessing (unpack, voxeliser, PillarVFE) of batch t+1: the front leaves "
+                         "the critical stream; detections come out two steps after ingest")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
@@ -479,7 +482,7 @@ def main():
     # two captured graphs over two input sets: the prefetch writes straight into the set the next
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
     d2h_stage = None
-    piped = post_split = False
+    piped = post_split = front_next = False
     # (not with the RCCL gather captured in the step graph: two graphs replaying the same
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
@@ -500,6 +503,7 @@ def main():
             for lp in lids:
                 lp.build_fast()
             blocks_front = len(lids[0].fast.bb.blocks) - 1 if args.lidar_pipeline == 4 else None
+            front_next = args.lidar_pipeline == 5
             side2 = torch.cuda.Stream()
             lside = side if side is not None else torch.cuda.Stream()
             # (the canvas clear moved from the front into the back half: 7.60 vs 7.60 ms, not kept;
@@ -512,7 +516,13 @@ def main():
                     main = torch.cuda.current_stream()
                     lside.wait_stream(main)
                     side2.wait_stream(main)
-                    if post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
+                    if front_next:  # graph k: pipeline k's blocks beside pipeline 1-k's neck / NMS + next front
+                        with torch.cuda.stream(lside):
+                            lids[k].step_blocks()
+                        with torch.cuda.stream(side2):
+                            r3 = lids[1 - k].step_back()
+                            lids[1 - k].step_pre()
+                    elif post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
                         with torch.cuda.stream(lside):
                             lids[k].step_front(neck_back=args.lidar_pipeline >= 3, blocks_front=blocks_front)
                         with torch.cuda.stream(side2):
@@ -539,7 +549,7 @@ def main():
             if not piped:
                 return list(zip(in_sets[k], host_src))
             pairs = [(in_sets[k][0], host_src[0])] if use_cam else []
-            p = k if post_split else 1 - k  # the pipeline whose preprocessing graph k runs
+            p = k if post_split and not front_next else 1 - k  # the pipeline whose preprocessing graph k runs
             return pairs + [(lids[p].data, pc_host[0]), (lids[p].frame_n, n_host[0])]
 
         def stage_copy(dst_, src_):
@@ -603,8 +613,13 @@ def main():
             db_h2d(k)  # both sets hold valid frames before either graph's eager warm-up reads them
         torch.cuda.synchronize()
         if piped:  # prologue: graph 0's first replay finishes a batch of pipeline 0 (mode 1) / 1 (mode 2)
-            lids[1].step_front(neck_back=args.lidar_pipeline >= 3, blocks_front=blocks_front) if post_split \
-                else lids[0].step_pre()
+            if front_next:  # mode 5: pipeline 0's canvas and pipeline 1's down blocks
+                lids[0].step_pre()
+                lids[1].step_front(neck_back=True)
+            elif post_split:
+                lids[1].step_front(neck_back=args.lidar_pipeline >= 3, blocks_front=blocks_front)
+            else:
+                lids[0].step_pre()
             torch.cuda.synchronize()
 
         class _DoubleBuffered:
@@ -851,7 +866,8 @@ def main():
                 "branch_streams": (3 if piped else 2) if side is not None else 1,
                 "graph_mode": args.graph_mode if side is not None else "single",
                 "graph_input_sets": 2 if db else 1,
-                "lidar_pipelined": (["off", "pre", "post", "neck", "block3"][args.lidar_pipeline] if piped else "off"),
+                "lidar_pipelined": (["off", "pre", "post", "neck", "block3", "neck+next_front"][args.lidar_pipeline]
+                                    if piped else "off"),
                 "lidar_pipeline_note": ("two LiDAR pipelines alternate: each timed step runs one full batch through "
                                         "every stage, one batch's first half beside the previous batch's second "
                                         "half (split point: lidar_pipelined); detections leave one step later"

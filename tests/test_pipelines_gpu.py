@@ -142,6 +142,62 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, blocks_front)
             assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)
 
 
+def test_lidar_front_next_pipelining_matches_step(cuda):
+    """bench.py --lidar-pipeline 5: pipeline A's down blocks on one stream beside pipeline B's
+    neck + head + decode + NMS and then B's preprocessing of its NEXT batch on another; the two
+    pipelines swap roles every step.  Every batch gets exactly the detections of a plain step()."""
+    spec = LidarSpec(rings=32, azimuth_steps=1024, sensor_height=3.23)
+    la = LidarPipeline(batch=2, max_points=32768, device=cuda)
+    _load_lidar(la, spec, [5, 6])
+    la.calibrate_detection_density(500.0)
+    lb = LidarPipeline(la.model, batch=2, max_points=32768, device=cuda)
+
+    def snap(r):
+        return [t.clone() for t in (r.box, r.score, r.count)]
+
+    seeds = {"a1": [5, 6], "b1": [7, 8], "a2": [7, 8], "b2": [5, 6]}
+    ref = {}
+    for name in ("a1", "b1", "a2", "b2"):
+        lp = la if name[0] == "a" else lb
+        _load_lidar(lp, spec, seeds[name])
+        ref[name] = snap(lp.step())
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    # prologue: A's canvas (a1), B's down blocks (b1)
+    _load_lidar(la, spec, seeds["a1"])
+    _load_lidar(lb, spec, seeds["b1"])
+    la.step_pre()
+    lb.step_front(neck_back=True)
+    torch.cuda.synchronize()
+    got = {}
+    # step k: X = blocks on s1, Y = back + next front on s2; Y's data holds its next batch
+    plan = [(la, lb, "b1", "b2"), (lb, la, "a1", "a2"), (la, lb, "b2", None), (lb, la, "a2", None)]
+    for x, y, done, nxt in plan:
+        if nxt is not None:
+            _load_lidar(y, spec, seeds[nxt])
+        torch.cuda.synchronize()
+        s1.wait_stream(main)
+        s2.wait_stream(main)
+        with torch.cuda.stream(s1):
+            x.step_blocks()
+        with torch.cuda.stream(s2):
+            got[done] = snap(y.step_back())
+            if nxt is not None:
+                y.step_pre()
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+        torch.cuda.synchronize()
+    for name in ref:
+        r, g = ref[name], got[name]
+        assert int(r[2].sum()) > 0, name
+        for b in range(2):
+            n = int(r[2][b])
+            assert n == int(g[2][b]), (name, b)
+            assert torch.equal(r[0][b, :n], g[0][b, :n]), (name, b)
+            assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)
+
+
 @pytest.mark.parametrize("lazy", [True, False], ids=["occ_clear", "full_clear"])
 def test_lidar_occupancy_only_clear_matches_fresh_pipeline(cuda, monkeypatch, lazy):
     """With the fast plan's first conv gating its canvas loads on the occupancy bytes, a frame's

@@ -10,6 +10,9 @@ if [ "${SET:-1}" = "2" ]; then  # the follow-up on another box: the two candidat
   CONFIGS=("default||" "neck2|TCA_NECK_VARIANT=2|" "vfelin2|TCA_VFE_LIN2=1|" "both|TCA_NECK_VARIANT=2 TCA_VFE_LIN2=1|")
 elif [ "${SET:-1}" = "3" ]; then  # after both became the default: against the previous defaults
   CONFIGS=("default||" "r6start|TCA_NECK_VARIANT=0 TCA_VFE_LIN2=0|")
+elif [ "${SET:-1}" = "5" ]; then  # the LiDAR software-pipeline split points
+  CONFIGS=("default||" "pipe5||--lidar-pipeline 5" "pipe1||--lidar-pipeline 1" "lidar3||--only lidar"
+           "lidar5||--only lidar --lidar-pipeline 5")
 elif [ "${SET:-1}" = "4" ]; then  # launch shapes and tiles (TCA_VFE_GRID, TCA_NECK_GRID, TCA_*_TILE)
   CONFIGS=("default||" "vfeg1024|TCA_VFE_GRID=1024|" "vfeg4096|TCA_VFE_GRID=4096|" "neckg192|TCA_NECK_GRID=192|"
            "neckg224|TCA_NECK_GRID=224|" "hx3t5|TCA_HX3_TILE=5|" "hx3t4|TCA_HX3_TILE=4|" "winot1|TCA_WINO_TILE=1|"

@@ -8,6 +8,8 @@ the captured step; everything else is ``bench.py`` unchanged (same flags).
   WHATIF=novox   the LiDAR unpack + voxeliser chain (pc2_unpack, canvas clear, assign, finish):
                  only the PillarVFE scatter runs, over the slots of the warm-up batches
   WHATIF=nofront the whole LiDAR front (voxeliser + PillarVFE): the BEV blocks read a stale canvas
+  WHATIF=nopost  the LiDAR anchor decode + rotated NMS: the step returns the warm-up batches' result
+  WHATIF=noneck  the fused neck + head: the decode + NMS read the warm-up batches' head maps
 
     WHATIF=novox python tools/whatif_bench.py --steps 30 --warmup 5
 """
@@ -46,10 +48,26 @@ def main():
             return self.enc.encode_from_slots(self._whatif_pts, self.vox)
         return self.enc.canvas_nchw()  # nofront
 
+    @torch.no_grad()
+    def step_back(self):
+        n = getattr(self, "_whatif_back", 0)
+        self._whatif_back = n + 1
+        if n < warm:  # LidarPipeline.step_back
+            head = self._head if self._blocks is None else self.fast.forward_neck(self._blocks)
+            self._whatif_res = self.post(*head)
+            return self._whatif_res
+        if mode == "nopost":
+            if self._blocks is not None:
+                self.fast.forward_neck(self._blocks)
+            return self._whatif_res
+        return self.post(*self.fast.head_maps())  # noneck
+
     if mode in ("novox", "nofront"):
         lidar_mod.LidarPipeline.step_pre = step_pre
+    elif mode in ("nopost", "noneck"):
+        lidar_mod.LidarPipeline.step_back = step_back
     elif mode:
-        raise SystemExit(f"WHATIF={mode!r}: novox or nofront")
+        raise SystemExit(f"WHATIF={mode!r}: novox, nofront, nopost or noneck")
     import bench
     bench.main()
 

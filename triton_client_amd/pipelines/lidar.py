@@ -145,14 +145,22 @@ class LidarPipeline:
         (--lidar-pipeline 3): stop after the down blocks; step_back runs the fused neck +
         head as well.  blocks_front (--lidar-pipeline 4): only the first blocks_front down
         blocks here; step_back runs the rest before the neck."""
-        canvas = self.step_pre()
+        self.step_pre()
+        self.step_blocks(neck_back, blocks_front)
+
+    @torch.no_grad()
+    def step_blocks(self, neck_back: bool = True, blocks_front: Optional[int] = None):
+        """The BEV network over the canvas the last step_pre filled (the down blocks only with
+        neck_back; step_back finishes the batch).  bench.py --lidar-pipeline 5 runs it alone on the
+        critical stream: this pipeline's next step_pre then runs after its step_back, beside the
+        other pipeline's blocks."""
         self._blocks = self._head = None
         if self.use_fast and neck_back and self.fast.neck is not None:
             self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc(), blocks_front)
         elif self.use_fast:
             self._head = self.fast.forward(self.enc.canvas_nhwc())
         else:
-            self._head = self.model.bev_forward(canvas)
+            self._head = self.model.bev_forward(self.enc.canvas_nchw())
 
     @torch.no_grad()
     def step_back(self):
