@@ -75,18 +75,19 @@ def parse():
                          "(models/fast.py DETECT_FUSED; A/B)")
     ap.add_argument("--dense-bev", action="store_true",
                     help="PointPillars first block without uniform-tile skipping (models/fast.py BEV_UNIFORM; A/B)")
-    ap.add_argument("--lidar-pipeline", type=int, default=3, choices=[0, 1, 2, 3, 4, 5],
+    ap.add_argument("--lidar-pipeline", type=int, default=5, choices=[0, 1, 2, 3, 4, 5],
                     help="LiDAR software pipeline over two LidarPipelines sharing one model (double-buffered "
                          "graphs only; every step still runs one full batch through every stage, results come "
                          "out one step later). 0: off. 1: network + NMS of batch t beside preprocessing of "
                          "batch t+1. 2: preprocessing + network of batch t beside decode + NMS of batch t-1. "
-                         "3 (default): preprocessing + down blocks of batch t beside the fused neck + head + "
+                         "3: preprocessing + down blocks of batch t beside the fused neck + head + "
                          "decode + NMS of batch t-1 (7.27-7.44 vs 8.0 ms per step off; profiles/r3/lpipe/). "
                          "4: as 3 with the last down block in the back half too (bit-identical; 3241-3267 vs "
-                         "4699-4792 frame pairs/s: its convs starve the camera, profiles/r5/split4/). 5: the "
-                         "down blocks of batch t alone beside the fused neck + head + decode + NMS of batch t-1 "
-                         "and then the preprocessing (unpack, voxeliser, PillarVFE) of batch t+1: the front leaves "
-                         "the critical stream; detections come out two steps after ingest")
+                         "4699-4792 frame pairs/s: its convs starve the camera, profiles/r5/split4/). 5 "
+                         "(default since round 6): the down blocks of batch t alone beside the fused neck + head + "
+                         "decode + NMS of batch t-1 and then the preprocessing (unpack, voxeliser, PillarVFE) of "
+                         "batch t+1: the front leaves the critical stream, +0.9%% over 3 on two boxes "
+                         "(profiles/r6/knobs/); detections come out two steps after ingest")
     ap.add_argument("--single-input-set", action="store_true",
                     help="one set of graph inputs (prefetch into landing buffers + a D2D copy per step) instead "
                          "of two captured graphs alternating over two input sets")
@@ -868,9 +869,13 @@ def main():
                 "graph_input_sets": 2 if db else 1,
                 "lidar_pipelined": (["off", "pre", "post", "neck", "block3", "neck+next_front"][args.lidar_pipeline]
                                     if piped else "off"),
-                "lidar_pipeline_note": ("two LiDAR pipelines alternate: each timed step runs one full batch through "
-                                        "every stage, one batch's first half beside the previous batch's second "
-                                        "half (split point: lidar_pipelined); detections leave one step later"
+                "lidar_pipeline_note": (("two LiDAR pipelines alternate: each timed step runs one full batch "
+                                         "through every stage: batch t's down blocks beside batch t-1's neck, "
+                                         "head, decode and NMS followed by batch t+1's preprocessing; "
+                                         "detections leave two steps after ingest") if piped and front_next else
+                                        ("two LiDAR pipelines alternate: each timed step runs one full batch through "
+                                         "every stage, one batch's first half beside the previous batch's second "
+                                         "half (split point: lidar_pipelined); detections leave one step later")
                                         if piped else None),
                 "host_bytes_per_gpu_per_step": step_bytes,
                 "dp_comm_us_per_step": comm_us,
