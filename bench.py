@@ -406,6 +406,14 @@ def main():
             print(f"[bench] rank {info.rank}: native RCCL communicator unavailable ({e}); "
                   f"using torch.distributed p2p", file=sys.stderr, flush=True)
             native = None
+        if native is not None:
+            # the step's gather pattern, eager and in two alternately replayed graphs, under a time
+            # limit: a communicator that cannot run it is aborted and the process group serves instead
+            from triton_client_amd.parallel.rccl import native_selftest
+            ok_, why = native_selftest(native, info.rank, info.world)
+            print(f"[bench] rank {info.rank}: native RCCL self-test: {why}", file=sys.stderr, flush=True)
+            if not ok_:
+                native = None
         import torch.distributed as dist
         ok = torch.tensor([1 if native is not None else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same path

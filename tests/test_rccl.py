@@ -181,3 +181,18 @@ def test_native_gather_plan_in_two_double_buffered_graphs():
         for r in runs:  # the graphs go before the communicator (GraphRunner.release)
             r.release()
         comm.abort()
+
+
+@pytest.mark.gpu
+def test_native_selftest_world1():
+    """bench.py's pre-flight of the native communicator (parallel/rccl.py native_selftest): the
+    gather plan eagerly and in two alternately replayed graphs, values checked on rank 0."""
+    from triton_client_amd.parallel.rccl import NativeComm, native_selftest
+
+    torch.cuda.set_device(0)
+    comm = NativeComm(0, 1)
+    try:
+        ok, why = native_selftest(comm, 0, 1, timeout_s=30)
+        assert ok, why
+    finally:
+        comm.abort()

@@ -120,3 +120,88 @@ class NativeComm:
         if self._comm:
             self._check(self.lib.tca_rccl_comm_destroy(self._comm), "ncclCommDestroy")
             self._comm = ctypes.c_void_p()
+
+
+def native_selftest(comm: "NativeComm", rank: int, world: int, timeout_s: float = 60.0) -> Tuple[bool, str]:
+    """Exercise the DP step's detection-gather pattern on ``comm`` before the real step uses it:
+    every rank sends two small tensors to rank 0 as one grouped p2p plan, first eagerly, then
+    captured into two hipGraphs (the double-buffered step's layout: one plan per graph over the
+    one communicator) replayed alternately three times.  Rank 0 checks every received value.
+    Each phase is waited for by polling an event; past ``timeout_s`` the communicator is aborted
+    (its kernels leave their waits) and the test fails, so a caller can fall back to the process
+    group's own p2p instead of hanging its first timed step.  Collective: every rank must call it.
+    Returns (ok, detail)."""
+    import time
+
+    from ..pipelines.graph import GraphRunner
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.Stream(device=dev)
+    src = [torch.zeros(4, 3, device=dev), torch.zeros(4, dtype=torch.int32, device=dev)]
+    dst = [[[torch.full_like(t, -1) for t in src] for _ in range(world)] for _ in range(2)] if rank == 0 else None
+    vals = torch.zeros(2, device=dev)
+
+    def plan(k):
+        if rank == 0:
+            ops = [(RECV, d, r) for r in range(world) for d in dst[k][r]]
+        else:
+            ops = []
+        return ops + [(SEND, s, 0) for s in src]
+
+    def wait(what: str) -> Optional[str]:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        t0 = time.perf_counter()
+        while not ev.query():
+            if time.perf_counter() - t0 > timeout_s:
+                comm.abort()
+                return f"{what}: no completion within {timeout_s:.0f} s (communicator aborted)"
+            time.sleep(0.001)
+        return None
+
+    def check(k: int, v: float) -> Optional[str]:
+        if rank != 0:
+            return None
+        for r in range(world):
+            want = v + r
+            if float(dst[k][r][0].reshape(-1)[0]) != want or int(dst[k][r][1][0]) != int(want):
+                return f"graph {k}: rank {r}'s tensors arrived wrong ({float(dst[k][r][0].reshape(-1)[0])} vs {want})"
+        return None
+
+    runs = []
+    try:
+        with torch.cuda.stream(stream):
+            src[0].fill_(1.0 + rank)
+            src[1].fill_(1 + rank)
+            comm.group_p2p(plan(0))
+        err = wait("eager grouped p2p")
+        if err is None:
+            err = check(0, 1.0)
+        if err is not None:
+            return False, err
+
+        def step(k):
+            def fn():
+                src[0].copy_((vals[k] + rank).expand_as(src[0]))
+                src[1].copy_((vals[k] + rank).to(torch.int32).expand_as(src[1]))
+                comm.group_p2p(plan(k))
+                return src
+            return fn
+        with torch.cuda.stream(stream):
+            runs = [GraphRunner(step(0)), GraphRunner(step(1))]
+            for run in runs:
+                run.capture()
+        for t, v in enumerate((2.0, 5.0, 9.0)):
+            k = t % 2
+            with torch.cuda.stream(stream):
+                vals[k].fill_(v)
+                runs[k]()
+            err = wait(f"graph replay {t}") or check(k, v)
+            if err is not None:
+                return False, err
+        return True, "eager and two-graph grouped p2p gather delivered"
+    except Exception as e:  # noqa: BLE001 - reported to the caller, which falls back
+        return False, f"{type(e).__name__}: {e}"
+    finally:
+        for r in runs:  # the graphs go before the communicator
+            r.release()
