@@ -395,6 +395,7 @@ def main():
     native = None
     comm_used = "torch" if info.world > 1 else "none"
     rccl_ranks = 1
+    selftest = None
     if args.comm == "native" and info.world > 1 and not gloo_rehearsal:
         from triton_client_amd.parallel.rccl import NativeComm
 
@@ -411,6 +412,7 @@ def main():
             # limit: a communicator that cannot run it is aborted and the process group serves instead
             from triton_client_amd.parallel.rccl import native_selftest
             ok_, why = native_selftest(native, info.rank, info.world)
+            selftest = why
             print(f"[bench] rank {info.rank}: native RCCL self-test: {why}", file=sys.stderr, flush=True)
             if not ok_:
                 native = None
@@ -426,6 +428,7 @@ def main():
     if info.world > 1 and not gloo_rehearsal and rccl_ranks != args.gpus:
         raise SystemExit(f"RCCL communicator spans {rccl_ranks} ranks, expected --gpus {args.gpus}")
     preflight = _preflight(info, dev, rccl_ranks, comm_used)
+    preflight["native_selftest"] = selftest
     ex = FrameExchange(info, native=native)
     # with the native RCCL communicator the detection gather (grouped send / recv of fixed-shape
     # result buffers) is stream work: it is captured inside the step graph(s), so a step is one
