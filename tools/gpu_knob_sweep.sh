@@ -15,6 +15,10 @@ elif [ "${SET:-1}" = "5" ]; then  # the LiDAR software-pipeline split points
            "lidar5||--only lidar --lidar-pipeline 5")
 elif [ "${SET:-1}" = "6" ]; then  # mode 5 against mode 3 (the default) only
   CONFIGS=("default||" "pipe5||--lidar-pipeline 5")
+elif [ "${SET:-1}" = "10" ]; then  # fewer workgroups for the neck (it runs beside the first down blocks in mode 5)
+  CONFIGS=("default||" "neckg128|TCA_NECK_GRID=128|" "neckg160|TCA_NECK_GRID=160|" "neckg192|TCA_NECK_GRID=192|")
+elif [ "${SET:-1}" = "11" ]; then  # the 3/4-CU neck grid (default) against the full grid
+  CONFIGS=("default||" "neckfull|TCA_NECK_GRID=256|")
 elif [ "${SET:-1}" = "4" ]; then  # launch shapes and tiles (TCA_VFE_GRID, TCA_NECK_GRID, TCA_*_TILE)
   CONFIGS=("default||" "vfeg1024|TCA_VFE_GRID=1024|" "vfeg4096|TCA_VFE_GRID=4096|" "neckg192|TCA_NECK_GRID=192|"
            "neckg224|TCA_NECK_GRID=224|" "hx3t5|TCA_HX3_TILE=5|" "hx3t4|TCA_HX3_TILE=4|" "winot1|TCA_WINO_TILE=1|"

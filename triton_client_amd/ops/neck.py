@@ -72,10 +72,13 @@ class FusedNeckHead:
         self.dtype = head.dtype
         self.nbr = len(self.ups)
         self.nh = head.N
-        # persistent kernel: one workgroup per CU (a multiple of 8: tiles are split per XCD)
+        # persistent kernel: workgroup slots over 3/4 of the CUs (a multiple of 8: tiles are split per XCD).
+        # The neck runs beside the first down blocks of the next batch (bench.py --lidar-pipeline 5); leaving
+        # them a quarter of the CUs measured +0.5% / +0.7% over the full grid on two boxes
+        # (profiles/r6/knobs/sweep4_shapes.txt, sweep10_neck_grid.txt); TCA_NECK_GRID overrides
         if grid <= 0:
             grid = int(os.environ.get("TCA_NECK_GRID", "0")) or \
-                torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+                torch.cuda.get_device_properties(torch.device(device)).multi_processor_count * 3 // 4
         self.grid = max(8, grid // 8 * 8)
         # fp32 tiling (bev_neck.hip tca_bev_neck_head_x3v): 0 = <8 waves, 2 stages>, 99.6 KiB LDS; 1 = <8, 3>,
         # 149 KiB; 2 = <4, 2>, two workgroups per CU (66 KiB each), the fastest alone (883 vs 1056 us).  In
