@@ -26,6 +26,8 @@
 // All scratch is self-resetting, so the dense cell grids (even the 90 M-cell
 // SECOND grid: 720 MB, affordable in 288 GB of HBM) are cleared in O(points)
 // per frame instead of O(cells); they are initialised once at allocation.
+#include <cstdlib>
+
 #include "tca_common.h"
 
 using namespace tca;
@@ -96,23 +98,25 @@ __device__ __forceinline__ Run wave_run(int key) {
 __global__ void __launch_bounds__(kBlock) vox_cell_kernel(const float* __restrict__ pts, int pstride, int max_pts,
                                                           const int* __restrict__ npts, VoxGeom g,
                                                           int* __restrict__ cell_first, int* __restrict__ point_cell) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int cell = -1;
-  if (i < max_pts && i < npts[b]) {
-    const float* p = pts + ((long)b * max_pts + i) * pstride;
-    int cx, cy, cz;
-    cell = cell_of(p, g, cx, cy, cz);
+  const int b = blockIdx.y, n = npts[b];
+  for (int ch = blockIdx.x; ch * kBlock < max_pts; ch += gridDim.x) {  // 256-point chunks (vox_pgrid)
+    const int i = ch * kBlock + threadIdx.x;
+    int cell = -1;
+    if (i < max_pts && i < n) {
+      const float* p = pts + ((long)b * max_pts + i) * pstride;
+      int cx, cy, cz;
+      cell = cell_of(p, g, cx, cy, cz);
+    }
+    // the run head holds the run's smallest index: atomicMin of the others cannot change the cell
+    const Run r = wave_run(cell);
+    if (g.keys) {  // hash mode: the head claims the run's table slot
+      int slot = r.head ? hash_slot(g.keys + (long)b * g.cells, g.hbits, cell) : -1;
+      slot = __shfl(slot, r.head_lane, 64);
+      if (cell >= 0) cell = slot;
+    }
+    if (r.head) atomicMin(&cell_first[(long)b * g.cells + cell], i);
+    if (i < max_pts) point_cell[(long)b * max_pts + i] = cell;
   }
-  // the run head holds the run's smallest index: atomicMin of the others cannot change the cell
-  const Run r = wave_run(cell);
-  if (g.keys) {  // hash mode: the head claims the run's table slot
-    int slot = r.head ? hash_slot(g.keys + (long)b * g.cells, g.hbits, cell) : -1;
-    slot = __shfl(slot, r.head_lane, 64);
-    if (cell >= 0) cell = slot;
-  }
-  if (r.head) atomicMin(&cell_first[(long)b * g.cells + cell], i);
-  if (i < max_pts) point_cell[(long)b * max_pts + i] = cell;
 }
 
 __device__ __forceinline__ int first_flag(const int* pc, const int* cf, long cbase, int i, int n) {
@@ -288,14 +292,17 @@ __global__ void __launch_bounds__(kBlock) vox_count_kernel(const int* __restrict
                                                            const int* __restrict__ npts, long cells,
                                                            const int* __restrict__ cell_vid, int max_voxels,
                                                            int* __restrict__ vcount) {
-  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-  int vid = -1;
-  if (i < npts[b] && i < max_pts) {
-    const int c = point_cell[(long)b * max_pts + i];
-    if (c >= 0) vid = cell_vid[(long)b * cells + c];
+  const int b = blockIdx.y, n = npts[b];
+  for (int ch = blockIdx.x; ch * kBlock < max_pts; ch += gridDim.x) {  // 256-point chunks (vox_pgrid)
+    const int i = ch * kBlock + threadIdx.x;
+    int vid = -1;
+    if (i < n && i < max_pts) {
+      const int c = point_cell[(long)b * max_pts + i];
+      if (c >= 0) vid = cell_vid[(long)b * cells + c];
+    }
+    const Run r = wave_run(vid);  // one atomic per run of points in one voxel
+    if (r.head) atomicAdd(&vcount[(long)b * max_voxels + vid], r.len);
   }
-  const Run r = wave_run(vid);  // one atomic per run of points in one voxel
-  if (r.head) atomicAdd(&vcount[(long)b * max_voxels + vid], r.len);
 }
 
 constexpr int kScanT = 1024;
@@ -340,19 +347,22 @@ __global__ void __launch_bounds__(kBlock) vox_fill_kernel(const int* __restrict_
                                                           const int* __restrict__ npts, long cells,
                                                           const int* __restrict__ cell_vid, int max_voxels,
                                                           int* __restrict__ cursor, int* __restrict__ csr) {
-  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-  int vid = -1;
-  if (i < npts[b] && i < max_pts) {
-    const int c = point_cell[(long)b * max_pts + i];
-    if (c >= 0) vid = cell_vid[(long)b * cells + c];
+  const int b = blockIdx.y, n = npts[b];
+  for (int ch = blockIdx.x; ch * kBlock < max_pts; ch += gridDim.x) {  // 256-point chunks (vox_pgrid)
+    const int i = ch * kBlock + threadIdx.x;
+    int vid = -1;
+    if (i < n && i < max_pts) {
+      const int c = point_cell[(long)b * max_pts + i];
+      if (c >= 0) vid = cell_vid[(long)b * cells + c];
+    }
+    // one cursor atomic per run: the head reserves the run's positions, its lanes take them in order
+    // (a voxel's list is sorted by the next stage, so only the set of positions matters)
+    const Run r = wave_run(vid);
+    int base = 0;
+    if (r.head) base = atomicAdd(&cursor[(long)b * max_voxels + vid], r.len);
+    base = __shfl(base, r.head_lane, 64);
+    if (vid >= 0) csr[(long)b * max_pts + base + r.rank] = i;
   }
-  // one cursor atomic per run: the head reserves the run's positions, its lanes take them in order
-  // (a voxel's list is sorted by the next stage, so only the set of positions matters)
-  const Run r = wave_run(vid);
-  int base = 0;
-  if (r.head) base = atomicAdd(&cursor[(long)b * max_voxels + vid], r.len);
-  base = __shfl(base, r.head_lane, 64);
-  if (vid >= 0) csr[(long)b * max_pts + base + r.rank] = i;
 }
 
 __device__ __forceinline__ void cswap(int& a, int& b) {
@@ -462,12 +472,29 @@ __global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const 
                                                              const int* __restrict__ point_cell, long cells,
                                                              int* __restrict__ cell_first, int* __restrict__ cell_vid,
                                                              int* __restrict__ keys) {
-  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
-  const int c = i < npts[b] && i < max_pts ? point_cell[(long)b * max_pts + i] : -1;
-  if (!wave_run(c).head) return;  // one reset per run of points in one cell
-  cell_first[(long)b * cells + c] = kEmpty;
-  cell_vid[(long)b * cells + c] = -1;
-  if (keys) keys[(long)b * cells + c] = -1;
+  const int b = blockIdx.y, n = npts[b];
+  for (int ch = blockIdx.x; ch * 256 < max_pts; ch += gridDim.x) {  // 256-point chunks (vox_pgrid)
+    const int i = ch * 256 + threadIdx.x;
+    const int c = i < n && i < max_pts ? point_cell[(long)b * max_pts + i] : -1;
+    if (!wave_run(c).head) continue;  // one reset per run of points in one cell
+    cell_first[(long)b * cells + c] = kEmpty;
+    cell_vid[(long)b * cells + c] = -1;
+    if (keys) keys[(long)b * cells + c] = -1;
+  }
+}
+
+// workgroups per frame of the per-point passes (vox_cell / vox_count / vox_fill / vox_cell_reset): each
+// walks 256-point chunks blockIdx.x, blockIdx.x + gridDim.x, ... .  One chunk per workgroup (15,104
+// workgroups per 32-sweep batch) floods the dispatcher beside the BEV convs; TCA_VOX_GRID caps it
+int vox_pgrid(int max_points) {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("TCA_VOX_GRID");
+    cap = e ? atoi(e) : 0;
+    cap = cap < 0 ? 0 : cap;
+  }
+  const int chunks = (max_points + kBlock - 1) / kBlock;
+  return cap > 0 && cap < chunks ? cap : chunks;
 }
 
 VoxGeom make_geom(const float* range, const float* vsize, const int* grid, int* keys, int hbits) {
@@ -504,7 +531,7 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
     return (int)hipErrorInvalidValue;  // the probe loop needs free slots: load <= 1/2
   VoxGeom g = make_geom(range, vsize, grid, keys, hash_bits);
   const int bpf = (max_points + kPtsPerBlock - 1) / kPtsPerBlock;
-  dim3 pgrid((max_points + kBlock - 1) / kBlock, batch);
+  dim3 pgrid(vox_pgrid(max_points), batch);
   dim3 sgrid(bpf, batch);
   if (mode & 1) {
     vox_cell_kernel<<<pgrid, kBlock, 0, stream>>>(pts, pstride, max_points, npts, g, cell_first, point_cell);
@@ -541,7 +568,7 @@ TCA_API int tca_vox_slots_csr(const int* point_cell, int max_points, const int* 
   if (batch <= 0) return 0;
   if (P > 64 || P < 1) return (int)hipErrorInvalidValue;
   const long cells = hash_bits > 0 ? (1L << hash_bits) : (long)grid[0] * grid[1] * grid[2];
-  dim3 pgrid((max_points + kBlock - 1) / kBlock, batch);
+  dim3 pgrid(vox_pgrid(max_points), batch);
   vox_count_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, cells, cell_vid, max_voxels, vcount);
   vox_scan_kernel<<<batch, kScanT, 0, stream>>>(voxel_count, max_voxels, vcount, offs, cursor, dense_count);
   vox_fill_kernel<<<pgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, cells, cell_vid, max_voxels, cursor,
