@@ -60,6 +60,10 @@ def main(argv=None):
     ap.add_argument("--target", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--server-procs", type=int, default=1, help="server processes sharing the port (--procs)")
+    ap.add_argument("--model-procs", action="store_true",
+                    help="one server process per model, each on its own port (camera clients -> the YOLOv5 "
+                         "server, LiDAR clients -> the PointPillars server): two GILs, and each model's dynamic "
+                         "batcher still sees all of its requests")
     ap.add_argument("--client-hw-queues", type=int, default=0,
                     help="multi-process runs: GPU_MAX_HW_QUEUES of each client process (0: HIP's default); fewer "
                          "queues per client leave more of the hardware scheduler's mapped queues to the server")
@@ -249,35 +253,48 @@ def multi_proc(a) -> int:
     import socket
     import subprocess
 
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    target = f"127.0.0.1:{port}"
+    def free_port():
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            return sk.getsockname()[1]
+
     here = os.path.abspath(__file__)
-    server = subprocess.Popen([sys.executable, "-X", "faulthandler", "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
-                               str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
-                               "--models", "YOLOv5nCOCO,pointpillar_kitti", "--procs", str(a.server_procs)],
-                              cwd=os.path.dirname(os.path.dirname(here)),
-                              env=dict(os.environ, **({"TCA_SERVER_PROFILE": os.path.abspath(a.server_profile)}
-                                                      if a.server_profile else {})))
+    models = {"camera": "YOLOv5nCOCO", "lidar": "pointpillar_kitti"}
+    groups = [list(models.values())] if not a.model_procs else [[m] for m in models.values()]
+    servers, targets = [], {}
+    for i, g in enumerate(groups):
+        port = free_port()
+        env = dict(os.environ)
+        if a.server_profile:
+            prof = os.path.abspath(a.server_profile)
+            env["TCA_SERVER_PROFILE"] = prof if len(groups) == 1 else prof.replace(".json", f"_{g[0]}.json")
+        servers.append(subprocess.Popen(
+            [sys.executable, "-X", "faulthandler", "-m", "triton_client_amd.server", "--host", "127.0.0.1", "--port",
+             str(port), "--workers", str(a.workers), "--metrics-port", "0", "--device", a.device,
+             "--models", ",".join(g), "--procs", str(a.server_procs)],
+            cwd=os.path.dirname(os.path.dirname(here)), env=env))
+        for m in g:
+            targets[m] = f"127.0.0.1:{port}"
     common = ["--frames", str(a.frames), "--warmup", str(a.warmup), "--window", str(a.window), "--device", a.device,
-              "--cam", a.cam, "--rings", str(a.rings), "--columns", str(a.columns), "--wire", a.wire,
-              "--target", target] + (["--burst"] if a.burst else [])
+              "--cam", a.cam, "--rings", str(a.rings), "--columns", str(a.columns), "--wire", a.wire] + \
+        (["--burst"] if a.burst else [])
     clients = []
     cenv = dict(os.environ, **({"GPU_MAX_HW_QUEUES": str(a.client_hw_queues)} if a.client_hw_queues > 0 else {}))
     try:
         for p in range(a.client_procs):
             for role in ("camera", "lidar"):
-                clients.append(subprocess.Popen([sys.executable, here, "--role", role, "--seed", str(p)] + common,
+                clients.append(subprocess.Popen([sys.executable, here, "--role", role, "--seed", str(p), "--target",
+                                                 targets[models[role]]] + common,
                                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
                                                 env=cenv))
         for c in clients:
             line = c.stdout.readline()
             if line.strip() != "READY":
-                raise RuntimeError(f"client failed before READY: {line!r} (server exit code {server.poll()})")
+                raise RuntimeError(f"client failed before READY: {line!r} "
+                                   f"(server exit codes {[s.poll() for s in servers]})")
         import psutil
 
-        procs = [psutil.Process(server.pid)] + [psutil.Process(c.pid) for c in clients]
+        procs = [psutil.Process(s.pid) for s in servers] + [psutil.Process(c.pid) for c in clients]
 
         def cpu_s():  # user + system seconds of the server (and its children) and the clients
             tot = 0.0
@@ -306,22 +323,24 @@ def multi_proc(a) -> int:
                 raise RuntimeError("a client process failed")
         from triton_client_amd.channel.grpc_channel import GRPCChannel
 
-        ch = GRPCChannel({"grpc_channel": target}, SimpleNamespace(model_name="YOLOv5nCOCO", model_version="",
-                                                                   batch_size=64, verbose=False))
         rpe = {}
-        for m in ("YOLOv5nCOCO", "pointpillar_kitti"):
+        for m in models.values():
+            ch = GRPCChannel({"grpc_channel": targets[m]}, SimpleNamespace(model_name=m, model_version="",
+                                                                           batch_size=64, verbose=False))
             st = ch.model_statistics(m).model_stats[0]
             rpe[m] = round(st.inference_count / max(1, st.execution_count), 2)
     finally:
         for c in clients:
             if c.poll() is None:
                 c.kill()
-        server.terminate()
-        try:
-            server.wait(30)
-        except subprocess.TimeoutExpired:  # e.g. under a tracer that flushes at exit: the results stand
-            server.kill()
-            server.wait(30)
+        for server in servers:
+            server.terminate()
+        for server in servers:
+            try:
+                server.wait(30)
+            except subprocess.TimeoutExpired:  # e.g. under a tracer that flushes at exit: the results stand
+                server.kill()
+                server.wait(30)
 
     def mean_ms(role):
         rs = [o for o in outs if o["role"] == role]
@@ -335,8 +354,9 @@ def multi_proc(a) -> int:
             "client_wall_s": {o["role"] + str(i // 2): round(o["wall_s"], 3) for i, o in enumerate(outs)},
             "server_requests_per_execution": rpe,
             "host_cpu_cores_busy": round(cpu_cores, 2), "host_cpus_in_affinity": cpu_avail,
-            "topology": (f"{a.server_procs} server process{'es' if a.server_procs > 1 else ''} + {a.client_procs} camera "
-                         f"and {a.client_procs} LiDAR client processes"),
+            "topology": ((f"one server process per model ({a.server_procs} each)" if a.model_procs else
+                          f"{a.server_procs} server process{'es' if a.server_procs > 1 else ''}") +
+                         f" + {a.client_procs} camera and {a.client_procs} LiDAR client processes"),
             "wire": a.wire, "window_mode": "burst" if a.burst else "sliding", "server_workers": a.workers,
             "client_hw_queues": a.client_hw_queues or None,
             "path": {"raw": "tensors inside the gRPC messages (C++ codec both ends)",
