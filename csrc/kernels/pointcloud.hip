@@ -13,6 +13,8 @@
 //           (a wave-strided sum; <= a few hundred ints), in-block ordered
 //           compaction with a block scan, intensity scaling and z offset.
 // Output order == input order (skip_nans semantics).
+#include <cstdlib>
+
 #include "tca_common.h"
 
 using namespace tca;
@@ -47,11 +49,17 @@ __device__ __forceinline__ float load_field(const uint8_t* rec, int off, int dt)
   }
 }
 
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+
+// NT: the payload's last read (pc2_compact, TCA_VOX_NT=1) as a non-temporal load, so the streamed
+// records do not displace the L2 lines of the BEV convs running beside the front
+template <bool NT = false>
 __device__ __forceinline__ bool load_point(const uint8_t* base, int i, int step, const FieldDesc& fd, float* v,
                                            int fast) {
   const uint8_t* rec = base + (long)i * step;
   if (fast == 2) {
-    const float4 q = *reinterpret_cast<const float4*>(rec);
+    const nt_f4 q = NT ? __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(rec))
+                       : *reinterpret_cast<const nt_f4*>(rec);
     v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
   } else if (fast == 1) {
 #pragma unroll
@@ -107,6 +115,7 @@ __global__ void __launch_bounds__(kBlock) pc2_count_kernel(const uint8_t* __rest
   }
 }
 
+template <bool NT>
 __global__ void __launch_bounds__(kBlock) pc2_compact_kernel(const uint8_t* __restrict__ data,
                                                              const long* __restrict__ frame_off,
                                                              const int* __restrict__ frame_n, int step, FieldDesc fd,
@@ -145,7 +154,7 @@ __global__ void __launch_bounds__(kBlock) pc2_compact_kernel(const uint8_t* __re
 #pragma unroll
   for (int k = 0; k < kPtsPerThread; ++k) {
     const int i = first + k;
-    ok[k] = i < n && load_point(base, i, step, fd, v[k], fast);
+    ok[k] = i < n && load_point<NT>(base, i, step, fd, v[k], fast);
     cnt += ok[k];
   }
   int total;
@@ -198,7 +207,8 @@ TCA_API int tca_pc2_unpack(const void* data, const long* frame_off, const int* f
   dim3 grid(bpf, batch);
   const uint8_t* d = (const uint8_t*)data;
   pc2_count_kernel<<<grid, kBlock, 0, stream>>>(d, frame_off, frame_n, point_step, fd, bpf, block_count, frame_imax);
-  pc2_compact_kernel<<<grid, kBlock, 0, stream>>>(d, frame_off, frame_n, point_step, fd, bpf, block_count, frame_imax,
+  static const bool nt = getenv("TCA_VOX_NT") && atoi(getenv("TCA_VOX_NT")) != 0;
+  (nt ? pc2_compact_kernel<true> : pc2_compact_kernel<false>)<<<grid, kBlock, 0, stream>>>(d, frame_off, frame_n, point_step, fd, bpf, block_count, frame_imax,
                                                   normalize_intensity, z_offset, out, out_stride, max_points, out_count);
   TCA_LAUNCH_CHECK();
 }

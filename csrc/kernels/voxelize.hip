@@ -63,10 +63,14 @@ __device__ __forceinline__ int hash_slot(int* keys, int hbits, int cell) {
   }
 }
 
+template <bool NT = false>
 __device__ __forceinline__ int cell_of(const float* p, const VoxGeom& g, int& cx, int& cy, int& cz) {
-  cx = (int)floorf((p[0] - g.r0) / g.vs0);
-  cy = (int)floorf((p[1] - g.r1) / g.vs1);
-  cz = (int)floorf((p[2] - g.r2) / g.vs2);
+  const float x = NT ? __builtin_nontemporal_load(p) : p[0];
+  const float y = NT ? __builtin_nontemporal_load(p + 1) : p[1];
+  const float z = NT ? __builtin_nontemporal_load(p + 2) : p[2];
+  cx = (int)floorf((x - g.r0) / g.vs0);
+  cy = (int)floorf((y - g.r1) / g.vs1);
+  cz = (int)floorf((z - g.r2) / g.vs2);
   if (cx < 0 || cx >= g.nx || cy < 0 || cy >= g.ny || cz < 0 || cz >= g.nz) return -1;
   return (cz * g.ny + cy) * g.nx + cx;
 }
@@ -95,6 +99,9 @@ __device__ __forceinline__ Run wave_run(int key) {
   return r;
 }
 
+// NT (TCA_VOX_NT=1): the point coordinates (vox_cell) and point_cell's last read (vox_cell_reset) as
+// non-temporal loads
+template <bool NT>
 __global__ void __launch_bounds__(kBlock) vox_cell_kernel(const float* __restrict__ pts, int pstride, int max_pts,
                                                           const int* __restrict__ npts, VoxGeom g,
                                                           int* __restrict__ cell_first, int* __restrict__ point_cell) {
@@ -105,7 +112,7 @@ __global__ void __launch_bounds__(kBlock) vox_cell_kernel(const float* __restric
     if (i < max_pts && i < n) {
       const float* p = pts + ((long)b * max_pts + i) * pstride;
       int cx, cy, cz;
-      cell = cell_of(p, g, cx, cy, cz);
+      cell = cell_of<NT>(p, g, cx, cy, cz);
     }
     // the run head holds the run's smallest index: atomicMin of the others cannot change the cell
     const Run r = wave_run(cell);
@@ -468,6 +475,7 @@ __global__ void __launch_bounds__(256) vox_slot_reset_kernel(int max_voxels, int
   }
 }
 
+template <bool NT>
 __global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const int* __restrict__ npts,
                                                              const int* __restrict__ point_cell, long cells,
                                                              int* __restrict__ cell_first, int* __restrict__ cell_vid,
@@ -475,7 +483,8 @@ __global__ void __launch_bounds__(256) vox_cell_reset_kernel(int max_pts, const 
   const int b = blockIdx.y, n = npts[b];
   for (int ch = blockIdx.x; ch * 256 < max_pts; ch += gridDim.x) {  // 256-point chunks (vox_pgrid)
     const int i = ch * 256 + threadIdx.x;
-    const int c = i < n && i < max_pts ? point_cell[(long)b * max_pts + i] : -1;
+    const int* pc = point_cell + (long)b * max_pts + i;
+    const int c = i < n && i < max_pts ? (NT ? __builtin_nontemporal_load(pc) : *pc) : -1;
     if (!wave_run(c).head) continue;  // one reset per run of points in one cell
     cell_first[(long)b * cells + c] = kEmpty;
     cell_vid[(long)b * cells + c] = -1;
@@ -495,6 +504,11 @@ int vox_pgrid(int max_points) {
   }
   const int chunks = (max_points + kBlock - 1) / kBlock;
   return cap > 0 && cap < chunks ? cap : chunks;
+}
+
+bool vox_nt() {
+  static const bool nt = getenv("TCA_VOX_NT") && atoi(getenv("TCA_VOX_NT")) != 0;
+  return nt;
 }
 
 VoxGeom make_geom(const float* range, const float* vsize, const int* grid, int* keys, int hbits) {
@@ -534,7 +548,7 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
   dim3 pgrid(vox_pgrid(max_points), batch);
   dim3 sgrid(bpf, batch);
   if (mode & 1) {
-    vox_cell_kernel<<<pgrid, kBlock, 0, stream>>>(pts, pstride, max_points, npts, g, cell_first, point_cell);
+    (vox_nt() ? vox_cell_kernel<true> : vox_cell_kernel<false>)<<<pgrid, kBlock, 0, stream>>>(pts, pstride, max_points, npts, g, cell_first, point_cell);
     vox_count_first_kernel<<<sgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g.cells, cell_first, bpf,
                                                          block_count);
     vox_assign_kernel<<<sgrid, kBlock, 0, stream>>>(point_cell, max_points, npts, g, cell_first, bpf, block_count,
@@ -547,7 +561,7 @@ TCA_API int tca_voxelize(const float* pts, int pstride, int max_points, const in
     const int need = (max_voxels * (P / 4) + 255) / 256;
     vox_slot_reset_kernel<<<dim3(need < 32 ? need : 32, batch), 256, 0, stream>>>(
         max_voxels, P, voxel_count, vcount, slots, num_points);
-    vox_cell_reset_kernel<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid,
+    (vox_nt() ? vox_cell_reset_kernel<true> : vox_cell_reset_kernel<false>)<<<pgrid, kBlock, 0, stream>>>(max_points, npts, point_cell, g.cells, cell_first, cell_vid,
                                                         g.keys);
   } else if (mode & 2) {
     vox_gather_reset_kernel<<<1024, 256, 0, stream>>>(pts, pstride, max_points, npts, nfeat, batch,
