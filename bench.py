@@ -495,6 +495,7 @@ def main():
     # replay reads, so no per-step D2D copy from landing buffers (BEV / camera frames: ~60 us)
     d2h_stage = None
     piped = post_split = front_next = False
+    front_after = 0
     # (not with the RCCL gather captured in the step graph: two graphs replaying the same
     # communicator's p2p have not run on a multi-GPU node yet, so that path keeps one graph)
     # (split mode keeps one input set: double-buffering its two per-branch graphs measured slower,
@@ -516,6 +517,12 @@ def main():
                 lp.build_fast()
             blocks_front = len(lids[0].fast.bb.blocks) - 1 if args.lidar_pipeline == 4 else None
             front_next = args.lidar_pipeline == 5
+            # mode 5: the next batch's front waits until lside has issued the first TCA_FRONT_AFTER
+            # down blocks (default 1: the voxeliser chain runs beside blocks 2-3, not beside block 1's
+            # hx3 convs; +1.7% median on one box, profiles/r6/knobs/ sweep 16); 0: right after the
+            # neck / NMS
+            front_after = int(os.environ.get("TCA_FRONT_AFTER", "1")) if front_next else 0
+            front_ev = [torch.cuda.Event(), torch.cuda.Event()]
             side2 = torch.cuda.Stream()
             lside = side if side is not None else torch.cuda.Stream()
             # (the canvas clear moved from the front into the back half: 7.60 vs 7.60 ms, not kept;
@@ -530,9 +537,11 @@ def main():
                     side2.wait_stream(main)
                     if front_next:  # graph k: pipeline k's blocks beside pipeline 1-k's neck / NMS + next front
                         with torch.cuda.stream(lside):
-                            lids[k].step_blocks()
+                            lids[k].step_blocks(mark=(front_after, front_ev[k]) if front_after else None)
                         with torch.cuda.stream(side2):
                             r3 = lids[1 - k].step_back()
+                            if front_after:
+                                side2.wait_event(front_ev[k])
                             lids[1 - k].step_pre()
                     elif post_split:  # graph k: pipeline k's front beside pipeline 1-k's decode / NMS
                         with torch.cuda.stream(lside):
@@ -882,8 +891,10 @@ def main():
                                     if piped else "off"),
                 "lidar_pipeline_note": (("two LiDAR pipelines alternate: each timed step runs one full batch "
                                          "through every stage: batch t's down blocks beside batch t-1's neck, "
-                                         "head, decode and NMS followed by batch t+1's preprocessing; "
-                                         "detections leave two steps after ingest") if piped and front_next else
+                                         "head, decode and NMS followed by batch t+1's preprocessing"
+                                         + (f" (which waits until batch t's first {front_after} down block(s) are "
+                                            "issued)" if front_after else "")
+                                         + "; detections leave two steps after ingest") if piped and front_next else
                                         ("two LiDAR pipelines alternate: each timed step runs one full batch through "
                                          "every stage, one batch's first half beside the previous batch's second "
                                          "half (split point: lidar_pipelined); detections leave one step later")

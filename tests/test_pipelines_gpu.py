@@ -142,7 +142,8 @@ def test_lidar_post_split_pipelining_matches_step(cuda, neck_back, blocks_front)
             assert torch.equal(r[1][b, :n], g[1][b, :n]), (name, b)
 
 
-def test_lidar_front_next_pipelining_matches_step(cuda):
+@pytest.mark.parametrize("front_after", [0, 1])
+def test_lidar_front_next_pipelining_matches_step(cuda, front_after):
     """bench.py --lidar-pipeline 5: pipeline A's down blocks on one stream beside pipeline B's
     neck + head + decode + NMS and then B's preprocessing of its NEXT batch on another; the two
     pipelines swap roles every step.  Every batch gets exactly the detections of a plain step()."""
@@ -173,17 +174,20 @@ def test_lidar_front_next_pipelining_matches_step(cuda):
     got = {}
     # step k: X = blocks on s1, Y = back + next front on s2; Y's data holds its next batch
     plan = [(la, lb, "b1", "b2"), (lb, la, "a1", "a2"), (la, lb, "b2", None), (lb, la, "a2", None)]
+    ev = torch.cuda.Event()
     for x, y, done, nxt in plan:
         if nxt is not None:
             _load_lidar(y, spec, seeds[nxt])
         torch.cuda.synchronize()
         s1.wait_stream(main)
         s2.wait_stream(main)
-        with torch.cuda.stream(s1):
-            x.step_blocks()
+        with torch.cuda.stream(s1):  # front_after: Y's next front waits for X's first down block
+            x.step_blocks(mark=(front_after, ev) if front_after else None)
         with torch.cuda.stream(s2):
             got[done] = snap(y.step_back())
             if nxt is not None:
+                if front_after:
+                    s2.wait_event(ev)
                 y.step_pre()
         main.wait_stream(s1)
         main.wait_stream(s2)

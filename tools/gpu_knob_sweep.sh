@@ -27,6 +27,10 @@ elif [ "${SET:-1}" = "14" ]; then  # the follow-up: the two best caps of set 13 
   CONFIGS=("default||" "voxg16|TCA_VOX_GRID=16|" "voxg32|TCA_VOX_GRID=32|")
 elif [ "${SET:-1}" = "15" ]; then  # non-temporal loads of the streamed point data in the LiDAR front (TCA_VOX_NT)
   CONFIGS=("default||" "voxnt|TCA_VOX_NT=1|")
+elif [ "${SET:-1}" = "16" ]; then  # mode 5: the next front waits for the first 1 / 2 down blocks (TCA_FRONT_AFTER)
+  CONFIGS=("default||" "fa1|TCA_FRONT_AFTER=1|" "fa2|TCA_FRONT_AFTER=2|")
+elif [ "${SET:-1}" = "17" ]; then  # after TCA_FRONT_AFTER=1 became the default: against 0 (the front right after the neck / NMS)
+  CONFIGS=("default||" "fa0|TCA_FRONT_AFTER=0|")
 elif [ "${SET:-1}" = "4" ]; then  # launch shapes and tiles (TCA_VFE_GRID, TCA_NECK_GRID, TCA_*_TILE)
   CONFIGS=("default||" "vfeg1024|TCA_VFE_GRID=1024|" "vfeg4096|TCA_VFE_GRID=4096|" "neckg192|TCA_NECK_GRID=192|"
            "neckg224|TCA_NECK_GRID=224|" "hx3t5|TCA_HX3_TILE=5|" "hx3t4|TCA_HX3_TILE=4|" "winot1|TCA_WINO_TILE=1|"
