@@ -522,6 +522,9 @@ def main():
             # hx3 convs; +1.7% median on one box, profiles/r6/knobs/ sweep 16); 0: right after the
             # neck / NMS
             front_after = int(os.environ.get("TCA_FRONT_AFTER", "1")) if front_next else 0
+            # (TCA_FRONT_AFTER_CONVS: the gate after that many convs instead of whole blocks)
+            front_convs = (int(os.environ.get("TCA_FRONT_AFTER_CONVS", "0"))
+                           or lids[0].fast.bb.convs_before(front_after)) if front_after else 0
             front_ev = [torch.cuda.Event(), torch.cuda.Event()]
             side2 = torch.cuda.Stream()
             lside = side if side is not None else torch.cuda.Stream()
@@ -537,7 +540,7 @@ def main():
                     side2.wait_stream(main)
                     if front_next:  # graph k: pipeline k's blocks beside pipeline 1-k's neck / NMS + next front
                         with torch.cuda.stream(lside):
-                            lids[k].step_blocks(mark=(front_after, front_ev[k]) if front_after else None)
+                            lids[k].step_blocks(mark=(front_convs, front_ev[k]) if front_after else None)
                         with torch.cuda.stream(side2):
                             r3 = lids[1 - k].step_back()
                             if front_after:

@@ -182,7 +182,7 @@ def test_lidar_front_next_pipelining_matches_step(cuda, front_after):
         s1.wait_stream(main)
         s2.wait_stream(main)
         with torch.cuda.stream(s1):  # front_after: Y's next front waits for X's first down block
-            x.step_blocks(mark=(front_after, ev) if front_after else None)
+            x.step_blocks(mark=(x.fast.bb.convs_before(front_after), ev) if front_after else None)
         with torch.cuda.stream(s2):
             got[done] = snap(y.step_back())
             if nxt is not None:

@@ -7,4 +7,4 @@ mkdir -p gpurun_out/r6/frontafter
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_pipelines_gpu.py \
   -k "front_next or post_split" > gpurun_out/r6/frontafter/tests.log 2>&1 || { tail -30 gpurun_out/r6/frontafter/tests.log; exit 1; }
 tail -1 gpurun_out/r6/frontafter/tests.log
-SET=17 TAG=frontafter17 ROUNDS=${ROUNDS:-8} bash tools/gpu_knob_sweep.sh
+SET=${SET:-17} TAG=frontafter${SET:-17} ROUNDS=${ROUNDS:-8} bash tools/gpu_knob_sweep.sh

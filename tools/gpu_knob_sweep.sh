@@ -31,6 +31,9 @@ elif [ "${SET:-1}" = "16" ]; then  # mode 5: the next front waits for the first 
   CONFIGS=("default||" "fa1|TCA_FRONT_AFTER=1|" "fa2|TCA_FRONT_AFTER=2|")
 elif [ "${SET:-1}" = "17" ]; then  # after TCA_FRONT_AFTER=1 became the default: against 0 (the front right after the neck / NMS)
   CONFIGS=("default||" "fa0|TCA_FRONT_AFTER=0|")
+elif [ "${SET:-1}" = "18" ]; then  # the front gate at conv granularity (default: after block 1 = 4 convs)
+  CONFIGS=("default||" "fc2|TCA_FRONT_AFTER_CONVS=2|" "fc3|TCA_FRONT_AFTER_CONVS=3|" "fc5|TCA_FRONT_AFTER_CONVS=5|"
+           "fc6|TCA_FRONT_AFTER_CONVS=6|")
 elif [ "${SET:-1}" = "4" ]; then  # launch shapes and tiles (TCA_VFE_GRID, TCA_NECK_GRID, TCA_*_TILE)
   CONFIGS=("default||" "vfeg1024|TCA_VFE_GRID=1024|" "vfeg4096|TCA_VFE_GRID=4096|" "neckg192|TCA_NECK_GRID=192|"
            "neckg224|TCA_NECK_GRID=224|" "hx3t5|TCA_HX3_TILE=5|" "hx3t4|TCA_HX3_TILE=4|" "winot1|TCA_WINO_TILE=1|"

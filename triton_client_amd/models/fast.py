@@ -412,12 +412,14 @@ class _BEVBackbonePlan:
         torch.cuda.synchronize(device)
         return vals
 
-    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None, outs: Optional[List[NHWC]] = None) -> List[NHWC]:
+    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None, outs: Optional[List[NHWC]] = None,
+                       mark: Optional[tuple] = None) -> List[NHWC]:
         """The down blocks only: each block's output (the deblocks' inputs).  With the canvas
         occupancy, the first block's stride-1 convs store their constant on the tiles whose
         receptive field holds no occupied cell (tca_bev_uniform_depth); bit-identical.
         stop: run blocks [0, stop) only; outs: the outputs of the blocks already run (continue
-        from the last one -- bench.py --lidar-pipeline 4 runs the last block in the back half)."""
+        from the last one -- bench.py --lidar-pipeline 4 runs the last block in the back half).
+        mark = (n, event): record the event on the current stream after the first n convs."""
         outs = list(outs or [])
         x = outs[-1] if outs else canvas
         first = len(outs)
@@ -429,6 +431,7 @@ class _BEVBackbonePlan:
             assert (ny, nx) == (self.ny, self.nx) and B == self.depth.shape[0], (canvas.occ.shape, self.depth.shape)
             _native.call("tca_bev_uniform_depth", _native.ptr(canvas.occ), B, ny, nx, len(self.blocks[0][0]),
                          _native.ptr(self.depth), _native.stream_ptr(None))
+        issued = sum(len(c) for c, _, _, _ in self.blocks[:first])
         for bi, (convs, pp, H, W) in enumerate(self.blocks):
             if bi < first or bi >= stop:
                 continue
@@ -437,8 +440,15 @@ class _BEVBackbonePlan:
                 u = (self.depth, i + 1, self.uni_vals[i]) if uni and bi == 0 else None
                 o = pp[i % 2] if self.out_pair(convs, i) else NHWC(pp[i % 2].t, pair=False)
                 x = cv(x, out=o, uni=u)
+                issued += 1
+                if mark is not None and issued == mark[0]:
+                    mark[1].record()
             outs.append(x)
         return outs
+
+    def convs_before(self, n_blocks: int) -> int:
+        """Convs in the first n_blocks down blocks."""
+        return sum(len(c) for c, _, _, _ in self.blocks[:n_blocks])
 
     def up_strides(self, bb) -> List[float]:
         return [float(u.s) for u in bb.deblocks]
@@ -517,12 +527,12 @@ class FastBEV:
             self.head(self.bb.forward(canvas), out=self.hout)
         return self.head_maps()
 
-    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None) -> List[NHWC]:
+    def forward_blocks(self, canvas: NHWC, stop: Optional[int] = None, mark: Optional[tuple] = None) -> List[NHWC]:
         """The down blocks only (pair canvas), or the first ``stop`` of them; forward_neck finishes
         the batch from their outputs, which stay in this plan's buffers until its next
-        forward_blocks."""
+        forward_blocks.  mark = (n, event): the event is recorded after the first n convs."""
         assert self.neck is not None and canvas.pair == self.pair
-        return self.bb.forward_blocks(canvas, stop)
+        return self.bb.forward_blocks(canvas, stop, mark=mark)
 
     def forward_neck(self, blocks: List[NHWC]):
         if len(blocks) < len(self.bb.blocks):  # the remaining down blocks first

@@ -155,18 +155,12 @@ class LidarPipeline:
         neck_back; step_back finishes the batch).  bench.py --lidar-pipeline 5 runs it alone on the
         critical stream: this pipeline's next step_pre then runs after its step_back, beside the
         other pipeline's blocks.  mark = (n, event): record the event on the current stream once
-        the first n down blocks are issued (the other pipeline's next front waits for it, so that
-        the voxeliser runs beside blocks 2-3 instead of block 1's full-register-file convs)."""
+        the first n convs of the down blocks are issued (the other pipeline's next front waits for it, so that
+        the voxeliser runs beside blocks 2-3 instead of block 1's full-register-file convs;
+        ``self.fast.bb.convs_before(blocks)`` gives n for whole blocks)."""
         self._blocks = self._head = None
         if self.use_fast and neck_back and self.fast.neck is not None:
-            canvas = self.enc.canvas_nhwc()
-            if mark is not None and blocks_front is None:
-                n, ev = mark
-                outs = self.fast.forward_blocks(canvas, n)
-                ev.record()
-                self._blocks = self.fast.bb.forward_blocks(None, outs=outs)
-                return
-            self._blocks = self.fast.forward_blocks(canvas, blocks_front)
+            self._blocks = self.fast.forward_blocks(self.enc.canvas_nhwc(), blocks_front, mark=mark)
         elif self.use_fast:
             self._head = self.fast.forward(self.enc.canvas_nhwc())
         else:
